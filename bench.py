@@ -1,0 +1,335 @@
+"""Headline benchmark: Z3 encode points/s + st_contains join pairs/s on MI355X (BASELINE.json).
+
+  python bench.py [--gpus N --steps K --warmup W]           (N > 1: launched by torch.distributed.run)
+
+A step of the headline is one pass of Z3IndexKeySpace.toIndexKey's batch form (BinnedTime(week) +
+Z3SFC.index) over the rank's resident 1B-point shard (BASELINE configs[1]); `value` = points of all
+ranks / max-over-ranks time.  The st_contains join (configs[3]: 1B points x 3,200 county polygons,
+polygon set broadcast over RCCL) is timed the same way and reported under "pip_join"; the remaining
+hot-path kernels are reported under "extra".  Inputs are generated on the device (SplitMix64) before
+the timed region; the CPU restatement (oracle/) is timed on a bounded sample as cpu_baseline.
+"""
+import argparse
+import json
+import os
+import sys
+import threading
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "points/sec Z3 encode + point-in-polygon join pairs/sec at 1/2/4/8 MI355X"
+SEED = 0x67656F6D65736121
+T2020, T2021 = 1577836800000, 1609459200000
+CONUS = (-125.0, 24.0, -66.0, 50.0)
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+FP64_PEAK_TFLOPS = 78.6        # FP64 vector
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--points", type=int, default=1_000_000_000, help="points per GPU (Z3 encode)")
+    p.add_argument("--join-points", type=int, default=1_000_000_000, help="points per GPU (join)")
+    p.add_argument("--join-steps", type=int, default=5)
+    p.add_argument("--no-extra", action="store_true")
+    p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=8.0)
+    p.add_argument("--only", default="", help="comma list: z3,join,extra (profiling)")
+    return p.parse_args()
+
+
+class Dist:
+    def __init__(self, ngpus):
+        import torch
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        torch.cuda.set_device(self.local)
+        self.pg = None
+        if self.world > 1:
+            import torch.distributed as dist
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            dist.init_process_group("nccl", device_id=torch.device("cuda", self.local))
+            self.pg = dist
+
+    def barrier(self):
+        import torch
+        torch.cuda.synchronize()
+        if self.pg:
+            self.pg.barrier()
+        torch.cuda.synchronize()
+
+    def max(self, v):
+        import torch
+        if not self.pg:
+            return v
+        t = torch.tensor([v], dtype=torch.float64, device="cuda")
+        self.pg.all_reduce(t, op=self.pg.ReduceOp.MAX)
+        return float(t.item())
+
+    def sum(self, v):
+        import torch
+        if not self.pg:
+            return v
+        t = torch.tensor([v], dtype=torch.float64, device="cuda")
+        self.pg.all_reduce(t, op=self.pg.ReduceOp.SUM)
+        return float(t.item())
+
+
+def timed(dist, fn, steps, warmup):
+    """Barrier + sync on both sides; HIP events on the stream the kernels run on; max over ranks."""
+    import torch
+    for _ in range(warmup):
+        fn()
+    dist.barrier()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(steps):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    ms = s.elapsed_time(e) / steps
+    dist.barrier()
+    return dist.max(ms)
+
+
+def gen_points(ctx, n, base, box, x, y, t):
+    from geomesa_amd import _lib
+    _lib.check(ctx.lib.gm_gen_points(ctx.handle, SEED, n, base, box[0], box[2], box[1], box[3], T2020, T2021,
+                                     _lib.ptr(x), _lib.ptr(y), _lib.ptr(t)), "gm_gen_points")
+
+
+def load_pmc(name, n):
+    """Per-launch HBM traffic from a committed rocprofv3 PMC summary (profiles/), if it matches n."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        d = json.load(open(p))[name]
+        if int(d["n"]) == int(n):
+            return float(d["bytes_per_launch"])
+    except Exception:
+        pass
+    return None
+
+
+def roofline(bytes_per_launch, ms, traffic=None):
+    gbs = bytes_per_launch / (ms * 1e-3) / 1e9
+    return {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": traffic}
+
+
+# ------------------------------------------------------------------------------ CPU baselines
+
+def cpu_threads():
+    return max(1, min(16, os.cpu_count() or 1))
+
+
+def cpu_z3_baseline(seconds):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    nt = cpu_threads()
+    per = 4_000_000
+    rng = np.random.default_rng(7)
+    x = rng.uniform(-180, 180, per); y = rng.uniform(-90, 90, per); t = rng.integers(T2020, T2021, per)
+    O.z3_index_key_batch(x[:8], y[:8], t[:8])
+    done = [0] * nt
+    stop = time.time() + seconds
+
+    def work(k):
+        while time.time() < stop:
+            O.z3_index_key_batch(x, y, t)
+            done[k] += per
+    th = [threading.Thread(target=work, args=(k,)) for k in range(nt)]
+    t0 = time.time()
+    for h in th:
+        h.start()
+    for h in th:
+        h.join()
+    dt = time.time() - t0
+    return {"value": sum(done) / dt, "unit": "points/s", "cores": nt, "kind": "port",
+            "sample": "%d threads x repeated 4M-point batches of the C restatement (oracle/gm_oracle.c "
+                      "gmo_z3_index_key_batch, week) for %.1f s: %d points" % (nt, dt, sum(done))}
+
+
+def cpu_join_baseline(seconds, ps):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    from geomesa_amd.join import synthetic_points
+    nt = cpu_threads()
+    op = O.OraclePolySet(*ps.to_arrays())
+    n = 200_000
+    px, py = synthetic_points(n, seed=SEED + 5)
+    t0 = time.time()
+    op.join(px[:1000], py[:1000], nthreads=1)
+    one = time.time() - t0
+    # size the sample for ~`seconds` of work on nt threads
+    est = max(one, 1e-4) / 1000
+    n = int(min(50_000_000, max(100_000, seconds * nt / est)))
+    px, py = synthetic_points(n, seed=SEED + 5)
+    t0 = time.time()
+    pt, _ = op.join(px, py, nthreads=nt)
+    dt = time.time() - t0
+    return {"value": n * ps.n_polys / dt, "unit": "pairs/s", "cores": nt, "kind": "port",
+            "sample": "%d CONUS points x %d polygons, C restatement (grid candidates + JTS contains per "
+                      "pair, %d pthreads): %.2f s, %d matches" % (n, ps.n_polys, nt, dt, len(pt))}
+
+
+# ------------------------------------------------------------------------------ main
+
+def main():
+    a = parse()
+    import torch
+    from geomesa_amd import _lib
+    from geomesa_amd.curve import Z3SFC, Z2SFC
+    dist = Dist(a.gpus)
+    ctx = _lib.context(dist.local)
+    only = set(a.only.split(",")) if a.only else {"z3", "join", "extra"}
+    dev = torch.device("cuda", dist.local)
+    N = a.points
+    out = {"metric": METRIC, "unit": "points/s", "n_gpus": dist.world, "steps": a.steps, "warmup": a.warmup,
+           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64+int64",
+           "data": "synthetic (SplitMix64 on device; lon U[-180,180), lat U[-90,90), t U[2020,2021) ms)"}
+    extra = {}
+
+    # ---------------------------------------------------------------- Z3 encode (headline)
+    x = torch.empty(N, dtype=torch.float64, device=dev)
+    y = torch.empty(N, dtype=torch.float64, device=dev)
+    t = torch.empty(N, dtype=torch.int64, device=dev)
+    b = torch.empty(N, dtype=torch.int16, device=dev)
+    z = torch.empty(N, dtype=torch.int64, device=dev)
+    gen_points(ctx, N, dist.rank * N, (-180.0, -90.0, 180.0, 90.0), x, y, t)
+    sfc = Z3SFC("week")
+    lib, h = ctx.lib, ctx.handle
+    P = _lib.ptr
+
+    def z3_step():
+        lib.gm_z3_index_key(h, P(x), P(y), P(t), N, 1, 0, P(b), P(z), None, None)
+    ms = None
+    if "z3" in only:
+        ms = timed(dist, z3_step, a.steps, a.warmup)
+        st = _lib.BatchStatus()
+        _lib.check(lib.gm_z3_index_key(h, P(x), P(y), P(t), N, 1, 0, P(b), P(z), None, __import__("ctypes").byref(st)),
+                   "z3")
+        assert st.n_errors == 0
+        total = N * dist.world
+        out.update({"value": total / (ms * 1e-3), "ms_per_step": ms})
+        out["roofline"] = roofline(34.0 * N, ms, load_pmc("z3_index_key", N))
+        out["roofline"]["bytes_per_unit"] = 34
+        out["roofline"]["kernel"] = "k_z3_index_key<WEEK,false,false,4>"
+    out["config"] = {"workload": "Z3IndexKeySpace.toIndexKey batch (BinnedTime week + Z3SFC(week).index) over "
+                                 "%d resident synthetic points per GPU (BASELINE configs[1])" % N,
+                     "points_per_gpu": N, "period": "week", "parallelism": "point shards, no collective"}
+
+    # ---------------------------------------------------------------- extra hot-path kernels on the same data
+    if "extra" in only and not a.no_extra:
+        def rec(name, fn, bytes_per_unit, n_units, unit="points/s", steps=max(3, a.steps // 2)):
+            m = timed(dist, fn, steps, 1)
+            extra[name] = {"value": n_units * dist.world / (m * 1e-3), "unit": unit, "ms_per_step": m,
+                           "roofline": roofline(bytes_per_unit * n_units, m, load_pmc(name, n_units))}
+        xi = torch.empty_like(x); yi = torch.empty_like(y); ti = torch.empty_like(t)
+        rec("z3_invert", lambda: lib.gm_z3_invert(h, P(z), N, 1, 21, P(xi), P(yi), P(ti)), 32, N)
+        del xi, yi, ti
+        z2 = torch.empty_like(z)
+        rec("z2_index", lambda: lib.gm_z2_index(h, P(x), P(y), N, 31, 0, P(z2), None, None), 24, N)
+        rec("z2_invert", lambda: lib.gm_z2_invert(h, P(z2), N, 31, P(x), P(y)), 24, N)
+        del z2
+        # filter scan, key space (configs[2] query on the resident keys)
+        from geomesa_amd import filters as F
+        from geomesa_amd.keyspace import Z3IndexKeySpace, during
+        ks = Z3IndexKeySpace()
+        v = ks.get_index_values([(-10, 35, 30, 60)], [during(1590969600000, 1591617600000)])
+        fb = F.serialize_to_bytes(F.Z3Filter.from_values(v))
+        import ctypes
+        fbuf = (ctypes.c_uint8 * len(fb)).from_buffer_copy(fb)
+        br = np.asarray(ks.bin_ranges(v), np.int16).reshape(-1)
+        mask = torch.empty((N + 63) // 64, dtype=torch.int64, device=dev)
+        rec("z3filter_scan", lambda: lib.gm_z3filter_scan(h, fbuf, len(fb), br.ctypes.data, len(br) // 2, P(b), P(z),
+                                                         N, P(mask), None, 0, None), 10.125, N, unit="rows/s")
+        del mask
+        # XZ2 index of envelopes (configs[4]): reuse x/y as min corners, jittered max corners
+        NX = min(N, 200_000_000)
+        xmax = torch.clamp(x[:NX] + 0.01, max=180.0); ymax = torch.clamp(y[:NX] + 0.005, max=90.0)
+        xo = torch.empty(NX, dtype=torch.int64, device=dev)
+        rec("xz2_index", lambda: lib.gm_xz2_index(h, P(x), P(y), P(xmax), P(ymax), NX, 12, 0, P(xo), None, None), 40,
+            NX, unit="envelopes/s")
+        del xmax, ymax, xo
+        # batched ranges (configs[4]/[0]): 4096 Z3 queries with target 2000
+        rng = np.random.default_rng(1)
+        qs = []
+        for _ in range(4096):
+            w = 10 ** rng.uniform(-1, 1); hh = 10 ** rng.uniform(-1, 1)
+            cx = rng.uniform(-170, 170); cy = rng.uniform(-80, 80); t0 = int(rng.integers(0, 500000))
+            qs.append(([(cx - w, cy - hh, cx + w, cy + hh)], [(t0, t0 + 86400)]))
+        t0w = time.time()
+        for _ in range(2):
+            sfc.ranges_batch(qs, 64, 2000)
+        torch.cuda.synchronize()
+        dt = (time.time() - t0w) / 2
+        extra["z3_ranges_batch"] = {"value": len(qs) * dist.world / dt, "unit": "queries/s",
+                                    "ms_per_step": dt * 1e3, "note": "host-driven incl. H2D/D2H, 4096 queries, "
+                                                                     "maxRanges 2000"}
+    del x, y, t, b, z
+    torch.cuda.empty_cache()
+
+    # ---------------------------------------------------------------- st_contains join (configs[3])
+    if "join" in only:
+        from geomesa_amd.join import PolygonIndex, PolygonSet, synthetic_counties
+        J = a.join_points
+        ps = synthetic_counties() if dist.rank == 0 else None
+        if dist.world > 1:
+            # polygon set broadcast over RCCL (the reference ships it with the Spark join shuffle)
+            arrs = ps.to_arrays() if ps else None
+            sizes = torch.tensor([len(v) for v in arrs] if arrs else [0] * 5, dtype=torch.int64, device=dev)
+            dist.pg.broadcast(sizes, 0)
+            tens = []
+            for k, (sz, dt_) in enumerate(zip(sizes.tolist(), [torch.int32] * 3 + [torch.float64] * 2)):
+                tt = torch.from_numpy(arrs[k]).to(dev) if arrs else torch.empty(sz, dtype=dt_, device=dev)
+                dist.pg.broadcast(tt, 0)
+                tens.append(tt.cpu().numpy())
+            ps = PolygonSet(*tens)
+        ix = PolygonIndex(ps, ctx)
+        px = torch.empty(J, dtype=torch.float64, device=dev)
+        py = torch.empty(J, dtype=torch.float64, device=dev)
+        gen_points(ctx, J, dist.rank * J + (1 << 40), CONUS, px, py, None)
+        cnt = ix.join(px, py, count_only=True)
+        cap = int(cnt * 1.05) + 1024
+        ptids = torch.empty(cap, dtype=torch.int64, device=dev)
+        plids = torch.empty(cap, dtype=torch.int32, device=dev)
+        npairs = __import__("ctypes").c_int64()
+
+        def join_step():
+            lib.gm_pip_join(h, ix._h, P(px), P(py), J, dist.rank * J, P(ptids), P(plids), cap, None)
+        jms = timed(dist, join_step, a.join_steps, 1)
+        _lib.check(lib.gm_pip_join(h, ix._h, P(px), P(py), J, dist.rank * J, P(ptids), P(plids), cap,
+                                   __import__("ctypes").byref(npairs)), "join")
+        matches = int(dist.sum(npairs.value))
+        pairs = J * ps.n_polys * dist.world
+        pj = {"value": pairs / (jms * 1e-3), "unit": "pairs/s", "ms_per_step": jms, "points_per_gpu": J,
+              "polygons": ps.n_polys, "vertices": ps.n_vertices, "matches": matches,
+              "matches_per_s": matches / (jms * 1e-3),
+              "roofline": roofline(16.0 * J + 12.0 * npairs.value, jms, load_pmc("pip_join", J)),
+              "workload": "st_contains(polygon, point) join, %d CONUS points/GPU x %d synthetic county polygons "
+                          "(BASELINE configs[3]); polygon set broadcast over RCCL when N > 1" % (J, ps.n_polys)}
+        pj["roofline"]["bytes_per_unit"] = "16 B/point + 12 B/pair"
+        if dist.rank == 0 and not a.no_cpu:
+            pj["cpu_baseline"] = cpu_join_baseline(a.cpu_seconds, ps)
+        out["pip_join"] = pj
+        del px, py, ptids, plids, ix
+
+    if dist.rank == 0 and not a.no_cpu and "z3" in only:
+        out["cpu_baseline"] = cpu_z3_baseline(a.cpu_seconds)
+    if extra:
+        out["extra"] = extra
+    if dist.rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist.pg:
+        dist.pg.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

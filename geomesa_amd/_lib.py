@@ -1,0 +1,179 @@
+"""Loader for the in-tree HIP library (geomesa_amd/lib/libgeomesa_hip.so).
+
+The product path is the HIP library only: there is no CPU fallback.  If the library is missing or
+no GPU is visible, every compute entry point raises GeomesaHipUnavailable.
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libgeomesa_hip.so")
+HEADER = os.path.join(os.path.dirname(HERE), "include", "geomesa_hip.h")
+
+GM_OK = 0
+GM_E_INVALID = -1
+GM_E_HIP = -2
+GM_E_CAPACITY = -3
+GM_E_ELEMENT = -4
+
+GM_ST_OK = 0
+GM_ST_OUT_OF_BOUNDS = 1
+GM_ST_BAD_TIME = 2
+GM_ST_UNORDERED = 3
+
+
+class GeomesaHipUnavailable(RuntimeError):
+    """The HIP library or a GPU is not available (no silent fallback exists)."""
+
+
+class GeomesaHipError(RuntimeError):
+    pass
+
+
+class BatchStatus(ctypes.Structure):
+    _fields_ = [("n_errors", ctypes.c_int64), ("first_index", ctypes.c_int64),
+                ("first_code", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
+class Range(ctypes.Structure):
+    _fields_ = [("lower", ctypes.c_int64), ("upper", ctypes.c_int64),
+                ("contained", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
+class PolySetC(ctypes.Structure):
+    _fields_ = [("n_polys", ctypes.c_int32),
+                ("poly_part_off", ctypes.c_void_p), ("part_ring_off", ctypes.c_void_p),
+                ("ring_vert_off", ctypes.c_void_p), ("vx", ctypes.c_void_p), ("vy", ctypes.c_void_p)]
+
+
+vp = ctypes.c_void_p
+i64 = ctypes.c_int64
+i32 = ctypes.c_int32
+cint = ctypes.c_int
+d = ctypes.c_double
+sz = ctypes.c_size_t
+
+# every symbol include/geomesa_hip.h declares, with its ctypes signature
+SIGNATURES = {
+    "gm_abi_version": (cint, []),
+    "gm_ctx_create": (cint, [cint, vp, vp]),
+    "gm_ctx_destroy": (cint, [vp]),
+    "gm_ctx_sync": (cint, [vp]),
+    "gm_ctx_stream": (vp, [vp]),
+    "gm_last_error": (ctypes.c_char_p, []),
+    "gm_device_alloc": (cint, [vp, sz, vp]),
+    "gm_device_free": (cint, [vp, vp]),
+    "gm_copy_to_device": (cint, [vp, vp, vp, sz]),
+    "gm_copy_to_host": (cint, [vp, vp, vp, sz]),
+    "gm_timer_start": (cint, [vp]),
+    "gm_timer_stop": (cint, [vp, vp]),
+    "gm_z3_index": (cint, [vp, vp, vp, vp, i64, cint, cint, cint, vp, vp, vp]),
+    "gm_z3_index_key": (cint, [vp, vp, vp, vp, i64, cint, cint, vp, vp, vp, vp]),
+    "gm_z3_invert": (cint, [vp, vp, i64, cint, cint, vp, vp, vp]),
+    "gm_z2_index": (cint, [vp, vp, vp, i64, cint, cint, vp, vp, vp]),
+    "gm_z2_invert": (cint, [vp, vp, i64, cint, vp, vp]),
+    "gm_binned_time": (cint, [vp, vp, i64, cint, vp, vp, vp, vp]),
+    "gm_xz2_index": (cint, [vp, vp, vp, vp, vp, i64, cint, cint, vp, vp, vp]),
+    "gm_xz3_index": (cint, [vp, vp, vp, vp, vp, vp, vp, i64, cint, cint, cint, vp, vp, vp]),
+    "gm_z3_ranges": (cint, [vp, i64, vp, vp, vp, vp, cint, cint, cint, cint, cint, vp, vp, i64, vp, vp]),
+    "gm_z2_ranges": (cint, [vp, i64, vp, vp, cint, cint, cint, cint, vp, vp, i64, vp, vp]),
+    "gm_xz2_ranges": (cint, [vp, i64, vp, vp, cint, cint, vp, vp, i64, vp, vp]),
+    "gm_xz3_ranges": (cint, [vp, i64, vp, vp, cint, cint, cint, vp, vp, i64, vp, vp]),
+    "gm_z3filter_scan": (cint, [vp, vp, sz, vp, cint, vp, vp, i64, vp, vp, i64, vp]),
+    "gm_z2filter_scan": (cint, [vp, vp, sz, vp, i64, vp, vp, i64, vp]),
+    "gm_strict_scan": (cint, [vp, vp, vp, vp, i64, vp, cint, i64, i64, vp, vp, i64, vp]),
+    "gm_pip_index_create": (cint, [vp, vp, vp]),
+    "gm_pip_index_destroy": (cint, [vp]),
+    "gm_pip_join": (cint, [vp, vp, vp, vp, i64, i64, vp, vp, i64, vp]),
+    "gm_gen_points": (cint, [vp, ctypes.c_uint64, i64, i64, d, d, d, d, i64, i64, vp, vp, vp]),
+}
+
+_lib = None
+
+
+def load():
+    """Load the HIP library (torch is imported first so one HIP runtime serves both)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    import torch  # noqa: F401  -- binds libamdhip64.so.7 before our library resolves it
+    if not os.path.exists(LIB_PATH):
+        raise GeomesaHipUnavailable(
+            "libgeomesa_hip.so not built (%s); run `python -m geomesa_amd.build`" % LIB_PATH)
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = lib
+    return lib
+
+
+def last_error():
+    return load().gm_last_error().decode(errors="replace")
+
+
+def check(rc, what):
+    if rc == GM_OK:
+        return
+    raise GeomesaHipError("%s failed: rc=%d (%s)" % (what, rc, last_error()))
+
+
+class Context:
+    """One gm_ctx bound to a device and a HIP stream (torch's current stream by default)."""
+
+    def __init__(self, device=0, stream=None):
+        import torch
+        lib = load()
+        if not torch.cuda.is_available():
+            raise GeomesaHipUnavailable("no GPU visible: the geomesa_amd product path needs a MI355X")
+        torch.cuda.set_device(device)
+        if stream is None:
+            stream = torch.cuda.current_stream(device).cuda_stream
+        self.device = device
+        self._h = ctypes.c_void_p()
+        check(lib.gm_ctx_create(device, ctypes.c_void_p(stream), ctypes.byref(self._h)), "gm_ctx_create")
+        self.lib = lib
+
+    @property
+    def handle(self):
+        return self._h
+
+    def sync(self):
+        check(self.lib.gm_ctx_sync(self._h), "gm_ctx_sync")
+
+    def close(self):
+        if self._h:
+            self.lib.gm_ctx_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+_contexts = {}
+
+
+def context(device=None):
+    """Per-(device, stream) cached context."""
+    import torch
+    if device is None:
+        device = torch.cuda.current_device() if torch.cuda.is_available() else 0
+    if not torch.cuda.is_available():
+        load()
+        raise GeomesaHipUnavailable("no GPU visible: the geomesa_amd product path needs a MI355X")
+    stream = torch.cuda.current_stream(device).cuda_stream
+    key = (device, stream)
+    if key not in _contexts:
+        _contexts[key] = Context(device, stream)
+    return _contexts[key]
+
+
+def ptr(t):
+    """Device pointer of a torch tensor (None passes through)."""
+    if t is None:
+        return None
+    return ctypes.c_void_p(t.data_ptr())

@@ -1,0 +1,40 @@
+"""Builds libgeomesa_hip.so in-tree for gfx950 (hipcc, -ffp-contract=off: the JVM never fuses)."""
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SRC = ["gm_ctx.hip", "gm_curve.hip", "gm_filter.hip", "gm_pip.hip", "gm_ranges.hip"]
+OUT = os.path.join(HERE, "lib", "libgeomesa_hip.so")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math", "-fPIC", "-shared",
+         "-Wall", "-Wno-unused-function"]
+
+
+def sources():
+    return [os.path.join(HERE, "csrc", s) for s in SRC if os.path.exists(os.path.join(HERE, "csrc", s))]
+
+
+def needs_build():
+    if not os.path.exists(OUT):
+        return True
+    t = os.path.getmtime(OUT)
+    deps = sources() + [os.path.join(HERE, "csrc", f) for f in os.listdir(os.path.join(HERE, "csrc"))]
+    deps.append(os.path.join(os.path.dirname(HERE), "include", "geomesa_hip.h"))
+    return any(os.path.getmtime(f) > t for f in deps)
+
+
+def build(force=False, verbose=True):
+    if not force and not needs_build():
+        return OUT
+    os.makedirs(os.path.dirname(OUT), exist_ok=True)
+    cmd = [HIPCC] + FLAGS + ["-o", OUT + ".tmp"] + sources()
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.check_call(cmd)
+    os.replace(OUT + ".tmp", OUT)
+    return OUT
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv)

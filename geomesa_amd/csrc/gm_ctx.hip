@@ -1,0 +1,177 @@
+// gm_ctx.hip -- context lifecycle, error plumbing, memory helpers, timers, synthetic data.
+#include <stdio.h>
+#include <string.h>
+
+#include <mutex>
+#include <string>
+
+#include "gm_internal.hpp"
+
+namespace {
+thread_local std::string g_last_error;
+}
+
+namespace gm {
+
+void set_error(const std::string& msg) { g_last_error = msg; }
+
+int hip_fail(hipError_t e, const char* what) {
+  g_last_error = std::string(what) + ": " + hipGetErrorString(e);
+  return GM_E_HIP;
+}
+
+int begin_summary(gm_ctx* ctx, gm_batch_status* summary) {
+  if (!summary) return GM_OK;
+  const int64_t init[2] = {0, INT64_MAX};
+  GM_HIP(hipMemcpyAsync(ctx->d_err, init, sizeof(init), hipMemcpyHostToDevice, ctx->stream));
+  return GM_OK;
+}
+
+int end_summary(gm_ctx* ctx, gm_batch_status* summary) {
+  if (!summary) return GM_OK;
+  GM_HIP(hipMemcpyAsync(ctx->h_pinned, ctx->d_err, 2 * sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+  GM_HIP(hipStreamSynchronize(ctx->stream));
+  summary->n_errors = ctx->h_pinned[0];
+  if (ctx->h_pinned[0] > 0) {
+    summary->first_index = ctx->h_pinned[1] >> 8;
+    summary->first_code = (int32_t)(ctx->h_pinned[1] & 0xff);
+  } else {
+    summary->first_index = -1;
+    summary->first_code = 0;
+  }
+  summary->reserved = 0;
+  return GM_OK;
+}
+
+// SplitMix64 (Steele, Lea, Flood 2014), keyed by (seed, index)
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+  x += 0x9e3779b97f4a7c15ull;
+  x = (x ^ (x >> 30)) * 0xbf58476d1ce4e5b9ull;
+  x = (x ^ (x >> 27)) * 0x94d049bb133111ebull;
+  return x ^ (x >> 31);
+}
+__device__ __forceinline__ double unit_double(uint64_t r) { return (double)(r >> 11) * 0x1.0p-53; }
+
+__global__ __launch_bounds__(256) void k_gen_points(uint64_t seed, int64_t n, int64_t base, double lon0,
+                                                    double lon1, double lat0, double lat1, int64_t t0,
+                                                    int64_t t1, double* __restrict__ x, double* __restrict__ y,
+                                                    int64_t* __restrict__ t) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint64_t k = (uint64_t)(base + i);
+  uint64_t r0 = splitmix64(seed ^ (k * 3 + 0) * 0xd1b54a32d192ed03ull);
+  uint64_t r1 = splitmix64(seed ^ (k * 3 + 1) * 0xd1b54a32d192ed03ull);
+  uint64_t r2 = splitmix64(seed ^ (k * 3 + 2) * 0xd1b54a32d192ed03ull);
+  if (x) x[i] = __dadd_rn(lon0, __dmul_rn(unit_double(r0), __dsub_rn(lon1, lon0)));
+  if (y) y[i] = __dadd_rn(lat0, __dmul_rn(unit_double(r1), __dsub_rn(lat1, lat0)));
+  if (t) {
+    uint64_t span = (uint64_t)(t1 - t0);
+    t[i] = t0 + (int64_t)(span ? (r2 % span) : 0);
+  }
+}
+
+}  // namespace gm
+
+extern "C" {
+
+int gm_abi_version(void) { return GM_ABI_VERSION; }
+
+const char* gm_last_error(void) { return g_last_error.c_str(); }
+
+int gm_ctx_create(int device, void* stream, gm_ctx** out) {
+  if (!out) return GM_E_INVALID;
+  *out = nullptr;
+  int ndev = 0;
+  GM_HIP(hipGetDeviceCount(&ndev));
+  if (device < 0 || device >= ndev) {
+    gm::set_error("gm_ctx_create: no such device");
+    return GM_E_INVALID;
+  }
+  GM_HIP(hipSetDevice(device));
+  gm_ctx* c = new gm_ctx();
+  c->device = device;
+  if (stream) {
+    c->stream = (hipStream_t)stream;
+  } else {
+    hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) { delete c; return gm::hip_fail(e, "hipStreamCreate"); }
+    c->own_stream = true;
+  }
+  hipError_t e = hipMalloc(&c->d_err, 4 * sizeof(int64_t));
+  if (e == hipSuccess) e = hipMalloc(&c->d_scratch, 64 * sizeof(int64_t));
+  if (e == hipSuccess) e = hipHostMalloc(&c->h_pinned, 64 * sizeof(int64_t), hipHostMallocDefault);
+  if (e == hipSuccess) e = hipEventCreate(&c->ev0);
+  if (e == hipSuccess) e = hipEventCreate(&c->ev1);
+  if (e != hipSuccess) { gm_ctx_destroy(c); return gm::hip_fail(e, "gm_ctx_create"); }
+  *out = c;
+  return GM_OK;
+}
+
+int gm_ctx_destroy(gm_ctx* c) {
+  if (!c) return GM_OK;
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->d_err) (void)hipFree(c->d_err);
+  if (c->d_scratch) (void)hipFree(c->d_scratch);
+  if (c->h_pinned) (void)hipHostFree(c->h_pinned);
+  if (c->ev0) (void)hipEventDestroy(c->ev0);
+  if (c->ev1) (void)hipEventDestroy(c->ev1);
+  if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+  return GM_OK;
+}
+
+int gm_ctx_sync(gm_ctx* c) {
+  if (!c) return GM_E_INVALID;
+  GM_HIP(hipStreamSynchronize(c->stream));
+  return GM_OK;
+}
+
+void* gm_ctx_stream(gm_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+int gm_device_alloc(gm_ctx* c, size_t bytes, void** ptr) {
+  if (!c || !ptr) return GM_E_INVALID;
+  GM_HIP(hipSetDevice(c->device));
+  GM_HIP(hipMalloc(ptr, bytes ? bytes : 1));
+  return GM_OK;
+}
+int gm_device_free(gm_ctx* c, void* ptr) {
+  if (!c) return GM_E_INVALID;
+  if (ptr) GM_HIP(hipFree(ptr));
+  return GM_OK;
+}
+int gm_copy_to_device(gm_ctx* c, void* dst, const void* src, size_t bytes) {
+  if (!c) return GM_E_INVALID;
+  GM_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream));
+  GM_HIP(hipStreamSynchronize(c->stream));
+  return GM_OK;
+}
+int gm_copy_to_host(gm_ctx* c, void* dst, const void* src, size_t bytes) {
+  if (!c) return GM_E_INVALID;
+  GM_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream));
+  GM_HIP(hipStreamSynchronize(c->stream));
+  return GM_OK;
+}
+int gm_timer_start(gm_ctx* c) {
+  if (!c) return GM_E_INVALID;
+  GM_HIP(hipEventRecord(c->ev0, c->stream));
+  return GM_OK;
+}
+int gm_timer_stop(gm_ctx* c, float* ms) {
+  if (!c || !ms) return GM_E_INVALID;
+  GM_HIP(hipEventRecord(c->ev1, c->stream));
+  GM_HIP(hipEventSynchronize(c->ev1));
+  GM_HIP(hipEventElapsedTime(ms, c->ev0, c->ev1));
+  return GM_OK;
+}
+
+int gm_gen_points(gm_ctx* c, uint64_t seed, int64_t n, int64_t base, double lon0, double lon1, double lat0,
+                  double lat1, int64_t t0, int64_t t1, double* x, double* y, int64_t* t) {
+  if (!c || n < 0) return GM_E_INVALID;
+  if (n == 0) return GM_OK;
+  hipLaunchKernelGGL(gm::k_gen_points, dim3(gm::grid_for(n, 256)), dim3(256), 0, c->stream, seed, n, base, lon0,
+                     lon1, lat0, lat1, t0, t1, x, y, t);
+  GM_CHECK_LAUNCH();
+  return GM_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,668 @@
+// gm_curve.hip -- Z3/Z2 encode+decode, BinnedTime and XZ2/XZ3 envelope keys on gfx950.
+//
+// All of these are HBM-streaming element-wise kernels (34 B/point for the Z3 key, 32 B for the Z3
+// invert, 24 B for Z2, 40/56 B for XZ): no reuse, no LDS, no MFMA.  Shape: 256-thread workgroups,
+// each lane moves 2 consecutive elements with 16-byte loads/stores (one dwordx4 per column per
+// lane), UNROLL independent pairs in flight per lane, fully coalesced per wave instruction
+// (pair p of lane l in step u sits at block_base + u*256 + l).  One chunk per workgroup -- the
+// grid is large (N / 2048 workgroups at UNROLL = 4), so all 256 CUs x 8 XCDs fill.
+#include "gm_internal.hpp"
+
+namespace gm {
+
+constexpr int TPB = 256;
+
+// clang ext-vector types: one dwordx4 per lane; usable with the nontemporal builtins
+typedef double dv2 __attribute__((ext_vector_type(2)));
+typedef long long lv2 __attribute__((ext_vector_type(2)));
+
+#ifndef GM_NT
+#define GM_NT 1
+#endif
+template <class T>
+__device__ __forceinline__ T ld_stream(const T* p) {
+#if GM_NT
+  return __builtin_nontemporal_load(p);
+#else
+  return *p;
+#endif
+}
+template <class T>
+__device__ __forceinline__ void st_stream(T v, T* p) {
+#if GM_NT
+  __builtin_nontemporal_store(v, p);
+#else
+  *p = v;
+#endif
+}
+
+// ------------------------------------------------------------------ per-element bodies
+
+// Z3SFC.index (z3/curve/Z3SFC.scala:37-52); t is the offset within the period (Long)
+template <bool LENIENT>
+__device__ __forceinline__ uint8_t z3_index_one(double x, double y, int64_t t, const NDim& lon, const NDim& lat,
+                                                const NDim& tim, int64_t& z) {
+  double td = (double)t;  // Long compared to / normalized as Double
+  bool inb = x >= lon.min && x <= lon.max && y >= lat.min && y <= lat.max && td >= tim.min && td <= tim.max;
+  if (!inb) {
+    if (!LENIENT) { z = 0; return ST_OUT_OF_BOUNDS; }
+    // lenientIndex (Z3SFC.scala:47-52): NaN falls through every comparison
+    x = x < lon.min ? lon.min : (x > lon.max ? lon.max : x);
+    y = y < lat.min ? lat.min : (y > lat.max ? lat.max : y);
+    td = td < tim.min ? tim.min : (td > tim.max ? tim.max : td);
+  }
+  z = z3_apply(normalize(lon, x), normalize(lat, y), normalize(tim, td));
+  return ST_OK;
+}
+
+// Z3IndexKeySpace.toIndexKey (idx/index/z3/Z3IndexKeySpace.scala:71-76): BinnedTime throws even
+// when lenient (it sits outside the try at :74); then sfc.index(x, y, offset, lenient)
+template <int PERIOD, bool LENIENT>
+__device__ __forceinline__ uint8_t z3_key_one(double x, double y, int64_t ms, const NDim& lon, const NDim& lat,
+                                              const NDim& tim, int16_t& bin, int64_t& z) {
+  int64_t off;
+  uint8_t st = binned_time<PERIOD>(ms, bin, off);
+  if (st == ST_OK) st = z3_index_one<LENIENT>(x, y, off, lon, lat, tim, z);
+  if (st != ST_OK) { bin = 0; z = 0; }
+  return st;
+}
+
+template <bool LENIENT>
+__device__ __forceinline__ uint8_t z2_index_one(double x, double y, const NDim& lon, const NDim& lat,
+                                                int64_t& z) {
+  bool inb = x >= lon.min && x <= lon.max && y >= lat.min && y <= lat.max;
+  if (!inb) {
+    if (!LENIENT) { z = 0; return ST_OUT_OF_BOUNDS; }
+    x = x < lon.min ? lon.min : (x > lon.max ? lon.max : x);
+    y = y < lat.min ? lat.min : (y > lat.max ? lat.max : y);
+  }
+  z = z2_apply(normalize(lon, x), normalize(lat, y));
+  return ST_OK;
+}
+
+// ------------------------------------------------------------------ Z3 key (epoch ms -> bin, z)
+
+template <int PERIOD, bool LENIENT, bool STATUS, int UNROLL>
+__global__ __launch_bounds__(TPB) void k_z3_index_key(const dv2* __restrict__ x, const dv2* __restrict__ y,
+                                                      const lv2* __restrict__ t, int64_t n,
+                                                      short2* __restrict__ bin, lv2* __restrict__ z,
+                                                      uchar2* __restrict__ status, NDim lon, NDim lat, NDim tim,
+                                                      int64_t* __restrict__ err) {
+  const int64_t npairs = n >> 1;
+  const int64_t base = (int64_t)blockIdx.x * (TPB * UNROLL) + threadIdx.x;
+  dv2 xv[UNROLL], yv[UNROLL];
+  lv2 tv[UNROLL];
+#pragma unroll
+  for (int u = 0; u < UNROLL; ++u) {
+    const int64_t p = base + (int64_t)u * TPB;
+    if (p < npairs) {
+      xv[u] = ld_stream(&x[p]);
+      yv[u] = ld_stream(&y[p]);
+      tv[u] = ld_stream(&t[p]);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < UNROLL; ++u) {
+    const int64_t p = base + (int64_t)u * TPB;
+    if (p < npairs) {
+      int16_t b0, b1;
+      int64_t z0, z1;
+      uint8_t s0 = z3_key_one<PERIOD, LENIENT>(xv[u].x, yv[u].x, tv[u].x, lon, lat, tim, b0, z0);
+      uint8_t s1 = z3_key_one<PERIOD, LENIENT>(xv[u].y, yv[u].y, tv[u].y, lon, lat, tim, b1, z1);
+      st_stream(lv2{z0, z1}, &z[p]);
+      bin[p] = make_short2(b0, b1);
+      if (STATUS) status[p] = make_uchar2(s0, s1);
+      if (s0) report_error(err, 2 * p, s0);
+      if (s1) report_error(err, 2 * p + 1, s1);
+    }
+  }
+  if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
+    const int64_t i = n - 1;
+    int16_t b;
+    int64_t zz;
+    uint8_t s = z3_key_one<PERIOD, LENIENT>(((const double*)x)[i], ((const double*)y)[i],
+                                            ((const int64_t*)t)[i], lon, lat, tim, b, zz);
+    ((int16_t*)bin)[i] = b;
+    ((int64_t*)z)[i] = zz;
+    if (STATUS) ((uint8_t*)status)[i] = s;
+    if (s) report_error(err, i, s);
+  }
+}
+
+// scalar fallback for unaligned columns
+template <int PERIOD, bool LENIENT, bool STATUS>
+__global__ __launch_bounds__(TPB) void k_z3_index_key_s(const double* __restrict__ x, const double* __restrict__ y,
+                                                        const int64_t* __restrict__ t, int64_t n,
+                                                        int16_t* __restrict__ bin, int64_t* __restrict__ z,
+                                                        uint8_t* __restrict__ status, NDim lon, NDim lat, NDim tim,
+                                                        int64_t* __restrict__ err) {
+  for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < n; i += (int64_t)gridDim.x * TPB) {
+    int16_t b;
+    int64_t zz;
+    uint8_t s = z3_key_one<PERIOD, LENIENT>(x[i], y[i], t[i], lon, lat, tim, b, zz);
+    bin[i] = b;
+    z[i] = zz;
+    if (STATUS) status[i] = s;
+    if (s) report_error(err, i, s);
+  }
+}
+
+// ------------------------------------------------------------------ Z3SFC.index (offset t)
+
+template <bool LENIENT, bool STATUS>
+__global__ __launch_bounds__(TPB) void k_z3_index(const double* __restrict__ x, const double* __restrict__ y,
+                                                  const int64_t* __restrict__ t, int64_t n, int64_t* __restrict__ z,
+                                                  uint8_t* __restrict__ status, NDim lon, NDim lat, NDim tim,
+                                                  int64_t* __restrict__ err) {
+  for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < n; i += (int64_t)gridDim.x * TPB) {
+    int64_t zz;
+    uint8_t s = z3_index_one<LENIENT>(x[i], y[i], t[i], lon, lat, tim, zz);
+    z[i] = zz;
+    if (STATUS) status[i] = s;
+    if (s) report_error(err, i, s);
+  }
+}
+
+// ------------------------------------------------------------------ Z3SFC.invert
+
+template <int UNROLL>
+__global__ __launch_bounds__(TPB) void k_z3_invert(const lv2* __restrict__ z, int64_t n, dv2* __restrict__ x,
+                                                   dv2* __restrict__ y, lv2* __restrict__ t, NDim lon,
+                                                   NDim lat, NDim tim) {
+  const int64_t npairs = n >> 1;
+  const int64_t base = (int64_t)blockIdx.x * (TPB * UNROLL) + threadIdx.x;
+  lv2 zv[UNROLL];
+#pragma unroll
+  for (int u = 0; u < UNROLL; ++u) {
+    const int64_t p = base + (int64_t)u * TPB;
+    if (p < npairs) zv[u] = ld_stream(&z[p]);
+  }
+#pragma unroll
+  for (int u = 0; u < UNROLL; ++u) {
+    const int64_t p = base + (int64_t)u * TPB;
+    if (p < npairs) {
+      const int64_t a = zv[u].x, b = zv[u].y;
+      st_stream(dv2{denormalize(lon, z3_combine(a)), denormalize(lon, z3_combine(b))},
+                                  &x[p]);
+      st_stream(
+          dv2{denormalize(lat, z3_combine(a >> 1)), denormalize(lat, z3_combine(b >> 1))}, &y[p]);
+      st_stream(lv2{jvm_d2l(denormalize(tim, z3_combine(a >> 2))), jvm_d2l(denormalize(tim, z3_combine(b >> 2)))},
+                &t[p]);
+    }
+  }
+  if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
+    const int64_t i = n - 1;
+    const int64_t a = ((const int64_t*)z)[i];
+    ((double*)x)[i] = denormalize(lon, z3_combine(a));
+    ((double*)y)[i] = denormalize(lat, z3_combine(a >> 1));
+    ((int64_t*)t)[i] = jvm_d2l(denormalize(tim, z3_combine(a >> 2)));
+  }
+}
+
+__global__ __launch_bounds__(TPB) void k_z3_invert_s(const int64_t* __restrict__ z, int64_t n, double* __restrict__ x,
+                                                     double* __restrict__ y, int64_t* __restrict__ t, NDim lon,
+                                                     NDim lat, NDim tim) {
+  for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < n; i += (int64_t)gridDim.x * TPB) {
+    const int64_t a = z[i];
+    x[i] = denormalize(lon, z3_combine(a));
+    y[i] = denormalize(lat, z3_combine(a >> 1));
+    t[i] = jvm_d2l(denormalize(tim, z3_combine(a >> 2)));
+  }
+}
+
+// ------------------------------------------------------------------ Z2SFC.index / invert
+
+template <bool LENIENT, bool STATUS, int UNROLL>
+__global__ __launch_bounds__(TPB) void k_z2_index(const dv2* __restrict__ x, const dv2* __restrict__ y,
+                                                  int64_t n, lv2* __restrict__ z, uchar2* __restrict__ status,
+                                                  NDim lon, NDim lat, int64_t* __restrict__ err) {
+  const int64_t npairs = n >> 1;
+  const int64_t base = (int64_t)blockIdx.x * (TPB * UNROLL) + threadIdx.x;
+  dv2 xv[UNROLL], yv[UNROLL];
+#pragma unroll
+  for (int u = 0; u < UNROLL; ++u) {
+    const int64_t p = base + (int64_t)u * TPB;
+    if (p < npairs) {
+      xv[u] = ld_stream(&x[p]);
+      yv[u] = ld_stream(&y[p]);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < UNROLL; ++u) {
+    const int64_t p = base + (int64_t)u * TPB;
+    if (p < npairs) {
+      int64_t z0, z1;
+      uint8_t s0 = z2_index_one<LENIENT>(xv[u].x, yv[u].x, lon, lat, z0);
+      uint8_t s1 = z2_index_one<LENIENT>(xv[u].y, yv[u].y, lon, lat, z1);
+      st_stream(lv2{z0, z1}, &z[p]);
+      if (STATUS) status[p] = make_uchar2(s0, s1);
+      if (s0) report_error(err, 2 * p, s0);
+      if (s1) report_error(err, 2 * p + 1, s1);
+    }
+  }
+  if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
+    const int64_t i = n - 1;
+    int64_t zz;
+    uint8_t s = z2_index_one<LENIENT>(((const double*)x)[i], ((const double*)y)[i], lon, lat, zz);
+    ((int64_t*)z)[i] = zz;
+    if (STATUS) ((uint8_t*)status)[i] = s;
+    if (s) report_error(err, i, s);
+  }
+}
+
+template <bool LENIENT, bool STATUS>
+__global__ __launch_bounds__(TPB) void k_z2_index_s(const double* __restrict__ x, const double* __restrict__ y,
+                                                    int64_t n, int64_t* __restrict__ z, uint8_t* __restrict__ status,
+                                                    NDim lon, NDim lat, int64_t* __restrict__ err) {
+  for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < n; i += (int64_t)gridDim.x * TPB) {
+    int64_t zz;
+    uint8_t s = z2_index_one<LENIENT>(x[i], y[i], lon, lat, zz);
+    z[i] = zz;
+    if (STATUS) status[i] = s;
+    if (s) report_error(err, i, s);
+  }
+}
+
+template <int UNROLL>
+__global__ __launch_bounds__(TPB) void k_z2_invert(const lv2* __restrict__ z, int64_t n, dv2* __restrict__ x,
+                                                   dv2* __restrict__ y, NDim lon, NDim lat) {
+  const int64_t npairs = n >> 1;
+  const int64_t base = (int64_t)blockIdx.x * (TPB * UNROLL) + threadIdx.x;
+  lv2 zv[UNROLL];
+#pragma unroll
+  for (int u = 0; u < UNROLL; ++u) {
+    const int64_t p = base + (int64_t)u * TPB;
+    if (p < npairs) zv[u] = ld_stream(&z[p]);
+  }
+#pragma unroll
+  for (int u = 0; u < UNROLL; ++u) {
+    const int64_t p = base + (int64_t)u * TPB;
+    if (p < npairs) {
+      const int64_t a = zv[u].x, b = zv[u].y;
+      st_stream(dv2{denormalize(lon, z2_combine(a)), denormalize(lon, z2_combine(b))},
+                                  &x[p]);
+      st_stream(
+          dv2{denormalize(lat, z2_combine(a >> 1)), denormalize(lat, z2_combine(b >> 1))}, &y[p]);
+    }
+  }
+  if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
+    const int64_t i = n - 1;
+    const int64_t a = ((const int64_t*)z)[i];
+    ((double*)x)[i] = denormalize(lon, z2_combine(a));
+    ((double*)y)[i] = denormalize(lat, z2_combine(a >> 1));
+  }
+}
+
+__global__ __launch_bounds__(TPB) void k_z2_invert_s(const int64_t* __restrict__ z, int64_t n, double* __restrict__ x,
+                                                     double* __restrict__ y, NDim lon, NDim lat) {
+  for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < n; i += (int64_t)gridDim.x * TPB) {
+    const int64_t a = z[i];
+    x[i] = denormalize(lon, z2_combine(a));
+    y[i] = denormalize(lat, z2_combine(a >> 1));
+  }
+}
+
+// ------------------------------------------------------------------ BinnedTime
+
+template <int PERIOD, bool STATUS>
+__global__ __launch_bounds__(TPB) void k_binned_time(const int64_t* __restrict__ t, int64_t n,
+                                                     int16_t* __restrict__ bin, int64_t* __restrict__ off,
+                                                     uint8_t* __restrict__ status, int64_t* __restrict__ err) {
+  for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < n; i += (int64_t)gridDim.x * TPB) {
+    int16_t b;
+    int64_t o;
+    uint8_t s = binned_time<PERIOD>(t[i], b, o);
+    bin[i] = b;
+    off[i] = o;
+    if (STATUS) status[i] = s;
+    if (s) report_error(err, i, s);
+  }
+}
+
+// ------------------------------------------------------------------ XZ2 / XZ3
+
+__device__ __forceinline__ double clampd(double v, double lo, double hi) { return v < lo ? lo : (v > hi ? hi : v); }
+__device__ __forceinline__ double jmax(double a, double b) { return a >= b ? a : b; }  // operands never NaN/-0 here
+
+// (4^g - 1) / 3 and (8^g - 1) / 7 computed exactly in integers (math.pow(4|8, n).toLong is exact
+// for these n); the per-level steps follow from s_{i+1} = (s_i - 1) / base.
+__device__ __forceinline__ int64_t geom_sum(int base_log2, int g) {
+  int64_t p = (int64_t)1 << (base_log2 * g);
+  return (p - 1) / (base_log2 == 2 ? 3 : 7);
+}
+
+// XZ2SFC.index (z3/curve/XZ2SFC.scala:54-77) with normalize (:318-350), sequenceCode (:264-286)
+template <bool LENIENT>
+__device__ __forceinline__ uint8_t xz2_one(int g, double xmin, double ymin, double xmax, double ymax, int64_t& out) {
+  if (!(xmin <= xmax && ymin <= ymax)) { out = 0; return ST_UNORDERED; }
+  if (!(xmin >= -180.0 && xmax <= 180.0 && ymin >= -90.0 && ymax <= 90.0)) {
+    if (!LENIENT) { out = 0; return ST_OUT_OF_BOUNDS; }
+    xmin = clampd(xmin, -180.0, 180.0); ymin = clampd(ymin, -90.0, 90.0);
+    xmax = clampd(xmax, -180.0, 180.0); ymax = clampd(ymax, -90.0, 90.0);
+  }
+  const double nxmin = __ddiv_rn(__dsub_rn(xmin, -180.0), 360.0);
+  const double nymin = __ddiv_rn(__dsub_rn(ymin, -90.0), 180.0);
+  const double nxmax = __ddiv_rn(__dsub_rn(xmax, -180.0), 360.0);
+  const double nymax = __ddiv_rn(__dsub_rn(ymax, -90.0), 180.0);
+  const double maxdim = jmax(__dsub_rn(nxmax, nxmin), __dsub_rn(nymax, nymin));
+  const int32_t l1 = xz_l1(maxdim);
+  int length;
+  if (l1 >= g) {
+    length = g;
+  } else {
+    const double w2 = ldexp(1.0, -(l1 + 1));  // math.pow(0.5, l1 + 1), exact
+    auto pred = [w2](double mn, double mx) {
+      return mx <= __dadd_rn(__dmul_rn(floor(__ddiv_rn(mn, w2)), w2), __dmul_rn(2.0, w2));
+    };
+    length = (pred(nxmin, nxmax) && pred(nymin, nymax)) ? l1 + 1 : l1;
+  }
+  double x0 = 0.0, y0 = 0.0, x1 = 1.0, y1 = 1.0;
+  int64_t cs = 0, step = geom_sum(2, g);
+  for (int i = 0; i < length; ++i) {
+    const double xc = __dadd_rn(x0, x1) * 0.5, yc = __dadd_rn(y0, y1) * 0.5;
+    const bool xl = nxmin < xc, yl = nymin < yc;
+    cs += 1 + (int64_t)((xl ? 0 : 1) + (yl ? 0 : 2)) * step;
+    if (xl) x1 = xc; else x0 = xc;
+    if (yl) y1 = yc; else y0 = yc;
+    step = (step - 1) >> 2;
+  }
+  out = cs;
+  return ST_OK;
+}
+
+// XZ3SFC.index (z3/curve/XZ3SFC.scala:53-76) with normalize (:338-380), sequenceCode (:275-304)
+template <bool LENIENT>
+__device__ __forceinline__ uint8_t xz3_one(int g, double zhi, double xmin, double ymin, double zmin, double xmax,
+                                           double ymax, double zmax, int64_t& out) {
+  if (!(xmin <= xmax && ymin <= ymax && zmin <= zmax)) { out = 0; return ST_UNORDERED; }
+  if (!(xmin >= -180.0 && xmax <= 180.0 && ymin >= -90.0 && ymax <= 90.0 && zmin >= 0.0 && zmax <= zhi)) {
+    if (!LENIENT) { out = 0; return ST_OUT_OF_BOUNDS; }
+    xmin = clampd(xmin, -180.0, 180.0); ymin = clampd(ymin, -90.0, 90.0); zmin = clampd(zmin, 0.0, zhi);
+    xmax = clampd(xmax, -180.0, 180.0); ymax = clampd(ymax, -90.0, 90.0); zmax = clampd(zmax, 0.0, zhi);
+  }
+  const double zsize = __dsub_rn(zhi, 0.0);
+  const double nxmin = __ddiv_rn(__dsub_rn(xmin, -180.0), 360.0);
+  const double nymin = __ddiv_rn(__dsub_rn(ymin, -90.0), 180.0);
+  const double nzmin = __ddiv_rn(__dsub_rn(zmin, 0.0), zsize);
+  const double nxmax = __ddiv_rn(__dsub_rn(xmax, -180.0), 360.0);
+  const double nymax = __ddiv_rn(__dsub_rn(ymax, -90.0), 180.0);
+  const double nzmax = __ddiv_rn(__dsub_rn(zmax, 0.0), zsize);
+  const double maxdim = jmax(jmax(__dsub_rn(nxmax, nxmin), __dsub_rn(nymax, nymin)), __dsub_rn(nzmax, nzmin));
+  const int32_t l1 = xz_l1(maxdim);
+  int length;
+  if (l1 >= g) {
+    length = g;
+  } else {
+    const double w2 = ldexp(1.0, -(l1 + 1));
+    auto pred = [w2](double mn, double mx) {
+      return mx <= __dadd_rn(__dmul_rn(floor(__ddiv_rn(mn, w2)), w2), __dmul_rn(2.0, w2));
+    };
+    length = (pred(nxmin, nxmax) && pred(nymin, nymax) && pred(nzmin, nzmax)) ? l1 + 1 : l1;
+  }
+  double x0 = 0.0, y0 = 0.0, z0 = 0.0, x1 = 1.0, y1 = 1.0, z1 = 1.0;
+  int64_t cs = 0, step = geom_sum(3, g);
+  for (int i = 0; i < length; ++i) {
+    const double xc = __dadd_rn(x0, x1) * 0.5, yc = __dadd_rn(y0, y1) * 0.5, zc = __dadd_rn(z0, z1) * 0.5;
+    const bool xl = nxmin < xc, yl = nymin < yc, zl = nzmin < zc;
+    cs += 1 + (int64_t)((xl ? 0 : 1) + (yl ? 0 : 2) + (zl ? 0 : 4)) * step;
+    if (xl) x1 = xc; else x0 = xc;
+    if (yl) y1 = yc; else y0 = yc;
+    if (zl) z1 = zc; else z0 = zc;
+    step = (step - 1) >> 3;
+  }
+  out = cs;
+  return ST_OK;
+}
+
+template <bool LENIENT, bool STATUS>
+__global__ __launch_bounds__(TPB) void k_xz2_index(const double* __restrict__ xmin, const double* __restrict__ ymin,
+                                                   const double* __restrict__ xmax, const double* __restrict__ ymax,
+                                                   int64_t n, int g, int64_t* __restrict__ out,
+                                                   uint8_t* __restrict__ status, int64_t* __restrict__ err) {
+  for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < n; i += (int64_t)gridDim.x * TPB) {
+    int64_t o;
+    uint8_t s = xz2_one<LENIENT>(g, xmin[i], ymin[i], xmax[i], ymax[i], o);
+    out[i] = o;
+    if (STATUS) status[i] = s;
+    if (s) report_error(err, i, s);
+  }
+}
+
+template <bool LENIENT, bool STATUS>
+__global__ __launch_bounds__(TPB) void k_xz3_index(const double* __restrict__ xmin, const double* __restrict__ ymin,
+                                                   const double* __restrict__ zmin, const double* __restrict__ xmax,
+                                                   const double* __restrict__ ymax, const double* __restrict__ zmax,
+                                                   int64_t n, int g, double zhi, int64_t* __restrict__ out,
+                                                   uint8_t* __restrict__ status, int64_t* __restrict__ err) {
+  for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < n; i += (int64_t)gridDim.x * TPB) {
+    int64_t o;
+    uint8_t s = xz3_one<LENIENT>(g, zhi, xmin[i], ymin[i], zmin[i], xmax[i], ymax[i], zmax[i], o);
+    out[i] = o;
+    if (STATUS) status[i] = s;
+    if (s) report_error(err, i, s);
+  }
+}
+
+// ------------------------------------------------------------------ host-side launchers
+
+constexpr int UNROLL_KEY = 4;
+constexpr int UNROLL_INV = 4;
+
+inline unsigned stride_grid(int64_t n) {
+  int64_t b = (n + TPB - 1) / TPB;
+  if (b > 256 * 16) b = 256 * 16;
+  return (unsigned)(b < 1 ? 1 : b);
+}
+
+template <int PERIOD, bool LENIENT, bool STATUS>
+void launch_key(hipStream_t s, const double* x, const double* y, const int64_t* t, int64_t n, int16_t* bin,
+                int64_t* z, uint8_t* status, NDim lon, NDim lat, NDim tim, int64_t* err, bool vec) {
+  if (vec) {
+    unsigned grid = grid_for((n >> 1) > 0 ? (n >> 1) : 1, (int64_t)TPB * UNROLL_KEY);
+    hipLaunchKernelGGL((k_z3_index_key<PERIOD, LENIENT, STATUS, UNROLL_KEY>), dim3(grid), dim3(TPB), 0, s,
+                       (const dv2*)x, (const dv2*)y, (const lv2*)t, n, (short2*)bin, (lv2*)z,
+                       (uchar2*)status, lon, lat, tim, err);
+  } else {
+    hipLaunchKernelGGL((k_z3_index_key_s<PERIOD, LENIENT, STATUS>), dim3(stride_grid(n)), dim3(TPB), 0, s, x, y, t,
+                       n, bin, z, status, lon, lat, tim, err);
+  }
+}
+
+template <int PERIOD>
+void launch_key_p(hipStream_t s, const double* x, const double* y, const int64_t* t, int64_t n, int16_t* bin,
+                  int64_t* z, uint8_t* status, NDim lon, NDim lat, NDim tim, int64_t* err, bool lenient, bool vec) {
+  if (lenient) {
+    if (status) launch_key<PERIOD, true, true>(s, x, y, t, n, bin, z, status, lon, lat, tim, err, vec);
+    else launch_key<PERIOD, true, false>(s, x, y, t, n, bin, z, status, lon, lat, tim, err, vec);
+  } else {
+    if (status) launch_key<PERIOD, false, true>(s, x, y, t, n, bin, z, status, lon, lat, tim, err, vec);
+    else launch_key<PERIOD, false, false>(s, x, y, t, n, bin, z, status, lon, lat, tim, err, vec);
+  }
+}
+
+inline bool valid_period(int p) { return p >= DAY && p <= YEAR; }
+
+inline NDim lon_dim(int p) { return make_ndim(-180.0, 180.0, p); }
+inline NDim lat_dim(int p) { return make_ndim(-90.0, 90.0, p); }
+inline NDim time_dim(int period, int p) { return make_ndim(0.0, (double)max_offset(period), p); }
+
+}  // namespace gm
+
+using namespace gm;
+
+extern "C" {
+
+int gm_z3_index_key(gm_ctx* ctx, const double* x, const double* y, const int64_t* t_ms, int64_t n, int period,
+                    int lenient, int16_t* bin, int64_t* z, uint8_t* status, gm_batch_status* summary) {
+  if (!ctx || n < 0 || !valid_period(period)) return GM_E_INVALID;
+  if (n == 0) { if (summary) *summary = gm_batch_status{0, -1, 0, 0}; return GM_OK; }
+  if (!x || !y || !t_ms || !bin || !z) return GM_E_INVALID;
+  int rc = begin_summary(ctx, summary);
+  if (rc) return rc;
+  const NDim lon = lon_dim(21), lat = lat_dim(21), tim = time_dim(period, 21);
+  const bool vec = aligned16(x) && aligned16(y) && aligned16(t_ms) && aligned16(z) &&
+                   (((uintptr_t)bin & 3u) == 0) && (((uintptr_t)status & 1u) == 0);
+  switch (period) {
+    case DAY: launch_key_p<DAY>(ctx->stream, x, y, t_ms, n, bin, z, status, lon, lat, tim, ctx->d_err, lenient, vec); break;
+    case WEEK: launch_key_p<WEEK>(ctx->stream, x, y, t_ms, n, bin, z, status, lon, lat, tim, ctx->d_err, lenient, vec); break;
+    case MONTH: launch_key_p<MONTH>(ctx->stream, x, y, t_ms, n, bin, z, status, lon, lat, tim, ctx->d_err, lenient, vec); break;
+    default: launch_key_p<YEAR>(ctx->stream, x, y, t_ms, n, bin, z, status, lon, lat, tim, ctx->d_err, lenient, vec); break;
+  }
+  GM_CHECK_LAUNCH();
+  return end_summary(ctx, summary);
+}
+
+int gm_z3_index(gm_ctx* ctx, const double* x, const double* y, const int64_t* t, int64_t n, int period,
+                int precision, int lenient, int64_t* z, uint8_t* status, gm_batch_status* summary) {
+  if (!ctx || n < 0 || !valid_period(period) || precision < 1 || precision > 21) return GM_E_INVALID;
+  if (n == 0) { if (summary) *summary = gm_batch_status{0, -1, 0, 0}; return GM_OK; }
+  if (!x || !y || !t || !z) return GM_E_INVALID;
+  int rc = begin_summary(ctx, summary);
+  if (rc) return rc;
+  const NDim lon = lon_dim(precision), lat = lat_dim(precision), tim = time_dim(period, precision);
+  const unsigned grid = stride_grid(n);
+  if (lenient) {
+    if (status) hipLaunchKernelGGL((k_z3_index<true, true>), dim3(grid), dim3(TPB), 0, ctx->stream, x, y, t, n, z, status, lon, lat, tim, ctx->d_err);
+    else hipLaunchKernelGGL((k_z3_index<true, false>), dim3(grid), dim3(TPB), 0, ctx->stream, x, y, t, n, z, status, lon, lat, tim, ctx->d_err);
+  } else {
+    if (status) hipLaunchKernelGGL((k_z3_index<false, true>), dim3(grid), dim3(TPB), 0, ctx->stream, x, y, t, n, z, status, lon, lat, tim, ctx->d_err);
+    else hipLaunchKernelGGL((k_z3_index<false, false>), dim3(grid), dim3(TPB), 0, ctx->stream, x, y, t, n, z, status, lon, lat, tim, ctx->d_err);
+  }
+  GM_CHECK_LAUNCH();
+  return end_summary(ctx, summary);
+}
+
+int gm_z3_invert(gm_ctx* ctx, const int64_t* z, int64_t n, int period, int precision, double* x, double* y,
+                 int64_t* t) {
+  if (!ctx || n < 0 || !valid_period(period) || precision < 1 || precision > 21) return GM_E_INVALID;
+  if (n == 0) return GM_OK;
+  if (!z || !x || !y || !t) return GM_E_INVALID;
+  const NDim lon = lon_dim(precision), lat = lat_dim(precision), tim = time_dim(period, precision);
+  if (aligned16(z) && aligned16(x) && aligned16(y) && aligned16(t)) {
+    unsigned grid = grid_for((n >> 1) > 0 ? (n >> 1) : 1, (int64_t)TPB * UNROLL_INV);
+    hipLaunchKernelGGL((k_z3_invert<UNROLL_INV>), dim3(grid), dim3(TPB), 0, ctx->stream, (const lv2*)z, n,
+                       (dv2*)x, (dv2*)y, (lv2*)t, lon, lat, tim);
+  } else {
+    hipLaunchKernelGGL(k_z3_invert_s, dim3(stride_grid(n)), dim3(TPB), 0, ctx->stream, z, n, x, y, t, lon, lat, tim);
+  }
+  GM_CHECK_LAUNCH();
+  return GM_OK;
+}
+
+int gm_z2_index(gm_ctx* ctx, const double* x, const double* y, int64_t n, int precision, int lenient, int64_t* z,
+                uint8_t* status, gm_batch_status* summary) {
+  if (!ctx || n < 0 || precision < 1 || precision > 31) return GM_E_INVALID;
+  if (n == 0) { if (summary) *summary = gm_batch_status{0, -1, 0, 0}; return GM_OK; }
+  if (!x || !y || !z) return GM_E_INVALID;
+  int rc = begin_summary(ctx, summary);
+  if (rc) return rc;
+  const NDim lon = lon_dim(precision), lat = lat_dim(precision);
+  const bool vec = aligned16(x) && aligned16(y) && aligned16(z) && (((uintptr_t)status & 1u) == 0);
+  hipStream_t s = ctx->stream;
+  if (vec) {
+    unsigned grid = grid_for((n >> 1) > 0 ? (n >> 1) : 1, (int64_t)TPB * UNROLL_KEY);
+    const dv2* x2 = (const dv2*)x; const dv2* y2 = (const dv2*)y;
+    lv2* z2 = (lv2*)z; uchar2* s2 = (uchar2*)status;
+    if (lenient) {
+      if (status) hipLaunchKernelGGL((k_z2_index<true, true, UNROLL_KEY>), dim3(grid), dim3(TPB), 0, s, x2, y2, n, z2, s2, lon, lat, ctx->d_err);
+      else hipLaunchKernelGGL((k_z2_index<true, false, UNROLL_KEY>), dim3(grid), dim3(TPB), 0, s, x2, y2, n, z2, s2, lon, lat, ctx->d_err);
+    } else {
+      if (status) hipLaunchKernelGGL((k_z2_index<false, true, UNROLL_KEY>), dim3(grid), dim3(TPB), 0, s, x2, y2, n, z2, s2, lon, lat, ctx->d_err);
+      else hipLaunchKernelGGL((k_z2_index<false, false, UNROLL_KEY>), dim3(grid), dim3(TPB), 0, s, x2, y2, n, z2, s2, lon, lat, ctx->d_err);
+    }
+  } else {
+    unsigned grid = stride_grid(n);
+    if (lenient) {
+      if (status) hipLaunchKernelGGL((k_z2_index_s<true, true>), dim3(grid), dim3(TPB), 0, s, x, y, n, z, status, lon, lat, ctx->d_err);
+      else hipLaunchKernelGGL((k_z2_index_s<true, false>), dim3(grid), dim3(TPB), 0, s, x, y, n, z, status, lon, lat, ctx->d_err);
+    } else {
+      if (status) hipLaunchKernelGGL((k_z2_index_s<false, true>), dim3(grid), dim3(TPB), 0, s, x, y, n, z, status, lon, lat, ctx->d_err);
+      else hipLaunchKernelGGL((k_z2_index_s<false, false>), dim3(grid), dim3(TPB), 0, s, x, y, n, z, status, lon, lat, ctx->d_err);
+    }
+  }
+  GM_CHECK_LAUNCH();
+  return end_summary(ctx, summary);
+}
+
+int gm_z2_invert(gm_ctx* ctx, const int64_t* z, int64_t n, int precision, double* x, double* y) {
+  if (!ctx || n < 0 || precision < 1 || precision > 31) return GM_E_INVALID;
+  if (n == 0) return GM_OK;
+  if (!z || !x || !y) return GM_E_INVALID;
+  const NDim lon = lon_dim(precision), lat = lat_dim(precision);
+  if (aligned16(z) && aligned16(x) && aligned16(y)) {
+    unsigned grid = grid_for((n >> 1) > 0 ? (n >> 1) : 1, (int64_t)TPB * UNROLL_INV);
+    hipLaunchKernelGGL((k_z2_invert<UNROLL_INV>), dim3(grid), dim3(TPB), 0, ctx->stream, (const lv2*)z, n,
+                       (dv2*)x, (dv2*)y, lon, lat);
+  } else {
+    hipLaunchKernelGGL(k_z2_invert_s, dim3(stride_grid(n)), dim3(TPB), 0, ctx->stream, z, n, x, y, lon, lat);
+  }
+  GM_CHECK_LAUNCH();
+  return GM_OK;
+}
+
+int gm_binned_time(gm_ctx* ctx, const int64_t* t_ms, int64_t n, int period, int16_t* bin, int64_t* offset,
+                   uint8_t* status, gm_batch_status* summary) {
+  if (!ctx || n < 0 || !valid_period(period)) return GM_E_INVALID;
+  if (n == 0) { if (summary) *summary = gm_batch_status{0, -1, 0, 0}; return GM_OK; }
+  if (!t_ms || !bin || !offset) return GM_E_INVALID;
+  int rc = begin_summary(ctx, summary);
+  if (rc) return rc;
+  const unsigned grid = stride_grid(n);
+  hipStream_t s = ctx->stream;
+#define GM_BT(P)                                                                                          \
+  if (status) hipLaunchKernelGGL((k_binned_time<P, true>), dim3(grid), dim3(TPB), 0, s, t_ms, n, bin, offset, status, ctx->d_err); \
+  else hipLaunchKernelGGL((k_binned_time<P, false>), dim3(grid), dim3(TPB), 0, s, t_ms, n, bin, offset, status, ctx->d_err);
+  switch (period) {
+    case DAY: GM_BT(DAY) break;
+    case WEEK: GM_BT(WEEK) break;
+    case MONTH: GM_BT(MONTH) break;
+    default: GM_BT(YEAR) break;
+  }
+#undef GM_BT
+  GM_CHECK_LAUNCH();
+  return end_summary(ctx, summary);
+}
+
+int gm_xz2_index(gm_ctx* ctx, const double* xmin, const double* ymin, const double* xmax, const double* ymax,
+                 int64_t n, int g, int lenient, int64_t* out, uint8_t* status, gm_batch_status* summary) {
+  if (!ctx || n < 0 || g < 1 || g > 30) return GM_E_INVALID;
+  if (n == 0) { if (summary) *summary = gm_batch_status{0, -1, 0, 0}; return GM_OK; }
+  if (!xmin || !ymin || !xmax || !ymax || !out) return GM_E_INVALID;
+  int rc = begin_summary(ctx, summary);
+  if (rc) return rc;
+  const unsigned grid = stride_grid(n);
+  hipStream_t s = ctx->stream;
+  if (lenient) {
+    if (status) hipLaunchKernelGGL((k_xz2_index<true, true>), dim3(grid), dim3(TPB), 0, s, xmin, ymin, xmax, ymax, n, g, out, status, ctx->d_err);
+    else hipLaunchKernelGGL((k_xz2_index<true, false>), dim3(grid), dim3(TPB), 0, s, xmin, ymin, xmax, ymax, n, g, out, status, ctx->d_err);
+  } else {
+    if (status) hipLaunchKernelGGL((k_xz2_index<false, true>), dim3(grid), dim3(TPB), 0, s, xmin, ymin, xmax, ymax, n, g, out, status, ctx->d_err);
+    else hipLaunchKernelGGL((k_xz2_index<false, false>), dim3(grid), dim3(TPB), 0, s, xmin, ymin, xmax, ymax, n, g, out, status, ctx->d_err);
+  }
+  GM_CHECK_LAUNCH();
+  return end_summary(ctx, summary);
+}
+
+int gm_xz3_index(gm_ctx* ctx, const double* xmin, const double* ymin, const double* zmin, const double* xmax,
+                 const double* ymax, const double* zmax, int64_t n, int g, int period, int lenient, int64_t* out,
+                 uint8_t* status, gm_batch_status* summary) {
+  if (!ctx || n < 0 || g < 1 || g > 20 || !valid_period(period)) return GM_E_INVALID;
+  if (n == 0) { if (summary) *summary = gm_batch_status{0, -1, 0, 0}; return GM_OK; }
+  if (!xmin || !ymin || !zmin || !xmax || !ymax || !zmax || !out) return GM_E_INVALID;
+  int rc = begin_summary(ctx, summary);
+  if (rc) return rc;
+  const unsigned grid = stride_grid(n);
+  const double zhi = (double)max_offset(period);
+  hipStream_t s = ctx->stream;
+  if (lenient) {
+    if (status) hipLaunchKernelGGL((k_xz3_index<true, true>), dim3(grid), dim3(TPB), 0, s, xmin, ymin, zmin, xmax, ymax, zmax, n, g, zhi, out, status, ctx->d_err);
+    else hipLaunchKernelGGL((k_xz3_index<true, false>), dim3(grid), dim3(TPB), 0, s, xmin, ymin, zmin, xmax, ymax, zmax, n, g, zhi, out, status, ctx->d_err);
+  } else {
+    if (status) hipLaunchKernelGGL((k_xz3_index<false, true>), dim3(grid), dim3(TPB), 0, s, xmin, ymin, zmin, xmax, ymax, zmax, n, g, zhi, out, status, ctx->d_err);
+    else hipLaunchKernelGGL((k_xz3_index<false, false>), dim3(grid), dim3(TPB), 0, s, xmin, ymin, zmin, xmax, ymax, zmax, n, g, zhi, out, status, ctx->d_err);
+  }
+  GM_CHECK_LAUNCH();
+  return end_summary(ctx, summary);
+}
+
+}  // extern "C"

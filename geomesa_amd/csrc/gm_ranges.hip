@@ -1,0 +1,889 @@
+// gm_ranges.hip -- batched range decomposition: ZN.zranges (Z2/Z3) and XZ2/XZ3 ranges on gfx950.
+//
+// One 256-thread workgroup per query.  The Scala code walks a FIFO queue one node at a time
+// (ZN.scala:193-218, XZ2SFC.scala:205-227) and its maxRanges budget truncates at an exact FIFO
+// position.  Here a whole tree level is processed in parallel and the FIFO semantics are
+// reconstructed with block-wide prefix sums:
+//
+//   Z curves   after node i of a level the queue holds (K-i-1) level nodes + the queued children,
+//              so the budget fires at the first i with
+//                 nR + CC(i) + CO(i) + (K - i - 1) >= rangeStop          (ZN.scala:214)
+//              (CC/CO = inclusive counts of contained / overlapping children).  Nodes after i are
+//              bottomed out as overlapping ranges at their own level, queued children at theirs.
+//   XZ curves  the budget is checked before every element (ranges.size < rangeStop,
+//              XZ2SFC.scala:205), so the first unprocessed element is the first i with
+//                 nR + A(i-1) >= rangeStop        (A = inclusive count of non-disjoint elements);
+//              bottom-out emits full intervals at the current and the next level (:219-227).
+//
+// Emitted ranges are tree nodes that never nest, so after the walk they are disjoint; an LDS
+// bitonic sort on `lower` (global memory above 4096 ranges) followed by a parallel adjacency merge
+// reproduces the sort + merge of ZN.scala:221-241 / XZ2SFC.scala:231-249 exactly.
+//
+// Frontier and range lists live in per-query global workspaces (HBM is plentiful); the zbounds /
+// normalized query windows sit in LDS.
+#include <algorithm>
+#include <vector>
+
+#include "gm_internal.hpp"
+
+namespace gm {
+
+constexpr int RTPB = 256;
+constexpr int RNW = RTPB / 64;
+constexpr int MAXB = 256;       // zbounds / windows per query
+constexpr int LDS_SORT = 4096;  // ranges sorted in LDS; larger lists sort in global memory
+
+enum : int32_t { QS_OK = 0, QS_OUT_OF_BOUNDS = 1, QS_UNORDERED = 3, QS_CAPACITY = 4, QS_TOO_MANY_BOUNDS = 5 };
+
+// ------------------------------------------------------------------ block helpers
+
+__device__ __forceinline__ int64_t block_exscan(int64_t v, int64_t* s_tmp, int64_t& total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int64_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    int64_t y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) s_tmp[w] = x;
+  __syncthreads();
+  int64_t pre = 0, tot = 0;
+#pragma unroll
+  for (int k = 0; k < RNW; ++k) {
+    const int64_t t = s_tmp[k];
+    if (k < w) pre += t;
+    tot += t;
+  }
+  __syncthreads();
+  total = tot;
+  return pre + x - v;
+}
+
+// Java `(1L << s) - 1` with the shift distance masked to 6 bits
+__device__ __forceinline__ int64_t low_mask(int s) { return (int64_t)(((uint64_t)1 << (s & 63)) - 1u); }
+__device__ __forceinline__ int64_t jshl(int64_t v, int s) { return (int64_t)((uint64_t)v << (s & 63)); }
+
+template <int D>
+__device__ __forceinline__ int32_t zdim(int64_t z, int d) {
+  return D == 3 ? z3_combine(z >> d) : z2_combine(z >> d);
+}
+
+// Z3.contains / Z2.contains (Z3.scala:93-98, Z2.scala:186-189) on decoded dims
+template <int D>
+__device__ __forceinline__ bool z_contains(const int32_t* b, int64_t v) {
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    const int32_t x = zdim<D>(v, d);
+    if (!(x >= b[d] && x <= b[D + d])) return false;
+  }
+  return true;
+}
+
+// bitonic sort of (key, idx) pairs, P a power of two, keys padded with INT64_MAX
+template <class K, class I>
+__device__ void bitonic(K* key, I* idx, int P) {
+  for (int k = 2; k <= P; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = threadIdx.x; i < P; i += RTPB) {
+        const int ixj = i ^ j;
+        if (ixj > i) {
+          const bool up = (i & k) == 0;
+          const int64_t a = key[i], b = key[ixj];
+          if ((a > b) == up) {
+            key[i] = b; key[ixj] = a;
+            const auto t = idx[i]; idx[i] = idx[ixj]; idx[ixj] = t;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// sort the n ranges of this query by lower and merge adjacent ones into out (ZN.scala:221-241);
+// returns the merged count (same on every thread)
+__device__ int sort_merge(const int64_t* rlo, const int64_t* rhi, const uint8_t* rc, int n, int64_t* gkey,
+                          int32_t* gidx, gm_range* out, int64_t* s_key, int16_t* s_idx, int64_t* s_tmp) {
+  if (n == 0) return 0;
+  int P = 1;
+  while (P < n) P <<= 1;
+  const bool lds = P <= LDS_SORT;
+  for (int i = threadIdx.x; i < P; i += RTPB) {
+    const int64_t k = i < n ? rlo[i] : INT64_MAX;
+    if (lds) { s_key[i] = k; s_idx[i] = (int16_t)i; }
+    else { gkey[i] = k; gidx[i] = i; }
+  }
+  __syncthreads();
+  if (lds) bitonic(s_key, s_idx, P);
+  else bitonic(gkey, gidx, P);
+  // run starts: lower > previous upper + 1 (Java long wrap); sorted disjoint ranges have increasing
+  // uppers, so the previous upper is the merged run's max (ZN.scala:228-230)
+  int64_t* run_of = lds ? s_key : gkey;  // keys are dead after the sort: reuse for run ids
+  int64_t base = 0;
+  for (int c = 0; c < n; c += RTPB) {
+    const int j = c + threadIdx.x;
+    int start = 0, src = 0;
+    if (j < n) {
+      src = lds ? (int)(uint16_t)s_idx[j] : gidx[j];
+      if (j == 0) start = 1;
+      else {
+        const int prev = lds ? (int)(uint16_t)s_idx[j - 1] : gidx[j - 1];
+        start = !(rlo[src] <= (int64_t)((uint64_t)rhi[prev] + 1u));
+      }
+    }
+    int64_t tot;
+    const int64_t ex = block_exscan(start, s_tmp, tot);
+    if (j < n) {
+      const int64_t run = base + ex + start - 1;
+      run_of[j] = run;
+      if (start) { out[run].lower = rlo[src]; out[run].contained = 1; out[run].reserved = 0; }
+      bool last = (j == n - 1);
+      if (!last) {
+        const int nx = lds ? (int)(uint16_t)s_idx[j + 1] : gidx[j + 1];
+        last = !(rlo[nx] <= (int64_t)((uint64_t)rhi[src] + 1u));
+      }
+      if (last) out[run].upper = rhi[src];
+    }
+    base += tot;
+  }
+  __syncthreads();
+  // contained = AND over the run
+  for (int j = threadIdx.x; j < n; j += RTPB) {
+    const int src = lds ? (int)(uint16_t)s_idx[j] : gidx[j];
+    if (!rc[src]) out[run_of[j]].contained = 0;
+  }
+  __syncthreads();
+  const int total_runs = (int)base;
+  return total_runs;
+}
+
+// ------------------------------------------------------------------ Z ranges kernel
+
+struct ZRangesArgs {
+  const int32_t* box_off;   // [nq + 1]
+  const double* xy;         // 4 per box
+  const int32_t* time_off;  // [nq + 1] (Z3 only)
+  const int64_t* t;         // 2 per interval
+  int64_t q0;               // first query of this chunk
+  NDim lon, lat, tim;
+  int range_precision, range_stop, recurse_stop;
+  int64_t fcap, rcap;
+  int64_t* fa;              // frontier ping
+  int64_t* fb;              // frontier pong
+  int64_t* rlo;
+  int64_t* rhi;
+  uint8_t* rc;
+  int64_t* gkey;
+  int32_t* gidx;
+  gm_range* out;            // merged ranges, rcap per query
+  int32_t* out_count;
+  int32_t* status;
+};
+
+template <int D>
+__global__ __launch_bounds__(RTPB) void k_zranges(ZRangesArgs a) {
+  __shared__ int64_t s_zb[2 * MAXB];
+  __shared__ int32_t s_dim[2 * D * MAXB];  // decoded min dims, max dims per bound
+  __shared__ int64_t s_tmp[RNW];
+  __shared__ int s_err, s_stop;
+  __shared__ int64_t s_prefix;
+  __shared__ int s_common;
+  __shared__ int64_t s_key[LDS_SORT];
+  __shared__ int16_t s_idx[LDS_SORT];
+
+  const int64_t qc = blockIdx.x;            // query within the chunk
+  const int64_t q = a.q0 + qc;
+  int64_t* F = a.fa + qc * a.fcap;
+  int64_t* G = a.fb + qc * a.fcap;
+  int64_t* rlo = a.rlo + qc * a.rcap;
+  int64_t* rhi = a.rhi + qc * a.rcap;
+  uint8_t* rc = a.rc + qc * a.rcap;
+
+  const int b0 = a.box_off[q], nbx = a.box_off[q + 1] - b0;
+  int t0 = 0, ntm = 1;
+  if (D == 3) { t0 = a.time_off[q]; ntm = a.time_off[q + 1] - t0; }
+  const int nb = nbx * ntm;
+  if (threadIdx.x == 0) s_err = (nb > MAXB) ? QS_TOO_MANY_BOUNDS : QS_OK;
+  __syncthreads();
+  if (s_err || nb <= 0) {
+    if (threadIdx.x == 0) { a.out_count[qc] = 0; a.status[qc] = s_err; }
+    return;
+  }
+  // zbounds: Z3SFC.ranges builds ZRange(index(xmin, ymin, tmin), index(xmax, ymax, tmax)) for the
+  // cross product xy x t, non-lenient (Z3SFC.scala:63-65); Z2SFC.ranges likewise (Z2SFC.scala:151)
+  for (int j = threadIdx.x; j < nb; j += RTPB) {
+    const double* bx = a.xy + 4 * (int64_t)(b0 + j / ntm);
+    int64_t lo = 0, hi = 0;
+    uint8_t st;
+    if (D == 3) {
+      const int64_t* tt = a.t + 2 * (int64_t)(t0 + j % ntm);
+      auto idx = [&](double x, double y, int64_t tv, int64_t& z) -> uint8_t {
+        const double td = (double)tv;
+        if (!(x >= a.lon.min && x <= a.lon.max && y >= a.lat.min && y <= a.lat.max && td >= a.tim.min &&
+              td <= a.tim.max))
+          return ST_OUT_OF_BOUNDS;
+        z = z3_apply(normalize(a.lon, x), normalize(a.lat, y), normalize(a.tim, td));
+        return ST_OK;
+      };
+      st = idx(bx[0], bx[1], tt[0], lo);
+      if (!st) st = idx(bx[2], bx[3], tt[1], hi);
+    } else {
+      auto idx = [&](double x, double y, int64_t& z) -> uint8_t {
+        if (!(x >= a.lon.min && x <= a.lon.max && y >= a.lat.min && y <= a.lat.max)) return ST_OUT_OF_BOUNDS;
+        z = z2_apply(normalize(a.lon, x), normalize(a.lat, y));
+        return ST_OK;
+      };
+      st = idx(bx[0], bx[1], lo);
+      if (!st) st = idx(bx[2], bx[3], hi);
+    }
+    if (!st && lo > hi) st = QS_UNORDERED;  // ZRange require(min <= max) (package.scala:220)
+    if (st) atomicMax(&s_err, (int)st);
+    s_zb[2 * j] = lo;
+    s_zb[2 * j + 1] = hi;
+    for (int d = 0; d < D; ++d) {
+      s_dim[(2 * D) * j + d] = zdim<D>(lo, d);
+      s_dim[(2 * D) * j + D + d] = zdim<D>(hi, d);
+    }
+  }
+  __syncthreads();
+  if (s_err) {
+    if (threadIdx.x == 0) { a.out_count[qc] = 0; a.status[qc] = s_err; }
+    return;
+  }
+  // longestCommonPrefix (ZN.scala:272-281)
+  if (threadIdx.x == 0) {
+    const int total_bits = D == 3 ? 63 : 62;
+    int shift = total_bits - D;
+    int64_t head = (int64_t)((uint64_t)s_zb[0] >> (shift & 63));
+    for (;;) {
+      bool all = true;
+      for (int i = 1; i < 2 * nb; ++i)
+        if ((int64_t)((uint64_t)s_zb[i] >> (shift & 63)) != head) { all = false; break; }
+      if (!(all && shift > -1)) break;
+      shift -= D;
+      head = (int64_t)((uint64_t)s_zb[0] >> (shift & 63));
+    }
+    shift += D;
+    s_prefix = s_zb[0] & jshl(INT64_MAX, shift);
+    s_common = 64 - shift;
+  }
+  __syncthreads();
+
+  auto is_contained = [&](int64_t mn, int64_t mx) {
+    for (int i = 0; i < nb; ++i)
+      if (z_contains<D>(&s_dim[2 * D * i], mn) && z_contains<D>(&s_dim[2 * D * i], mx)) return true;
+    return false;
+  };
+  auto is_overlapped = [&](int64_t mn, int64_t mx) {
+    for (int i = 0; i < nb; ++i) {
+      const int32_t* b = &s_dim[2 * D * i];
+      bool ok = true;
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        const int32_t v1 = zdim<D>(mn, d), v2 = zdim<D>(mx, d);
+        const int32_t lo = b[d] > v1 ? b[d] : v1, hi = b[D + d] < v2 ? b[D + d] : v2;
+        ok = ok && (lo <= hi);
+      }
+      if (ok) return true;
+    }
+    return false;
+  };
+
+  const int64_t range_stop = a.range_stop;
+  int offset = 64 - s_common;
+  int64_t nR = 0, K = 0;
+  // initial level: checkValue(commonPrefix, 0) (ZN.scala:183)
+  if (threadIdx.x == 0) {
+    const int64_t mn = s_prefix, mx = mn | low_mask(offset);
+    if (is_contained(mn, mx) || offset < 64 - a.range_precision) {
+      rlo[0] = mn; rhi[0] = mx; rc[0] = 1; s_stop = 1;
+    } else if (is_overlapped(mn, mx)) {
+      F[0] = mn; s_stop = 2;
+    } else {
+      s_stop = 0;
+    }
+  }
+  __syncthreads();
+  if (s_stop == 1) nR = 1;
+  if (s_stop == 2) K = 1;
+  offset -= D;
+  int level = 0;
+  bool done = (K == 0);
+  int err = QS_OK;
+  while (!done) {
+    // process level: K nodes in F at child offset `offset`; children -> G
+    int64_t cc_carry = 0, co_carry = 0;
+    int64_t stop_at = -1;
+    for (int64_t c = 0; c < K; c += RTPB) {
+      const int64_t i = c + threadIdx.x;
+      uint32_t cmask = 0, omask = 0;
+      int64_t p = 0;
+      if (i < K) {
+        p = F[i];
+        for (int qd = 0; qd < (1 << D); ++qd) {
+          const int64_t mn = p | jshl(qd, offset);
+          const int64_t mx = mn | low_mask(offset);
+          if (is_contained(mn, mx) || offset < 64 - a.range_precision) cmask |= 1u << qd;
+          else if (is_overlapped(mn, mx)) omask |= 1u << qd;
+        }
+      }
+      const int cc = __popc(cmask), co = __popc(omask);
+      int64_t cct, cot;
+      const int64_t ccx = block_exscan(cc, s_tmp, cct);
+      const int64_t cox = block_exscan(co, s_tmp, cot);
+      // budget (ZN.scala:214) after node i
+      if (threadIdx.x == 0) s_stop = INT32_MAX;
+      __syncthreads();
+      if (i < K) {
+        const int64_t f = nR + cc_carry + ccx + cc + co_carry + cox + co + (K - i - 1);
+        if (f >= range_stop) atomicMin(&s_stop, (int)threadIdx.x);
+      }
+      __syncthreads();
+      const int sl = s_stop;
+      const bool emit = (i < K) && (sl == INT32_MAX || (int)threadIdx.x <= sl);
+      if (emit) {
+        int64_t rpos = nR + cc_carry + ccx, fpos = co_carry + cox;
+        if (rpos + cc > a.rcap || fpos + co > a.fcap) {
+          atomicMax(&s_err, QS_CAPACITY);
+        } else {
+          for (int qd = 0; qd < (1 << D); ++qd) {
+            const int64_t mn = p | jshl(qd, offset);
+            if (cmask >> qd & 1) { rlo[rpos] = mn; rhi[rpos] = mn | low_mask(offset); rc[rpos] = 1; ++rpos; }
+            else if (omask >> qd & 1) { G[fpos++] = mn; }
+          }
+        }
+      }
+      if (sl != INT32_MAX) {
+        // counts up to and including node c + sl
+        __shared__ int64_t s_cc_upto, s_co_upto;
+        if ((int)threadIdx.x == sl) { s_cc_upto = cc_carry + ccx + cc; s_co_upto = co_carry + cox + co; }
+        __syncthreads();
+        stop_at = c + sl;
+        cc_carry = s_cc_upto;
+        co_carry = s_co_upto;
+        break;
+      }
+      cc_carry += cct;
+      co_carry += cot;
+      __syncthreads();
+    }
+    __syncthreads();
+    if (s_err) { err = s_err; break; }
+    if (stop_at >= 0) {
+      // bottomOut (ZN.scala:173-180): rest of this level, then the queued children, as overlapping
+      int64_t pos = nR + cc_carry;
+      const int64_t rest = K - stop_at - 1, kids = co_carry;
+      if (pos + rest + kids > a.rcap) { err = QS_CAPACITY; break; }
+      for (int64_t j = threadIdx.x; j < rest; j += RTPB) {
+        const int64_t mn = F[stop_at + 1 + j];
+        rlo[pos + j] = mn; rhi[pos + j] = mn | low_mask(offset + D); rc[pos + j] = 0;
+      }
+      pos += rest;
+      for (int64_t j = threadIdx.x; j < kids; j += RTPB) {
+        const int64_t mn = G[j];
+        rlo[pos + j] = mn; rhi[pos + j] = mn | low_mask(offset); rc[pos + j] = 0;
+      }
+      nR = pos + kids;
+      break;
+    }
+    nR += cc_carry;
+    K = co_carry;
+    if (K == 0) break;
+    // level terminator (ZN.scala:195-205)
+    level += 1;
+    offset -= D;
+    int64_t* tmp = F; F = G; G = tmp;
+    if (level >= a.recurse_stop || offset < 0) {
+      if (nR + K > a.rcap) { err = QS_CAPACITY; break; }
+      for (int64_t j = threadIdx.x; j < K; j += RTPB) {
+        const int64_t mn = F[j];
+        rlo[nR + j] = mn; rhi[nR + j] = mn | low_mask(offset + D); rc[nR + j] = 0;
+      }
+      nR += K;
+      break;
+    }
+    __syncthreads();
+  }
+  __syncthreads();
+  if (err) {
+    if (threadIdx.x == 0) { a.out_count[qc] = 0; a.status[qc] = err; }
+    return;
+  }
+  const int m = sort_merge(rlo, rhi, rc, (int)nR, a.gkey + qc * a.rcap, a.gidx + qc * a.rcap, a.out + qc * a.rcap,
+                           s_key, s_idx, s_tmp);
+  if (threadIdx.x == 0) { a.out_count[qc] = m; a.status[qc] = QS_OK; }
+}
+
+}  // namespace gm
+
+namespace gm {
+
+// ------------------------------------------------------------------ XZ ranges kernel
+
+struct XZRangesArgs {
+  const int32_t* win_off;   // [nq + 1]
+  const double* win;        // 2*D doubles per window, user space (mins then maxs)
+  int64_t q0;
+  int g;
+  double zhi;               // XZ3 z upper bound (maxOffset(period))
+  int range_stop;
+  int64_t fcap, rcap;
+  uint64_t* fa;
+  uint64_t* fb;
+  int64_t* rlo;
+  int64_t* rhi;
+  uint8_t* rc;
+  int64_t* gkey;
+  int32_t* gidx;
+  gm_range* out;
+  int32_t* out_count;
+  int32_t* status;
+};
+
+// element (ix, iy[, iz]) at level L packed 30 (XZ2) / 20 (XZ3) bits per coordinate
+template <int D>
+__device__ __forceinline__ uint32_t xcoord(uint64_t e, int d) {
+  return D == 2 ? (uint32_t)((e >> (30 * d)) & 0x3fffffffu) : (uint32_t)((e >> (20 * d)) & 0xfffffu);
+}
+template <int D>
+__device__ __forceinline__ uint64_t xpack(const uint32_t* c) {
+  uint64_t e = 0;
+  for (int d = 0; d < D; ++d) e |= (uint64_t)c[d] << ((D == 2 ? 30 : 20) * d);
+  return e;
+}
+
+// sequenceCode (XZ2SFC.scala:264-286, XZ3SFC.scala:275-304) of an element's lower corner: the
+// descent compares x < xCenter at every level, i.e. reads the element's coordinate bits MSB first
+template <int D>
+__device__ __forceinline__ int64_t xseq(uint64_t e, int L, int g) {
+  const int sh = D == 2 ? 2 : 3;
+  int64_t step = (((int64_t)1 << (sh * g)) - 1) / ((1 << D) - 1);
+  int64_t cs = 0;
+  for (int i = 0; i < L; ++i) {
+    const int b = L - 1 - i;
+    int qd = 0;
+    for (int d = 0; d < D; ++d) qd |= (int)((xcoord<D>(e, d) >> b) & 1u) << d;
+    cs += 1 + (int64_t)qd * step;
+    step = (step - 1) >> sh;
+  }
+  return cs;
+}
+// sequenceInterval full width: (base^(g - L + 1) - 1) / (base - 1) (XZ2SFC.scala:303)
+template <int D>
+__device__ __forceinline__ int64_t xspan(int L, int g) {
+  const int sh = D == 2 ? 2 : 3;
+  return (((int64_t)1 << (sh * (g - L + 1))) - 1) / ((1 << D) - 1);
+}
+
+template <int D>
+__global__ __launch_bounds__(RTPB) void k_xzranges(XZRangesArgs a) {
+  __shared__ double s_w[2 * D * MAXB];
+  __shared__ int64_t s_tmp[RNW];
+  __shared__ int s_err, s_stop;
+  __shared__ int64_t s_key[LDS_SORT];
+  __shared__ int16_t s_idx[LDS_SORT];
+
+  const int64_t qc = blockIdx.x;
+  const int64_t q = a.q0 + qc;
+  uint64_t* F = a.fa + qc * a.fcap;
+  uint64_t* G = a.fb + qc * a.fcap;
+  int64_t* rlo = a.rlo + qc * a.rcap;
+  int64_t* rhi = a.rhi + qc * a.rcap;
+  uint8_t* rc = a.rc + qc * a.rcap;
+  const int g = a.g;
+
+  const int w0 = a.win_off[q], nw = a.win_off[q + 1] - w0;
+  if (threadIdx.x == 0) s_err = nw > MAXB ? QS_TOO_MANY_BOUNDS : QS_OK;
+  __syncthreads();
+  if (s_err || nw <= 0) {
+    if (threadIdx.x == 0) { a.out_count[qc] = 0; a.status[qc] = s_err; }
+    return;
+  }
+  // normalize windows, non-lenient (XZ2SFC.scala:132-135 / XZ3SFC.scala:142-145 -> normalize)
+  for (int j = threadIdx.x; j < nw; j += RTPB) {
+    const double* w = a.win + 2 * D * (int64_t)(w0 + j);
+    const double lo[3] = {-180.0, -90.0, 0.0}, hi[3] = {180.0, 90.0, a.zhi};
+    bool ordered = true, inb = true;
+    for (int d = 0; d < D; ++d) {
+      ordered = ordered && (w[d] <= w[D + d]);
+      inb = inb && (w[d] >= lo[d]) && (w[D + d] <= hi[d]);
+    }
+    if (!ordered) atomicMax(&s_err, QS_UNORDERED);
+    else if (!inb) atomicMax(&s_err, QS_OUT_OF_BOUNDS);
+    for (int d = 0; d < D; ++d) {
+      const double size = __dsub_rn(hi[d], lo[d]);
+      s_w[2 * D * j + d] = __ddiv_rn(__dsub_rn(w[d], lo[d]), size);
+      s_w[2 * D * j + D + d] = __ddiv_rn(__dsub_rn(w[D + d], lo[d]), size);
+    }
+  }
+  __syncthreads();
+  if (s_err) {
+    if (threadIdx.x == 0) { a.out_count[qc] = 0; a.status[qc] = s_err; }
+    return;
+  }
+
+  // LevelOneElements: the 2^D children of the unit element, in XElement.children order
+  int64_t K = 1 << D;
+  for (int k = threadIdx.x; k < K; k += RTPB) {
+    uint32_t c[3] = {(uint32_t)(k & 1), (uint32_t)((k >> 1) & 1), (uint32_t)((k >> 2) & 1)};
+    F[k] = xpack<D>(c);
+  }
+  __syncthreads();
+  int level = 1;
+  int64_t nR = 0;
+  int err = QS_OK;
+  const int64_t range_stop = a.range_stop;
+  bool bottom = false;   // bottom out F at `level`, children G (n_kids) at level + 1
+  int64_t first_rest = 0, n_kids = 0;
+  while (true) {
+    if (level >= g) { bottom = true; first_rest = 0; n_kids = 0; break; }  // while (level < g ...)
+    const double len = ldexp(1.0, -level);
+    int64_t a_carry = 0, co_carry = 0;
+    int64_t stop_at = -1;
+    for (int64_t c = 0; c < K; c += RTPB) {
+      const int64_t i = c + threadIdx.x;
+      int kind = 0;  // 0 disjoint, 1 contained, 2 overlapping
+      uint64_t e = 0;
+      if (i < K) {
+        e = F[i];
+        double mn[3], ext[3];
+        for (int d = 0; d < D; ++d) {
+          const double ci = (double)xcoord<D>(e, d);
+          mn[d] = __dmul_rn(ci, len);                    // xmin
+          ext[d] = __dmul_rn(__dadd_rn(ci, 2.0), len);   // xext = xmax + length
+        }
+        bool cont = false, ovl = false;
+        for (int w = 0; w < nw && !cont; ++w) {   // XElement.isContained (XZ2SFC.scala:400-401)
+          const double* W = &s_w[2 * D * w];
+          bool ok = true;
+          for (int d = 0; d < D; ++d) ok = ok && (W[d] <= mn[d]) && (W[D + d] >= ext[d]);
+          cont = ok;
+        }
+        if (!cont) {
+          for (int w = 0; w < nw && !ovl; ++w) {  // XElement.overlaps (XZ2SFC.scala:403-404)
+            const double* W = &s_w[2 * D * w];
+            bool ok = true;
+            for (int d = 0; d < D; ++d) ok = ok && (W[D + d] >= mn[d]) && (W[d] <= ext[d]);
+            ovl = ok;
+          }
+        }
+        kind = cont ? 1 : (ovl ? 2 : 0);
+      }
+      const int ai = kind != 0, co = kind == 2 ? (1 << D) : 0;
+      int64_t at, cot;
+      const int64_t ax = block_exscan(ai, s_tmp, at);
+      const int64_t cox = block_exscan(co, s_tmp, cot);
+      // budget: element i is processed only if nR + A(i-1) < rangeStop (XZ2SFC.scala:205)
+      if (threadIdx.x == 0) s_stop = INT32_MAX;
+      __syncthreads();
+      if (i < K && nR + a_carry + ax >= range_stop) atomicMin(&s_stop, (int)threadIdx.x);
+      __syncthreads();
+      const int sl = s_stop;
+      if (i < K && (sl == INT32_MAX || (int)threadIdx.x < sl) && kind) {
+        const int64_t rpos = nR + a_carry + ax;
+        const int64_t fpos = co_carry + cox;
+        if (rpos >= a.rcap || fpos + co > a.fcap) {
+          atomicMax(&s_err, QS_CAPACITY);
+        } else {
+          const int64_t cs = xseq<D>(e, level, g);
+          rlo[rpos] = cs;
+          if (kind == 1) { rhi[rpos] = cs + xspan<D>(level, g); rc[rpos] = 1; }
+          else {
+            rhi[rpos] = cs; rc[rpos] = 0;
+            for (int k = 0; k < (1 << D); ++k) {   // XElement.children order
+              uint32_t cc[3];
+              for (int d = 0; d < D; ++d) cc[d] = 2 * xcoord<D>(e, d) + ((k >> d) & 1);
+              G[fpos + k] = xpack<D>(cc);
+            }
+          }
+        }
+      }
+      if (sl != INT32_MAX) {
+        __shared__ int64_t s_a_upto, s_co_upto;
+        if ((int)threadIdx.x == 0) { s_a_upto = 0; s_co_upto = 0; }
+        __syncthreads();
+        if ((int)threadIdx.x == sl) { s_a_upto = a_carry + ax; s_co_upto = co_carry + cox; }
+        __syncthreads();
+        stop_at = c + sl;   // first unprocessed element
+        a_carry = s_a_upto;
+        co_carry = s_co_upto;
+        break;
+      }
+      a_carry += at;
+      co_carry += cot;
+      __syncthreads();
+    }
+    __syncthreads();
+    if (s_err) { err = s_err; break; }
+    nR += a_carry;
+    if (stop_at >= 0) { bottom = true; first_rest = stop_at; n_kids = co_carry; break; }
+    K = co_carry;
+    if (K == 0) break;
+    level += 1;   // LevelTerminator (XZ2SFC.scala:207-212)
+    uint64_t* tmp = F; F = G; G = tmp;
+    __syncthreads();
+  }
+  if (!err && bottom) {
+    // bottom out (XZ2SFC.scala:219-227): rest of F at `level`, then G at level + 1, full intervals
+    const int64_t rest = K - first_rest;
+    if (nR + rest + n_kids > a.rcap) err = QS_CAPACITY;
+    else {
+      for (int64_t j = threadIdx.x; j < rest; j += RTPB) {
+        const int64_t cs = xseq<D>(F[first_rest + j], level, g);
+        rlo[nR + j] = cs; rhi[nR + j] = cs + xspan<D>(level, g); rc[nR + j] = 0;
+      }
+      for (int64_t j = threadIdx.x; j < n_kids; j += RTPB) {
+        const int64_t cs = xseq<D>(G[j], level + 1, g);
+        rlo[nR + rest + j] = cs; rhi[nR + rest + j] = cs + xspan<D>(level + 1, g); rc[nR + rest + j] = 0;
+      }
+      nR += rest + n_kids;
+    }
+  }
+  __syncthreads();
+  if (err) {
+    if (threadIdx.x == 0) { a.out_count[qc] = 0; a.status[qc] = err; }
+    return;
+  }
+  const int m = sort_merge(rlo, rhi, rc, (int)nR, a.gkey + qc * a.rcap, a.gidx + qc * a.rcap, a.out + qc * a.rcap,
+                           s_key, s_idx, s_tmp);
+  if (threadIdx.x == 0) { a.out_count[qc] = m; a.status[qc] = QS_OK; }
+}
+
+// gather each query's merged ranges into the contiguous output
+__global__ __launch_bounds__(RTPB) void k_gather_ranges(const gm_range* __restrict__ ws, int64_t rcap,
+                                                        const int64_t* __restrict__ off, gm_range* __restrict__ out) {
+  const int64_t qc = blockIdx.x;
+  const int64_t a = off[qc], n = off[qc + 1] - a;
+  for (int64_t j = threadIdx.x; j < n; j += RTPB) out[a + j] = ws[qc * rcap + j];
+}
+
+// ------------------------------------------------------------------ host driver
+
+struct RangesJob {
+  int kind;  // 2 = Z2, 3 = Z3, 12 = XZ2, 13 = XZ3
+  int64_t nq;
+  int range_stop;
+};
+
+inline int64_t next_pow2(int64_t v) { int64_t p = 1; while (p < v) p <<= 1; return p; }
+
+}  // namespace gm
+
+using namespace gm;
+
+namespace {
+
+template <class T>
+int to_dev(hipStream_t s, const T* h, size_t n, T** d) {
+  GM_HIP(hipMallocAsync((void**)d, std::max<size_t>(n * sizeof(T), 16), s));
+  if (n) GM_HIP(hipMemcpyAsync(*d, h, n * sizeof(T), hipMemcpyHostToDevice, s));
+  return GM_OK;
+}
+
+// shared driver: per chunk of queries allocate workspaces, launch, read counts, gather, copy out
+template <class LaunchFn>
+int run_ranges(gm_ctx* ctx, int64_t nq, int64_t fcap, int64_t rcap, size_t felem, LaunchFn launch, int64_t* out_off,
+               gm_range* out, int64_t cap, int64_t* needed, int32_t* query_status) {
+  hipStream_t s = ctx->stream;
+  rcap = next_pow2(std::max<int64_t>(rcap, 16));
+  // chunk so that the workspace stays within ~2 GiB
+  const int64_t per_q = fcap * (int64_t)felem * 2 + rcap * (8 + 8 + 1 + 8 + 4 + (int64_t)sizeof(gm_range));
+  int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(nq, ((int64_t)2 << 30) / std::max<int64_t>(per_q, 1)));
+  chunk = std::min<int64_t>(chunk, 65535);
+  std::vector<int32_t> counts((size_t)nq), stats((size_t)nq);
+  std::vector<int64_t> offs((size_t)nq + 1, 0);
+  out_off[0] = 0;
+  int64_t total = 0;
+  bool overflow = false;
+  for (int64_t q0 = 0; q0 < nq; q0 += chunk) {
+    const int64_t m = std::min(chunk, nq - q0);
+    char *fa, *fb;
+    int64_t *rlo, *rhi, *gkey, *doff;
+    uint8_t* rc;
+    int32_t *gidx, *dcnt, *dst;
+    gm_range *ws, *dout;
+    GM_HIP(hipMallocAsync((void**)&fa, (size_t)(m * fcap) * felem, s));
+    GM_HIP(hipMallocAsync((void**)&fb, (size_t)(m * fcap) * felem, s));
+    GM_HIP(hipMallocAsync((void**)&rlo, (size_t)(m * rcap) * 8, s));
+    GM_HIP(hipMallocAsync((void**)&rhi, (size_t)(m * rcap) * 8, s));
+    GM_HIP(hipMallocAsync((void**)&rc, (size_t)(m * rcap), s));
+    GM_HIP(hipMallocAsync((void**)&gkey, (size_t)(m * rcap) * 8, s));
+    GM_HIP(hipMallocAsync((void**)&gidx, (size_t)(m * rcap) * 4, s));
+    GM_HIP(hipMallocAsync((void**)&ws, (size_t)(m * rcap) * sizeof(gm_range), s));
+    GM_HIP(hipMallocAsync((void**)&dcnt, (size_t)m * 4, s));
+    GM_HIP(hipMallocAsync((void**)&dst, (size_t)m * 4, s));
+    launch(q0, m, fcap, rcap, fa, fb, rlo, rhi, rc, gkey, gidx, ws, dcnt, dst);
+    GM_CHECK_LAUNCH();
+    GM_HIP(hipMemcpyAsync(counts.data() + q0, dcnt, (size_t)m * 4, hipMemcpyDeviceToHost, s));
+    GM_HIP(hipMemcpyAsync(stats.data() + q0, dst, (size_t)m * 4, hipMemcpyDeviceToHost, s));
+    GM_HIP(hipStreamSynchronize(s));
+    int64_t ctotal = 0;
+    std::vector<int64_t> loff((size_t)m + 1, 0);
+    for (int64_t i = 0; i < m; ++i) {
+      loff[i + 1] = loff[i] + counts[q0 + i];
+      out_off[q0 + i + 1] = total + loff[i + 1];
+    }
+    ctotal = loff[m];
+    if (total + ctotal <= cap && ctotal > 0) {
+      GM_HIP(hipMallocAsync((void**)&doff, (size_t)(m + 1) * 8, s));
+      GM_HIP(hipMallocAsync((void**)&dout, (size_t)ctotal * sizeof(gm_range), s));
+      GM_HIP(hipMemcpyAsync(doff, loff.data(), (size_t)(m + 1) * 8, hipMemcpyHostToDevice, s));
+      hipLaunchKernelGGL(k_gather_ranges, dim3((unsigned)m), dim3(RTPB), 0, s, ws, rcap, doff, dout);
+      GM_CHECK_LAUNCH();
+      GM_HIP(hipMemcpyAsync(out + total, dout, (size_t)ctotal * sizeof(gm_range), hipMemcpyDeviceToHost, s));
+      GM_HIP(hipFreeAsync(doff, s));
+      GM_HIP(hipFreeAsync(dout, s));
+    } else if (total + ctotal > cap) {
+      overflow = true;
+    }
+    total += ctotal;
+    for (void* p : {(void*)fa, (void*)fb, (void*)rlo, (void*)rhi, (void*)rc, (void*)gkey, (void*)gidx, (void*)ws,
+                    (void*)dcnt, (void*)dst})
+      GM_HIP(hipFreeAsync(p, s));
+    GM_HIP(hipStreamSynchronize(s));
+  }
+  if (query_status) for (int64_t i = 0; i < nq; ++i) query_status[i] = stats[i];
+  if (needed) *needed = total;
+  return overflow ? GM_E_CAPACITY : GM_OK;
+}
+
+inline int stop_of(int max_ranges) { return max_ranges <= 0 ? INT32_MAX : max_ranges; }
+
+// workspace sizing: the FIFO never holds more than rangeStop + 2^D items before the budget fires
+inline int64_t z_caps(int max_ranges, int D, int64_t cap_hint) {
+  if (max_ranges > 0) return (int64_t)max_ranges + (1 << D) + 16;
+  return std::max<int64_t>(cap_hint, 1 << 16);
+}
+
+}  // namespace
+
+extern "C" {
+
+int gm_z3_ranges(gm_ctx* ctx, int64_t nq, const int32_t* box_off, const double* xy, const int32_t* time_off,
+                 const int64_t* t, int period, int precision, int range_precision, int max_ranges, int max_recurse,
+                 int64_t* out_off, gm_range* out, int64_t cap, int64_t* needed, int32_t* query_status) {
+  if (!ctx || nq < 0 || !box_off || !time_off || !out_off || period < 0 || period > 3 || precision < 1 ||
+      precision > 21 || range_precision < 1 || range_precision > 64)
+    return GM_E_INVALID;
+  if (nq == 0) { out_off[0] = 0; if (needed) *needed = 0; return GM_OK; }
+  hipStream_t s = ctx->stream;
+  const int64_t nbox = box_off[nq], ntim = time_off[nq];
+  int32_t *dbo, *dto;
+  double* dxy;
+  int64_t* dt;
+  int rc = to_dev(s, box_off, (size_t)nq + 1, &dbo);
+  if (!rc) rc = to_dev(s, time_off, (size_t)nq + 1, &dto);
+  if (!rc) rc = to_dev(s, xy, (size_t)nbox * 4, &dxy);
+  if (!rc) rc = to_dev(s, t, (size_t)ntim * 2, &dt);
+  if (rc) return rc;
+  ZRangesArgs a{};
+  a.box_off = dbo; a.xy = dxy; a.time_off = dto; a.t = dt;
+  a.lon = make_ndim(-180.0, 180.0, precision);
+  a.lat = make_ndim(-90.0, 90.0, precision);
+  a.tim = make_ndim(0.0, (double)max_offset(period), precision);
+  a.range_precision = range_precision;
+  a.range_stop = stop_of(max_ranges);
+  a.recurse_stop = max_recurse < 0 ? INT32_MAX : max_recurse;   // Z3SFC.MaxRecursion = Int.MaxValue
+  const int64_t zc = z_caps(max_ranges, 3, cap);
+  rc = run_ranges(ctx, nq, zc, zc, 8,
+                  [&](int64_t q0, int64_t m, int64_t fcap, int64_t rcap, char* fa, char* fb, int64_t* rlo, int64_t* rhi,
+                      uint8_t* rcb, int64_t* gkey, int32_t* gidx, gm_range* ws, int32_t* dcnt, int32_t* dst) {
+                    ZRangesArgs b = a;
+                    b.q0 = q0; b.fcap = fcap; b.rcap = rcap;
+                    b.fa = (int64_t*)fa; b.fb = (int64_t*)fb; b.rlo = rlo; b.rhi = rhi; b.rc = rcb;
+                    b.gkey = gkey; b.gidx = gidx; b.out = ws; b.out_count = dcnt; b.status = dst;
+                    hipLaunchKernelGGL(k_zranges<3>, dim3((unsigned)m), dim3(RTPB), 0, s, b);
+                  },
+                  out_off, out, cap, needed, query_status);
+  (void)hipFreeAsync(dbo, s); (void)hipFreeAsync(dto, s); (void)hipFreeAsync(dxy, s); (void)hipFreeAsync(dt, s);
+  return rc;
+}
+
+int gm_z2_ranges(gm_ctx* ctx, int64_t nq, const int32_t* box_off, const double* xy, int precision,
+                 int range_precision, int max_ranges, int max_recurse, int64_t* out_off, gm_range* out, int64_t cap,
+                 int64_t* needed, int32_t* query_status) {
+  if (!ctx || nq < 0 || !box_off || !out_off || precision < 1 || precision > 31 || range_precision < 1 ||
+      range_precision > 64)
+    return GM_E_INVALID;
+  if (nq == 0) { out_off[0] = 0; if (needed) *needed = 0; return GM_OK; }
+  hipStream_t s = ctx->stream;
+  const int64_t nbox = box_off[nq];
+  int32_t* dbo;
+  double* dxy;
+  int rc = to_dev(s, box_off, (size_t)nq + 1, &dbo);
+  if (!rc) rc = to_dev(s, xy, (size_t)nbox * 4, &dxy);
+  if (rc) return rc;
+  ZRangesArgs a{};
+  a.box_off = dbo; a.xy = dxy; a.time_off = nullptr; a.t = nullptr;
+  a.lon = make_ndim(-180.0, 180.0, precision);
+  a.lat = make_ndim(-90.0, 90.0, precision);
+  a.range_precision = range_precision;
+  a.range_stop = stop_of(max_ranges);
+  a.recurse_stop = max_recurse < 0 ? 7 : max_recurse;   // ZN.DefaultRecurse (ZN.scala:293)
+  const int64_t zc = z_caps(max_ranges, 2, cap);
+  rc = run_ranges(ctx, nq, zc, zc, 8,
+                  [&](int64_t q0, int64_t m, int64_t fcap, int64_t rcap, char* fa, char* fb, int64_t* rlo, int64_t* rhi,
+                      uint8_t* rcb, int64_t* gkey, int32_t* gidx, gm_range* ws, int32_t* dcnt, int32_t* dst) {
+                    ZRangesArgs b = a;
+                    b.q0 = q0; b.fcap = fcap; b.rcap = rcap;
+                    b.fa = (int64_t*)fa; b.fb = (int64_t*)fb; b.rlo = rlo; b.rhi = rhi; b.rc = rcb;
+                    b.gkey = gkey; b.gidx = gidx; b.out = ws; b.out_count = dcnt; b.status = dst;
+                    hipLaunchKernelGGL(k_zranges<2>, dim3((unsigned)m), dim3(RTPB), 0, s, b);
+                  },
+                  out_off, out, cap, needed, query_status);
+  (void)hipFreeAsync(dbo, s); (void)hipFreeAsync(dxy, s);
+  return rc;
+}
+
+static int xz_ranges(gm_ctx* ctx, int D, int64_t nq, const int32_t* win_off, const double* windows, int g,
+                     int period, int max_ranges, int64_t* out_off, gm_range* out, int64_t cap, int64_t* needed,
+                     int32_t* query_status) {
+  if (!ctx || nq < 0 || !win_off || !out_off || g < 1 || g > (D == 2 ? 29 : 19) || period < 0 || period > 3)
+    return GM_E_INVALID;
+  if (nq == 0) { out_off[0] = 0; if (needed) *needed = 0; return GM_OK; }
+  hipStream_t s = ctx->stream;
+  const int64_t nw = win_off[nq];
+  int32_t* dwo;
+  double* dw;
+  int rc = to_dev(s, win_off, (size_t)nq + 1, &dwo);
+  if (!rc) rc = to_dev(s, windows, (size_t)nw * 2 * D, &dw);
+  if (rc) return rc;
+  XZRangesArgs a{};
+  a.win_off = dwo; a.win = dw; a.g = g; a.zhi = (double)max_offset(period);
+  a.range_stop = stop_of(max_ranges);
+  // each processed element adds one range and at most 2^D queued children
+  int64_t fcap, rcap;
+  if (max_ranges > 0) {
+    fcap = ((int64_t)max_ranges + 2) << D;
+    rcap = (int64_t)max_ranges + 2 * fcap + 16;
+  } else {
+    fcap = std::max<int64_t>(cap, 1 << 16);
+    rcap = 3 * fcap;
+  }
+  rc = run_ranges(ctx, nq, fcap, rcap, 8,
+                  [&](int64_t q0, int64_t m, int64_t fc, int64_t rcp, char* fa, char* fb, int64_t* rlo, int64_t* rhi,
+                      uint8_t* rcb, int64_t* gkey, int32_t* gidx, gm_range* ws, int32_t* dcnt, int32_t* dst) {
+                    XZRangesArgs b = a;
+                    b.q0 = q0; b.fcap = fc; b.rcap = rcp;
+                    b.fa = (uint64_t*)fa; b.fb = (uint64_t*)fb; b.rlo = rlo; b.rhi = rhi; b.rc = rcb;
+                    b.gkey = gkey; b.gidx = gidx; b.out = ws; b.out_count = dcnt; b.status = dst;
+                    if (D == 2) hipLaunchKernelGGL(k_xzranges<2>, dim3((unsigned)m), dim3(RTPB), 0, s, b);
+                    else hipLaunchKernelGGL(k_xzranges<3>, dim3((unsigned)m), dim3(RTPB), 0, s, b);
+                  },
+                  out_off, out, cap, needed, query_status);
+  (void)hipFreeAsync(dwo, s); (void)hipFreeAsync(dw, s);
+  return rc;
+}
+
+int gm_xz2_ranges(gm_ctx* ctx, int64_t nq, const int32_t* win_off, const double* windows, int g, int max_ranges,
+                  int64_t* out_off, gm_range* out, int64_t cap, int64_t* needed, int32_t* query_status) {
+  return xz_ranges(ctx, 2, nq, win_off, windows, g, GM_WEEK, max_ranges, out_off, out, cap, needed, query_status);
+}
+
+int gm_xz3_ranges(gm_ctx* ctx, int64_t nq, const int32_t* win_off, const double* windows, int g, int period,
+                  int max_ranges, int64_t* out_off, gm_range* out, int64_t cap, int64_t* needed,
+                  int32_t* query_status) {
+  return xz_ranges(ctx, 3, nq, win_off, windows, g, period, max_ranges, out_off, out, cap, needed, query_status);
+}
+
+}  // extern "C"

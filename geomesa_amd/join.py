@@ -1,0 +1,197 @@
+"""st_contains point-in-polygon join on the GPU (JTS 1.20 Geometry.contains semantics).
+
+Replaces the per-pair UDF evaluation of the Spark-SQL spatial join:
+  SQLRules.SpatialJoinStrategy -> GeoMesaJoinRelation.sweeplineJoin -> OverlapAction.overlap ->
+  ST_Contains(geom1, geom2) = geom1.contains(geom2)
+(geomesa-spark/geomesa-spark-sql/.../GeoMesaJoinRelation.scala:41-91, OverlapAction.scala:25-41,
+ geomesa-spark/geomesa-spark-jts/.../udf/SpatialRelationFunctions.scala:29,94).
+
+Polygons travel as CSR (polygon -> parts -> rings -> vertices, rings closed).  Points are device
+columns.  The result is the set of (point id, polygon id) pairs; like the reference RDD it is
+unordered (tests compare as sets).  `st_contains(poly, point)` of a null argument is null
+(SQLFunctionHelper.nullableUDF, SQLFunctionHelper.scala:27-33) -- here: rows flagged null are
+skipped by the caller.
+"""
+import ctypes
+import re
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, ptr
+
+
+class PolygonSet:
+    """CSR polygon set.  `polys` is a list of polygons; a polygon is a list of parts; a part is a
+    list of rings (shell first); a ring is an (k, 2) array-like of vertices (closed or not -- it is
+    closed here the way JTS LinearRing requires)."""
+
+    def __init__(self, poly_part_off, part_ring_off, ring_vert_off, vx, vy):
+        self.poly_part_off = np.ascontiguousarray(poly_part_off, np.int32)
+        self.part_ring_off = np.ascontiguousarray(part_ring_off, np.int32)
+        self.ring_vert_off = np.ascontiguousarray(ring_vert_off, np.int32)
+        self.vx = np.ascontiguousarray(vx, np.float64)
+        self.vy = np.ascontiguousarray(vy, np.float64)
+
+    @property
+    def n_polys(self):
+        return len(self.poly_part_off) - 1
+
+    @property
+    def n_vertices(self):
+        return len(self.vx)
+
+    @classmethod
+    def from_polygons(cls, polys):
+        ppo, pro, rvo, vx, vy = [0], [0], [0], [], []
+        for poly in polys:
+            for part in poly:
+                for ring in part:
+                    r = np.asarray(ring, np.float64).reshape(-1, 2)
+                    if len(r) and (r[0, 0] != r[-1, 0] or r[0, 1] != r[-1, 1]):
+                        r = np.vstack([r, r[:1]])
+                    vx.append(r[:, 0]); vy.append(r[:, 1])
+                    rvo.append(rvo[-1] + len(r))
+                pro.append(len(rvo) - 1)
+            ppo.append(len(pro) - 1)
+        vx = np.concatenate(vx) if vx else np.zeros(0)
+        vy = np.concatenate(vy) if vy else np.zeros(0)
+        return cls(ppo, pro, rvo, vx, vy)
+
+    @classmethod
+    def from_wkt(cls, wkts):
+        return cls.from_polygons([parse_wkt_polygon(w) for w in wkts])
+
+    def c_struct(self):
+        return _lib.PolySetC(self.n_polys, self.poly_part_off.ctypes.data, self.part_ring_off.ctypes.data,
+                             self.ring_vert_off.ctypes.data, self.vx.ctypes.data, self.vy.ctypes.data)
+
+    def to_arrays(self):
+        return (self.poly_part_off, self.part_ring_off, self.ring_vert_off, self.vx, self.vy)
+
+
+_num = r"[-+]?(?:\d+\.?\d*|\.\d+)(?:[eE][-+]?\d+)?"
+
+
+def _ring(s):
+    pts = [tuple(float(v) for v in p.split()) for p in s.split(",")]
+    return np.array([(p[0], p[1]) for p in pts], np.float64)
+
+
+def parse_wkt_polygon(wkt):
+    """POLYGON / MULTIPOLYGON WKT -> list of parts -> list of rings."""
+    w = wkt.strip()
+    up = w.upper()
+    if up.startswith("MULTIPOLYGON"):
+        body = w[w.index("(") + 1:w.rindex(")")]
+        parts = re.findall(r"\(\s*(\(.*?\)(?:\s*,\s*\(.*?\))*)\s*\)", body)
+        return [[_ring(r) for r in re.findall(r"\(([^()]*)\)", p)] for p in parts]
+    if up.startswith("POLYGON"):
+        body = w[w.index("(") + 1:w.rindex(")")]
+        return [[_ring(r) for r in re.findall(r"\(([^()]*)\)", body)]]
+    raise ValueError("not a polygon: %s" % wkt[:40])
+
+
+class PolygonIndex:
+    """Device-side join index for a PolygonSet (gm_pip_index_create)."""
+
+    def __init__(self, polyset, ctx=None):
+        self.polyset = polyset
+        self.ctx = ctx or _lib.context()
+        self._cs = polyset.c_struct()
+        self._h = ctypes.c_void_p()
+        check(self.ctx.lib.gm_pip_index_create(self.ctx.handle, ctypes.byref(self._cs), ctypes.byref(self._h)),
+              "gm_pip_index_create")
+
+    def join(self, px, py, id_base=0, cap=None, count_only=False):
+        """Returns (pt_ids, poly_ids) device tensors (or the pair count when count_only)."""
+        import torch
+        from .curve import _dev_col
+        px = _dev_col(px, torch.float64)
+        py = _dev_col(py, torch.float64)
+        n = px.numel()
+        npairs = ctypes.c_int64()
+        if count_only:
+            check(self.ctx.lib.gm_pip_join(self.ctx.handle, self._h, ptr(px), ptr(py), n, id_base, None, None, 0,
+                                           ctypes.byref(npairs)), "gm_pip_join")
+            return npairs.value
+        if cap is None:
+            cap = max(1024, n + n // 4)
+        while True:
+            pt = torch.empty(cap, dtype=torch.int64, device=px.device)
+            pl = torch.empty(cap, dtype=torch.int32, device=px.device)
+            rc = self.ctx.lib.gm_pip_join(self.ctx.handle, self._h, ptr(px), ptr(py), n, id_base, ptr(pt), ptr(pl),
+                                          cap, ctypes.byref(npairs))
+            if rc == _lib.GM_E_CAPACITY:
+                cap = npairs.value
+                continue
+            check(rc, "gm_pip_join")
+            k = npairs.value
+            return pt[:k], pl[:k]
+
+    def close(self):
+        if self._h:
+            self.ctx.lib.gm_pip_index_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def st_contains_join(polyset, px, py):
+    """All (point, polygon) pairs with st_contains(polygon, point) = true."""
+    return PolygonIndex(polyset).join(px, py)
+
+
+# ------------------------------------------------------------------------------ synthetic inputs
+
+CONUS = (-125.0, 24.0, -66.0, 50.0)
+
+
+def synthetic_counties(nx=80, ny=40, seed=0x67656f6d65736121, box=CONUS, vmin=64, vmax=256,
+                       hole_frac=0.10, multi_frac=0.05):
+    """Seeded jittered nx x ny grid of star-shaped 'county' polygons (BASELINE config 4).
+
+    Each polygon lies inside its own grid cell, so neighbours share no edges and contains() is
+    order independent; ~hole_frac get a hole, ~multi_frac are 2-part MultiPolygons."""
+    rng = np.random.default_rng(seed & 0xFFFFFFFFFFFFFFFF)
+    x0, y0, x1, y1 = box
+    cw, ch = (x1 - x0) / nx, (y1 - y0) / ny
+    R = 0.45 * min(cw, ch)
+    polys = []
+    for j in range(ny):
+        for i in range(nx):
+            cx = x0 + (i + 0.5) * cw + rng.uniform(-0.03, 0.03) * R
+            cy = y0 + (j + 0.5) * ch + rng.uniform(-0.03, 0.03) * R
+            nv = int(rng.integers(vmin, vmax + 1))
+            ang = np.sort(rng.uniform(0, 2 * np.pi, nv))
+            rad = R * (0.6 + 0.35 * rng.uniform(0, 1, nv))
+            shell = np.stack([cx + rad * np.cos(ang), cy + rad * np.sin(ang)], 1)
+            rings = [shell]
+            if rng.uniform() < hole_frac:
+                hn = int(rng.integers(8, 32))
+                ha = np.sort(rng.uniform(0, 2 * np.pi, hn))
+                hr = 0.25 * R * (0.5 + 0.5 * rng.uniform(0, 1, hn))
+                rings.append(np.stack([cx + hr * np.cos(ha), cy + hr * np.sin(ha)], 1))
+            parts = [rings]
+            if rng.uniform() < multi_frac:
+                k = int(rng.integers(0, 4))
+                ux, uy = (1 if k & 1 else -1) * cw / 2, (1 if k & 2 else -1) * ch / 2
+                nrm = np.hypot(ux, uy)
+                d = 0.82 * nrm
+                px_, py_ = cx + ux / nrm * d, cy + uy / nrm * d
+                sn = int(rng.integers(8, 24))
+                sa = np.sort(rng.uniform(0, 2 * np.pi, sn))
+                sr = 0.05 * R * (0.6 + 0.4 * rng.uniform(0, 1, sn))
+                parts.append([np.stack([px_ + sr * np.cos(sa), py_ + sr * np.sin(sa)], 1)])
+            polys.append(parts)
+    return PolygonSet.from_polygons(polys)
+
+
+def synthetic_points(n, seed=0x67656f6d65736121, box=CONUS):
+    rng = np.random.default_rng((seed + 1) & 0xFFFFFFFFFFFFFFFF)
+    x0, y0, x1, y1 = box
+    return rng.uniform(x0, x1, n), rng.uniform(y0, y1, n)

@@ -1,0 +1,215 @@
+/*
+ * geomesa_hip.h -- C ABI of the MI355X-native GeoMesa hot path (libgeomesa_hip.so, gfx950).
+ *
+ * Drop-in boundary for the Scala/JVM surface of liyq0307/geomesa's spatio-temporal
+ * index-and-filter path.  Every entry point names the reference interface it replaces
+ * (paths abbreviated: z3/ = geomesa-z3/src/main/scala/org/locationtech/geomesa/,
+ *  idx/ = geomesa-index-api/src/main/scala/org/locationtech/geomesa/index/).
+ * A JVM binding (JNI or Java FFM) is sketched in INTEGRATION.md.
+ *
+ * Conventions
+ *  - Plain pointers and sizes only.  Array arguments are DEVICE pointers (hipMalloc'd, or
+ *    any device allocation of the caller) unless the parameter says "host".  Buffers are
+ *    caller-owned; the library never retains a pointer past the call (or past gm_ctx_sync()
+ *    for the asynchronous entry points).
+ *  - Every call returns an int status: GM_OK (0) or a negative GM_E_* code.
+ *  - Per-element failures mirror the JVM exceptions: an optional device uint8 status[] gets
+ *    GM_ST_* per element, and an optional host gm_batch_status receives the error count and
+ *    the first failing element, so a shim can throw the same IllegalArgumentException the
+ *    Scala code throws on the first bad element.  Passing summary = NULL keeps the call
+ *    fully asynchronous on the context's stream.
+ *  - Thread safety: one gm_ctx per thread; calls on different contexts are independent.
+ *  - Configuration knobs the Scala code reads from system properties
+ *    (geomesa.scan.ranges.target, geomesa.scan.ranges.recurse, XZ precision g, ...) are
+ *    explicit parameters here, never globals.
+ */
+#ifndef GEOMESA_HIP_H
+#define GEOMESA_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GM_ABI_VERSION 1
+
+/* return codes */
+#define GM_OK 0
+#define GM_E_INVALID (-1)     /* bad argument (null pointer, bad period/precision, malformed filter) */
+#define GM_E_HIP (-2)         /* HIP runtime failure; see gm_last_error() */
+#define GM_E_CAPACITY (-3)    /* output capacity too small; the needed size is reported */
+#define GM_E_ELEMENT (-4)     /* at least one element failed (only when no status[] and no summary) */
+
+/* per-element status codes */
+#define GM_ST_OK 0
+#define GM_ST_OUT_OF_BOUNDS 1 /* Z3SFC/Z2SFC/XZ2SFC/XZ3SFC require(...) -> IllegalArgumentException */
+#define GM_ST_BAD_TIME 2      /* BinnedTime require(...): before 1970-01-01 or past the period's max date */
+#define GM_ST_UNORDERED 3     /* XZ require(xmin <= xmax ...) / ZRange require(min <= max) */
+
+/* TimePeriod (z3/curve/BinnedTime.scala:283-291) */
+#define GM_DAY 0
+#define GM_WEEK 1
+#define GM_MONTH 2
+#define GM_YEAR 3
+
+typedef struct gm_ctx gm_ctx;
+
+typedef struct {
+  int64_t n_errors;     /* number of failed elements */
+  int64_t first_index;  /* index of the first failed element, -1 if none */
+  int32_t first_code;   /* GM_ST_* of that element */
+  int32_t reserved;
+} gm_batch_status;
+
+/* IndexRange (z3/zorder/sfcurve/package.scala:241-272): CoveredRange when contained = 1 */
+typedef struct {
+  int64_t lower;
+  int64_t upper;
+  int32_t contained;
+  int32_t reserved;
+} gm_range;
+
+/* ------------------------------------------------------------------ context */
+int gm_abi_version(void);
+/* stream: a hipStream_t to launch on (NULL = a new non-blocking stream owned by the context) */
+int gm_ctx_create(int device, void* stream, gm_ctx** out);
+int gm_ctx_destroy(gm_ctx* ctx);
+int gm_ctx_sync(gm_ctx* ctx);
+void* gm_ctx_stream(gm_ctx* ctx);
+const char* gm_last_error(void);
+/* device memory helpers for callers without their own allocator (e.g. a JNI shim) */
+int gm_device_alloc(gm_ctx* ctx, size_t bytes, void** ptr);
+int gm_device_free(gm_ctx* ctx, void* ptr);
+int gm_copy_to_device(gm_ctx* ctx, void* dst, const void* host_src, size_t bytes);
+int gm_copy_to_host(gm_ctx* ctx, void* host_dst, const void* src, size_t bytes);
+/* HIP-event timing on the context stream: brackets any sequence of calls */
+int gm_timer_start(gm_ctx* ctx);
+int gm_timer_stop(gm_ctx* ctx, float* ms);
+
+/* ------------------------------------------------------------------ Z-curve keys */
+/* Z3SFC.index(x, y, t, lenient) (z3/curve/Z3SFC.scala:37-52), t = offset within the period
+   (BinnedTime units).  precision = bits per dimension, 1..21 (StandardZ3Dimensions, :92-99). */
+int gm_z3_index(gm_ctx* ctx, const double* x, const double* y, const int64_t* t, int64_t n, int period,
+                int precision, int lenient, int64_t* z, uint8_t* status, gm_batch_status* summary);
+
+/* Z3IndexKeySpace.toIndexKey lines 71-76 (idx/index/z3/Z3IndexKeySpace.scala): epoch millis ->
+   BinnedTime.timeToBinnedTime(period) (z3/curve/BinnedTime.scala:73-86) -> Z3SFC(period).index.
+   Produces the [bin][z] key columns (the row key is [shard?][bin BE16][z BE64][id], :81-92). */
+int gm_z3_index_key(gm_ctx* ctx, const double* x, const double* y, const int64_t* t_ms, int64_t n,
+                    int period, int lenient, int16_t* bin, int64_t* z, uint8_t* status,
+                    gm_batch_status* summary);
+
+/* Z3SFC.invert (z3/curve/Z3SFC.scala:54-57) */
+int gm_z3_invert(gm_ctx* ctx, const int64_t* z, int64_t n, int period, int precision, double* x, double* y,
+                 int64_t* t);
+
+/* Z2SFC.index / invert (z3/curve/Z2SFC.scala:127-146); precision 1..31 (Z2SFC object uses 31) */
+int gm_z2_index(gm_ctx* ctx, const double* x, const double* y, int64_t n, int precision, int lenient,
+                int64_t* z, uint8_t* status, gm_batch_status* summary);
+int gm_z2_invert(gm_ctx* ctx, const int64_t* z, int64_t n, int precision, double* x, double* y);
+
+/* BinnedTime.timeToBinnedTime(period) (z3/curve/BinnedTime.scala:73-86) */
+int gm_binned_time(gm_ctx* ctx, const int64_t* t_ms, int64_t n, int period, int16_t* bin, int64_t* offset,
+                   uint8_t* status, gm_batch_status* summary);
+
+/* XZ2SFC(g).index(xmin, ymin, xmax, ymax, lenient) (z3/curve/XZ2SFC.scala:54-77) */
+int gm_xz2_index(gm_ctx* ctx, const double* xmin, const double* ymin, const double* xmax, const double* ymax,
+                 int64_t n, int g, int lenient, int64_t* out, uint8_t* status, gm_batch_status* summary);
+/* XZ3SFC(g, period).index(xmin, ymin, zmin, xmax, ymax, zmax, lenient) (z3/curve/XZ3SFC.scala:53-76) */
+int gm_xz3_index(gm_ctx* ctx, const double* xmin, const double* ymin, const double* zmin, const double* xmax,
+                 const double* ymax, const double* zmax, int64_t n, int g, int period, int lenient,
+                 int64_t* out, uint8_t* status, gm_batch_status* summary);
+
+/* ------------------------------------------------------------------ range decomposition */
+/* Batched ZN.zranges (z3/zorder/sfcurve/ZN.scala:110-242) as reached from Z3SFC.ranges
+   (z3/curve/Z3SFC.scala:59-67) and Z2SFC.ranges (z3/curve/Z2SFC.scala:148-153).
+   Host inputs, one query per entry of query_off: query q owns boxes [box_off[q], box_off[q+1]) of
+   xy (host, 4 doubles each) and, for Z3, times [time_off[q], time_off[q+1]) of t (host, 2 int64
+   each, offsets within the period).  The z-bounds of a query are the cross product, as in
+   Z3SFC.ranges.  max_ranges <= 0 means None; max_recurse < 0 means the default (Z3:
+   Int.MaxValue, Z2: ZN.DefaultRecurse = 7).  Output (host): ranges of query q are
+   out[out_off[q] .. out_off[q+1]); capacity in ranges.  Returns GM_E_CAPACITY with
+   *needed set when cap is too small. */
+int gm_z3_ranges(gm_ctx* ctx, int64_t n_queries, const int32_t* box_off, const double* xy,
+                 const int32_t* time_off, const int64_t* t, int period, int precision, int range_precision,
+                 int max_ranges, int max_recurse, int64_t* out_off, gm_range* out, int64_t cap,
+                 int64_t* needed, int32_t* query_status);
+int gm_z2_ranges(gm_ctx* ctx, int64_t n_queries, const int32_t* box_off, const double* xy, int precision,
+                 int range_precision, int max_ranges, int max_recurse, int64_t* out_off, gm_range* out,
+                 int64_t cap, int64_t* needed, int32_t* query_status);
+/* Batched XZ2SFC.ranges / XZ3SFC.ranges (z3/curve/XZ2SFC.scala:130-252, XZ3SFC.scala:139-262);
+   windows as above (4 or 6 doubles each, user space). */
+int gm_xz2_ranges(gm_ctx* ctx, int64_t n_queries, const int32_t* win_off, const double* windows, int g,
+                  int max_ranges, int64_t* out_off, gm_range* out, int64_t cap, int64_t* needed,
+                  int32_t* query_status);
+int gm_xz3_ranges(gm_ctx* ctx, int64_t n_queries, const int32_t* win_off, const double* windows, int g,
+                  int period, int max_ranges, int64_t* out_off, gm_range* out, int64_t cap, int64_t* needed,
+                  int32_t* query_status);
+
+/* ------------------------------------------------------------------ filter scans */
+/* Z3Filter.inBounds over columnar keys (idx/filters/Z3Filter.scala:26-62), RowFilterIterator's
+   per-row call (geomesa-accumulo-iterators/.../RowFilterIterator.scala:57) as one pass.
+   filter_bytes (host) is exactly Z3Filter.serializeToBytes (Z3Filter.scala:112-137).
+   bin_ranges (host, n_bin_ranges pairs of int16, inclusive) restricts the scan to the query's
+   epochs (the bins Z3IndexKeySpace.getRanges scans, Z3IndexKeySpace.scala:161-194);
+   n_bin_ranges = 0 scans every bin.
+   Outputs (device, each optional): mask = 1 bit per row (bit i%64 of word i/64, ceil(n/64) words),
+   ids = compacted matching row indices (ids_cap entries, in ascending order).
+   *n_match (host) receives the match count (this call synchronises when n_match != NULL). */
+int gm_z3filter_scan(gm_ctx* ctx, const uint8_t* filter_bytes, size_t filter_len, const int16_t* bin_ranges,
+                     int n_bin_ranges, const int16_t* bin, const int64_t* z, int64_t n, uint64_t* mask,
+                     int64_t* ids, int64_t ids_cap, int64_t* n_match);
+/* Z2Filter.inBounds (idx/filters/Z2Filter.scala:20-35) */
+int gm_z2filter_scan(gm_ctx* ctx, const uint8_t* filter_bytes, size_t filter_len, const int64_t* z, int64_t n,
+                     uint64_t* mask, int64_t* ids, int64_t ids_cap, int64_t* n_match);
+/* Strict full-filter evaluation on raw columns (useFullFilter, Z3IndexKeySpace.scala:240-254):
+   GeoTools BBOX on a point (geomesa-filter/.../GeometryProcessing.scala:129, inclusive) AND
+   FastDuring (geomesa-filter/.../FastTemporalOperator.scala:123-126, exclusive at both ends, ms).
+   bbox (host) = xmin, ymin, xmax, ymax; has_during = 0 skips the time test. */
+int gm_strict_scan(gm_ctx* ctx, const double* x, const double* y, const int64_t* t_ms, int64_t n,
+                   const double* bbox, int has_during, int64_t during_lo_ms, int64_t during_hi_ms,
+                   uint64_t* mask, int64_t* ids, int64_t ids_cap, int64_t* n_match);
+
+/* ------------------------------------------------------------------ st_contains join */
+/* Polygon set in CSR form (host arrays): polygon -> parts (a MultiPolygon's components; a
+   Polygon has one) -> rings (first ring of each part is the shell, the rest are holes) ->
+   vertices.  Rings are closed (first vertex == last vertex), as JTS LinearRings are. */
+typedef struct {
+  int32_t n_polys;
+  const int32_t* poly_part_off; /* [n_polys + 1] */
+  const int32_t* part_ring_off; /* [n_parts + 1] */
+  const int32_t* ring_vert_off; /* [n_rings + 1] */
+  const double* vx;             /* [n_verts] */
+  const double* vy;             /* [n_verts] */
+} gm_polyset;
+
+typedef struct gm_pip_index gm_pip_index;
+
+/* Uploads the polygon set and builds the device-side join index (uniform grid over polygon
+   envelopes -- the analogue of RelationUtils.grid, geomesa-spark-sql/.../RelationUtils.scala:30-157 --
+   plus per-ring y-slab edge buckets). */
+int gm_pip_index_create(gm_ctx* ctx, const gm_polyset* polys, gm_pip_index** out);
+int gm_pip_index_destroy(gm_pip_index* index);
+
+/* ST_Contains(polygon, point) = JTS Geometry.contains (geomesa-spark-jts/.../udf/
+   SpatialRelationFunctions.scala:29), evaluated for every (point, polygon) pair -- the result of
+   GeoMesaJoinRelation.sweeplineJoin + OverlapAction (geomesa-spark-sql/.../GeoMesaJoinRelation.scala:41-91,
+   OverlapAction.scala:25-41) as one batch.  Points are device columns.  Matching pairs go to
+   pt_ids / poly_ids (device, cap entries; point ids are id_base + row); order within the output is
+   unspecified (the reference returns an unordered RDD).  *n_pairs (host) receives the pair count;
+   when it exceeds cap, GM_E_CAPACITY is returned and no pair beyond cap is written.  With
+   pt_ids = poly_ids = NULL the call only counts. */
+int gm_pip_join(gm_ctx* ctx, const gm_pip_index* index, const double* px, const double* py, int64_t n,
+                int64_t id_base, int64_t* pt_ids, int32_t* poly_ids, int64_t cap, int64_t* n_pairs);
+
+/* ------------------------------------------------------------------ synthetic data (bench/tests) */
+/* SplitMix64 keyed by (seed, index): lon U[lon0,lon1), lat U[lat0,lat1), t_ms U[t0,t1) */
+int gm_gen_points(gm_ctx* ctx, uint64_t seed, int64_t n, int64_t index_base, double lon0, double lon1,
+                  double lat0, double lat1, int64_t t0, int64_t t1, double* x, double* y, int64_t* t_ms);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GEOMESA_HIP_H */

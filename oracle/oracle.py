@@ -1,0 +1,332 @@
+"""ctypes wrapper around the C restatement (oracle/gm_oracle.c).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg -- never by the geomesa_amd product package.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "build", "libgm_oracle.so")
+
+DAY, WEEK, MONTH, YEAR = 0, 1, 2, 3
+PERIODS = {"day": DAY, "week": WEEK, "month": MONTH, "year": YEAR}
+
+OK, OUT_OF_BOUNDS, BAD_TIME, UNORDERED = 0, 1, 2, 3
+
+
+class Range(ctypes.Structure):
+    _fields_ = [("lower", ctypes.c_int64), ("upper", ctypes.c_int64),
+                ("contained", ctypes.c_int32), ("pad", ctypes.c_int32)]
+
+
+class PolySet(ctypes.Structure):
+    _fields_ = [("n_polys", ctypes.c_int32),
+                ("poly_part_off", ctypes.c_void_p), ("part_ring_off", ctypes.c_void_p),
+                ("ring_vert_off", ctypes.c_void_p), ("vx", ctypes.c_void_p), ("vy", ctypes.c_void_p)]
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", HERE])
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < os.path.getmtime(
+                os.path.join(HERE, "gm_oracle.c")):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        i64, i32, d, vp = ctypes.c_int64, ctypes.c_int32, ctypes.c_double, ctypes.c_void_p
+        sig = {
+            "gmo_d2i": (i32, [d]), "gmo_d2l": (i64, [d]),
+            "gmo_z3_split": (i64, [i64]), "gmo_z3_combine": (i32, [i64]),
+            "gmo_z3_apply": (i64, [i32, i32, i32]),
+            "gmo_z2_split": (i64, [i64]), "gmo_z2_combine": (i32, [i64]),
+            "gmo_z2_apply": (i64, [i32, i32]),
+            "gmo_zdivide": (None, [ctypes.c_int, i64, i64, i64, vp, vp]),
+            "gmo_zn_contains": (ctypes.c_int, [ctypes.c_int, i64, i64, i64]),
+            "gmo_zn_overlaps": (ctypes.c_int, [ctypes.c_int, i64, i64, i64, i64]),
+            "gmo_zranges": (i64, [ctypes.c_int, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, i64]),
+            "gmo_normalize": (i32, [d, d, ctypes.c_int, d]),
+            "gmo_denormalize": (d, [d, d, ctypes.c_int, i32]),
+            "gmo_max_offset": (i64, [ctypes.c_int]),
+            "gmo_binned_time": (ctypes.c_int, [ctypes.c_int, i64, vp, vp]),
+            "gmo_binned_to_millis": (i64, [ctypes.c_int, ctypes.c_int16, i64]),
+            "gmo_z3_index": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, d, d, i64, ctypes.c_int, vp]),
+            "gmo_z3_invert": (None, [ctypes.c_int, ctypes.c_int, i64, vp, vp, vp]),
+            "gmo_z2_index": (ctypes.c_int, [ctypes.c_int, d, d, ctypes.c_int, vp]),
+            "gmo_z2_invert": (None, [ctypes.c_int, i64, vp, vp]),
+            "gmo_z3_index_key_batch": (None, [ctypes.c_int, vp, vp, vp, i64, ctypes.c_int, vp, vp, vp]),
+            "gmo_z2_index_batch": (None, [vp, vp, i64, ctypes.c_int, vp, vp]),
+            "gmo_z3_invert_batch": (None, [ctypes.c_int, vp, i64, vp, vp, vp]),
+            "gmo_z2_invert_batch": (None, [vp, i64, vp, vp]),
+            "gmo_z3_ranges": (i64, [ctypes.c_int, ctypes.c_int, vp, ctypes.c_int, vp, ctypes.c_int,
+                                    ctypes.c_int, ctypes.c_int, vp, i64]),
+            "gmo_z2_ranges": (i64, [ctypes.c_int, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, i64]),
+            "gmo_xz2_index": (ctypes.c_int, [ctypes.c_int, d, d, d, d, ctypes.c_int, vp]),
+            "gmo_xz3_index": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, d, d, d, d, d, d, ctypes.c_int, vp]),
+            "gmo_xz2_ranges": (i64, [ctypes.c_int, vp, ctypes.c_int, ctypes.c_int, vp, i64]),
+            "gmo_xz3_ranges": (i64, [ctypes.c_int, ctypes.c_int, vp, ctypes.c_int, ctypes.c_int, vp, i64]),
+            "gmo_z3filter_in_bounds": (ctypes.c_int, [vp, ctypes.c_size_t, vp, ctypes.c_int]),
+            "gmo_z2filter_in_bounds": (ctypes.c_int, [vp, ctypes.c_size_t, vp, ctypes.c_int]),
+            "gmo_z3filter_scan": (i64, [vp, ctypes.c_size_t, vp, ctypes.c_int, vp, vp, i64, vp]),
+            "gmo_z2filter_scan": (i64, [vp, ctypes.c_size_t, vp, i64, vp]),
+            "gmo_strict_scan": (i64, [vp, vp, vp, i64, vp, ctypes.c_int, i64, i64, vp]),
+            "gmo_orientation_index": (ctypes.c_int, [d, d, d, d, d, d]),
+            "gmo_locate": (ctypes.c_int, [vp, ctypes.c_int, d, d]),
+            "gmo_contains": (ctypes.c_int, [vp, ctypes.c_int, d, d]),
+            "gmo_pip_join": (i64, [vp, vp, vp, i64, vp, vp, i64, ctypes.c_int]),
+        }
+        for name, (res, args) in sig.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data if a is not None else None
+
+
+# ---------------------------------------------------------------- scalar helpers
+
+def z3_split(v): return lib().gmo_z3_split(v)
+def z3_combine(z): return lib().gmo_z3_combine(z)
+def z3_apply(x, y, t): return lib().gmo_z3_apply(x, y, t)
+def z2_split(v): return lib().gmo_z2_split(v)
+def z2_combine(z): return lib().gmo_z2_combine(z)
+def z2_apply(x, y): return lib().gmo_z2_apply(x, y)
+def d2i(d): return lib().gmo_d2i(d)
+def normalize(mn, mx, p, x): return lib().gmo_normalize(mn, mx, p, x)
+def denormalize(mn, mx, p, i): return lib().gmo_denormalize(mn, mx, p, i)
+def max_offset(period): return lib().gmo_max_offset(period)
+
+
+def zdivide(dims, p, rmin, rmax):
+    a, b = ctypes.c_int64(), ctypes.c_int64()
+    lib().gmo_zdivide(dims, p, rmin, rmax, ctypes.byref(a), ctypes.byref(b))
+    return a.value, b.value
+
+
+def binned_time(period, ms):
+    b, o = ctypes.c_int16(), ctypes.c_int64()
+    st = lib().gmo_binned_time(period, ms, ctypes.byref(b), ctypes.byref(o))
+    return st, b.value, o.value
+
+
+def binned_to_millis(period, b, off): return lib().gmo_binned_to_millis(period, b, off)
+
+
+def z3_index(x, y, t, lenient=False, period=WEEK, precision=21):
+    z = ctypes.c_int64()
+    st = lib().gmo_z3_index(period, precision, x, y, t, int(lenient), ctypes.byref(z))
+    return st, z.value
+
+
+def z3_invert(z, period=WEEK, precision=21):
+    x, y, t = ctypes.c_double(), ctypes.c_double(), ctypes.c_int64()
+    lib().gmo_z3_invert(period, precision, z, ctypes.byref(x), ctypes.byref(y), ctypes.byref(t))
+    return x.value, y.value, t.value
+
+
+def z2_index(x, y, lenient=False, precision=31):
+    z = ctypes.c_int64()
+    st = lib().gmo_z2_index(precision, x, y, int(lenient), ctypes.byref(z))
+    return st, z.value
+
+
+def z2_invert(z, precision=31):
+    x, y = ctypes.c_double(), ctypes.c_double()
+    lib().gmo_z2_invert(precision, z, ctypes.byref(x), ctypes.byref(y))
+    return x.value, y.value
+
+
+def xz2_index(xmin, ymin, xmax, ymax, lenient=False, g=12):
+    z = ctypes.c_int64()
+    st = lib().gmo_xz2_index(g, xmin, ymin, xmax, ymax, int(lenient), ctypes.byref(z))
+    return st, z.value
+
+
+def xz3_index(xmin, ymin, zmin, xmax, ymax, zmax, lenient=False, g=12, period=WEEK):
+    z = ctypes.c_int64()
+    st = lib().gmo_xz3_index(g, period, xmin, ymin, zmin, xmax, ymax, zmax, int(lenient), ctypes.byref(z))
+    return st, z.value
+
+
+def _ranges_call(fn, *args, cap=1 << 16):
+    while True:
+        out = (Range * cap)()
+        n = fn(*args, ctypes.cast(out, ctypes.c_void_p), cap)
+        if n < -(1 << 62):
+            raise ValueError("ranges error code %d" % (n - (-(1 << 63))))
+        if n < 0:
+            cap = -n
+            continue
+        return [(out[i].lower, out[i].upper, bool(out[i].contained)) for i in range(n)]
+
+
+def zranges(dims, bounds, precision=64, max_ranges=None, max_recurse=7):
+    b = np.ascontiguousarray(np.asarray(bounds, dtype=np.int64).reshape(-1))
+    mr = 2147483647 if max_ranges is None else max_ranges
+    rec = 2147483647 if max_recurse is None else max_recurse
+    return _ranges_call(lib().gmo_zranges, dims, _p(b), len(b) // 2, precision, mr, rec)
+
+
+def z3_ranges(xy, t, precision=64, max_ranges=None, period=WEEK):
+    a = np.ascontiguousarray(np.asarray(xy, dtype=np.float64).reshape(-1))
+    tt = np.ascontiguousarray(np.asarray(t, dtype=np.int64).reshape(-1))
+    mr = 2147483647 if max_ranges is None else max_ranges
+    return _ranges_call(lib().gmo_z3_ranges, period, 21, _p(a), len(a) // 4, _p(tt), len(tt) // 2, precision, mr)
+
+
+def z2_ranges(xy, precision=64, max_ranges=None):
+    a = np.ascontiguousarray(np.asarray(xy, dtype=np.float64).reshape(-1))
+    mr = 2147483647 if max_ranges is None else max_ranges
+    return _ranges_call(lib().gmo_z2_ranges, 31, _p(a), len(a) // 4, precision, mr)
+
+
+def xz2_ranges(queries, max_ranges=None, g=12):
+    a = np.ascontiguousarray(np.asarray(queries, dtype=np.float64).reshape(-1))
+    mr = 2147483647 if max_ranges is None else max_ranges
+    return _ranges_call(lib().gmo_xz2_ranges, g, _p(a), len(a) // 4, mr)
+
+
+def xz3_ranges(queries, max_ranges=None, g=12, period=WEEK):
+    a = np.ascontiguousarray(np.asarray(queries, dtype=np.float64).reshape(-1))
+    mr = 2147483647 if max_ranges is None else max_ranges
+    return _ranges_call(lib().gmo_xz3_ranges, g, period, _p(a), len(a) // 6, mr)
+
+
+# ---------------------------------------------------------------- batch helpers (numpy)
+
+def z3_index_key_batch(x, y, t_ms, lenient=False, period=WEEK):
+    x = np.ascontiguousarray(x, np.float64); y = np.ascontiguousarray(y, np.float64)
+    t = np.ascontiguousarray(t_ms, np.int64)
+    n = len(x)
+    b = np.empty(n, np.int16); z = np.empty(n, np.int64); st = np.empty(n, np.uint8)
+    lib().gmo_z3_index_key_batch(period, _p(x), _p(y), _p(t), n, int(lenient), _p(b), _p(z), _p(st))
+    return b, z, st
+
+
+def z2_index_batch(x, y, lenient=False):
+    x = np.ascontiguousarray(x, np.float64); y = np.ascontiguousarray(y, np.float64)
+    n = len(x)
+    z = np.empty(n, np.int64); st = np.empty(n, np.uint8)
+    lib().gmo_z2_index_batch(_p(x), _p(y), n, int(lenient), _p(z), _p(st))
+    return z, st
+
+
+def z3_invert_batch(z, period=WEEK):
+    z = np.ascontiguousarray(z, np.int64)
+    n = len(z)
+    x = np.empty(n); y = np.empty(n); t = np.empty(n, np.int64)
+    lib().gmo_z3_invert_batch(period, _p(z), n, _p(x), _p(y), _p(t))
+    return x, y, t
+
+
+def z2_invert_batch(z):
+    z = np.ascontiguousarray(z, np.int64)
+    n = len(z)
+    x = np.empty(n); y = np.empty(n)
+    lib().gmo_z2_invert_batch(_p(z), n, _p(x), _p(y))
+    return x, y
+
+
+def xz2_index_batch(env, lenient=False, g=12):
+    env = np.asarray(env, np.float64).reshape(-1, 4)
+    out = np.empty(len(env), np.int64); st = np.empty(len(env), np.uint8)
+    for i, (a, b, c, d) in enumerate(env):
+        s, z = xz2_index(a, b, c, d, lenient, g)
+        out[i] = z; st[i] = s
+    return out, st
+
+
+def xz3_index_batch(env, lenient=False, g=12, period=WEEK):
+    env = np.asarray(env, np.float64).reshape(-1, 6)
+    out = np.empty(len(env), np.int64); st = np.empty(len(env), np.uint8)
+    for i, e in enumerate(env):
+        s, z = xz3_index(*e, lenient=lenient, g=g, period=period)
+        out[i] = z; st[i] = s
+    return out, st
+
+
+def z3filter_scan(filter_bytes, bin_ranges, bins, zs):
+    fb = np.frombuffer(bytes(filter_bytes), np.uint8).copy()
+    br = np.ascontiguousarray(np.asarray(bin_ranges, np.int16).reshape(-1))
+    bins = np.ascontiguousarray(bins, np.int16); zs = np.ascontiguousarray(zs, np.int64)
+    m = np.empty(len(zs), np.uint8)
+    c = lib().gmo_z3filter_scan(_p(fb), len(fb), _p(br) if len(br) else None, len(br) // 2, _p(bins), _p(zs),
+                                len(zs), _p(m))
+    if c < 0:
+        raise ValueError("bad filter bytes")
+    return m.astype(bool)
+
+
+def z2filter_scan(filter_bytes, zs):
+    fb = np.frombuffer(bytes(filter_bytes), np.uint8).copy()
+    zs = np.ascontiguousarray(zs, np.int64)
+    m = np.empty(len(zs), np.uint8)
+    c = lib().gmo_z2filter_scan(_p(fb), len(fb), _p(zs), len(zs), _p(m))
+    if c < 0:
+        raise ValueError("bad filter bytes")
+    return m.astype(bool)
+
+
+def z3filter_in_bounds(filter_bytes, row, offset=0):
+    fb = np.frombuffer(bytes(filter_bytes), np.uint8).copy()
+    rb = np.frombuffer(bytes(row), np.uint8).copy()
+    return bool(lib().gmo_z3filter_in_bounds(_p(fb), len(fb), _p(rb), offset))
+
+
+def strict_scan(x, y, t_ms, bbox, during=None):
+    x = np.ascontiguousarray(x, np.float64); y = np.ascontiguousarray(y, np.float64)
+    t = np.ascontiguousarray(t_ms if t_ms is not None else np.zeros(len(x), np.int64), np.int64)
+    bb = np.ascontiguousarray(bbox, np.float64)
+    m = np.empty(len(x), np.uint8)
+    lo, hi = during if during is not None else (0, 0)
+    lib().gmo_strict_scan(_p(x), _p(y), _p(t), len(x), _p(bb), int(during is not None), lo, hi, _p(m))
+    return m.astype(bool)
+
+
+class OraclePolySet:
+    """Keeps numpy CSR arrays alive for the C gmo_polyset view."""
+
+    def __init__(self, poly_part_off, part_ring_off, ring_vert_off, vx, vy):
+        self.arrs = [np.ascontiguousarray(a, np.int32) for a in (poly_part_off, part_ring_off, ring_vert_off)]
+        self.vx = np.ascontiguousarray(vx, np.float64)
+        self.vy = np.ascontiguousarray(vy, np.float64)
+        self.c = PolySet(len(self.arrs[0]) - 1, _p(self.arrs[0]), _p(self.arrs[1]), _p(self.arrs[2]),
+                         _p(self.vx), _p(self.vy))
+
+    def contains(self, poly, x, y):
+        return bool(lib().gmo_contains(ctypes.byref(self.c), poly, x, y))
+
+    def locate(self, poly, x, y):
+        return lib().gmo_locate(ctypes.byref(self.c), poly, x, y)
+
+    def join(self, px, py, nthreads=1):
+        px = np.ascontiguousarray(px, np.float64); py = np.ascontiguousarray(py, np.float64)
+        cap = max(1024, len(px) // 4)
+        while True:
+            pt = np.empty(cap, np.int64); pl = np.empty(cap, np.int32)
+            n = lib().gmo_pip_join(ctypes.byref(self.c), _p(px), _p(py), len(px), _p(pt), _p(pl), cap, nthreads)
+            if n < 0:
+                cap = -n
+                continue
+            return pt[:n].copy(), pl[:n].copy()
+
+
+def orientation_index(p1x, p1y, p2x, p2y, qx, qy):
+    return lib().gmo_orientation_index(p1x, p1y, p2x, p2y, qx, qy)
+
+
+def zn_contains(dims, rmin, rmax, v): return bool(lib().gmo_zn_contains(dims, rmin, rmax, v))
+def zn_overlaps(dims, rmin, rmax, vmin, vmax): return bool(lib().gmo_zn_overlaps(dims, rmin, rmax, vmin, vmax))

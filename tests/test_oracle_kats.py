@@ -1,0 +1,434 @@
+"""Pins the C oracle (oracle/gm_oracle.c) to the reference's own known-answer tests.
+
+Every test cites the reference test it transcribes (paths relative to /root/reference,
+  z3t/ = geomesa-z3/src/test/scala/org/locationtech/geomesa/).
+CPU only: no GPU and no HIP library involved.
+"""
+import datetime
+import math
+
+import pytest
+
+from conftest import load_geoms
+
+WEEK = 1
+UTC = datetime.timezone.utc
+
+
+def ms(s):
+    d = datetime.datetime.fromisoformat(s.replace("Z", "+00:00"))
+    return int(round(d.timestamp() * 1000))
+
+
+# ---------------------------------------------------------------- zorder/sfcurve/Z2Test.scala
+def test_z2_interleave(oracle):  # z3t/zorder/sfcurve/Z2Test.scala:20-29
+    O = oracle
+    assert [O.z2_apply(1, 0), O.z2_apply(2, 0), O.z2_apply(3, 0), O.z2_apply(0, 1), O.z2_apply(0, 2),
+            O.z2_apply(0, 3)] == [1, 4, 5, 2, 8, 10]
+
+
+def test_z2_deinterleave(oracle):  # Z2Test.scala:30-35
+    O = oracle
+    M = 2**31 - 1
+    for (x, y) in [(23, 13), (M, 0), (0, M), (M, M)]:
+        z = O.z2_apply(x, y)
+        assert (O.z2_combine(z), O.z2_combine(z >> 1)) == (x, y)
+
+
+def test_z2_tropf_and_wikipedia(oracle):  # Z2Test.scala:43-72
+    O = oracle
+    rmin, rmax, p = O.z2_apply(5, 3), O.z2_apply(10, 5), O.z2_apply(4, 7)
+    assert (rmin, rmax, p) == (27, 102, 58)
+    assert O.zdivide(2, p, rmin, rmax) == (55, 74)
+    rmin, rmax, p = O.z2_apply(2, 2), O.z2_apply(3, 6), O.z2_apply(5, 1)
+    assert (rmin, rmax, p) == (12, 45, 19)
+    assert O.zdivide(2, p, rmin, rmax) == (15, 36)
+
+
+# the 10 ZRanges of Z2Test.scala:74-85; their endpoints are Z2SFC.index outputs (the inline
+# comments pair coordinates with the wrong lines -- the pairing below is the verified one)
+Z2_GOLDEN = [
+    ((-180, -90), 0), ((180, 90), 4611686018427387903), ((35, 65), 4105065703422263800),
+    ((45, 75), 4261005727442805282), ((-90, -45), 864691128455135232), ((90, 45), 4323455642275676160),
+    ((35, 55), 4069591195588206970), ((37, 68), 4202182393016524625), ((40, 70), 4203729178335734358),
+    ((39.999, 60.999), 4097762467352558080), ((40.001, 61.001), 4097762468106131815),
+    ((51.0, 51.0), 4117455696967246884), ((51.1, 51.1), 4117458209718964953),
+    ((51.001, 51.001), 4117455697154258685), ((51.0000001, 51.0000001), 4117455696967246886)]
+Z2_RANGES = [(0, 4611686018427387903), (864691128455135232, 4323455642275676160),
+             (4105065703422263800, 4261005727442805282), (4069591195588206970, 4261005727442805282),
+             (4105065703422263800, 4202182393016524625), (4105065703422263800, 4203729178335734358),
+             (4097762467352558080, 4097762468106131815), (4117455696967246884, 4117458209718964953),
+             (4117455696967246884, 4117455697154258685), (4117455696967246884, 4117455696967246886)]
+
+
+def test_z2sfc_golden_values(oracle):  # Z2Test.scala:74-85
+    for (x, y), z in Z2_GOLDEN:
+        assert oracle.z2_index(float(x), float(y)) == (0, z)
+
+
+def test_z2_max_ranges(oracle):  # Z2Test.scala:74-93
+    for r in Z2_RANGES:
+        ret = oracle.zranges(2, [r], max_ranges=1000)
+        assert 0 <= len(ret) <= 1000
+
+
+# ---------------------------------------------------------------- zorder/sfcurve/Z3Test.scala
+def test_z3_interleave(oracle):  # z3t/zorder/sfcurve/Z3Test.scala:19-25
+    O = oracle
+    assert [O.z3_apply(1, 0, 0), O.z3_apply(0, 1, 0), O.z3_apply(0, 0, 1), O.z3_apply(1, 1, 1)] == [1, 2, 4, 7]
+
+
+def test_z3_deinterleave_chop(oracle):  # Z3Test.scala:27-33
+    O = oracle
+    M = 2**31 - 1
+
+    def dec(z):
+        return O.z3_combine(z), O.z3_combine(z >> 1), O.z3_combine(z >> 2)
+    assert dec(O.z3_apply(23, 13, 200)) == (23, 13, 200)
+    assert dec(O.z3_apply(M, 0, 0)) == (2097151, 0, 0)
+    assert dec(O.z3_apply(M, 0, M)) == (2097151, 0, 2097151)
+
+
+# ---------------------------------------------------------------- zorder/sfcurve/Z3RangeTest.scala
+def _cut(O, dims, r, xd, in_range):  # ZN.cut (ZN.scala:250-265)
+    lo, hi = r
+    if lo == hi:
+        return []
+    if in_range:
+        if xd == lo:
+            return [(hi, hi)]
+        if xd == hi:
+            return [(lo, lo)]
+        return [(lo, xd - 1), (xd + 1, hi)]
+    litmax, bigmin = O.zdivide(dims, xd, lo, hi)
+    return [(lo, litmax), (bigmin, hi)]
+
+
+def test_z3_range(oracle):  # z3t/zorder/sfcurve/Z3RangeTest.scala:24-61
+    O = oracle
+    Z = O.z3_apply
+    zmin, zmax = Z(2, 2, 0), Z(3, 6, 0)
+    rng = (zmin, zmax)
+    assert _cut(O, 3, (zmin, zmin), Z(0, 0, 0), False) == []
+    assert _cut(O, 3, rng, Z(5, 1, 0), False) == [(zmin, Z(3, 3, 0)), (Z(2, 4, 0), zmax)]
+    assert zmax - zmin + 1 == 130
+    ov = lambda a, b: O.zn_overlaps(3, rng[0], rng[1], a, b)  # noqa: E731
+    assert ov(*rng) and ov(Z(3, 0, 0), Z(3, 2, 0)) and ov(Z(0, 0, 0), Z(2, 2, 0)) and ov(Z(1, 6, 0), Z(4, 6, 0))
+    assert not ov(Z(2, 0, 0), Z(3, 1, 0)) and not ov(Z(4, 6, 0), Z(6, 7, 0))
+
+    def ct(a, b):
+        return O.zn_contains(3, rng[0], rng[1], a) and O.zn_contains(3, rng[0], rng[1], b)
+    assert ct(*rng) and ct(Z(2, 2, 0), Z(3, 3, 0)) and ct(Z(3, 5, 0), Z(3, 6, 0))
+    assert not ct(Z(2, 2, 0), Z(4, 3, 0)) and not ct(Z(2, 1, 0), Z(3, 3, 0)) and not ct(Z(2, 1, 0), Z(3, 7, 0))
+
+
+# ---------------------------------------------------------------- curve/Z3Test.scala, curve/Z2Test.scala
+@pytest.mark.parametrize("dims", [2, 3])
+def test_split_bit_patterns(oracle, jrandom, dims):  # z3t/curve/Z3Test.scala:77-90, Z2Test.scala:64-77
+    O = oracle
+    rand = jrandom(-574)
+    max_int = 2**21 - 1 if dims == 3 else 2**31 - 1
+    nxt = lambda: rand.nextInt(max_int)  # noqa: E731
+    # the specs consume three (Z3) / two (Z2) draws for "apply and unapply" first
+    for _ in range(dims):
+        nxt()
+    splits = [0x00000000ffffff, 0, 1, 0x000000000c0f02, 0x00000000000802] + [nxt() for _ in range(10)]
+    width = 63 if dims == 3 else 62
+    split = O.z3_split if dims == 3 else O.z2_split
+    for v in splits:
+        expected = "".join(("00" if dims == 3 else "0") + c for c in bin(v)[2:])
+        expected = expected.rjust(width, "0")[-width:]
+        got = bin(split(v))[2:].rjust(width, "0")[-width:]
+        assert got == expected
+
+
+@pytest.mark.parametrize("dims", [2, 3])
+def test_bigmin_litmax(oracle, dims):  # curve/Z3Test.scala:110-124, curve/Z2Test.scala:88-101
+    O = oracle
+    if dims == 3:
+        Z = lambda x, y: O.z3_apply(x, y, 0)  # noqa: E731
+        dec = lambda z: (O.z3_combine(z), O.z3_combine(z >> 1), O.z3_combine(z >> 2))  # noqa: E731
+        _, bigmin = O.zdivide(3, Z(5, 1), Z(2, 2), Z(3, 6))
+        litmax, _ = O.zdivide(3, Z(1, 7), Z(2, 2), Z(3, 6))
+        assert dec(bigmin) == (2, 4, 0) and dec(litmax) == (3, 5, 0)
+    else:
+        Z = O.z2_apply
+        dec = lambda z: (O.z2_combine(z), O.z2_combine(z >> 1))  # noqa: E731
+        _, bigmin = O.zdivide(2, Z(5, 1), Z(2, 2), Z(3, 6))
+        litmax, _ = O.zdivide(2, Z(1, 7), Z(2, 2), Z(3, 6))
+        assert dec(bigmin) == (2, 4) and dec(litmax) == (3, 5)
+
+
+def test_calculate_ranges(oracle):  # curve/Z3Test.scala:169-180, curve/Z2Test.scala:103-115
+    O = oracle
+    Z = lambda x, y: O.z3_apply(x, y, 0)  # noqa: E731
+    r = O.zranges(3, [(Z(2, 2), Z(3, 6))])
+    assert sorted(r) == sorted([(Z(2, 2), Z(3, 3), True), (Z(2, 4), Z(3, 5), True), (Z(2, 6), Z(3, 6), True)])
+    Z2 = O.z2_apply
+    r = O.zranges(2, [(Z2(2, 2), Z2(3, 6))])
+    assert sorted(r) == sorted([(Z2(2, 2), Z2(3, 3), True), (Z2(2, 4), Z2(3, 5), True), (Z2(2, 6), Z2(3, 6), True)])
+
+
+def z3_test_boxes(O):
+    """The 17 query boxes of curve/Z3Test.scala:188-206 (modern Z3SFC(Week))."""
+    week = 604800
+    day, hour = week // 7, week // 168
+    idx = lambda x, y, t: O.z3_index(float(x), float(y), int(t))[1]  # noqa: E731
+    b = [
+        (idx(-180, -90, 0), idx(180, 90, week)), (idx(-180, -90, day), idx(180, 90, day * 2)),
+        (idx(-180, -90, hour * 10), idx(180, 90, hour * 11)), (idx(-180, -90, hour * 10), idx(180, 90, hour * 64)),
+        (idx(-180, -90, day * 2), idx(180, 90, week)), (idx(-90, -45, week // 4), idx(90, 45, 3 * week // 4)),
+        (idx(35, 65, 0), idx(45, 75, day)), (idx(35, 55, 0), idx(45, 65, week)),
+        (idx(35, 55, day), idx(45, 75, day * 2)), (idx(35, 55, day + hour * 6), idx(45, 75, day * 2)),
+        (idx(35, 65, day + hour), idx(45, 75, day * 6)), (idx(35, 65, day), idx(37, 68, day + hour * 6)),
+        (idx(35, 65, day), idx(40, 70, day + hour * 6)),
+        (idx(39.999, 60.999, day + 3000), idx(40.001, 61.001, day + 3120)),
+        (idx(51.0, 51.0, 6000), idx(51.1, 51.1, 6100)), (idx(51.0, 51.0, 30000), idx(51.001, 51.001, 30100)),
+        (idx(51.0, 51.0, 30000) - 1, idx(51.0, 51.0, 30000) + 1)]
+    return b
+
+
+def test_z3_nonempty_ranges(oracle):  # curve/Z3Test.scala:182-220
+    for r in z3_test_boxes(oracle):
+        ret = oracle.zranges(3, [r], max_ranges=1000)
+        assert 0 < len(ret) <= 1000
+
+
+def test_z2_nonempty_ranges(oracle):  # curve/Z2Test.scala:117-143
+    O = oracle
+    idx = lambda x, y: O.z2_index(float(x), float(y))[1]  # noqa: E731
+    boxes = [((-180, -90), (180, 90)), ((-90, -45), (90, 45)), ((35, 65), (45, 75)), ((35, 55), (45, 75)),
+             ((35, 65), (37, 68)), ((35, 65), (40, 70)), ((39.999, 60.999), (40.001, 61.001)),
+             ((51.0, 51.0), (51.1, 51.1)), ((51.0, 51.0), (51.001, 51.001)), ((51.0, 51.0), (51.0000001, 51.0000001))]
+    for a, b in boxes:
+        ret = O.zranges(2, [(idx(*a), idx(*b))], max_ranges=1000)
+        assert 0 < len(ret) <= 1000
+
+
+@pytest.mark.parametrize("period", [0, 1, 2, 3])
+def test_z3_fail_out_of_bounds(oracle, period):  # curve/Z3Test.scala:58-75
+    O = oracle
+    tmax = O.max_offset(period)
+    for (x, y, t) in [(-180.1, 0, 0), (180.1, 0, 0), (0, -90.1, 0), (0, 90.1, 0), (0, 0, -1), (0, 0, tmax + 1),
+                      (-181, -91, -1), (181, 91, tmax + 1)]:
+        assert O.z3_index(float(x), float(y), int(t), period=period)[0] == O.OUT_OF_BOUNDS
+        assert O.z3_index(float(x), float(y), int(t), lenient=True, period=period)[0] == O.OK
+
+
+def test_z2_fail_out_of_bounds(oracle):  # curve/Z2Test.scala:57-62
+    for (x, y) in [(-180.1, 0), (0, -90.1), (180.1, 0), (0, 90.1), (-181, -91), (181, 91)]:
+        assert oracle.z2_index(float(x), float(y))[0] == oracle.OUT_OF_BOUNDS
+
+
+def test_z3_apply_unapply_max(oracle):  # curve/Z3Test.scala:44-56
+    O = oracle
+    m = 2**21 - 1
+    z = O.z3_apply(m, m, m)
+    assert (O.z3_combine(z), O.z3_combine(z >> 1), O.z3_combine(z >> 2)) == (m, m, m)
+    assert z == 2**63 - 1  # full-range key is Long.MaxValue
+
+
+# ---------------------------------------------------------------- curve/NormalizedDimensionTest.scala
+@pytest.mark.parametrize("mn,mx", [(-90.0, 90.0), (-180.0, 180.0)])
+def test_normalized_dimension(oracle, mn, mx):  # z3t/curve/NormalizedDimensionTest.scala:24-58
+    O = oracle
+    p = 31
+    max_bin = 2**31 - 1
+    assert O.normalize(mn, mx, p, O.denormalize(mn, mx, p, 0)) == 0
+    assert O.normalize(mn, mx, p, O.denormalize(mn, mx, p, max_bin)) == max_bin
+    assert O.normalize(mn, mx, p, mn) == 0
+    assert O.normalize(mn, mx, p, mx) == max_bin
+    width = (mx - mn) / (max_bin + 1)
+    assert O.denormalize(mn, mx, p, 0) == mn + width / 2.0
+    assert O.denormalize(mn, mx, p, max_bin) == mx - width / 2.0
+
+
+# ---------------------------------------------------------------- curve/BinnedTimeTest.scala
+def _seeded_times(jrandom):
+    """The 10 dates of BinnedTimeTest.scala:28-38 (Random(-574))."""
+    rand = jrandom(-574)
+    out = []
+    for _ in range(10):
+        years, months, days = rand.nextInt(40), rand.nextInt(12), rand.nextInt(28)
+        hours, mins, secs, millis = rand.nextInt(24), rand.nextInt(60), rand.nextInt(60), rand.nextInt(1000)
+        y, m = 1970 + years + (months // 12), 1 + months % 12
+        d = datetime.datetime(y, m, 1, tzinfo=UTC) + datetime.timedelta(days=days, hours=hours, minutes=mins,
+                                                                         seconds=secs, milliseconds=millis)
+        out.append(int(round(d.timestamp() * 1000)))
+    return out
+
+
+def test_binned_time_round_trips(oracle, jrandom):  # BinnedTimeTest.scala:61-90
+    O = oracle
+    for t in _seeded_times(jrandom):
+        sub_ms = t % 1000
+        for period, expect in [(O.WEEK, t - sub_ms), (O.DAY, t), (O.MONTH, t - sub_ms),
+                               (O.YEAR, t - sub_ms - ((t // 1000) % 60) * 1000)]:
+            st, b, off = O.binned_time(period, t)
+            assert st == O.OK
+            assert O.binned_to_millis(period, b, off) == expect
+
+
+def test_binned_time_joda_compat(oracle, jrandom):  # BinnedTimeTest.scala:92-119 (Joda *Between semantics)
+    O = oracle
+    epoch = datetime.datetime(1970, 1, 1, tzinfo=UTC)
+    for t in _seeded_times(jrandom):
+        dt = epoch + datetime.timedelta(milliseconds=t)
+        days = t // 86400000
+        assert O.binned_time(O.DAY, t)[1:] == (days, t - days * 86400000)
+        weeks = days // 7
+        assert O.binned_time(O.WEEK, t)[1:] == (weeks, (t - weeks * 604800000) // 1000)
+        months = (dt.year - 1970) * 12 + dt.month - 1
+        mstart = datetime.datetime(dt.year, dt.month, 1, tzinfo=UTC)
+        assert O.binned_time(O.MONTH, t)[1:] == (months, (t - int(mstart.timestamp() * 1000)) // 1000)
+        ystart = datetime.datetime(dt.year, 1, 1, tzinfo=UTC)
+        assert O.binned_time(O.YEAR, t)[1:] == (dt.year - 1970, (t - int(ystart.timestamp() * 1000)) // 60000)
+
+
+def test_binned_time_bounds(oracle):  # BinnedTime.scala:62-65,222-226 (require before/after)
+    O = oracle
+    assert O.binned_time(O.WEEK, -1)[0] == O.BAD_TIME
+    assert O.binned_time(O.WEEK, 32768 * 604800000 - 1)[0] == O.OK
+    assert O.binned_time(O.WEEK, 32768 * 604800000)[0] == O.BAD_TIME
+    assert O.binned_time(O.DAY, 32768 * 86400000)[0] == O.BAD_TIME
+    # months: 1970-01 + 32768 months = 4700-09-01
+    m_end = int(datetime.datetime(4700, 9, 1, tzinfo=UTC).timestamp() * 1000)
+    assert O.binned_time(O.MONTH, m_end - 1)[0] == O.OK
+    assert O.binned_time(O.MONTH, m_end)[0] == O.BAD_TIME
+
+
+# ---------------------------------------------------------------- curve/XZ2SFCTest.scala / XZ3SFCTest.scala
+CONTAINING = [(9.0, 9.0, 13.0, 13.0), (-180.0, -90.0, 180.0, 90.0), (0.0, 0.0, 180.0, 90.0), (0.0, 0.0, 20.0, 20.0)]
+OVERLAPPING = [(11.0, 11.0, 13.0, 13.0), (9.0, 9.0, 11.0, 11.0), (10.5, 10.5, 11.5, 11.5), (11.0, 11.0, 11.0, 11.0)]
+DISJOINT = [(-180.0, -90.0, 8.0, 8.0), (0.0, 0.0, 8.0, 8.0), (9.0, 9.0, 9.5, 9.5), (20.0, 20.0, 180.0, 90.0)]
+
+
+def _hit(ranges, v):
+    return any(lo <= v <= hi for (lo, hi, _) in ranges)
+
+
+def test_xz2_polygons_and_points(oracle):  # z3t/curve/XZ2SFCTest.scala:24-103
+    O = oracle
+    poly = O.xz2_index(10, 10, 12, 12)[1]
+    for b in CONTAINING + OVERLAPPING:
+        assert _hit(O.xz2_ranges([b]), poly)
+    for b in DISJOINT:
+        assert not _hit(O.xz2_ranges([b]), poly)
+    pt = O.xz2_index(11, 11, 11, 11)[1]
+    for b in CONTAINING + OVERLAPPING:
+        assert _hit(O.xz2_ranges([b]), pt)
+    for b in DISJOINT + [(12.5, 12.5, 13.5, 13.5)]:
+        assert not _hit(O.xz2_ranges([b]), pt)
+
+
+def test_xz2_geoms_list(oracle):  # XZ2SFCTest.scala:105-128
+    geoms = load_geoms()
+    assert len(geoms) == 135
+    ranges = oracle.xz2_ranges([(45.0, 23.0, 48.0, 27.0)])
+    for g in geoms:
+        st, v = oracle.xz2_index(*g)
+        assert st == 0 and _hit(ranges, v)
+
+
+def test_xz2_fail_out_of_bounds(oracle):  # XZ2SFCTest.scala:130-148
+    for b in [(-180.1, 0, -179.9, 1), (179.9, 0, 180.1, 1), (-180.3, 0, -180.1, 1), (180.1, 0, 180.3, 1),
+              (-180.1, 0, 180.1, 1), (0, -90.1, 1, -89.9), (0, 89.9, 1, 90.1), (0, -90.3, 1, -90.1),
+              (0, 90.1, 1, 90.3), (0, -90.1, 1, 90.1), (-181, -91, 0, 0), (0, 0, 181, 91)]:
+        assert oracle.xz2_index(*[float(v) for v in b])[0] == oracle.OUT_OF_BOUNDS
+
+
+def _w3(b):
+    return (b[0], b[1], 900.0, b[2], b[3], 1100.0)
+
+
+def test_xz3_polygons_and_points(oracle):  # z3t/curve/XZ3SFCTest.scala:24-103
+    O = oracle
+    poly = O.xz3_index(10, 10, 1000, 12, 12, 1000)[1]
+    for b in CONTAINING + OVERLAPPING:
+        assert _hit(O.xz3_ranges([_w3(b)], max_ranges=10000), poly)
+    for b in DISJOINT:
+        assert not _hit(O.xz3_ranges([_w3(b)], max_ranges=10000), poly)
+    pt = O.xz3_index(11, 11, 1000, 11, 11, 1000)[1]
+    for b in CONTAINING + OVERLAPPING:
+        assert _hit(O.xz3_ranges([_w3(b)], max_ranges=10000), pt)
+    for b in DISJOINT:
+        assert not _hit(O.xz3_ranges([_w3(b)], max_ranges=10000), pt)
+
+
+def test_xz3_geoms_list(oracle):  # XZ3SFCTest.scala:105-128
+    ranges = oracle.xz3_ranges([(45.0, 23.0, 900.0, 48.0, 27.0, 1100.0)], max_ranges=10000)
+    for g in load_geoms():
+        st, v = oracle.xz3_index(g[0], g[1], 1000.0, g[2], g[3], 1000.0)
+        assert st == 0 and _hit(ranges, v)
+
+
+def test_xz3_fail_out_of_bounds(oracle):  # XZ3SFCTest.scala:130-154
+    tmin, tmax = 0.0, 604800.0
+    for b in [(-180.1, 0, 0, -179.9, 1, 1), (179.9, 0, 0, 180.1, 1, 1), (-180.3, 0, 0, -180.1, 1, 1),
+              (180.1, 0, 0, 180.3, 1, 1), (-180.1, 0, 0, 180.1, 1, 1), (0, -90.1, 0, 1, -89.9, 1),
+              (0, 89.9, 0, 1, 90.1, 1), (0, -90.3, 0, 1, -90.1, 1), (0, 90.1, 0, 1, 90.3, 1),
+              (0, -90.1, 0, 1, 90.1, 1), (0, 0, tmin - 0.1, 1, 1, tmin + 0.1), (0, 0, tmax - 0.1, 1, 1, tmax + 0.1),
+              (0, 0, tmin - 0.3, 1, 1, tmin - 0.1), (0, 0, tmax + 0.1, 1, 1, tmax + 0.3),
+              (0, 0, tmin - 0.1, 1, 1, tmax + 0.1), (-181, -91, tmin - 1, 0, 0, 0), (0, 0, 0, 181, 91, tmax + 1)]:
+        assert oracle.xz3_index(*[float(v) for v in b])[0] == oracle.OUT_OF_BOUNDS
+
+
+# ---------------------------------------------------------------- SURVEY Appendix A hazards
+def test_normalize_overshoot_wrap(oracle):  # SURVEY Appendix A.3 (Z3 wraps lon index to 0)
+    O = oracle
+    x = math.nextafter(180.0, 0.0)
+    assert O.normalize(-180.0, 180.0, 21, x) == 2**21
+    st, z = O.z3_index(x, 0.0, 0)
+    assert st == 0 and O.z3_combine(z) == 0
+    assert O.normalize(-180.0, 180.0, 31, x) == 2**31 - 1  # Z2: saturates to Int.MaxValue
+
+
+def test_jvm_d2i(oracle):
+    O = oracle
+    assert O.d2i(float("nan")) == 0 and O.d2i(1e300) == 2**31 - 1 and O.d2i(-1e300) == -2**31
+    assert O.d2i(-1.5) == -1 and O.d2i(2147483647.9) == 2**31 - 1
+
+
+# ---------------------------------------------------------------- JTS st_contains box KATs
+def test_st_contains_box(oracle):  # geomesa-spark-jts/.../SpatialRelationFunctionsTest.scala:85-107
+    box = [[[[(0, 0), (0, 10), (10, 10), (10, 0), (0, 0)]]]]
+    ps = _polyset(box)
+    assert ps.contains(0, 5.0, 5.0)
+    assert not ps.contains(0, 0.0, 5.0)    # edge
+    assert not ps.contains(0, 0.0, 0.0)    # corner
+    assert not ps.contains(0, -5.0, 0.0)   # exterior
+
+
+def _polyset(polys):
+    import numpy as np
+    ppo, pro, rvo, vx, vy = [0], [0], [0], [], []
+    for poly in polys:
+        for part in poly:
+            for ring in part:
+                for (x, y) in ring:
+                    vx.append(float(x)); vy.append(float(y))
+                rvo.append(len(vx))
+            pro.append(len(rvo) - 1)
+        ppo.append(len(pro) - 1)
+    import oracle as O
+    return O.OraclePolySet(np.array(ppo), np.array(pro), np.array(rvo), np.array(vx), np.array(vy))
+
+
+def test_contains_holes_and_mod2(oracle):  # JTS PointLocator semantics (parity unpinned beyond the box KATs)
+    sq = lambda x0, y0, x1, y1: [(x0, y0), (x0, y1), (x1, y1), (x1, y0), (x0, y0)]  # noqa: E731
+    ps = _polyset([[[sq(0, 0, 10, 10), sq(3, 3, 6, 6)]],             # polygon with hole
+                   [[sq(0, 0, 5, 10)], [sq(5, 0, 10, 10)]]])          # 2 parts sharing the edge x = 5
+    assert ps.contains(0, 1.0, 1.0)
+    assert not ps.contains(0, 4.0, 4.0)      # in hole -> exterior
+    assert not ps.contains(0, 3.0, 4.0)      # hole boundary -> boundary
+    assert ps.contains(1, 5.0, 5.0)          # shared edge: 2 boundaries, Mod-2 -> interior
+    assert ps.contains(1, 2.0, 5.0)
+    assert not ps.contains(1, 0.0, 5.0)
+
+
+def test_orientation_dd_path(oracle):
+    O = oracle
+    # collinear points exactly, and a near-collinear case that needs the DD fallback
+    assert O.orientation_index(0.0, 0.0, 1.0, 1.0, 2.0, 2.0) == 0
+    assert O.orientation_index(0.0, 0.0, 1.0, 1.0, 0.5, 0.5000000000000001) == 1
+    assert O.orientation_index(0.0, 0.0, 1.0, 1.0, 0.5000000000000001, 0.5) == -1
