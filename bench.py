@@ -208,7 +208,9 @@ def main():
     P = _lib.ptr
 
     def z3_step():
-        lib.gm_z3_index_key(h, P(x), P(y), P(t), N, 1, 0, P(b), P(z), None, None)
+        rc = lib.gm_z3_index_key(h, P(x), P(y), P(t), N, 1, 0, P(b), P(z), None, None)
+        if rc:
+            _lib.check(rc, "gm_z3_index_key")
     ms = None
     if "z3" in only:
         ms = timed(dist, z3_step, a.steps, a.warmup)
@@ -228,7 +230,11 @@ def main():
     # ---------------------------------------------------------------- extra hot-path kernels on the same data
     if "extra" in only and not a.no_extra:
         def rec(name, fn, bytes_per_unit, n_units, unit="points/s", steps=max(3, a.steps // 2)):
-            m = timed(dist, fn, steps, 1)
+            def step():
+                rc = fn()
+                if rc:
+                    _lib.check(rc, name)
+            m = timed(dist, step, steps, 1)
             extra[name] = {"value": n_units * dist.world / (m * 1e-3), "unit": unit, "ms_per_step": m,
                            "roofline": roofline(bytes_per_unit * n_units, m, load_pmc(name, n_units))}
         xi = torch.empty_like(x); yi = torch.empty_like(y); ti = torch.empty_like(t)
@@ -265,14 +271,17 @@ def main():
             w = 10 ** rng.uniform(-1, 1); hh = 10 ** rng.uniform(-1, 1)
             cx = rng.uniform(-170, 170); cy = rng.uniform(-80, 80); t0 = int(rng.integers(0, 500000))
             qs.append(([(cx - w, cy - hh, cx + w, cy + hh)], [(t0, t0 + 86400)]))
+        from geomesa_amd import ranges as R
+        fn, args, nq, cap = R.prepare_z3(sfc, qs, 64, 2000)
+        offs, rr, _ = R.call_raw(fn, args, nq, cap)
         t0w = time.time()
-        for _ in range(2):
-            sfc.ranges_batch(qs, 64, 2000)
-        torch.cuda.synchronize()
-        dt = (time.time() - t0w) / 2
+        for _ in range(3):
+            R.call_raw(fn, args, nq, cap)
+        dt = (time.time() - t0w) / 3
         extra["z3_ranges_batch"] = {"value": len(qs) * dist.world / dt, "unit": "queries/s",
-                                    "ms_per_step": dt * 1e3, "note": "host-driven incl. H2D/D2H, 4096 queries, "
-                                                                     "maxRanges 2000"}
+                                    "ms_per_step": dt * 1e3, "ranges": int(offs[-1]),
+                                    "note": "C-ABI call incl. H2D of queries and D2H of ranges; 4096 Z3 queries "
+                                            "(0.2-20 deg boxes x 1 day), maxRanges 2000 (ScanRangesTarget)"}
     del x, y, t, b, z
     torch.cuda.empty_cache()
 
@@ -303,7 +312,9 @@ def main():
         npairs = __import__("ctypes").c_int64()
 
         def join_step():
-            lib.gm_pip_join(h, ix._h, P(px), P(py), J, dist.rank * J, P(ptids), P(plids), cap, None)
+            rc = lib.gm_pip_join(h, ix._h, P(px), P(py), J, dist.rank * J, P(ptids), P(plids), cap, None)
+            if rc:
+                _lib.check(rc, "gm_pip_join")
         jms = timed(dist, join_step, a.join_steps, 1)
         _lib.check(lib.gm_pip_join(h, ix._h, P(px), P(py), J, dist.rank * J, P(ptids), P(plids), cap,
                                    __import__("ctypes").byref(npairs)), "join")

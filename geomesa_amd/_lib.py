@@ -57,6 +57,7 @@ sz = ctypes.c_size_t
 SIGNATURES = {
     "gm_abi_version": (cint, []),
     "gm_ctx_create": (cint, [cint, vp, vp]),
+    "gm_ctx_create_owned": (cint, [cint, vp]),
     "gm_ctx_destroy": (cint, [vp]),
     "gm_ctx_sync": (cint, [vp]),
     "gm_ctx_stream": (vp, [vp]),

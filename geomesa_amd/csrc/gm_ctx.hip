@@ -78,7 +78,7 @@ int gm_abi_version(void) { return GM_ABI_VERSION; }
 
 const char* gm_last_error(void) { return g_last_error.c_str(); }
 
-int gm_ctx_create(int device, void* stream, gm_ctx** out) {
+static int ctx_create(int device, void* stream, bool own, gm_ctx** out) {
   if (!out) return GM_E_INVALID;
   *out = nullptr;
   int ndev = 0;
@@ -90,8 +90,8 @@ int gm_ctx_create(int device, void* stream, gm_ctx** out) {
   GM_HIP(hipSetDevice(device));
   gm_ctx* c = new gm_ctx();
   c->device = device;
-  if (stream) {
-    c->stream = (hipStream_t)stream;
+  if (!own) {
+    c->stream = (hipStream_t)stream;  // NULL = the device's default (null) stream
   } else {
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e != hipSuccess) { delete c; return gm::hip_fail(e, "hipStreamCreate"); }
@@ -106,6 +106,10 @@ int gm_ctx_create(int device, void* stream, gm_ctx** out) {
   *out = c;
   return GM_OK;
 }
+
+int gm_ctx_create(int device, void* stream, gm_ctx** out) { return ctx_create(device, stream, false, out); }
+
+int gm_ctx_create_owned(int device, gm_ctx** out) { return ctx_create(device, nullptr, true, out); }
 
 int gm_ctx_destroy(gm_ctx* c) {
   if (!c) return GM_OK;

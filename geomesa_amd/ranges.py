@@ -16,26 +16,59 @@ _QS_MSG = {1: "Value(s) out of bounds", 3: "Bounds must be ordered", 4: "range w
            5: "too many bounds in one query (max 256)"}
 
 
-def _run(fn, args, nq, cap):
+RANGE_DTYPE = np.dtype([("lower", "<i8"), ("upper", "<i8"), ("contained", "<i4"), ("reserved", "<i4")])
+
+
+class RangeList:
+    """Ranges of one query: a sequence of IndexRange backed by the numpy result of the batch."""
+
+    def __init__(self, arr):
+        self.arr = arr
+
+    def __len__(self):
+        return len(self.arr)
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            return [self[k] for k in range(*i.indices(len(self)))]
+        r = self.arr[i]
+        return IndexRange(int(r["lower"]), int(r["upper"]), bool(r["contained"]))
+
+    def __iter__(self):
+        lo, hi, c = self.arr["lower"].tolist(), self.arr["upper"].tolist(), self.arr["contained"].tolist()
+        return (IndexRange(a, b, bool(k)) for a, b, k in zip(lo, hi, c))
+
+    def __eq__(self, o):
+        return list(self) == list(o)
+
+    def __repr__(self):
+        return repr(list(self))
+
+
+def call_raw(fn, args, nq, cap):
+    """Runs one batched ranges entry point; returns (offsets[nq+1], ranges structured array, status)."""
     cap = max(int(cap), 1024)
     while True:
         out_off = np.zeros(nq + 1, np.int64)
-        out = (_lib.Range * cap)()
+        out = np.zeros(cap, RANGE_DTYPE)
         needed = ctypes.c_int64()
         qst = np.zeros(max(nq, 1), np.int32)
-        rc = fn(*args, out_off.ctypes.data, ctypes.cast(out, ctypes.c_void_p), cap, ctypes.byref(needed),
-                qst.ctypes.data)
+        rc = fn(*args, out_off.ctypes.data, out.ctypes.data, cap, ctypes.byref(needed), qst.ctypes.data)
         if rc == _lib.GM_E_CAPACITY:
             cap = needed.value + 1024
             continue
         check(rc, fn.__name__)
-        res = []
-        for q in range(nq):
-            if qst[q] != 0:
-                raise IllegalArgumentException("query %d: %s" % (q, _QS_MSG.get(int(qst[q]), "error %d" % qst[q])))
-            res.append([IndexRange(out[i].lower, out[i].upper, bool(out[i].contained))
-                        for i in range(int(out_off[q]), int(out_off[q + 1]))])
-        return res
+        return out_off, out, qst
+
+
+def _run(fn, args, nq, cap):
+    out_off, out, qst = call_raw(fn, args, nq, cap)
+    res = []
+    for q in range(nq):
+        if qst[q] != 0:
+            raise IllegalArgumentException("query %d: %s" % (q, _QS_MSG.get(int(qst[q]), "error %d" % qst[q])))
+        res.append(RangeList(out[int(out_off[q]):int(out_off[q + 1])]))
+    return res
 
 
 def _mr(max_ranges):
@@ -44,6 +77,11 @@ def _mr(max_ranges):
 
 def z3_ranges(sfc, queries, precision=64, max_ranges=None, max_recurse=None):
     """queries: [(xy boxes [(xmin, ymin, xmax, ymax)], t intervals [(tmin, tmax)])]."""
+    return _run(*prepare_z3(sfc, queries, precision, max_ranges, max_recurse))
+
+
+def prepare_z3(sfc, queries, precision=64, max_ranges=None, max_recurse=None):
+    """(entry point, argument tuple, n_queries, capacity) for gm_z3_ranges (host arrays kept alive)."""
     ctx = _lib.context()
     nq = len(queries)
     box_off, time_off, xy, tt = [0], [0], [], []
@@ -59,7 +97,12 @@ def z3_ranges(sfc, queries, precision=64, max_ranges=None, max_recurse=None):
     cap = nq * (max_ranges + 16 if max_ranges else 4096)
     args = (ctx.handle, nq, bo.ctypes.data, xya.ctypes.data, to.ctypes.data, ta.ctypes.data, sfc.period,
             sfc.precision, int(precision), _mr(max_ranges), -1 if max_recurse is None else int(max_recurse))
-    return _run(ctx.lib.gm_z3_ranges, args, nq, cap)
+    _keep.append((bo, to, xya, ta))
+    del _keep[:-8]
+    return ctx.lib.gm_z3_ranges, args, nq, cap
+
+
+_keep = []
 
 
 def z2_ranges(sfc, queries, precision=64, max_ranges=None, max_recurse=None):

@@ -73,8 +73,11 @@ typedef struct {
 
 /* ------------------------------------------------------------------ context */
 int gm_abi_version(void);
-/* stream: a hipStream_t to launch on (NULL = a new non-blocking stream owned by the context) */
+/* stream: the hipStream_t every call of this context launches on (NULL = the default null stream,
+   which is also PyTorch's default stream) */
 int gm_ctx_create(int device, void* stream, gm_ctx** out);
+/* same, on a new non-blocking stream owned (and destroyed) by the context */
+int gm_ctx_create_owned(int device, gm_ctx** out);
 int gm_ctx_destroy(gm_ctx* ctx);
 int gm_ctx_sync(gm_ctx* ctx);
 void* gm_ctx_stream(gm_ctx* ctx);

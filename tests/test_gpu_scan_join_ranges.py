@@ -176,7 +176,7 @@ def test_z3_ranges_batch_parity(gpu, oracle, max_ranges):
     from geomesa_amd.curve import Z3SFC
     qs = ranges_queries(40 if max_ranges is None else 300)
     if max_ranges is None:
-        qs = [((b[0], b[1], b[0] + 0.01, b[1] + 0.01), (t[0], t[0] + 600)) for b, t in qs]
+        qs = [((b[0], b[1], b[0] + 0.001, b[1] + 0.001), (t[0], t[0] + 60)) for b, t in qs]
     got = Z3SFC("week").ranges_batch([([b], [t]) for b, t in qs], 64, max_ranges)
     for (b, t), g in zip(qs, got):
         exp = oracle.z3_ranges([b], [t], max_ranges=max_ranges)
