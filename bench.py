@@ -41,6 +41,7 @@ def parse():
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=8.0)
     p.add_argument("--only", default="", help="comma list: z3,join,extra (profiling)")
+    p.add_argument("--cells-per-poly", type=int, default=0, help="join grid density (0 = library default)")
     return p.parse_args()
 
 
@@ -301,7 +302,9 @@ def main():
                 dist.pg.broadcast(tt, 0)
                 tens.append(tt.cpu().numpy())
             ps = PolygonSet(*tens)
-        ix = PolygonIndex(ps, ctx)
+        t_ix = time.time()
+        ix = PolygonIndex(ps, ctx, a.cells_per_poly)
+        t_ix = time.time() - t_ix
         px = torch.empty(J, dtype=torch.float64, device=dev)
         py = torch.empty(J, dtype=torch.float64, device=dev)
         gen_points(ctx, J, dist.rank * J + (1 << 40), CONUS, px, py, None)
@@ -322,7 +325,7 @@ def main():
         pairs = J * ps.n_polys * dist.world
         pj = {"value": pairs / (jms * 1e-3), "unit": "pairs/s", "ms_per_step": jms, "points_per_gpu": J,
               "polygons": ps.n_polys, "vertices": ps.n_vertices, "matches": matches,
-              "matches_per_s": matches / (jms * 1e-3),
+              "matches_per_s": matches / (jms * 1e-3), "index_build_s": round(t_ix, 3), "index": ix.stats(),
               "roofline": roofline(16.0 * J + 12.0 * npairs.value, jms, load_pmc("pip_join", J)),
               "workload": "st_contains(polygon, point) join, %d CONUS points/GPU x %d synthetic county polygons "
                           "(BASELINE configs[3]); polygon set broadcast over RCCL when N > 1" % (J, ps.n_polys)}

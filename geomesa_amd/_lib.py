@@ -84,7 +84,9 @@ SIGNATURES = {
     "gm_z2filter_scan": (cint, [vp, vp, sz, vp, i64, vp, vp, i64, vp]),
     "gm_strict_scan": (cint, [vp, vp, vp, vp, i64, vp, cint, i64, i64, vp, vp, i64, vp]),
     "gm_pip_index_create": (cint, [vp, vp, vp]),
+    "gm_pip_index_create_ex": (cint, [vp, vp, cint, vp]),
     "gm_pip_index_destroy": (cint, [vp]),
+    "gm_pip_index_stats": (cint, [vp, vp]),
     "gm_pip_join": (cint, [vp, vp, vp, vp, i64, i64, vp, vp, i64, vp]),
     "gm_gen_points": (cint, [vp, ctypes.c_uint64, i64, i64, d, d, d, d, i64, i64, vp, vp, vp]),
 }

@@ -7,16 +7,23 @@
 // relate -> PointLocator with the Mod-2 boundary rule; rings via RayCrossingCounter with the robust
 // CGAlgorithmsDD orientation (filter + double-double).  Boundary points are NOT contained.
 //
-// Index (built once on the host from the polygon CSR, uploaded; the analogue of broadcasting the
-// polygon side):
-//   * uniform grid over the polygon set's envelope; every (cell, polygon) whose envelopes meet is
-//     classified INTERIOR (no edge of the polygon touches the closed cell, cell inside: every point
-//     of the cell is contained -- no edge test at all), EXTERIOR (dropped) or BOUNDARY (exact test);
-//   * per ring: y-slab buckets of its segments, so a BOUNDARY test only visits the segments whose
-//     y-range holds the point's y -- the only ones RayCrossingCounter.countSegment can count.
-// The classification is exact: a closed cell that no segment bbox meets lies in one connected
-// component of the plane minus the polygon boundary, and every segment straddling a point's y in
-// such a cell is at least a cell away, where the JTS orientation filter is already exact.
+// Index (built once on the host from the polygon CSR and uploaded -- the analogue of broadcasting
+// the polygon side of the join):
+//   * a uniform grid over the polygon set's envelope.  Every (cell, polygon) pair whose envelopes
+//     meet is INTERIOR (no segment of the polygon meets the inflated cell and the cell is inside:
+//     every point of the cell is contained, no arithmetic at all), EXTERIOR (dropped) or BOUNDARY;
+//   * a BOUNDARY pair carries one record per ring of the polygon: the ring segments that meet the
+//     inflated cell (tested exactly with RayCrossingCounter.countSegment), plus the crossing parity
+//     of all segments to the RIGHT of the cell as a function of the point's y.  Within the cell's
+//     y-band a segment that misses the inflated cell lies wholly left (never counted) or wholly
+//     right (counted iff it straddles y: ymin <= y < ymax, the half-open rule of countSegment), so
+//     that parity is piecewise constant with breakpoints at segment end-point y values; it is
+//     precomputed per interval (<= 63 breakpoints, else the record falls back to the slab walk).
+//     Geometric and JTS answers agree there: those segments are at least one cell away from the
+//     point, where the orientation filter is exact.
+//   * per ring y-slab buckets of all segments: the fallback walk (every segment whose y-range holds
+//     the point's y -- the only ones countSegment can count).
+// A point costs one cell lookup plus, in a boundary cell, ~2 exact segment tests.
 #include <math.h>
 #include <string.h>
 
@@ -40,16 +47,35 @@ struct Edge {
 };
 
 struct PipDev {
-  const double* poly_env;       // 4 per polygon (minx, miny, maxx, maxy)
-  const int32_t* poly_part_off;
-  const int32_t* part_ring_off;
-  const RingDev* rings;
+  const RingDev* rings;          // fallback slab walk
   const int32_t* slab_off;
-  const Edge* edges;
-  const int32_t* cell_off;
-  const int32_t* cell_ent;      // poly | kind << 30 (kind 1 = interior, 2 = boundary)
+  const Edge* slab_edges;
+  const uint32_t* coarse_word;   // per coarse cell (CF x CF fine cells): EMPTY, INTERIOR or LIST = "look at the fine word"
+  const uint32_t* cell_word;     // per cell: kind << 30 | payload (see CELL_*)
+  const int32_t* list_off;       // multi-entry cells: entries list_ent[list_off[i] .. list_off[i+1])
+  const uint32_t* list_ent;      // entries in cell-word form (kind INTERIOR or BOUNDARY)
+  const double* blob;            // boundary blobs, 16-byte aligned
   double gx0, gy0, gx1, gy1, inv_cw, inv_ch;
-  int32_t gx, gy;
+  int32_t gx, gy, gxc;
+};
+
+constexpr int CF_LOG = 2;   // coarse cell = 4 x 4 fine cells: the coarse table stays L2-resident
+
+// cell word kinds
+enum : uint32_t { CELL_INTERIOR = 0, CELL_BOUNDARY = 1, CELL_LIST = 2, CELL_EMPTY = 3 };
+
+// Boundary blob (one per BOUNDARY (cell, polygon) pair; 8-byte words, 16-byte aligned):
+//   w0: int32 polygon | int32 n_rings
+//   per ring, in CSR order:
+//     w: int16 n_edge | int16 n_brk | int16 flags (1 = first ring of a part, 2 = slow walk) | pad
+//     w: parity bits (slow walk: int32 ring id)
+//     n_edge x 4 words: segments meeting the inflated cell (p1 = ring[i], p2 = ring[i-1])
+//     n_brk words: breakpoint y values (ascending)
+// The polygon / ring envelope tests of Geometry.contains and PointLocator are not stored: for a point
+// outside a ring's envelope the crossing count is even and no segment holds the point, so the ring
+// walk returns EXTERIOR exactly as the early exit does.
+struct RingHdr {
+  int16_t n_edge, n_brk, flags, pad;
 };
 
 __device__ __forceinline__ int cell_of(double v, double v0, double inv, int g) {
@@ -59,131 +85,217 @@ __device__ __forceinline__ int cell_of(double v, double v0, double inv, int g) {
   return (int)c;
 }
 
-// RayCrossingCounter.locatePointInRing over the point's slab (PointLocator.locateInPolygonRing
-// first rejects points outside the ring envelope)
-__device__ int locate_ring(const PipDev& d, int r, double px, double py) {
+// RayCrossingCounter.countSegment (JTS 1.20); returns true when the point is on the segment
+__device__ __forceinline__ bool count_segment(double p1x, double p1y, double p2x, double p2y, double px, double py,
+                                              int& crossings) {
+  if (p1x < px && p2x < px) return false;
+  if (px == p2x && py == p2y) return true;
+  if (p1y == py && p2y == py) {
+    double mn = p1x, mx = p2x;
+    if (mn > mx) { mn = p2x; mx = p1x; }
+    return px >= mn && px <= mx;
+  }
+  if (((p1y > py) && (p2y <= py)) || ((p2y > py) && (p1y <= py))) {
+    int orient = jts_orientation(p1x, p1y, p2x, p2y, px, py);
+    if (orient == 0) return true;
+    if (p2y < p1y) orient = -orient;
+    if (orient == 1) crossings++;
+  }
+  return false;
+}
+
+// fallback: RayCrossingCounter.locatePointInRing over the point's y-slab
+__device__ __noinline__ int locate_ring_slab(const PipDev& d, int r, double px, double py) {
   const RingDev rd = d.rings[r];
   if (!(px >= rd.minx && px <= rd.maxx && py >= rd.miny && py <= rd.maxy)) return LOC_EXTERIOR;
   const int s = cell_of(py, rd.y0, rd.inv_h, rd.ns);
   const int e0 = d.slab_off[rd.slab_base + s], e1 = d.slab_off[rd.slab_base + s + 1];
   int crossings = 0;
   for (int e = e0; e < e1; ++e) {
-    const Edge g = d.edges[e];
-    if (g.p1x < px && g.p2x < px) continue;
-    if (px == g.p2x && py == g.p2y) return LOC_BOUNDARY;
-    if (g.p1y == py && g.p2y == py) {
-      double mn = g.p1x, mx = g.p2x;
-      if (mn > mx) { mn = g.p2x; mx = g.p1x; }
-      if (px >= mn && px <= mx) return LOC_BOUNDARY;
-      continue;
-    }
-    if (((g.p1y > py) && (g.p2y <= py)) || ((g.p2y > py) && (g.p1y <= py))) {
-      int orient = jts_orientation(g.p1x, g.p1y, g.p2x, g.p2y, px, py);
-      if (orient == 0) return LOC_BOUNDARY;
-      if (g.p2y < g.p1y) orient = -orient;
-      if (orient == 1) crossings++;
-    }
+    const Edge g = d.slab_edges[e];
+    if (count_segment(g.p1x, g.p1y, g.p2x, g.p2y, px, py, crossings)) return LOC_BOUNDARY;
   }
   return (crossings & 1) ? LOC_INTERIOR : LOC_EXTERIOR;
 }
 
-// PointLocator.locate over the polygon's components (Mod-2 rule) with locateInPolygon per part
-__device__ int locate_poly(const PipDev& d, int poly, double px, double py) {
-  const int p0 = d.poly_part_off[poly], p1 = d.poly_part_off[poly + 1];
-  bool is_in = false;
-  int nb = 0;
-  for (int p = p0; p < p1; ++p) {
-    const int r0 = d.part_ring_off[p], r1 = d.part_ring_off[p + 1];
-    if (r1 <= r0) continue;
-    int loc = locate_ring(d, r0, px, py);
-    if (loc == LOC_INTERIOR) {
-      for (int r = r0 + 1; r < r1; ++r) {
-        const int hl = locate_ring(d, r, px, py);
-        if (hl == LOC_INTERIOR) { loc = LOC_EXTERIOR; break; }
-        if (hl == LOC_BOUNDARY) { loc = LOC_BOUNDARY; break; }
-      }
+// Geometry.contains(point) for a BOUNDARY pair from its blob: envelope covers, then PointLocator
+// over the polygon's parts (locateInPolygon: shell, then holes) with the Mod-2 rule across parts
+__device__ bool blob_contains(const PipDev& d, const double* b, int2 h, double px, double py) {
+  const double* w = b + 1;
+  bool is_in = false, skip = true, started = false;
+  int nb = 0, cur = LOC_EXTERIOR;
+  for (int r = 0; r < h.y; ++r) {
+    const RingHdr rh = *(const RingHdr*)w;
+    const uint64_t parity = *(const uint64_t*)(w + 1);
+    const double* eg = w + 2;
+    const double* bk = eg + 4 * rh.n_edge;
+    w = bk + rh.n_brk;
+    if (rh.flags & 1) {  // a new part: settle the previous one
+      if (started) { if (cur == LOC_INTERIOR) is_in = true; if (cur == LOC_BOUNDARY) nb++; }
+      started = true;
+      skip = false;
+    } else if (skip) {
+      continue;
     }
-    if (loc == LOC_INTERIOR) is_in = true;
-    if (loc == LOC_BOUNDARY) nb++;
+    int loc;
+    if (rh.flags & 2) {
+      loc = locate_ring_slab(d, (int)(uint32_t)parity, px, py);
+    } else {
+      int k = 0;
+      for (int j = 0; j < rh.n_brk; ++j) k += bk[j] <= py;
+      int crossings = (int)((parity >> k) & 1ull);
+      loc = -1;
+      for (int j = 0; j < rh.n_edge; ++j)
+        if (count_segment(eg[4 * j], eg[4 * j + 1], eg[4 * j + 2], eg[4 * j + 3], px, py, crossings)) {
+          loc = LOC_BOUNDARY;
+          break;
+        }
+      if (loc < 0) loc = (crossings & 1) ? LOC_INTERIOR : LOC_EXTERIOR;
+    }
+    if (rh.flags & 1) {          // shell
+      cur = loc;
+      skip = loc != LOC_INTERIOR;
+    } else {                     // hole of a part whose shell holds the point
+      if (loc == LOC_INTERIOR) { cur = LOC_EXTERIOR; skip = true; }
+      else if (loc == LOC_BOUNDARY) { cur = LOC_BOUNDARY; skip = true; }
+    }
   }
-  if (nb & 1) return LOC_BOUNDARY;
-  if (nb > 0 || is_in) return LOC_INTERIOR;
-  return LOC_EXTERIOR;
+  if (started) { if (cur == LOC_INTERIOR) is_in = true; if (cur == LOC_BOUNDARY) nb++; }
+  if (nb & 1) return false;      // BOUNDARY
+  return nb > 0 || is_in;        // INTERIOR
 }
 
-// Geometry.contains(point) for candidate entry e of the point's cell
-__device__ __forceinline__ bool entry_contains(const PipDev& d, int32_t e, double px, double py) {
-  const int poly = e & 0x3fffffff;
-  if ((e >> 30) == 1) return true;
-  const double* env = d.poly_env + 4 * (int64_t)poly;
-  if (!(px >= env[0] && px <= env[2] && py >= env[1] && py <= env[3])) return false;
-  return locate_poly(d, poly, px, py) == LOC_INTERIOR;
+__device__ __forceinline__ bool entry_contains(const PipDev& d, uint32_t e, double x, double y, int& poly) {
+  if ((e >> 30) == CELL_INTERIOR) { poly = (int)(e & 0x3fffffffu); return true; }
+  const double* b = d.blob + 2 * (uint64_t)(e & 0x3fffffffu);
+  const int2 h = *(const int2*)b;
+  poly = h.x;
+  return blob_contains(d, b, h, x, y);
 }
 
-constexpr int JTPB = 512;
-constexpr int JCAP = 8192;  // LDS pair staging per block (8 B each: 64 KiB -> 2 blocks per CU)
+constexpr int JTPB = 256;             // 4 waves
+constexpr int JILP = 4;               // points per lane per iteration, their loads issued together
+constexpr int WCAP = 1024;            // LDS pair staging per wave (8 KiB)
+constexpr int JTILE = JTPB * JILP;
 
-// one point per lane per tile; persistent grid-stride over tiles of JTPB points
+__device__ __forceinline__ int lanes_below(uint64_t m) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// Persistent grid-stride over tiles of JTILE points.  Each iteration runs in stages so the JILP
+// points of a lane overlap their memory latency: coordinates -> coarse words -> fine words ->
+// boundary blob header (+ a touch of the blob's second 64-B line) -> evaluation.  Matches are staged
+// per wave in LDS (ballot + mbcnt slots, no block barriers) and flushed with one global atomic per
+// ~1K pairs.  At most 2 matches per point are staged; more go straight to global.
 template <bool WRITE>
 __global__ __launch_bounds__(JTPB) void k_pip_join(const double* __restrict__ px, const double* __restrict__ py,
                                                    int64_t n, int64_t id_base, PipDev d, int64_t* __restrict__ pt_ids,
                                                    int32_t* __restrict__ poly_ids, int64_t cap,
                                                    unsigned long long* __restrict__ counter) {
-  __shared__ uint32_t s_pt[WRITE ? JCAP : 1];
-  __shared__ int32_t s_poly[WRITE ? JCAP : 1];
-  __shared__ int s_n;
-  __shared__ unsigned long long s_base;
-  __shared__ int s_cnt;
-  if (threadIdx.x == 0) { s_n = 0; s_cnt = 0; }
-  __syncthreads();
-  const int64_t ntiles = (n + JTPB - 1) / JTPB;
+  __shared__ uint32_t s_pt[WRITE ? JTPB / 64 * WCAP : 1];
+  __shared__ int32_t s_poly[WRITE ? JTPB / 64 * WCAP : 1];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint32_t* wpt = s_pt + (WRITE ? wv * WCAP : 0);
+  int32_t* wpl = s_poly + (WRITE ? wv * WCAP : 0);
+  int wn = 0;   // wave-uniform fill of this wave's staging buffer
   int my_count = 0;
+  uint32_t touch = 0;
+  const int64_t ntiles = (n + JTILE - 1) / JTILE;
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const int64_t i = tile * JTPB + threadIdx.x;
-    if (i < n) {
-      const double x = __builtin_nontemporal_load(&px[i]);
-      const double y = __builtin_nontemporal_load(&py[i]);
-      if (x >= d.gx0 && x <= d.gx1 && y >= d.gy0 && y <= d.gy1) {
-        const int cx = cell_of(x, d.gx0, d.inv_cw, d.gx), cy = cell_of(y, d.gy0, d.inv_ch, d.gy);
-        const int64_t c = (int64_t)cy * d.gx + cx;
-        const int k0 = d.cell_off[c], k1 = d.cell_off[c + 1];
-        for (int k = k0; k < k1; ++k) {
-          const int32_t e = d.cell_ent[k];
-          if (!entry_contains(d, e, x, y)) continue;
+    double x[JILP], y[JILP];
+    int64_t i[JILP];
+    uint32_t cw[JILP];
+    int2 hd[JILP];
+#pragma unroll
+    for (int u = 0; u < JILP; ++u) {
+      i[u] = tile * JTILE + u * JTPB + threadIdx.x;
+      x[u] = y[u] = NAN;
+      if (i[u] < n) { x[u] = __builtin_nontemporal_load(&px[i[u]]); y[u] = __builtin_nontemporal_load(&py[i[u]]); }
+    }
+    int cxs[JILP], cys[JILP];
+#pragma unroll
+    for (int u = 0; u < JILP; ++u) {
+      cw[u] = 0xffffffffu;
+      cxs[u] = cys[u] = 0;
+      if (x[u] >= d.gx0 && x[u] <= d.gx1 && y[u] >= d.gy0 && y[u] <= d.gy1) {
+        cxs[u] = cell_of(x[u], d.gx0, d.inv_cw, d.gx);
+        cys[u] = cell_of(y[u], d.gy0, d.inv_ch, d.gy);
+        cw[u] = d.coarse_word[(int64_t)(cys[u] >> CF_LOG) * d.gxc + (cxs[u] >> CF_LOG)];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < JILP; ++u)
+      if ((cw[u] >> 30) == CELL_LIST) cw[u] = d.cell_word[(int64_t)cys[u] * d.gx + cxs[u]];
+#pragma unroll
+    for (int u = 0; u < JILP; ++u) {
+      hd[u] = make_int2(0, 0);
+      if ((cw[u] >> 30) == CELL_BOUNDARY) {
+        const double* b = d.blob + 2 * (uint64_t)(cw[u] & 0x3fffffffu);
+        hd[u] = *(const int2*)b;
+        touch ^= *(const uint32_t*)(b + 8);   // bring the blob's second 64-B line in alongside
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < JILP; ++u) {
+      int cnt = 0, m0 = 0, m1 = 0;
+      const uint32_t kind = cw[u] >> 30;
+      if (kind == CELL_INTERIOR) {
+        m0 = (int)(cw[u] & 0x3fffffffu);
+        cnt = 1;
+        if (!WRITE) my_count++;
+      } else if (kind == CELL_BOUNDARY) {
+        const double* b = d.blob + 2 * (uint64_t)(cw[u] & 0x3fffffffu);
+        if (blob_contains(d, b, hd[u], x[u], y[u])) {
+          m0 = hd[u].x;
+          cnt = 1;
+          if (!WRITE) my_count++;
+        }
+      } else if (kind == CELL_LIST) {
+        const int li = (int)(cw[u] & 0x3fffffffu);
+        const int k1 = d.list_off[li + 1];
+        for (int k = d.list_off[li]; k < k1; ++k) {
+          int poly;
+          if (!entry_contains(d, d.list_ent[k], x[u], y[u], poly)) continue;
           if (!WRITE) { my_count++; continue; }
-          const int off = atomicAdd(&s_n, 1);
-          if (off < JCAP) {
-            s_pt[off] = (uint32_t)i;
-            s_poly[off] = e & 0x3fffffff;
-          } else {  // LDS full inside one tile (heavily overlapping polygons): direct write
+          if (cnt == 0) m0 = poly;
+          else if (cnt == 1) m1 = poly;
+          else {  // > 2 polygons contain one point: direct global append (rare)
             const unsigned long long slot = atomicAdd(counter, 1ull);
-            if ((int64_t)slot < cap) { pt_ids[slot] = id_base + i; poly_ids[slot] = e & 0x3fffffff; }
+            if ((int64_t)slot < cap) { pt_ids[slot] = id_base + i[u]; poly_ids[slot] = poly; }
           }
+          cnt++;
+        }
+      }
+      if (WRITE) {
+        const uint64_t b1 = __ballot(cnt >= 1), b2 = __ballot(cnt >= 2);
+        const int wtot = __popcll(b1) + __popcll(b2);
+        if (wtot) {
+          const int off = wn + lanes_below(b1) + lanes_below(b2);
+          if (cnt >= 1) { wpt[off] = (uint32_t)i[u]; wpl[off] = m0; }
+          if (cnt >= 2) { wpt[off + 1] = (uint32_t)i[u]; wpl[off + 1] = m1; }
+          wn += wtot;
         }
       }
     }
-    if (WRITE) {
-      __syncthreads();
-      const int cnt = s_n < JCAP ? s_n : JCAP;
-      if (cnt > JCAP / 2 || (tile + gridDim.x >= ntiles && cnt > 0)) {
-        if (threadIdx.x == 0) s_base = atomicAdd(counter, (unsigned long long)cnt);
-        __syncthreads();
-        for (int j = threadIdx.x; j < cnt; j += JTPB) {
-          const int64_t slot = (int64_t)s_base + j;
-          if (slot < cap) { pt_ids[slot] = id_base + (int64_t)s_pt[j]; poly_ids[slot] = s_poly[j]; }
-        }
-        __syncthreads();
-        if (threadIdx.x == 0) s_n = 0;
+    if (WRITE && (wn > WCAP - 2 * 64 * JILP || (tile + gridDim.x >= ntiles && wn > 0))) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      unsigned long long base = 0;
+      if (lane == 0) base = atomicAdd(counter, (unsigned long long)wn);
+      base = __shfl(base, 0, 64);
+      for (int j = lane; j < wn; j += 64) {
+        const int64_t slot = (int64_t)base + j;
+        if (slot < cap) { pt_ids[slot] = id_base + (int64_t)wpt[j]; poly_ids[slot] = wpl[j]; }
       }
-      __syncthreads();
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      wn = 0;
     }
   }
+  if (touch == 0x9e3779b9u && my_count == -1) counter[1] = touch;   // keeps the prefetch loads alive
   if (!WRITE) {
-    // wave reduce then one LDS add per wave, one global add per block
     for (int off = 32; off > 0; off >>= 1) my_count += __shfl_down(my_count, off, 64);
-    if ((threadIdx.x & 63) == 0 && my_count) atomicAdd(&s_cnt, my_count);
-    __syncthreads();
-    if (threadIdx.x == 0 && s_cnt) atomicAdd(counter, (unsigned long long)s_cnt);
+    if (lane == 0 && my_count) atomicAdd(counter, (unsigned long long)my_count);
   }
 }
 
@@ -312,7 +424,6 @@ static inline int cell_of(double v, double v0, double inv, int g) {
 }
 
 }  // namespace host
-
 }  // namespace gm
 
 struct gm_pip_index {
@@ -320,7 +431,7 @@ struct gm_pip_index {
   gm::PipDev dev{};
   std::vector<void*> allocs;
   int32_t n_polys = 0;
-  int64_t n_entries = 0, n_edges = 0, n_cells = 0;
+  int64_t n_entries = 0, n_boundary = 0, n_records = 0, n_slow = 0, n_cells = 0, blob_bytes = 0;
 };
 
 using namespace gm;
@@ -337,12 +448,22 @@ int upload(gm_pip_index* ix, const std::vector<T>& v, const T** out) {
   return GM_OK;
 }
 
+struct BandSeg {
+  int32_t seg;   // global vertex id of the segment end (segment = v[seg-1] -> v[seg])
+  double minx, maxx, ymin, ymax;
+  int32_t vmin, vmax;  // vertex ids holding ymin / ymax
+};
+
 }  // namespace
 
 extern "C" {
 
 int gm_pip_index_create(gm_ctx* ctx, const gm_polyset* ps, gm_pip_index** out) {
-  if (!ctx || !ps || !out || ps->n_polys < 0) return GM_E_INVALID;
+  return gm_pip_index_create_ex(ctx, ps, 0, out);
+}
+
+int gm_pip_index_create_ex(gm_ctx* ctx, const gm_polyset* ps, int cells_per_poly_in, gm_pip_index** out) {
+  if (!ctx || !ps || !out || ps->n_polys < 0 || cells_per_poly_in < 0) return GM_E_INVALID;
   *out = nullptr;
   const int P = ps->n_polys;
   if (P > 0 && (!ps->poly_part_off || !ps->part_ring_off || !ps->ring_vert_off)) return GM_E_INVALID;
@@ -350,20 +471,23 @@ int gm_pip_index_create(gm_ctx* ctx, const gm_polyset* ps, gm_pip_index** out) {
   const int n_rings = n_parts ? ps->part_ring_off[n_parts] : 0;
   const int n_verts = n_rings ? ps->ring_vert_off[n_rings] : 0;
   if (n_verts > 0 && (!ps->vx || !ps->vy)) return GM_E_INVALID;
+  const double* vx = ps->vx;
+  const double* vy = ps->vy;
 
-  // ---- rings: envelopes + y-slab segment buckets
+  // ---- rings: envelopes + y-slab segment buckets (fallback walk); segments by end vertex
   std::vector<RingDev> rings((size_t)n_rings);
   std::vector<int32_t> slab_off;
-  std::vector<Edge> edges;
+  std::vector<Edge> slab_edges, segs((size_t)std::max(n_verts, 1));  // segs: segment ending at vertex i
   for (int r = 0; r < n_rings; ++r) {
     const int v0 = ps->ring_vert_off[r], v1 = ps->ring_vert_off[r + 1];
     RingDev& rd = rings[r];
     rd.minx = rd.miny = INFINITY;
     rd.maxx = rd.maxy = -INFINITY;
     for (int v = v0; v < v1; ++v) {
-      rd.minx = std::min(rd.minx, ps->vx[v]); rd.maxx = std::max(rd.maxx, ps->vx[v]);
-      rd.miny = std::min(rd.miny, ps->vy[v]); rd.maxy = std::max(rd.maxy, ps->vy[v]);
+      rd.minx = std::min(rd.minx, vx[v]); rd.maxx = std::max(rd.maxx, vx[v]);
+      rd.miny = std::min(rd.miny, vy[v]); rd.maxy = std::max(rd.maxy, vy[v]);
     }
+    for (int i = v0 + 1; i < v1; ++i) segs[i] = Edge{vx[i], vy[i], vx[i - 1], vy[i - 1]};
     const int nseg = std::max(0, v1 - v0 - 1);
     int ns = std::max(1, std::min(4096, nseg / 2));
     const double hgt = rd.maxy - rd.miny;
@@ -373,26 +497,20 @@ int gm_pip_index_create(gm_ctx* ctx, const gm_polyset* ps, gm_pip_index** out) {
     rd.ns = ns;
     rd.slab_base = (int32_t)slab_off.size();
     std::vector<std::vector<int32_t>> buckets((size_t)ns);
-    for (int j = 0; j < nseg; ++j) {
-      const int i = v0 + 1 + j;
-      const double ya = ps->vy[i], yb = ps->vy[i - 1];
-      const int s0 = host::cell_of(std::min(ya, yb), rd.y0, rd.inv_h, ns);
-      const int s1 = host::cell_of(std::max(ya, yb), rd.y0, rd.inv_h, ns);
-      for (int k = s0; k <= s1; ++k) buckets[k].push_back(j);
+    for (int i = v0 + 1; i < v1; ++i) {
+      const int s0 = host::cell_of(std::min(vy[i], vy[i - 1]), rd.y0, rd.inv_h, ns);
+      const int s1 = host::cell_of(std::max(vy[i], vy[i - 1]), rd.y0, rd.inv_h, ns);
+      for (int k = s0; k <= s1; ++k) buckets[k].push_back(i);
     }
-    // slab-major copies of the segments: a slab's segments are contiguous (32 B each)
     for (int k = 0; k < ns; ++k) {
-      slab_off.push_back((int32_t)edges.size());
-      for (int32_t j : buckets[k]) {
-        const int i = v0 + 1 + j;
-        edges.push_back(Edge{ps->vx[i], ps->vy[i], ps->vx[i - 1], ps->vy[i - 1]});
-      }
+      slab_off.push_back((int32_t)slab_edges.size());
+      for (int32_t i : buckets[k]) slab_edges.push_back(segs[i]);
     }
   }
-  slab_off.push_back((int32_t)edges.size());
+  slab_off.push_back((int32_t)slab_edges.size());
 
   // ---- polygon envelopes (JTS: Polygon envelope = shell envelope; MultiPolygon = union)
-  std::vector<double> env((size_t)P * 4);
+  std::vector<double> env((size_t)std::max(P, 1) * 4);
   double G[4] = {INFINITY, INFINITY, -INFINITY, -INFINITY};
   for (int p = 0; p < P; ++p) {
     double e[4] = {INFINITY, INFINITY, -INFINITY, -INFINITY};
@@ -412,105 +530,211 @@ int gm_pip_index_create(gm_ctx* ctx, const gm_polyset* ps, gm_pip_index** out) {
   const bool any = G[0] <= G[2];
   if (!any) { G[0] = G[1] = 0.0; G[2] = G[3] = -1.0; }  // nothing can match
 
-  // ---- grid
+  // ---- grid: ~cells_per_poly cells per polygon over the set's envelope
   const double W = any ? G[2] - G[0] : 0.0, H = any ? G[3] - G[1] : 0.0;
-  int64_t target = std::min<int64_t>(std::max<int64_t>((int64_t)P * 1024, 64), (int64_t)1 << 24);
+  const int64_t cells_per_poly = cells_per_poly_in > 0 ? cells_per_poly_in : 2048;
+  int64_t target = std::min<int64_t>(std::max<int64_t>((int64_t)P * cells_per_poly, 64), (int64_t)1 << 24);
   int gx = 1, gy = 1;
-  if (W > 0 && H > 0) {
+  const bool degenerate = !(W > 0 && H > 0);
+  if (!degenerate) {
     gx = (int)std::max<double>(1.0, std::floor(std::sqrt((double)target * W / H)));
     gy = (int)std::max<int64_t>(1, target / gx);
-  } else if (W > 0) {
-    gx = (int)std::min<int64_t>(target, 1 << 20);
-  } else if (H > 0) {
-    gy = (int)std::min<int64_t>(target, 1 << 20);
   }
-  const double inv_cw = W > 0 ? (double)gx / W : 0.0, inv_ch = H > 0 ? (double)gy / H : 0.0;
+  const double inv_cw = degenerate ? 0.0 : (double)gx / W, inv_ch = degenerate ? 0.0 : (double)gy / H;
   const double epsx = W > 0 ? W * 1e-9 : 1e-9, epsy = H > 0 ? H * 1e-9 : 1e-9;
   const int64_t ncell = (int64_t)gx * gy;
 
-  // ---- (cell, polygon) classification
-  std::vector<int32_t> counts((size_t)ncell + 1, 0);
-  struct Ent { int64_t cell; int32_t e; };
+  // ---- (cell, polygon) classification + boundary blobs
+  struct Ent { int64_t cell; uint32_t e; };
   std::vector<Ent> ents;
+  std::vector<int32_t> per_cell((size_t)ncell, 0);
+  std::vector<double> blob;            // 8-byte words; each blob starts 16-byte aligned
+  auto put_i32x2 = [&](int32_t a, int32_t b) {
+    double w; int32_t v[2] = {a, b}; memcpy(&w, v, 8); blob.push_back(w);
+  };
+  auto put_u64 = [&](uint64_t u) { double w; memcpy(&w, &u, 8); blob.push_back(w); };
+  int64_t n_slow = 0, n_boundary = 0, n_records = 0;
+  struct RingRef { int32_t ring; bool shell; };
+  std::vector<RingRef> ring_list;
+  std::vector<std::vector<BandSeg>> band;  // per ring of the polygon, segments meeting the row band
+  std::vector<int32_t> a_edges;
+  std::vector<const BandSeg*> right;
+  std::vector<std::pair<double, int32_t>> bk;
   for (int p = 0; p < P && any; ++p) {
     const double* e = &env[4 * (size_t)p];
     if (!(e[0] <= e[2])) continue;
-    const int cx0 = host::cell_of(e[0], G[0], inv_cw, gx), cx1 = host::cell_of(e[2], G[0], inv_cw, gx);
-    const int cy0 = host::cell_of(e[1], G[1], inv_ch, gy), cy1 = host::cell_of(e[3], G[1], inv_ch, gy);
-    const int bw = cx1 - cx0 + 1, bh = cy1 - cy0 + 1;
-    std::vector<uint8_t> bnd((size_t)bw * bh, 0);
+    ring_list.clear();
     for (int q = ps->poly_part_off[p]; q < ps->poly_part_off[p + 1]; ++q)
       for (int r = ps->part_ring_off[q]; r < ps->part_ring_off[q + 1]; ++r)
-        for (int v = ps->ring_vert_off[r] + 1; v < ps->ring_vert_off[r + 1]; ++v) {
-          const double ax = ps->vx[v - 1], ay = ps->vy[v - 1], bx = ps->vx[v], by = ps->vy[v];
-          int a0 = host::cell_of(std::min(ax, bx) - epsx, G[0], inv_cw, gx) - cx0;
-          int a1 = host::cell_of(std::max(ax, bx) + epsx, G[0], inv_cw, gx) - cx0;
-          int b0 = host::cell_of(std::min(ay, by) - epsy, G[1], inv_ch, gy) - cy0;
-          int b1 = host::cell_of(std::max(ay, by) + epsy, G[1], inv_ch, gy) - cy0;
-          a0 = std::max(a0, 0); b0 = std::max(b0, 0); a1 = std::min(a1, bw - 1); b1 = std::min(b1, bh - 1);
-          for (int yy = b0; yy <= b1; ++yy)
-            for (int xx = a0; xx <= a1; ++xx) bnd[(size_t)yy * bw + xx] = 1;
+        ring_list.push_back(RingRef{r, r == ps->part_ring_off[q]});
+    const int nr = (int)ring_list.size();
+    band.assign((size_t)nr, {});
+    const int cx0 = host::cell_of(e[0], G[0], inv_cw, gx), cx1 = host::cell_of(e[2], G[0], inv_cw, gx);
+    const int cy0 = host::cell_of(e[1], G[1], inv_ch, gy), cy1 = host::cell_of(e[3], G[1], inv_ch, gy);
+    for (int cy = cy0; cy <= cy1; ++cy) {
+      const double yb0 = degenerate ? -INFINITY : G[1] + (double)cy / inv_ch - epsy;
+      const double yb1 = degenerate ? INFINITY : G[1] + (double)(cy + 1) / inv_ch + epsy;
+      for (int k = 0; k < nr; ++k) {
+        band[k].clear();
+        const int r = ring_list[k].ring;
+        for (int i = ps->ring_vert_off[r] + 1; i < ps->ring_vert_off[r + 1]; ++i) {
+          const double ya = vy[i - 1], yb = vy[i];
+          const double ymin = std::min(ya, yb), ymax = std::max(ya, yb);
+          if (ymax < yb0 || ymin > yb1) continue;
+          band[k].push_back(BandSeg{i, std::min(vx[i - 1], vx[i]), std::max(vx[i - 1], vx[i]), ymin, ymax,
+                                    ya <= yb ? i - 1 : i, ya <= yb ? i : i - 1});
         }
-    for (int yy = 0; yy < bh; ++yy) {
+      }
       int run_loc = -1;
-      for (int xx = 0; xx < bw; ++xx) {
-        const int64_t cell = (int64_t)(cy0 + yy) * gx + (cx0 + xx);
-        int kind;
-        if (bnd[(size_t)yy * bw + xx]) {
-          kind = 2;
-          run_loc = -1;
-        } else {
+      for (int cx = cx0; cx <= cx1; ++cx) {
+        const int64_t cell = (int64_t)cy * gx + cx;
+        const double xb0 = degenerate ? -INFINITY : G[0] + (double)cx / inv_cw - epsx;
+        const double xb1 = degenerate ? INFINITY : G[0] + (double)(cx + 1) / inv_cw + epsx;
+        bool bnd = degenerate;
+        for (int k = 0; k < nr && !bnd; ++k)
+          for (const BandSeg& sg : band[k])
+            if (sg.maxx >= xb0 && sg.minx <= xb1) { bnd = true; break; }
+        if (!bnd) {
           if (run_loc < 0) {
             // any point of the cell: its nominal centre, checked to map back to the cell
-            const double cxm = G[0] + ((double)(cx0 + xx) + 0.5) / inv_cw;
-            const double cym = G[1] + ((double)(cy0 + yy) + 0.5) / inv_ch;
-            if ((inv_cw > 0 && host::cell_of(cxm, G[0], inv_cw, gx) != cx0 + xx) ||
-                (inv_ch > 0 && host::cell_of(cym, G[1], inv_ch, gy) != cy0 + yy) || inv_cw == 0 || inv_ch == 0) {
-              kind = 2;
-              ents.push_back(Ent{cell, (int32_t)(p | (kind << 30))});
-              counts[cell + 1]++;
+            const double cxm = G[0] + ((double)cx + 0.5) / inv_cw;
+            const double cym = G[1] + ((double)cy + 0.5) / inv_ch;
+            if (host::cell_of(cxm, G[0], inv_cw, gx) != cx || host::cell_of(cym, G[1], inv_ch, gy) != cy) bnd = true;
+            else run_loc = host::locate_poly(ps, p, cxm, cym);
+          }
+          if (!bnd) {
+            if (run_loc == LOC_EXTERIOR) continue;
+            if (run_loc == LOC_INTERIOR) {
+              ents.push_back(Ent{cell, (CELL_INTERIOR << 30) | (uint32_t)p});
+              per_cell[cell]++;
               continue;
             }
-            run_loc = host::locate_poly(ps, p, cxm, cym);
+            bnd = true;  // a boundary location cannot occur in a segment-free cell; stay exact anyway
           }
-          if (run_loc == LOC_EXTERIOR) continue;
-          kind = run_loc == LOC_INTERIOR ? 1 : 2;
         }
-        ents.push_back(Ent{cell, (int32_t)(p | (kind << 30))});
-        counts[cell + 1]++;
+        run_loc = -1;
+        // ---- boundary blob
+        if (blob.size() & 1) blob.push_back(0.0);
+        const uint64_t boff = blob.size() / 2;
+        if (boff >= (1u << 30)) { gm::set_error("gm_pip_index_create: boundary blob too large"); return GM_E_CAPACITY; }
+        put_i32x2(p, nr);
+        for (int k = 0; k < nr; ++k) {
+          a_edges.clear(); right.clear(); bk.clear();
+          for (const BandSeg& sg : band[k]) {
+            if (sg.maxx >= xb0 && sg.minx <= xb1) a_edges.push_back(sg.seg);
+            else if (sg.minx > xb1) right.push_back(&sg);
+          }
+          // breakpoints: right-segment end-point y values inside (yb0, yb1], ascending, unique
+          for (const BandSeg* sg : right) {
+            if (sg->ymin > yb0 && sg->ymin <= yb1) bk.push_back({sg->ymin, sg->vmin});
+            if (sg->ymax > yb0 && sg->ymax <= yb1) bk.push_back({sg->ymax, sg->vmax});
+          }
+          std::sort(bk.begin(), bk.end(),
+                    [](const std::pair<double, int32_t>& x, const std::pair<double, int32_t>& y) { return x.first < y.first; });
+          bk.erase(std::unique(bk.begin(), bk.end(),
+                               [](const std::pair<double, int32_t>& x, const std::pair<double, int32_t>& y) {
+                                 return x.first == y.first;
+                               }),
+                   bk.end());
+          const int r = ring_list[k].ring;
+          const bool slow = degenerate || a_edges.size() > 4096 || bk.size() > 63;
+          RingHdr rh{};
+          rh.flags = (int16_t)((ring_list[k].shell ? 1 : 0) | (slow ? 2 : 0));
+          rh.n_edge = slow ? 0 : (int16_t)a_edges.size();
+          rh.n_brk = slow ? 0 : (int16_t)bk.size();
+          { double w; memcpy(&w, &rh, 8); blob.push_back(w); }
+          uint64_t parity = 0;
+          if (!slow) {
+            // parity of right segments straddling y (ymin <= y < ymax) at each interval's left end
+            for (size_t j = 0; j <= bk.size(); ++j) {
+              const double yk = j == 0 ? yb0 : bk[j - 1].first;
+              int c = 0;
+              for (const BandSeg* sg : right) c += (sg->ymin <= yk && yk < sg->ymax);
+              if (c & 1) parity |= 1ull << j;
+            }
+          } else {
+            n_slow++;
+            parity = (uint32_t)r;
+          }
+          put_u64(parity);
+          if (!slow) {
+            for (int32_t i : a_edges) {
+              blob.push_back(vx[i]); blob.push_back(vy[i]); blob.push_back(vx[i - 1]); blob.push_back(vy[i - 1]);
+            }
+            for (auto& b : bk) blob.push_back(b.first);
+          }
+          n_records++;
+        }
+        n_boundary++;
+        ents.push_back(Ent{cell, (CELL_BOUNDARY << 30) | (uint32_t)boff});
+        per_cell[cell]++;
       }
     }
   }
-  for (int64_t c = 0; c < ncell; ++c) counts[c + 1] += counts[c];
-  std::vector<int32_t> cell_ent(ents.size());
+  if (blob.empty()) blob.push_back(0.0);
+  // ---- cell words: single entries inline, multi-entry cells through a list (polygons ascending)
+  std::vector<uint32_t> cell_word((size_t)ncell, 0xffffffffu);
+  std::vector<int32_t> list_off(1, 0);
+  std::vector<uint32_t> list_ent;
   {
-    std::vector<int32_t> fill(counts.begin(), counts.end() - 1);
-    for (const Ent& e : ents) cell_ent[fill[e.cell]++] = e.e;  // polys visited in ascending order
+    std::vector<int32_t> start((size_t)ncell + 1, 0);
+    for (int64_t c = 0; c < ncell; ++c) start[c + 1] = start[c] + per_cell[c];
+    std::vector<uint32_t> all(ents.size());
+    std::vector<int32_t> fill(start.begin(), start.end() - 1);
+    for (const Ent& en : ents) all[fill[en.cell]++] = en.e;
+    for (int64_t c = 0; c < ncell; ++c) {
+      const int k = per_cell[c];
+      if (k == 1) cell_word[c] = all[start[c]];
+      else if (k > 1) {
+        cell_word[c] = (CELL_LIST << 30) | (uint32_t)(list_off.size() - 1);
+        for (int j = 0; j < k; ++j) list_ent.push_back(all[start[c] + j]);
+        list_off.push_back((int32_t)list_ent.size());
+      }
+    }
   }
+  if (list_ent.empty()) list_ent.push_back(0);
+  // coarse words: EMPTY when every fine cell is empty, the fine word when all fine cells carry the
+  // same INTERIOR word, otherwise CELL_LIST ("read the fine word")
+  const int gxc = (gx + (1 << CF_LOG) - 1) >> CF_LOG, gyc = (gy + (1 << CF_LOG) - 1) >> CF_LOG;
+  std::vector<uint32_t> coarse_word((size_t)gxc * gyc, 0xffffffffu);
+  for (int yc = 0; yc < gyc; ++yc)
+    for (int xc = 0; xc < gxc; ++xc) {
+      uint32_t w = 0xffffffffu;
+      bool first = true, mixed = false;
+      for (int yy = yc << CF_LOG; yy < std::min(gy, (yc + 1) << CF_LOG) && !mixed; ++yy)
+        for (int xx = xc << CF_LOG; xx < std::min(gx, (xc + 1) << CF_LOG); ++xx) {
+          const uint32_t f = cell_word[(size_t)yy * gx + xx];
+          if (first) { w = f; first = false; }
+          else if (f != w) { mixed = true; break; }
+        }
+      const uint32_t kind = w >> 30;
+      coarse_word[(size_t)yc * gxc + xc] =
+          (!mixed && (kind == CELL_EMPTY || kind == CELL_INTERIOR)) ? w : (CELL_LIST << 30);
+    }
 
   gm_pip_index* ix = new gm_pip_index();
   ix->ctx = ctx;
   ix->n_polys = P;
-  ix->n_entries = (int64_t)cell_ent.size();
-  ix->n_edges = (int64_t)edges.size();
+  ix->n_entries = (int64_t)ents.size();
+  ix->n_boundary = n_boundary;
+  ix->n_records = n_records;
+  ix->n_slow = n_slow;
   ix->n_cells = ncell;
-  std::vector<int32_t> ppo(ps->poly_part_off, ps->poly_part_off + P + 1);
-  std::vector<int32_t> pro(ps->part_ring_off, ps->part_ring_off + n_parts + 1);
-  if (P == 0) { ppo.assign(1, 0); pro.assign(1, 0); }
+  ix->blob_bytes = (int64_t)blob.size() * 8;
   int rc = GM_OK;
   GM_HIP(hipSetDevice(ctx->device));
-  if (!rc) rc = upload(ix, env, &ix->dev.poly_env);
-  if (!rc) rc = upload(ix, ppo, &ix->dev.poly_part_off);
-  if (!rc) rc = upload(ix, pro, &ix->dev.part_ring_off);
   if (!rc) rc = upload(ix, rings, &ix->dev.rings);
   if (!rc) rc = upload(ix, slab_off, &ix->dev.slab_off);
-  if (!rc) rc = upload(ix, edges, &ix->dev.edges);
-  if (!rc) rc = upload(ix, counts, &ix->dev.cell_off);
-  if (!rc) rc = upload(ix, cell_ent, &ix->dev.cell_ent);
+  if (!rc) rc = upload(ix, slab_edges, &ix->dev.slab_edges);
+  if (!rc) rc = upload(ix, cell_word, &ix->dev.cell_word);
+  if (!rc) rc = upload(ix, coarse_word, &ix->dev.coarse_word);
+  if (!rc) rc = upload(ix, list_off, &ix->dev.list_off);
+  if (!rc) rc = upload(ix, list_ent, &ix->dev.list_ent);
+  if (!rc) rc = upload(ix, blob, &ix->dev.blob);
   if (rc) { gm_pip_index_destroy(ix); return rc; }
   ix->dev.gx0 = G[0]; ix->dev.gy0 = G[1]; ix->dev.gx1 = G[2]; ix->dev.gy1 = G[3];
   ix->dev.inv_cw = inv_cw; ix->dev.inv_ch = inv_ch;
-  ix->dev.gx = gx; ix->dev.gy = gy;
+  ix->dev.gx = gx; ix->dev.gy = gy; ix->dev.gxc = gxc;
   *out = ix;
   return GM_OK;
 }
@@ -519,6 +743,17 @@ int gm_pip_index_destroy(gm_pip_index* ix) {
   if (!ix) return GM_OK;
   for (void* p : ix->allocs) (void)hipFree(p);
   delete ix;
+  return GM_OK;
+}
+
+int gm_pip_index_stats(const gm_pip_index* ix, int64_t* stats) {
+  if (!ix || !stats) return GM_E_INVALID;
+  stats[0] = ix->n_cells;
+  stats[1] = ix->n_entries;
+  stats[2] = ix->n_boundary;
+  stats[3] = ix->n_records;
+  stats[4] = ix->n_slow;
+  stats[5] = ix->blob_bytes;
   return GM_OK;
 }
 

@@ -95,13 +95,20 @@ def parse_wkt_polygon(wkt):
 class PolygonIndex:
     """Device-side join index for a PolygonSet (gm_pip_index_create)."""
 
-    def __init__(self, polyset, ctx=None):
+    def __init__(self, polyset, ctx=None, cells_per_poly=0):
         self.polyset = polyset
         self.ctx = ctx or _lib.context()
         self._cs = polyset.c_struct()
         self._h = ctypes.c_void_p()
-        check(self.ctx.lib.gm_pip_index_create(self.ctx.handle, ctypes.byref(self._cs), ctypes.byref(self._h)),
-              "gm_pip_index_create")
+        check(self.ctx.lib.gm_pip_index_create_ex(self.ctx.handle, ctypes.byref(self._cs), int(cells_per_poly),
+                                                  ctypes.byref(self._h)), "gm_pip_index_create_ex")
+
+    def stats(self):
+        """(cells, (cell, polygon) entries, boundary entries, ring records, slow-walk records)."""
+        import numpy as np
+        st = np.zeros(6, np.int64)
+        check(self.ctx.lib.gm_pip_index_stats(self._h, st.ctypes.data), "gm_pip_index_stats")
+        return dict(zip(["cells", "entries", "boundary", "records", "slow", "blob_bytes"], st.tolist()))
 
     def join(self, px, py, id_base=0, cap=None, count_only=False):
         """Returns (pt_ids, poly_ids) device tensors (or the pair count when count_only)."""

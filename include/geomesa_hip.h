@@ -194,7 +194,13 @@ typedef struct gm_pip_index gm_pip_index;
    envelopes -- the analogue of RelationUtils.grid, geomesa-spark-sql/.../RelationUtils.scala:30-157 --
    plus per-ring y-slab edge buckets). */
 int gm_pip_index_create(gm_ctx* ctx, const gm_polyset* polys, gm_pip_index** out);
+/* same with an explicit grid density: ~cells_per_poly grid cells per polygon over the set's
+   envelope (0 = default 1024; a coarse 4x4-cell table in front of it stays L2-resident) */
+int gm_pip_index_create_ex(gm_ctx* ctx, const gm_polyset* polys, int cells_per_poly, gm_pip_index** out);
 int gm_pip_index_destroy(gm_pip_index* index);
+/* index statistics: stats[0..5] = cells, (cell, polygon) entries, boundary entries, ring records,
+   ring records that fall back to the slab walk, boundary blob bytes */
+int gm_pip_index_stats(const gm_pip_index* index, int64_t* stats);
 
 /* ST_Contains(polygon, point) = JTS Geometry.contains (geomesa-spark-jts/.../udf/
    SpatialRelationFunctions.scala:29), evaluated for every (point, polygon) pair -- the result of

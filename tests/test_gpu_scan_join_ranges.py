@@ -123,8 +123,9 @@ def test_st_contains_holes_multipolygon_gpu(gpu, oracle):
     assert (k(5, 5), 1) in got  # shared component edge: Mod-2 -> interior
 
 
-@pytest.mark.parametrize("grid", [(20, 10), (80, 40)])
-def test_pip_join_synthetic_counties(gpu, oracle, grid):
+@pytest.mark.parametrize("grid,cells_per_poly", [((20, 10), 0), ((80, 40), 0), ((20, 10), 1), ((20, 10), 16),
+                                                 ((20, 10), 4096)])
+def test_pip_join_synthetic_counties(gpu, oracle, grid, cells_per_poly):
     from geomesa_amd.join import PolygonIndex, synthetic_counties, synthetic_points
     ps = synthetic_counties(*grid)
     px, py = synthetic_points(400_000)
@@ -132,7 +133,9 @@ def test_pip_join_synthetic_counties(gpu, oracle, grid):
     vx, vy = ps.vx[::3], ps.vy[::3]
     px = np.concatenate([px, vx, (ps.vx[1:] + ps.vx[:-1]) / 2, np.full(1000, -95.5)])
     py = np.concatenate([py, vy, (ps.vy[1:] + ps.vy[:-1]) / 2, np.linspace(24, 50, 1000)])
-    ix = PolygonIndex(ps)
+    ix = PolygonIndex(ps, cells_per_poly=cells_per_poly)
+    if cells_per_poly == 1:
+        assert ix.stats()["slow"] > 0   # exercises the slab-walk fallback
     pt, pl = ix.join(px, py)
     import oracle as O
     opt, opl = O.OraclePolySet(*ps.to_arrays()).join(px, py, nthreads=8)
