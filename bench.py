@@ -21,6 +21,8 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+from geomesa_amd.shard import all_reduce_scalar, broadcast_polyset, shard_bounds  # noqa: E402
+
 METRIC = "points/sec Z3 encode + point-in-polygon join pairs/sec at 1/2/4/8 MI355X"
 SEED = 0x67656F6D65736121
 T2020, T2021 = 1577836800000, 1609459200000
@@ -41,6 +43,7 @@ def parse():
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=8.0)
     p.add_argument("--only", default="", help="comma list: z3,join,extra (profiling)")
+    p.add_argument("--join-mode", default="auto", choices=["auto", "direct", "partitioned"])
     p.add_argument("--cells-per-poly", type=int, default=0, help="join grid density (0 = library default)")
     return p.parse_args()
 
@@ -67,20 +70,10 @@ class Dist:
         torch.cuda.synchronize()
 
     def max(self, v):
-        import torch
-        if not self.pg:
-            return v
-        t = torch.tensor([v], dtype=torch.float64, device="cuda")
-        self.pg.all_reduce(t, op=self.pg.ReduceOp.MAX)
-        return float(t.item())
+        return all_reduce_scalar(self.pg, v, "max")
 
     def sum(self, v):
-        import torch
-        if not self.pg:
-            return v
-        t = torch.tensor([v], dtype=torch.float64, device="cuda")
-        self.pg.all_reduce(t, op=self.pg.ReduceOp.SUM)
-        return float(t.item())
+        return all_reduce_scalar(self.pg, v, "sum")
 
 
 def timed(dist, fn, steps, warmup):
@@ -203,7 +196,8 @@ def main():
     t = torch.empty(N, dtype=torch.int64, device=dev)
     b = torch.empty(N, dtype=torch.int16, device=dev)
     z = torch.empty(N, dtype=torch.int64, device=dev)
-    gen_points(ctx, N, dist.rank * N, (-180.0, -90.0, 180.0, 90.0), x, y, t)
+    lo, _ = shard_bounds(N * dist.world, dist.rank, dist.world)   # this rank's rows of the global set
+    gen_points(ctx, N, lo, (-180.0, -90.0, 180.0, 90.0), x, y, t)
     sfc = Z3SFC("week")
     lib, h = ctx.lib, ctx.handle
     P = _lib.ptr
@@ -293,39 +287,33 @@ def main():
         ps = synthetic_counties() if dist.rank == 0 else None
         if dist.world > 1:
             # polygon set broadcast over RCCL (the reference ships it with the Spark join shuffle)
-            arrs = ps.to_arrays() if ps else None
-            sizes = torch.tensor([len(v) for v in arrs] if arrs else [0] * 5, dtype=torch.int64, device=dev)
-            dist.pg.broadcast(sizes, 0)
-            tens = []
-            for k, (sz, dt_) in enumerate(zip(sizes.tolist(), [torch.int32] * 3 + [torch.float64] * 2)):
-                tt = torch.from_numpy(arrs[k]).to(dev) if arrs else torch.empty(sz, dtype=dt_, device=dev)
-                dist.pg.broadcast(tt, 0)
-                tens.append(tt.cpu().numpy())
-            ps = PolygonSet(*tens)
+            ps = broadcast_polyset(dist.pg, ps)
         t_ix = time.time()
         ix = PolygonIndex(ps, ctx, a.cells_per_poly)
         t_ix = time.time() - t_ix
         px = torch.empty(J, dtype=torch.float64, device=dev)
         py = torch.empty(J, dtype=torch.float64, device=dev)
-        gen_points(ctx, J, dist.rank * J + (1 << 40), CONUS, px, py, None)
-        cnt = ix.join(px, py, count_only=True)
+        jlo, _ = shard_bounds(J * dist.world, dist.rank, dist.world)
+        gen_points(ctx, J, jlo + (1 << 40), CONUS, px, py, None)
+        jmode = PolygonIndex.MODES[a.join_mode]
+        cnt = ix.join(px, py, count_only=True, mode=a.join_mode)
         cap = int(cnt * 1.05) + 1024
         ptids = torch.empty(cap, dtype=torch.int64, device=dev)
         plids = torch.empty(cap, dtype=torch.int32, device=dev)
         npairs = __import__("ctypes").c_int64()
 
         def join_step():
-            rc = lib.gm_pip_join(h, ix._h, P(px), P(py), J, dist.rank * J, P(ptids), P(plids), cap, None)
+            rc = lib.gm_pip_join_ex(h, ix._h, P(px), P(py), J, jlo, P(ptids), P(plids), cap, None, jmode)
             if rc:
                 _lib.check(rc, "gm_pip_join")
         jms = timed(dist, join_step, a.join_steps, 1)
-        _lib.check(lib.gm_pip_join(h, ix._h, P(px), P(py), J, dist.rank * J, P(ptids), P(plids), cap,
-                                   __import__("ctypes").byref(npairs)), "join")
+        _lib.check(lib.gm_pip_join_ex(h, ix._h, P(px), P(py), J, jlo, P(ptids), P(plids), cap,
+                                      __import__("ctypes").byref(npairs), jmode), "join")
         matches = int(dist.sum(npairs.value))
         pairs = J * ps.n_polys * dist.world
         pj = {"value": pairs / (jms * 1e-3), "unit": "pairs/s", "ms_per_step": jms, "points_per_gpu": J,
               "polygons": ps.n_polys, "vertices": ps.n_vertices, "matches": matches,
-              "matches_per_s": matches / (jms * 1e-3), "index_build_s": round(t_ix, 3), "index": ix.stats(),
+              "matches_per_s": matches / (jms * 1e-3), "index_build_s": round(t_ix, 3), "index": ix.stats(), "mode": a.join_mode,
               "roofline": roofline(16.0 * J + 12.0 * npairs.value, jms, load_pmc("pip_join", J)),
               "workload": "st_contains(polygon, point) join, %d CONUS points/GPU x %d synthetic county polygons "
                           "(BASELINE configs[3]); polygon set broadcast over RCCL when N > 1" % (J, ps.n_polys)}

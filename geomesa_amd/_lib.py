@@ -21,6 +21,10 @@ GM_ST_OUT_OF_BOUNDS = 1
 GM_ST_BAD_TIME = 2
 GM_ST_UNORDERED = 3
 
+GM_JOIN_AUTO = 0
+GM_JOIN_DIRECT = 1
+GM_JOIN_PARTITIONED = 2
+
 
 class GeomesaHipUnavailable(RuntimeError):
     """The HIP library or a GPU is not available (no silent fallback exists)."""
@@ -88,6 +92,7 @@ SIGNATURES = {
     "gm_pip_index_destroy": (cint, [vp]),
     "gm_pip_index_stats": (cint, [vp, vp]),
     "gm_pip_join": (cint, [vp, vp, vp, vp, i64, i64, vp, vp, i64, vp]),
+    "gm_pip_join_ex": (cint, [vp, vp, vp, vp, i64, i64, vp, vp, i64, vp, cint]),
     "gm_gen_points": (cint, [vp, ctypes.c_uint64, i64, i64, d, d, d, d, i64, i64, vp, vp, vp]),
 }
 

@@ -105,14 +105,17 @@ __device__ __forceinline__ bool count_segment(double p1x, double p1y, double p2x
 }
 
 // fallback: RayCrossingCounter.locatePointInRing over the point's y-slab
-__device__ __noinline__ int locate_ring_slab(const PipDev& d, int r, double px, double py) {
-  const RingDev rd = d.rings[r];
+// (takes the three arrays by value: a reference to the kernel's PipDev argument would force the
+// whole struct into scratch and put scratch loads in front of every index lookup)
+__device__ __noinline__ int locate_ring_slab(const RingDev* __restrict__ rings, const int32_t* __restrict__ slab_off,
+                                             const Edge* __restrict__ slab_edges, int r, double px, double py) {
+  const RingDev rd = rings[r];
   if (!(px >= rd.minx && px <= rd.maxx && py >= rd.miny && py <= rd.maxy)) return LOC_EXTERIOR;
   const int s = cell_of(py, rd.y0, rd.inv_h, rd.ns);
-  const int e0 = d.slab_off[rd.slab_base + s], e1 = d.slab_off[rd.slab_base + s + 1];
+  const int e0 = slab_off[rd.slab_base + s], e1 = slab_off[rd.slab_base + s + 1];
   int crossings = 0;
   for (int e = e0; e < e1; ++e) {
-    const Edge g = d.slab_edges[e];
+    const Edge g = slab_edges[e];
     if (count_segment(g.p1x, g.p1y, g.p2x, g.p2y, px, py, crossings)) return LOC_BOUNDARY;
   }
   return (crossings & 1) ? LOC_INTERIOR : LOC_EXTERIOR;
@@ -139,7 +142,7 @@ __device__ bool blob_contains(const PipDev& d, const double* b, int2 h, double p
     }
     int loc;
     if (rh.flags & 2) {
-      loc = locate_ring_slab(d, (int)(uint32_t)parity, px, py);
+      loc = locate_ring_slab(d.rings, d.slab_off, d.slab_edges, (int)(uint32_t)parity, px, py);
     } else {
       int k = 0;
       for (int j = 0; j < rh.n_brk; ++j) k += bk[j] <= py;
@@ -174,48 +177,107 @@ __device__ __forceinline__ bool entry_contains(const PipDev& d, uint32_t e, doub
 }
 
 constexpr int JTPB = 256;             // 4 waves
-constexpr int JILP = 4;               // points per lane per iteration, their loads issued together
-constexpr int WCAP = 1024;            // LDS pair staging per wave (8 KiB)
+constexpr int JILP = 2;               // points per lane per tile (their lookups overlap)
+constexpr int WCAP = 512;             // LDS pair staging per wave (4 KiB)
+constexpr int QCAP = 128;             // LDS blob work queue per wave (3 KiB)
 constexpr int JTILE = JTPB * JILP;
 
 __device__ __forceinline__ int lanes_below(uint64_t m) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
-// Persistent grid-stride over tiles of JTILE points.  Each iteration runs in stages so the JILP
-// points of a lane overlap their memory latency: coordinates -> coarse words -> fine words ->
-// boundary blob header (+ a touch of the blob's second 64-B line) -> evaluation.  Matches are staged
-// per wave in LDS (ballot + mbcnt slots, no block barriers) and flushed with one global atomic per
-// ~1K pairs.  At most 2 matches per point are staged; more go straight to global.
-template <bool WRITE>
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// one global atomic reserves the wave's staged pairs; lanes copy them out
+__device__ __forceinline__ void flush_pairs(const uint32_t* wpt, const int32_t* wpl, int wn, int lane, int64_t id_base,
+                                            int64_t* __restrict__ pt_ids, int32_t* __restrict__ poly_ids,
+                                            int64_t cap, unsigned long long* __restrict__ counter) {
+  wave_lds_sync();
+  unsigned long long base = 0;
+  if (lane == 0) base = atomicAdd(counter, (unsigned long long)wn);
+  base = __shfl(base, 0, 64);
+  for (int j = lane; j < wn; j += 64) {
+    const int64_t slot = (int64_t)base + j;
+    if (slot < cap) { pt_ids[slot] = id_base + (int64_t)wpt[j]; poly_ids[slot] = wpl[j]; }
+  }
+  wave_lds_sync();
+}
+
+// Row-band partitioned point record (24 B): the join's input after k_band_scatter.
+struct PtRec {
+  double x, y;
+  uint32_t idx;   // row within the chunk
+  uint32_t pad;
+};
+
+// Persistent grid-stride over tiles of JTILE points; every wave works independently.
+// A point's candidate work is a list of items: its cell word (INTERIOR -> match, BOUNDARY -> one
+// blob), or, for a LIST cell, one item per (cell, polygon) entry.  Items are walked one per lane per
+// step (wave-uniform loop): INTERIOR items emit their pair at once, blob items are compacted into a
+// per-wave LDS queue (ballot + mbcnt), and whenever 64 are queued the wave evaluates them with all
+// lanes busy (JTS RayCrossingCounter over the blob's segments).  This keeps the long boundary walk
+// off the lanes whose points sit in uniform cells.  Pairs are staged per wave in LDS and flushed
+// with one global atomic per few hundred pairs.
+template <bool WRITE, bool REC>
 __global__ __launch_bounds__(JTPB) void k_pip_join(const double* __restrict__ px, const double* __restrict__ py,
+                                                   const PtRec* __restrict__ rec, const uint32_t* __restrict__ n_rec,
                                                    int64_t n, int64_t id_base, PipDev d, int64_t* __restrict__ pt_ids,
                                                    int32_t* __restrict__ poly_ids, int64_t cap,
                                                    unsigned long long* __restrict__ counter) {
-  __shared__ uint32_t s_pt[WRITE ? JTPB / 64 * WCAP : 1];
-  __shared__ int32_t s_poly[WRITE ? JTPB / 64 * WCAP : 1];
+  constexpr int NW = JTPB / 64;
+  __shared__ uint32_t s_pt[WRITE ? NW * WCAP : 1];
+  __shared__ int32_t s_poly[WRITE ? NW * WCAP : 1];
+  __shared__ double s_qx[NW * QCAP], s_qy[NW * QCAP];
+  __shared__ uint32_t s_qid[NW * QCAP], s_qb[NW * QCAP];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   uint32_t* wpt = s_pt + (WRITE ? wv * WCAP : 0);
   int32_t* wpl = s_poly + (WRITE ? wv * WCAP : 0);
-  int wn = 0;   // wave-uniform fill of this wave's staging buffer
+  double* qx = s_qx + wv * QCAP;
+  double* qy = s_qy + wv * QCAP;
+  uint32_t* qid = s_qid + wv * QCAP;
+  uint32_t* qb = s_qb + wv * QCAP;
+  int wn = 0, qn = 0;   // wave-uniform fills of the pair staging and the blob queue
   int my_count = 0;
-  uint32_t touch = 0;
+  if (REC) n = *n_rec;
   const int64_t ntiles = (n + JTILE - 1) / JTILE;
-  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+  // REC: band-sorted input -> XCD-aware mapping (workgroups are dispatched round-robin over the 8
+  // XCDs): each XCD sweeps its own contiguous eighth of the records.
+  int64_t tile = blockIdx.x, t_end = ntiles, t_step = gridDim.x;
+  if (REC) {
+    const int nx = 8, xcd = blockIdx.x % nx;
+    tile = ntiles * xcd / nx + blockIdx.x / nx;
+    t_end = ntiles * (xcd + 1) / nx;
+    t_step = gridDim.x / nx;
+  }
+  for (;;) {
+    const bool have = tile < t_end;   // block-uniform
     double x[JILP], y[JILP];
-    int64_t i[JILP];
-    uint32_t cw[JILP];
-    int2 hd[JILP];
+    uint32_t id[JILP], cw[JILP];
+    int lo[JILP], ni[JILP];
 #pragma unroll
     for (int u = 0; u < JILP; ++u) {
-      i[u] = tile * JTILE + u * JTPB + threadIdx.x;
+      const int64_t i = tile * JTILE + u * JTPB + threadIdx.x;
       x[u] = y[u] = NAN;
-      if (i[u] < n) { x[u] = __builtin_nontemporal_load(&px[i[u]]); y[u] = __builtin_nontemporal_load(&py[i[u]]); }
+      id[u] = (uint32_t)i;
+      if (have && i < n) {
+        if (REC) {
+          const PtRec* r = rec + i;
+          x[u] = __builtin_nontemporal_load(&r->x);
+          y[u] = __builtin_nontemporal_load(&r->y);
+          id[u] = __builtin_nontemporal_load(&r->idx);
+        } else {
+          x[u] = __builtin_nontemporal_load(&px[i]);
+          y[u] = __builtin_nontemporal_load(&py[i]);
+        }
+      }
     }
     int cxs[JILP], cys[JILP];
 #pragma unroll
     for (int u = 0; u < JILP; ++u) {
-      cw[u] = 0xffffffffu;
+      cw[u] = CELL_EMPTY << 30;
       cxs[u] = cys[u] = 0;
       if (x[u] >= d.gx0 && x[u] <= d.gx1 && y[u] >= d.gy0 && y[u] <= d.gy1) {
         cxs[u] = cell_of(x[u], d.gx0, d.inv_cw, d.gx);
@@ -228,74 +290,197 @@ __global__ __launch_bounds__(JTPB) void k_pip_join(const double* __restrict__ px
       if ((cw[u] >> 30) == CELL_LIST) cw[u] = d.cell_word[(int64_t)cys[u] * d.gx + cxs[u]];
 #pragma unroll
     for (int u = 0; u < JILP; ++u) {
-      hd[u] = make_int2(0, 0);
-      if ((cw[u] >> 30) == CELL_BOUNDARY) {
-        const double* b = d.blob + 2 * (uint64_t)(cw[u] & 0x3fffffffu);
-        hd[u] = *(const int2*)b;
-        touch ^= *(const uint32_t*)(b + 8);   // bring the blob's second 64-B line in alongside
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < JILP; ++u) {
-      int cnt = 0, m0 = 0, m1 = 0;
       const uint32_t kind = cw[u] >> 30;
-      if (kind == CELL_INTERIOR) {
-        m0 = (int)(cw[u] & 0x3fffffffu);
-        cnt = 1;
-        if (!WRITE) my_count++;
-      } else if (kind == CELL_BOUNDARY) {
-        const double* b = d.blob + 2 * (uint64_t)(cw[u] & 0x3fffffffu);
-        if (blob_contains(d, b, hd[u], x[u], y[u])) {
-          m0 = hd[u].x;
-          cnt = 1;
-          if (!WRITE) my_count++;
-        }
-      } else if (kind == CELL_LIST) {
+      lo[u] = 0;
+      ni[u] = kind == CELL_EMPTY ? 0 : 1;
+      if (kind == CELL_LIST) {
         const int li = (int)(cw[u] & 0x3fffffffu);
-        const int k1 = d.list_off[li + 1];
-        for (int k = d.list_off[li]; k < k1; ++k) {
-          int poly;
-          if (!entry_contains(d, d.list_ent[k], x[u], y[u], poly)) continue;
-          if (!WRITE) { my_count++; continue; }
-          if (cnt == 0) m0 = poly;
-          else if (cnt == 1) m1 = poly;
-          else {  // > 2 polygons contain one point: direct global append (rare)
-            const unsigned long long slot = atomicAdd(counter, 1ull);
-            if ((int64_t)slot < cap) { pt_ids[slot] = id_base + i[u]; poly_ids[slot] = poly; }
-          }
-          cnt++;
-        }
-      }
-      if (WRITE) {
-        const uint64_t b1 = __ballot(cnt >= 1), b2 = __ballot(cnt >= 2);
-        const int wtot = __popcll(b1) + __popcll(b2);
-        if (wtot) {
-          const int off = wn + lanes_below(b1) + lanes_below(b2);
-          if (cnt >= 1) { wpt[off] = (uint32_t)i[u]; wpl[off] = m0; }
-          if (cnt >= 2) { wpt[off + 1] = (uint32_t)i[u]; wpl[off + 1] = m1; }
-          wn += wtot;
-        }
+        lo[u] = d.list_off[li];
+        ni[u] = d.list_off[li + 1] - lo[u];
       }
     }
-    if (WRITE && (wn > WCAP - 2 * 64 * JILP || (tile + gridDim.x >= ntiles && wn > 0))) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      unsigned long long base = 0;
-      if (lane == 0) base = atomicAdd(counter, (unsigned long long)wn);
-      base = __shfl(base, 0, 64);
-      for (int j = lane; j < wn; j += 64) {
-        const int64_t slot = (int64_t)base + j;
-        if (slot < cap) { pt_ids[slot] = id_base + (int64_t)wpt[j]; poly_ids[slot] = wpl[j]; }
+    // item walk; after the last tile the same loop drains the queue and ends
+    const int ntot = ni[0] + (JILP > 1 ? ni[JILP - 1] : 0);
+    for (int k = 0;; ++k) {
+      const bool act = k < ntot;
+      const bool any = __ballot(act) != 0;
+      if (!any && (have ? qn < 64 : qn == 0)) break;
+      if (any) {
+        const bool second = JILP > 1 && k >= ni[0];
+        const int kk = second ? k - ni[0] : k;
+        const uint32_t w = second ? cw[JILP - 1] : cw[0];
+        uint32_t e = w;
+        if (act && (w >> 30) == CELL_LIST) e = d.list_ent[(second ? lo[JILP - 1] : lo[0]) + kk];
+        const double ex = second ? x[JILP - 1] : x[0], ey = second ? y[JILP - 1] : y[0];
+        const uint32_t eid = second ? id[JILP - 1] : id[0];
+        const bool hit = act && (e >> 30) == CELL_INTERIOR;
+        const bool blob = act && (e >> 30) != CELL_INTERIOR;
+        if (!WRITE) my_count += hit;
+        if (WRITE) {
+          const uint64_t m = __ballot(hit);
+          if (hit) { const int o = wn + lanes_below(m); wpt[o] = eid; wpl[o] = (int32_t)(e & 0x3fffffffu); }
+          wn += __popcll(m);
+        }
+        const uint64_t mq = __ballot(blob);
+        if (blob) {
+          const int o = qn + lanes_below(mq);
+          qx[o] = ex; qy[o] = ey; qid[o] = eid; qb[o] = e & 0x3fffffffu;
+        }
+        qn += __popcll(mq);
       }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      wn = 0;
+      if (qn >= 64 || (!have && !any && qn > 0)) {   // evaluate the newest min(qn, 64) queued items
+        wave_lds_sync();
+        const int kq = qn < 64 ? qn : 64;
+        const int slot = qn - kq + lane;
+        bool hit = false;
+        int poly = 0;
+        uint32_t eid = 0;
+        if (lane < kq) {
+          const double* b = d.blob + 2 * (uint64_t)qb[slot];
+          const double ex = qx[slot], ey = qy[slot];
+          eid = qid[slot];
+          const int2 h = *(const int2*)b;
+          poly = h.x;
+          hit = blob_contains(d, b, h, ex, ey);
+        }
+        wave_lds_sync();
+        qn -= kq;
+        if (!WRITE) my_count += hit;
+        if (WRITE) {
+          const uint64_t m = __ballot(hit);
+          if (hit) { const int o = wn + lanes_below(m); wpt[o] = eid; wpl[o] = poly; }
+          wn += __popcll(m);
+        }
+      }
+      if (WRITE && wn > WCAP - 128) {
+        flush_pairs(wpt, wpl, wn, lane, id_base, pt_ids, poly_ids, cap, counter);
+        wn = 0;
+      }
     }
+    if (!have) break;
+    tile += t_step;
   }
-  if (touch == 0x9e3779b9u && my_count == -1) counter[1] = touch;   // keeps the prefetch loads alive
+  if (WRITE && wn > 0) flush_pairs(wpt, wpl, wn, lane, id_base, pt_ids, poly_ids, cap, counter);
   if (!WRITE) {
     for (int off = 32; off > 0; off >>= 1) my_count += __shfl_down(my_count, off, 64);
     if (lane == 0 && my_count) atomicAdd(counter, (unsigned long long)my_count);
+  }
+}
+
+// ------------------------------------------------------------------ row-band partition
+// Large joins first group the points by horizontal band of grid rows (a one-pass counting sort,
+// the device analogue of RelationUtils.grid's shuffle of both sides into grid cells,
+// geomesa-spark-sql/.../RelationUtils.scala:30-157).  A band's cell words and blobs then stay
+// L2-resident while the join sweeps its points.  Points whose y is outside the grid (or NaN) are
+// dropped here: no polygon can contain them.
+constexpr int NBAND = 256;          // max bands (band id fits LDS histograms of one wave-multiple)
+constexpr int PTPB = 256;           // partition block
+constexpr int PTILE = 2048;         // scatter tile: 8 points per thread, sorted by band in LDS
+
+__device__ __forceinline__ int band_of(double y, const PipDev& d, int rows_per_band, int nb) {
+  if (!(y >= d.gy0 && y <= d.gy1)) return nb;   // drop bin
+  return cell_of(y, d.gy0, d.inv_ch, d.gy) / rows_per_band;
+}
+
+// per-block band histogram, band-major: hist[band * gridDim.x + block]
+__global__ __launch_bounds__(PTPB) void k_band_hist(const double* __restrict__ py, int64_t n, int64_t per_block,
+                                                    PipDev d, int rows_per_band, int nb, uint32_t* __restrict__ hist) {
+  __shared__ uint32_t h[NBAND + 1];
+  for (int b = threadIdx.x; b <= nb; b += PTPB) h[b] = 0;
+  __syncthreads();
+  const int64_t b0 = (int64_t)blockIdx.x * per_block, b1 = min(n, b0 + per_block);
+  for (int64_t j = b0 + threadIdx.x; j < b1; j += PTPB)
+    atomicAdd(&h[band_of(__builtin_nontemporal_load(&py[j]), d, rows_per_band, nb)], 1u);
+  __syncthreads();
+  for (int b = threadIdx.x; b < nb; b += PTPB) hist[(int64_t)b * gridDim.x + blockIdx.x] = h[b];
+}
+
+// in-place exclusive scan of hist[0, len) by one 1024-thread block; hist[len] = total kept points
+__global__ __launch_bounds__(1024) void k_band_scan(uint32_t* __restrict__ hist, int64_t len) {
+  __shared__ uint32_t part[1024];
+  const int t = threadIdx.x;
+  const int64_t per = (len + 1023) / 1024, a = t * per, b = min(len, a + per);
+  uint32_t s = 0;
+  for (int64_t k = a; k < b; ++k) s += hist[k];
+  part[t] = s;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {
+    const uint32_t v = t >= off ? part[t - off] : 0u;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  uint32_t run = part[t] - s;
+  for (int64_t k = a; k < b; ++k) { const uint32_t c = hist[k]; hist[k] = run; run += c; }
+  if (t == 1023) hist[len] = part[1023];
+}
+
+// Scatter: tile of PTILE points -> LDS counting sort by band -> each band's run written as
+// consecutive 24-B records at the block's running cursor for that band.
+__global__ __launch_bounds__(PTPB) void k_band_scatter(const double* __restrict__ px, const double* __restrict__ py,
+                                                       int64_t n, int64_t per_block, PipDev d, int rows_per_band,
+                                                       int nb, const uint32_t* __restrict__ off,
+                                                       PtRec* __restrict__ rec) {
+  constexpr int PER_T = PTILE / PTPB;
+  __shared__ uint32_t cnt[NBAND + 1], loff[NBAND + 2], gcur[NBAND];
+  __shared__ double sx[PTILE], sy[PTILE];
+  __shared__ uint32_t sid[PTILE];
+  __shared__ uint16_t sband[PTILE];
+  const int t = threadIdx.x;
+  for (int b = t; b <= nb; b += PTPB) cnt[b] = 0;
+  for (int b = t; b < nb; b += PTPB) gcur[b] = off[(int64_t)b * gridDim.x + blockIdx.x];
+  __syncthreads();
+  const int64_t b0 = (int64_t)blockIdx.x * per_block, b1 = min(n, b0 + per_block);
+  for (int64_t t0 = b0; t0 < b1; t0 += PTILE) {
+    double x[PER_T], y[PER_T];
+    int band[PER_T];
+    uint32_t r[PER_T];
+#pragma unroll
+    for (int k = 0; k < PER_T; ++k) {
+      const int64_t j = t0 + k * PTPB + t;
+      band[k] = -1;
+      if (j < b1) {
+        x[k] = __builtin_nontemporal_load(&px[j]);
+        y[k] = __builtin_nontemporal_load(&py[j]);
+        band[k] = band_of(y[k], d, rows_per_band, nb);
+        r[k] = atomicAdd(&cnt[band[k]], 1u);
+      }
+    }
+    __syncthreads();
+    if (t < 64) {   // exclusive scan of cnt[0..nb] by one wave
+      constexpr int PER_L = (NBAND + 1 + 63) / 64;
+      uint32_t v[PER_L], s = 0;
+#pragma unroll
+      for (int k = 0; k < PER_L; ++k) { const int b = t * PER_L + k; v[k] = b <= nb ? cnt[b] : 0u; s += v[k]; }
+      uint32_t inc = s;
+      for (int o = 1; o < 64; o <<= 1) { const uint32_t w = __shfl_up(inc, o, 64); if (t >= o) inc += w; }
+      uint32_t run = inc - s;
+#pragma unroll
+      for (int k = 0; k < PER_L; ++k) { const int b = t * PER_L + k; if (b <= nb) loff[b] = run; run += v[k]; }
+      if (t == 63) loff[nb + 1] = inc;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < PER_T; ++k) {
+      if (band[k] < 0) continue;
+      const uint32_t pos = loff[band[k]] + r[k];
+      sx[pos] = x[k]; sy[pos] = y[k];
+      sid[pos] = (uint32_t)(t0 + k * PTPB + t);
+      sband[pos] = (uint16_t)band[k];
+    }
+    __syncthreads();
+    const int kept = (int)loff[nb];   // drop bin sorts last
+    for (int q = t; q < kept; q += PTPB) {
+      const int b = sband[q];
+      PtRec* o = rec + gcur[b] + (q - loff[b]);
+      o->x = sx[q]; o->y = sy[q]; o->idx = sid[q]; o->pad = 0;
+    }
+    __syncthreads();
+    for (int b = t; b <= nb; b += PTPB) {
+      if (b < nb) gcur[b] += cnt[b];
+      cnt[b] = 0;
+    }
+    __syncthreads();
   }
 }
 
@@ -455,6 +640,23 @@ struct BandSeg {
 };
 
 }  // namespace
+
+// persistent grid: exactly the resident block count of this kernel (a rounded multiple of 8 for
+// the XCD-aware mapping), so no partial second round of blocks forms a tail
+template <bool WRITE, bool REC>
+static unsigned join_grid(int device, int64_t ntiles) {
+  static int resident = 0;   // per instantiation; every device of the node is the same MI355X
+  if (!resident) {
+    int b = 0, n = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_pip_join<WRITE, REC>, JTPB, 0) != hipSuccess || b < 1) b = 4;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess) n = prop.multiProcessorCount;
+    resident = b * n;
+  }
+  int64_t g = std::min<int64_t>(resident, std::max<int64_t>(ntiles, 1));
+  if (REC) g = (g + 7) / 8 * 8;
+  return (unsigned)g;
+}
 
 extern "C" {
 
@@ -759,24 +961,70 @@ int gm_pip_index_stats(const gm_pip_index* ix, int64_t* stats) {
 
 int gm_pip_join(gm_ctx* ctx, const gm_pip_index* ix, const double* px, const double* py, int64_t n, int64_t id_base,
                 int64_t* pt_ids, int32_t* poly_ids, int64_t cap, int64_t* n_pairs) {
+  return gm_pip_join_ex(ctx, ix, px, py, n, id_base, pt_ids, poly_ids, cap, n_pairs, GM_JOIN_AUTO);
+}
+
+int gm_pip_join_ex(gm_ctx* ctx, const gm_pip_index* ix, const double* px, const double* py, int64_t n,
+                   int64_t id_base, int64_t* pt_ids, int32_t* poly_ids, int64_t cap, int64_t* n_pairs, int mode) {
   if (!ctx || !ix || n < 0 || cap < 0) return GM_E_INVALID;
+  if (mode != GM_JOIN_AUTO && mode != GM_JOIN_DIRECT && mode != GM_JOIN_PARTITIONED) return GM_E_INVALID;
   const bool write = pt_ids && poly_ids;
   if ((pt_ids == nullptr) != (poly_ids == nullptr)) return GM_E_INVALID;
   if (n > 0 && (!px || !py)) return GM_E_INVALID;
+  GM_HIP(hipSetDevice(ctx->device));
   unsigned long long* counter = (unsigned long long*)ctx->d_scratch;
   GM_HIP(hipMemsetAsync(counter, 0, 8, ctx->stream));
-  const int64_t CHUNK = (int64_t)1 << 31;  // LDS staging keeps 32-bit row offsets
-  for (int64_t c0 = 0; c0 < n; c0 += CHUNK) {
-    const int64_t m = std::min(CHUNK, n - c0);
-    const int64_t ntiles = (m + JTPB - 1) / JTPB;
-    const unsigned grid = (unsigned)std::min<int64_t>(ntiles, 256 * 2 * 4);
-    if (write)
-      hipLaunchKernelGGL((k_pip_join<true>), dim3(grid), dim3(JTPB), 0, ctx->stream, px + c0, py + c0, m, id_base + c0,
-                         ix->dev, pt_ids, poly_ids, cap, counter);
-    else
-      hipLaunchKernelGGL((k_pip_join<false>), dim3(grid), dim3(JTPB), 0, ctx->stream, px + c0, py + c0, m, id_base + c0,
-                         ix->dev, pt_ids, poly_ids, cap, counter);
-    GM_CHECK_LAUNCH();
+  const bool part = mode == GM_JOIN_PARTITIONED || (mode == GM_JOIN_AUTO && n >= ((int64_t)1 << 22));
+  if (!part) {
+    const int64_t CHUNK = (int64_t)1 << 31;  // LDS staging keeps 32-bit row offsets
+    for (int64_t c0 = 0; c0 < n; c0 += CHUNK) {
+      const int64_t m = std::min(CHUNK, n - c0);
+      const int64_t ntiles = (m + JTILE - 1) / JTILE;
+      const unsigned grid = write ? join_grid<true, false>(ctx->device, ntiles) : join_grid<false, false>(ctx->device, ntiles);
+      if (write)
+        hipLaunchKernelGGL((k_pip_join<true, false>), dim3(grid), dim3(JTPB), 0, ctx->stream, px + c0, py + c0,
+                           nullptr, nullptr, m, id_base + c0, ix->dev, pt_ids, poly_ids, cap, counter);
+      else
+        hipLaunchKernelGGL((k_pip_join<false, false>), dim3(grid), dim3(JTPB), 0, ctx->stream, px + c0, py + c0,
+                           nullptr, nullptr, m, id_base + c0, ix->dev, pt_ids, poly_ids, cap, counter);
+      GM_CHECK_LAUNCH();
+    }
+  } else if (n > 0) {
+    const int64_t CHUNK = (int64_t)1 << 28;  // 6 GiB of band-sorted records per pass
+    const int rows_per_band = (ix->dev.gy + NBAND - 1) / NBAND;
+    const int nb = (ix->dev.gy + rows_per_band - 1) / rows_per_band;
+    const int64_t mmax = std::min(CHUNK, n);
+    const int nblk = (int)std::max<int64_t>(1, std::min<int64_t>(512, (mmax + PTILE - 1) / PTILE));
+    const int64_t hlen = (int64_t)nb * nblk;
+    uint32_t* hist = nullptr;
+    PtRec* rec = nullptr;
+    GM_HIP(hipMallocAsync((void**)&hist, (size_t)(hlen + 1) * 4, ctx->stream));
+    hipError_t e = hipMallocAsync((void**)&rec, (size_t)mmax * sizeof(PtRec), ctx->stream);
+    if (e != hipSuccess) { (void)hipFreeAsync(hist, ctx->stream); return hip_fail(e, "hipMallocAsync(join records)"); }
+    int rc = GM_OK;
+    for (int64_t c0 = 0; c0 < n && rc == GM_OK; c0 += CHUNK) {
+      const int64_t m = std::min(CHUNK, n - c0);
+      const int64_t per = ((m + nblk - 1) / nblk + PTILE - 1) / PTILE * PTILE;
+      const unsigned pgrid = (unsigned)((m + per - 1) / per);   // <= nblk
+      hipLaunchKernelGGL(k_band_hist, dim3(pgrid), dim3(PTPB), 0, ctx->stream, py + c0, m, per, ix->dev,
+                         rows_per_band, nb, hist);
+      hipLaunchKernelGGL(k_band_scan, dim3(1), dim3(1024), 0, ctx->stream, hist, (int64_t)nb * pgrid);
+      hipLaunchKernelGGL(k_band_scatter, dim3(pgrid), dim3(PTPB), 0, ctx->stream, px + c0, py + c0, m, per, ix->dev,
+                         rows_per_band, nb, hist, rec);
+      const uint32_t* n_rec = hist + (int64_t)nb * pgrid;
+      const int64_t ntiles = (m + JTILE - 1) / JTILE;
+      const unsigned grid = write ? join_grid<true, true>(ctx->device, ntiles) : join_grid<false, true>(ctx->device, ntiles);
+      if (write)
+        hipLaunchKernelGGL((k_pip_join<true, true>), dim3(grid), dim3(JTPB), 0, ctx->stream, nullptr, nullptr, rec,
+                           n_rec, m, id_base + c0, ix->dev, pt_ids, poly_ids, cap, counter);
+      else
+        hipLaunchKernelGGL((k_pip_join<false, true>), dim3(grid), dim3(JTPB), 0, ctx->stream, nullptr, nullptr, rec,
+                           n_rec, m, id_base + c0, ix->dev, pt_ids, poly_ids, cap, counter);
+      if (hipGetLastError() != hipSuccess) rc = hip_fail(hipErrorLaunchFailure, "k_pip_join (partitioned)");
+    }
+    (void)hipFreeAsync(rec, ctx->stream);
+    (void)hipFreeAsync(hist, ctx->stream);
+    if (rc) return rc;
   }
   if (n_pairs) {
     GM_HIP(hipMemcpyAsync(ctx->h_pinned, counter, 8, hipMemcpyDeviceToHost, ctx->stream));

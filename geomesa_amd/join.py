@@ -110,8 +110,14 @@ class PolygonIndex:
         check(self.ctx.lib.gm_pip_index_stats(self._h, st.ctypes.data), "gm_pip_index_stats")
         return dict(zip(["cells", "entries", "boundary", "records", "slow", "blob_bytes"], st.tolist()))
 
-    def join(self, px, py, id_base=0, cap=None, count_only=False):
-        """Returns (pt_ids, poly_ids) device tensors (or the pair count when count_only)."""
+    MODES = {"auto": _lib.GM_JOIN_AUTO, "direct": _lib.GM_JOIN_DIRECT, "partitioned": _lib.GM_JOIN_PARTITIONED}
+
+    def join(self, px, py, id_base=0, cap=None, count_only=False, mode="auto"):
+        """Returns (pt_ids, poly_ids) device tensors (or the pair count when count_only).
+
+        mode: "auto", "direct" (one pass over the point columns) or "partitioned" (points
+        counting-sorted by grid-row band first); the pair set is the same for every mode."""
+        m = self.MODES[mode]
         import torch
         from .curve import _dev_col
         px = _dev_col(px, torch.float64)
@@ -119,16 +125,16 @@ class PolygonIndex:
         n = px.numel()
         npairs = ctypes.c_int64()
         if count_only:
-            check(self.ctx.lib.gm_pip_join(self.ctx.handle, self._h, ptr(px), ptr(py), n, id_base, None, None, 0,
-                                           ctypes.byref(npairs)), "gm_pip_join")
+            check(self.ctx.lib.gm_pip_join_ex(self.ctx.handle, self._h, ptr(px), ptr(py), n, id_base, None, None, 0,
+                                              ctypes.byref(npairs), m), "gm_pip_join")
             return npairs.value
         if cap is None:
             cap = max(1024, n + n // 4)
         while True:
             pt = torch.empty(cap, dtype=torch.int64, device=px.device)
             pl = torch.empty(cap, dtype=torch.int32, device=px.device)
-            rc = self.ctx.lib.gm_pip_join(self.ctx.handle, self._h, ptr(px), ptr(py), n, id_base, ptr(pt), ptr(pl),
-                                          cap, ctypes.byref(npairs))
+            rc = self.ctx.lib.gm_pip_join_ex(self.ctx.handle, self._h, ptr(px), ptr(py), n, id_base, ptr(pt),
+                                             ptr(pl), cap, ctypes.byref(npairs), m)
             if rc == _lib.GM_E_CAPACITY:
                 cap = npairs.value
                 continue

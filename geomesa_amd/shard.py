@@ -1,0 +1,50 @@
+"""Multi-GPU plumbing for the hot path: one process per GPU, points sharded by contiguous row range.
+
+Every operation on the path is independent per point (Z3/Z2/XZ keys, filter scans, the
+st_contains join against a replicated polygon set), so ranks shard the points and run with no
+data-path collective ("weak" scaling).  The only exchanges are the polygon-set broadcast before a
+join (the reference ships the smaller side of the join to every partition: GeoMesaJoinRelation /
+RelationUtils.grid, geomesa-spark-sql/.../GeoMesaJoinRelation.scala:41-91) and the scalar
+max/sum reductions of the benchmark.  Works with both RCCL ("nccl", device tensors) and gloo
+(CPU tensors, used by the multi-process tests).
+"""
+import numpy as np
+
+
+def shard_bounds(n_total, rank, world):
+    """Contiguous [lo, hi) rows of rank `rank` out of `world` (sizes differ by at most one)."""
+    if world < 1 or not 0 <= rank < world or n_total < 0:
+        raise ValueError("bad shard request: n=%d rank=%d world=%d" % (n_total, rank, world))
+    base, extra = divmod(n_total, world)
+    lo = rank * base + min(rank, extra)
+    return lo, lo + base + (1 if rank < extra else 0)
+
+
+def _device_of(pg):
+    return "cuda" if pg.get_backend() == "nccl" else "cpu"
+
+
+def broadcast_polyset(pg, ps, src=0):
+    """Broadcast a PolygonSet from rank `src`; other ranks pass ps=None and get the copy back."""
+    import torch
+    from .join import PolygonSet
+    dev = _device_of(pg)
+    arrs = ps.to_arrays() if pg.get_rank() == src else None
+    sizes = torch.tensor([len(v) for v in arrs] if arrs else [0] * 5, dtype=torch.int64, device=dev)
+    pg.broadcast(sizes, src)
+    out = []
+    for k, (sz, dt) in enumerate(zip(sizes.tolist(), [torch.int32] * 3 + [torch.float64] * 2)):
+        t = torch.from_numpy(np.ascontiguousarray(arrs[k])).to(dev) if arrs else torch.empty(sz, dtype=dt, device=dev)
+        pg.broadcast(t, src)
+        out.append(t.cpu().numpy())
+    return PolygonSet(*out)
+
+
+def all_reduce_scalar(pg, v, op="max"):
+    """max / sum of one float over all ranks (identity without a process group)."""
+    if pg is None:
+        return float(v)
+    import torch
+    t = torch.tensor([float(v)], dtype=torch.float64, device=_device_of(pg))
+    pg.all_reduce(t, op={"max": pg.ReduceOp.MAX, "sum": pg.ReduceOp.SUM}[op])
+    return float(t.item())

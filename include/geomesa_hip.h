@@ -43,6 +43,12 @@ extern "C" {
 #define GM_E_ELEMENT (-4)     /* at least one element failed (only when no status[] and no summary) */
 
 /* per-element status codes */
+/* BinnedTime periods (TimePeriod, z3/curve/BinnedTime.scala:283-291) */
+#define GM_PERIOD_DAY 0
+#define GM_PERIOD_WEEK 1
+#define GM_PERIOD_MONTH 2
+#define GM_PERIOD_YEAR 3
+
 #define GM_ST_OK 0
 #define GM_ST_OUT_OF_BOUNDS 1 /* Z3SFC/Z2SFC/XZ2SFC/XZ3SFC require(...) -> IllegalArgumentException */
 #define GM_ST_BAD_TIME 2      /* BinnedTime require(...): before 1970-01-01 or past the period's max date */
@@ -195,7 +201,7 @@ typedef struct gm_pip_index gm_pip_index;
    plus per-ring y-slab edge buckets). */
 int gm_pip_index_create(gm_ctx* ctx, const gm_polyset* polys, gm_pip_index** out);
 /* same with an explicit grid density: ~cells_per_poly grid cells per polygon over the set's
-   envelope (0 = default 1024; a coarse 4x4-cell table in front of it stays L2-resident) */
+   envelope (0 = default 2048; a coarse 4x4-cell table in front of it stays L2-resident) */
 int gm_pip_index_create_ex(gm_ctx* ctx, const gm_polyset* polys, int cells_per_poly, gm_pip_index** out);
 int gm_pip_index_destroy(gm_pip_index* index);
 /* index statistics: stats[0..5] = cells, (cell, polygon) entries, boundary entries, ring records,
@@ -212,6 +218,16 @@ int gm_pip_index_stats(const gm_pip_index* index, int64_t* stats);
    pt_ids = poly_ids = NULL the call only counts. */
 int gm_pip_join(gm_ctx* ctx, const gm_pip_index* index, const double* px, const double* py, int64_t n,
                 int64_t id_base, int64_t* pt_ids, int32_t* poly_ids, int64_t cap, int64_t* n_pairs);
+
+/* join strategies for gm_pip_join_ex */
+#define GM_JOIN_AUTO 0        /* partitioned from 2^22 points, direct below */
+#define GM_JOIN_DIRECT 1      /* one pass over the point columns (random index reads) */
+#define GM_JOIN_PARTITIONED 2 /* counting-sort the points by grid-row band first (device temp:
+                                 24 B per point, at most 2^28 points per pass), then join band by
+                                 band with the band's index data L2-resident */
+/* gm_pip_join with an explicit strategy; the pair set is identical for every mode */
+int gm_pip_join_ex(gm_ctx* ctx, const gm_pip_index* index, const double* px, const double* py, int64_t n,
+                   int64_t id_base, int64_t* pt_ids, int32_t* poly_ids, int64_t cap, int64_t* n_pairs, int mode);
 
 /* ------------------------------------------------------------------ synthetic data (bench/tests) */
 /* SplitMix64 keyed by (seed, index): lon U[lon0,lon1), lat U[lat0,lat1), t_ms U[t0,t1) */

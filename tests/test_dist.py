@@ -1,0 +1,86 @@
+"""Multi-process (gloo, world_size 2, CPU) tests of the sharding path bench.py and users run over RCCL.
+
+The product kernels need the GPU, so the per-rank compute here is the C oracle (test
+infrastructure): what is checked is the distributed bookkeeping -- shard bounds, the polygon-set
+broadcast, id_base offsets of per-rank join output, and the max/sum reductions -- which is the same
+code the RCCL path runs.
+"""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, n_total, q):
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import oracle as O
+        from geomesa_amd.join import synthetic_counties, synthetic_points
+        from geomesa_amd.shard import all_reduce_scalar, broadcast_polyset, shard_bounds
+        ps = synthetic_counties(20, 10) if rank == 0 else None
+        ps = broadcast_polyset(dist, ps)
+        px, py = synthetic_points(n_total, seed=21)
+        lo, hi = shard_bounds(n_total, rank, world)
+        pt, pl = O.OraclePolySet(*ps.to_arrays()).join(px[lo:hi], py[lo:hi], nthreads=2)
+        pairs = np.stack([pt + lo, pl.astype(np.int64)], 1)
+        gathered = [None] * world
+        dist.all_gather_object(gathered, pairs)
+        tot = all_reduce_scalar(dist, len(pairs), "sum")
+        mx = all_reduce_scalar(dist, float(rank + 1), "max")
+        if rank == 0:
+            q.put((np.concatenate(gathered), tot, mx, ps.vx.sum(), ps.n_polys))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2])
+def test_sharded_join_equals_global(world, oracle):
+    from geomesa_amd.join import synthetic_counties, synthetic_points
+    n_total = 60_001
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n_total, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    got, tot, mx, vxsum, npoly = res
+    ps = synthetic_counties(20, 10)
+    assert npoly == ps.n_polys and vxsum == ps.vx.sum()      # broadcast delivered the same set
+    px, py = synthetic_points(n_total, seed=21)
+    opt, opl = oracle.OraclePolySet(*ps.to_arrays()).join(px, py, nthreads=4)
+    exp = np.stack([opt, opl.astype(np.int64)], 1)
+    got = got[np.lexsort((got[:, 1], got[:, 0]))]
+    assert np.array_equal(got, exp)
+    assert tot == len(exp) and mx == float(world)
+
+
+def test_shard_bounds():
+    from geomesa_amd.shard import shard_bounds
+    for n in (0, 1, 7, 1000, 10**9 + 3):
+        for w in (1, 2, 3, 8):
+            b = [shard_bounds(n, r, w) for r in range(w)]
+            assert b[0][0] == 0 and b[-1][1] == n
+            assert all(b[i][1] == b[i + 1][0] for i in range(w - 1))
+            assert max(h - l for l, h in b) - min(h - l for l, h in b) <= 1
+    with pytest.raises(ValueError):
+        shard_bounds(10, 2, 2)

@@ -136,17 +136,54 @@ def test_pip_join_synthetic_counties(gpu, oracle, grid, cells_per_poly):
     ix = PolygonIndex(ps, cells_per_poly=cells_per_poly)
     if cells_per_poly == 1:
         assert ix.stats()["slow"] > 0   # exercises the slab-walk fallback
-    pt, pl = ix.join(px, py)
     import oracle as O
     opt, opl = O.OraclePolySet(*ps.to_arrays()).join(px, py, nthreads=8)
-    got = np.stack([as_np(pt), as_np(pl).astype(np.int64)], 1)
-    got = got[np.lexsort((got[:, 1], got[:, 0]))]
     exp = np.stack([opt, opl.astype(np.int64)], 1)
-    assert got.shape == exp.shape and np.array_equal(got, exp)
-    assert ix.join(px, py, count_only=True) == len(exp)
-    # capacity path
-    pt2, pl2 = ix.join(px, py, cap=10)
-    assert len(pt2) == len(exp)
+    for mode in ("direct", "partitioned"):
+        pt, pl = ix.join(px, py, mode=mode)
+        assert np.array_equal(_sorted_pairs(pt, pl), exp), mode
+        assert ix.join(px, py, count_only=True, mode=mode) == len(exp)
+        # capacity path
+        pt2, pl2 = ix.join(px, py, cap=10, mode=mode)
+        assert len(pt2) == len(exp)
+
+
+def _sorted_pairs(pt, pl):
+    got = np.stack([as_np(pt), as_np(pl).astype(np.int64)], 1)
+    return got[np.lexsort((got[:, 1], got[:, 0]))]
+
+
+def test_pip_join_partitioned_edges(gpu, oracle):
+    """Row-band partition: NaN / off-grid points are dropped, id_base offsets ids, empty input."""
+    from geomesa_amd.join import PolygonIndex, synthetic_counties, synthetic_points
+    ps = synthetic_counties(20, 10)
+    ix = PolygonIndex(ps)
+    px, py = synthetic_points(300_000, seed=5)
+    px[::97] = np.nan; py[::89] = np.nan
+    py[::101] = 1e9; px[::103] = -1e9
+    py[::107] = np.inf; px[::109] = -np.inf
+    import oracle as O
+    opt, opl = O.OraclePolySet(*ps.to_arrays()).join(px, py, nthreads=8)
+    exp = np.stack([opt + 1000, opl.astype(np.int64)], 1)
+    for mode in ("direct", "partitioned"):
+        pt, pl = ix.join(px, py, id_base=1000, mode=mode)
+        assert np.array_equal(_sorted_pairs(pt, pl), exp), mode
+        assert ix.join(px[:0], py[:0], mode=mode)[0].numel() == 0
+        assert ix.join(px[:1], py[:1], count_only=True, mode=mode) == int((opt == 0).sum())
+
+
+def test_pip_join_auto_large(gpu, oracle):
+    """Auto mode switches to the partitioned join at 2^22 points; results equal the oracle."""
+    from geomesa_amd.join import PolygonIndex, synthetic_counties, synthetic_points
+    ps = synthetic_counties(80, 40)
+    ix = PolygonIndex(ps)
+    px, py = synthetic_points(5_000_000, seed=9)
+    import oracle as O
+    opt, opl = O.OraclePolySet(*ps.to_arrays()).join(px, py, nthreads=16)
+    exp = np.stack([opt, opl.astype(np.int64)], 1)
+    pt, pl = ix.join(px, py)
+    assert np.array_equal(_sorted_pairs(pt, pl), exp)
+    assert ix.join(px, py, count_only=True, mode="direct") == len(exp)
 
 
 # ---------------------------------------------------------------- batched ranges
