@@ -7,7 +7,8 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libgeomesa_hip.so")
+# GEOMESA_HIP_LIB selects another in-tree build of the same library (variant builds for profiling)
+LIB_PATH = os.environ.get("GEOMESA_HIP_LIB", os.path.join(HERE, "lib", "libgeomesa_hip.so"))
 HEADER = os.path.join(os.path.dirname(HERE), "include", "geomesa_hip.h")
 
 GM_OK = 0

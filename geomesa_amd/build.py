@@ -24,17 +24,22 @@ def needs_build():
     return any(os.path.getmtime(f) > t for f in deps)
 
 
-def build(force=False, verbose=True):
-    if not force and not needs_build():
+def build(force=False, verbose=True, out=OUT, defines=()):
+    """Compile every HIP unit into one shared library; `defines` builds a tuning variant (e.g.
+    GM_JILP=8) to another path for side-by-side measurement."""
+    if out == OUT and not defines and not force and not needs_build():
         return OUT
-    os.makedirs(os.path.dirname(OUT), exist_ok=True)
-    cmd = [HIPCC] + FLAGS + ["-o", OUT + ".tmp"] + sources()
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    cmd = [HIPCC] + FLAGS + ["-D" + d for d in defines] + ["-o", out + ".tmp"] + sources()
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.check_call(cmd)
-    os.replace(OUT + ".tmp", OUT)
-    return OUT
+    os.replace(out + ".tmp", out)
+    return out
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv)
+    args = sys.argv[1:]
+    defs = [a[2:] for a in args if a.startswith("-D")]
+    outs = [a.split("=", 1)[1] for a in args if a.startswith("--out=")]
+    build(force="--force" in args, out=outs[0] if outs else OUT, defines=defs)

@@ -12,9 +12,6 @@ namespace gm {
 
 constexpr int TPB = 256;
 
-// clang ext-vector types: one dwordx4 per lane; usable with the nontemporal builtins
-typedef double dv2 __attribute__((ext_vector_type(2)));
-typedef long long lv2 __attribute__((ext_vector_type(2)));
 
 #ifndef GM_NT
 #define GM_NT 1

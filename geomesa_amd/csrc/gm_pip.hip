@@ -29,6 +29,8 @@
 
 #include <algorithm>
 #include <vector>
+#include <cstdio>
+#include <cstdlib>
 
 #include "gm_internal.hpp"
 
@@ -52,7 +54,7 @@ struct PipDev {
   const Edge* slab_edges;
   const uint32_t* coarse_word;   // per coarse cell (CF x CF fine cells): EMPTY, INTERIOR or LIST = "look at the fine word"
   const uint32_t* cell_word;     // per cell: kind << 30 | payload (see CELL_*)
-  const int32_t* list_off;       // multi-entry cells: entries list_ent[list_off[i] .. list_off[i+1])
+  const double* compact;         // compact blobs: 16 words (one 128-B line) each
   const uint32_t* list_ent;      // entries in cell-word form (kind INTERIOR or BOUNDARY)
   const double* blob;            // boundary blobs, 16-byte aligned
   double gx0, gy0, gx1, gy1, inv_cw, inv_ch;
@@ -61,19 +63,24 @@ struct PipDev {
 
 constexpr int CF_LOG = 2;   // coarse cell = 4 x 4 fine cells: the coarse table stays L2-resident
 
-// cell word kinds
+// cell word kinds (2 high bits; 30-bit payload)
 enum : uint32_t { CELL_INTERIOR = 0, CELL_BOUNDARY = 1, CELL_LIST = 2, CELL_EMPTY = 3 };
+// BOUNDARY payload: bit 29 set = compact blob index, else generic blob offset (16-B units)
+constexpr uint32_t BLOB_COMPACT = 1u << 29;
+// LIST payload: list_ent offset << 4 | count; count 15 = long list whose count is list_ent[offset]
+constexpr int LIST_LONG = 15;
 
-// Boundary blob (one per BOUNDARY (cell, polygon) pair; 8-byte words, 16-byte aligned):
-//   w0: int32 polygon | int32 n_rings
-//   per ring, in CSR order:
-//     w: int16 n_edge | int16 n_brk | int16 flags (1 = first ring of a part, 2 = slow walk) | pad
-//     w: parity bits (slow walk: int32 ring id)
-//     n_edge x 4 words: segments meeting the inflated cell (p1 = ring[i], p2 = ring[i-1])
-//     n_brk words: breakpoint y values (ascending)
-// The polygon / ring envelope tests of Geometry.contains and PointLocator are not stored: for a point
-// outside a ring's envelope the crossing count is even and no segment holds the point, so the ring
-// walk returns EXTERIOR exactly as the early exit does.
+// Compact blob (single-ring polygon, 4 * segments + breakpoints <= 30 in the cell): one or two
+// 128-B lines of 16 words in `compact`, addressed by line index.
+//   w0: int32 polygon | int32 meta (segments | lines << 8), w1: parity bits,
+//   segment j (p1x p1y p2x p2y) at words CSEG[j] = 2, 6, 10 (line 0), 16, 20, 24, 28 (line 1);
+//   every other word of the record is a breakpoint slot (+inf when unused).
+// The breakpoint count k = #(slots <= y) does not depend on slot order, so the record is evaluated
+// with static indexing, line by line: crossings = parity bit k + segment crossings, exactly the
+// RayCrossingCounter walk of a generic one-ring blob.
+constexpr int CSEG_MAX = 7;
+__host__ __device__ constexpr int cseg_word(int j) { return j < 3 ? 2 + 4 * j : 16 + 4 * (j - 3); }
+
 struct RingHdr {
   int16_t n_edge, n_brk, flags, pad;
 };
@@ -168,16 +175,50 @@ __device__ bool blob_contains(const PipDev& d, const double* b, int2 h, double p
   return nb > 0 || is_in;        // INTERIOR
 }
 
-__device__ __forceinline__ bool entry_contains(const PipDev& d, uint32_t e, double x, double y, int& poly) {
-  if ((e >> 30) == CELL_INTERIOR) { poly = (int)(e & 0x3fffffffu); return true; }
-  const double* b = d.blob + 2 * (uint64_t)(e & 0x3fffffffu);
-  const int2 h = *(const int2*)b;
-  poly = h.x;
-  return blob_contains(d, b, h, x, y);
+// one line (16 words, 8 independent 16-B loads) of a compact blob: breakpoint count and segments
+template <int LINE>
+__device__ __forceinline__ void compact_line(const dv2* __restrict__ c, int E, double px, double py, int& k,
+                                             int& cr, bool& on) {
+  dv2 q[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) q[i] = c[8 * LINE + i];
+  auto word = [&](int w) -> double { return (w & 1) ? q[(w & 15) >> 1].y : q[(w & 15) >> 1].x; };
+#pragma unroll
+  for (int w = 16 * LINE; w < 16 * LINE + 16; ++w) {
+    if (w < 2) continue;
+    int seg = -1;   // segment group holding word w (compile-time)
+#pragma unroll
+    for (int j = 0; j < CSEG_MAX; ++j)
+      if (w >= cseg_word(j) && w < cseg_word(j) + 4) seg = j;
+    if (seg < 0 || seg >= E) k += word(w) <= py;     // a breakpoint slot (+inf when unused)
+  }
+#pragma unroll
+  for (int j = 0; j < CSEG_MAX; ++j) {
+    if (cseg_word(j) / 16 != LINE) continue;
+    const int w0 = cseg_word(j);
+    if (j < E && !on) on = count_segment(word(w0), word(w0 + 1), word(w0 + 2), word(w0 + 3), px, py, cr);
+  }
+}
+
+__device__ __forceinline__ bool compact_contains(const dv2* __restrict__ c, double px, double py, int& poly) {
+  const dv2 h = c[0];
+  const int64_t meta = __double_as_longlong(h.x);
+  poly = (int)meta;
+  const int E = (int)((meta >> 32) & 0xff), lines = (int)((meta >> 40) & 0xff);
+  int k = 0, cr = 0;
+  bool on = false;
+  compact_line<0>(c, E, px, py, k, cr, on);
+  if (lines > 1) compact_line<1>(c, E, px, py, k, cr, on);
+  if (on) return false;
+  cr += (int)(((uint64_t)__double_as_longlong(h.y) >> k) & 1ull);
+  return cr & 1;
 }
 
 constexpr int JTPB = 256;             // 4 waves
-constexpr int JILP = 2;               // points per lane per tile (their lookups overlap)
+#ifndef GM_JILP
+#define GM_JILP 2
+#endif
+constexpr int JILP = GM_JILP;         // points per lane per tile (their lookups overlap)
 constexpr int WCAP = 512;             // LDS pair staging per wave (4 KiB)
 constexpr int QCAP = 128;             // LDS blob work queue per wave (3 KiB)
 constexpr int JTILE = JTPB * JILP;
@@ -257,6 +298,7 @@ __global__ __launch_bounds__(JTPB) void k_pip_join(const double* __restrict__ px
     double x[JILP], y[JILP];
     uint32_t id[JILP], cw[JILP];
     int lo[JILP], ni[JILP];
+    uint4 lq[JILP];
 #pragma unroll
     for (int u = 0; u < JILP; ++u) {
       const int64_t i = tile * JTILE + u * JTPB + threadIdx.x;
@@ -293,26 +335,44 @@ __global__ __launch_bounds__(JTPB) void k_pip_join(const double* __restrict__ px
       const uint32_t kind = cw[u] >> 30;
       lo[u] = 0;
       ni[u] = kind == CELL_EMPTY ? 0 : 1;
+      lq[u] = make_uint4(cw[u], 0u, 0u, 0u);
       if (kind == CELL_LIST) {
-        const int li = (int)(cw[u] & 0x3fffffffu);
-        lo[u] = d.list_off[li];
-        ni[u] = d.list_off[li + 1] - lo[u];
+        lo[u] = 4 * (int)((cw[u] & 0x3fffffffu) >> 4);
+        ni[u] = (int)(cw[u] & 15u);
+        lq[u] = *(const uint4*)(d.list_ent + lo[u]);   // the first four slots, all points at once
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < JILP; ++u) {
+      if (ni[u] == LIST_LONG && (cw[u] >> 30) == CELL_LIST) {   // long list: [count, entries...]
+        ni[u] = (int)lq[u].x;
+        lo[u] += 1;
+        lq[u] = make_uint4(lq[u].y, lq[u].z, lq[u].w, 0u);
       }
     }
     // item walk; after the last tile the same loop drains the queue and ends
-    const int ntot = ni[0] + (JILP > 1 ? ni[JILP - 1] : 0);
+    int pre[JILP + 1];
+    pre[0] = 0;
+#pragma unroll
+    for (int u = 0; u < JILP; ++u) pre[u + 1] = pre[u] + ni[u];
+    const int ntot = pre[JILP];
     for (int k = 0;; ++k) {
       const bool act = k < ntot;
       const bool any = __ballot(act) != 0;
       if (!any && (have ? qn < 64 : qn == 0)) break;
       if (any) {
-        const bool second = JILP > 1 && k >= ni[0];
-        const int kk = second ? k - ni[0] : k;
-        const uint32_t w = second ? cw[JILP - 1] : cw[0];
-        uint32_t e = w;
-        if (act && (w >> 30) == CELL_LIST) e = d.list_ent[(second ? lo[JILP - 1] : lo[0]) + kk];
-        const double ex = second ? x[JILP - 1] : x[0], ey = second ? y[JILP - 1] : y[0];
-        const uint32_t eid = second ? id[JILP - 1] : id[0];
+        // item k belongs to the last point u with pre[u] <= k (static selects, no register indexing)
+        double ex = x[0], ey = y[0];
+        uint32_t eid = id[0], w = cw[0];
+        uint4 q = lq[0];
+        int j = k, base = lo[0];
+#pragma unroll
+        for (int u = 1; u < JILP; ++u)
+          if (k >= pre[u]) { ex = x[u]; ey = y[u]; eid = id[u]; w = cw[u]; q = lq[u]; j = k - pre[u]; base = lo[u]; }
+        // slot j of the point's list: registers for the first slots, a load beyond them (long lists)
+        uint32_t e = j == 0 ? q.x : j == 1 ? q.y : j == 2 ? q.z : q.w;
+        if (act && (w >> 30) == CELL_LIST && j >= 3 && !(j == 3 && (w & 15u) != LIST_LONG))
+          e = d.list_ent[base + j];
         const bool hit = act && (e >> 30) == CELL_INTERIOR;
         const bool blob = act && (e >> 30) != CELL_INTERIOR;
         if (!WRITE) my_count += hit;
@@ -336,12 +396,18 @@ __global__ __launch_bounds__(JTPB) void k_pip_join(const double* __restrict__ px
         int poly = 0;
         uint32_t eid = 0;
         if (lane < kq) {
-          const double* b = d.blob + 2 * (uint64_t)qb[slot];
+          const uint32_t ref = qb[slot];
           const double ex = qx[slot], ey = qy[slot];
           eid = qid[slot];
-          const int2 h = *(const int2*)b;
-          poly = h.x;
-          hit = blob_contains(d, b, h, ex, ey);
+          if (ref & BLOB_COMPACT) {
+            const dv2* c = (const dv2*)(d.compact + 16 * (uint64_t)(ref & (BLOB_COMPACT - 1)));
+            hit = compact_contains(c, ex, ey, poly);
+          } else {
+            const double* b = d.blob + 2 * (uint64_t)ref;
+            const int2 h = *(const int2*)b;
+            poly = h.x;
+            hit = blob_contains(d, b, h, ex, ey);
+          }
         }
         wave_lds_sync();
         qn -= kq;
@@ -616,7 +682,7 @@ struct gm_pip_index {
   gm::PipDev dev{};
   std::vector<void*> allocs;
   int32_t n_polys = 0;
-  int64_t n_entries = 0, n_boundary = 0, n_records = 0, n_slow = 0, n_cells = 0, blob_bytes = 0;
+  int64_t n_entries = 0, n_boundary = 0, n_records = 0, n_slow = 0, n_cells = 0, blob_bytes = 0, n_compact = 0;
 };
 
 using namespace gm;
@@ -638,6 +704,36 @@ struct BandSeg {
   double minx, maxx, ymin, ymax;
   int32_t vmin, vmax;  // vertex ids holding ymin / ymax
 };
+
+// breakpoints of a cell: y values of right-of-cell segment end points inside (yb0, yb1], ascending, unique
+void collect_breakpoints(const std::vector<const BandSeg*>& right, double yb0, double yb1,
+                         std::vector<std::pair<double, int32_t>>& bk) {
+  bk.clear();
+  for (const BandSeg* sg : right) {
+    if (sg->ymin > yb0 && sg->ymin <= yb1) bk.push_back({sg->ymin, sg->vmin});
+    if (sg->ymax > yb0 && sg->ymax <= yb1) bk.push_back({sg->ymax, sg->vmax});
+  }
+  std::sort(bk.begin(), bk.end(),
+            [](const std::pair<double, int32_t>& x, const std::pair<double, int32_t>& y) { return x.first < y.first; });
+  bk.erase(std::unique(bk.begin(), bk.end(),
+                       [](const std::pair<double, int32_t>& x, const std::pair<double, int32_t>& y) {
+                         return x.first == y.first;
+                       }),
+           bk.end());
+}
+
+// parity of right-of-cell segments straddling y (ymin <= y < ymax) at each breakpoint interval's left end
+uint64_t right_parity(const std::vector<const BandSeg*>& right, double yb0,
+                      const std::vector<std::pair<double, int32_t>>& bk) {
+  uint64_t parity = 0;
+  for (size_t j = 0; j <= bk.size(); ++j) {
+    const double yk = j == 0 ? yb0 : bk[j - 1].first;
+    int c = 0;
+    for (const BandSeg* sg : right) c += (sg->ymin <= yk && yk < sg->ymax);
+    if (c & 1) parity |= 1ull << j;
+  }
+  return parity;
+}
 
 }  // namespace
 
@@ -755,7 +851,10 @@ int gm_pip_index_create_ex(gm_ctx* ctx, const gm_polyset* ps, int cells_per_poly
     double w; int32_t v[2] = {a, b}; memcpy(&w, v, 8); blob.push_back(w);
   };
   auto put_u64 = [&](uint64_t u) { double w; memcpy(&w, &u, 8); blob.push_back(w); };
-  int64_t n_slow = 0, n_boundary = 0, n_records = 0;
+  int64_t n_slow = 0, n_boundary = 0, n_records = 0, n_compact = 0;
+  std::vector<double> compact;         // 16-word (128-B) compact blobs
+  const bool dbg = getenv("GM_PIP_DEBUG") != nullptr;
+  std::vector<int64_t> dbg_hist(16 * 64, 0);
   struct RingRef { int32_t ring; bool shell; };
   std::vector<RingRef> ring_list;
   std::vector<std::vector<BandSeg>> band;  // per ring of the polygon, segments meeting the row band
@@ -815,6 +914,47 @@ int gm_pip_index_create_ex(gm_ctx* ctx, const gm_polyset* ps, int cells_per_poly
           }
         }
         run_loc = -1;
+        // ---- compact blob: single-ring polygon, <= 2 segments, <= 4 breakpoints -> one 128-B line
+        if (nr == 1 && !degenerate) {
+          a_edges.clear(); right.clear(); bk.clear();
+          for (const BandSeg& sg : band[0]) {
+            if (sg.maxx >= xb0 && sg.minx <= xb1) a_edges.push_back(sg.seg);
+            else if (sg.minx > xb1) right.push_back(&sg);
+          }
+          collect_breakpoints(right, yb0, yb1, bk);
+          if (dbg) dbg_hist[std::min<size_t>(a_edges.size(), 15) * 64 + std::min<size_t>(bk.size(), 63)]++;
+          if (4 * a_edges.size() + bk.size() <= 30) {
+            const int E = (int)a_edges.size(), B = (int)bk.size();
+            const int lines = (4 * E + B <= 14 && E <= 3) ? 1 : 2;
+            const uint64_t ci = compact.size() / 16;
+            if (ci + lines >= (1u << 29)) { gm::set_error("gm_pip_index_create: too many compact blobs"); return GM_E_CAPACITY; }
+            double rec[32];
+            for (double& w : rec) w = INFINITY;
+            { int32_t v[2] = {p, E | (lines << 8)}; memcpy(&rec[0], v, 8); }
+            { const uint64_t par = right_parity(right, yb0, bk); memcpy(&rec[1], &par, 8); }
+            bool used[32] = {};
+            used[0] = used[1] = true;
+            for (int j = 0; j < E; ++j) {
+              const int32_t i = a_edges[j];
+              double* eg = rec + cseg_word(j);
+              eg[0] = vx[i]; eg[1] = vy[i]; eg[2] = vx[i - 1]; eg[3] = vy[i - 1];
+              for (int q = 0; q < 4; ++q) used[cseg_word(j) + q] = true;
+            }
+            int w = 2;
+            for (int j = 0; j < B; ++j) {
+              while (used[w]) ++w;
+              rec[w] = bk[j].first;
+              used[w] = true;
+            }
+            if (w >= 16 * lines) { gm::set_error("gm_pip_index_create: compact layout"); return GM_E_INVALID; }
+            compact.insert(compact.end(), rec, rec + 16 * lines);
+            n_boundary++;
+            n_compact++;
+            ents.push_back(Ent{cell, (CELL_BOUNDARY << 30) | BLOB_COMPACT | (uint32_t)ci});
+            per_cell[cell]++;
+            continue;
+          }
+        }
         // ---- boundary blob
         if (blob.size() & 1) blob.push_back(0.0);
         const uint64_t boff = blob.size() / 2;
@@ -826,18 +966,7 @@ int gm_pip_index_create_ex(gm_ctx* ctx, const gm_polyset* ps, int cells_per_poly
             if (sg.maxx >= xb0 && sg.minx <= xb1) a_edges.push_back(sg.seg);
             else if (sg.minx > xb1) right.push_back(&sg);
           }
-          // breakpoints: right-segment end-point y values inside (yb0, yb1], ascending, unique
-          for (const BandSeg* sg : right) {
-            if (sg->ymin > yb0 && sg->ymin <= yb1) bk.push_back({sg->ymin, sg->vmin});
-            if (sg->ymax > yb0 && sg->ymax <= yb1) bk.push_back({sg->ymax, sg->vmax});
-          }
-          std::sort(bk.begin(), bk.end(),
-                    [](const std::pair<double, int32_t>& x, const std::pair<double, int32_t>& y) { return x.first < y.first; });
-          bk.erase(std::unique(bk.begin(), bk.end(),
-                               [](const std::pair<double, int32_t>& x, const std::pair<double, int32_t>& y) {
-                                 return x.first == y.first;
-                               }),
-                   bk.end());
+          collect_breakpoints(right, yb0, yb1, bk);
           const int r = ring_list[k].ring;
           const bool slow = degenerate || a_edges.size() > 4096 || bk.size() > 63;
           RingHdr rh{};
@@ -847,13 +976,7 @@ int gm_pip_index_create_ex(gm_ctx* ctx, const gm_polyset* ps, int cells_per_poly
           { double w; memcpy(&w, &rh, 8); blob.push_back(w); }
           uint64_t parity = 0;
           if (!slow) {
-            // parity of right segments straddling y (ymin <= y < ymax) at each interval's left end
-            for (size_t j = 0; j <= bk.size(); ++j) {
-              const double yk = j == 0 ? yb0 : bk[j - 1].first;
-              int c = 0;
-              for (const BandSeg* sg : right) c += (sg->ymin <= yk && yk < sg->ymax);
-              if (c & 1) parity |= 1ull << j;
-            }
+            parity = right_parity(right, yb0, bk);
           } else {
             n_slow++;
             parity = (uint32_t)r;
@@ -873,10 +996,15 @@ int gm_pip_index_create_ex(gm_ctx* ctx, const gm_polyset* ps, int cells_per_poly
       }
     }
   }
+  if (dbg) {
+    fprintf(stderr, "[gm_pip] one-ring boundary cells by (segments, breakpoints):\n");
+    for (int e = 0; e < 16; ++e)
+      for (int b = 0; b < 64; ++b)
+        if (dbg_hist[e * 64 + b]) fprintf(stderr, "  E=%d B=%d: %lld\n", e, b, (long long)dbg_hist[e * 64 + b]);
+  }
   if (blob.empty()) blob.push_back(0.0);
   // ---- cell words: single entries inline, multi-entry cells through a list (polygons ascending)
   std::vector<uint32_t> cell_word((size_t)ncell, 0xffffffffu);
-  std::vector<int32_t> list_off(1, 0);
   std::vector<uint32_t> list_ent;
   {
     std::vector<int32_t> start((size_t)ncell + 1, 0);
@@ -888,13 +1016,18 @@ int gm_pip_index_create_ex(gm_ctx* ctx, const gm_polyset* ps, int cells_per_poly
       const int k = per_cell[c];
       if (k == 1) cell_word[c] = all[start[c]];
       else if (k > 1) {
-        cell_word[c] = (CELL_LIST << 30) | (uint32_t)(list_off.size() - 1);
+        // payload = (list offset / 4) << 4 | count (15 = long list: true count in the first slot);
+        // lists start 16-B aligned so one uint4 load brings the first four slots
+        while (list_ent.size() & 3) list_ent.push_back(0);
+        const size_t off = list_ent.size() / 4;
+        if (off + k + 1 >= ((size_t)1 << 26)) { gm::set_error("gm_pip_index_create: cell lists too large"); return GM_E_CAPACITY; }
+        cell_word[c] = (CELL_LIST << 30) | (uint32_t)(off << 4) | (uint32_t)std::min(k, LIST_LONG);
+        if (k >= LIST_LONG) list_ent.push_back((uint32_t)k);
         for (int j = 0; j < k; ++j) list_ent.push_back(all[start[c] + j]);
-        list_off.push_back((int32_t)list_ent.size());
       }
     }
   }
-  if (list_ent.empty()) list_ent.push_back(0);
+  while (list_ent.size() < 4 || (list_ent.size() & 3)) list_ent.push_back(0);
   // coarse words: EMPTY when every fine cell is empty, the fine word when all fine cells carry the
   // same INTERIOR word, otherwise CELL_LIST ("read the fine word")
   const int gxc = (gx + (1 << CF_LOG) - 1) >> CF_LOG, gyc = (gy + (1 << CF_LOG) - 1) >> CF_LOG;
@@ -921,8 +1054,9 @@ int gm_pip_index_create_ex(gm_ctx* ctx, const gm_polyset* ps, int cells_per_poly
   ix->n_boundary = n_boundary;
   ix->n_records = n_records;
   ix->n_slow = n_slow;
+  ix->n_compact = n_compact;
   ix->n_cells = ncell;
-  ix->blob_bytes = (int64_t)blob.size() * 8;
+  ix->blob_bytes = (int64_t)(blob.size() + compact.size()) * 8;
   int rc = GM_OK;
   GM_HIP(hipSetDevice(ctx->device));
   if (!rc) rc = upload(ix, rings, &ix->dev.rings);
@@ -930,7 +1064,8 @@ int gm_pip_index_create_ex(gm_ctx* ctx, const gm_polyset* ps, int cells_per_poly
   if (!rc) rc = upload(ix, slab_edges, &ix->dev.slab_edges);
   if (!rc) rc = upload(ix, cell_word, &ix->dev.cell_word);
   if (!rc) rc = upload(ix, coarse_word, &ix->dev.coarse_word);
-  if (!rc) rc = upload(ix, list_off, &ix->dev.list_off);
+  if (compact.empty()) compact.assign(16, 0.0);
+  if (!rc) rc = upload(ix, compact, &ix->dev.compact);
   if (!rc) rc = upload(ix, list_ent, &ix->dev.list_ent);
   if (!rc) rc = upload(ix, blob, &ix->dev.blob);
   if (rc) { gm_pip_index_destroy(ix); return rc; }
@@ -956,6 +1091,7 @@ int gm_pip_index_stats(const gm_pip_index* ix, int64_t* stats) {
   stats[3] = ix->n_records;
   stats[4] = ix->n_slow;
   stats[5] = ix->blob_bytes;
+  stats[6] = ix->n_compact;
   return GM_OK;
 }
 

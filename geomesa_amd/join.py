@@ -104,11 +104,12 @@ class PolygonIndex:
                                                   ctypes.byref(self._h)), "gm_pip_index_create_ex")
 
     def stats(self):
-        """(cells, (cell, polygon) entries, boundary entries, ring records, slow-walk records)."""
+        """Index statistics: cells, (cell, polygon) entries, boundary entries, ring records,
+        slow-walk records, blob bytes, compact blobs."""
         import numpy as np
-        st = np.zeros(6, np.int64)
+        st = np.zeros(7, np.int64)
         check(self.ctx.lib.gm_pip_index_stats(self._h, st.ctypes.data), "gm_pip_index_stats")
-        return dict(zip(["cells", "entries", "boundary", "records", "slow", "blob_bytes"], st.tolist()))
+        return dict(zip(["cells", "entries", "boundary", "records", "slow", "blob_bytes", "compact"], st.tolist()))
 
     MODES = {"auto": _lib.GM_JOIN_AUTO, "direct": _lib.GM_JOIN_DIRECT, "partitioned": _lib.GM_JOIN_PARTITIONED}
 

@@ -204,8 +204,8 @@ int gm_pip_index_create(gm_ctx* ctx, const gm_polyset* polys, gm_pip_index** out
    envelope (0 = default 2048; a coarse 4x4-cell table in front of it stays L2-resident) */
 int gm_pip_index_create_ex(gm_ctx* ctx, const gm_polyset* polys, int cells_per_poly, gm_pip_index** out);
 int gm_pip_index_destroy(gm_pip_index* index);
-/* index statistics: stats[0..5] = cells, (cell, polygon) entries, boundary entries, ring records,
-   ring records that fall back to the slab walk, boundary blob bytes */
+/* index statistics: stats[0..6] = cells, (cell, polygon) entries, boundary entries, ring records,
+   ring records that fall back to the slab walk, boundary blob bytes, compact (one-line) blobs */
 int gm_pip_index_stats(const gm_pip_index* index, int64_t* stats);
 
 /* ST_Contains(polygon, point) = JTS Geometry.contains (geomesa-spark-jts/.../udf/

@@ -12,7 +12,11 @@ groups=(
   "TCC_HIT_sum TCC_MISS_sum"
   "FETCH_SIZE"
   "WRITE_SIZE"
+  "SQ_INST_LEVEL_VMEM SQ_INSTS_VMEM SQ_INST_LEVEL_LDS SQ_INSTS_SMEM"
+  "SQ_INST_LEVEL_SMEM SQ_WAIT_INST_LDS SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64"
 )
+# PMC_GROUPS="A B;C D" overrides the default passes
+if [ -n "$PMC_GROUPS" ]; then IFS=";" read -ra groups <<< "$PMC_GROUPS"; fi
 i=0
 for g in "${groups[@]}"; do
   timeout -k 10 240 rocprofv3 --kernel-trace --output-format csv --pmc $g -d "$out/p$i" -o run -- "$@" > "$out/p$i.log" 2>&1
