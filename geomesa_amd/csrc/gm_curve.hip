@@ -321,11 +321,25 @@ __global__ __launch_bounds__(TPB) void k_binned_time(const int64_t* __restrict__
 __device__ __forceinline__ double clampd(double v, double lo, double hi) { return v < lo ? lo : (v > hi ? hi : v); }
 __device__ __forceinline__ double jmax(double a, double b) { return a >= b ? a : b; }  // operands never NaN/-0 here
 
-// (4^g - 1) / 3 and (8^g - 1) / 7 computed exactly in integers (math.pow(4|8, n).toLong is exact
-// for these n); the per-level steps follow from s_{i+1} = (s_i - 1) / base.
-__device__ __forceinline__ int64_t geom_sum(int base_log2, int g) {
-  int64_t p = (int64_t)1 << (base_log2 * g);
-  return (p - 1) / (base_log2 == 2 ? 3 : 7);
+// The XZ sequence code without the per-level FP loop.  XZ2SFC.sequenceCode (XZ2SFC.scala:264-286)
+// halves [x0, x1] `length` times and compares the normalized minimum with the exact dyadic centre:
+// at level i the cell is [k 2^-i, (k + 1) 2^-i) and `v < centre` is bit i+1 of v's binary
+// expansion, so the `length` answers are the leading bits of floor(v 2^length) (v = 1.0 takes the
+// upper half every time: 2^length - 1).  With q_i = x_i + 2 y_i (+ 4 z_i) the code is
+//   cs = sum_{i<L} (1 + q_i (B^(g-i) - 1) / (B - 1)),  B = 4 (8)
+//      = L + (interleave(x, y[, z]) B^(g-L+1) - sum_i q_i) / (B - 1),
+// the interleave being exactly the Z2 / Z3 bit spread.  Integer-only and exact.
+__device__ __forceinline__ uint32_t xz_cell(double v, int L) {
+  const double s = floor(__dmul_rn(v, ldexp(1.0, L)));   // exact: power-of-two scaling
+  const uint32_t m = (1u << L) - 1u;                      // L <= 30
+  const uint32_t c = (uint32_t)s;                         // v in [0, 1] -> s in [0, 2^L]
+  return c > m ? m : c;
+}
+
+// the `length` predicate (XZ2SFC.scala:66-74): mx <= floor(mn / w2) * w2 + 2 * w2 with w2 = 2^-(l1+1).
+// Dividing by a power of two is exact, so mn * 2^(l1+1) gives the identical double.
+__device__ __forceinline__ bool xz_fits(double mn, double mx, double w2, double inv_w2) {
+  return mx <= __dadd_rn(__dmul_rn(floor(__dmul_rn(mn, inv_w2)), w2), __dmul_rn(2.0, w2));
 }
 
 // XZ2SFC.index (z3/curve/XZ2SFC.scala:54-77) with normalize (:318-350), sequenceCode (:264-286)
@@ -347,23 +361,14 @@ __device__ __forceinline__ uint8_t xz2_one(int g, double xmin, double ymin, doub
   if (l1 >= g) {
     length = g;
   } else {
-    const double w2 = ldexp(1.0, -(l1 + 1));  // math.pow(0.5, l1 + 1), exact
-    auto pred = [w2](double mn, double mx) {
-      return mx <= __dadd_rn(__dmul_rn(floor(__ddiv_rn(mn, w2)), w2), __dmul_rn(2.0, w2));
-    };
-    length = (pred(nxmin, nxmax) && pred(nymin, nymax)) ? l1 + 1 : l1;
+    const double w2 = ldexp(1.0, -(l1 + 1)), inv = ldexp(1.0, l1 + 1);   // math.pow(0.5, l1 + 1), exact
+    length = (xz_fits(nxmin, nxmax, w2, inv) && xz_fits(nymin, nymax, w2, inv)) ? l1 + 1 : l1;
   }
-  double x0 = 0.0, y0 = 0.0, x1 = 1.0, y1 = 1.0;
-  int64_t cs = 0, step = geom_sum(2, g);
-  for (int i = 0; i < length; ++i) {
-    const double xc = __dadd_rn(x0, x1) * 0.5, yc = __dadd_rn(y0, y1) * 0.5;
-    const bool xl = nxmin < xc, yl = nymin < yc;
-    cs += 1 + (int64_t)((xl ? 0 : 1) + (yl ? 0 : 2)) * step;
-    if (xl) x1 = xc; else x0 = xc;
-    if (yl) y1 = yc; else y0 = yc;
-    step = (step - 1) >> 2;
-  }
-  out = cs;
+  if (length == 0) { out = 0; return ST_OK; }
+  const uint32_t ix = xz_cell(nxmin, length), iy = xz_cell(nymin, length);
+  const uint64_t il = z2_split(ix) | (z2_split(iy) << 1);
+  const uint64_t num = (il << (2 * (g - length + 1))) - (uint64_t)(__popc(ix) + 2 * __popc(iy));
+  out = (int64_t)length + (int64_t)(num / 3u);
   return ST_OK;
 }
 
@@ -390,24 +395,15 @@ __device__ __forceinline__ uint8_t xz3_one(int g, double zhi, double xmin, doubl
   if (l1 >= g) {
     length = g;
   } else {
-    const double w2 = ldexp(1.0, -(l1 + 1));
-    auto pred = [w2](double mn, double mx) {
-      return mx <= __dadd_rn(__dmul_rn(floor(__ddiv_rn(mn, w2)), w2), __dmul_rn(2.0, w2));
-    };
-    length = (pred(nxmin, nxmax) && pred(nymin, nymax) && pred(nzmin, nzmax)) ? l1 + 1 : l1;
+    const double w2 = ldexp(1.0, -(l1 + 1)), inv = ldexp(1.0, l1 + 1);
+    length = (xz_fits(nxmin, nxmax, w2, inv) && xz_fits(nymin, nymax, w2, inv) && xz_fits(nzmin, nzmax, w2, inv))
+                 ? l1 + 1 : l1;
   }
-  double x0 = 0.0, y0 = 0.0, z0 = 0.0, x1 = 1.0, y1 = 1.0, z1 = 1.0;
-  int64_t cs = 0, step = geom_sum(3, g);
-  for (int i = 0; i < length; ++i) {
-    const double xc = __dadd_rn(x0, x1) * 0.5, yc = __dadd_rn(y0, y1) * 0.5, zc = __dadd_rn(z0, z1) * 0.5;
-    const bool xl = nxmin < xc, yl = nymin < yc, zl = nzmin < zc;
-    cs += 1 + (int64_t)((xl ? 0 : 1) + (yl ? 0 : 2) + (zl ? 0 : 4)) * step;
-    if (xl) x1 = xc; else x0 = xc;
-    if (yl) y1 = yc; else y0 = yc;
-    if (zl) z1 = zc; else z0 = zc;
-    step = (step - 1) >> 3;
-  }
-  out = cs;
+  if (length == 0) { out = 0; return ST_OK; }
+  const uint32_t ix = xz_cell(nxmin, length), iy = xz_cell(nymin, length), iz = xz_cell(nzmin, length);
+  const uint64_t il = z3_split(ix) | (z3_split(iy) << 1) | (z3_split(iz) << 2);
+  const uint64_t num = (il << (3 * (g - length + 1))) - (uint64_t)(__popc(ix) + 2 * __popc(iy) + 4 * __popc(iz));
+  out = (int64_t)length + (int64_t)(num / 7u);
   return ST_OK;
 }
 
@@ -440,10 +436,95 @@ __global__ __launch_bounds__(TPB) void k_xz3_index(const double* __restrict__ xm
   }
 }
 
+// 16-B form: 2 envelopes per lane per column (one dwordx4 each), UNROLL pairs in flight per lane,
+// the same coalesced layout as the Z3 key kernel; the odd last envelope goes to lane 0 of block 0.
+template <bool LENIENT, bool STATUS, int UNROLL>
+__global__ __launch_bounds__(TPB) void k_xz2_index_v(const dv2* __restrict__ xmin, const dv2* __restrict__ ymin,
+                                                     const dv2* __restrict__ xmax, const dv2* __restrict__ ymax,
+                                                     int64_t n, int g, lv2* __restrict__ out,
+                                                     uchar2* __restrict__ status, int64_t* __restrict__ err) {
+  const int64_t npairs = n >> 1;
+  const int64_t base = (int64_t)blockIdx.x * (TPB * UNROLL) + threadIdx.x;
+  dv2 a[UNROLL], b[UNROLL], c[UNROLL], d[UNROLL];
+#pragma unroll
+  for (int u = 0; u < UNROLL; ++u) {
+    const int64_t p = base + (int64_t)u * TPB;
+    if (p < npairs) {
+      a[u] = ld_stream(&xmin[p]); b[u] = ld_stream(&ymin[p]);
+      c[u] = ld_stream(&xmax[p]); d[u] = ld_stream(&ymax[p]);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < UNROLL; ++u) {
+    const int64_t p = base + (int64_t)u * TPB;
+    if (p < npairs) {
+      int64_t o0, o1;
+      const uint8_t s0 = xz2_one<LENIENT>(g, a[u].x, b[u].x, c[u].x, d[u].x, o0);
+      const uint8_t s1 = xz2_one<LENIENT>(g, a[u].y, b[u].y, c[u].y, d[u].y, o1);
+      st_stream(lv2{o0, o1}, &out[p]);
+      if (STATUS) status[p] = make_uchar2(s0, s1);
+      if (s0) report_error(err, 2 * p, s0);
+      if (s1) report_error(err, 2 * p + 1, s1);
+    }
+  }
+  if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
+    const int64_t i = n - 1;
+    int64_t o;
+    const uint8_t s = xz2_one<LENIENT>(g, ((const double*)xmin)[i], ((const double*)ymin)[i],
+                                       ((const double*)xmax)[i], ((const double*)ymax)[i], o);
+    ((int64_t*)out)[i] = o;
+    if (STATUS) ((uint8_t*)status)[i] = s;
+    if (s) report_error(err, i, s);
+  }
+}
+
+template <bool LENIENT, bool STATUS, int UNROLL>
+__global__ __launch_bounds__(TPB) void k_xz3_index_v(const dv2* __restrict__ xmin, const dv2* __restrict__ ymin,
+                                                     const dv2* __restrict__ zmin, const dv2* __restrict__ xmax,
+                                                     const dv2* __restrict__ ymax, const dv2* __restrict__ zmax,
+                                                     int64_t n, int g, double zhi, lv2* __restrict__ out,
+                                                     uchar2* __restrict__ status, int64_t* __restrict__ err) {
+  const int64_t npairs = n >> 1;
+  const int64_t base = (int64_t)blockIdx.x * (TPB * UNROLL) + threadIdx.x;
+  dv2 a[UNROLL], b[UNROLL], c[UNROLL], d[UNROLL], e[UNROLL], f[UNROLL];
+#pragma unroll
+  for (int u = 0; u < UNROLL; ++u) {
+    const int64_t p = base + (int64_t)u * TPB;
+    if (p < npairs) {
+      a[u] = ld_stream(&xmin[p]); b[u] = ld_stream(&ymin[p]); c[u] = ld_stream(&zmin[p]);
+      d[u] = ld_stream(&xmax[p]); e[u] = ld_stream(&ymax[p]); f[u] = ld_stream(&zmax[p]);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < UNROLL; ++u) {
+    const int64_t p = base + (int64_t)u * TPB;
+    if (p < npairs) {
+      int64_t o0, o1;
+      const uint8_t s0 = xz3_one<LENIENT>(g, zhi, a[u].x, b[u].x, c[u].x, d[u].x, e[u].x, f[u].x, o0);
+      const uint8_t s1 = xz3_one<LENIENT>(g, zhi, a[u].y, b[u].y, c[u].y, d[u].y, e[u].y, f[u].y, o1);
+      st_stream(lv2{o0, o1}, &out[p]);
+      if (STATUS) status[p] = make_uchar2(s0, s1);
+      if (s0) report_error(err, 2 * p, s0);
+      if (s1) report_error(err, 2 * p + 1, s1);
+    }
+  }
+  if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
+    const int64_t i = n - 1;
+    int64_t o;
+    const uint8_t s = xz3_one<LENIENT>(g, zhi, ((const double*)xmin)[i], ((const double*)ymin)[i],
+                                       ((const double*)zmin)[i], ((const double*)xmax)[i], ((const double*)ymax)[i],
+                                       ((const double*)zmax)[i], o);
+    ((int64_t*)out)[i] = o;
+    if (STATUS) ((uint8_t*)status)[i] = s;
+    if (s) report_error(err, i, s);
+  }
+}
+
 // ------------------------------------------------------------------ host-side launchers
 
 constexpr int UNROLL_KEY = 4;
 constexpr int UNROLL_INV = 4;
+constexpr int UNROLL_XZ = 2;
 
 inline unsigned stride_grid(int64_t n) {
   int64_t b = (n + TPB - 1) / TPB;
@@ -629,7 +710,20 @@ int gm_xz2_index(gm_ctx* ctx, const double* xmin, const double* ymin, const doub
   if (rc) return rc;
   const unsigned grid = stride_grid(n);
   hipStream_t s = ctx->stream;
-  if (lenient) {
+  if (aligned16(xmin) && aligned16(ymin) && aligned16(xmax) && aligned16(ymax) && aligned16(out) &&
+      (((uintptr_t)status & 1u) == 0)) {
+    const unsigned vg = grid_for((n >> 1) > 0 ? (n >> 1) : 1, (int64_t)TPB * UNROLL_XZ);
+    const dv2 *a = (const dv2*)xmin, *b = (const dv2*)ymin, *c = (const dv2*)xmax, *d = (const dv2*)ymax;
+    lv2* o = (lv2*)out;
+    uchar2* st = (uchar2*)status;
+    if (lenient) {
+      if (status) hipLaunchKernelGGL((k_xz2_index_v<true, true, UNROLL_XZ>), dim3(vg), dim3(TPB), 0, s, a, b, c, d, n, g, o, st, ctx->d_err);
+      else hipLaunchKernelGGL((k_xz2_index_v<true, false, UNROLL_XZ>), dim3(vg), dim3(TPB), 0, s, a, b, c, d, n, g, o, st, ctx->d_err);
+    } else {
+      if (status) hipLaunchKernelGGL((k_xz2_index_v<false, true, UNROLL_XZ>), dim3(vg), dim3(TPB), 0, s, a, b, c, d, n, g, o, st, ctx->d_err);
+      else hipLaunchKernelGGL((k_xz2_index_v<false, false, UNROLL_XZ>), dim3(vg), dim3(TPB), 0, s, a, b, c, d, n, g, o, st, ctx->d_err);
+    }
+  } else if (lenient) {
     if (status) hipLaunchKernelGGL((k_xz2_index<true, true>), dim3(grid), dim3(TPB), 0, s, xmin, ymin, xmax, ymax, n, g, out, status, ctx->d_err);
     else hipLaunchKernelGGL((k_xz2_index<true, false>), dim3(grid), dim3(TPB), 0, s, xmin, ymin, xmax, ymax, n, g, out, status, ctx->d_err);
   } else {
@@ -651,7 +745,21 @@ int gm_xz3_index(gm_ctx* ctx, const double* xmin, const double* ymin, const doub
   const unsigned grid = stride_grid(n);
   const double zhi = (double)max_offset(period);
   hipStream_t s = ctx->stream;
-  if (lenient) {
+  if (aligned16(xmin) && aligned16(ymin) && aligned16(zmin) && aligned16(xmax) && aligned16(ymax) &&
+      aligned16(zmax) && aligned16(out) && (((uintptr_t)status & 1u) == 0)) {
+    const unsigned vg = grid_for((n >> 1) > 0 ? (n >> 1) : 1, (int64_t)TPB * UNROLL_XZ);
+    const dv2 *a = (const dv2*)xmin, *b = (const dv2*)ymin, *c = (const dv2*)zmin;
+    const dv2 *d = (const dv2*)xmax, *e = (const dv2*)ymax, *f = (const dv2*)zmax;
+    lv2* o = (lv2*)out;
+    uchar2* st = (uchar2*)status;
+    if (lenient) {
+      if (status) hipLaunchKernelGGL((k_xz3_index_v<true, true, UNROLL_XZ>), dim3(vg), dim3(TPB), 0, s, a, b, c, d, e, f, n, g, zhi, o, st, ctx->d_err);
+      else hipLaunchKernelGGL((k_xz3_index_v<true, false, UNROLL_XZ>), dim3(vg), dim3(TPB), 0, s, a, b, c, d, e, f, n, g, zhi, o, st, ctx->d_err);
+    } else {
+      if (status) hipLaunchKernelGGL((k_xz3_index_v<false, true, UNROLL_XZ>), dim3(vg), dim3(TPB), 0, s, a, b, c, d, e, f, n, g, zhi, o, st, ctx->d_err);
+      else hipLaunchKernelGGL((k_xz3_index_v<false, false, UNROLL_XZ>), dim3(vg), dim3(TPB), 0, s, a, b, c, d, e, f, n, g, zhi, o, st, ctx->d_err);
+    }
+  } else if (lenient) {
     if (status) hipLaunchKernelGGL((k_xz3_index<true, true>), dim3(grid), dim3(TPB), 0, s, xmin, ymin, zmin, xmax, ymax, zmax, n, g, zhi, out, status, ctx->d_err);
     else hipLaunchKernelGGL((k_xz3_index<true, false>), dim3(grid), dim3(TPB), 0, s, xmin, ymin, zmin, xmax, ymax, zmax, n, g, zhi, out, status, ctx->d_err);
   } else {

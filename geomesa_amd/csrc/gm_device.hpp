@@ -251,7 +251,10 @@ __device__ __forceinline__ int32_t xz_l1(double maxdim) {
   } else if (__dsub_rn(1.0, f) < 0.5 * NEAR) {
     lg = log_near_pow2(e, __dsub_rn(f, 1.0));                         // exact: f - 1
   } else {
-    lg = log(maxdim);
+    // maxdim = f 2^e with |f - 0.5|, |1 - f| >= 2^-20: the quotient log(maxdim)/log(0.5) = -e - log2(f)
+    // lies in (-e, -e + 1), at least 1.4e-6 away from either integer -- far beyond the few ulps by
+    // which the JVM's rounded log and division can move it -- so its floor is exactly -e.
+    return -e;
   }
   return jvm_d2i(floor(__ddiv_rn(lg, LOG_HALF)));
 }

@@ -10,6 +10,9 @@
 //   pass B  k_scan_counts: exclusive scan of the per-block counts (single workgroup)
 //   pass C  k_mask_to_ids: expand mask bits into row ids at the scanned offsets
 // Pass C reads n/8 bytes of mask, so the ids cost ~1/80 of pass A's traffic plus 8 B per match.
+#include <string.h>
+
+#include <algorithm>
 #include <vector>
 
 #include "gm_internal.hpp"
@@ -26,6 +29,8 @@ constexpr int FROWS = FTPB * FELEMS;  // rows per block (2048) -> 64 mask words
 //   [5 .. 5+4*nxy)        xy boxes (xmin, ymin, xmax, ymax) in normalized cells
 //   then nt (start, end) interval index pairs, (-1, -1) for a null epoch
 //   then the intervals (t0, t1)
+__device__ __forceinline__ bool z3_in_bounds_time(const int32_t* f, int16_t epoch, int64_t z);
+
 // Z3Filter.pointInBounds && timeInBounds (Z3Filter.scala:31-62)
 __device__ __forceinline__ bool z3_in_bounds(const int32_t* f, int16_t epoch, int64_t z) {
   const int nxy = f[0];
@@ -37,6 +42,13 @@ __device__ __forceinline__ bool z3_in_bounds(const int32_t* f, int16_t epoch, in
     if (x >= q[0] && x <= q[2] && y >= q[1] && y <= q[3]) { pin = true; break; }
   }
   if (!pin) return false;
+  return z3_in_bounds_time(f, epoch, z);
+}
+
+// timeInBounds part of Z3Filter.inBounds (Z3Filter.scala:45-62)
+__device__ __forceinline__ bool z3_in_bounds_time(const int32_t* f, int16_t epoch, int64_t z) {
+  const int nxy = f[0];
+  const int32_t* xy = f + 5;
   const int min_e = f[1], max_e = f[2];
   if (epoch > max_e || epoch < min_e) return true;   // whole epochs are left out (:46-47)
   const int nt = f[3];
@@ -164,6 +176,197 @@ __global__ __launch_bounds__(FTPB) void k_strict_mask(const double* __restrict__
   block_count(local, block_counts);
 }
 
+// ------------------------------------------------------------------ vectorised pass A
+// The kernels above move 2 B (bin) and 8 B (z) per lane per load instruction; on gfx950 narrow
+// per-lane accesses stream at roughly half the 16-B rate.  The _v variants use the layout of the
+// encode kernels: each lane takes PAIRS of consecutive rows, one 16-B load per 8-byte column
+// (z, x, y, t) and one 4-B load of the two bins, and pair p of lane l in step u sits at
+// block_base + u*256 + l, so every wave instruction reads one contiguous 1 KiB run.  A wave step
+// covers 128 rows: ballot(row 2l) and ballot(row 2l+1) interleave bit by bit into the two 64-bit
+// mask words of those rows.  A block still covers FROWS = 2048 rows (4 steps), so block_counts,
+// k_scan_counts and k_mask_to_ids are shared with the scalar kernels.
+typedef short sv2 __attribute__((ext_vector_type(2)));
+constexpr int FPAIRS = FELEMS / 2;   // pair steps per lane
+
+// 32 -> 64-bit bit spread (bit k -> bit 2k)
+__device__ __forceinline__ uint64_t spread2_32(uint32_t v) {
+  return (uint64_t)spread2_16(v & 0xffffu) | ((uint64_t)spread2_16(v >> 16) << 32);
+}
+
+// the wave's two mask words from the even-row and odd-row ballots; lanes 0 and 1 store one each
+__device__ __forceinline__ void put_pair_words(uint64_t even, uint64_t odd, uint64_t* __restrict__ mask, int64_t word,
+                                               int64_t nwords) {
+  const int lane = threadIdx.x & 63;
+  if (lane < 2) {
+    const uint32_t e = (uint32_t)(lane ? (even >> 32) : even), o = (uint32_t)(lane ? (odd >> 32) : odd);
+    if (word + lane < nwords) mask[word + lane] = spread2_32(e) | (spread2_32(o) << 1);
+  }
+}
+
+__device__ __forceinline__ void block_count_waves(int wave_cnt, int32_t* block_counts) {
+  __shared__ int s_wc[FTPB / 64];
+  if ((threadIdx.x & 63) == 0) s_wc[threadIdx.x >> 6] = wave_cnt;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int s = 0;
+#pragma unroll
+    for (int i = 0; i < FTPB / 64; ++i) s += s_wc[i];
+    block_counts[blockIdx.x] = s;
+  }
+}
+
+// Row predicate over a pair layout: LOAD(p, u) stages pair p, ROW(u, j) evaluates row j (0/1) of the
+// staged pair, TAIL(u) evaluates the odd last row n-1 (pair index n/2) with scalar loads.
+template <class Load, class Row, class Tail>
+__device__ __forceinline__ void pair_scan(int64_t n, uint64_t* __restrict__ mask, int32_t* __restrict__ block_counts,
+                                          Load load, Row row, Tail tail) {
+  const int64_t npairs = n >> 1, nwords = (n + 63) >> 6;
+  const int wave = threadIdx.x >> 6;
+  const int64_t pbase = (int64_t)blockIdx.x * (FTPB * FPAIRS);
+#pragma unroll
+  for (int u = 0; u < FPAIRS; ++u) {
+    const int64_t p = pbase + (int64_t)u * FTPB + threadIdx.x;
+    if (p < npairs) load(p, u);
+  }
+  int cnt = 0;
+#pragma unroll
+  for (int u = 0; u < FPAIRS; ++u) {
+    const int64_t p = pbase + (int64_t)u * FTPB + threadIdx.x;
+    bool e = false, o = false;
+    if (p < npairs) { e = row(u, 0); o = row(u, 1); }
+    else if (p == npairs && (n & 1)) e = tail(p);
+    const uint64_t be = __ballot(e), bo = __ballot(o);
+    cnt += __popcll(be) + __popcll(bo);
+    put_pair_words(be, bo, mask, ((pbase + (int64_t)u * FTPB + wave * 64) * 2) >> 6, nwords);
+  }
+  block_count_waves(cnt, block_counts);
+}
+
+// Descriptor access.  Per-row reads of even wave-uniform descriptor words cost scalar loads plus
+// loop and exec-mask bookkeeping, and decoding x and y with Z3.combine costs ~60 VALU per row
+// (PMC: ~110 VALU per row, issue-bound at 45% of HBM).  The fast path (<= FBOX boxes,
+// <= FBIN bin ranges: every bbox/during query) instead keeps the boxes as DILATED bounds in
+// registers: spreading bits to every third position preserves order, so
+//     lo <= Z3.combine(z) <= hi   <=>   dilate(lo) <= (z & X_BITS) <= dilate(hi)     (unsigned)
+// (and likewise for y with the mask shifted by one).  A row then costs two ANDs and four 64-bit
+// compares per box.  Bounds outside the 21-bit dimension are clamped on the host (an empty box gets
+// lo > hi).  Only rows that pass bin + box read the per-epoch interval table (lane-varying, L1/L2).
+constexpr int FBOX = 4, FBIN = 4;
+constexpr uint64_t Z3_XBITS = 0x1249249249249249ull;   // Z3.combine's mask (Z3.scala:84)
+
+// bin_allowed && Z3Filter.inBounds with dilated boxes and bin ranges in registers
+__device__ __forceinline__ bool z3_row_fast(const uint64_t* bx, int nxy, const int32_t* br, int nbr,
+                                            const int32_t* __restrict__ fdesc, int16_t b, int64_t z) {
+  bool ba = nbr == 0;
+#pragma unroll
+  for (int i = 0; i < FBIN; ++i) {
+    if (i >= nbr) break;
+    ba |= (b >= br[2 * i]) & (b <= br[2 * i + 1]);
+  }
+  const uint64_t xv = (uint64_t)z & Z3_XBITS, yv = (uint64_t)z & (Z3_XBITS << 1);
+  bool pin = false;
+#pragma unroll
+  for (int i = 0; i < FBOX; ++i) {
+    if (i >= nxy) break;
+    pin |= (xv >= bx[4 * i]) & (xv <= bx[4 * i + 1]) & (yv >= bx[4 * i + 2]) & (yv <= bx[4 * i + 3]);
+  }
+  if (!(ba && pin)) return false;
+  return z3_in_bounds_time(fdesc, b, z);
+}
+
+// The generic path reads the descriptor straight from global memory with wave-uniform indices.
+template <bool FAST>
+__global__ __launch_bounds__(FTPB) void k_z3filter_mask_v(const sv2* __restrict__ bin2, const lv2* __restrict__ z2,
+                                                          int64_t n, const uint64_t* __restrict__ dil,
+                                                          const int32_t* __restrict__ fdesc,
+                                                          const int32_t* __restrict__ bins, int nbr,
+                                                          uint64_t* __restrict__ mask, int32_t* __restrict__ block_counts) {
+  sv2 bv[FPAIRS];
+  lv2 zv[FPAIRS];
+  const int nxy = fdesc[0];
+  uint64_t bx[4 * FBOX];
+  int32_t br[2 * FBIN];
+#pragma unroll
+  for (int i = 0; i < 4 * FBOX; ++i) bx[i] = (FAST && i < 4 * nxy) ? dil[i] : 0;
+#pragma unroll
+  for (int i = 0; i < 2 * FBIN; ++i) br[i] = (FAST && i < 2 * nbr) ? bins[i] : 0;
+  auto pred = [&](int16_t b, int64_t z) {
+    if (FAST) return z3_row_fast(bx, nxy, br, nbr, fdesc, b, z);
+    return bin_allowed(bins, nbr, b) && z3_in_bounds(fdesc, b, z);
+  };
+  pair_scan(
+      n, mask, block_counts,
+      [&](int64_t p, int u) { bv[u] = __builtin_nontemporal_load(&bin2[p]); zv[u] = __builtin_nontemporal_load(&z2[p]); },
+      [&](int u, int j) { return j ? pred(bv[u].y, zv[u].y) : pred(bv[u].x, zv[u].x); },
+      [&](int64_t p) { return pred(((const int16_t*)bin2)[2 * p], ((const int64_t*)z2)[2 * p]); });
+}
+
+__device__ __forceinline__ bool z2_in_xy(const int32_t* __restrict__ xy, int nxy, int64_t zz) {
+  const int32_t x = z2_combine(zz), y = z2_combine(zz >> 1);
+  for (int k = 0; k < nxy; ++k) {
+    const int32_t* q = xy + 4 * k;
+    if (x >= q[0] && x <= q[2] && y >= q[1] && y <= q[3]) return true;
+  }
+  return false;
+}
+
+// Z2: Z2.combine yields 32 bits (z bit 62 -> x bit 31, the sign bit of z -> y bit 31) compared as
+// signed Ints, so the dilated form flips the dimension's top bit (signed -> unsigned order) on both
+// sides: lo <= x  <=>  dilate(lo ^ 2^31) <= (z & X_BITS) ^ top.
+constexpr uint64_t Z2_XBITS = 0x5555555555555555ull;
+
+template <bool FAST>
+__global__ __launch_bounds__(FTPB) void k_z2filter_mask_v(const lv2* __restrict__ z2, int64_t n,
+                                                          const uint64_t* __restrict__ dil,
+                                                          const int32_t* __restrict__ xy, int nxy,
+                                                          uint64_t* __restrict__ mask, int32_t* __restrict__ block_counts) {
+  lv2 zv[FPAIRS];
+  uint64_t bx[4 * FBOX];
+#pragma unroll
+  for (int i = 0; i < 4 * FBOX; ++i) bx[i] = (FAST && i < 4 * nxy) ? dil[i] : 0;
+  auto pred = [&](int64_t zz) {
+    if (!FAST) return z2_in_xy(xy, nxy, zz);
+    const uint64_t xv = ((uint64_t)zz & Z2_XBITS) ^ (1ull << 62), yv = ((uint64_t)zz & (Z2_XBITS << 1)) ^ (1ull << 63);
+    bool pin = false;
+#pragma unroll
+    for (int i = 0; i < FBOX; ++i) {
+      if (i >= nxy) break;
+      pin |= (xv >= bx[4 * i]) & (xv <= bx[4 * i + 1]) & (yv >= bx[4 * i + 2]) & (yv <= bx[4 * i + 3]);
+    }
+    return pin;
+  };
+  pair_scan(
+      n, mask, block_counts, [&](int64_t p, int u) { zv[u] = __builtin_nontemporal_load(&z2[p]); },
+      [&](int u, int j) { return pred(j ? zv[u].y : zv[u].x); },
+      [&](int64_t p) { return pred(((const int64_t*)z2)[2 * p]); });
+}
+
+template <bool DURING>
+__global__ __launch_bounds__(FTPB) void k_strict_mask_v(const dv2* __restrict__ x, const dv2* __restrict__ y,
+                                                        const lv2* __restrict__ t, int64_t n, double bx0, double by0,
+                                                        double bx1, double by1, int64_t lo, int64_t hi,
+                                                        uint64_t* __restrict__ mask, int32_t* __restrict__ block_counts) {
+  auto pred = [&](double px, double py, int64_t tt) {
+    bool ok = px >= bx0 && px <= bx1 && py >= by0 && py <= by1;
+    if (DURING) ok = ok && tt > lo && tt < hi;
+    return ok;
+  };
+  dv2 xv[FPAIRS], yv[FPAIRS];
+  lv2 tv[FPAIRS];
+  pair_scan(
+      n, mask, block_counts,
+      [&](int64_t p, int u) {
+        xv[u] = __builtin_nontemporal_load(&x[p]);
+        yv[u] = __builtin_nontemporal_load(&y[p]);
+        if (DURING) tv[u] = __builtin_nontemporal_load(&t[p]);
+        else tv[u] = lv2{0, 0};
+      },
+      [&](int u, int j) { return j ? pred(xv[u].y, yv[u].y, tv[u].y) : pred(xv[u].x, yv[u].x, tv[u].x); },
+      [&](int64_t p) {
+        return pred(((const double*)x)[2 * p], ((const double*)y)[2 * p], DURING ? ((const int64_t*)t)[2 * p] : 0);
+      });
+}
+
 // pass B: exclusive scan of block counts by one workgroup of 1024 threads; total -> out[nb]
 __global__ __launch_bounds__(1024) void k_scan_counts(const int32_t* __restrict__ counts, int64_t nb,
                                                       int64_t* __restrict__ offsets) {
@@ -227,6 +430,40 @@ static inline int32_t be32(const uint8_t* p) {
   return (int32_t)((uint32_t)p[0] << 24 | (uint32_t)p[1] << 16 | (uint32_t)p[2] << 8 | (uint32_t)p[3]);
 }
 static inline int16_t be16(const uint8_t* p) { return (int16_t)(uint16_t)((uint16_t)p[0] << 8 | p[1]); }
+
+// bit spread with `stride` (2 or 3), the host mirror of Z2.split / Z3.split without masking
+static uint64_t dilate(uint64_t v, int bits, int stride) {
+  uint64_t o = 0;
+  for (int i = 0; i < bits; ++i) o |= ((v >> i) & 1ull) << (stride * i);
+  return o;
+}
+
+// Z3 boxes (xmin, ymin, xmax, ymax) as dilated (xlo, xhi, ylo, yhi); dims are 21-bit, non-negative
+static void z3_dilated_boxes(const int32_t* xy, int nxy, std::vector<uint64_t>& out) {
+  out.clear();
+  const int64_t top = (1 << 21) - 1;
+  for (int i = 0; i < nxy; ++i) {
+    for (int d = 0; d < 2; ++d) {
+      const int64_t lo = std::max<int64_t>(xy[4 * i + d], 0), hi = std::min<int64_t>(xy[4 * i + 2 + d], top);
+      if (lo > hi || lo > top || hi < 0) { out.push_back(1ull << 63); out.push_back(0); continue; }   // empty
+      out.push_back(dilate((uint64_t)lo, 21, 3) << d);
+      out.push_back(dilate((uint64_t)hi, 21, 3) << d);
+    }
+  }
+}
+
+// Z2 boxes: signed 32-bit dims, top bit flipped into unsigned order
+static void z2_dilated_boxes(const int32_t* xy, int nxy, std::vector<uint64_t>& out) {
+  out.clear();
+  for (int i = 0; i < nxy; ++i) {
+    for (int d = 0; d < 2; ++d) {
+      const int32_t lo = xy[4 * i + d], hi = xy[4 * i + 2 + d];
+      if (lo > hi) { out.push_back(~0ull); out.push_back(0); continue; }   // empty
+      out.push_back(dilate((uint32_t)lo ^ 0x80000000u, 32, 2) << d);
+      out.push_back(dilate((uint32_t)hi ^ 0x80000000u, 32, 2) << d);
+    }
+  }
+}
 
 // Z3Filter.deserializeFromBytes (Z3Filter.scala:139-153) -> flat descriptor
 static bool build_z3_desc(const uint8_t* b, size_t len, std::vector<int32_t>& d) {
@@ -333,15 +570,31 @@ int gm_z3filter_scan(gm_ctx* ctx, const uint8_t* filter_bytes, size_t filter_len
   if (!bin || !z) return GM_E_INVALID;
   const int fwords = (int)desc.size();
   for (int i = 0; i < n_bin_ranges; ++i) { desc.push_back(bin_ranges[2 * i]); desc.push_back(bin_ranges[2 * i + 1]); }
+  // device layout: [dilated boxes u64 x 4 nxy][descriptor][bin ranges]
+  std::vector<uint64_t> dil;
+  z3_dilated_boxes(desc.data() + 5, desc[0], dil);
+  std::vector<int32_t> buf(2 * dil.size() + desc.size());
+  if (!dil.empty()) memcpy(buf.data(), dil.data(), dil.size() * 8);
+  memcpy(buf.data() + 2 * dil.size(), desc.data(), desc.size() * 4);
   ScanBufs b;
-  int rc = alloc_scan(ctx, n, mask, desc.size(), b);
+  int rc = alloc_scan(ctx, n, mask, buf.size(), b);
   if (rc) return rc;
-  GM_HIP(hipMemcpyAsync(b.desc, desc.data(), desc.size() * 4, hipMemcpyHostToDevice, ctx->stream));
-  GM_HIP(hipStreamSynchronize(ctx->stream));  // desc is pageable host memory
+  GM_HIP(hipMemcpyAsync(b.desc, buf.data(), buf.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+  GM_HIP(hipStreamSynchronize(ctx->stream));  // buf is pageable host memory
+  const uint64_t* d_dil = (const uint64_t*)b.desc;
+  const int32_t* d_desc = b.desc + 2 * dil.size();
   const int64_t nblocks = (n + FROWS - 1) / FROWS;
   const size_t lds = desc.size() * 4;
-  hipLaunchKernelGGL(k_z3filter_mask, dim3((unsigned)nblocks), dim3(FTPB), lds, ctx->stream, bin, z, n, b.desc, fwords,
-                     b.desc + fwords, n_bin_ranges, b.mask, b.counts);
+  const bool fast = desc[0] <= FBOX && n_bin_ranges <= FBIN;
+  if (aligned16(bin) && aligned16(z) && fast)
+    hipLaunchKernelGGL(k_z3filter_mask_v<true>, dim3((unsigned)nblocks), dim3(FTPB), 0, ctx->stream, (const sv2*)bin,
+                       (const lv2*)z, n, d_dil, d_desc, d_desc + fwords, n_bin_ranges, b.mask, b.counts);
+  else if (aligned16(bin) && aligned16(z))
+    hipLaunchKernelGGL(k_z3filter_mask_v<false>, dim3((unsigned)nblocks), dim3(FTPB), 0, ctx->stream, (const sv2*)bin,
+                       (const lv2*)z, n, d_dil, d_desc, d_desc + fwords, n_bin_ranges, b.mask, b.counts);
+  else
+    hipLaunchKernelGGL(k_z3filter_mask, dim3((unsigned)nblocks), dim3(FTPB), lds, ctx->stream, bin, z, n, d_desc,
+                       fwords, d_desc + fwords, n_bin_ranges, b.mask, b.counts);
   GM_CHECK_LAUNCH();
   rc = finish_scan(ctx, n, b, ids, ids_cap, n_match);
   free_scan(ctx, mask, b);
@@ -362,14 +615,29 @@ int gm_z2filter_scan(gm_ctx* ctx, const uint8_t* filter_bytes, size_t filter_len
   if (!z) return GM_E_INVALID;
   std::vector<int32_t> xy((size_t)nxy * 4);
   for (size_t i = 0; i < xy.size(); ++i) xy[i] = be32(filter_bytes + 4 + 4 * i);
+  // device layout: [dilated boxes u64 x 4 nxy][boxes int32 x 4 nxy]
+  std::vector<uint64_t> dil;
+  z2_dilated_boxes(xy.data(), nxy, dil);
+  std::vector<int32_t> buf(2 * dil.size() + xy.size() + 1);
+  if (!dil.empty()) memcpy(buf.data(), dil.data(), dil.size() * 8);
+  if (!xy.empty()) memcpy(buf.data() + 2 * dil.size(), xy.data(), xy.size() * 4);
   ScanBufs b;
-  int rc = alloc_scan(ctx, n, mask, xy.size() + 1, b);
+  int rc = alloc_scan(ctx, n, mask, buf.size(), b);
   if (rc) return rc;
-  if (!xy.empty()) GM_HIP(hipMemcpyAsync(b.desc, xy.data(), xy.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+  GM_HIP(hipMemcpyAsync(b.desc, buf.data(), buf.size() * 4, hipMemcpyHostToDevice, ctx->stream));
   GM_HIP(hipStreamSynchronize(ctx->stream));
+  const uint64_t* d_dil = (const uint64_t*)b.desc;
+  const int32_t* d_xy = b.desc + 2 * dil.size();
   const int64_t nblocks = (n + FROWS - 1) / FROWS;
-  hipLaunchKernelGGL(k_z2filter_mask, dim3((unsigned)nblocks), dim3(FTPB), xy.size() * 4 + 4, ctx->stream, z, n,
-                     b.desc, nxy, b.mask, b.counts);
+  if (aligned16(z) && nxy <= FBOX)
+    hipLaunchKernelGGL(k_z2filter_mask_v<true>, dim3((unsigned)nblocks), dim3(FTPB), 0, ctx->stream, (const lv2*)z, n,
+                       d_dil, d_xy, nxy, b.mask, b.counts);
+  else if (aligned16(z))
+    hipLaunchKernelGGL(k_z2filter_mask_v<false>, dim3((unsigned)nblocks), dim3(FTPB), 0, ctx->stream, (const lv2*)z, n,
+                       d_dil, d_xy, nxy, b.mask, b.counts);
+  else
+    hipLaunchKernelGGL(k_z2filter_mask, dim3((unsigned)nblocks), dim3(FTPB), xy.size() * 4 + 4, ctx->stream, z, n,
+                       d_xy, nxy, b.mask, b.counts);
   GM_CHECK_LAUNCH();
   rc = finish_scan(ctx, n, b, ids, ids_cap, n_match);
   free_scan(ctx, mask, b);
@@ -388,7 +656,18 @@ int gm_strict_scan(gm_ctx* ctx, const double* x, const double* y, const int64_t*
   int rc = alloc_scan(ctx, n, mask, 0, b);
   if (rc) return rc;
   const int64_t nblocks = (n + FROWS - 1) / FROWS;
-  if (has_during)
+  if (aligned16(x) && aligned16(y) && (!has_during || aligned16(t_ms))) {
+    const dv2* x2 = (const dv2*)x;
+    const dv2* y2 = (const dv2*)y;
+    const lv2* t2 = (const lv2*)t_ms;
+    uint64_t* m8 = b.mask;
+    if (has_during)
+      hipLaunchKernelGGL((k_strict_mask_v<true>), dim3((unsigned)nblocks), dim3(FTPB), 0, ctx->stream, x2, y2, t2, n,
+                         bbox[0], bbox[1], bbox[2], bbox[3], lo, hi, m8, b.counts);
+    else
+      hipLaunchKernelGGL((k_strict_mask_v<false>), dim3((unsigned)nblocks), dim3(FTPB), 0, ctx->stream, x2, y2, t2, n,
+                         bbox[0], bbox[1], bbox[2], bbox[3], lo, hi, m8, b.counts);
+  } else if (has_during)
     hipLaunchKernelGGL((k_strict_mask<true>), dim3((unsigned)nblocks), dim3(FTPB), 0, ctx->stream, x, y, t_ms, n,
                        bbox[0], bbox[1], bbox[2], bbox[3], lo, hi, b.mask, b.counts);
   else

@@ -171,6 +171,11 @@ def test_xz2_index_parity(gpu, oracle, lenient):
     out, s = XZ2SFC(12).index(*env, lenient=lenient, status=True)
     oo, os_ = oracle.xz2_index_batch(np.stack(env, 1), lenient)
     assert np.array_equal(as_np(s), os_) and np.array_equal(as_np(out), oo)
+    # misaligned device views (one row in) take the scalar kernel
+    import torch
+    dev = [torch.from_numpy(e).cuda()[1:] for e in env]
+    out1, s1 = XZ2SFC(12).index(*dev, lenient=lenient, status=True)
+    assert np.array_equal(as_np(s1), os_[1:]) and np.array_equal(as_np(out1), oo[1:])
 
 
 @pytest.mark.parametrize("lenient", [False, True])
@@ -180,6 +185,10 @@ def test_xz3_index_parity(gpu, oracle, lenient):
     out, s = XZ3SFC(12, "week").index(*env, lenient=lenient, status=True)
     oo, os_ = oracle.xz3_index_batch(np.stack(env, 1), lenient)
     assert np.array_equal(as_np(s), os_) and np.array_equal(as_np(out), oo)
+    import torch
+    dev = [torch.from_numpy(e).cuda()[1:] for e in env]
+    out1, s1 = XZ3SFC(12, "week").index(*dev, lenient=lenient, status=True)
+    assert np.array_equal(as_np(s1), os_[1:]) and np.array_equal(as_np(out1), oo[1:])
 
 
 def test_z3_roundtrip_property_large(gpu):

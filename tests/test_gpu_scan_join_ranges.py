@@ -88,6 +88,84 @@ def test_strict_scan_parity(gpu, oracle, with_during):
     assert np.array_equal(as_np(m), om) and np.array_equal(as_np(ids), np.nonzero(om)[0])
 
 
+@pytest.mark.parametrize("n", [1, 7, 8, 63, 64, 65, 2047, 2048, 2049, 100_003])
+def test_scans_ragged_and_unaligned(gpu, oracle, n):
+    """Vectorised scans (8 rows per lane, 16-B loads) at ragged sizes, and the scalar kernels they
+    fall back to when a column is not 16-B aligned (a view starting one row in)."""
+    import torch
+    x, y, t = random_keys(n + 1, seed=n)
+    ks = Z3IndexKeySpace()
+    q = QUERIES[1]
+    v = ks.get_index_values(q[0], [q[1]])
+    f = F.Z3Filter.from_values(v)
+    fb = F.serialize_to_bytes(f)
+    br = ks.bin_ranges(v)
+    b, z = ks.sfc.index_keys(x, y, t)
+    from geomesa_amd.curve import Z2SFC
+    from geomesa_amd.keyspace import Z2IndexKeySpace
+    z2 = Z2SFC().index(x, y)
+    f2 = F.Z2Filter.from_values(Z2IndexKeySpace().get_index_values([(-10, 35, 30, 60), (100, -40, 120, -10)]))
+    dx, dy, dt = (torch.from_numpy(a).cuda() for a in (x, y, t))
+    bbox, dur = (-10, 35, 30, 60), (ms("2020-03-01T00:00:00.000Z"), ms("2020-05-08T12:00:00.000Z"))
+    for off in (0, 1):   # off = 1: misaligned views -> scalar kernels
+        sl = slice(off, off + n)
+        m, ids, k = F.scan(f, b[sl], z[sl], br, want_ids=True)
+        om = oracle.z3filter_scan(fb, br, as_np(b)[sl], as_np(z)[sl])
+        assert np.array_equal(as_np(m), om) and np.array_equal(as_np(ids), np.nonzero(om)[0]) and k == int(om.sum())
+        m, ids, k = F.z2_scan(f2, z2[sl], want_ids=True)
+        om = oracle.z2filter_scan(F.z2_serialize_to_bytes(f2), as_np(z2)[sl])
+        assert np.array_equal(as_np(m), om) and np.array_equal(as_np(ids), np.nonzero(om)[0]) and k == int(om.sum())
+        for d in (None, dur):
+            m, ids, k = F.strict_scan(dx[sl], dy[sl], dt[sl], bbox, d, want_ids=True)
+            om = oracle.strict_scan(x[sl], y[sl], t[sl], bbox, d)
+            assert np.array_equal(as_np(m), om) and np.array_equal(as_np(ids), np.nonzero(om)[0])
+
+
+ADVERSARIAL_Z3 = [
+    # boxes past the 21-bit range, negative, empty (min > max), whole-range; epochs with null, empty
+    # and multi-interval entries (Z3Filter.scala:31-62 decodes any row bytes, valid key or not)
+    F.Z3Filter([[-5, 100, 3_000_000, 2_000_000], [10, 10, 5, 5], [0, 0, 2097151, 2097151]],
+               [[[0, 1000], [500_000, 2_097_151]], None, [], [[-3, 7]]], 3, 6),
+    F.Z3Filter([[2_000_000, -1, 2_097_152, 10]], [[[5, 5]]], -1, -1),
+    F.Z3Filter([[0, 0, 0, 0], [7, 7, 7, 7]], [], 32767, -32768),
+]
+
+
+@pytest.mark.parametrize("k", range(len(ADVERSARIAL_Z3)))
+def test_filters_on_arbitrary_row_bits(gpu, oracle, k):
+    """Dilated-bound fast paths vs the oracle on arbitrary 64-bit z words (sign bit, bit 62 and 63
+    set) and int16 bins, with filter bounds outside the dimension ranges."""
+    rng = np.random.default_rng(31 + k)
+    n = 300_001
+    z = rng.integers(-2**63, 2**63 - 1, n, dtype=np.int64, endpoint=True)
+    z[:4096] &= 0x7FFFFFFF  # small coordinates: boxes near 0 hit
+    b = rng.integers(-4, 10, n).astype(np.int16)
+    f = ADVERSARIAL_Z3[k]
+    for br in ([], [(2, 4)], [(-4, -1), (3, 3), (5, 9)]):
+        m, ids, cnt = F.scan(f, b, z, br, want_ids=True)
+        om = oracle.z3filter_scan(F.serialize_to_bytes(f), br, b, z)
+        assert np.array_equal(as_np(m), om) and cnt == int(om.sum())
+    f2 = F.Z2Filter([[-2**31, -5, 2**31 - 1, 100], [10, 10, 5, 5], [0, 0, 1 << 20, 1 << 20],
+                     [-(1 << 30), -(1 << 31), -1, -1]][: k + 2])
+    m, ids, cnt = F.z2_scan(f2, z, want_ids=True)
+    om = oracle.z2filter_scan(F.z2_serialize_to_bytes(f2), z)
+    assert np.array_equal(as_np(m), om) and np.array_equal(as_np(ids), np.nonzero(om)[0])
+
+
+def test_filter_scan_many_boxes_generic_path(gpu, oracle):
+    """More than 4 boxes / bin ranges takes the generic (descriptor-walking) kernel."""
+    x, y, t = random_keys(200_003, seed=77)
+    ks = Z3IndexKeySpace()
+    b, z = ks.sfc.index_keys(x, y, t)
+    boxes = [(-170 + 30 * i, -60, -160 + 30 * i, 60) for i in range(6)]
+    v = ks.get_index_values(boxes, [during(ms("2020-02-01T00:00:00.000Z"), ms("2020-09-08T12:00:00.000Z"))])
+    f = F.Z3Filter.from_values(v)
+    br = [(2611, 2612), (2614, 2614), (2620, 2630), (2633, 2640), (2645, 2650)]
+    m, ids, n = F.scan(f, b, z, br, want_ids=True)
+    om = oracle.z3filter_scan(F.serialize_to_bytes(f), br, as_np(b), as_np(z))
+    assert np.array_equal(as_np(m), om) and np.array_equal(as_np(ids), np.nonzero(om)[0])
+
+
 def test_filter_scan_empty(gpu):
     f = F.Z3Filter([[0, 0, 10, 10]], [], 32767, -32768)
     m, ids, n = F.scan(f, np.zeros(0, np.int16), np.zeros(0, np.int64), [], want_ids=True)
