@@ -1,0 +1,90 @@
+"""Per-launch HBM traffic from rocprofv3 FETCH_SIZE / WRITE_SIZE passes -> profiles/pmc_traffic.json.
+
+usage: python tools/make_traffic.py PMC_DIR OUT_JSON [points] [join_points]
+
+FETCH_SIZE and WRITE_SIZE are in KiB per dispatch.  MI355X_MICROARCH.md (HBM section): on gfx950
+FETCH_SIZE reports exactly half of the bytes of a wide coalesced streaming read (16 B per lane), so
+it is doubled for the streaming kernels; WRITE_SIZE reads 16-B-per-lane streaming stores exactly.
+The join's gathers (index lookups) are other access widths the guide leaves uncalibrated: its
+FETCH_SIZE is reported raw and doubled side by side, and `bytes_per_launch` uses the doubled value
+(an upper bound for the gathers, exact for the streaming record reads).
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+# bench name -> (kernel-name substring, unit count per launch key, algorithmic bytes per unit)
+STREAMING = {
+    "z3_index_key": ("k_z3_index_key<", "points", 34.0),
+    "z3_invert": ("k_z3_invert<", "points", 32.0),
+    "z2_index": ("k_z2_index<", "points", 24.0),
+    "z2_invert": ("k_z2_invert<", "points", 24.0),
+    "z3filter_scan": ("k_z3filter_mask_v", "points", 10.125),
+    "xz2_index": ("k_xz2_index_v", "xz", 40.0),
+}
+# join step kernels and the points per dispatch: direct = one pass per 2^31 points, partitioned =
+# hist + scan + scatter + join per 2^28-point chunk
+JOIN_MODES = {"direct": (["k_pip_join<true, false>"], 1 << 31),
+              "partitioned": (["k_band_hist", "k_band_scan", "k_band_scatter", "k_pip_join<true, true>"], 1 << 28)}
+
+
+def per_dispatch(root):
+    """kernel name -> counter -> list of per-dispatch values (summed over the counter's instances)."""
+    acc = defaultdict(lambda: defaultdict(float))
+    names = {}
+    for f in sorted(glob.glob(os.path.join(root, "p*", "*counter_collection.csv"))):
+        for r in csv.DictReader(open(f)):
+            key = (f, r["Dispatch_Id"])
+            names[key] = r["Kernel_Name"]
+            acc[key][r["Counter_Name"]] += float(r["Counter_Value"])
+    out = defaultdict(lambda: defaultdict(list))
+    for key, cs in acc.items():
+        for c, v in cs.items():
+            out[names[key]][c].append(v)
+    return out
+
+
+def mean_for(d, sub, counter):
+    vals = [v for k, cs in d.items() if sub in k for v in cs.get(counter, [])]
+    return sum(vals) / len(vals) if vals else None
+
+
+def main(root, out, points=1_000_000_000, join_points=1_000_000_000):
+    d = per_dispatch(root)
+    res = {}
+    for name, (sub, unit, alg) in STREAMING.items():
+        f, w = mean_for(d, sub, "FETCH_SIZE"), mean_for(d, sub, "WRITE_SIZE")
+        if f is None or w is None:
+            continue
+        n = points if unit == "points" else min(points, 200_000_000)
+        fb, wb = 2.0 * f * 1024, w * 1024
+        res[name] = {"n": n, "kernel": sub, "bytes_per_launch": fb + wb, "fetch_bytes": fb, "write_bytes": wb,
+                     "fetch_size_raw_kib": f, "write_size_kib": w, "algorithmic_bytes": alg * n,
+                     "traffic_over_algorithmic": round((fb + wb) / (alg * n), 4),
+                     "correction": "FETCH_SIZE x2 (gfx950, 16-B/lane streaming reads)"}
+    for mode, (kernels, chunk) in JOIN_MODES.items():
+        nchunks = -(-join_points // chunk)
+        parts, total_raw, total = {}, 0.0, 0.0
+        for k in kernels:
+            f, w = mean_for(d, k, "FETCH_SIZE"), mean_for(d, k, "WRITE_SIZE")
+            if f is None or w is None:
+                continue
+            parts[k] = {"fetch_size_raw_kib": f, "write_size_kib": w}
+            total_raw += (f + w) * 1024 * nchunks
+            total += (2 * f + w) * 1024 * nchunks
+        if len(parts) == len(kernels):
+            res["pip_join"] = {"n": join_points, "mode": mode, "kernels": parts, "dispatches": nchunks,
+                               "bytes_per_launch": total, "bytes_raw": total_raw,
+                               "note": "whole join step; FETCH_SIZE doubled (exact for the streaming point reads, "
+                                       "uncalibrated for the index gathers: raw value in bytes_raw)"}
+    json.dump(res, open(out, "w"), indent=1, sort_keys=True)
+    for k, v in res.items():
+        print("%-14s %8.2f GB/launch" % (k, v["bytes_per_launch"] / 1e9))
+
+
+if __name__ == "__main__":
+    a = sys.argv[1:]
+    main(a[0], a[1], *(int(v) for v in a[2:]))
