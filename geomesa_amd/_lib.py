@@ -45,6 +45,11 @@ class Range(ctypes.Structure):
                 ("contained", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
 
+class KeyRange(ctypes.Structure):
+    _fields_ = [("z_lo", ctypes.c_int64), ("z_hi", ctypes.c_int64), ("bin_lo", ctypes.c_int16),
+                ("bin_hi", ctypes.c_int16), ("shard", ctypes.c_uint8), ("reserved", ctypes.c_uint8 * 3)]
+
+
 class PolySetC(ctypes.Structure):
     _fields_ = [("n_polys", ctypes.c_int32),
                 ("poly_part_off", ctypes.c_void_p), ("part_ring_off", ctypes.c_void_p),
@@ -94,6 +99,9 @@ SIGNATURES = {
     "gm_pip_index_stats": (cint, [vp, vp]),
     "gm_pip_join": (cint, [vp, vp, vp, vp, i64, i64, vp, vp, i64, vp]),
     "gm_pip_join_ex": (cint, [vp, vp, vp, vp, i64, i64, vp, vp, i64, vp, cint]),
+    "gm_z3_key_bytes": (cint, [vp, vp, vp, vp, i64, vp]),
+    "gm_sort_keys": (cint, [vp, vp, vp, vp, i64, vp, vp, vp, vp]),
+    "gm_key_range_scan": (cint, [vp, vp, vp, vp, i64, vp, i64, vp, sz, vp, vp, i64, vp, vp]),
     "gm_gen_points": (cint, [vp, ctypes.c_uint64, i64, i64, d, d, d, d, i64, i64, vp, vp, vp]),
 }
 

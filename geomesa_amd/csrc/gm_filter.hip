@@ -424,6 +424,120 @@ __global__ __launch_bounds__(FTPB) void k_mask_to_ids(const uint64_t* __restrict
   }
 }
 
+// ------------------------------------------------------------------ range scan of a sorted table
+// gm_key_range_scan: the seek-and-filter loop of a Z3 query against a table sorted by gm_sort_keys.
+// Each range [lo, hi] of the (shard, bin, z) key prefix (getRangeBytes, Z3IndexKeySpace.scala:196-238)
+// maps to a row interval by two binary searches; the intervals' rows are the candidates
+// (Accumulo/HBase scan), and Z3Filter.inBounds runs on each (RowFilterIterator.scala:52-66) in the
+// same mask -> block scan -> ordered compaction pipeline as the full scans.
+struct DevRange {
+  uint64_t z_lo, z_hi;
+  uint32_t kb_lo, kb_hi;   // shard << 16 | (uint16) bin
+};
+
+__device__ __forceinline__ bool key_lt(uint32_t ka, uint64_t za, uint32_t kb, uint64_t zb) {
+  return ka < kb || (ka == kb && za < zb);
+}
+
+__device__ __forceinline__ uint32_t row_kb(const uint8_t* sh, const uint16_t* bin, int64_t i) {
+  return ((uint32_t)(sh ? sh[i] : 0) << 16) | bin[i];
+}
+
+// row interval of each range: [first row >= lo, first row > hi)
+__global__ __launch_bounds__(FTPB) void k_range_bounds(const uint8_t* __restrict__ sh, const uint16_t* __restrict__ bin,
+                                                       const uint64_t* __restrict__ z, int64_t n,
+                                                       const DevRange* __restrict__ rg, int64_t nr,
+                                                       int64_t* __restrict__ start, int64_t* __restrict__ len) {
+  const int64_t r = (int64_t)blockIdx.x * FTPB + threadIdx.x;
+  if (r >= nr) return;
+  const DevRange q = rg[r];
+  int64_t lo = 0, hi = n;  // lower_bound(lo key)
+  while (lo < hi) {
+    const int64_t m = (lo + hi) >> 1;
+    if (key_lt(row_kb(sh, bin, m), z[m], q.kb_lo, q.z_lo)) lo = m + 1; else hi = m;
+  }
+  const int64_t a = lo;
+  hi = n;  // upper_bound(hi key)
+  while (lo < hi) {
+    const int64_t m = (lo + hi) >> 1;
+    if (!key_lt(q.kb_hi, q.z_hi, row_kb(sh, bin, m), z[m])) lo = m + 1; else hi = m;
+  }
+  start[r] = a;
+  len[r] = lo - a;
+}
+
+// in-place exclusive scan of int64 lengths (one block); total -> a[len]
+__global__ __launch_bounds__(1024) void k_scan_i64(int64_t* __restrict__ a, int64_t len) {
+  __shared__ int64_t part[1024];
+  const int t = threadIdx.x;
+  const int64_t per = (len + 1023) / 1024, lo = t * per, hi = min(len, lo + per);
+  int64_t s = 0;
+  for (int64_t k = lo; k < hi; ++k) s += a[k];
+  part[t] = s;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {
+    const int64_t v = t >= off ? part[t - off] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  int64_t run = part[t] - s;
+  for (int64_t k = lo; k < hi; ++k) { const int64_t c = a[k]; a[k] = run; run += c; }
+  if (t == 1023) a[len] = part[1023];
+}
+
+// candidate c -> its range (upper_bound over the scanned offsets, minus one) -> table row
+__device__ __forceinline__ int64_t cand_row(const int64_t* __restrict__ coff, const int64_t* __restrict__ start,
+                                            int64_t nr, int64_t c) {
+  int64_t lo = 0, hi = nr;
+  while (lo < hi) {
+    const int64_t m = (lo + hi) >> 1;
+    if (coff[m] <= c) lo = m + 1; else hi = m;
+  }
+  const int64_t r = lo - 1;
+  return start[r] + (c - coff[r]);
+}
+
+
+// candidate-space mask: candidate c = the c-th row inside the (disjoint, sorted) intervals
+template <bool FILTER>
+__global__ __launch_bounds__(FTPB) void k_range_mask(const uint16_t* __restrict__ bin, const uint64_t* __restrict__ z,
+                                                     const int64_t* __restrict__ coff, const int64_t* __restrict__ start,
+                                                     int64_t nr, int64_t total, const int32_t* __restrict__ fdesc,
+                                                     uint64_t* __restrict__ mask, int32_t* __restrict__ block_counts) {
+  const int64_t base = (int64_t)blockIdx.x * FROWS;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int local = 0;
+  for (int u = 0; u < FELEMS; ++u) {
+    const int64_t c = base + (int64_t)u * FTPB + threadIdx.x;
+    bool ok = false;
+    if (c < total) {
+      ok = true;
+      if (FILTER) {
+        const int64_t row = cand_row(coff, start, nr, c);
+        ok = z3_in_bounds(fdesc, (int16_t)bin[row], (int64_t)z[row]);
+      }
+    }
+    const uint64_t w = __ballot(ok);
+    if (lane == 0) {
+      const int64_t word = (base + (int64_t)u * FTPB + wave * 64) >> 6;
+      if ((word << 6) < total) mask[word] = w;
+      local += __popcll(w);
+    }
+  }
+  block_count(local, block_counts);
+}
+
+// compacted candidate indices -> table rows (-> input rows through perm)
+__global__ __launch_bounds__(FTPB) void k_cand_to_row(int64_t* __restrict__ ids, int64_t m,
+                                                      const int64_t* __restrict__ coff, const int64_t* __restrict__ start,
+                                                      int64_t nr, const int64_t* __restrict__ perm) {
+  for (int64_t j = (int64_t)blockIdx.x * FTPB + threadIdx.x; j < m; j += (int64_t)gridDim.x * FTPB) {
+    const int64_t row = cand_row(coff, start, nr, ids[j]);
+    ids[j] = perm ? perm[row] : row;
+  }
+}
+
 // ------------------------------------------------------------------ host side
 
 static inline int32_t be32(const uint8_t* p) {
@@ -555,6 +669,17 @@ int finish_scan(gm_ctx* ctx, int64_t n, ScanBufs& b, int64_t* ids, int64_t ids_c
 
 }  // namespace
 
+namespace {
+
+// host mirror of the table's key order: (shard << 16 | bin as uint16, z as uint64)
+struct HostRange {
+  uint32_t kb_lo, kb_hi;
+  uint64_t z_lo, z_hi;
+};
+inline bool h_lt(uint32_t ka, uint64_t za, uint32_t kb, uint64_t zb) { return ka < kb || (ka == kb && za < zb); }
+
+}  // namespace
+
 extern "C" {
 
 int gm_z3filter_scan(gm_ctx* ctx, const uint8_t* filter_bytes, size_t filter_len, const int16_t* bin_ranges,
@@ -678,6 +803,100 @@ int gm_strict_scan(gm_ctx* ctx, const double* x, const double* y, const int64_t*
   free_scan(ctx, mask, b);
   if (rc) return rc;
   if (n_match && ids && *n_match > ids_cap) return GM_E_CAPACITY;
+  return GM_OK;
+}
+
+int gm_key_range_scan(gm_ctx* ctx, const uint8_t* shard, const int16_t* bin, const int64_t* z, int64_t n,
+                      const gm_key_range* ranges, int64_t n_ranges, const uint8_t* filter_bytes, size_t filter_len,
+                      const int64_t* perm, int64_t* ids, int64_t ids_cap, int64_t* n_match, int64_t* n_scanned) {
+  if (!ctx || n < 0 || n_ranges < 0 || (n_ranges > 0 && !ranges) || ids_cap < 0) return GM_E_INVALID;
+  if (n > 0 && (!bin || !z)) return GM_E_INVALID;
+  // the BatchScanner's view of the ranges: sorted, overlapping / adjacent ones merged
+  std::vector<HostRange> rs;
+  rs.reserve((size_t)n_ranges);
+  for (int64_t i = 0; i < n_ranges; ++i) {
+    const gm_key_range& r = ranges[i];
+    HostRange h{((uint32_t)r.shard << 16) | (uint16_t)r.bin_lo, ((uint32_t)r.shard << 16) | (uint16_t)r.bin_hi,
+                (uint64_t)r.z_lo, (uint64_t)r.z_hi};
+    if (h_lt(h.kb_hi, h.z_hi, h.kb_lo, h.z_lo)) continue;  // empty
+    rs.push_back(h);
+  }
+  std::sort(rs.begin(), rs.end(), [](const HostRange& a, const HostRange& b) { return h_lt(a.kb_lo, a.z_lo, b.kb_lo, b.z_lo); });
+  std::vector<DevRange> dr;
+  for (const HostRange& h : rs) {
+    if (!dr.empty()) {
+      DevRange& last = dr.back();
+      // merge when h.lo <= last.hi + 1 in key order
+      const bool le = !h_lt(last.kb_hi, last.z_hi, h.kb_lo, h.z_lo) ||
+                      (last.z_hi != ~0ull && last.kb_hi == h.kb_lo && last.z_hi + 1 == h.z_lo) ||
+                      (last.z_hi == ~0ull && h.z_lo == 0 && last.kb_hi + 1 == h.kb_lo);
+      if (le) {
+        if (h_lt(last.kb_hi, last.z_hi, h.kb_hi, h.z_hi)) { last.kb_hi = h.kb_hi; last.z_hi = h.z_hi; }
+        continue;
+      }
+    }
+    dr.push_back(DevRange{h.z_lo, h.z_hi, h.kb_lo, h.kb_hi});
+  }
+  const int64_t nr = (int64_t)dr.size();
+  if (n == 0 || nr == 0) {
+    if (n_match) *n_match = 0;
+    if (n_scanned) *n_scanned = 0;
+    return GM_OK;
+  }
+  hipStream_t s = ctx->stream;
+  DevRange* d_rg = nullptr;
+  int64_t *start = nullptr, *coff = nullptr;
+  GM_HIP(hipMallocAsync((void**)&d_rg, (size_t)nr * sizeof(DevRange), s));
+  GM_HIP(hipMallocAsync((void**)&start, (size_t)nr * 8, s));
+  GM_HIP(hipMallocAsync((void**)&coff, (size_t)(nr + 1) * 8, s));
+  GM_HIP(hipMemcpyAsync(d_rg, dr.data(), (size_t)nr * sizeof(DevRange), hipMemcpyHostToDevice, s));
+  hipLaunchKernelGGL(k_range_bounds, dim3((unsigned)((nr + FTPB - 1) / FTPB)), dim3(FTPB), 0, s, shard,
+                     (const uint16_t*)bin, (const uint64_t*)z, n, d_rg, nr, start, coff);
+  hipLaunchKernelGGL(k_scan_i64, dim3(1), dim3(1024), 0, s, coff, nr);
+  GM_CHECK_LAUNCH();
+  GM_HIP(hipMemcpyAsync(ctx->h_pinned, coff + nr, 8, hipMemcpyDeviceToHost, s));
+  GM_HIP(hipStreamSynchronize(s));  // dr is pageable; the candidate count sizes the pass below
+  const int64_t total = ctx->h_pinned[0];
+  if (n_scanned) *n_scanned = total;
+  int rc = GM_OK;
+  int64_t nm = 0;
+  if (total > 0) {
+    std::vector<int32_t> desc;
+    if (filter_bytes && !build_z3_desc(filter_bytes, filter_len, desc)) {
+      set_error("gm_key_range_scan: malformed Z3Filter bytes");
+      rc = GM_E_INVALID;
+    }
+    ScanBufs b;
+    if (!rc) rc = alloc_scan(ctx, total, nullptr, desc.size(), b);
+    if (!rc) {
+      if (!desc.empty()) {
+        GM_HIP(hipMemcpyAsync(b.desc, desc.data(), desc.size() * 4, hipMemcpyHostToDevice, s));
+        GM_HIP(hipStreamSynchronize(s));
+      }
+      const int64_t nblocks = (total + FROWS - 1) / FROWS;
+      if (filter_bytes)
+        hipLaunchKernelGGL(k_range_mask<true>, dim3((unsigned)nblocks), dim3(FTPB), 0, s, (const uint16_t*)bin,
+                           (const uint64_t*)z, coff, start, nr, total, b.desc, b.mask, b.counts);
+      else
+        hipLaunchKernelGGL(k_range_mask<false>, dim3((unsigned)nblocks), dim3(FTPB), 0, s, (const uint16_t*)bin,
+                           (const uint64_t*)z, coff, start, nr, total, b.desc, b.mask, b.counts);
+      if (hipGetLastError() != hipSuccess) rc = hip_fail(hipErrorLaunchFailure, "k_range_mask");
+      if (!rc) rc = finish_scan(ctx, total, b, ids, ids_cap, &nm);
+      if (!rc && ids && nm > 0) {
+        const int64_t m = std::min(nm, ids_cap);
+        hipLaunchKernelGGL(k_cand_to_row, dim3((unsigned)std::min<int64_t>(4096, (m + FTPB - 1) / FTPB)), dim3(FTPB), 0,
+                           s, ids, m, coff, start, nr, perm);
+        if (hipGetLastError() != hipSuccess) rc = hip_fail(hipErrorLaunchFailure, "k_cand_to_row");
+      }
+      free_scan(ctx, nullptr, b);
+    }
+  }
+  (void)hipFreeAsync(d_rg, s);
+  (void)hipFreeAsync(start, s);
+  (void)hipFreeAsync(coff, s);
+  if (rc) return rc;
+  if (n_match) *n_match = nm;
+  if (ids && nm > ids_cap) return GM_E_CAPACITY;
   return GM_OK;
 }
 

@@ -1,0 +1,116 @@
+"""A Z3 index table resident in HBM: ingest (keys -> table order) and seek-and-filter queries.
+
+Mirrors the write and read sides of a GeoMesa Z3 index over a sorted key-value store:
+  * ingest  -- Z3IndexKeySpace.toIndexKey (geomesa-index-api/.../index/z3/Z3IndexKeySpace.scala:63-95)
+               for every feature, rows kept in key byte order by the store.  Here: gm_z3_index_key
+               (bin, z columns), then gm_sort_keys into table order (the store's sort);
+  * query   -- getIndexValues / getRanges / getRangeBytes (:97-238) plan the scan ranges, the
+               store seeks each range and RowFilterIterator runs the Z3Filter on every row inside
+               (geomesa-accumulo-iterators/.../RowFilterIterator.scala:52-66).  Here: ranges from
+               the batched GPU ZN.zranges, then gm_key_range_scan (binary-searched row intervals +
+               Z3Filter mask + ordered compaction).
+
+The shard byte (ShardStrategy.scala:75-80: shards(feature.idHash % n)) is a column the caller
+supplies; feature ids stay with the caller (results are input row indices).
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from . import filters as F
+from ._lib import check, ptr
+from .keyspace import Z3IndexKeySpace
+
+_ALL64 = -1  # 0xFFFF... as int64
+
+
+def key_ranges(scan_ranges, shards=None):
+    """getRangeBytes (Z3IndexKeySpace.scala:196-238) as gm_key_range rows: one per scan range and
+    shard.  scan_ranges are Z3IndexKeySpace.get_ranges tuples."""
+    out = []
+    for kind, lo, hi in scan_ranges:
+        if kind == "bounded":
+            r = (lo[1], hi[1], lo[0], hi[0])
+        elif kind == "lower":
+            r = (lo[1], _ALL64, lo[0], -1)
+        elif kind == "upper":
+            r = (0, hi[1], 0, hi[0])
+        else:  # unbounded
+            r = (0, _ALL64, 0, -1)
+        for s in (range(shards) if shards else [0]):
+            out.append(r + (s,))
+    arr = (_lib.KeyRange * max(1, len(out)))()
+    for i, (zl, zh, bl, bh, s) in enumerate(out):
+        arr[i].z_lo, arr[i].z_hi, arr[i].bin_lo, arr[i].bin_hi, arr[i].shard = zl, zh, bl, bh, s
+    return arr, len(out)
+
+
+class Z3Table:
+    """Sorted (shard, bin, z) key columns of one GPU's slice of a Z3 index table."""
+
+    def __init__(self, bins, z, shard=None, period="week"):
+        import torch
+        from .curve import _dev_col
+        self.ks = Z3IndexKeySpace(period)
+        self.ctx = _lib.context()
+        bins, z = _dev_col(bins, torch.int16), _dev_col(z, torch.int64)
+        self.n = z.numel()
+        dev = z.device
+        self.bin = torch.empty_like(bins)
+        self.z = torch.empty_like(z)
+        self.perm = torch.empty(self.n, dtype=torch.int64, device=dev)
+        self.shards = None
+        self.shard = None
+        sh_in = None
+        if shard is not None:
+            sh_in = torch.as_tensor(np.asarray(shard, np.uint8) if not isinstance(shard, torch.Tensor) else shard,
+                                    dtype=torch.uint8).to(dev).contiguous()
+            self.shard = torch.empty_like(sh_in)
+            self.shards = int(sh_in.max().item()) + 1 if self.n else 1
+        check(self.ctx.lib.gm_sort_keys(self.ctx.handle, ptr(sh_in), ptr(bins), ptr(z), self.n, ptr(self.shard),
+                                        ptr(self.bin), ptr(self.z), ptr(self.perm)), "gm_sort_keys")
+
+    @classmethod
+    def from_points(cls, x, y, t_ms, shard=None, period="week", lenient=False):
+        ks = Z3IndexKeySpace(period)
+        bins, z = ks.sfc.index_keys(x, y, t_ms, lenient=lenient)
+        return cls(bins, z, shard, period)
+
+    def key_bytes(self):
+        """The table's row-key prefixes in table order, (n, 10|11) uint8 (gm_z3_key_bytes)."""
+        import torch
+        klen = 11 if self.shard is not None else 10
+        out = torch.empty((self.n, klen), dtype=torch.uint8, device=self.z.device)
+        check(self.ctx.lib.gm_z3_key_bytes(self.ctx.handle, ptr(self.shard), ptr(self.bin), ptr(self.z), self.n,
+                                           ptr(out)), "gm_z3_key_bytes")
+        return out
+
+    def scan(self, scan_ranges, z3filter=None, map_rows=True, ids_cap=None):
+        """Rows in any scan range that pass `z3filter` (a Z3Filter, its bytes, or None).
+
+        Returns (ids tensor, n_match, n_scanned); ids are input rows (map_rows) or table rows."""
+        import torch
+        arr, nr = key_ranges(scan_ranges, self.shards)
+        fb = None
+        if z3filter is not None:
+            fb = F.serialize_to_bytes(z3filter) if not isinstance(z3filter, (bytes, bytearray)) else bytes(z3filter)
+        fbuf = (ctypes.c_uint8 * len(fb)).from_buffer_copy(fb) if fb else None
+        cap = self.n if ids_cap is None else ids_cap
+        ids = torch.empty(max(cap, 1), dtype=torch.int64, device=self.z.device)
+        nm, ns = ctypes.c_int64(), ctypes.c_int64()
+        rc = self.ctx.lib.gm_key_range_scan(self.ctx.handle, ptr(self.shard), ptr(self.bin), ptr(self.z), self.n,
+                                            arr, nr, fbuf, len(fb) if fb else 0, ptr(self.perm) if map_rows else None,
+                                            ptr(ids), cap, ctypes.byref(nm), ctypes.byref(ns))
+        if rc != _lib.GM_E_CAPACITY:
+            check(rc, "gm_key_range_scan")
+        return ids[:min(nm.value, cap)], nm.value, ns.value
+
+    def query(self, bboxes=None, intervals=None, target=2000):
+        """bbox + during query through the index (loose bbox, the default: Z3Filter only)."""
+        v = self.ks.get_index_values(bboxes, intervals)
+        if v.disjoint:
+            import torch
+            return torch.zeros(0, dtype=torch.int64, device=self.z.device), 0, 0
+        sr = self.ks.get_ranges(v, target=target)
+        return self.scan(sr, F.Z3Filter.from_values(v))

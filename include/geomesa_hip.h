@@ -201,7 +201,7 @@ typedef struct gm_pip_index gm_pip_index;
    plus per-ring y-slab edge buckets). */
 int gm_pip_index_create(gm_ctx* ctx, const gm_polyset* polys, gm_pip_index** out);
 /* same with an explicit grid density: ~cells_per_poly grid cells per polygon over the set's
-   envelope (0 = default 2048; a coarse 4x4-cell table in front of it stays L2-resident) */
+   envelope (0 = default 4096; a coarse 4x4-cell table in front of it stays L2-resident) */
 int gm_pip_index_create_ex(gm_ctx* ctx, const gm_polyset* polys, int cells_per_poly, gm_pip_index** out);
 int gm_pip_index_destroy(gm_pip_index* index);
 /* index statistics: stats[0..6] = cells, (cell, polygon) entries, boundary entries, ring records,
@@ -220,7 +220,7 @@ int gm_pip_join(gm_ctx* ctx, const gm_pip_index* index, const double* px, const 
                 int64_t id_base, int64_t* pt_ids, int32_t* poly_ids, int64_t cap, int64_t* n_pairs);
 
 /* join strategies for gm_pip_join_ex */
-#define GM_JOIN_AUTO 0        /* partitioned from 2^22 points, direct below */
+#define GM_JOIN_AUTO 0        /* the faster strategy on MI355X: currently DIRECT */
 #define GM_JOIN_DIRECT 1      /* one pass over the point columns (random index reads) */
 #define GM_JOIN_PARTITIONED 2 /* counting-sort the points by grid-row band first (device temp:
                                  24 B per point, at most 2^28 points per pass), then join band by
@@ -228,6 +228,47 @@ int gm_pip_join(gm_ctx* ctx, const gm_pip_index* index, const double* px, const 
 /* gm_pip_join with an explicit strategy; the pair set is identical for every mode */
 int gm_pip_join_ex(gm_ctx* ctx, const gm_pip_index* index, const double* px, const double* py, int64_t n,
                    int64_t id_base, int64_t* pt_ids, int32_t* poly_ids, int64_t cap, int64_t* n_pairs, int mode);
+
+/* ------------------------------------------------------------------ sorted key table */
+/* The row-key prefix [shard?][bin BE16][z BE64] of Z3IndexKeySpace.toIndexKey (idx/index/z3/
+   Z3IndexKeySpace.scala:81-92; ByteArrays.writeShort / writeLong, geomesa-utils/.../index/
+   ByteArrays.scala:51,90-99) for n rows: out (device) gets n * key_len bytes, key_len = 11 with a
+   shard column (device uint8, ShardStrategy.scala:75-80), 10 when shard = NULL.  The feature id
+   the store appends after the prefix is the caller's. */
+int gm_z3_key_bytes(gm_ctx* ctx, const uint8_t* shard, const int16_t* bin, const int64_t* z, int64_t n,
+                    uint8_t* out);
+
+/* Sorts key columns into the table's row order -- the byte order of the row keys above: shard,
+   then bin as an unsigned big-endian short, then z as an unsigned big-endian long (what Accumulo /
+   HBase keep sorted).  Stable; perm_out[i] = the input row of table row i.  shard / shard_out may
+   be NULL together (unsharded table).  n < 2^32.  Device temporaries: about 23 B per row. */
+int gm_sort_keys(gm_ctx* ctx, const uint8_t* shard, const int16_t* bin, const int64_t* z, int64_t n,
+                 uint8_t* shard_out, int16_t* bin_out, int64_t* z_out, int64_t* perm_out);
+
+/* A scan range over the key prefix, inclusive at both ends in table order: what getRangeBytes
+   makes of a ScanRange (idx/index/z3/Z3IndexKeySpace.scala:196-238), [toBytes(lo),
+   toBytesFollowingPrefix(hi)) = every row whose [shard][bin][z] prefix lies in [lo, hi].
+   BoundedRange(bin, lo, hi): bin_lo = bin_hi = bin; LowerBoundedRange: z_hi/bin_hi = all ones;
+   UpperBoundedRange: bin_lo = z_lo = 0; UnboundedRange: both.  bin and z compare unsigned. */
+typedef struct {
+  int64_t z_lo;
+  int64_t z_hi;
+  int16_t bin_lo;
+  int16_t bin_hi;
+  uint8_t shard;       /* 0 for an unsharded table */
+  uint8_t reserved[3];
+} gm_key_range;
+
+/* Seek-and-filter over a sorted table (gm_sort_keys order): every row inside any of the ranges
+   (host array; sorted and merged here the way a BatchScanner merges overlapping ranges), then
+   Z3Filter.inBounds on each (idx/filters/Z3Filter.scala:26-62, RowFilterIterator.scala:52-66) when
+   filter_bytes (host, Z3Filter.serializeToBytes) is not NULL.  ids (device, optional) receives the
+   matching rows in table order, mapped through perm (device, optional) to input rows.
+   *n_match / *n_scanned (host) receive the match and candidate counts; GM_E_CAPACITY when the
+   matches exceed ids_cap.  Synchronises the context stream. */
+int gm_key_range_scan(gm_ctx* ctx, const uint8_t* shard, const int16_t* bin, const int64_t* z, int64_t n,
+                      const gm_key_range* ranges, int64_t n_ranges, const uint8_t* filter_bytes, size_t filter_len,
+                      const int64_t* perm, int64_t* ids, int64_t ids_cap, int64_t* n_match, int64_t* n_scanned);
 
 /* ------------------------------------------------------------------ synthetic data (bench/tests) */
 /* SplitMix64 keyed by (seed, index): lon U[lon0,lon1), lat U[lat0,lat1), t_ms U[t0,t1) */

@@ -1,0 +1,155 @@
+"""GPU parity for the sorted key table: key bytes, table-order sort, and seek-and-filter range scans.
+
+The expected table order is the store's byte order of [shard][bin BE16][z BE64]
+(Z3IndexKeySpace.scala:81-92, ByteArrays.scala:51,90-99), computed here with a stable numpy lexsort
+on the unsigned views; range scans are checked against the full-column Z3Filter scan (which the
+oracle pins) and the Z3IdxStrategyTest KATs."""
+import numpy as np
+import pytest
+
+from test_host_planning import IDX_STRATEGY_KATS, idx_strategy_features, ms
+from geomesa_amd import filters as F
+from geomesa_amd.keyspace import Z3IndexKeySpace, during
+
+pytestmark = pytest.mark.gpu
+
+T2020, T2021 = 1577836800000, 1609459200000
+
+
+def as_np(t):
+    return t.detach().cpu().numpy()
+
+
+def expected_order(bins, z, shard=None):
+    keys = [np.asarray(z).view(np.uint64), np.asarray(bins).view(np.uint16)]
+    if shard is not None:
+        keys.append(np.asarray(shard, np.uint8))
+    return np.lexsort(keys)   # stable; last key is primary
+
+
+@pytest.mark.parametrize("n,kind", [(1, "rand"), (2, "rand"), (2047, "rand"), (2049, "rand"), (300_001, "rand"),
+                                    (100_000, "equal"), (100_000, "few"), (1_000_003, "keys")])
+@pytest.mark.parametrize("sharded", [False, True])
+def test_sort_keys_parity(gpu, n, kind, sharded):
+    import torch
+    from geomesa_amd import _lib
+    rng = np.random.default_rng(n + sharded)
+    if kind == "rand":     # every bit pattern: negative bins / z sort as unsigned bytes
+        bins = rng.integers(-2**15, 2**15, n).astype(np.int16)
+        z = rng.integers(-2**63, 2**63 - 1, n, dtype=np.int64, endpoint=True)
+    elif kind == "equal":  # every digit pass skipped
+        bins = np.full(n, 2610, np.int16); z = np.full(n, 123456789, np.int64)
+    elif kind == "few":    # heavy duplicates: stability decides the permutation
+        bins = rng.integers(2608, 2611, n).astype(np.int16); z = rng.integers(0, 5, n).astype(np.int64)
+    else:                  # real keys
+        x = rng.uniform(-180, 180, n); y = rng.uniform(-90, 90, n); t = rng.integers(T2020, T2021, n)
+        b, zz = Z3IndexKeySpace().sfc.index_keys(x, y, t)
+        bins, z = as_np(b), as_np(zz)
+    shard = rng.integers(0, 4, n).astype(np.uint8) if sharded else None
+    ctx = _lib.context()
+    db, dz = torch.from_numpy(bins).cuda(), torch.from_numpy(z).cuda()
+    ds = torch.from_numpy(shard).cuda() if sharded else None
+    ob, oz, op = torch.empty_like(db), torch.empty_like(dz), torch.empty(n, dtype=torch.int64, device="cuda")
+    os_ = torch.empty_like(ds) if sharded else None
+    _lib.check(ctx.lib.gm_sort_keys(ctx.handle, _lib.ptr(ds), _lib.ptr(db), _lib.ptr(dz), n, _lib.ptr(os_),
+                                    _lib.ptr(ob), _lib.ptr(oz), _lib.ptr(op)), "sort")
+    order = expected_order(bins, z, shard)
+    assert np.array_equal(as_np(op), order)
+    assert np.array_equal(as_np(ob), bins[order]) and np.array_equal(as_np(oz), z[order])
+    if sharded:
+        assert np.array_equal(as_np(os_), shard[order])
+
+
+@pytest.mark.parametrize("sharded", [False, True])
+def test_key_bytes(gpu, sharded):
+    from geomesa_amd.table import Z3Table
+    rng = np.random.default_rng(5)
+    n = 70_001
+    bins = rng.integers(-2**15, 2**15, n).astype(np.int16)
+    z = rng.integers(-2**63, 2**63 - 1, n, dtype=np.int64, endpoint=True)
+    shard = rng.integers(0, 4, n).astype(np.uint8) if sharded else None
+    tb = Z3Table(bins, z, shard)
+    kb = as_np(tb.key_bytes())
+    order = expected_order(bins, z, shard)
+    exp = Z3IndexKeySpace.key_bytes(bins[order], z[order], None if shard is None else shard[order])
+    assert np.array_equal(kb, exp)
+    # table order is the byte order of the keys (what Accumulo / HBase keep sorted)
+    rows = [bytes(r) for r in kb[:: 97]]
+    assert rows == sorted(rows)
+
+
+@pytest.mark.parametrize("bbox,interval,expected", IDX_STRATEGY_KATS)
+def test_table_query_idx_strategy_kats(gpu, bbox, interval, expected):  # Z3IdxStrategyTest.scala:96-181
+    from geomesa_amd.table import Z3Table
+    feats = idx_strategy_features()
+    ids = np.array([f[0] for f in feats])
+    tb = Z3Table.from_points([f[1] for f in feats], [f[2] for f in feats], [f[3] for f in feats])
+    got, n, scanned = tb.query([bbox], [interval])
+    assert set(ids[as_np(got)].tolist()) == expected and n == len(expected) and scanned >= n
+
+
+def random_points(n, seed):
+    rng = np.random.default_rng(seed)
+    return rng.uniform(-180, 180, n), rng.uniform(-90, 90, n), rng.integers(T2020, T2021, n)
+
+
+QUERIES = [
+    ([(-10, 35, 30, 60)], [during(ms("2020-06-01T00:00:00.000Z"), ms("2020-06-08T12:00:00.000Z"))]),
+    ([(-10, 35, 30, 60), (100, -40, 120, -10)], [during(ms("2020-03-01T00:00:00.000Z"),
+                                                        ms("2020-05-08T12:00:00.000Z"))]),
+    ([(0.0, 0.0, 0.5, 0.5)], [during(ms("2020-01-01T00:00:00.000Z"), ms("2020-01-09T00:00:00.500Z"))]),
+    ([(-180, -90, 180, 90)], [during(ms("2020-12-30T00:00:00.000Z"), ms("2021-01-01T00:00:00.000Z"))]),
+    ([(-50, -50, 50, 50)], None),   # no time predicate: one unbounded range
+]
+
+
+@pytest.mark.parametrize("q", range(len(QUERIES)))
+@pytest.mark.parametrize("sharded", [False, True])
+def test_table_query_equals_full_scan(gpu, oracle, q, sharded):
+    """Seek-and-filter over the sorted table returns exactly the rows of a full-column scan with
+    the same Z3Filter and epoch restriction (the claim of SURVEY 8(e)), which the oracle pins."""
+    from geomesa_amd.table import Z3Table
+    x, y, t = random_points(1_000_003, seed=40 + q)
+    shard = np.arange(len(x)) % 4 if sharded else None
+    ks = Z3IndexKeySpace()
+    b, z = ks.sfc.index_keys(x, y, t)
+    tb = Z3Table(b, z, shard)
+    bb, iv = QUERIES[q]
+    got, n, scanned = tb.query(bb, iv)
+    v = ks.get_index_values(bb, iv)
+    f = F.Z3Filter.from_values(v)
+    om = oracle.z3filter_scan(F.serialize_to_bytes(f), ks.bin_ranges(v), as_np(b), as_np(z))
+    assert n == int(om.sum()) and np.array_equal(np.sort(as_np(got)), np.nonzero(om)[0])
+    assert scanned >= n and (q == 4 or scanned < len(x) // 4)   # the ranges prune
+    # table-order ids are ascending
+    tid, n2, _ = tb.scan(ks.get_ranges(v), f, map_rows=False)
+    assert n2 == n and np.all(np.diff(as_np(tid)) > 0)
+
+
+def test_table_scan_open_ranges_and_capacity(gpu):
+    """Lower/upper-bounded and unbounded scan ranges (after / before predicates), overlapping ranges
+    merged as a BatchScanner does, and the GM_E_CAPACITY path."""
+    from geomesa_amd.table import Z3Table
+    x, y, t = random_points(200_001, seed=3)
+    ks = Z3IndexKeySpace()
+    b, z = ks.sfc.index_keys(x, y, t)
+    tb = Z3Table(b, z)
+    bn, zn = as_np(b).astype(np.int64), as_np(z)
+    keys = as_np(b).view(np.uint16).astype(np.int64)   # bins compare as unsigned bytes
+    for kind, lo, hi, sel in [
+            ("lower", (2630, 0), None, keys >= 2630),
+            ("upper", None, (2620, 2**63 - 1), keys <= 2620),
+            ("unbounded", (0, 0), None, np.ones(len(keys), bool))]:
+        got, n, scanned = tb.scan([(kind, lo, hi)], None)
+        assert n == int(sel.sum()) == scanned and np.array_equal(np.sort(as_np(got)), np.nonzero(sel)[0])
+    # overlapping bounded ranges scan each row once
+    zs = np.sort(zn[bn == 2640])
+    r1 = ("bounded", (2640, int(zs[10])), (2640, int(zs[500])))
+    r2 = ("bounded", (2640, int(zs[300])), (2640, int(zs[900])))
+    got, n, scanned = tb.scan([r1, r2, r1], None)
+    exp = np.nonzero((bn == 2640) & (zn >= zs[10]) & (zn <= zs[900]))[0]
+    assert n == len(exp) == scanned and np.array_equal(np.sort(as_np(got)), exp)
+    got, n, _ = tb.scan([r1, r2], None, ids_cap=7)
+    assert n == len(exp) and len(got) == 7
+    # empty table / no ranges
+    assert tb.scan([], None)[1] == 0
