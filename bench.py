@@ -42,7 +42,9 @@ def parse():
     p.add_argument("--no-extra", action="store_true")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=8.0)
-    p.add_argument("--only", default="", help="comma list: z3,join,extra (profiling)")
+    p.add_argument("--only", default="", help="comma list: z3,join,extra,table (profiling)")
+    p.add_argument("--table-rows", type=int, default=250_000_000,
+                   help="rows per GPU of the sorted-table leg (configs[2]: 2B rows over 8 GPUs)")
     p.add_argument("--join-mode", default="auto", choices=["auto", "direct", "partitioned"])
     p.add_argument("--cells-per-poly", type=int, default=0, help="join grid density (0 = library default)")
     return p.parse_args()
@@ -173,6 +175,59 @@ def cpu_join_baseline(seconds, ps):
                       "pair, %d pthreads): %.2f s, %d matches" % (n, ps.n_polys, nt, dt, len(pt))}
 
 
+def bench_table(a, dist, ctx, b, z):
+    """configs[2]: the rank's slice of a range-sharded Z3 table (2B rows over 8 GPUs = 250M per GPU):
+    gm_sort_keys into table order (ingest), then the configs[2] bbox + during query as ranges +
+    gm_key_range_scan (seek + Z3Filter).  Reported: sort rows/s and queries/s, with the rows the
+    seeks touched."""
+    import ctypes
+    import torch
+    from geomesa_amd import _lib
+    from geomesa_amd import filters as F
+    from geomesa_amd.keyspace import Z3IndexKeySpace, during
+    from geomesa_amd.table import Z3Table, key_ranges
+    NT = min(a.table_rows, b.numel())
+    lib, h, P = ctx.lib, ctx.handle, _lib.ptr
+    bs, zs = b[:NT], z[:NT]
+    ob, oz = torch.empty_like(bs), torch.empty_like(zs)
+    perm = torch.empty(NT, dtype=torch.int64, device=zs.device)
+
+    def sort_step():
+        _lib.check(lib.gm_sort_keys(h, None, P(bs), P(zs), NT, None, P(ob), P(oz), P(perm)), "gm_sort_keys")
+    ms_sort = timed(dist, sort_step, 3, 1)
+    tb = Z3Table.__new__(Z3Table)   # wrap the sorted columns without re-sorting
+    tb.ks, tb.ctx, tb.n, tb.bin, tb.z, tb.perm, tb.shard, tb.shards = Z3IndexKeySpace(), ctx, NT, ob, oz, perm, None, None
+    ks = tb.ks
+    v = ks.get_index_values([(-10, 35, 30, 60)], [during(1590969600000, 1591617600000)])
+    t0 = time.time()
+    sr = ks.get_ranges(v)
+    plan_ms = (time.time() - t0) * 1e3
+    arr, nr = key_ranges(sr)
+    fb = F.serialize_to_bytes(F.Z3Filter.from_values(v))
+    fbuf = (ctypes.c_uint8 * len(fb)).from_buffer_copy(fb)
+    cap = NT // 100
+    ids = torch.empty(cap, dtype=torch.int64, device=zs.device)
+    nm, ns = ctypes.c_int64(), ctypes.c_int64()
+
+    def scan_step():
+        _lib.check(lib.gm_key_range_scan(h, None, P(ob), P(oz), NT, arr, nr, fbuf, len(fb), P(perm), P(ids), cap,
+                                         ctypes.byref(nm), ctypes.byref(ns)), "gm_key_range_scan")
+    ms_scan = timed(dist, scan_step, 10, 2)
+    del ob, oz, perm, ids
+    return {
+        "sort_keys": {"value": NT * dist.world / (ms_sort * 1e-3), "unit": "rows/s", "ms_per_step": ms_sort,
+                      "rows_per_gpu": NT, "roofline": None,
+                      "note": "stable LSD radix sort of (bin, z) into table byte order (ingest side)"},
+        "table_query": {"value": dist.world / (ms_scan * 1e-3), "unit": "queries/s", "ms_per_step": ms_scan,
+                        "rows_per_gpu": NT, "ranges": nr, "rows_scanned": ns.value, "matches": nm.value,
+                        "plan_ms": round(plan_ms, 2),
+                        "equivalent_scan_rate": NT * dist.world / (ms_scan * 1e-3),
+                        "note": "configs[2] query bbox(-10,35,30,60) during 2020-06-01/06-08T12 on a sorted "
+                                "table slice: binary-searched ranges + Z3Filter on the rows inside (ranges "
+                                "planned on the GPU once, plan_ms, not in ms_per_step)"},
+    }
+
+
 # ------------------------------------------------------------------------------ main
 
 def main():
@@ -182,7 +237,7 @@ def main():
     from geomesa_amd.curve import Z3SFC, Z2SFC
     dist = Dist(a.gpus)
     ctx = _lib.context(dist.local)
-    only = set(a.only.split(",")) if a.only else {"z3", "join", "extra"}
+    only = set(a.only.split(",")) if a.only else {"z3", "join", "extra", "table"}
     dev = torch.device("cuda", dist.local)
     N = a.points
     out = {"metric": METRIC, "unit": "points/s", "n_gpus": dist.world, "steps": a.steps, "warmup": a.warmup,
@@ -277,6 +332,9 @@ def main():
                                     "ms_per_step": dt * 1e3, "ranges": int(offs[-1]),
                                     "note": "C-ABI call incl. H2D of queries and D2H of ranges; 4096 Z3 queries "
                                             "(0.2-20 deg boxes x 1 day), maxRanges 2000 (ScanRangesTarget)"}
+    # ---------------------------------------------------------------- sorted table: ingest sort + seek-and-filter
+    if "table" in only and not a.no_extra:
+        extra.update(bench_table(a, dist, ctx, b, z))
     del x, y, t, b, z
     torch.cuda.empty_cache()
 
