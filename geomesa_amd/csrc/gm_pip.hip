@@ -62,9 +62,12 @@ struct PipDev {
 };
 
 #ifndef GM_CF_LOG
-#define GM_CF_LOG 2
+#define GM_CF_LOG 3
 #endif
-constexpr int CF_LOG = GM_CF_LOG;   // coarse cell = 4 x 4 fine cells: the coarse table stays L2-resident
+#ifndef GM_MAX_CELLS_LOG
+#define GM_MAX_CELLS_LOG 26
+#endif
+constexpr int CF_LOG = GM_CF_LOG;   // coarse cell = 8 x 8 fine cells: the coarse table (<= 4 MB) stays L2-resident
 
 // cell word kinds (2 high bits; 30-bit payload)
 enum : uint32_t { CELL_INTERIOR = 0, CELL_BOUNDARY = 1, CELL_LIST = 2, CELL_EMPTY = 3 };
@@ -241,7 +244,11 @@ __device__ __forceinline__ void flush_pairs(const uint32_t* wpt, const int32_t* 
                                             int64_t cap, unsigned long long* __restrict__ counter) {
   wave_lds_sync();
   unsigned long long base = 0;
+#ifdef GM_JX_NOATOMIC   // timing experiment only: no output counter (pairs land in a per-wave window)
+  base = ((uint64_t)(blockIdx.x * 4 + (threadIdx.x >> 6)) * 4096) % (uint64_t)(cap > 4096 ? cap - 4096 : 1);
+#else
   if (lane == 0) base = atomicAdd(counter, (unsigned long long)wn);
+#endif
   base = __shfl(base, 0, 64);
   for (int j = lane; j < wn; j += 64) {
     const int64_t slot = (int64_t)base + j;
@@ -335,7 +342,13 @@ __global__ __launch_bounds__(JTPB, GM_JOIN_WAVES) void k_pip_join(const double* 
     }
 #pragma unroll
     for (int u = 0; u < JILP; ++u)
-      if ((cw[u] >> 30) == CELL_LIST) cw[u] = d.cell_word[(int64_t)cys[u] * d.gx + cxs[u]];
+      if ((cw[u] >> 30) == CELL_LIST) {
+#ifdef GM_JX_NOFINE   // timing experiment only: stop at the coarse level
+        cw[u] = CELL_EMPTY << 30;
+#else
+        cw[u] = d.cell_word[(int64_t)cys[u] * d.gx + cxs[u]];
+#endif
+      }
 #pragma unroll
     for (int u = 0; u < JILP; ++u) {
       const uint32_t kind = cw[u] >> 30;
@@ -405,6 +418,11 @@ __global__ __launch_bounds__(JTPB, GM_JOIN_WAVES) void k_pip_join(const double* 
           const uint32_t ref = qb[slot];
           const double ex = qx[slot], ey = qy[slot];
           eid = qid[slot];
+#ifdef GM_JX_NOBLOB   // timing experiment only: no blob evaluation
+          if (true) {
+            poly = 0; hit = false;
+          } else
+#endif
           if (ref & BLOB_COMPACT) {
             const dv2* c = (const dv2*)(d.compact + 16 * (uint64_t)(ref & (BLOB_COMPACT - 1)));
             hit = compact_contains(c, ex, ey, poly);
@@ -836,8 +854,8 @@ int gm_pip_index_create_ex(gm_ctx* ctx, const gm_polyset* ps, int cells_per_poly
 
   // ---- grid: ~cells_per_poly cells per polygon over the set's envelope
   const double W = any ? G[2] - G[0] : 0.0, H = any ? G[3] - G[1] : 0.0;
-  const int64_t cells_per_poly = cells_per_poly_in > 0 ? cells_per_poly_in : 4096;
-  int64_t target = std::min<int64_t>(std::max<int64_t>((int64_t)P * cells_per_poly, 64), (int64_t)1 << 24);
+  const int64_t cells_per_poly = cells_per_poly_in > 0 ? cells_per_poly_in : 8192;
+  int64_t target = std::min<int64_t>(std::max<int64_t>((int64_t)P * cells_per_poly, 64), (int64_t)1 << GM_MAX_CELLS_LOG);
   int gx = 1, gy = 1;
   const bool degenerate = !(W > 0 && H > 0);
   if (!degenerate) {
