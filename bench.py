@@ -47,6 +47,9 @@ def parse():
                    help="rows per GPU of the sorted-table leg (configs[2]: 2B rows over 8 GPUs)")
     p.add_argument("--join-mode", default="auto", choices=["auto", "direct", "partitioned"])
     p.add_argument("--cells-per-poly", type=int, default=0, help="join grid density (0 = library default)")
+    p.add_argument("--join-grid", default="80x40", help="synthetic county grid (experiments)")
+    p.add_argument("--no-gather", action="store_true", help="skip the join's result gather to rank 0")
+    p.add_argument("--join-sorted", action="store_true", help="experiment: points pre-sorted by latitude")
     return p.parse_args()
 
 
@@ -173,6 +176,28 @@ def cpu_join_baseline(seconds, ps):
     return {"value": n * ps.n_polys / dt, "unit": "pairs/s", "cores": nt, "kind": "port",
             "sample": "%d CONUS points x %d polygons, C restatement (grid candidates + JTS contains per "
                       "pair, %d pthreads): %.2f s, %d matches" % (n, ps.n_polys, nt, dt, len(pt))}
+
+
+def gather_pairs(dist, ptids, plids, k):
+    """Result gather of the join: per-rank pair counts, then every rank's
+    (point id, polygon id) pairs to rank 0 over RCCL (shard.gather_rows), timed max over ranks.
+    Reported, never part of the join's ms_per_step.  A failure is reported, not raised, so the
+    scaling line survives it."""
+    import torch
+    from geomesa_amd.shard import gather_rows
+    try:
+        dist.barrier()
+        t0 = time.time()
+        g = gather_rows(dist.pg, [ptids[:k], plids[:k]])
+        torch.cuda.synchronize()
+        ms = dist.max((time.time() - t0) * 1e3)
+        n = int(g[0].numel()) if g is not None else 0
+        del g
+        torch.cuda.empty_cache()
+        return {"ms": ms, "pairs_on_rank0": n if dist.rank == 0 else None, "bytes": 12 * n,
+                "how": "all_gather of counts + padded gather to rank 0 (grouped send/recv over xGMI)"}
+    except Exception as e:  # noqa: BLE001 -- reported in the JSON line
+        return {"error": repr(e)[:200]}
 
 
 def bench_table(a, dist, ctx, b, z):
@@ -342,7 +367,8 @@ def main():
     if "join" in only:
         from geomesa_amd.join import PolygonIndex, PolygonSet, synthetic_counties
         J = a.join_points
-        ps = synthetic_counties() if dist.rank == 0 else None
+        gx, gy = (int(v) for v in a.join_grid.split("x"))
+        ps = synthetic_counties(gx, gy) if dist.rank == 0 else None
         if dist.world > 1:
             # polygon set broadcast over RCCL (the reference ships it with the Spark join shuffle)
             ps = broadcast_polyset(dist.pg, ps)
@@ -353,6 +379,10 @@ def main():
         py = torch.empty(J, dtype=torch.float64, device=dev)
         jlo, _ = shard_bounds(J * dist.world, dist.rank, dist.world)
         gen_points(ctx, J, jlo + (1 << 40), CONUS, px, py, None)
+        if a.join_sorted:   # locality experiment only (not a bench configuration)
+            py, order = torch.sort(py)
+            px = px[order]
+            del order
         jmode = PolygonIndex.MODES[a.join_mode]
         cnt = ix.join(px, py, count_only=True, mode=a.join_mode)
         cap = int(cnt * 1.05) + 1024
@@ -376,10 +406,14 @@ def main():
               "workload": "st_contains(polygon, point) join, %d CONUS points/GPU x %d synthetic county polygons "
                           "(BASELINE configs[3]); polygon set broadcast over RCCL when N > 1" % (J, ps.n_polys)}
         pj["roofline"]["bytes_per_unit"] = "16 B/point + 12 B/pair"
+        del px, py
+        torch.cuda.empty_cache()
+        if not a.no_gather:
+            pj["gather"] = gather_pairs(dist, ptids, plids, int(npairs.value))
         if dist.rank == 0 and not a.no_cpu:
             pj["cpu_baseline"] = cpu_join_baseline(a.cpu_seconds, ps)
         out["pip_join"] = pj
-        del px, py, ptids, plids, ix
+        del ptids, plids, ix
 
     if dist.rank == 0 and not a.no_cpu and "z3" in only:
         out["cpu_baseline"] = cpu_z3_baseline(a.cpu_seconds)

@@ -5,8 +5,9 @@ st_contains join against a replicated polygon set), so ranks shard the points an
 data-path collective ("weak" scaling).  The only exchanges are the polygon-set broadcast before a
 join (the reference ships the smaller side of the join to every partition: GeoMesaJoinRelation /
 RelationUtils.grid, geomesa-spark-sql/.../GeoMesaJoinRelation.scala:41-91) and the scalar
-max/sum reductions of the benchmark.  Works with both RCCL ("nccl", device tensors) and gloo
-(CPU tensors, used by the multi-process tests).
+max/sum reductions of the benchmark, plus the result gather: per-rank match counts, then the
+ids / (point, polygon) pairs to one rank (gather_rows).  Works with both RCCL ("nccl", device
+tensors) and gloo (CPU tensors, used by the multi-process tests).
 """
 import numpy as np
 
@@ -48,3 +49,31 @@ def all_reduce_scalar(pg, v, op="max"):
     t = torch.tensor([float(v)], dtype=torch.float64, device=_device_of(pg))
     pg.all_reduce(t, op={"max": pg.ReduceOp.MAX, "sum": pg.ReduceOp.SUM}[op])
     return float(t.item())
+
+
+def gather_rows(pg, cols, dst=0):
+    """Gather variable-length per-rank result columns (1-D tensors of equal length per rank: ids,
+    or point ids + polygon ids) to rank `dst`, in rank order.
+
+    One all_gather of the per-rank counts (8 B each), then one gather of each column padded to the
+    largest count: over RCCL a gather is a grouped send/recv, so rank `dst` receives from every
+    peer at once over its own xGMI link (padding costs at most the imbalance between ranks).
+    Returns the concatenated columns on `dst` and None elsewhere; with pg None, `cols`."""
+    if pg is None:
+        return list(cols)
+    import torch
+    dev = _device_of(pg)
+    world = pg.get_world_size()
+    n = torch.tensor([int(cols[0].numel())], dtype=torch.int64, device=dev)
+    counts = [torch.zeros_like(n) for _ in range(world)]
+    pg.all_gather(counts, n)
+    counts = [int(c.item()) for c in counts]
+    mx = max(counts)
+    out = []
+    for c in cols:
+        buf = torch.zeros(mx, dtype=c.dtype, device=dev)
+        buf[:c.numel()] = c.to(dev)
+        parts = [torch.empty_like(buf) for _ in range(world)] if pg.get_rank() == dst else None
+        pg.gather(buf, parts, dst=dst)
+        out.append(torch.cat([p[:k] for p, k in zip(parts, counts)]) if pg.get_rank() == dst else None)
+    return out if pg.get_rank() == dst else None

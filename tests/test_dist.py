@@ -32,19 +32,23 @@ def _worker(rank, world, port, n_total, q):
     try:
         import oracle as O
         from geomesa_amd.join import synthetic_counties, synthetic_points
-        from geomesa_amd.shard import all_reduce_scalar, broadcast_polyset, shard_bounds
+        import torch
+        from geomesa_amd.shard import all_reduce_scalar, broadcast_polyset, gather_rows, shard_bounds
         ps = synthetic_counties(20, 10) if rank == 0 else None
         ps = broadcast_polyset(dist, ps)
         px, py = synthetic_points(n_total, seed=21)
         lo, hi = shard_bounds(n_total, rank, world)
         pt, pl = O.OraclePolySet(*ps.to_arrays()).join(px[lo:hi], py[lo:hi], nthreads=2)
-        pairs = np.stack([pt + lo, pl.astype(np.int64)], 1)
-        gathered = [None] * world
-        dist.all_gather_object(gathered, pairs)
-        tot = all_reduce_scalar(dist, len(pairs), "sum")
+        if rank == 1:   # unequal per-rank counts exercise the padded gather
+            pt, pl = pt[: len(pt) // 2], pl[: len(pl) // 2]
+        g = gather_rows(dist, [torch.from_numpy(pt + lo), torch.from_numpy(pl.astype(np.int32))])
+        tot = all_reduce_scalar(dist, len(pt), "sum")
         mx = all_reduce_scalar(dist, float(rank + 1), "max")
         if rank == 0:
-            q.put((np.concatenate(gathered), tot, mx, ps.vx.sum(), ps.n_polys))
+            pairs = np.stack([g[0].numpy(), g[1].numpy().astype(np.int64)], 1)
+            q.put((pairs, tot, mx, ps.vx.sum(), ps.n_polys))
+        else:
+            assert g is None
     finally:
         dist.destroy_process_group()
 
@@ -67,8 +71,17 @@ def test_sharded_join_equals_global(world, oracle):
     ps = synthetic_counties(20, 10)
     assert npoly == ps.n_polys and vxsum == ps.vx.sum()      # broadcast delivered the same set
     px, py = synthetic_points(n_total, seed=21)
-    opt, opl = oracle.OraclePolySet(*ps.to_arrays()).join(px, py, nthreads=4)
-    exp = np.stack([opt, opl.astype(np.int64)], 1)
+    from geomesa_amd.shard import shard_bounds
+    exp = []
+    for r in range(world):   # each rank's shard joined alone (rank 1 keeps half its pairs)
+        lo, hi = shard_bounds(n_total, r, world)
+        opt, opl = oracle.OraclePolySet(*ps.to_arrays()).join(px[lo:hi], py[lo:hi], nthreads=4)
+        if r == 1:
+            opt, opl = opt[: len(opt) // 2], opl[: len(opl) // 2]
+        exp.append(np.stack([opt + lo, opl.astype(np.int64)], 1))
+    exp = np.concatenate(exp)
+    assert np.array_equal(got, exp)             # rank order, each rank's order kept
+    exp = exp[np.lexsort((exp[:, 1], exp[:, 0]))]
     got = got[np.lexsort((got[:, 1], got[:, 0]))]
     assert np.array_equal(got, exp)
     assert tot == len(exp) and mx == float(world)
