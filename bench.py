@@ -332,13 +332,42 @@ def main():
         rec("z3filter_scan", lambda: lib.gm_z3filter_scan(h, fbuf, len(fb), br.ctypes.data, len(br) // 2, P(b), P(z),
                                                          N, P(mask), None, 0, None), 10.125, N, unit="rows/s")
         del mask
-        # XZ2 index of envelopes (configs[4]): reuse x/y as min corners, jittered max corners
-        NX = min(N, 200_000_000)
-        xmax = torch.clamp(x[:NX] + 0.01, max=180.0); ymax = torch.clamp(y[:NX] + 0.005, max=90.0)
+        # XZ2 / XZ3 index of 100M envelopes (configs[4]): x/y as min corners, max corners a log-uniform
+        # [1e-6, 10] deg away; XZ3 time extent 1 s .. 1 day inside the week
+        NX = min(N, 100_000_000)
+        g = torch.Generator(device=dev).manual_seed(11)
+        w = torch.pow(10.0, torch.rand(NX, device=dev, dtype=torch.float64, generator=g) * 7 - 6)
+        hgt = torch.pow(10.0, torch.rand(NX, device=dev, dtype=torch.float64, generator=g) * 7 - 6)
+        xmax = torch.clamp(x[:NX] + w, max=180.0); ymax = torch.clamp(y[:NX] + hgt, max=90.0)
+        del w, hgt
         xo = torch.empty(NX, dtype=torch.int64, device=dev)
         rec("xz2_index", lambda: lib.gm_xz2_index(h, P(x), P(y), P(xmax), P(ymax), NX, 12, 0, P(xo), None, None), 40,
             NX, unit="envelopes/s")
-        del xmax, ymax, xo
+        zmin = torch.remainder(t[:NX], 604_800_000).to(torch.float64) / 1000.0
+        zmax = torch.clamp(zmin + torch.pow(10.0, torch.rand(NX, device=dev, dtype=torch.float64, generator=g) * 4.94),
+                           max=604800.0)
+        rec("xz3_index", lambda: lib.gm_xz3_index(h, P(x), P(y), P(zmin), P(xmax), P(ymax), P(zmax), NX, 12, 1, 0, P(xo),
+                                                 None, None), 56, NX, unit="envelopes/s")
+        del xmax, ymax, xo, zmin, zmax
+        # batched XZ2 ranges (configs[4]): 100k query windows, log-uniform 0.01..20 deg, maxRanges 2000
+        rng = np.random.default_rng(2)
+        nq = 100_000
+        wq = 10 ** rng.uniform(-2, np.log10(20), (nq, 2)) / 2
+        cq = np.stack([rng.uniform(-180 + wq[:, 0], 180 - wq[:, 0]), rng.uniform(-90 + wq[:, 1], 90 - wq[:, 1])], 1)
+        win = np.ascontiguousarray(np.concatenate([cq - wq, cq + wq], 1).reshape(-1))
+        woff = np.arange(nq + 1, dtype=np.int32)
+        from geomesa_amd import ranges as R
+        args = (h, nq, woff.ctypes.data, win.ctypes.data, 12, 2000)
+        offs, rr, _ = R.call_raw(lib.gm_xz2_ranges, args, nq, nq * 256, pinned=True)
+        t0w = time.time()
+        for _ in range(3):
+            offs, rr, _ = R.call_raw(lib.gm_xz2_ranges, args, nq, int(offs[-1]) + 1024, pinned=True)
+        dt = (time.time() - t0w) / 3
+        extra["xz2_ranges_batch"] = {"value": nq * dist.world / dt, "unit": "queries/s", "ms_per_step": dt * 1e3,
+                                     "ranges": int(offs[-1]),
+                                     "note": "C-ABI call incl. H2D of windows and D2H of ranges (pinned host output); 100k XZ2 query "
+                                             "windows (0.01-20 deg), maxRanges 2000, g = 12"}
+        del rr
         # batched ranges (configs[4]/[0]): 4096 Z3 queries with target 2000
         rng = np.random.default_rng(1)
         qs = []
@@ -348,14 +377,14 @@ def main():
             qs.append(([(cx - w, cy - hh, cx + w, cy + hh)], [(t0, t0 + 86400)]))
         from geomesa_amd import ranges as R
         fn, args, nq, cap = R.prepare_z3(sfc, qs, 64, 2000)
-        offs, rr, _ = R.call_raw(fn, args, nq, cap)
+        offs, rr, _ = R.call_raw(fn, args, nq, cap, pinned=True)
         t0w = time.time()
         for _ in range(3):
-            R.call_raw(fn, args, nq, cap)
+            R.call_raw(fn, args, nq, cap, pinned=True)
         dt = (time.time() - t0w) / 3
         extra["z3_ranges_batch"] = {"value": len(qs) * dist.world / dt, "unit": "queries/s",
                                     "ms_per_step": dt * 1e3, "ranges": int(offs[-1]),
-                                    "note": "C-ABI call incl. H2D of queries and D2H of ranges; 4096 Z3 queries "
+                                    "note": "C-ABI call incl. H2D of queries and D2H of ranges (pinned host output); 4096 Z3 queries "
                                             "(0.2-20 deg boxes x 1 day), maxRanges 2000 (ScanRangesTarget)"}
     # ---------------------------------------------------------------- sorted table: ingest sort + seek-and-filter
     if "table" in only and not a.no_extra:

@@ -13,6 +13,84 @@ thread_local std::string g_last_error;
 
 namespace gm {
 
+constexpr size_t STAGE_HALF = (size_t)16 << 20;   // two 16 MiB halves
+
+static bool is_pinned(const void* p) {
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();   // unregistered pageable memory reports an error: clear it
+    return false;
+  }
+  return a.type == hipMemoryTypeHost || a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged;
+}
+
+static int stage(gm_ctx* ctx) {
+  if (!ctx->h_stage) GM_HIP(hipHostMalloc((void**)&ctx->h_stage, 2 * STAGE_HALF, hipHostMallocDefault));
+  return GM_OK;
+}
+
+int copy_d2h(gm_ctx* ctx, void* host, const void* dev, size_t bytes) {
+  if (!bytes) return GM_OK;
+  if (bytes <= 4096 || is_pinned(host)) {
+    GM_HIP(hipMemcpyAsync(host, dev, bytes, hipMemcpyDeviceToHost, ctx->stream));
+    GM_HIP(hipStreamSynchronize(ctx->stream));
+    return GM_OK;
+  }
+  int rc = stage(ctx);
+  if (rc) return rc;
+  // piece k lands in half k % 2; piece k's host copy overlaps piece k + 1's DMA
+  const char* src = (const char*)dev;
+  char* dst = (char*)host;
+  size_t off = 0, prev_off = 0, prev_len = 0;
+  int k = 0;
+  while (off < bytes || prev_len) {
+    size_t len = 0;
+    if (off < bytes) {
+      len = std::min(STAGE_HALF, bytes - off);
+      GM_HIP(hipMemcpyAsync(ctx->h_stage + (k % 2) * STAGE_HALF, src + off, len, hipMemcpyDeviceToHost, ctx->stream));
+    }
+    if (prev_len) memcpy(dst + prev_off, ctx->h_stage + ((k + 1) % 2) * STAGE_HALF, prev_len);
+    GM_HIP(hipStreamSynchronize(ctx->stream));
+    prev_off = off; prev_len = len; off += len; ++k;
+  }
+  return GM_OK;
+}
+
+int ctx_workspace(gm_ctx* ctx, int slot, size_t bytes, void** p) {
+  if (ctx->ws_cap[slot] < bytes) {
+    GM_HIP(hipStreamSynchronize(ctx->stream));
+    if (ctx->ws[slot]) GM_HIP(hipFree(ctx->ws[slot]));
+    ctx->ws[slot] = nullptr;
+    ctx->ws_cap[slot] = 0;
+    const size_t want = (bytes + bytes / 4 + 4095) & ~(size_t)4095;
+    GM_HIP(hipMalloc(&ctx->ws[slot], want));
+    ctx->ws_cap[slot] = want;
+  }
+  *p = ctx->ws[slot];
+  return GM_OK;
+}
+
+int copy_h2d(gm_ctx* ctx, void* dev, const void* host, size_t bytes) {
+  if (!bytes) return GM_OK;
+  if (bytes <= 4096 || is_pinned(host)) {
+    GM_HIP(hipMemcpyAsync(dev, host, bytes, hipMemcpyHostToDevice, ctx->stream));
+    GM_HIP(hipStreamSynchronize(ctx->stream));
+    return GM_OK;
+  }
+  int rc = stage(ctx);
+  if (rc) return rc;
+  const char* src = (const char*)host;
+  char* dst = (char*)dev;
+  for (size_t off = 0; off < bytes; off += STAGE_HALF) {
+    const size_t len = std::min(STAGE_HALF, bytes - off);
+    memcpy(ctx->h_stage, src + off, len);
+    GM_HIP(hipMemcpyAsync(dst + off, ctx->h_stage, len, hipMemcpyHostToDevice, ctx->stream));
+    GM_HIP(hipStreamSynchronize(ctx->stream));
+  }
+  return GM_OK;
+}
+
+
 void set_error(const std::string& msg) { g_last_error = msg; }
 
 int hip_fail(hipError_t e, const char* what) {
@@ -103,6 +181,15 @@ static int ctx_create(int device, void* stream, bool own, gm_ctx** out) {
   if (e == hipSuccess) e = hipEventCreate(&c->ev0);
   if (e == hipSuccess) e = hipEventCreate(&c->ev1);
   if (e != hipSuccess) { gm_ctx_destroy(c); return gm::hip_fail(e, "gm_ctx_create"); }
+  // The scans, sort, partitioned join and range batches take their temporaries with
+  // hipMallocAsync.  With the pool's default release threshold (0) every synchronisation hands the
+  // memory back and the next call maps it again (seconds for multi-GB range workspaces), so the
+  // device's default pool keeps what it has reserved, as a caching allocator does.
+  hipMemPool_t pool = nullptr;
+  if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess && pool) {
+    uint64_t keep = UINT64_MAX;
+    (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+  }
   *out = c;
   return GM_OK;
 }
@@ -117,6 +204,9 @@ int gm_ctx_destroy(gm_ctx* c) {
   if (c->d_err) (void)hipFree(c->d_err);
   if (c->d_scratch) (void)hipFree(c->d_scratch);
   if (c->h_pinned) (void)hipHostFree(c->h_pinned);
+  if (c->h_stage) (void)hipHostFree(c->h_stage);
+  for (void* w : c->ws)
+    if (w) (void)hipFree(w);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
@@ -144,16 +234,12 @@ int gm_device_free(gm_ctx* c, void* ptr) {
   return GM_OK;
 }
 int gm_copy_to_device(gm_ctx* c, void* dst, const void* src, size_t bytes) {
-  if (!c) return GM_E_INVALID;
-  GM_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream));
-  GM_HIP(hipStreamSynchronize(c->stream));
-  return GM_OK;
+  if (!c || (bytes && (!dst || !src))) return GM_E_INVALID;
+  return gm::copy_h2d(c, dst, src, bytes);
 }
 int gm_copy_to_host(gm_ctx* c, void* dst, const void* src, size_t bytes) {
-  if (!c) return GM_E_INVALID;
-  GM_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream));
-  GM_HIP(hipStreamSynchronize(c->stream));
-  return GM_OK;
+  if (!c || (bytes && (!dst || !src))) return GM_E_INVALID;
+  return gm::copy_d2h(c, dst, src, bytes);
 }
 int gm_timer_start(gm_ctx* c) {
   if (!c) return GM_E_INVALID;

@@ -628,24 +628,27 @@ struct ScanBufs {
   int32_t* desc = nullptr;
 };
 
-// scratch buffers per call (hipMallocAsync keeps them stream-ordered)
+// scratch buffers per call, carved from the context's scan workspace (stream-ordered reuse)
 int alloc_scan(gm_ctx* ctx, int64_t n, uint64_t* user_mask, size_t desc_words, ScanBufs& b) {
   const int64_t nblocks = (n + FROWS - 1) / FROWS;
   const int64_t nwords = nblocks * (FROWS / 64);
-  if (!user_mask) GM_HIP(hipMallocAsync((void**)&b.mask, (size_t)nwords * 8, ctx->stream));
-  else b.mask = (uint64_t*)user_mask;
-  GM_HIP(hipMallocAsync((void**)&b.counts, (size_t)nblocks * 4 + 4, ctx->stream));
-  GM_HIP(hipMallocAsync((void**)&b.offsets, (size_t)(nblocks + 1) * 8, ctx->stream));
-  if (desc_words) GM_HIP(hipMallocAsync((void**)&b.desc, desc_words * 4, ctx->stream));
+  const size_t a_mask = user_mask ? 0 : (size_t)nwords * 8;
+  const size_t a_cnt = ((size_t)nblocks * 4 + 4 + 15) & ~(size_t)15;
+  const size_t a_off = ((size_t)(nblocks + 1) * 8 + 15) & ~(size_t)15;
+  const size_t a_desc = (desc_words * 4 + 15) & ~(size_t)15;
+  void* base = nullptr;
+  int rc = ctx_workspace(ctx, WS_SCAN, a_mask + a_cnt + a_off + a_desc + 16, &base);
+  if (rc) return rc;
+  char* p = (char*)base;
+  b.mask = user_mask ? user_mask : (uint64_t*)p;
+  p += a_mask;
+  b.counts = (int32_t*)p; p += a_cnt;
+  b.offsets = (int64_t*)p; p += a_off;
+  b.desc = desc_words ? (int32_t*)p : nullptr;
   return GM_OK;
 }
 
-void free_scan(gm_ctx* ctx, uint64_t* user_mask, ScanBufs& b) {
-  if (!user_mask && b.mask) (void)hipFreeAsync(b.mask, ctx->stream);
-  if (b.counts) (void)hipFreeAsync(b.counts, ctx->stream);
-  if (b.offsets) (void)hipFreeAsync(b.offsets, ctx->stream);
-  if (b.desc) (void)hipFreeAsync(b.desc, ctx->stream);
-}
+void free_scan(gm_ctx*, uint64_t*, ScanBufs&) {}   // workspace memory stays with the context
 
 // passes B and C + count readback
 int finish_scan(gm_ctx* ctx, int64_t n, ScanBufs& b, int64_t* ids, int64_t ids_cap, int64_t* n_match) {
@@ -849,7 +852,8 @@ int gm_key_range_scan(gm_ctx* ctx, const uint8_t* shard, const int16_t* bin, con
   GM_HIP(hipMallocAsync((void**)&d_rg, (size_t)nr * sizeof(DevRange), s));
   GM_HIP(hipMallocAsync((void**)&start, (size_t)nr * 8, s));
   GM_HIP(hipMallocAsync((void**)&coff, (size_t)(nr + 1) * 8, s));
-  GM_HIP(hipMemcpyAsync(d_rg, dr.data(), (size_t)nr * sizeof(DevRange), hipMemcpyHostToDevice, s));
+  int crc = copy_h2d(ctx, d_rg, dr.data(), (size_t)nr * sizeof(DevRange));
+  if (crc) return crc;
   hipLaunchKernelGGL(k_range_bounds, dim3((unsigned)((nr + FTPB - 1) / FTPB)), dim3(FTPB), 0, s, shard,
                      (const uint16_t*)bin, (const uint64_t*)z, n, d_rg, nr, start, coff);
   hipLaunchKernelGGL(k_scan_i64, dim3(1), dim3(1024), 0, s, coff, nr);

@@ -16,6 +16,9 @@ struct gm_ctx {
   int64_t* d_err = nullptr;        // [0] error count, [1] packed (first index << 8 | code)
   int64_t* d_scratch = nullptr;    // small device scratch: counters
   int64_t* h_pinned = nullptr;     // pinned host mirror for summaries / counters
+  char* h_stage = nullptr;         // pinned staging for copies to / from pageable host memory (2 halves)
+  void* ws[4] = {nullptr, nullptr, nullptr, nullptr};   // reusable device workspaces (see ctx_workspace)
+  size_t ws_cap[4] = {0, 0, 0, 0};
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
 };
 
@@ -37,6 +40,21 @@ __device__ __forceinline__ void report_error(int64_t* err, int64_t idx, uint8_t 
   atomicAdd((unsigned long long*)&err[0], 1ull);
   atomicMin((long long*)&err[1], (long long)((idx << 8) | code));
 }
+
+// Host <-> device copies of caller host memory.  Pinned (hipHostMalloc'd / registered) memory is
+// copied directly; pageable memory goes through the context's pinned staging buffer in
+// double-buffered pieces (direct DMA to pageable memory degrades badly on this stack: a 256 MB
+// result copy took 0.3-7 s and grew from call to call, against 80 ms through pinned memory).
+// Both synchronise the context stream.
+int copy_d2h(gm_ctx* ctx, void* host, const void* dev, size_t bytes);
+int copy_h2d(gm_ctx* ctx, void* dev, const void* host, size_t bytes);
+
+// A device workspace owned by the context, grown on demand and reused by later calls (calls on
+// one context are stream-ordered, so reuse is safe).  Large per-call temporaries come from here
+// rather than hipMallocAsync: on this stack multi-GB pool allocations were re-mapped on every call
+// (0.7-6 s stalls between launches).  slot: 0 = range batches, 1 = sort, 2 = scans, 3 = join.
+enum : int { WS_RANGES = 0, WS_SORT = 1, WS_SCAN = 2, WS_JOIN = 3 };
+int ctx_workspace(gm_ctx* ctx, int slot, size_t bytes, void** p);
 
 // reset the error summary before a call that reports one
 int begin_summary(gm_ctx* ctx, gm_batch_status* summary);

@@ -718,9 +718,8 @@ int upload(gm_pip_index* ix, const std::vector<T>& v, const T** out) {
   void* p = nullptr;
   GM_HIP(hipMalloc(&p, std::max<size_t>(v.size() * sizeof(T), 16)));
   ix->allocs.push_back(p);
-  if (!v.empty()) GM_HIP(hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
   *out = (const T*)p;
-  return GM_OK;
+  return v.empty() ? GM_OK : copy_h2d(ix->ctx, p, v.data(), v.size() * sizeof(T));
 }
 
 struct BandSeg {
@@ -1160,9 +1159,14 @@ int gm_pip_join_ex(gm_ctx* ctx, const gm_pip_index* ix, const double* px, const 
     const int64_t hlen = (int64_t)nb * nblk;
     uint32_t* hist = nullptr;
     PtRec* rec = nullptr;
-    GM_HIP(hipMallocAsync((void**)&hist, (size_t)(hlen + 1) * 4, ctx->stream));
-    hipError_t e = hipMallocAsync((void**)&rec, (size_t)mmax * sizeof(PtRec), ctx->stream);
-    if (e != hipSuccess) { (void)hipFreeAsync(hist, ctx->stream); return hip_fail(e, "hipMallocAsync(join records)"); }
+    {  // context-owned workspace: records | histogram
+      const size_t a_rec = (size_t)mmax * sizeof(PtRec), a_h = (size_t)(hlen + 1) * 4;
+      void* base = nullptr;
+      int wrc = ctx_workspace(ctx, WS_JOIN, a_rec + a_h, &base);
+      if (wrc) return wrc;
+      rec = (PtRec*)base;
+      hist = (uint32_t*)((char*)base + a_rec);
+    }
     int rc = GM_OK;
     for (int64_t c0 = 0; c0 < n && rc == GM_OK; c0 += CHUNK) {
       const int64_t m = std::min(CHUNK, n - c0);
@@ -1184,8 +1188,6 @@ int gm_pip_join_ex(gm_ctx* ctx, const gm_pip_index* ix, const double* px, const 
                            n_rec, m, id_base + c0, ix->dev, pt_ids, poly_ids, cap, counter);
       if (hipGetLastError() != hipSuccess) rc = hip_fail(hipErrorLaunchFailure, "k_pip_join (partitioned)");
     }
-    (void)hipFreeAsync(rec, ctx->stream);
-    (void)hipFreeAsync(hist, ctx->stream);
     if (rc) return rc;
   }
   if (n_pairs) {

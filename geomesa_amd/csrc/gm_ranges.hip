@@ -674,10 +674,9 @@ using namespace gm;
 namespace {
 
 template <class T>
-int to_dev(hipStream_t s, const T* h, size_t n, T** d) {
-  GM_HIP(hipMallocAsync((void**)d, std::max<size_t>(n * sizeof(T), 16), s));
-  if (n) GM_HIP(hipMemcpyAsync(*d, h, n * sizeof(T), hipMemcpyHostToDevice, s));
-  return GM_OK;
+int to_dev(gm_ctx* ctx, const T* h, size_t n, T** d) {
+  GM_HIP(hipMallocAsync((void**)d, std::max<size_t>(n * sizeof(T), 16), ctx->stream));
+  return copy_h2d(ctx, *d, h, n * sizeof(T));
 }
 
 // shared driver: per chunk of queries allocate workspaces, launch, read counts, gather, copy out
@@ -686,9 +685,14 @@ int run_ranges(gm_ctx* ctx, int64_t nq, int64_t fcap, int64_t rcap, size_t felem
                gm_range* out, int64_t cap, int64_t* needed, int32_t* query_status) {
   hipStream_t s = ctx->stream;
   rcap = next_pow2(std::max<int64_t>(rcap, 16));
-  // chunk so that the workspace stays within ~2 GiB
+  // chunk so that the workspace stays within min(4 GiB, 1/4 of free HBM): the worst-case caps per
+  // query are large but mostly untouched, and fewer chunks mean fewer launches and host syncs
   const int64_t per_q = fcap * (int64_t)felem * 2 + rcap * (8 + 8 + 1 + 8 + 4 + (int64_t)sizeof(gm_range));
-  int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(nq, ((int64_t)2 << 30) / std::max<int64_t>(per_q, 1)));
+  size_t free_b = 0, total_b = 0;
+  int64_t budget = (int64_t)2 << 30;
+  if (hipMemGetInfo(&free_b, &total_b) == hipSuccess)
+    budget = std::max<int64_t>(budget, std::min<int64_t>((int64_t)4 << 30, (int64_t)(free_b / 4)));
+  int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(nq, budget / std::max<int64_t>(per_q, 1)));
   chunk = std::min<int64_t>(chunk, 65535);
   std::vector<int32_t> counts((size_t)nq), stats((size_t)nq);
   std::vector<int64_t> offs((size_t)nq + 1, 0);
@@ -702,21 +706,26 @@ int run_ranges(gm_ctx* ctx, int64_t nq, int64_t fcap, int64_t rcap, size_t felem
     uint8_t* rc;
     int32_t *gidx, *dcnt, *dst;
     gm_range *ws, *dout;
-    GM_HIP(hipMallocAsync((void**)&fa, (size_t)(m * fcap) * felem, s));
-    GM_HIP(hipMallocAsync((void**)&fb, (size_t)(m * fcap) * felem, s));
-    GM_HIP(hipMallocAsync((void**)&rlo, (size_t)(m * rcap) * 8, s));
-    GM_HIP(hipMallocAsync((void**)&rhi, (size_t)(m * rcap) * 8, s));
-    GM_HIP(hipMallocAsync((void**)&rc, (size_t)(m * rcap), s));
-    GM_HIP(hipMallocAsync((void**)&gkey, (size_t)(m * rcap) * 8, s));
-    GM_HIP(hipMallocAsync((void**)&gidx, (size_t)(m * rcap) * 4, s));
-    GM_HIP(hipMallocAsync((void**)&ws, (size_t)(m * rcap) * sizeof(gm_range), s));
-    GM_HIP(hipMallocAsync((void**)&dcnt, (size_t)m * 4, s));
-    GM_HIP(hipMallocAsync((void**)&dst, (size_t)m * 4, s));
+    {  // one context-owned workspace, carved into the per-chunk arrays (16-B aligned pieces)
+      const size_t sizes[10] = {(size_t)(m * fcap) * felem, (size_t)(m * fcap) * felem, (size_t)(m * rcap) * 8,
+                                (size_t)(m * rcap) * 8,     (size_t)(m * rcap),          (size_t)(m * rcap) * 8,
+                                (size_t)(m * rcap) * 4,     (size_t)(m * rcap) * sizeof(gm_range),
+                                (size_t)m * 4,              (size_t)m * 4};
+      size_t total_b = 0, offs[10];
+      for (int i = 0; i < 10; ++i) { offs[i] = total_b; total_b += (sizes[i] + 15) & ~(size_t)15; }
+      void* base = nullptr;
+      int wrc = ctx_workspace(ctx, WS_RANGES, total_b, &base);
+      if (wrc) return wrc;
+      char* b = (char*)base;
+      fa = b + offs[0]; fb = b + offs[1]; rlo = (int64_t*)(b + offs[2]); rhi = (int64_t*)(b + offs[3]);
+      rc = (uint8_t*)(b + offs[4]); gkey = (int64_t*)(b + offs[5]); gidx = (int32_t*)(b + offs[6]);
+      ws = (gm_range*)(b + offs[7]); dcnt = (int32_t*)(b + offs[8]); dst = (int32_t*)(b + offs[9]);
+    }
     launch(q0, m, fcap, rcap, fa, fb, rlo, rhi, rc, gkey, gidx, ws, dcnt, dst);
     GM_CHECK_LAUNCH();
-    GM_HIP(hipMemcpyAsync(counts.data() + q0, dcnt, (size_t)m * 4, hipMemcpyDeviceToHost, s));
-    GM_HIP(hipMemcpyAsync(stats.data() + q0, dst, (size_t)m * 4, hipMemcpyDeviceToHost, s));
-    GM_HIP(hipStreamSynchronize(s));
+    int crc = copy_d2h(ctx, counts.data() + q0, dcnt, (size_t)m * 4);
+    if (!crc) crc = copy_d2h(ctx, stats.data() + q0, dst, (size_t)m * 4);
+    if (crc) return crc;
     int64_t ctotal = 0;
     std::vector<int64_t> loff((size_t)m + 1, 0);
     for (int64_t i = 0; i < m; ++i) {
@@ -725,21 +734,22 @@ int run_ranges(gm_ctx* ctx, int64_t nq, int64_t fcap, int64_t rcap, size_t felem
     }
     ctotal = loff[m];
     if (total + ctotal <= cap && ctotal > 0) {
-      GM_HIP(hipMallocAsync((void**)&doff, (size_t)(m + 1) * 8, s));
-      GM_HIP(hipMallocAsync((void**)&dout, (size_t)ctotal * sizeof(gm_range), s));
-      GM_HIP(hipMemcpyAsync(doff, loff.data(), (size_t)(m + 1) * 8, hipMemcpyHostToDevice, s));
+      void* gbase = nullptr;
+      const size_t oa = ((size_t)(m + 1) * 8 + 15) & ~(size_t)15;
+      int crc = ctx_workspace(ctx, WS_SCAN, oa + (size_t)ctotal * sizeof(gm_range), &gbase);
+      if (crc) return crc;
+      doff = (int64_t*)gbase;
+      dout = (gm_range*)((char*)gbase + oa);
+      crc = copy_h2d(ctx, doff, loff.data(), (size_t)(m + 1) * 8);
+      if (crc) return crc;
       hipLaunchKernelGGL(k_gather_ranges, dim3((unsigned)m), dim3(RTPB), 0, s, ws, rcap, doff, dout);
       GM_CHECK_LAUNCH();
-      GM_HIP(hipMemcpyAsync(out + total, dout, (size_t)ctotal * sizeof(gm_range), hipMemcpyDeviceToHost, s));
-      GM_HIP(hipFreeAsync(doff, s));
-      GM_HIP(hipFreeAsync(dout, s));
+      crc = copy_d2h(ctx, out + total, dout, (size_t)ctotal * sizeof(gm_range));
+      if (crc) return crc;
     } else if (total + ctotal > cap) {
       overflow = true;
     }
     total += ctotal;
-    for (void* p : {(void*)fa, (void*)fb, (void*)rlo, (void*)rhi, (void*)rc, (void*)gkey, (void*)gidx, (void*)ws,
-                    (void*)dcnt, (void*)dst})
-      GM_HIP(hipFreeAsync(p, s));
     GM_HIP(hipStreamSynchronize(s));
   }
   if (query_status) for (int64_t i = 0; i < nq; ++i) query_status[i] = stats[i];
@@ -771,10 +781,10 @@ int gm_z3_ranges(gm_ctx* ctx, int64_t nq, const int32_t* box_off, const double* 
   int32_t *dbo, *dto;
   double* dxy;
   int64_t* dt;
-  int rc = to_dev(s, box_off, (size_t)nq + 1, &dbo);
-  if (!rc) rc = to_dev(s, time_off, (size_t)nq + 1, &dto);
-  if (!rc) rc = to_dev(s, xy, (size_t)nbox * 4, &dxy);
-  if (!rc) rc = to_dev(s, t, (size_t)ntim * 2, &dt);
+  int rc = to_dev(ctx, box_off, (size_t)nq + 1, &dbo);
+  if (!rc) rc = to_dev(ctx, time_off, (size_t)nq + 1, &dto);
+  if (!rc) rc = to_dev(ctx, xy, (size_t)nbox * 4, &dxy);
+  if (!rc) rc = to_dev(ctx, t, (size_t)ntim * 2, &dt);
   if (rc) return rc;
   ZRangesArgs a{};
   a.box_off = dbo; a.xy = dxy; a.time_off = dto; a.t = dt;
@@ -810,8 +820,8 @@ int gm_z2_ranges(gm_ctx* ctx, int64_t nq, const int32_t* box_off, const double* 
   const int64_t nbox = box_off[nq];
   int32_t* dbo;
   double* dxy;
-  int rc = to_dev(s, box_off, (size_t)nq + 1, &dbo);
-  if (!rc) rc = to_dev(s, xy, (size_t)nbox * 4, &dxy);
+  int rc = to_dev(ctx, box_off, (size_t)nq + 1, &dbo);
+  if (!rc) rc = to_dev(ctx, xy, (size_t)nbox * 4, &dxy);
   if (rc) return rc;
   ZRangesArgs a{};
   a.box_off = dbo; a.xy = dxy; a.time_off = nullptr; a.t = nullptr;
@@ -845,8 +855,8 @@ static int xz_ranges(gm_ctx* ctx, int D, int64_t nq, const int32_t* win_off, con
   const int64_t nw = win_off[nq];
   int32_t* dwo;
   double* dw;
-  int rc = to_dev(s, win_off, (size_t)nq + 1, &dwo);
-  if (!rc) rc = to_dev(s, windows, (size_t)nw * 2 * D, &dw);
+  int rc = to_dev(ctx, win_off, (size_t)nq + 1, &dwo);
+  if (!rc) rc = to_dev(ctx, windows, (size_t)nw * 2 * D, &dw);
   if (rc) return rc;
   XZRangesArgs a{};
   a.win_off = dwo; a.win = dw; a.g = g; a.zhi = (double)max_offset(period);

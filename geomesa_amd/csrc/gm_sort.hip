@@ -290,12 +290,21 @@ int gm_sort_keys(gm_ctx* ctx, const uint8_t* shard, const int16_t* bin, const in
   uint16_t* tbin = nullptr;
   uint64_t* tz = nullptr;
   uint32_t *p0 = nullptr, *p1 = nullptr, *hist = nullptr;
-  if (sh) GM_HIP(hipMallocAsync((void**)&tsh, (size_t)n, s));
-  GM_HIP(hipMallocAsync((void**)&tbin, (size_t)n * 2, s));
-  GM_HIP(hipMallocAsync((void**)&tz, (size_t)n * 8, s));
-  GM_HIP(hipMallocAsync((void**)&p0, (size_t)n * 4, s));
-  GM_HIP(hipMallocAsync((void**)&p1, (size_t)n * 4, s));
-  GM_HIP(hipMallocAsync((void**)&hist, (size_t)256 * grid * 4, s));
+  {  // context-owned workspace: z | perm 0 | perm 1 | bin | hist | shard, 16-B aligned pieces
+    auto al = [](size_t v) { return (v + 15) & ~(size_t)15; };
+    const size_t a_z = al((size_t)n * 8), a_p = al((size_t)n * 4), a_b = al((size_t)n * 2),
+                 a_h = al((size_t)256 * grid * 4), a_s = sh ? al((size_t)n) : 0;
+    void* base = nullptr;
+    int wrc = ctx_workspace(ctx, WS_SORT, a_z + 2 * a_p + a_b + a_h + a_s, &base);
+    if (wrc) return wrc;
+    char* q = (char*)base;
+    tz = (uint64_t*)q; q += a_z;
+    p0 = (uint32_t*)q; q += a_p;
+    p1 = (uint32_t*)q; q += a_p;
+    tbin = (uint16_t*)q; q += a_b;
+    hist = (uint32_t*)q; q += a_h;
+    if (sh) tsh = (uint8_t*)q;
+  }
   const uint8_t* ish = sh;
   const uint16_t* ibin = (const uint16_t*)bin;
   const uint64_t* iz = (const uint64_t*)z;
@@ -319,8 +328,6 @@ int gm_sort_keys(gm_ctx* ctx, const uint8_t* shard, const int16_t* bin, const in
                        iperm, n, perm_out);
     if (hipGetLastError() != hipSuccess) rc = hip_fail(hipErrorLaunchFailure, "k_widen_perm");
   }
-  for (void* p : {(void*)tsh, (void*)tbin, (void*)tz, (void*)p0, (void*)p1, (void*)hist})
-    if (p) (void)hipFreeAsync(p, s);
   return rc;
 }
 
