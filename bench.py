@@ -45,7 +45,7 @@ def parse():
     p.add_argument("--only", default="", help="comma list: z3,join,extra,table (profiling)")
     p.add_argument("--table-rows", type=int, default=250_000_000,
                    help="rows per GPU of the sorted-table leg (configs[2]: 2B rows over 8 GPUs)")
-    p.add_argument("--join-mode", default="auto", choices=["auto", "direct", "partitioned"])
+    p.add_argument("--join-mode", default="auto", choices=["auto", "direct", "partitioned", "split"])
     p.add_argument("--cells-per-poly", type=int, default=0, help="join grid density (0 = library default)")
     p.add_argument("--join-grid", default="80x40", help="synthetic county grid (experiments)")
     p.add_argument("--no-gather", action="store_true", help="skip the join's result gather to rank 0")

@@ -25,6 +25,7 @@ GM_ST_UNORDERED = 3
 GM_JOIN_AUTO = 0
 GM_JOIN_DIRECT = 1
 GM_JOIN_PARTITIONED = 2
+GM_JOIN_SPLIT = 3
 
 
 class GeomesaHipUnavailable(RuntimeError):

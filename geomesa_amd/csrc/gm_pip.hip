@@ -227,6 +227,8 @@ constexpr int JTPB = 256;             // 4 waves
 constexpr int JILP = GM_JILP;         // points per lane per tile (their lookups overlap)
 constexpr int WCAP = 512;             // LDS pair staging per wave (4 KiB)
 constexpr int QCAP = 128;             // LDS blob work queue per wave (3 KiB)
+constexpr int WCAP_S = 256;           // split mode: pair staging per wave (2 KiB)
+constexpr int QCAP_S = 256;           // split mode: (row, blob) work items per wave (2 KiB)
 constexpr int JTILE = JTPB * JILP;
 
 __device__ __forceinline__ int lanes_below(uint64_t m) {
@@ -264,6 +266,35 @@ struct PtRec {
   uint32_t pad;
 };
 
+// Split-pass outputs.  Every wave of the split pass owns a private segment of the work list and of
+// the pair list, sized for the points it can see (its block's tiles x 64 lanes x JILP, times the
+// most boundary / total entries any cell has), and appends with a wave-uniform cursor: no atomics.
+// A shared head word was the bottleneck of the first split version -- one returning atomic per
+// flush saturates near 88 per us chip-wide (MI355X_MICROARCH.md, dequeue row): 3.2M flushes cost
+// 13 ms of the pass.  k_pip_blobs walks the segments and appends its hits to the same segment's
+// pairs (an atomic on that segment's count, contended by one block only); k_pip_compact packs the
+// segments into the caller's arrays.
+struct SplitArgs {
+  uint2* items;        // [nseg][ipw] (row, blob ref)
+  uint32_t* item_cnt;  // [nseg]
+  int64_t ipw;
+  uint2* pairs;        // [nseg][ppw] (row, polygon)
+  uint32_t* pair_cnt;  // [nseg]
+  int64_t ppw;
+  int64_t* pair_off;   // [nseg + 1] scanned pair counts (k_pip_compact)
+  int32_t nseg;
+};
+
+// append cnt staged entries at the wave's cursor (wave-uniform), clipped to the segment capacity
+__device__ __forceinline__ void append_seg(const uint2* src, int cnt, int lane, uint2* __restrict__ seg, int64_t& cur,
+                                           int64_t segcap) {
+  wave_lds_sync();
+  for (int j = lane; j < cnt; j += 64)
+    if (cur + j < segcap) seg[cur + j] = src[j];
+  cur += cnt;
+  wave_lds_sync();
+}
+
 // Persistent grid-stride over tiles of JTILE points; every wave works independently.
 // A point's candidate work is a list of items: its cell word (INTERIOR -> match, BOUNDARY -> one
 // blob), or, for a LIST cell, one item per (cell, polygon) entry.  Items are walked one per lane per
@@ -275,24 +306,36 @@ struct PtRec {
 #ifndef GM_JOIN_WAVES
 #define GM_JOIN_WAVES 1
 #endif
-template <bool WRITE, bool REC>
+//
+// SPLIT (the direct pass): blob items are not evaluated here but appended, as (row, blob) pairs of
+// 8 B, to a global work list that k_pip_blobs evaluates next.  Without the blob code the kernel fits
+// 64 VGPRs and 16 KiB of LDS per block, i.e. 8 waves per SIMD instead of 4, which is what the
+// lookup chain (point -> coarse word -> fine word -> list) needs to hide its latency.
+template <bool WRITE, bool REC, bool SPLIT>
 __global__ __launch_bounds__(JTPB, GM_JOIN_WAVES) void k_pip_join(const double* __restrict__ px, const double* __restrict__ py,
                                                    const PtRec* __restrict__ rec, const uint32_t* __restrict__ n_rec,
                                                    int64_t n, int64_t id_base, PipDev d, int64_t* __restrict__ pt_ids,
                                                    int32_t* __restrict__ poly_ids, int64_t cap,
-                                                   unsigned long long* __restrict__ counter) {
+                                                   unsigned long long* __restrict__ counter, SplitArgs sp) {
   constexpr int NW = JTPB / 64;
-  __shared__ uint32_t s_pt[WRITE ? NW * WCAP : 1];
-  __shared__ int32_t s_poly[WRITE ? NW * WCAP : 1];
-  __shared__ double s_qx[NW * QCAP], s_qy[NW * QCAP];
-  __shared__ uint32_t s_qid[NW * QCAP], s_qb[NW * QCAP];
+  constexpr int WC = SPLIT ? WCAP_S : WCAP;
+  __shared__ uint32_t s_pt[WRITE && !SPLIT ? NW * WC : 1];
+  __shared__ int32_t s_poly[WRITE && !SPLIT ? NW * WC : 1];
+  __shared__ uint2 s_pp[WRITE && SPLIT ? NW * WC : 1];     // split: (row, polygon) staging
+  __shared__ double s_qx[SPLIT ? 1 : NW * QCAP], s_qy[SPLIT ? 1 : NW * QCAP];
+  __shared__ uint32_t s_qid[SPLIT ? 1 : NW * QCAP], s_qb[SPLIT ? 1 : NW * QCAP];
+  __shared__ uint2 s_qi[SPLIT ? NW * QCAP_S : 1];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  uint32_t* wpt = s_pt + (WRITE ? wv * WCAP : 0);
-  int32_t* wpl = s_poly + (WRITE ? wv * WCAP : 0);
-  double* qx = s_qx + wv * QCAP;
-  double* qy = s_qy + wv * QCAP;
-  uint32_t* qid = s_qid + wv * QCAP;
-  uint32_t* qb = s_qb + wv * QCAP;
+  uint32_t* wpt = s_pt + (WRITE ? wv * WC : 0);
+  int32_t* wpl = s_poly + (WRITE ? wv * WC : 0);
+  double* qx = s_qx + (SPLIT ? 0 : wv * QCAP);
+  double* qy = s_qy + (SPLIT ? 0 : wv * QCAP);
+  uint32_t* qid = s_qid + (SPLIT ? 0 : wv * QCAP);
+  uint32_t* qb = s_qb + (SPLIT ? 0 : wv * QCAP);
+  uint2* qi = s_qi + (SPLIT ? wv * QCAP_S : 0);
+  uint2* wpp = s_pp + (WRITE && SPLIT ? wv * WC : 0);
+  const int64_t seg = (int64_t)blockIdx.x * NW + wv;   // split: this wave's private segments
+  int64_t icur = 0, pcur = 0;
   int wn = 0, qn = 0;   // wave-uniform fills of the pair staging and the blob queue
   int my_count = 0;
   if (REC) n = *n_rec;
@@ -378,7 +421,7 @@ __global__ __launch_bounds__(JTPB, GM_JOIN_WAVES) void k_pip_join(const double* 
     for (int k = 0;; ++k) {
       const bool act = k < ntot;
       const bool any = __ballot(act) != 0;
-      if (!any && (have ? qn < 64 : qn == 0)) break;
+      if (!any && (have ? qn < (SPLIT ? QCAP_S - 64 : 64) : qn == 0)) break;
       if (any) {
         // item k belongs to the last point u with pre[u] <= k (static selects, no register indexing)
         double ex = x[0], ey = y[0];
@@ -397,17 +440,30 @@ __global__ __launch_bounds__(JTPB, GM_JOIN_WAVES) void k_pip_join(const double* 
         if (!WRITE) my_count += hit;
         if (WRITE) {
           const uint64_t m = __ballot(hit);
-          if (hit) { const int o = wn + lanes_below(m); wpt[o] = eid; wpl[o] = (int32_t)(e & 0x3fffffffu); }
+          if (hit) {
+            const int o = wn + lanes_below(m);
+            if (SPLIT) wpp[o] = make_uint2(eid, e & 0x3fffffffu);
+            else { wpt[o] = eid; wpl[o] = (int32_t)(e & 0x3fffffffu); }
+          }
           wn += __popcll(m);
         }
         const uint64_t mq = __ballot(blob);
         if (blob) {
           const int o = qn + lanes_below(mq);
-          qx[o] = ex; qy[o] = ey; qid[o] = eid; qb[o] = e & 0x3fffffffu;
+          if (SPLIT) {
+            qi[o] = make_uint2(eid, e & 0x3fffffffu);
+          } else {
+            qx[o] = ex; qy[o] = ey; qid[o] = eid; qb[o] = e & 0x3fffffffu;
+          }
         }
         qn += __popcll(mq);
       }
-      if (qn >= 64 || (!have && !any && qn > 0)) {   // evaluate the newest min(qn, 64) queued items
+      if (SPLIT) {
+        if (qn >= QCAP_S - 64 || (!have && !any && qn > 0)) {   // hand the wave's items to the work list
+          append_seg(qi, qn, lane, sp.items + seg * sp.ipw, icur, sp.ipw);
+          qn = 0;
+        }
+      } else if (qn >= 64 || (!have && !any && qn > 0)) {   // evaluate the newest min(qn, 64) queued items
         wave_lds_sync();
         const int kq = qn < 64 ? qn : 64;
         const int slot = qn - kq + lane;
@@ -442,19 +498,130 @@ __global__ __launch_bounds__(JTPB, GM_JOIN_WAVES) void k_pip_join(const double* 
           wn += __popcll(m);
         }
       }
-      if (WRITE && wn > WCAP - 128) {
-        flush_pairs(wpt, wpl, wn, lane, id_base, pt_ids, poly_ids, cap, counter);
+      if (WRITE && wn > WC - 128) {
+        if (SPLIT) append_seg(wpp, wn, lane, sp.pairs + seg * sp.ppw, pcur, sp.ppw);
+        else flush_pairs(wpt, wpl, wn, lane, id_base, pt_ids, poly_ids, cap, counter);
         wn = 0;
       }
     }
     if (!have) break;
     tile += t_step;
   }
-  if (WRITE && wn > 0) flush_pairs(wpt, wpl, wn, lane, id_base, pt_ids, poly_ids, cap, counter);
+  if (WRITE && wn > 0) {
+    if (SPLIT) append_seg(wpp, wn, lane, sp.pairs + seg * sp.ppw, pcur, sp.ppw);
+    else flush_pairs(wpt, wpl, wn, lane, id_base, pt_ids, poly_ids, cap, counter);
+  }
+  if (SPLIT && lane == 0) {
+    sp.item_cnt[seg] = (uint32_t)min(icur, sp.ipw);
+    if (WRITE) sp.pair_cnt[seg] = (uint32_t)min(pcur, sp.ppw);
+  }
   if (!WRITE) {
     for (int off = 32; off > 0; off >>= 1) my_count += __shfl_down(my_count, off, 64);
     if (lane == 0 && my_count) atomicAdd(counter, (unsigned long long)my_count);
   }
+}
+
+// Evaluation of the split pass's work list: one (row, blob) item per lane, every lane busy with
+// the same kind of work (JTS RayCrossingCounter over the blob's segments, compact or generic).
+// The row's coordinates are re-read from the point columns; items come in roughly ascending row
+// order (per wave and tile), so those reads stay within few lines per wave.
+template <bool WRITE>
+__global__ __launch_bounds__(JTPB) void k_pip_blobs(const double* __restrict__ px, const double* __restrict__ py,
+                                                    PipDev d, unsigned long long* __restrict__ counter, SplitArgs sp) {
+  constexpr int NW = JTPB / 64;
+  __shared__ uint2 s_pp[WRITE ? NW * WCAP : 1];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint2* wpp = s_pp + (WRITE ? wv * WCAP : 0);
+  int my_count = 0;
+  for (int64_t seg = blockIdx.x; seg < sp.nseg; seg += gridDim.x) {   // block-uniform
+    const uint2* items = sp.items + seg * sp.ipw;
+    const int64_t n = sp.item_cnt[seg];
+    int wn = 0;
+    for (int64_t b0 = wv * 64; b0 < n; b0 += JTPB) {   // wave-uniform
+      const int64_t i = b0 + lane;
+      bool hit = false;
+      int poly = 0;
+      uint32_t row = 0;
+      if (i < n) {
+        const uint2 it = items[i];
+        row = it.x;
+        const uint32_t ref = it.y;
+        const double ex = px[row], ey = py[row];
+        if (ref & BLOB_COMPACT) {
+          const dv2* c = (const dv2*)(d.compact + 16 * (uint64_t)(ref & (BLOB_COMPACT - 1)));
+          hit = compact_contains(c, ex, ey, poly);
+        } else {
+          const double* b = d.blob + 2 * (uint64_t)ref;
+          const int2 h = *(const int2*)b;
+          poly = h.x;
+          hit = blob_contains(d, b, h, ex, ey);
+        }
+      }
+      if (!WRITE) my_count += hit;
+      if (WRITE) {
+        const uint64_t m = __ballot(hit);
+        if (hit) wpp[wn + lanes_below(m)] = make_uint2(row, (uint32_t)poly);
+        wn += __popcll(m);
+        if (wn > WCAP - 64 || b0 + JTPB >= n) {   // the segment's last step flushes too
+          if (wn > 0) {
+            wave_lds_sync();
+            uint32_t base = 0;
+            if (lane == 0) base = atomicAdd(&sp.pair_cnt[seg], (uint32_t)wn);
+            base = __shfl(base, 0, 64);
+            uint2* dst = sp.pairs + seg * sp.ppw;
+            for (int j = lane; j < wn; j += 64)
+              if ((int64_t)base + j < sp.ppw) dst[base + j] = wpp[j];
+            wave_lds_sync();
+          }
+          wn = 0;
+        }
+      }
+    }
+  }
+  if (!WRITE) {
+    for (int off = 32; off > 0; off >>= 1) my_count += __shfl_down(my_count, off, 64);
+    if (lane == 0 && my_count) atomicAdd(counter, (unsigned long long)my_count);
+  }
+}
+
+// exclusive scan of the segments' pair counts (one block); total -> pair_off[nseg]
+__global__ __launch_bounds__(1024) void k_pip_scan_segs(SplitArgs sp) {
+  __shared__ int64_t part[1024];
+  const int t = threadIdx.x;
+  const int64_t len = sp.nseg, per = (len + 1023) / 1024, lo = t * per, hi = min(len, lo + per);
+  int64_t s = 0;
+  for (int64_t k = lo; k < hi; ++k) s += min((int64_t)sp.pair_cnt[k], sp.ppw);
+  part[t] = s;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {
+    const int64_t v = t >= off ? part[t - off] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  int64_t run = part[t] - s;
+  for (int64_t k = lo; k < hi; ++k) { sp.pair_off[k] = run; run += min((int64_t)sp.pair_cnt[k], sp.ppw); }
+  if (t == 1023) sp.pair_off[len] = part[1023];
+}
+
+// packs the segments into the caller's arrays after the pairs of earlier chunks (counter[0]);
+// pairs beyond cap are counted, not written
+__global__ __launch_bounds__(JTPB) void k_pip_compact(SplitArgs sp, const unsigned long long* __restrict__ counter,
+                                                      int64_t id_base, int64_t* __restrict__ pt_ids,
+                                                      int32_t* __restrict__ poly_ids, int64_t cap) {
+  const int64_t base = (int64_t)*counter;
+  for (int64_t seg = blockIdx.x; seg < sp.nseg; seg += gridDim.x) {
+    const int64_t o = base + sp.pair_off[seg], k = sp.pair_off[seg + 1] - sp.pair_off[seg];
+    const uint2* src = sp.pairs + seg * sp.ppw;
+    for (int64_t j = threadIdx.x; j < k; j += JTPB) {
+      const uint2 pr = src[j];
+      if (o + j < cap) { pt_ids[o + j] = id_base + (int64_t)pr.x; poly_ids[o + j] = (int32_t)pr.y; }
+    }
+  }
+}
+
+__global__ void k_pip_chunk_done(SplitArgs sp, unsigned long long* __restrict__ counter) {
+  if (threadIdx.x == 0) *counter += (unsigned long long)sp.pair_off[sp.nseg];
 }
 
 // ------------------------------------------------------------------ row-band partition
@@ -707,6 +874,8 @@ struct gm_pip_index {
   std::vector<void*> allocs;
   int32_t n_polys = 0;
   int64_t n_entries = 0, n_boundary = 0, n_records = 0, n_slow = 0, n_cells = 0, blob_bytes = 0, n_compact = 0;
+  int64_t max_bnd_per_cell = 0;   // most BOUNDARY (cell, polygon) entries of any cell: work items per point
+  int64_t max_ent_per_cell = 0;   // most (cell, polygon) entries of any cell: pairs per point
 };
 
 using namespace gm;
@@ -762,19 +931,24 @@ uint64_t right_parity(const std::vector<const BandSeg*>& right, double yb0,
 
 // persistent grid: exactly the resident block count of this kernel (a rounded multiple of 8 for
 // the XCD-aware mapping), so no partial second round of blocks forms a tail
-template <bool WRITE, bool REC>
-static unsigned join_grid(int device, int64_t ntiles) {
-  static int resident = 0;   // per instantiation; every device of the node is the same MI355X
+template <class K>
+static unsigned resident_grid(K kernel, int device, int64_t ntiles, bool xcd_multiple) {
+  static int resident = 0;   // per kernel instantiation; every device of the node is the same MI355X
   if (!resident) {
     int b = 0, n = 256;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_pip_join<WRITE, REC>, JTPB, 0) != hipSuccess || b < 1) b = 4;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kernel, JTPB, 0) != hipSuccess || b < 1) b = 4;
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess) n = prop.multiProcessorCount;
     resident = b * n;
   }
   int64_t g = std::min<int64_t>(resident, std::max<int64_t>(ntiles, 1));
-  if (REC) g = (g + 7) / 8 * 8;
+  if (xcd_multiple) g = (g + 7) / 8 * 8;
   return (unsigned)g;
+}
+
+template <bool WRITE, bool REC, bool SPLIT>
+static unsigned join_grid(int device, int64_t ntiles) {
+  return resident_grid(k_pip_join<WRITE, REC, SPLIT>, device, ntiles, REC);
 }
 
 extern "C" {
@@ -868,7 +1042,7 @@ int gm_pip_index_create_ex(gm_ctx* ctx, const gm_polyset* ps, int cells_per_poly
   // ---- (cell, polygon) classification + boundary blobs
   struct Ent { int64_t cell; uint32_t e; };
   std::vector<Ent> ents;
-  std::vector<int32_t> per_cell((size_t)ncell, 0);
+  std::vector<int32_t> per_cell((size_t)ncell, 0), bnd_cell((size_t)ncell, 0);
   std::vector<double> blob;            // 8-byte words; each blob starts 16-byte aligned
   auto put_i32x2 = [&](int32_t a, int32_t b) {
     double w; int32_t v[2] = {a, b}; memcpy(&w, v, 8); blob.push_back(w);
@@ -975,6 +1149,7 @@ int gm_pip_index_create_ex(gm_ctx* ctx, const gm_polyset* ps, int cells_per_poly
             n_compact++;
             ents.push_back(Ent{cell, (CELL_BOUNDARY << 30) | BLOB_COMPACT | (uint32_t)ci});
             per_cell[cell]++;
+            bnd_cell[cell]++;
             continue;
           }
         }
@@ -1016,6 +1191,7 @@ int gm_pip_index_create_ex(gm_ctx* ctx, const gm_polyset* ps, int cells_per_poly
         n_boundary++;
         ents.push_back(Ent{cell, (CELL_BOUNDARY << 30) | (uint32_t)boff});
         per_cell[cell]++;
+        bnd_cell[cell]++;
       }
     }
   }
@@ -1072,6 +1248,8 @@ int gm_pip_index_create_ex(gm_ctx* ctx, const gm_polyset* ps, int cells_per_poly
 
   gm_pip_index* ix = new gm_pip_index();
   ix->ctx = ctx;
+  ix->max_bnd_per_cell = ncell ? *std::max_element(bnd_cell.begin(), bnd_cell.end()) : 0;
+  ix->max_ent_per_cell = ncell ? *std::max_element(per_cell.begin(), per_cell.end()) : 0;
   ix->n_polys = P;
   ix->n_entries = (int64_t)ents.size();
   ix->n_boundary = n_boundary;
@@ -1126,29 +1304,98 @@ int gm_pip_join(gm_ctx* ctx, const gm_pip_index* ix, const double* px, const dou
 int gm_pip_join_ex(gm_ctx* ctx, const gm_pip_index* ix, const double* px, const double* py, int64_t n,
                    int64_t id_base, int64_t* pt_ids, int32_t* poly_ids, int64_t cap, int64_t* n_pairs, int mode) {
   if (!ctx || !ix || n < 0 || cap < 0) return GM_E_INVALID;
-  if (mode != GM_JOIN_AUTO && mode != GM_JOIN_DIRECT && mode != GM_JOIN_PARTITIONED) return GM_E_INVALID;
+  if (mode != GM_JOIN_AUTO && mode != GM_JOIN_DIRECT && mode != GM_JOIN_PARTITIONED && mode != GM_JOIN_SPLIT)
+    return GM_E_INVALID;
   const bool write = pt_ids && poly_ids;
   if ((pt_ids == nullptr) != (poly_ids == nullptr)) return GM_E_INVALID;
   if (n > 0 && (!px || !py)) return GM_E_INVALID;
   GM_HIP(hipSetDevice(ctx->device));
   unsigned long long* counter = (unsigned long long*)ctx->d_scratch;
   GM_HIP(hipMemsetAsync(counter, 0, 8, ctx->stream));
-  // AUTO = DIRECT: measured on MI355X (1B CONUS points x 3,200 polygons) the direct pass takes 22 ms
-  // against 39 ms for partition + join (profiles/); the partitioned mode stays selectable
-  const bool part = mode == GM_JOIN_PARTITIONED;
-  if (!part) {
+  // AUTO = DIRECT: measured on MI355X (1B CONUS points x 3,200 polygons) the direct pass takes 20 ms,
+  // against 23 ms for the split pass and 39 ms for partition + join; the others stay
+  // selectable
+  if ((mode == GM_JOIN_AUTO || mode == GM_JOIN_DIRECT) && n > 0) {
     const int64_t CHUNK = (int64_t)1 << 31;  // LDS staging keeps 32-bit row offsets
     for (int64_t c0 = 0; c0 < n; c0 += CHUNK) {
       const int64_t m = std::min(CHUNK, n - c0);
       const int64_t ntiles = (m + JTILE - 1) / JTILE;
-      const unsigned grid = write ? join_grid<true, false>(ctx->device, ntiles) : join_grid<false, false>(ctx->device, ntiles);
+      const unsigned grid = write ? join_grid<true, false, false>(ctx->device, ntiles)
+                                  : join_grid<false, false, false>(ctx->device, ntiles);
       if (write)
-        hipLaunchKernelGGL((k_pip_join<true, false>), dim3(grid), dim3(JTPB), 0, ctx->stream, px + c0, py + c0,
-                           nullptr, nullptr, m, id_base + c0, ix->dev, pt_ids, poly_ids, cap, counter);
+        hipLaunchKernelGGL((k_pip_join<true, false, false>), dim3(grid), dim3(JTPB), 0, ctx->stream, px + c0, py + c0,
+                           nullptr, nullptr, m, id_base + c0, ix->dev, pt_ids, poly_ids, cap, counter, SplitArgs{});
       else
-        hipLaunchKernelGGL((k_pip_join<false, false>), dim3(grid), dim3(JTPB), 0, ctx->stream, px + c0, py + c0,
-                           nullptr, nullptr, m, id_base + c0, ix->dev, pt_ids, poly_ids, cap, counter);
+        hipLaunchKernelGGL((k_pip_join<false, false, false>), dim3(grid), dim3(JTPB), 0, ctx->stream, px + c0, py + c0,
+                           nullptr, nullptr, m, id_base + c0, ix->dev, pt_ids, poly_ids, cap, counter, SplitArgs{});
       GM_CHECK_LAUNCH();
+    }
+  } else if (mode == GM_JOIN_SPLIT && n > 0) {
+    // split pass per chunk: lookups + interior pairs + work list -> blob evaluations -> pack the
+    // pair regions.  Worst-case region sizes follow from the index (entries per cell); the chunk is
+    // sized so that items + pairs fit a 6 GiB context workspace (and rows stay 32-bit).
+#ifdef GM_JX_CAPS   // timing experiment only: unsafe small segment capacities
+    const int64_t per_b = 1, per_e = 1;
+#else
+    const int64_t per_b = std::max<int64_t>(1, ix->max_bnd_per_cell);
+    const int64_t per_e = std::max<int64_t>(1, ix->max_ent_per_cell);
+#endif
+    if (getenv("GM_PIP_DEBUG")) fprintf(stderr, "[gm_pip] split: per_b %lld per_e %lld\n", (long long)per_b, (long long)per_e);
+#ifndef GM_JOIN_WS_GB
+#define GM_JOIN_WS_GB 6
+#endif
+    const int64_t budget = (int64_t)GM_JOIN_WS_GB << 30;
+    int64_t CHUNK = std::min<int64_t>((int64_t)1 << 31, budget / ((per_b + (write ? per_e : 0)) * (int64_t)sizeof(uint2)));
+    CHUNK = std::max<int64_t>(JTILE * 8, CHUNK / (JTILE * 8) * (JTILE * 8));
+    const int64_t mmax = std::min(CHUNK, n);
+    const int64_t ntiles_max = (mmax + JTILE - 1) / JTILE;
+    const unsigned grid_a = write ? join_grid<true, false, true>(ctx->device, ntiles_max)
+                                  : join_grid<false, false, true>(ctx->device, ntiles_max);
+    SplitArgs sp{};
+    sp.nseg = (int32_t)grid_a * (JTPB / 64);
+    const int64_t seg_pts = (ntiles_max + grid_a - 1) / grid_a * (int64_t)(64 * JILP);   // points one wave sees
+    sp.ipw = seg_pts * per_b;
+    sp.ppw = write ? seg_pts * per_e : 0;
+    {
+      auto al = [](size_t v) { return (v + 15) & ~(size_t)15; };
+      const size_t a_items = al((size_t)sp.nseg * sp.ipw * sizeof(uint2)), a_pairs = al((size_t)sp.nseg * sp.ppw * sizeof(uint2));
+      const size_t a_cnt = al((size_t)sp.nseg * 4), a_off = al((size_t)(sp.nseg + 1) * 8);
+      void* base = nullptr;
+      int wrc = ctx_workspace(ctx, WS_JOIN, a_items + a_pairs + 2 * a_cnt + a_off, &base);
+      if (wrc) return wrc;
+      char* q = (char*)base;
+      sp.items = (uint2*)q; q += a_items;
+      sp.pairs = (uint2*)q; q += a_pairs;
+      sp.item_cnt = (uint32_t*)q; q += a_cnt;
+      sp.pair_cnt = (uint32_t*)q; q += a_cnt;
+      sp.pair_off = (int64_t*)q;
+    }
+    for (int64_t c0 = 0; c0 < n; c0 += CHUNK) {
+      const int64_t m = std::min(CHUNK, n - c0);
+      // every segment is written (counts) by its wave; the grid stays grid_a for every chunk
+      if (write)
+        hipLaunchKernelGGL((k_pip_join<true, false, true>), dim3(grid_a), dim3(JTPB), 0, ctx->stream, px + c0, py + c0,
+                           nullptr, nullptr, m, id_base + c0, ix->dev, pt_ids, poly_ids, cap, counter, sp);
+      else
+        hipLaunchKernelGGL((k_pip_join<false, false, true>), dim3(grid_a), dim3(JTPB), 0, ctx->stream, px + c0,
+                           py + c0, nullptr, nullptr, m, id_base + c0, ix->dev, pt_ids, poly_ids, cap, counter, sp);
+      GM_CHECK_LAUNCH();
+      const unsigned bgrid = write ? resident_grid(k_pip_blobs<true>, ctx->device, sp.nseg, false)
+                                   : resident_grid(k_pip_blobs<false>, ctx->device, sp.nseg, false);
+      if (write)
+        hipLaunchKernelGGL((k_pip_blobs<true>), dim3(bgrid), dim3(JTPB), 0, ctx->stream, px + c0, py + c0, ix->dev,
+                           counter, sp);
+      else
+        hipLaunchKernelGGL((k_pip_blobs<false>), dim3(bgrid), dim3(JTPB), 0, ctx->stream, px + c0, py + c0, ix->dev,
+                           counter, sp);
+      GM_CHECK_LAUNCH();
+      if (write) {
+        hipLaunchKernelGGL(k_pip_scan_segs, dim3(1), dim3(1024), 0, ctx->stream, sp);
+        hipLaunchKernelGGL(k_pip_compact, dim3(std::min<int32_t>(sp.nseg, 4096)), dim3(JTPB), 0, ctx->stream, sp, counter,
+                           id_base + c0, pt_ids, poly_ids, cap);
+        hipLaunchKernelGGL(k_pip_chunk_done, dim3(1), dim3(64), 0, ctx->stream, sp, counter);
+        GM_CHECK_LAUNCH();
+      }
     }
   } else if (n > 0) {
     const int64_t CHUNK = (int64_t)1 << 28;  // 6 GiB of band-sorted records per pass
@@ -1179,13 +1426,14 @@ int gm_pip_join_ex(gm_ctx* ctx, const gm_pip_index* ix, const double* px, const 
                          rows_per_band, nb, hist, rec);
       const uint32_t* n_rec = hist + (int64_t)nb * pgrid;
       const int64_t ntiles = (m + JTILE - 1) / JTILE;
-      const unsigned grid = write ? join_grid<true, true>(ctx->device, ntiles) : join_grid<false, true>(ctx->device, ntiles);
+      const unsigned grid = write ? join_grid<true, true, false>(ctx->device, ntiles)
+                                  : join_grid<false, true, false>(ctx->device, ntiles);
       if (write)
-        hipLaunchKernelGGL((k_pip_join<true, true>), dim3(grid), dim3(JTPB), 0, ctx->stream, nullptr, nullptr, rec,
-                           n_rec, m, id_base + c0, ix->dev, pt_ids, poly_ids, cap, counter);
+        hipLaunchKernelGGL((k_pip_join<true, true, false>), dim3(grid), dim3(JTPB), 0, ctx->stream, nullptr, nullptr,
+                           rec, n_rec, m, id_base + c0, ix->dev, pt_ids, poly_ids, cap, counter, SplitArgs{});
       else
-        hipLaunchKernelGGL((k_pip_join<false, true>), dim3(grid), dim3(JTPB), 0, ctx->stream, nullptr, nullptr, rec,
-                           n_rec, m, id_base + c0, ix->dev, pt_ids, poly_ids, cap, counter);
+        hipLaunchKernelGGL((k_pip_join<false, true, false>), dim3(grid), dim3(JTPB), 0, ctx->stream, nullptr, nullptr,
+                           rec, n_rec, m, id_base + c0, ix->dev, pt_ids, poly_ids, cap, counter, SplitArgs{});
       if (hipGetLastError() != hipSuccess) rc = hip_fail(hipErrorLaunchFailure, "k_pip_join (partitioned)");
     }
     if (rc) return rc;

@@ -111,13 +111,15 @@ class PolygonIndex:
         check(self.ctx.lib.gm_pip_index_stats(self._h, st.ctypes.data), "gm_pip_index_stats")
         return dict(zip(["cells", "entries", "boundary", "records", "slow", "blob_bytes", "compact"], st.tolist()))
 
-    MODES = {"auto": _lib.GM_JOIN_AUTO, "direct": _lib.GM_JOIN_DIRECT, "partitioned": _lib.GM_JOIN_PARTITIONED}
+    MODES = {"auto": _lib.GM_JOIN_AUTO, "direct": _lib.GM_JOIN_DIRECT, "partitioned": _lib.GM_JOIN_PARTITIONED,
+             "split": _lib.GM_JOIN_SPLIT}
 
     def join(self, px, py, id_base=0, cap=None, count_only=False, mode="auto"):
         """Returns (pt_ids, poly_ids) device tensors (or the pair count when count_only).
 
-        mode: "auto", "direct" (one pass over the point columns) or "partitioned" (points
-        counting-sorted by grid-row band first); the pair set is the same for every mode."""
+        mode: "auto", "direct" (one pass over the point columns), "partitioned" (points
+        counting-sorted by grid-row band first) or "split" (lookups, then a work list of boundary
+        evaluations); the pair set is the same for every mode."""
         m = self.MODES[mode]
         import torch
         from .curve import _dev_col

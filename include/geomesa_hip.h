@@ -226,6 +226,9 @@ int gm_pip_join(gm_ctx* ctx, const gm_pip_index* index, const double* px, const 
 #define GM_JOIN_PARTITIONED 2 /* counting-sort the points by grid-row band first (device temp:
                                  24 B per point, at most 2^28 points per pass), then join band by
                                  band with the band's index data L2-resident */
+#define GM_JOIN_SPLIT 3       /* two passes: cell lookups + interior pairs + a work list of boundary
+                                 (point, blob) items, then the items' exact evaluation (device temp
+                                 per point: 8 B x the most entries of any cell) */
 /* gm_pip_join with an explicit strategy; the pair set is identical for every mode */
 int gm_pip_join_ex(gm_ctx* ctx, const gm_pip_index* index, const double* px, const double* py, int64_t n,
                    int64_t id_base, int64_t* pt_ids, int32_t* poly_ids, int64_t cap, int64_t* n_pairs, int mode);

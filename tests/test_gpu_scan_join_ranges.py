@@ -217,7 +217,7 @@ def test_pip_join_synthetic_counties(gpu, oracle, grid, cells_per_poly):
     import oracle as O
     opt, opl = O.OraclePolySet(*ps.to_arrays()).join(px, py, nthreads=8)
     exp = np.stack([opt, opl.astype(np.int64)], 1)
-    for mode in ("direct", "partitioned"):
+    for mode in ("direct", "partitioned", "split"):
         pt, pl = ix.join(px, py, mode=mode)
         assert np.array_equal(_sorted_pairs(pt, pl), exp), mode
         assert ix.join(px, py, count_only=True, mode=mode) == len(exp)
@@ -243,7 +243,7 @@ def test_pip_join_partitioned_edges(gpu, oracle):
     import oracle as O
     opt, opl = O.OraclePolySet(*ps.to_arrays()).join(px, py, nthreads=8)
     exp = np.stack([opt + 1000, opl.astype(np.int64)], 1)
-    for mode in ("direct", "partitioned"):
+    for mode in ("direct", "partitioned", "split"):
         pt, pl = ix.join(px, py, id_base=1000, mode=mode)
         assert np.array_equal(_sorted_pairs(pt, pl), exp), mode
         assert ix.join(px[:0], py[:0], mode=mode)[0].numel() == 0
@@ -262,6 +262,9 @@ def test_pip_join_auto_large(gpu, oracle):
     pt, pl = ix.join(px, py)
     assert np.array_equal(_sorted_pairs(pt, pl), exp)
     assert ix.join(px, py, count_only=True, mode="direct") == len(exp)
+    pt, pl = ix.join(px, py, mode="split")
+    assert np.array_equal(_sorted_pairs(pt, pl), exp)
+    assert ix.join(px, py, count_only=True, mode="split") == len(exp)
 
 
 # ---------------------------------------------------------------- batched ranges
