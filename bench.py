@@ -253,6 +253,21 @@ def bench_table(a, dist, ctx, b, z):
     }
 
 
+def query_polygon():
+    """A deterministic 1,024-vertex query polygon (lobed ring around (10, 47), radius 8-14 deg)
+    with a 64-vertex hole: the INTERSECTS geometry of the fused-filter bench lines."""
+    from geomesa_amd.join import PolygonSet
+    th = np.linspace(0, 2 * np.pi, 1025)[:-1]
+    r = 11 + 2.5 * np.sin(5 * th) + 0.5 * np.sin(37 * th)
+    ring = [(float(10 + 1.6 * r[i] * np.cos(th[i])), float(47 + r[i] * np.sin(th[i]))) for i in range(len(th))]
+    ring.append(ring[0])
+    th2 = np.linspace(0, 2 * np.pi, 65)[:-1]
+    hole = [(float(12 + 3 * np.cos(a)), float(46 - 2 * np.sin(a))) for a in th2]
+    hole.append(hole[0])
+    wkt = "POLYGON((%s), (%s))" % (", ".join("%r %r" % p for p in ring), ", ".join("%r %r" % p for p in hole))
+    return PolygonSet.from_wkt([wkt])
+
+
 # ------------------------------------------------------------------------------ main
 
 def main():
@@ -331,6 +346,24 @@ def main():
         mask = torch.empty((N + 63) // 64, dtype=torch.int64, device=dev)
         rec("z3filter_scan", lambda: lib.gm_z3filter_scan(h, fbuf, len(fb), br.ctypes.data, len(br) // 2, P(b), P(z),
                                                          N, P(mask), None, 0, None), 10.125, N, unit="rows/s")
+        # fused full filter (north star: bbox + time window + point-in-polygon in one pass) over the
+        # resident x/y/t columns: a 1,024-vertex query polygon with a hole around Europe, as
+        # (a) INTERSECTS + BBOX + DURING (the Z3 query of the filter scan above) and (b) INTERSECTS alone
+        from geomesa_amd.join import PolygonIndex, PolygonSet
+        qpoly = query_polygon()
+        qix = PolygonIndex(qpoly, cells_per_poly=65536)
+        bbq = (ctypes.c_double * 4)(-10.0, 35.0, 30.0, 60.0)
+        qmask = torch.empty((N + 63) // 64, dtype=torch.int64, device=dev)
+        rec("query_scan", lambda: lib.gm_query_scan(h, P(x), P(y), P(t), N, bbq, 1, 1590969600000, 1591617600000, qix._h,
+                                                   1, P(qmask), None, 0, None), 24.125, N, unit="rows/s")
+        rec("query_scan_polygon", lambda: lib.gm_query_scan(h, P(x), P(y), None, N, None, 0, 0, 0, qix._h, 1, P(qmask),
+                                                           None, 0, None), 16.125, N, unit="rows/s")
+        nm = ctypes.c_int64()
+        _lib.check(lib.gm_query_scan(h, P(x), P(y), None, N, None, 0, 0, 0, qix._h, 1, P(qmask), None, 0,
+                                     ctypes.byref(nm)), "query")
+        extra["query_scan_polygon"]["matches"] = nm.value
+        extra["query_scan_polygon"]["polygon"] = "1,024-vertex ring + 64-vertex hole, envelope 40 x 24 deg; 65,536-cell index"
+        del qmask, qix
         del mask
         # XZ2 / XZ3 index of 100M envelopes (configs[4]): x/y as min corners, max corners a log-uniform
         # [1e-6, 10] deg away; XZ3 time extent 1 s .. 1 day inside the week

@@ -26,6 +26,7 @@ GM_JOIN_AUTO = 0
 GM_JOIN_DIRECT = 1
 GM_JOIN_PARTITIONED = 2
 GM_JOIN_SPLIT = 3
+GM_SPATIAL_NONE, GM_SPATIAL_INTERSECTS, GM_SPATIAL_CONTAINS = 0, 1, 2
 
 
 class GeomesaHipUnavailable(RuntimeError):
@@ -94,6 +95,7 @@ SIGNATURES = {
     "gm_z3filter_scan": (cint, [vp, vp, sz, vp, cint, vp, vp, i64, vp, vp, i64, vp]),
     "gm_z2filter_scan": (cint, [vp, vp, sz, vp, i64, vp, vp, i64, vp]),
     "gm_strict_scan": (cint, [vp, vp, vp, vp, i64, vp, cint, i64, i64, vp, vp, i64, vp]),
+    "gm_query_scan": (cint, [vp, vp, vp, vp, i64, vp, cint, i64, i64, vp, cint, vp, vp, i64, vp]),
     "gm_pip_index_create": (cint, [vp, vp, vp]),
     "gm_pip_index_create_ex": (cint, [vp, vp, cint, vp]),
     "gm_pip_index_destroy": (cint, [vp]),

@@ -268,3 +268,38 @@ def strict_scan(x, y, t_ms, bbox, during=None, want_ids=False, ids_cap=None):
     if rc != _lib.GM_E_CAPACITY:
         check(rc, "gm_strict_scan")
     return _mask_to_bool(mask, n), (ids[:min(nm.value, cap)] if want_ids else None), nm.value
+
+
+SPATIAL_OPS = {None: _lib.GM_SPATIAL_NONE, "intersects": _lib.GM_SPATIAL_INTERSECTS,
+               "contains": _lib.GM_SPATIAL_CONTAINS, "within": _lib.GM_SPATIAL_CONTAINS}
+
+
+def query_scan(x, y, t_ms=None, bbox=None, during=None, geoms=None, op="intersects", want_ids=False, ids_cap=None):
+    """The full filter of a point query in one pass (gm_query_scan): BBOX (inclusive) AND during
+    (exclusive ms) AND, over the polygons of `geoms` (a join.PolygonIndex, or a join.PolygonSet that
+    is indexed here), OR of INTERSECTS(geom, P) (op "intersects") or CONTAINS(P, geom) /
+    WITHIN(geom, P) (op "contains" / "within").  Absent terms (None) are left out.
+    Returns (mask, ids, n_match) like strict_scan."""
+    import torch
+    from .join import PolygonIndex, PolygonSet
+    x, y = _cols((x, torch.float64), (y, torch.float64))
+    n = x.numel()
+    t = _cols((t_ms, torch.int64))[0] if during is not None else None
+    if geoms is None:
+        op = None
+    elif isinstance(geoms, PolygonSet):
+        geoms = PolygonIndex(geoms, cells_per_poly=65536)
+    if op not in SPATIAL_OPS:
+        raise ValueError("spatial op must be one of %s" % sorted(k for k in SPATIAL_OPS if k))
+    ctx = _lib.context()
+    cap = n if ids_cap is None else ids_cap
+    mask, ids = _outputs(n, x.device, want_ids, cap)
+    bb = (ctypes.c_double * 4)(*[float(v) for v in bbox]) if bbox is not None else None
+    lo, hi = during if during is not None else (0, 0)
+    nm = ctypes.c_int64()
+    rc = ctx.lib.gm_query_scan(ctx.handle, ptr(x), ptr(y), ptr(t), n, bb, int(during is not None), int(lo), int(hi),
+                               geoms._h if geoms is not None else None, SPATIAL_OPS[op], ptr(mask), ptr(ids), cap,
+                               ctypes.byref(nm))
+    if rc != _lib.GM_E_CAPACITY:
+        check(rc, "gm_query_scan")
+    return _mask_to_bool(mask, n), (ids[:min(nm.value, cap)] if want_ids else None), nm.value

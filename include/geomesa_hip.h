@@ -233,6 +233,24 @@ int gm_pip_join(gm_ctx* ctx, const gm_pip_index* index, const double* px, const 
 int gm_pip_join_ex(gm_ctx* ctx, const gm_pip_index* index, const double* px, const double* py, int64_t n,
                    int64_t id_base, int64_t* pt_ids, int32_t* poly_ids, int64_t cap, int64_t* n_pairs, int mode);
 
+/* ------------------------------------------------------------------ fused query filter */
+/* spatial terms of gm_query_scan */
+#define GM_SPATIAL_NONE 0
+#define GM_SPATIAL_INTERSECTS 1  /* INTERSECTS(geom, P): JTS P.intersects(point), boundary included */
+#define GM_SPATIAL_CONTAINS 2    /* CONTAINS(P, geom) / WITHIN(geom, P): JTS P.contains(point), interior only */
+/* The full filter of a point query in one pass (useFullFilter, Z3IndexKeySpace.scala:240-254):
+   BBOX (inclusive, geomesa-filter/.../GeometryProcessing.scala:129) AND during (exclusive ms,
+   FastTemporalOperator.scala:123-126) AND the OR over the polygons of `geoms` of the spatial term
+   (GeometryProcessing.process turns a split query geometry into an OR of its parts, :104-136).
+   bbox (host xmin, ymin, xmax, ymax) NULL = no BBOX term; has_during = 0 = no time term;
+   spatial_op GM_SPATIAL_NONE = no geometry term (geoms may be NULL).  geoms is any polygon index
+   (gm_pip_index_create_ex; a denser grid, e.g. 65536 cells for one query polygon, makes more rows
+   resolve in one lookup).  Outputs as gm_strict_scan: mask bits, ids ascending, *n_match. */
+int gm_query_scan(gm_ctx* ctx, const double* x, const double* y, const int64_t* t_ms, int64_t n,
+                  const double* bbox, int has_during, int64_t during_lo_ms, int64_t during_hi_ms,
+                  const gm_pip_index* geoms, int spatial_op, uint64_t* mask, int64_t* ids, int64_t ids_cap,
+                  int64_t* n_match);
+
 /* ------------------------------------------------------------------ sorted key table */
 /* The row-key prefix [shard?][bin BE16][z BE64] of Z3IndexKeySpace.toIndexKey (idx/index/z3/
    Z3IndexKeySpace.scala:81-92; ByteArrays.writeShort / writeLong, geomesa-utils/.../index/

@@ -1008,6 +1008,38 @@ int gmo_contains(const gmo_polyset* ps, int poly, double px, double py) {
   return gmo_locate(ps, poly, px, py) == LOC_INTERIOR;
 }
 
+/* Geometry.intersects(point): envelopes intersect, then relate -> not exterior
+   (RectangleIntersects, JTS 1.20, gives the same closed-rectangle answer for a point). */
+int gmo_intersects(const gmo_polyset* ps, int poly, double px, double py) {
+  double e[4]; poly_env(ps, poly, e);
+  if (!(px >= e[0] && px <= e[2] && py >= e[1] && py <= e[3])) return 0;
+  return gmo_locate(ps, poly, px, py) != LOC_EXTERIOR;
+}
+
+/* Full filter of a point query (Z3IndexKeySpace useFullFilter, Z3IndexKeySpace.scala:240-254):
+   BBOX (inclusive) AND during (exclusive, ms) AND the OR over the query geometries of
+   INTERSECTS(geom, P) (op 1) or CONTAINS(P, geom) / WITHIN(geom, P) (op 2)
+   (GeometryProcessing.process splits a query geometry into an OR of parts, GeometryProcessing.scala:104-136).
+   bbox NULL = no BBOX term; ps NULL or op 0 = no geometry term. */
+int64_t gmo_query_scan(const double* x, const double* y, const int64_t* t_ms, int64_t n, const double* bbox,
+                       int has_during, int64_t lo, int64_t hi, const gmo_polyset* ps, int op, uint8_t* match) {
+  int64_t cnt = 0;
+  for (int64_t i = 0; i < n; i++) {
+    int ok = 1;
+    if (bbox) ok = x[i] >= bbox[0] && x[i] <= bbox[2] && y[i] >= bbox[1] && y[i] <= bbox[3];
+    if (ok && has_during) ok = t_ms[i] > lo && t_ms[i] < hi;
+    if (ok && ps && op) {
+      int any = 0;
+      for (int k = 0; k < ps->n_polys && !any; k++)
+        any = op == 1 ? gmo_intersects(ps, k, x[i], y[i]) : gmo_contains(ps, k, x[i], y[i]);
+      ok = any;
+    }
+    if (match) match[i] = (uint8_t)ok;
+    cnt += ok;
+  }
+  return cnt;
+}
+
 /* ---- join: uniform grid over polygon envelopes (the restatement of RelationUtils.grid +
    GeoMesaJoinRelation.sweeplineJoin candidate generation), then JTS contains per candidate ---- */
 typedef struct {

@@ -116,6 +116,10 @@ int     gmo_orientation_index(double p1x, double p1y, double p2x, double p2y, do
 /* 0 = EXTERIOR, 1 = BOUNDARY, 2 = INTERIOR (PointLocator with Mod-2 rule) */
 int     gmo_locate(const gmo_polyset* ps, int poly, double px, double py);
 int     gmo_contains(const gmo_polyset* ps, int poly, double px, double py);
+int     gmo_intersects(const gmo_polyset* ps, int poly, double px, double py);
+/* bbox AND during AND (OR over polygons of intersects (op 1) / contains (op 2)); NULL/0 = term absent */
+int64_t gmo_query_scan(const double* x, const double* y, const int64_t* t_ms, int64_t n, const double* bbox,
+                       int has_during, int64_t lo, int64_t hi, const gmo_polyset* ps, int op, uint8_t* match);
 /* join: uniform-grid candidate generation + JTS contains. pairs written in (point, poly) order,
    sorted by point then poly. returns number of pairs (or -(needed) if cap too small). */
 int64_t gmo_pip_join(const gmo_polyset* ps, const double* px, const double* py, int64_t n,

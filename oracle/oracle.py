@@ -82,6 +82,8 @@ def lib():
             "gmo_orientation_index": (ctypes.c_int, [d, d, d, d, d, d]),
             "gmo_locate": (ctypes.c_int, [vp, ctypes.c_int, d, d]),
             "gmo_contains": (ctypes.c_int, [vp, ctypes.c_int, d, d]),
+            "gmo_intersects": (ctypes.c_int, [vp, ctypes.c_int, d, d]),
+            "gmo_query_scan": (i64, [vp, vp, vp, i64, vp, ctypes.c_int, i64, i64, vp, ctypes.c_int, vp]),
             "gmo_pip_join": (i64, [vp, vp, vp, i64, vp, vp, i64, ctypes.c_int]),
         }
         for name, (res, args) in sig.items():
@@ -296,6 +298,19 @@ def strict_scan(x, y, t_ms, bbox, during=None):
     return m.astype(bool)
 
 
+def query_scan(x, y, t_ms=None, bbox=None, during=None, polys=None, op=0):
+    """bbox AND during AND (OR over polys of INTERSECTS (op 1) / CONTAINS (op 2)); polys is an
+    OraclePolySet.  Returns the boolean match column."""
+    x = np.ascontiguousarray(x, np.float64); y = np.ascontiguousarray(y, np.float64)
+    t = np.ascontiguousarray(t_ms if t_ms is not None else np.zeros(len(x), np.int64), np.int64)
+    bb = np.ascontiguousarray(bbox, np.float64) if bbox is not None else None
+    m = np.empty(len(x), np.uint8)
+    lo, hi = during if during is not None else (0, 0)
+    ps = ctypes.byref(polys.c) if polys is not None else None
+    lib().gmo_query_scan(_p(x), _p(y), _p(t), len(x), _p(bb), int(during is not None), lo, hi, ps, op, _p(m))
+    return m.astype(bool)
+
+
 class OraclePolySet:
     """Keeps numpy CSR arrays alive for the C gmo_polyset view."""
 
@@ -311,6 +326,9 @@ class OraclePolySet:
 
     def locate(self, poly, x, y):
         return lib().gmo_locate(ctypes.byref(self.c), poly, x, y)
+
+    def intersects(self, poly, x, y):
+        return bool(lib().gmo_intersects(ctypes.byref(self.c), poly, x, y))
 
     def join(self, px, py, nthreads=1):
         px = np.ascontiguousarray(px, np.float64); py = np.ascontiguousarray(py, np.float64)

@@ -399,6 +399,31 @@ def test_st_contains_box(oracle):  # geomesa-spark-jts/.../SpatialRelationFuncti
     assert not ps.contains(0, -5.0, 0.0)   # exterior
 
 
+def test_st_intersects_within_box(oracle):  # SpatialRelationFunctionsTest.scala:239-262 (pt1-pt4), :359-362
+    box = [[[[(0, 0), (0, 10), (10, 10), (10, 0), (0, 0)]]]]
+    ps = _polyset(box)
+    pts = {"int": (5.0, 5.0), "edge": (0.0, 5.0), "corner": (0.0, 0.0), "ext": (-5.0, 0.0)}
+    assert [k for k, (x, y) in pts.items() if ps.intersects(0, x, y)] == ["int", "edge", "corner"]
+    # st_within(point, box) == box.contains(point)
+    assert [k for k, (x, y) in pts.items() if ps.contains(0, x, y)] == ["int"]
+
+
+def test_query_scan_oracle_terms(oracle):
+    """bbox AND during AND OR-over-polygons, each term optional (gmo_query_scan)."""
+    import numpy as np
+    sq = lambda x0, y0, x1, y1: [(x0, y0), (x0, y1), (x1, y1), (x1, y0), (x0, y0)]  # noqa: E731
+    ps = _polyset([[[sq(0, 0, 10, 10)]], [[sq(20, 0, 30, 10)]]])
+    x = np.array([5.0, 0.0, 25.0, 15.0, 30.0, np.nan])
+    y = np.array([5.0, 5.0, 5.0, 5.0, 10.0, 5.0])
+    t = np.array([10, 20, 30, 40, 50, 60], np.int64)
+    q = oracle.query_scan
+    assert q(x, y).tolist() == [True] * 6
+    assert q(x, y, polys=ps, op=1).tolist() == [True, True, True, False, True, False]
+    assert q(x, y, polys=ps, op=2).tolist() == [True, False, True, False, False, False]
+    assert q(x, y, t, bbox=[0, 0, 20, 10], polys=ps, op=1).tolist() == [True, True, False, False, False, False]
+    assert q(x, y, t, during=(10, 30), polys=ps, op=1).tolist() == [False, True, False, False, False, False]
+
+
 def _polyset(polys):
     import numpy as np
     ppo, pro, rvo, vx, vy = [0], [0], [0], [], []
