@@ -7,7 +7,7 @@
 //
 // Output pipeline (all on the context stream, deterministic, ids ascending):
 //   pass A  k_*_mask     : per-row predicate -> mask words + per-block match counts
-//   pass B  k_scan_counts: exclusive scan of the per-block counts (single workgroup)
+//   pass B  launch_excl_scan (gm_scan.hpp): exclusive scan of the per-block counts
 //   pass C  k_mask_to_ids: expand mask bits into row ids at the scanned offsets
 // Pass C reads n/8 bytes of mask, so the ids cost ~1/80 of pass A's traffic plus 8 B per match.
 #include <string.h>
@@ -297,31 +297,6 @@ __global__ __launch_bounds__(FTPB) void k_strict_mask_v(const dv2* __restrict__ 
       });
 }
 
-// pass B: exclusive scan of block counts by one workgroup of 1024 threads; total -> out[nb]
-__global__ __launch_bounds__(1024) void k_scan_counts(const int32_t* __restrict__ counts, int64_t nb,
-                                                      int64_t* __restrict__ offsets) {
-  __shared__ int64_t s_part[1024];
-  const int64_t per = (nb + 1023) / 1024;
-  const int64_t a = (int64_t)threadIdx.x * per;
-  const int64_t b = a + per < nb ? a + per : nb;
-  int64_t sum = 0;
-  for (int64_t i = a; i < b; ++i) sum += counts[i];
-  s_part[threadIdx.x] = sum;
-  __syncthreads();
-  for (int off = 1; off < 1024; off <<= 1) {
-    int64_t v = threadIdx.x >= off ? s_part[threadIdx.x - off] : 0;
-    __syncthreads();
-    s_part[threadIdx.x] += v;
-    __syncthreads();
-  }
-  int64_t run = s_part[threadIdx.x] - sum;  // exclusive
-  for (int64_t i = a; i < b; ++i) {
-    offsets[i] = run;
-    run += counts[i];
-  }
-  if (threadIdx.x == 1023) offsets[nb] = s_part[1023];
-}
-
 // pass C: one block per pass-A block; per (step, wave) popcount prefix gives each lane its slot
 __global__ __launch_bounds__(FTPB) void k_mask_to_ids(const uint64_t* __restrict__ mask, int64_t n,
                                                       const int64_t* __restrict__ offsets, int64_t* __restrict__ ids,
@@ -558,15 +533,17 @@ int alloc_scan(gm_ctx* ctx, int64_t n, uint64_t* user_mask, size_t desc_words, S
   const size_t a_mask = user_mask ? 0 : (size_t)nwords * 8;
   const size_t a_cnt = ((size_t)nblocks * 4 + 4 + 15) & ~(size_t)15;
   const size_t a_off = ((size_t)(nblocks + 1) * 8 + 15) & ~(size_t)15;
+  const size_t a_part = ((size_t)(nblocks / SCAN_CHUNK + 2) * 8 + 15) & ~(size_t)15;
   const size_t a_desc = (desc_words * 4 + 15) & ~(size_t)15;
   void* base = nullptr;
-  int rc = ctx_workspace(ctx, WS_SCAN, a_mask + a_cnt + a_off + a_desc + 16, &base);
+  int rc = ctx_workspace(ctx, WS_SCAN, a_mask + a_cnt + a_off + a_part + a_desc + 16, &base);
   if (rc) return rc;
   char* p = (char*)base;
   b.mask = user_mask ? user_mask : (uint64_t*)p;
   p += a_mask;
   b.counts = (int32_t*)p; p += a_cnt;
   b.offsets = (int64_t*)p; p += a_off;
+  b.partials = (int64_t*)p; p += a_part;
   b.desc = desc_words ? (int32_t*)p : nullptr;
   return GM_OK;
 }
@@ -577,7 +554,7 @@ void free_scan(gm_ctx*, uint64_t*, ScanBufs&) {}   // workspace memory stays wit
 int finish_scan(gm_ctx* ctx, int64_t n, ScanBufs& b, int64_t* ids, int64_t ids_cap, int64_t* n_match) {
   const int64_t nblocks = (n + FROWS - 1) / FROWS;
   if (ids || n_match) {
-    hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, ctx->stream, b.counts, nblocks, b.offsets);
+    launch_excl_scan(ctx->stream, b.counts, nblocks, b.offsets, b.partials, b.offsets + nblocks);
     GM_CHECK_LAUNCH();
   }
   if (ids) {

@@ -18,7 +18,7 @@ constexpr int FROWS = FTPB * FELEMS;  // rows per block (2048) -> 64 mask words
 // block_base + u*256 + l, so every wave instruction reads one contiguous 1 KiB run.  A wave step
 // covers 128 rows: ballot(row 2l) and ballot(row 2l+1) interleave bit by bit into the two 64-bit
 // mask words of those rows.  A block still covers FROWS = 2048 rows (4 steps), so block_counts,
-// k_scan_counts and k_mask_to_ids are shared with the scalar kernels.
+// the count scan and k_mask_to_ids are shared with the scalar kernels.
 typedef short sv2 __attribute__((ext_vector_type(2)));
 constexpr int FPAIRS = FELEMS / 2;   // pair steps per lane
 
@@ -76,10 +76,109 @@ __device__ __forceinline__ void pair_scan(int64_t n, uint64_t* __restrict__ mask
   block_count_waves(cnt, block_counts);
 }
 
+// Device-wide exclusive scan, two levels (block counts of the mask scans, radix-sort histograms).
+// A single workgroup walking ~500k counts took 1.2-1.5 ms per call -- a third of the 1B-row scan
+// it followed.
+//   k_scan_partials: one block per SCAN_CHUNK values -> chunk sums
+//   k_scan_chunks  : one workgroup scans the chunk sums (a few hundred) in place; total -> *total_out
+//   k_scan_apply   : per chunk, block-wide exclusive scan + the chunk's base -> out[] (in place is fine:
+//                    every thread reads its 16 values before writing them)
+constexpr int SCAN_TPB = 256;
+constexpr int SCAN_PER = 16;                          // consecutive counts per thread
+constexpr int SCAN_CHUNK = SCAN_TPB * SCAN_PER;       // 4096 counts per block
+
+// block-wide exclusive scan of one value per thread (256 threads); *total gets the block sum
+__device__ __forceinline__ int64_t block_excl_scan(int64_t v, int64_t* total) {
+  __shared__ int64_t s_w[SCAN_TPB / 64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int64_t inc = v;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int64_t o = __shfl_up(inc, off, 64);
+    if (lane >= off) inc += o;
+  }
+  if (lane == 63) s_w[w] = inc;
+  __syncthreads();
+  int64_t wbase = 0, tot = 0;
+#pragma unroll
+  for (int i = 0; i < SCAN_TPB / 64; ++i) {
+    if (i < w) wbase += s_w[i];
+    tot += s_w[i];
+  }
+  *total = tot;
+  return wbase + inc - v;
+}
+
+template <class TIn>
+__global__ __launch_bounds__(SCAN_TPB) void k_scan_partials(const TIn* __restrict__ counts, int64_t nb,
+                                                            int64_t* __restrict__ partials) {
+  const int64_t base = (int64_t)blockIdx.x * SCAN_CHUNK;
+  int64_t s = 0;
+#pragma unroll
+  for (int i = 0; i < SCAN_PER; ++i) {
+    const int64_t j = base + (int64_t)i * SCAN_TPB + threadIdx.x;   // coalesced
+    if (j < nb) s += counts[j];
+  }
+  int64_t tot;
+  block_excl_scan(s, &tot);
+  if (threadIdx.x == 0) partials[blockIdx.x] = tot;
+}
+
+static __global__ __launch_bounds__(SCAN_TPB) void k_scan_chunks(int64_t* __restrict__ partials, int64_t np,
+                                                          int64_t* __restrict__ total_out) {
+  int64_t run = 0;
+  for (int64_t c0 = 0; c0 < np; c0 += SCAN_TPB) {   // np is small: a few rounds at most
+    const int64_t j = c0 + threadIdx.x;
+    const int64_t v = j < np ? partials[j] : 0;
+    int64_t tot;
+    const int64_t ex = block_excl_scan(v, &tot);
+    if (j < np) partials[j] = run + ex;
+    run += tot;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0 && total_out) *total_out = run;
+}
+
+template <class TIn, class TOut>
+__global__ __launch_bounds__(SCAN_TPB) void k_scan_apply(const TIn* counts, int64_t nb,
+                                                         const int64_t* __restrict__ partials, TOut* offsets) {
+  const int64_t base = (int64_t)blockIdx.x * SCAN_CHUNK + (int64_t)threadIdx.x * SCAN_PER;   // 16 consecutive
+  TIn c[SCAN_PER];
+  int64_t s = 0;
+#pragma unroll
+  for (int i = 0; i < SCAN_PER; ++i) {
+    c[i] = base + i < nb ? counts[base + i] : 0;
+    s += c[i];
+  }
+  int64_t tot;
+  int64_t run = partials[blockIdx.x] + block_excl_scan(s, &tot);
+#pragma unroll
+  for (int i = 0; i < SCAN_PER; ++i) {
+    if (base + i < nb) offsets[base + i] = (TOut)run;
+    run += c[i];
+  }
+}
+
+inline int64_t scan_partials_len(int64_t n) { return (n + SCAN_CHUNK - 1) / SCAN_CHUNK + 1; }
+
+// out[i] = sum(in[0, i)), total -> *total_out (device, may be null); partials: scan_partials_len(n)
+// int64 of device scratch
+template <class TIn, class TOut>
+inline void launch_excl_scan(hipStream_t s, const TIn* in, int64_t n, TOut* out, int64_t* partials,
+                             int64_t* total_out) {
+  const int64_t nchunks = (n + SCAN_CHUNK - 1) / SCAN_CHUNK;
+  if (nchunks > 0)
+    hipLaunchKernelGGL((k_scan_partials<TIn>), dim3((unsigned)nchunks), dim3(SCAN_TPB), 0, s, in, n, partials);
+  hipLaunchKernelGGL(k_scan_chunks, dim3(1), dim3(SCAN_TPB), 0, s, partials, nchunks, total_out);
+  if (nchunks > 0)
+    hipLaunchKernelGGL((k_scan_apply<TIn, TOut>), dim3((unsigned)nchunks), dim3(SCAN_TPB), 0, s, in, n, partials, out);
+}
+
 struct ScanBufs {
   uint64_t* mask = nullptr;
   int32_t* counts = nullptr;
   int64_t* offsets = nullptr;
+  int64_t* partials = nullptr;   // chunk sums of the two-level count scan
   int32_t* desc = nullptr;
 };
 

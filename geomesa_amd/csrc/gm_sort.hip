@@ -18,7 +18,7 @@
 #include <algorithm>
 #include <vector>
 
-#include "gm_internal.hpp"
+#include "gm_scan.hpp"
 
 namespace gm {
 
@@ -74,25 +74,6 @@ __global__ __launch_bounds__(STPB) void k_sort_hist(const uint8_t* __restrict__ 
   }
   __syncthreads();
   hist[(int64_t)threadIdx.x * gridDim.x + blockIdx.x] = h[threadIdx.x];
-}
-
-// in-place exclusive scan of a[0, len) by one 1024-thread block (len <= a few 10^5)
-__global__ __launch_bounds__(1024) void k_scan_u32(uint32_t* __restrict__ a, int64_t len) {
-  __shared__ uint32_t part[1024];
-  const int t = threadIdx.x;
-  const int64_t per = (len + 1023) / 1024, lo = t * per, hi = min(len, lo + per);
-  uint32_t s = 0;
-  for (int64_t k = lo; k < hi; ++k) s += a[k];
-  part[t] = s;
-  __syncthreads();
-  for (int off = 1; off < 1024; off <<= 1) {
-    const uint32_t v = t >= off ? part[t - off] : 0u;
-    __syncthreads();
-    part[t] += v;
-    __syncthreads();
-  }
-  uint32_t run = part[t] - s;
-  for (int64_t k = lo; k < hi; ++k) { const uint32_t c = a[k]; a[k] = run; run += c; }
 }
 
 // Stable scatter of one digit pass.  Each block walks its segment in tiles of 2048 rows laid out
@@ -290,12 +271,14 @@ int gm_sort_keys(gm_ctx* ctx, const uint8_t* shard, const int16_t* bin, const in
   uint16_t* tbin = nullptr;
   uint64_t* tz = nullptr;
   uint32_t *p0 = nullptr, *p1 = nullptr, *hist = nullptr;
+  int64_t* hpart = nullptr;
   {  // context-owned workspace: z | perm 0 | perm 1 | bin | hist | shard, 16-B aligned pieces
     auto al = [](size_t v) { return (v + 15) & ~(size_t)15; };
     const size_t a_z = al((size_t)n * 8), a_p = al((size_t)n * 4), a_b = al((size_t)n * 2),
-                 a_h = al((size_t)256 * grid * 4), a_s = sh ? al((size_t)n) : 0;
+                 a_h = al((size_t)256 * grid * 4), a_s = sh ? al((size_t)n) : 0,
+                 a_pt = al((size_t)scan_partials_len((int64_t)256 * grid) * 8);
     void* base = nullptr;
-    int wrc = ctx_workspace(ctx, WS_SORT, a_z + 2 * a_p + a_b + a_h + a_s, &base);
+    int wrc = ctx_workspace(ctx, WS_SORT, a_z + 2 * a_p + a_b + a_h + a_pt + a_s, &base);
     if (wrc) return wrc;
     char* q = (char*)base;
     tz = (uint64_t*)q; q += a_z;
@@ -303,6 +286,7 @@ int gm_sort_keys(gm_ctx* ctx, const uint8_t* shard, const int16_t* bin, const in
     p1 = (uint32_t*)q; q += a_p;
     tbin = (uint16_t*)q; q += a_b;
     hist = (uint32_t*)q; q += a_h;
+    hpart = (int64_t*)q; q += a_pt;
     if (sh) tsh = (uint8_t*)q;
   }
   const uint8_t* ish = sh;
@@ -317,7 +301,7 @@ int gm_sort_keys(gm_ctx* ctx, const uint8_t* shard, const int16_t* bin, const in
     uint64_t* oz = to_user ? (uint64_t*)z_out : tz;
     uint32_t* operm = (k % 2) ? p1 : p0;
     hipLaunchKernelGGL(k_sort_hist, dim3(grid), dim3(STPB), 0, s, ish, ibin, iz, n, per, passes[k], hist);
-    hipLaunchKernelGGL(k_scan_u32, dim3(1), dim3(1024), 0, s, hist, (int64_t)256 * grid);
+    launch_excl_scan(s, hist, (int64_t)256 * grid, hist, hpart, (int64_t*)nullptr);
     hipLaunchKernelGGL(k_sort_scatter, dim3(grid), dim3(STPB), 0, s, ish, ibin, iz, iperm, osh, obin, oz, operm, n, per,
                        passes[k], hist);
     if (hipGetLastError() != hipSuccess) rc = hip_fail(hipErrorLaunchFailure, "k_sort_scatter");
