@@ -263,7 +263,17 @@ int gm_sort_keys(gm_ctx* ctx, const uint8_t* shard, const int16_t* bin, const in
     GM_CHECK_LAUNCH();
     return GM_OK;
   }
-  const int nblk = (int)std::max<int64_t>(1, std::min<int64_t>(1024, (n + STILE - 1) / STILE));
+  // one resident wave of blocks: the scatter's LDS (~47 KiB) allows 3 blocks per CU, and a grid of
+  // 1024 blocks ran as 768 + a second round of 256
+  static int resident = 0;
+  if (!resident) {
+    int b = 0, cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_sort_scatter, STPB, 0) != hipSuccess || b < 1) b = 2;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, ctx->device) == hipSuccess) cus = prop.multiProcessorCount;
+    resident = b * cus;
+  }
+  const int nblk = (int)std::max<int64_t>(1, std::min<int64_t>(resident, (n + STILE - 1) / STILE));
   const int64_t per = ((n + nblk - 1) / nblk + STILE - 1) / STILE * STILE;
   const int grid = (int)((n + per - 1) / per);
   // ping-pong: the user outputs and one temp set; the last pass lands in the user outputs
