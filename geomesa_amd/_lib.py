@@ -21,6 +21,7 @@ GM_ST_OK = 0
 GM_ST_OUT_OF_BOUNDS = 1
 GM_ST_BAD_TIME = 2
 GM_ST_UNORDERED = 3
+GM_ST_NULL_GEOM = 4
 
 GM_JOIN_AUTO = 0
 GM_JOIN_DIRECT = 1
@@ -105,6 +106,13 @@ SIGNATURES = {
     "gm_z3_key_bytes": (cint, [vp, vp, vp, vp, i64, vp]),
     "gm_sort_keys": (cint, [vp, vp, vp, vp, i64, vp, vp, vp, vp]),
     "gm_key_range_scan": (cint, [vp, vp, vp, vp, i64, vp, i64, vp, sz, vp, vp, i64, vp, vp]),
+    "gm_z3_index_key_arrow": (cint, [vp, vp, vp, i64, cint, cint, vp, vp, vp, vp]),
+    "gm_z2_index_key_arrow": (cint, [vp, vp, i64, cint, vp, vp, vp]),
+    "gm_xz2_index_key_arrow": (cint, [vp, vp, i64, cint, cint, vp, vp, vp]),
+    "gm_xz3_index_key_arrow": (cint, [vp, vp, vp, i64, cint, cint, cint, vp, vp, vp, vp]),
+    "gm_arrow_points_to_columns": (cint, [vp, vp, i64, vp, vp]),
+    "gm_pip_join_arrow": (cint, [vp, vp, vp, i64, i64, vp, vp, i64, vp, cint]),
+    "gm_pip_index_create_arrow": (cint, [vp, vp, i32, cint, vp]),
     "gm_gen_points": (cint, [vp, ctypes.c_uint64, i64, i64, d, d, d, d, i64, i64, vp, vp, vp]),
 }
 

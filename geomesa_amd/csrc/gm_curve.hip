@@ -6,76 +6,12 @@
 // lane), UNROLL independent pairs in flight per lane, fully coalesced per wave instruction
 // (pair p of lane l in step u sits at block_base + u*256 + l).  One chunk per workgroup -- the
 // grid is large (N / 2048 workgroups at UNROLL = 4), so all 256 CUs x 8 XCDs fill.
-#include "gm_internal.hpp"
+#include "gm_keys.hpp"
 
 namespace gm {
 
 constexpr int TPB = 256;
 
-
-#ifndef GM_NT
-#define GM_NT 1
-#endif
-template <class T>
-__device__ __forceinline__ T ld_stream(const T* p) {
-#if GM_NT
-  return __builtin_nontemporal_load(p);
-#else
-  return *p;
-#endif
-}
-template <class T>
-__device__ __forceinline__ void st_stream(T v, T* p) {
-#if GM_NT
-  __builtin_nontemporal_store(v, p);
-#else
-  *p = v;
-#endif
-}
-
-// ------------------------------------------------------------------ per-element bodies
-
-// Z3SFC.index (z3/curve/Z3SFC.scala:37-52); t is the offset within the period (Long)
-template <bool LENIENT>
-__device__ __forceinline__ uint8_t z3_index_one(double x, double y, int64_t t, const NDim& lon, const NDim& lat,
-                                                const NDim& tim, int64_t& z) {
-  double td = (double)t;  // Long compared to / normalized as Double
-  bool inb = x >= lon.min && x <= lon.max && y >= lat.min && y <= lat.max && td >= tim.min && td <= tim.max;
-  if (!inb) {
-    if (!LENIENT) { z = 0; return ST_OUT_OF_BOUNDS; }
-    // lenientIndex (Z3SFC.scala:47-52): NaN falls through every comparison
-    x = x < lon.min ? lon.min : (x > lon.max ? lon.max : x);
-    y = y < lat.min ? lat.min : (y > lat.max ? lat.max : y);
-    td = td < tim.min ? tim.min : (td > tim.max ? tim.max : td);
-  }
-  z = z3_apply(normalize(lon, x), normalize(lat, y), normalize(tim, td));
-  return ST_OK;
-}
-
-// Z3IndexKeySpace.toIndexKey (idx/index/z3/Z3IndexKeySpace.scala:71-76): BinnedTime throws even
-// when lenient (it sits outside the try at :74); then sfc.index(x, y, offset, lenient)
-template <int PERIOD, bool LENIENT>
-__device__ __forceinline__ uint8_t z3_key_one(double x, double y, int64_t ms, const NDim& lon, const NDim& lat,
-                                              const NDim& tim, int16_t& bin, int64_t& z) {
-  int64_t off;
-  uint8_t st = binned_time<PERIOD>(ms, bin, off);
-  if (st == ST_OK) st = z3_index_one<LENIENT>(x, y, off, lon, lat, tim, z);
-  if (st != ST_OK) { bin = 0; z = 0; }
-  return st;
-}
-
-template <bool LENIENT>
-__device__ __forceinline__ uint8_t z2_index_one(double x, double y, const NDim& lon, const NDim& lat,
-                                                int64_t& z) {
-  bool inb = x >= lon.min && x <= lon.max && y >= lat.min && y <= lat.max;
-  if (!inb) {
-    if (!LENIENT) { z = 0; return ST_OUT_OF_BOUNDS; }
-    x = x < lon.min ? lon.min : (x > lon.max ? lon.max : x);
-    y = y < lat.min ? lat.min : (y > lat.max ? lat.max : y);
-  }
-  z = z2_apply(normalize(lon, x), normalize(lat, y));
-  return ST_OK;
-}
 
 // ------------------------------------------------------------------ Z3 key (epoch ms -> bin, z)
 
@@ -316,97 +252,6 @@ __global__ __launch_bounds__(TPB) void k_binned_time(const int64_t* __restrict__
   }
 }
 
-// ------------------------------------------------------------------ XZ2 / XZ3
-
-__device__ __forceinline__ double clampd(double v, double lo, double hi) { return v < lo ? lo : (v > hi ? hi : v); }
-__device__ __forceinline__ double jmax(double a, double b) { return a >= b ? a : b; }  // operands never NaN/-0 here
-
-// The XZ sequence code without the per-level FP loop.  XZ2SFC.sequenceCode (XZ2SFC.scala:264-286)
-// halves [x0, x1] `length` times and compares the normalized minimum with the exact dyadic centre:
-// at level i the cell is [k 2^-i, (k + 1) 2^-i) and `v < centre` is bit i+1 of v's binary
-// expansion, so the `length` answers are the leading bits of floor(v 2^length) (v = 1.0 takes the
-// upper half every time: 2^length - 1).  With q_i = x_i + 2 y_i (+ 4 z_i) the code is
-//   cs = sum_{i<L} (1 + q_i (B^(g-i) - 1) / (B - 1)),  B = 4 (8)
-//      = L + (interleave(x, y[, z]) B^(g-L+1) - sum_i q_i) / (B - 1),
-// the interleave being exactly the Z2 / Z3 bit spread.  Integer-only and exact.
-__device__ __forceinline__ uint32_t xz_cell(double v, int L) {
-  const double s = floor(__dmul_rn(v, ldexp(1.0, L)));   // exact: power-of-two scaling
-  const uint32_t m = (1u << L) - 1u;                      // L <= 30
-  const uint32_t c = (uint32_t)s;                         // v in [0, 1] -> s in [0, 2^L]
-  return c > m ? m : c;
-}
-
-// the `length` predicate (XZ2SFC.scala:66-74): mx <= floor(mn / w2) * w2 + 2 * w2 with w2 = 2^-(l1+1).
-// Dividing by a power of two is exact, so mn * 2^(l1+1) gives the identical double.
-__device__ __forceinline__ bool xz_fits(double mn, double mx, double w2, double inv_w2) {
-  return mx <= __dadd_rn(__dmul_rn(floor(__dmul_rn(mn, inv_w2)), w2), __dmul_rn(2.0, w2));
-}
-
-// XZ2SFC.index (z3/curve/XZ2SFC.scala:54-77) with normalize (:318-350), sequenceCode (:264-286)
-template <bool LENIENT>
-__device__ __forceinline__ uint8_t xz2_one(int g, double xmin, double ymin, double xmax, double ymax, int64_t& out) {
-  if (!(xmin <= xmax && ymin <= ymax)) { out = 0; return ST_UNORDERED; }
-  if (!(xmin >= -180.0 && xmax <= 180.0 && ymin >= -90.0 && ymax <= 90.0)) {
-    if (!LENIENT) { out = 0; return ST_OUT_OF_BOUNDS; }
-    xmin = clampd(xmin, -180.0, 180.0); ymin = clampd(ymin, -90.0, 90.0);
-    xmax = clampd(xmax, -180.0, 180.0); ymax = clampd(ymax, -90.0, 90.0);
-  }
-  const double nxmin = __ddiv_rn(__dsub_rn(xmin, -180.0), 360.0);
-  const double nymin = __ddiv_rn(__dsub_rn(ymin, -90.0), 180.0);
-  const double nxmax = __ddiv_rn(__dsub_rn(xmax, -180.0), 360.0);
-  const double nymax = __ddiv_rn(__dsub_rn(ymax, -90.0), 180.0);
-  const double maxdim = jmax(__dsub_rn(nxmax, nxmin), __dsub_rn(nymax, nymin));
-  const int32_t l1 = xz_l1(maxdim);
-  int length;
-  if (l1 >= g) {
-    length = g;
-  } else {
-    const double w2 = ldexp(1.0, -(l1 + 1)), inv = ldexp(1.0, l1 + 1);   // math.pow(0.5, l1 + 1), exact
-    length = (xz_fits(nxmin, nxmax, w2, inv) && xz_fits(nymin, nymax, w2, inv)) ? l1 + 1 : l1;
-  }
-  if (length == 0) { out = 0; return ST_OK; }
-  const uint32_t ix = xz_cell(nxmin, length), iy = xz_cell(nymin, length);
-  const uint64_t il = z2_split(ix) | (z2_split(iy) << 1);
-  const uint64_t num = (il << (2 * (g - length + 1))) - (uint64_t)(__popc(ix) + 2 * __popc(iy));
-  out = (int64_t)length + (int64_t)(num / 3u);
-  return ST_OK;
-}
-
-// XZ3SFC.index (z3/curve/XZ3SFC.scala:53-76) with normalize (:338-380), sequenceCode (:275-304)
-template <bool LENIENT>
-__device__ __forceinline__ uint8_t xz3_one(int g, double zhi, double xmin, double ymin, double zmin, double xmax,
-                                           double ymax, double zmax, int64_t& out) {
-  if (!(xmin <= xmax && ymin <= ymax && zmin <= zmax)) { out = 0; return ST_UNORDERED; }
-  if (!(xmin >= -180.0 && xmax <= 180.0 && ymin >= -90.0 && ymax <= 90.0 && zmin >= 0.0 && zmax <= zhi)) {
-    if (!LENIENT) { out = 0; return ST_OUT_OF_BOUNDS; }
-    xmin = clampd(xmin, -180.0, 180.0); ymin = clampd(ymin, -90.0, 90.0); zmin = clampd(zmin, 0.0, zhi);
-    xmax = clampd(xmax, -180.0, 180.0); ymax = clampd(ymax, -90.0, 90.0); zmax = clampd(zmax, 0.0, zhi);
-  }
-  const double zsize = __dsub_rn(zhi, 0.0);
-  const double nxmin = __ddiv_rn(__dsub_rn(xmin, -180.0), 360.0);
-  const double nymin = __ddiv_rn(__dsub_rn(ymin, -90.0), 180.0);
-  const double nzmin = __ddiv_rn(__dsub_rn(zmin, 0.0), zsize);
-  const double nxmax = __ddiv_rn(__dsub_rn(xmax, -180.0), 360.0);
-  const double nymax = __ddiv_rn(__dsub_rn(ymax, -90.0), 180.0);
-  const double nzmax = __ddiv_rn(__dsub_rn(zmax, 0.0), zsize);
-  const double maxdim = jmax(jmax(__dsub_rn(nxmax, nxmin), __dsub_rn(nymax, nymin)), __dsub_rn(nzmax, nzmin));
-  const int32_t l1 = xz_l1(maxdim);
-  int length;
-  if (l1 >= g) {
-    length = g;
-  } else {
-    const double w2 = ldexp(1.0, -(l1 + 1)), inv = ldexp(1.0, l1 + 1);
-    length = (xz_fits(nxmin, nxmax, w2, inv) && xz_fits(nymin, nymax, w2, inv) && xz_fits(nzmin, nzmax, w2, inv))
-                 ? l1 + 1 : l1;
-  }
-  if (length == 0) { out = 0; return ST_OK; }
-  const uint32_t ix = xz_cell(nxmin, length), iy = xz_cell(nymin, length), iz = xz_cell(nzmin, length);
-  const uint64_t il = z3_split(ix) | (z3_split(iy) << 1) | (z3_split(iz) << 2);
-  const uint64_t num = (il << (3 * (g - length + 1))) - (uint64_t)(__popc(ix) + 2 * __popc(iy) + 4 * __popc(iz));
-  out = (int64_t)length + (int64_t)(num / 7u);
-  return ST_OK;
-}
-
 template <bool LENIENT, bool STATUS>
 __global__ __launch_bounds__(TPB) void k_xz2_index(const double* __restrict__ xmin, const double* __restrict__ ymin,
                                                    const double* __restrict__ xmax, const double* __restrict__ ymax,
@@ -558,11 +403,6 @@ void launch_key_p(hipStream_t s, const double* x, const double* y, const int64_t
   }
 }
 
-inline bool valid_period(int p) { return p >= DAY && p <= YEAR; }
-
-inline NDim lon_dim(int p) { return make_ndim(-180.0, 180.0, p); }
-inline NDim lat_dim(int p) { return make_ndim(-90.0, 90.0, p); }
-inline NDim time_dim(int period, int p) { return make_ndim(0.0, (double)max_offset(period), p); }
 
 }  // namespace gm
 

@@ -20,7 +20,7 @@ typedef double dv2 __attribute__((ext_vector_type(2)));
 typedef long long lv2 __attribute__((ext_vector_type(2)));
 
 // ---------------------------------------------------------------- status codes (per element)
-enum : uint8_t { ST_OK = 0, ST_OUT_OF_BOUNDS = 1, ST_BAD_TIME = 2, ST_UNORDERED = 3 };
+enum : uint8_t { ST_OK = 0, ST_OUT_OF_BOUNDS = 1, ST_BAD_TIME = 2, ST_UNORDERED = 3, ST_NULL_GEOM = 4 };
 enum : int { DAY = 0, WEEK = 1, MONTH = 2, YEAR = 3 };
 
 // ---------------------------------------------------------------- JVM conversions

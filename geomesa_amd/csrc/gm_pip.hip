@@ -32,6 +32,7 @@
 #include <cstdio>
 #include <cstdlib>
 
+#include "gm_arrow.hpp"
 #include "gm_scan.hpp"
 
 namespace gm {
@@ -320,12 +321,14 @@ __device__ __forceinline__ void append_seg(const uint2* src, int cnt, int lane, 
 // 8 B, to a global work list that k_pip_blobs evaluates next.  Without the blob code the kernel fits
 // 64 VGPRs and 16 KiB of LDS per block, i.e. 8 waves per SIMD instead of 4, which is what the
 // lookup chain (point -> coarse word -> fine word -> list) needs to hide its latency.
-template <bool WRITE, bool REC, bool SPLIT>
+// SRC: 0 = x / y columns, 1 / 2 = an Arrow point column of Float8 / Float4 tuples (ap)
+template <bool WRITE, bool REC, bool SPLIT, int SRC = 0>
 __global__ __launch_bounds__(JTPB, GM_JOIN_WAVES) void k_pip_join(const double* __restrict__ px, const double* __restrict__ py,
                                                    const PtRec* __restrict__ rec, const uint32_t* __restrict__ n_rec,
                                                    int64_t n, int64_t id_base, PipDev d, int64_t* __restrict__ pt_ids,
                                                    int32_t* __restrict__ poly_ids, int64_t cap,
-                                                   unsigned long long* __restrict__ counter, SplitArgs sp) {
+                                                   unsigned long long* __restrict__ counter, SplitArgs sp,
+                                                   ArrowPts ap) {
   constexpr int NW = JTPB / 64;
   constexpr int WC = SPLIT ? WCAP_S : WCAP;
   __shared__ uint32_t s_pt[WRITE && !SPLIT ? NW * WC : 1];
@@ -375,6 +378,8 @@ __global__ __launch_bounds__(JTPB, GM_JOIN_WAVES) void k_pip_join(const double* 
           x[u] = __builtin_nontemporal_load(&r->x);
           y[u] = __builtin_nontemporal_load(&r->y);
           id[u] = __builtin_nontemporal_load(&r->idx);
+        } else if (SRC != 0) {   // null slots keep NaN: no cell, no pair
+          if (arrow_valid(ap.valid, ap.voff, i)) arrow_tuple<SRC == 2>(ap.c, i, ap.flip, x[u], y[u]);
         } else {
           x[u] = __builtin_nontemporal_load(&px[i]);
           y[u] = __builtin_nontemporal_load(&py[i]);
@@ -1118,9 +1123,35 @@ static unsigned resident_grid(K kernel, int device, int64_t ntiles, bool xcd_mul
   return (unsigned)g;
 }
 
-template <bool WRITE, bool REC, bool SPLIT>
+template <bool WRITE, bool REC, bool SPLIT, int SRC = 0>
 static unsigned join_grid(int device, int64_t ntiles) {
-  return resident_grid(k_pip_join<WRITE, REC, SPLIT>, device, ntiles, REC);
+  return resident_grid(k_pip_join<WRITE, REC, SPLIT, SRC>, device, ntiles, REC);
+}
+
+// the direct pass over an Arrow point column (tuples read in place)
+template <int SRC>
+static int join_direct_arrow(gm_ctx* ctx, const gm_pip_index* ix, ArrowPts ap, int64_t n, int64_t id_base,
+                             int64_t* pt_ids, int32_t* poly_ids, int64_t cap, unsigned long long* counter) {
+  const bool write = pt_ids && poly_ids;
+  const int64_t CHUNK = (int64_t)1 << 31;
+  const size_t tb = SRC == 2 ? 8 : 16;
+  for (int64_t c0 = 0; c0 < n; c0 += CHUNK) {
+    const int64_t m = std::min(CHUNK, n - c0);
+    const int64_t ntiles = (m + JTILE - 1) / JTILE;
+    ArrowPts a = ap;
+    a.c = (const char*)ap.c + (size_t)c0 * tb;
+    a.voff = ap.voff + c0;
+    if (write)
+      hipLaunchKernelGGL((k_pip_join<true, false, false, SRC>), dim3(join_grid<true, false, false, SRC>(ctx->device, ntiles)),
+                         dim3(JTPB), 0, ctx->stream, nullptr, nullptr, nullptr, nullptr, m, id_base + c0, ix->dev,
+                         pt_ids, poly_ids, cap, counter, SplitArgs{}, a);
+    else
+      hipLaunchKernelGGL((k_pip_join<false, false, false, SRC>), dim3(join_grid<false, false, false, SRC>(ctx->device, ntiles)),
+                         dim3(JTPB), 0, ctx->stream, nullptr, nullptr, nullptr, nullptr, m, id_base + c0, ix->dev,
+                         pt_ids, poly_ids, cap, counter, SplitArgs{}, a);
+    GM_CHECK_LAUNCH();
+  }
+  return GM_OK;
 }
 
 extern "C" {
@@ -1496,10 +1527,10 @@ int gm_pip_join_ex(gm_ctx* ctx, const gm_pip_index* ix, const double* px, const 
                                   : join_grid<false, false, false>(ctx->device, ntiles);
       if (write)
         hipLaunchKernelGGL((k_pip_join<true, false, false>), dim3(grid), dim3(JTPB), 0, ctx->stream, px + c0, py + c0,
-                           nullptr, nullptr, m, id_base + c0, ix->dev, pt_ids, poly_ids, cap, counter, SplitArgs{});
+                           nullptr, nullptr, m, id_base + c0, ix->dev, pt_ids, poly_ids, cap, counter, SplitArgs{}, ArrowPts{});
       else
         hipLaunchKernelGGL((k_pip_join<false, false, false>), dim3(grid), dim3(JTPB), 0, ctx->stream, px + c0, py + c0,
-                           nullptr, nullptr, m, id_base + c0, ix->dev, pt_ids, poly_ids, cap, counter, SplitArgs{});
+                           nullptr, nullptr, m, id_base + c0, ix->dev, pt_ids, poly_ids, cap, counter, SplitArgs{}, ArrowPts{});
       GM_CHECK_LAUNCH();
     }
   } else if (mode == GM_JOIN_SPLIT && n > 0) {
@@ -1547,10 +1578,10 @@ int gm_pip_join_ex(gm_ctx* ctx, const gm_pip_index* ix, const double* px, const 
       // every segment is written (counts) by its wave; the grid stays grid_a for every chunk
       if (write)
         hipLaunchKernelGGL((k_pip_join<true, false, true>), dim3(grid_a), dim3(JTPB), 0, ctx->stream, px + c0, py + c0,
-                           nullptr, nullptr, m, id_base + c0, ix->dev, pt_ids, poly_ids, cap, counter, sp);
+                           nullptr, nullptr, m, id_base + c0, ix->dev, pt_ids, poly_ids, cap, counter, sp, ArrowPts{});
       else
         hipLaunchKernelGGL((k_pip_join<false, false, true>), dim3(grid_a), dim3(JTPB), 0, ctx->stream, px + c0,
-                           py + c0, nullptr, nullptr, m, id_base + c0, ix->dev, pt_ids, poly_ids, cap, counter, sp);
+                           py + c0, nullptr, nullptr, m, id_base + c0, ix->dev, pt_ids, poly_ids, cap, counter, sp, ArrowPts{});
       GM_CHECK_LAUNCH();
       const unsigned bgrid = write ? resident_grid(k_pip_blobs<true>, ctx->device, sp.nseg, false)
                                    : resident_grid(k_pip_blobs<false>, ctx->device, sp.nseg, false);
@@ -1602,10 +1633,10 @@ int gm_pip_join_ex(gm_ctx* ctx, const gm_pip_index* ix, const double* px, const 
                                   : join_grid<false, true, false>(ctx->device, ntiles);
       if (write)
         hipLaunchKernelGGL((k_pip_join<true, true, false>), dim3(grid), dim3(JTPB), 0, ctx->stream, nullptr, nullptr,
-                           rec, n_rec, m, id_base + c0, ix->dev, pt_ids, poly_ids, cap, counter, SplitArgs{});
+                           rec, n_rec, m, id_base + c0, ix->dev, pt_ids, poly_ids, cap, counter, SplitArgs{}, ArrowPts{});
       else
         hipLaunchKernelGGL((k_pip_join<false, true, false>), dim3(grid), dim3(JTPB), 0, ctx->stream, nullptr, nullptr,
-                           rec, n_rec, m, id_base + c0, ix->dev, pt_ids, poly_ids, cap, counter, SplitArgs{});
+                           rec, n_rec, m, id_base + c0, ix->dev, pt_ids, poly_ids, cap, counter, SplitArgs{}, ArrowPts{});
       if (hipGetLastError() != hipSuccess) rc = hip_fail(hipErrorLaunchFailure, "k_pip_join (partitioned)");
     }
     if (rc) return rc;
@@ -1617,6 +1648,38 @@ int gm_pip_join_ex(gm_ctx* ctx, const gm_pip_index* ix, const double* px, const 
     if (write && *n_pairs > cap) return GM_E_CAPACITY;
   }
   return GM_OK;
+}
+
+int gm_pip_join_arrow(gm_ctx* ctx, const gm_pip_index* ix, const gm_geom_column* pts, int64_t n, int64_t id_base,
+                      int64_t* pt_ids, int32_t* poly_ids, int64_t cap, int64_t* n_pairs, int mode) {
+  if (!ctx || !ix || n < 0 || cap < 0 || !pts) return GM_E_INVALID;
+  if (pts->type != GM_GEOM_POINT || (pts->ordinal_bits != 64 && pts->ordinal_bits != 32)) return GM_E_INVALID;
+  if (n > 0 && !pts->coords) return GM_E_INVALID;
+  if ((pt_ids == nullptr) != (poly_ids == nullptr)) return GM_E_INVALID;
+  if (mode != GM_JOIN_AUTO && mode != GM_JOIN_DIRECT && mode != GM_JOIN_PARTITIONED && mode != GM_JOIN_SPLIT)
+    return GM_E_INVALID;
+  GM_HIP(hipSetDevice(ctx->device));
+  const ArrowPts ap{pts->coords, pts->validity, pts->validity_offset, pts->flip_axis, pts->ordinal_bits == 32};
+  if (mode == GM_JOIN_AUTO || mode == GM_JOIN_DIRECT) {
+    unsigned long long* counter = (unsigned long long*)ctx->d_scratch;
+    GM_HIP(hipMemsetAsync(counter, 0, 8, ctx->stream));
+    int rc = n == 0 ? GM_OK
+             : ap.f32 ? join_direct_arrow<2>(ctx, ix, ap, n, id_base, pt_ids, poly_ids, cap, counter)
+                      : join_direct_arrow<1>(ctx, ix, ap, n, id_base, pt_ids, poly_ids, cap, counter);
+    if (rc) return rc;
+    GM_HIP(hipMemcpyAsync(ctx->h_pinned, counter, 8, hipMemcpyDeviceToHost, ctx->stream));
+    GM_HIP(hipStreamSynchronize(ctx->stream));
+    const int64_t total = ctx->h_pinned[0];
+    if (n_pairs) *n_pairs = total;
+    return (pt_ids && total > cap) ? GM_E_CAPACITY : GM_OK;
+  }
+  // the other strategies run on x / y columns
+  double* xy = nullptr;
+  GM_HIP(hipMallocAsync((void**)&xy, (size_t)std::max<int64_t>(n, 1) * 16, ctx->stream));
+  int rc = gm_arrow_points_to_columns(ctx, pts, n, xy, xy + n);
+  if (!rc) rc = gm_pip_join_ex(ctx, ix, xy, xy + n, n, id_base, pt_ids, poly_ids, cap, n_pairs, mode);
+  (void)hipFreeAsync(xy, ctx->stream);
+  return rc;
 }
 
 int gm_query_scan(gm_ctx* ctx, const double* x, const double* y, const int64_t* t_ms, int64_t n, const double* bbox,

@@ -53,6 +53,7 @@ extern "C" {
 #define GM_ST_OUT_OF_BOUNDS 1 /* Z3SFC/Z2SFC/XZ2SFC/XZ3SFC require(...) -> IllegalArgumentException */
 #define GM_ST_BAD_TIME 2      /* BinnedTime require(...): before 1970-01-01 or past the period's max date */
 #define GM_ST_UNORDERED 3     /* XZ require(xmin <= xmax ...) / ZRange require(min <= max) */
+#define GM_ST_NULL_GEOM 4     /* toIndexKey: "Null geometry in feature" (Z3IndexKeySpace.scala:66-68) */
 
 /* TimePeriod (z3/curve/BinnedTime.scala:283-291) */
 #define GM_DAY 0
@@ -250,6 +251,70 @@ int gm_query_scan(gm_ctx* ctx, const double* x, const double* y, const int64_t* 
                   const double* bbox, int has_during, int64_t during_lo_ms, int64_t during_hi_ms,
                   const gm_pip_index* geoms, int spatial_op, uint64_t* mask, int64_t* ids, int64_t ids_cap,
                   int64_t* n_match);
+
+/* ------------------------------------------------------------------ Arrow columnar input */
+/* GeoMesa's Arrow geometry vectors (geomesa-arrow-jts) as zero-copy device input.  A point column is
+   a FixedSizeList(2) of Float8 (PointVector) or Float4 (PointFloatVector) whose tuples hold [y, x]
+   by default and [x, y] when the vector's flipAxisOrder is set (AbstractPointVector.java:52-79);
+   line, polygon and multi-geometry columns nest List offsets around the same tuples
+   (AbstractLineStringVector.java, AbstractPolygonVector.java:56-84 -- rings, the first one the
+   shell --, AbstractMultiPolygonVector.java:61-95 -- polygons, rings).  Dates are Arrow int64 epoch
+   milliseconds.  Null slots come from the Arrow validity bitmaps (LSB bit order). */
+#define GM_GEOM_POINT 0
+#define GM_GEOM_LINESTRING 1      /* offsets[0]: slot -> tuples */
+#define GM_GEOM_POLYGON 2         /* offsets[0]: slot -> rings, offsets[1]: ring -> tuples */
+#define GM_GEOM_MULTIPOINT 3      /* offsets[0]: slot -> tuples */
+#define GM_GEOM_MULTILINESTRING 4 /* offsets[0]: slot -> lines, offsets[1]: line -> tuples */
+#define GM_GEOM_MULTIPOLYGON 5    /* offsets[0]: slot -> polygons, [1]: polygon -> rings, [2]: ring -> tuples */
+
+typedef struct {
+  int32_t type;              /* GM_GEOM_* */
+  int32_t ordinal_bits;      /* 64 (Float8 vectors) or 32 (Float4 "...FloatVector"s) */
+  int32_t flip_axis;         /* 0: [y, x] tuples (the default), 1: [x, y] */
+  int32_t reserved;
+  const void* coords;        /* tuple ordinates, tuple j at [2j], [2j + 1] (already advanced by the
+                                innermost child array's offset) */
+  const uint8_t* validity;   /* top-level validity bitmap, NULL = no nulls */
+  int64_t validity_offset;   /* bit index of slot 0 in validity (the Arrow array offset) */
+  const int32_t* offsets[3]; /* List offsets, outermost first, each advanced by its array's offset;
+                                unused levels NULL */
+} gm_geom_column;
+
+typedef struct {
+  const int64_t* millis;     /* epoch ms (Arrow Timestamp(ms) / Date(ms) / Int64) */
+  const uint8_t* validity;   /* NULL = no nulls */
+  int64_t validity_offset;
+} gm_time_column;
+
+/* Z3IndexKeySpace.toIndexKey over an Arrow batch (idx/index/z3/Z3IndexKeySpace.scala:63-95):
+   point column + date column (dtg NULL or a null slot -> time 0, :70).  A null geometry is
+   GM_ST_NULL_GEOM (the IllegalArgumentException of :66-68).  Device arrays, as gm_z3_index_key. */
+int gm_z3_index_key_arrow(gm_ctx* ctx, const gm_geom_column* geom, const gm_time_column* dtg, int64_t n,
+                          int period, int lenient, int16_t* bin, int64_t* z, uint8_t* status,
+                          gm_batch_status* summary);
+/* Z2IndexKeySpace.toIndexKey (idx/index/z2/Z2IndexKeySpace.scala:48-75): Z2SFC.index of a point column */
+int gm_z2_index_key_arrow(gm_ctx* ctx, const gm_geom_column* geom, int64_t n, int lenient, int64_t* z,
+                          uint8_t* status, gm_batch_status* summary);
+/* XZ2IndexKeySpace.toIndexKey (idx/index/z2/XZ2IndexKeySpace.scala:48-76): XZ2SFC(g).index of each
+   geometry's JTS envelope (Geometry.getEnvelopeInternal: a polygon's envelope is its shell's, a multi
+   geometry's the union of its parts'; an empty geometry has the null envelope -> GM_ST_UNORDERED). */
+int gm_xz2_index_key_arrow(gm_ctx* ctx, const gm_geom_column* geom, int64_t n, int g, int lenient, int64_t* xz,
+                           uint8_t* status, gm_batch_status* summary);
+/* XZ3IndexKeySpace.toIndexKey (idx/index/z3/XZ3IndexKeySpace.scala:60-95): bin + XZ3SFC(g, period).index
+   of (envelope, offset) with the time from dtg (NULL / null slot -> 0) */
+int gm_xz3_index_key_arrow(gm_ctx* ctx, const gm_geom_column* geom, const gm_time_column* dtg, int64_t n, int g,
+                           int period, int lenient, int16_t* bin, int64_t* xz, uint8_t* status,
+                           gm_batch_status* summary);
+/* A point column as x / y device columns (null slots -> NaN): the adapter for every other entry */
+int gm_arrow_points_to_columns(gm_ctx* ctx, const gm_geom_column* geom, int64_t n, double* x, double* y);
+/* gm_pip_join_ex over an Arrow point column (null points never match): the direct pass reads the
+   tuples in place; the partitioned and split strategies go through gm_arrow_points_to_columns */
+int gm_pip_join_arrow(gm_ctx* ctx, const gm_pip_index* index, const gm_geom_column* points, int64_t n,
+                      int64_t id_base, int64_t* pt_ids, int32_t* poly_ids, int64_t cap, int64_t* n_pairs, int mode);
+/* gm_pip_index_create_ex from an Arrow POLYGON or MULTIPOLYGON column given in HOST memory (the
+   broadcast side of the join is collected on the host); a null slot is an empty polygon */
+int gm_pip_index_create_arrow(gm_ctx* ctx, const gm_geom_column* polys, int32_t n, int cells_per_poly,
+                              gm_pip_index** out);
 
 /* ------------------------------------------------------------------ sorted key table */
 /* The row-key prefix [shard?][bin BE16][z BE64] of Z3IndexKeySpace.toIndexKey (idx/index/z3/

@@ -348,3 +348,136 @@ def orientation_index(p1x, p1y, p2x, p2y, qx, qy):
 
 def zn_contains(dims, rmin, rmax, v): return bool(lib().gmo_zn_contains(dims, rmin, rmax, v))
 def zn_overlaps(dims, rmin, rmax, vmin, vmax): return bool(lib().gmo_zn_overlaps(dims, rmin, rmax, vmin, vmax))
+
+
+# ---------------------------------------------------------------- Arrow geometry vectors (8(f).2)
+# Per-row restatement of reading geomesa-arrow-jts vectors: tuple order [y, x] unless flipAxisOrder
+# (impl/AbstractPointVector.java:52-79), shell-first rings (impl/AbstractPolygonVector.java:56-84),
+# and the JTS 1.20 envelope rules of Geometry.getEnvelopeInternal (Envelope.expandToInclude: a null
+# envelope reads back as (0, -1, 0, -1); Polygon -> its shell's; collections -> union of parts').
+# Pure Python loops: small cases only.
+
+NULL_GEOM = 4
+_DEPTH = {"point": 0, "linestring": 1, "multipoint": 1, "polygon": 2, "multilinestring": 2, "multipolygon": 3}
+
+
+def arrow_rows(arr, kind, flip_axis=False):
+    """pyarrow geometry array -> per-row nested lists of (x, y) (None for a null slot)."""
+    def xy(t):
+        return (t[0], t[1]) if flip_axis else (t[1], t[0])
+
+    def conv(v, depth):
+        return xy(v) if depth == 0 else [conv(c, depth - 1) for c in v]
+    return [None if v is None else conv(v, _DEPTH[kind]) for v in arr.to_pylist()]
+
+
+def _env_expand(e, x, y):
+    if e is None:
+        return [x, x, y, y]
+    if x < e[0]: e[0] = x
+    if x > e[1]: e[1] = x
+    if y < e[2]: e[2] = y
+    if y > e[3]: e[3] = y
+    return e
+
+
+def _env_merge(e, o):
+    if o is None:
+        return e
+    if e is None:
+        return list(o)
+    return _env_expand(_env_expand(e, o[0], o[2]), o[1], o[3])
+
+
+def jts_envelope(row, kind):
+    """(minx, miny, maxx, maxy) of a non-null row, JTS null envelope -> (0, 0, -1, -1)."""
+    def seq(ts):
+        e = None
+        for x, y in ts:
+            e = _env_expand(e, x, y)
+        return e
+    if kind == "point":
+        e = seq([row])
+    elif kind in ("linestring", "multipoint"):
+        e = seq(row)
+    elif kind == "polygon":
+        e = seq(row[0]) if row else None
+    elif kind == "multilinestring":
+        e = None
+        for line in row:
+            e = _env_merge(e, seq(line))
+    else:
+        e = None
+        for poly in row:
+            if poly:
+                e = _env_merge(e, seq(poly[0]))
+    if e is None:
+        return (0.0, 0.0, -1.0, -1.0)
+    return (e[0], e[2], e[1], e[3])
+
+
+def _times(dtg, n):
+    if dtg is None:
+        return [0] * n
+    vals = dtg.cast("int64").to_pylist() if hasattr(dtg, "cast") else list(dtg)
+    return [0 if v is None else int(v) for v in vals]
+
+
+def arrow_z3_keys(arr, dtg=None, lenient=False, period=WEEK, flip_axis=False):
+    """Z3IndexKeySpace.toIndexKey (Z3IndexKeySpace.scala:63-76) per Arrow row."""
+    rows = arrow_rows(arr, "point", flip_axis)
+    ts = _times(dtg, len(rows))
+    b = np.zeros(len(rows), np.int16); z = np.zeros(len(rows), np.int64); st = np.zeros(len(rows), np.uint8)
+    for i, (r, t) in enumerate(zip(rows, ts)):
+        if r is None:
+            st[i] = NULL_GEOM
+            continue
+        bb, zz, s = z3_index_key_batch([r[0]], [r[1]], [t], lenient, period)
+        b[i], z[i], st[i] = bb[0], zz[0], s[0]
+    return b, z, st
+
+
+def arrow_z2_keys(arr, lenient=False, flip_axis=False):
+    rows = arrow_rows(arr, "point", flip_axis)
+    z = np.zeros(len(rows), np.int64); st = np.zeros(len(rows), np.uint8)
+    for i, r in enumerate(rows):
+        if r is None:
+            st[i] = NULL_GEOM
+            continue
+        st[i], z[i] = z2_index(r[0], r[1], lenient)
+    return z, st
+
+
+def arrow_xz2_keys(arr, kind, g=12, lenient=False, flip_axis=False):
+    """XZ2IndexKeySpace.toIndexKey (XZ2IndexKeySpace.scala:48-58) per Arrow row."""
+    rows = arrow_rows(arr, kind, flip_axis)
+    z = np.zeros(len(rows), np.int64); st = np.zeros(len(rows), np.uint8)
+    for i, r in enumerate(rows):
+        if r is None:
+            st[i] = NULL_GEOM
+            continue
+        st[i], z[i] = xz2_index(*jts_envelope(r, kind), lenient=lenient, g=g)
+        if st[i]:
+            z[i] = 0
+    return z, st
+
+
+def arrow_xz3_keys(arr, dtg, kind, g=12, period=WEEK, lenient=False, flip_axis=False):
+    """XZ3IndexKeySpace.toIndexKey (XZ3IndexKeySpace.scala:60-76) per Arrow row."""
+    rows = arrow_rows(arr, kind, flip_axis)
+    ts = _times(dtg, len(rows))
+    b = np.zeros(len(rows), np.int16); z = np.zeros(len(rows), np.int64); st = np.zeros(len(rows), np.uint8)
+    for i, (r, t) in enumerate(zip(rows, ts)):
+        if r is None:
+            st[i] = NULL_GEOM
+            continue
+        s, bb, off = binned_time(period, t)
+        if s:
+            st[i] = s
+            continue
+        x0, y0, x1, y1 = jts_envelope(r, kind)
+        s, zz = xz3_index(x0, y0, float(off), x1, y1, float(off), lenient=lenient, g=g, period=period)
+        st[i] = s
+        if not s:
+            b[i], z[i] = bb, zz
+    return b, z, st
