@@ -334,6 +334,15 @@ def main():
         rec("z2_index", lambda: lib.gm_z2_index(h, P(x), P(y), N, 31, 0, P(z2), None, None), 24, N)
         rec("z2_invert", lambda: lib.gm_z2_invert(h, P(z2), N, 31, P(x), P(y)), 24, N)
         del z2
+        # the same encode from a geomesa-arrow-jts PointVector ([y, x] Float8 tuples) + date vector, read in place
+        from geomesa_amd.arrow import GeomColumnC, TimeColumnC
+        import ctypes
+        yx = torch.stack([y, x], 1)
+        gcol = GeomColumnC(0, 64, 0, 0, yx.data_ptr(), None, 0, (ctypes.c_void_p * 3)())
+        tcol = TimeColumnC(t.data_ptr(), None, 0)
+        rec("arrow_z3_keys", lambda: lib.gm_z3_index_key_arrow(h, ctypes.byref(gcol), ctypes.byref(tcol), N, 1, 0, P(b),
+                                                              P(z), None, None), 34, N)
+        del yx
         # filter scan, key space (configs[2] query on the resident keys)
         from geomesa_amd import filters as F
         from geomesa_amd.keyspace import Z3IndexKeySpace, during
@@ -468,6 +477,24 @@ def main():
               "workload": "st_contains(polygon, point) join, %d CONUS points/GPU x %d synthetic county polygons "
                           "(BASELINE configs[3]); polygon set broadcast over RCCL when N > 1" % (J, ps.n_polys)}
         pj["roofline"]["bytes_per_unit"] = "16 B/point + 12 B/pair"
+        # row-wise st_contains (the UDF path without the join rule): row i = (its cell's county, point i)
+        x0c, y0c, x1c, y1c = CONUS
+        rid = (torch.clamp(((py - y0c) / (y1c - y0c) * gy).long(), 0, gy - 1) * gx +
+               torch.clamp(((px - x0c) / (x1c - x0c) * gx).long(), 0, gx - 1)).to(torch.int32)
+        loc = torch.empty(J, dtype=torch.uint8, device=dev)
+
+        def relate_step():
+            rc = lib.gm_pip_relate(h, ix._h, P(rid), P(px), P(py), J, P(loc))
+            if rc:
+                _lib.check(rc, "gm_pip_relate")
+        rms = timed(dist, relate_step, max(3, a.join_steps), 1)
+        pj["row_predicate"] = {"value": J * dist.world / (rms * 1e-3), "unit": "rows/s", "ms_per_step": rms,
+                               "contains": int(dist.sum(int((loc == 2).sum()))),
+                               "roofline": roofline(21.0 * J, rms, load_pmc("pip_relate", J)),
+                               "workload": "st_contains(polygon_i, point_i) row by row over the join's points, "
+                                           "polygon_i = the county of the point's grid cell (21 B/row: 16 point + 4 id + 1 out)"}
+        del rid, loc
+
         del px, py
         torch.cuda.empty_cache()
         if not a.no_gather:

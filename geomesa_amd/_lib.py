@@ -113,6 +113,7 @@ SIGNATURES = {
     "gm_arrow_points_to_columns": (cint, [vp, vp, i64, vp, vp]),
     "gm_pip_join_arrow": (cint, [vp, vp, vp, i64, i64, vp, vp, i64, vp, cint]),
     "gm_pip_index_create_arrow": (cint, [vp, vp, i32, cint, vp]),
+    "gm_pip_relate": (cint, [vp, vp, vp, vp, vp, i64, vp]),
     "gm_gen_points": (cint, [vp, ctypes.c_uint64, i64, i64, d, d, d, d, i64, i64, vp, vp, vp]),
 }
 

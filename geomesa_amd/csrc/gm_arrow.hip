@@ -81,6 +81,77 @@ __global__ __launch_bounds__(ATPB) void k_z3_key_arrow(ArrowPts g, ArrowTime tc,
   }
 }
 
+// the aligned, full-pair form of k_z3_key_arrow: one chunk of ATPB * UNROLL pairs per workgroup, every
+// load of the chunk issued before any compute (as k_z3_index_key): tuples 2p, 2p+1 as two 16-B loads
+// (Float8) or one (Float4), the date pair as one 16-B load
+template <bool F32>
+__device__ __forceinline__ void arrow_tuple_pair(const void* __restrict__ c, int64_t p, dv2& a, dv2& b) {
+  if (F32) {
+    typedef float fv4 __attribute__((ext_vector_type(4)));
+    const fv4 f = __builtin_nontemporal_load(&((const fv4*)c)[p]);
+    a = dv2{(double)f.x, (double)f.y};
+    b = dv2{(double)f.z, (double)f.w};
+  } else {
+    a = __builtin_nontemporal_load(&((const dv2*)c)[2 * p]);
+    b = __builtin_nontemporal_load(&((const dv2*)c)[2 * p + 1]);
+  }
+}
+
+template <int PERIOD, bool LENIENT, bool F32, bool TIME, int UNROLL>
+__global__ __launch_bounds__(ATPB) void k_z3_key_arrow_v(ArrowPts g, ArrowTime tc, int64_t n, NDim lon, NDim lat,
+                                                         NDim tim, short2* __restrict__ bin, lv2* __restrict__ z,
+                                                         uchar2* __restrict__ status, int64_t* __restrict__ err) {
+  const int64_t npairs = n >> 1;
+  const int64_t base = (int64_t)blockIdx.x * (ATPB * UNROLL) + threadIdx.x;
+  dv2 a[UNROLL], b[UNROLL];
+  lv2 tv[UNROLL];
+#pragma unroll
+  for (int u = 0; u < UNROLL; ++u) {
+    const int64_t p = base + (int64_t)u * ATPB;
+    tv[u] = lv2{0, 0};
+    if (p < npairs) {
+      arrow_tuple_pair<F32>(g.c, p, a[u], b[u]);
+      if (TIME) tv[u] = __builtin_nontemporal_load(&((const lv2*)tc.ms)[p]);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < UNROLL; ++u) {
+    const int64_t p = base + (int64_t)u * ATPB;
+    if (p >= npairs) continue;
+    if (TIME && tc.valid) {
+      if (!arrow_valid(tc.valid, tc.voff, 2 * p)) tv[u].x = 0;
+      if (!arrow_valid(tc.valid, tc.voff, 2 * p + 1)) tv[u].y = 0;
+    }
+    int16_t b0 = 0, b1 = 0;
+    int64_t z0 = 0, z1 = 0;
+    const double x0 = g.flip ? a[u].x : a[u].y, y0 = g.flip ? a[u].y : a[u].x;
+    const double x1 = g.flip ? b[u].x : b[u].y, y1 = g.flip ? b[u].y : b[u].x;
+    uint8_t s0 = ST_NULL_GEOM, s1 = ST_NULL_GEOM;
+    if (arrow_valid(g.valid, g.voff, 2 * p)) s0 = z3_key_one<PERIOD, LENIENT>(x0, y0, tv[u].x, lon, lat, tim, b0, z0);
+    if (arrow_valid(g.valid, g.voff, 2 * p + 1)) s1 = z3_key_one<PERIOD, LENIENT>(x1, y1, tv[u].y, lon, lat, tim, b1, z1);
+    st_stream(lv2{z0, z1}, &z[p]);
+    bin[p] = make_short2(b0, b1);
+    if (status) status[p] = make_uchar2(s0, s1);
+    if (s0) report_error(err, 2 * p, s0);
+    if (s1) report_error(err, 2 * p + 1, s1);
+  }
+  if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {   // the odd last row
+    const int64_t i = n - 1;
+    int16_t bb = 0;
+    int64_t zz = 0;
+    uint8_t st = ST_NULL_GEOM;
+    if (arrow_valid(g.valid, g.voff, i)) {
+      double x, y;
+      arrow_tuple<F32>(g.c, i, g.flip, x, y);
+      st = z3_key_one<PERIOD, LENIENT>(x, y, TIME ? arrow_time(tc, i) : 0, lon, lat, tim, bb, zz);
+    }
+    ((int16_t*)bin)[i] = bb;
+    ((int64_t*)z)[i] = zz;
+    if (status) ((uint8_t*)status)[i] = st;
+    if (st) report_error(err, i, st);
+  }
+}
+
 template <bool LENIENT, bool F32, bool VEC>
 __global__ __launch_bounds__(ATPB) void k_z2_key_arrow(ArrowPts g, int64_t n, NDim lon, NDim lat,
                                                        int64_t* __restrict__ z, uint8_t* __restrict__ status,
@@ -263,9 +334,22 @@ inline ArrowTime to_time(const gm_time_column* t) {
   return t ? ArrowTime{t->millis, t->validity, t->validity_offset} : ArrowTime{nullptr, nullptr, 0};
 }
 
+constexpr int AUNROLL = 4;
+
 template <int PERIOD, bool LENIENT, bool F32>
 void launch_z3_arrow(hipStream_t s, bool vec, ArrowPts g, ArrowTime tc, int64_t n, NDim lon, NDim lat, NDim tim,
                      int16_t* bin, int64_t* z, uint8_t* status, int64_t* err) {
+  if (vec && aligned16(g.c) && n >= 2) {
+    const int64_t np = n >> 1;
+    const unsigned vg = (unsigned)((np + ATPB * AUNROLL - 1) / (ATPB * AUNROLL));
+    if (tc.ms)
+      hipLaunchKernelGGL((k_z3_key_arrow_v<PERIOD, LENIENT, F32, true, AUNROLL>), dim3(vg), dim3(ATPB), 0, s, g, tc, n,
+                         lon, lat, tim, (short2*)bin, (lv2*)z, (uchar2*)status, err);
+    else
+      hipLaunchKernelGGL((k_z3_key_arrow_v<PERIOD, LENIENT, F32, false, AUNROLL>), dim3(vg), dim3(ATPB), 0, s, g, tc, n,
+                         lon, lat, tim, (short2*)bin, (lv2*)z, (uchar2*)status, err);
+    return;
+  }
   const unsigned grid = agrid((n + 1) >> 1);
   if (vec) hipLaunchKernelGGL((k_z3_key_arrow<PERIOD, LENIENT, F32, true>), dim3(grid), dim3(ATPB), 0, s, g, tc, n, lon, lat, tim, bin, z, status, err);
   else hipLaunchKernelGGL((k_z3_key_arrow<PERIOD, LENIENT, F32, false>), dim3(grid), dim3(ATPB), 0, s, g, tc, n, lon, lat, tim, bin, z, status, err);

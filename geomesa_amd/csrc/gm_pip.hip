@@ -1024,6 +1024,145 @@ __global__ __launch_bounds__(FTPB, GM_QUERY_WAVES) void k_query_mask(const doubl
   block_count_waves(cnt, block_counts);
 }
 
+// ------------------------------------------------------------------ row-wise predicate (UDF path)
+// st_contains / st_covers / st_intersects / ... evaluated row by row, as Spark SQL runs the UDF when
+// the join rule does not apply (SpatialRelationFunctions.scala:29-37 over nullableUDF,
+// SQLFunctionHelper.scala:27-33): row i pairs polygon poly[i] with point i.  Every DE-9IM predicate
+// of an areal geometry and a point is a function of the point's location in the polygon
+// (PointLocator.locate), so the kernel writes that location (LOC_*) and the host maps it.
+// The lookup is the join's: cell word chain, then only the entry of polygon poly[i] -- INTERIOR
+// decides at once, a blob is walked; no entry means the cell misses the polygon (exterior).
+constexpr int RTPB = 256;
+constexpr uint8_t LOC_NULL = 0xff;
+
+__device__ __forceinline__ int entry_poly(const PipDev& d, uint32_t e) {
+  const uint32_t ref = e & 0x3fffffffu;
+  if ((e >> 30) == CELL_INTERIOR) return (int)ref;
+  if (ref & BLOB_COMPACT) return (int)__double_as_longlong(d.compact[16 * (uint64_t)(ref & (BLOB_COMPACT - 1))]);
+  return ((const int2*)(d.blob + 2 * (uint64_t)ref))->x;
+}
+
+__device__ __forceinline__ int entry_locate(const PipDev& d, uint32_t e, double px, double py) {
+  if ((e >> 30) == CELL_INTERIOR) return LOC_INTERIOR;
+  const uint32_t ref = e & 0x3fffffffu;
+  if (ref & BLOB_COMPACT) {
+    int poly;
+    return compact_locate((const dv2*)(d.compact + 16 * (uint64_t)(ref & (BLOB_COMPACT - 1))), px, py, poly);
+  }
+  const double* b = d.blob + 2 * (uint64_t)ref;
+  return blob_locate(d, b, *(const int2*)b, px, py);
+}
+
+__global__ __launch_bounds__(RTPB) void k_list_poly(PipDev d, int64_t n, int32_t* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * RTPB + threadIdx.x;
+  if (i < n) out[i] = entry_poly(d, d.list_ent[i]);   // count / padding slots read as INTERIOR: no load
+}
+
+// Per wave: RILP rows per lane per step.  A row resolves at once when its cell is empty, interior, or
+// a list without polygon poly[i] (list_poly search); a boundary entry of the row's polygon is queued
+// in LDS and the wave walks 64 queued blobs at a time (one per lane), as the join does -- every row
+// writes its location exactly once.
+constexpr int RILP = 2;
+constexpr int RQCAP = 64 * (RILP + 1);
+
+__global__ __launch_bounds__(RTPB) void k_pip_relate(const int32_t* __restrict__ poly, const double* __restrict__ px,
+                                                     const double* __restrict__ py, int64_t n, int32_t n_polys,
+                                                     PipDev d, const int32_t* __restrict__ list_poly,
+                                                     uint8_t* __restrict__ loc) {
+  constexpr int NW = RTPB / 64;
+  __shared__ double s_x[NW][RQCAP], s_y[NW][RQCAP];
+  __shared__ int64_t s_row[NW][RQCAP];
+  __shared__ uint32_t s_e[NW][RQCAP];
+  __shared__ int32_t s_p[NW][RQCAP];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  double* qx = s_x[wave]; double* qy = s_y[wave];
+  int64_t* qr = s_row[wave]; uint32_t* qe = s_e[wave]; int32_t* qp = s_p[wave];
+  int qn = 0;
+  const int64_t wstep = (int64_t)gridDim.x * NW * (64 * RILP);
+  for (int64_t w0 = ((int64_t)blockIdx.x * NW + wave) * (64 * RILP);; w0 += wstep) {
+    const bool have = w0 < n;   // uniform per wave
+    if (have) {
+      int64_t row[RILP];
+      int p[RILP];
+      double x[RILP], y[RILP];
+      uint32_t w[RILP];
+      int cx[RILP], cy[RILP];
+#pragma unroll
+      for (int u = 0; u < RILP; ++u) {
+        row[u] = w0 + u * 64 + lane;
+        p[u] = -1; x[u] = y[u] = 0.0;
+        if (row[u] < n) { p[u] = poly[row[u]]; x[u] = px[row[u]]; y[u] = py[row[u]]; }
+      }
+#pragma unroll
+      for (int u = 0; u < RILP; ++u) {
+        w[u] = CELL_EMPTY << 30;
+        if (p[u] >= 0 && p[u] < n_polys && x[u] >= d.gx0 && x[u] <= d.gx1 && y[u] >= d.gy0 && y[u] <= d.gy1) {
+          cx[u] = cell_of(x[u], d.gx0, d.inv_cw, d.gx);
+          cy[u] = cell_of(y[u], d.gy0, d.inv_ch, d.gy);
+          w[u] = d.coarse_word[(int64_t)(cy[u] >> CF_LOG) * d.gxc + (cx[u] >> CF_LOG)];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < RILP; ++u)
+        if ((w[u] >> 30) == CELL_LIST) w[u] = d.cell_word[(int64_t)cy[u] * d.gx + cx[u]];
+#pragma unroll
+      for (int u = 0; u < RILP; ++u) {
+        uint8_t r = LOC_EXTERIOR;
+        bool queue = false;
+        uint32_t e = w[u];
+        const uint32_t kind = e >> 30;
+        if (p[u] < 0 || p[u] >= n_polys) {
+          r = LOC_NULL;
+        } else if (kind == CELL_INTERIOR) {
+          r = (int)(e & 0x3fffffffu) == p[u] ? LOC_INTERIOR : LOC_EXTERIOR;
+        } else if (kind == CELL_BOUNDARY) {
+          queue = true;   // the blob's polygon is checked when it is walked
+        } else if (kind == CELL_LIST) {
+          int l0 = 4 * (int)((e & 0x3fffffffu) >> 4), ni = (int)(e & 15u);
+          if (ni == LIST_LONG) { ni = (int)d.list_ent[l0]; l0 += 1; }
+          int j = 0;
+          while (j < ni && list_poly[l0 + j] != p[u]) ++j;
+          if (j < ni) {
+            e = d.list_ent[l0 + j];
+            if ((e >> 30) == CELL_INTERIOR) r = LOC_INTERIOR;
+            else queue = true;
+          }
+        }
+        if (row[u] < n && !queue) loc[row[u]] = r;
+        const uint64_t m = __ballot(queue && row[u] < n);
+        if (queue && row[u] < n) {
+          const int o = qn + lanes_below(m);
+          qx[o] = x[u]; qy[o] = y[u]; qr[o] = row[u]; qe[o] = e; qp[o] = p[u];
+        }
+        qn += __popcll(m);
+      }
+    }
+    // walk min(qn, 64) queued blobs when the queue holds a full wave, and drain it at the end
+    while (qn >= 64 || (!have && qn > 0)) {
+      wave_lds_sync();
+      const int kq = qn < 64 ? qn : 64;
+      const int slot = qn - kq + lane;
+      if (lane < kq) {
+        const uint32_t ref = qe[slot] & 0x3fffffffu;
+        const double ex = qx[slot], ey = qy[slot];
+        int pl, l;
+        if (ref & BLOB_COMPACT) {
+          l = compact_locate((const dv2*)(d.compact + 16 * (uint64_t)(ref & (BLOB_COMPACT - 1))), ex, ey, pl);
+        } else {
+          const double* b = d.blob + 2 * (uint64_t)ref;
+          const int2 h = *(const int2*)b;
+          pl = h.x;
+          l = blob_locate(d, b, h, ex, ey);
+        }
+        loc[qr[slot]] = (uint8_t)(pl == qp[slot] ? l : LOC_EXTERIOR);
+      }
+      wave_lds_sync();
+      qn -= kq;
+    }
+    if (!have) break;
+  }
+}
+
 template <bool VEC, bool DURING>
 void launch_query(hipStream_t s, unsigned grid, int op, const double* x, const double* y, const int64_t* t, int64_t n,
                   int has_bbox, const double* bb, int64_t lo, int64_t hi, const PipDev& d, uint64_t* mask,
@@ -1053,6 +1192,7 @@ struct gm_pip_index {
   int64_t n_entries = 0, n_boundary = 0, n_records = 0, n_slow = 0, n_cells = 0, blob_bytes = 0, n_compact = 0;
   int64_t max_bnd_per_cell = 0;   // most BOUNDARY (cell, polygon) entries of any cell: work items per point
   int64_t max_ent_per_cell = 0;   // most (cell, polygon) entries of any cell: pairs per point
+  const int32_t* list_poly = nullptr;   // polygon of each list_ent slot (the row-wise predicate's list search)
 };
 
 using namespace gm;
@@ -1476,6 +1616,16 @@ int gm_pip_index_create_ex(gm_ctx* ctx, const gm_polyset* ps, int cells_per_poly
   ix->dev.gx0 = G[0]; ix->dev.gy0 = G[1]; ix->dev.gx1 = G[2]; ix->dev.gy1 = G[3];
   ix->dev.inv_cw = inv_cw; ix->dev.inv_ch = inv_ch;
   ix->dev.gx = gx; ix->dev.gy = gy; ix->dev.gxc = gxc;
+  {
+    const int64_t ns = (int64_t)list_ent.size();
+    void* lp = nullptr;
+    if (hipMalloc(&lp, (size_t)ns * 4) != hipSuccess) { gm_pip_index_destroy(ix); return hip_fail(hipErrorOutOfMemory, "list_poly"); }
+    ix->allocs.push_back(lp);
+    ix->list_poly = (const int32_t*)lp;
+    hipLaunchKernelGGL(k_list_poly, dim3((unsigned)((ns + RTPB - 1) / RTPB)), dim3(RTPB), 0, ctx->stream, ix->dev, ns,
+                       (int32_t*)lp);
+    if (hipGetLastError() != hipSuccess) { gm_pip_index_destroy(ix); return hip_fail(hipErrorLaunchFailure, "k_list_poly"); }
+  }
   *out = ix;
   return GM_OK;
 }
@@ -1711,6 +1861,19 @@ int gm_query_scan(gm_ctx* ctx, const double* x, const double* y, const int64_t* 
   free_scan(ctx, mask, b);
   if (rc) return rc;
   if (n_match && ids && *n_match > ids_cap) return GM_E_CAPACITY;
+  return GM_OK;
+}
+
+int gm_pip_relate(gm_ctx* ctx, const gm_pip_index* ix, const int32_t* poly, const double* px, const double* py,
+                  int64_t n, uint8_t* loc) {
+  if (!ctx || !ix || n < 0) return GM_E_INVALID;
+  if (n == 0) return GM_OK;
+  if (!poly || !px || !py || !loc) return GM_E_INVALID;
+  GM_HIP(hipSetDevice(ctx->device));
+  const unsigned grid = resident_grid(k_pip_relate, ctx->device, (n + RTPB * RILP - 1) / (RTPB * RILP), false);
+  hipLaunchKernelGGL(k_pip_relate, dim3(grid), dim3(RTPB), 0, ctx->stream, poly, px, py, n, ix->n_polys, ix->dev,
+                     ix->list_poly, loc);
+  GM_CHECK_LAUNCH();
   return GM_OK;
 }
 

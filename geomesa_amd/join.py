@@ -145,6 +145,29 @@ class PolygonIndex:
             k = npairs.value
             return pt[:k], pl[:k]
 
+    def relate(self, poly_ids, px, py):
+        """Per-row location of point i in polygon poly_ids[i] (LOC_EXTERIOR / BOUNDARY / INTERIOR, or
+        LOC_NULL where poly_ids[i] < 0 marks a null row): the row-wise UDF path (gm_pip_relate)."""
+        import torch
+        from .curve import _dev_col
+        px = _dev_col(px, torch.float64)
+        py = _dev_col(py, torch.float64)
+        pid = _dev_col(poly_ids, torch.int64).to(torch.int32)
+        n = px.numel()
+        if py.numel() != n or pid.numel() != n:
+            raise ValueError("poly_ids, px and py must have one entry per row")
+        loc = torch.empty(n, dtype=torch.uint8, device=px.device)
+        check(self.ctx.lib.gm_pip_relate(self.ctx.handle, self._h, ptr(pid), ptr(px), ptr(py), n, ptr(loc)),
+              "gm_pip_relate")
+        return loc
+
+    def predicate(self, name, poly_ids, px, py):
+        """Spark SQL's st_* relation UDF row by row (SpatialRelationFunctions.scala:29-37) for
+        (polygon, point) rows: returns (value, is_null) bool device tensors (nullableUDF: a null
+        argument gives null, SQLFunctionHelper.scala:27-33).  st_within takes (point, polygon)."""
+        loc = self.relate(poly_ids, px, py)
+        return ROW_PREDICATES[name](loc), loc == LOC_NULL
+
     def close(self):
         if self._h:
             self.ctx.lib.gm_pip_index_destroy(self._h)
@@ -155,6 +178,22 @@ class PolygonIndex:
             self.close()
         except Exception:
             pass
+
+
+LOC_EXTERIOR, LOC_BOUNDARY, LOC_INTERIOR, LOC_NULL = 0, 1, 2, 255
+
+# DE-9IM predicates of (areal geometry, point) as functions of PointLocator's location
+ROW_PREDICATES = {
+    "st_contains": lambda l: l == LOC_INTERIOR,
+    "st_within": lambda l: l == LOC_INTERIOR,        # st_within(point, polygon)
+    "st_covers": lambda l: (l == LOC_INTERIOR) | (l == LOC_BOUNDARY),
+    "st_intersects": lambda l: (l == LOC_INTERIOR) | (l == LOC_BOUNDARY),
+    "st_touches": lambda l: l == LOC_BOUNDARY,
+    "st_disjoint": lambda l: l == LOC_EXTERIOR,
+    "st_crosses": lambda l: l != l,                  # a point cannot cross an area (IM T*****T** needs 2 points)
+    "st_overlaps": lambda l: l != l,                 # different dimensions
+    "st_equals": lambda l: l != l,
+}
 
 
 def st_contains_join(polyset, px, py):

@@ -252,6 +252,21 @@ int gm_query_scan(gm_ctx* ctx, const double* x, const double* y, const int64_t* 
                   const gm_pip_index* geoms, int spatial_op, uint64_t* mask, int64_t* ids, int64_t ids_cap,
                   int64_t* n_match);
 
+/* ------------------------------------------------------------------ row-wise predicates (UDF path) */
+/* Spark SQL's st_* relation UDFs evaluated row by row (SpatialRelationFunctions.scala:29-37, null in
+   -> null out via nullableUDF, SQLFunctionHelper.scala:27-33): row i relates polygon poly[i] of the
+   index with point (px[i], py[i]) and gets PointLocator's location of the point in the polygon.
+   For an areal geometry and a point every DE-9IM predicate follows from it:
+     st_contains(P, pt) = st_within(pt, P) = INTERIOR;  st_covers / st_intersects = not EXTERIOR;
+     st_touches = BOUNDARY;  st_disjoint = EXTERIOR;  st_crosses / st_overlaps / st_equals = false.
+   poly[i] < 0 or >= the polygon count marks a null row (GM_LOC_NULL).  Device arrays. */
+#define GM_LOC_EXTERIOR 0
+#define GM_LOC_BOUNDARY 1
+#define GM_LOC_INTERIOR 2
+#define GM_LOC_NULL 255
+int gm_pip_relate(gm_ctx* ctx, const gm_pip_index* index, const int32_t* poly, const double* px, const double* py,
+                  int64_t n, uint8_t* loc);
+
 /* ------------------------------------------------------------------ Arrow columnar input */
 /* GeoMesa's Arrow geometry vectors (geomesa-arrow-jts) as zero-copy device input.  A point column is
    a FixedSizeList(2) of Float8 (PointVector) or Float4 (PointFloatVector) whose tuples hold [y, x]
