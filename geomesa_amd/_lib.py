@@ -103,6 +103,7 @@ SIGNATURES = {
     "gm_pip_index_stats": (cint, [vp, vp]),
     "gm_pip_join": (cint, [vp, vp, vp, vp, i64, i64, vp, vp, i64, vp]),
     "gm_pip_join_ex": (cint, [vp, vp, vp, vp, i64, i64, vp, vp, i64, vp, cint]),
+    "gm_pip_join_pred": (cint, [vp, vp, vp, vp, i64, i64, vp, vp, i64, vp, cint, cint]),
     "gm_z3_key_bytes": (cint, [vp, vp, vp, vp, i64, vp]),
     "gm_sort_keys": (cint, [vp, vp, vp, vp, i64, vp, vp, vp, vp]),
     "gm_key_range_scan": (cint, [vp, vp, vp, vp, i64, vp, i64, vp, sz, vp, vp, i64, vp, vp]),
@@ -111,7 +112,7 @@ SIGNATURES = {
     "gm_xz2_index_key_arrow": (cint, [vp, vp, i64, cint, cint, vp, vp, vp]),
     "gm_xz3_index_key_arrow": (cint, [vp, vp, vp, i64, cint, cint, cint, vp, vp, vp, vp]),
     "gm_arrow_points_to_columns": (cint, [vp, vp, i64, vp, vp]),
-    "gm_pip_join_arrow": (cint, [vp, vp, vp, i64, i64, vp, vp, i64, vp, cint]),
+    "gm_pip_join_arrow": (cint, [vp, vp, vp, i64, i64, vp, vp, i64, vp, cint, cint]),
     "gm_pip_index_create_arrow": (cint, [vp, vp, i32, cint, vp]),
     "gm_pip_relate": (cint, [vp, vp, vp, vp, vp, i64, vp]),
     "gm_gen_points": (cint, [vp, ctypes.c_uint64, i64, i64, d, d, d, d, i64, i64, vp, vp, vp]),

@@ -290,17 +290,19 @@ class ArrowPolygonIndex:
         self.index = PolygonIndex.__new__(PolygonIndex)
         self.index.polyset, self.index.ctx, self.index._h = None, self.ctx, h
 
-    def join(self, points, id_base=0, cap=None, count_only=False, mode="auto", flip_axis=False):
-        """(pt_ids, poly_ids) with st_contains(poly, point) over an Arrow point column."""
+    def join(self, points, id_base=0, cap=None, count_only=False, mode="auto", flip_axis=False,
+             predicate="st_contains"):
+        """(pt_ids, poly_ids) with predicate(poly, point) over an Arrow point column."""
         import torch
         g = _as_geom(points, "point", flip_axis)
         n = g.n
         m = self.index.MODES[mode]
+        pr = self.index.PREDICATES[predicate]
         npairs = ctypes.c_int64()
         lib, hctx, hix = self.ctx.lib, self.ctx.handle, self.index._h
         if count_only:
             check(lib.gm_pip_join_arrow(hctx, hix, ctypes.byref(g.c_struct()), n, id_base, None, None, 0,
-                                        ctypes.byref(npairs), m), "gm_pip_join_arrow")
+                                        ctypes.byref(npairs), m, pr), "gm_pip_join_arrow")
             return npairs.value
         if cap is None:
             cap = max(1024, n + n // 4)
@@ -309,7 +311,7 @@ class ArrowPolygonIndex:
             pt = torch.empty(cap, dtype=torch.int64, device=dev)
             pl = torch.empty(cap, dtype=torch.int32, device=dev)
             rc = lib.gm_pip_join_arrow(hctx, hix, ctypes.byref(g.c_struct()), n, id_base, ptr(pt), ptr(pl), cap,
-                                       ctypes.byref(npairs), m)
+                                       ctypes.byref(npairs), m, pr)
             if rc == _lib.GM_E_CAPACITY:
                 cap = npairs.value
                 continue

@@ -60,6 +60,7 @@ struct PipDev {
   const double* blob;            // boundary blobs, 16-byte aligned
   double gx0, gy0, gx1, gy1, inv_cw, inv_ch;
   int32_t gx, gy, gxc;
+  int32_t op;                    // join predicate: JOIN_CONTAINS (interior) or JOIN_INTERSECTS (not exterior)
 };
 
 #ifndef GM_CF_LOG
@@ -180,6 +181,12 @@ __device__ int blob_locate(const PipDev& d, const double* b, int2 h, double px, 
   if (started) { if (cur == LOC_INTERIOR) is_in = true; if (cur == LOC_BOUNDARY) nb++; }
   if (nb & 1) return LOC_BOUNDARY;
   return (nb > 0 || is_in) ? LOC_INTERIOR : LOC_EXTERIOR;
+}
+
+enum : int32_t { JOIN_CONTAINS = 0, JOIN_INTERSECTS = 1 };
+// the join predicate on a located point: Geometry.contains (INTERIOR) or intersects / covers (not EXTERIOR)
+__device__ __forceinline__ bool join_hit(int32_t op, int loc) {
+  return op == JOIN_INTERSECTS ? loc != LOC_EXTERIOR : loc == LOC_INTERIOR;
 }
 
 // Geometry.contains(point): INTERIOR only (a point on the boundary is not contained)
@@ -495,12 +502,12 @@ __global__ __launch_bounds__(JTPB, GM_JOIN_WAVES) void k_pip_join(const double* 
 #endif
           if (ref & BLOB_COMPACT) {
             const dv2* c = (const dv2*)(d.compact + 16 * (uint64_t)(ref & (BLOB_COMPACT - 1)));
-            hit = compact_contains(c, ex, ey, poly);
+            hit = join_hit(d.op, compact_locate(c, ex, ey, poly));
           } else {
             const double* b = d.blob + 2 * (uint64_t)ref;
             const int2 h = *(const int2*)b;
             poly = h.x;
-            hit = blob_contains(d, b, h, ex, ey);
+            hit = join_hit(d.op, blob_locate(d, b, h, ex, ey));
           }
         }
         wave_lds_sync();
@@ -563,12 +570,12 @@ __global__ __launch_bounds__(JTPB) void k_pip_blobs(const double* __restrict__ p
         const double ex = px[row], ey = py[row];
         if (ref & BLOB_COMPACT) {
           const dv2* c = (const dv2*)(d.compact + 16 * (uint64_t)(ref & (BLOB_COMPACT - 1)));
-          hit = compact_contains(c, ex, ey, poly);
+          hit = join_hit(d.op, compact_locate(c, ex, ey, poly));
         } else {
           const double* b = d.blob + 2 * (uint64_t)ref;
           const int2 h = *(const int2*)b;
           poly = h.x;
-          hit = blob_contains(d, b, h, ex, ey);
+          hit = join_hit(d.op, blob_locate(d, b, h, ex, ey));
         }
       }
       if (!WRITE) my_count += hit;
@@ -1271,7 +1278,9 @@ static unsigned join_grid(int device, int64_t ntiles) {
 // the direct pass over an Arrow point column (tuples read in place)
 template <int SRC>
 static int join_direct_arrow(gm_ctx* ctx, const gm_pip_index* ix, ArrowPts ap, int64_t n, int64_t id_base,
-                             int64_t* pt_ids, int32_t* poly_ids, int64_t cap, unsigned long long* counter) {
+                             int64_t* pt_ids, int32_t* poly_ids, int64_t cap, unsigned long long* counter, int32_t op) {
+  PipDev dv = ix->dev;
+  dv.op = op;
   const bool write = pt_ids && poly_ids;
   const int64_t CHUNK = (int64_t)1 << 31;
   const size_t tb = SRC == 2 ? 8 : 16;
@@ -1283,11 +1292,11 @@ static int join_direct_arrow(gm_ctx* ctx, const gm_pip_index* ix, ArrowPts ap, i
     a.voff = ap.voff + c0;
     if (write)
       hipLaunchKernelGGL((k_pip_join<true, false, false, SRC>), dim3(join_grid<true, false, false, SRC>(ctx->device, ntiles)),
-                         dim3(JTPB), 0, ctx->stream, nullptr, nullptr, nullptr, nullptr, m, id_base + c0, ix->dev,
+                         dim3(JTPB), 0, ctx->stream, nullptr, nullptr, nullptr, nullptr, m, id_base + c0, dv,
                          pt_ids, poly_ids, cap, counter, SplitArgs{}, a);
     else
       hipLaunchKernelGGL((k_pip_join<false, false, false, SRC>), dim3(join_grid<false, false, false, SRC>(ctx->device, ntiles)),
-                         dim3(JTPB), 0, ctx->stream, nullptr, nullptr, nullptr, nullptr, m, id_base + c0, ix->dev,
+                         dim3(JTPB), 0, ctx->stream, nullptr, nullptr, nullptr, nullptr, m, id_base + c0, dv,
                          pt_ids, poly_ids, cap, counter, SplitArgs{}, a);
     GM_CHECK_LAUNCH();
   }
@@ -1656,7 +1665,16 @@ int gm_pip_join(gm_ctx* ctx, const gm_pip_index* ix, const double* px, const dou
 
 int gm_pip_join_ex(gm_ctx* ctx, const gm_pip_index* ix, const double* px, const double* py, int64_t n,
                    int64_t id_base, int64_t* pt_ids, int32_t* poly_ids, int64_t cap, int64_t* n_pairs, int mode) {
+  return gm_pip_join_pred(ctx, ix, px, py, n, id_base, pt_ids, poly_ids, cap, n_pairs, mode, GM_SPATIAL_CONTAINS);
+}
+
+int gm_pip_join_pred(gm_ctx* ctx, const gm_pip_index* ix, const double* px, const double* py, int64_t n,
+                     int64_t id_base, int64_t* pt_ids, int32_t* poly_ids, int64_t cap, int64_t* n_pairs, int mode,
+                     int predicate) {
   if (!ctx || !ix || n < 0 || cap < 0) return GM_E_INVALID;
+  if (predicate != GM_SPATIAL_CONTAINS && predicate != GM_SPATIAL_INTERSECTS) return GM_E_INVALID;
+  PipDev dv = ix->dev;
+  dv.op = predicate == GM_SPATIAL_INTERSECTS ? JOIN_INTERSECTS : JOIN_CONTAINS;
   if (mode != GM_JOIN_AUTO && mode != GM_JOIN_DIRECT && mode != GM_JOIN_PARTITIONED && mode != GM_JOIN_SPLIT)
     return GM_E_INVALID;
   const bool write = pt_ids && poly_ids;
@@ -1677,10 +1695,10 @@ int gm_pip_join_ex(gm_ctx* ctx, const gm_pip_index* ix, const double* px, const 
                                   : join_grid<false, false, false>(ctx->device, ntiles);
       if (write)
         hipLaunchKernelGGL((k_pip_join<true, false, false>), dim3(grid), dim3(JTPB), 0, ctx->stream, px + c0, py + c0,
-                           nullptr, nullptr, m, id_base + c0, ix->dev, pt_ids, poly_ids, cap, counter, SplitArgs{}, ArrowPts{});
+                           nullptr, nullptr, m, id_base + c0, dv, pt_ids, poly_ids, cap, counter, SplitArgs{}, ArrowPts{});
       else
         hipLaunchKernelGGL((k_pip_join<false, false, false>), dim3(grid), dim3(JTPB), 0, ctx->stream, px + c0, py + c0,
-                           nullptr, nullptr, m, id_base + c0, ix->dev, pt_ids, poly_ids, cap, counter, SplitArgs{}, ArrowPts{});
+                           nullptr, nullptr, m, id_base + c0, dv, pt_ids, poly_ids, cap, counter, SplitArgs{}, ArrowPts{});
       GM_CHECK_LAUNCH();
     }
   } else if (mode == GM_JOIN_SPLIT && n > 0) {
@@ -1728,18 +1746,18 @@ int gm_pip_join_ex(gm_ctx* ctx, const gm_pip_index* ix, const double* px, const 
       // every segment is written (counts) by its wave; the grid stays grid_a for every chunk
       if (write)
         hipLaunchKernelGGL((k_pip_join<true, false, true>), dim3(grid_a), dim3(JTPB), 0, ctx->stream, px + c0, py + c0,
-                           nullptr, nullptr, m, id_base + c0, ix->dev, pt_ids, poly_ids, cap, counter, sp, ArrowPts{});
+                           nullptr, nullptr, m, id_base + c0, dv, pt_ids, poly_ids, cap, counter, sp, ArrowPts{});
       else
         hipLaunchKernelGGL((k_pip_join<false, false, true>), dim3(grid_a), dim3(JTPB), 0, ctx->stream, px + c0,
-                           py + c0, nullptr, nullptr, m, id_base + c0, ix->dev, pt_ids, poly_ids, cap, counter, sp, ArrowPts{});
+                           py + c0, nullptr, nullptr, m, id_base + c0, dv, pt_ids, poly_ids, cap, counter, sp, ArrowPts{});
       GM_CHECK_LAUNCH();
       const unsigned bgrid = write ? resident_grid(k_pip_blobs<true>, ctx->device, sp.nseg, false)
                                    : resident_grid(k_pip_blobs<false>, ctx->device, sp.nseg, false);
       if (write)
-        hipLaunchKernelGGL((k_pip_blobs<true>), dim3(bgrid), dim3(JTPB), 0, ctx->stream, px + c0, py + c0, ix->dev,
+        hipLaunchKernelGGL((k_pip_blobs<true>), dim3(bgrid), dim3(JTPB), 0, ctx->stream, px + c0, py + c0, dv,
                            counter, sp);
       else
-        hipLaunchKernelGGL((k_pip_blobs<false>), dim3(bgrid), dim3(JTPB), 0, ctx->stream, px + c0, py + c0, ix->dev,
+        hipLaunchKernelGGL((k_pip_blobs<false>), dim3(bgrid), dim3(JTPB), 0, ctx->stream, px + c0, py + c0, dv,
                            counter, sp);
       GM_CHECK_LAUNCH();
       if (write) {
@@ -1783,10 +1801,10 @@ int gm_pip_join_ex(gm_ctx* ctx, const gm_pip_index* ix, const double* px, const 
                                   : join_grid<false, true, false>(ctx->device, ntiles);
       if (write)
         hipLaunchKernelGGL((k_pip_join<true, true, false>), dim3(grid), dim3(JTPB), 0, ctx->stream, nullptr, nullptr,
-                           rec, n_rec, m, id_base + c0, ix->dev, pt_ids, poly_ids, cap, counter, SplitArgs{}, ArrowPts{});
+                           rec, n_rec, m, id_base + c0, dv, pt_ids, poly_ids, cap, counter, SplitArgs{}, ArrowPts{});
       else
         hipLaunchKernelGGL((k_pip_join<false, true, false>), dim3(grid), dim3(JTPB), 0, ctx->stream, nullptr, nullptr,
-                           rec, n_rec, m, id_base + c0, ix->dev, pt_ids, poly_ids, cap, counter, SplitArgs{}, ArrowPts{});
+                           rec, n_rec, m, id_base + c0, dv, pt_ids, poly_ids, cap, counter, SplitArgs{}, ArrowPts{});
       if (hipGetLastError() != hipSuccess) rc = hip_fail(hipErrorLaunchFailure, "k_pip_join (partitioned)");
     }
     if (rc) return rc;
@@ -1801,8 +1819,10 @@ int gm_pip_join_ex(gm_ctx* ctx, const gm_pip_index* ix, const double* px, const 
 }
 
 int gm_pip_join_arrow(gm_ctx* ctx, const gm_pip_index* ix, const gm_geom_column* pts, int64_t n, int64_t id_base,
-                      int64_t* pt_ids, int32_t* poly_ids, int64_t cap, int64_t* n_pairs, int mode) {
+                      int64_t* pt_ids, int32_t* poly_ids, int64_t cap, int64_t* n_pairs, int mode, int predicate) {
   if (!ctx || !ix || n < 0 || cap < 0 || !pts) return GM_E_INVALID;
+  if (predicate != GM_SPATIAL_CONTAINS && predicate != GM_SPATIAL_INTERSECTS) return GM_E_INVALID;
+  const int32_t op = predicate == GM_SPATIAL_INTERSECTS ? JOIN_INTERSECTS : JOIN_CONTAINS;
   if (pts->type != GM_GEOM_POINT || (pts->ordinal_bits != 64 && pts->ordinal_bits != 32)) return GM_E_INVALID;
   if (n > 0 && !pts->coords) return GM_E_INVALID;
   if ((pt_ids == nullptr) != (poly_ids == nullptr)) return GM_E_INVALID;
@@ -1814,8 +1834,8 @@ int gm_pip_join_arrow(gm_ctx* ctx, const gm_pip_index* ix, const gm_geom_column*
     unsigned long long* counter = (unsigned long long*)ctx->d_scratch;
     GM_HIP(hipMemsetAsync(counter, 0, 8, ctx->stream));
     int rc = n == 0 ? GM_OK
-             : ap.f32 ? join_direct_arrow<2>(ctx, ix, ap, n, id_base, pt_ids, poly_ids, cap, counter)
-                      : join_direct_arrow<1>(ctx, ix, ap, n, id_base, pt_ids, poly_ids, cap, counter);
+             : ap.f32 ? join_direct_arrow<2>(ctx, ix, ap, n, id_base, pt_ids, poly_ids, cap, counter, op)
+                      : join_direct_arrow<1>(ctx, ix, ap, n, id_base, pt_ids, poly_ids, cap, counter, op);
     if (rc) return rc;
     GM_HIP(hipMemcpyAsync(ctx->h_pinned, counter, 8, hipMemcpyDeviceToHost, ctx->stream));
     GM_HIP(hipStreamSynchronize(ctx->stream));
@@ -1827,7 +1847,7 @@ int gm_pip_join_arrow(gm_ctx* ctx, const gm_pip_index* ix, const gm_geom_column*
   double* xy = nullptr;
   GM_HIP(hipMallocAsync((void**)&xy, (size_t)std::max<int64_t>(n, 1) * 16, ctx->stream));
   int rc = gm_arrow_points_to_columns(ctx, pts, n, xy, xy + n);
-  if (!rc) rc = gm_pip_join_ex(ctx, ix, xy, xy + n, n, id_base, pt_ids, poly_ids, cap, n_pairs, mode);
+  if (!rc) rc = gm_pip_join_pred(ctx, ix, xy, xy + n, n, id_base, pt_ids, poly_ids, cap, n_pairs, mode, predicate);
   (void)hipFreeAsync(xy, ctx->stream);
   return rc;
 }

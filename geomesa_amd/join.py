@@ -114,13 +114,18 @@ class PolygonIndex:
     MODES = {"auto": _lib.GM_JOIN_AUTO, "direct": _lib.GM_JOIN_DIRECT, "partitioned": _lib.GM_JOIN_PARTITIONED,
              "split": _lib.GM_JOIN_SPLIT}
 
-    def join(self, px, py, id_base=0, cap=None, count_only=False, mode="auto"):
+    PREDICATES = {"st_contains": _lib.GM_SPATIAL_CONTAINS, "st_within": _lib.GM_SPATIAL_CONTAINS,
+                  "st_intersects": _lib.GM_SPATIAL_INTERSECTS, "st_covers": _lib.GM_SPATIAL_INTERSECTS}
+
+    def join(self, px, py, id_base=0, cap=None, count_only=False, mode="auto", predicate="st_contains"):
         """Returns (pt_ids, poly_ids) device tensors (or the pair count when count_only).
 
         mode: "auto", "direct" (one pass over the point columns), "partitioned" (points
         counting-sorted by grid-row band first) or "split" (lookups, then a work list of boundary
-        evaluations); the pair set is the same for every mode."""
+        evaluations); the pair set is the same for every mode.  predicate: the join condition's UDF,
+        st_contains(polygon, point) / st_within(point, polygon) or st_intersects / st_covers."""
         m = self.MODES[mode]
+        pr = self.PREDICATES[predicate]
         import torch
         from .curve import _dev_col
         px = _dev_col(px, torch.float64)
@@ -128,16 +133,16 @@ class PolygonIndex:
         n = px.numel()
         npairs = ctypes.c_int64()
         if count_only:
-            check(self.ctx.lib.gm_pip_join_ex(self.ctx.handle, self._h, ptr(px), ptr(py), n, id_base, None, None, 0,
-                                              ctypes.byref(npairs), m), "gm_pip_join")
+            check(self.ctx.lib.gm_pip_join_pred(self.ctx.handle, self._h, ptr(px), ptr(py), n, id_base, None, None,
+                                                0, ctypes.byref(npairs), m, pr), "gm_pip_join")
             return npairs.value
         if cap is None:
             cap = max(1024, n + n // 4)
         while True:
             pt = torch.empty(cap, dtype=torch.int64, device=px.device)
             pl = torch.empty(cap, dtype=torch.int32, device=px.device)
-            rc = self.ctx.lib.gm_pip_join_ex(self.ctx.handle, self._h, ptr(px), ptr(py), n, id_base, ptr(pt),
-                                             ptr(pl), cap, ctypes.byref(npairs), m)
+            rc = self.ctx.lib.gm_pip_join_pred(self.ctx.handle, self._h, ptr(px), ptr(py), n, id_base, ptr(pt),
+                                               ptr(pl), cap, ctypes.byref(npairs), m, pr)
             if rc == _lib.GM_E_CAPACITY:
                 cap = npairs.value
                 continue

@@ -234,6 +234,15 @@ int gm_pip_join(gm_ctx* ctx, const gm_pip_index* index, const double* px, const 
 int gm_pip_join_ex(gm_ctx* ctx, const gm_pip_index* index, const double* px, const double* py, int64_t n,
                    int64_t id_base, int64_t* pt_ids, int32_t* poly_ids, int64_t cap, int64_t* n_pairs, int mode);
 
+/* gm_pip_join_ex with the join's predicate: GM_SPATIAL_CONTAINS (st_contains(polygon, point) /
+   st_within(point, polygon): the point in the interior) or GM_SPATIAL_INTERSECTS (st_intersects /
+   st_covers: boundary included).  GeoMesaJoinRelation takes any (Geometry, Geometry) => Boolean UDF of
+   the join condition (GeoMesaJoinRelation.scala:67-79, SQLRules.scala:186-190); these are the ones with
+   a non-empty result over (polygon, point) pairs besides st_touches. */
+int gm_pip_join_pred(gm_ctx* ctx, const gm_pip_index* index, const double* px, const double* py, int64_t n,
+                     int64_t id_base, int64_t* pt_ids, int32_t* poly_ids, int64_t cap, int64_t* n_pairs, int mode,
+                     int predicate);
+
 /* ------------------------------------------------------------------ fused query filter */
 /* spatial terms of gm_query_scan */
 #define GM_SPATIAL_NONE 0
@@ -322,10 +331,11 @@ int gm_xz3_index_key_arrow(gm_ctx* ctx, const gm_geom_column* geom, const gm_tim
                            gm_batch_status* summary);
 /* A point column as x / y device columns (null slots -> NaN): the adapter for every other entry */
 int gm_arrow_points_to_columns(gm_ctx* ctx, const gm_geom_column* geom, int64_t n, double* x, double* y);
-/* gm_pip_join_ex over an Arrow point column (null points never match): the direct pass reads the
+/* gm_pip_join_pred over an Arrow point column (null points never match): the direct pass reads the
    tuples in place; the partitioned and split strategies go through gm_arrow_points_to_columns */
 int gm_pip_join_arrow(gm_ctx* ctx, const gm_pip_index* index, const gm_geom_column* points, int64_t n,
-                      int64_t id_base, int64_t* pt_ids, int32_t* poly_ids, int64_t cap, int64_t* n_pairs, int mode);
+                      int64_t id_base, int64_t* pt_ids, int32_t* poly_ids, int64_t cap, int64_t* n_pairs, int mode,
+                      int predicate);
 /* gm_pip_index_create_ex from an Arrow POLYGON or MULTIPOLYGON column given in HOST memory (the
    broadcast side of the join is collected on the host); a null slot is an empty polygon */
 int gm_pip_index_create_arrow(gm_ctx* ctx, const gm_geom_column* polys, int32_t n, int cells_per_poly,

@@ -89,3 +89,51 @@ def test_relate_box_kats(gpu):
     con, null = ix.predicate("st_contains", poly, px, py)
     assert as_np(con).tolist() == [True, False, False, False, False, True, False]
     assert as_np(null).tolist() == [False] * 6 + [True]
+
+
+def _envelopes(ps):
+    ppo, pro, rvo, vx, vy = ps.to_arrays()
+    env = []
+    for p in range(ps.n_polys):
+        a, b = rvo[pro[ppo[p]]], rvo[pro[ppo[p + 1]]]
+        env.append((vx[a:b].min(), vy[a:b].min(), vx[a:b].max(), vy[a:b].max()))
+    return np.array(env)
+
+
+def oracle_pairs(oracle, ps, px, py, pred):
+    ops = oracle.OraclePolySet(*ps.to_arrays())
+    env = _envelopes(ps)
+    out = set()
+    for i, (x, y) in enumerate(zip(px, py)):
+        cand = np.flatnonzero((env[:, 0] <= x) & (x <= env[:, 2]) & (env[:, 1] <= y) & (y <= env[:, 3]))
+        for p in cand:
+            if (ops.intersects if pred == "st_intersects" else ops.contains)(int(p), x, y):
+                out.add((i, int(p)))
+    return out
+
+
+@pytest.mark.parametrize("mode", ["auto", "split", "partitioned"])
+@pytest.mark.parametrize("pred", ["st_intersects", "st_contains"])
+def test_join_predicates_with_boundary_points(gpu, oracle, mode, pred):
+    """The join condition's UDF (GeoMesaJoinRelation.scala:67-79): st_intersects keeps the points on
+    polygon boundaries (vertices, edge midpoints) that st_contains drops."""
+    from geomesa_amd.join import PolygonIndex, synthetic_counties
+    ps = synthetic_counties(NX, NY)
+    _, px, py = rows(ps, 30_000, seed=21)
+    pt, pl = PolygonIndex(ps).join(px, py, mode=mode, predicate=pred)
+    got = set(zip(as_np(pt).tolist(), as_np(pl).tolist()))
+    exp = oracle_pairs(oracle, ps, px, py, pred)
+    assert got == exp
+    if pred == "st_intersects":
+        assert len(exp) > len(oracle_pairs(oracle, ps, px, py, "st_contains")) + 500
+
+
+def test_arrow_join_intersects(gpu, oracle):
+    from geomesa_amd import arrow
+    from geomesa_amd.join import synthetic_counties
+    from test_gpu_arrow import point_array, polyset_to_arrow
+    ps = synthetic_counties(NX, NY)
+    _, px, py = rows(ps, 20_000, seed=5)
+    ix = arrow.ArrowPolygonIndex(polyset_to_arrow(ps), kind="multipolygon")
+    pt, pl = ix.join(point_array(px, py), predicate="st_intersects")
+    assert set(zip(as_np(pt).tolist(), as_np(pl).tolist())) == oracle_pairs(oracle, ps, px, py, "st_intersects")
