@@ -343,6 +343,16 @@ def main():
         rec("arrow_z3_keys", lambda: lib.gm_z3_index_key_arrow(h, ctypes.byref(gcol), ctypes.byref(tcol), N, 1, 0, P(b),
                                                               P(z), None, None), 34, N)
         del yx
+        # Z3Histogram.observe over the same points (stats caller): 54 week bins of 2020 x 512
+        # counters fit the LDS-private path; x 1024 takes the device-atomic path
+        hp = torch.zeros(54, dtype=torch.uint8, device=x.device)
+        htl = torch.zeros(2, dtype=torch.int64, device=x.device)
+        for hl, nm in ((512, "z3_histogram"), (1024, "z3_histogram_1024")):
+            hc = torch.zeros((54, hl), dtype=torch.int64, device=x.device)
+            rec(nm, lambda: lib.gm_z3_histogram(h, P(x), P(y), P(t), N, 1, hl, 0, 2608, 54, P(hp), P(hc), P(htl)),
+                24, N)
+            extra[nm]["length"] = hl
+            del hc
         # filter scan, key space (configs[2] query on the resident keys)
         from geomesa_amd import filters as F
         from geomesa_amd.keyspace import Z3IndexKeySpace, during

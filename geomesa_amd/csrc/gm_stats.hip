@@ -1,0 +1,269 @@
+// gm_stats.hip -- Z3Histogram.observe / unobserve over a batch of point features on gfx950.
+//
+// Reference: Z3Histogram (utils/stats/Z3Histogram.scala:101-128): per feature toKey (:80-86) =
+// BinnedTime.timeToBinnedTime(period) + Z3SFC(period).index(centroid, offset, lenient), then
+// binMap(timeBin).add(z, +-1) where the bin array is BinnedArray(LongBinning(length, (minZ, maxZ)))
+// (utils/stats/BinnedArray.scala:59-64, 185-201) with minZ / maxZ the z of MinMaxGeometry.min / max
+// (MinMax.scala:191-192) at sfc.time.min / max (Z3Histogram.scala:53-54).
+//
+// Shape: the same streaming read as the Z3 key kernel (24 B/point, 16-B pair loads) with the
+// write side replaced by an increment.  Every workgroup keeps a private int32 copy of a block of
+// time-bin rows of the [n_bins][length] counters in LDS (<= 32768 int32 = 128 KB) and flushes the
+// nonzero counters with one 64-bit device atomic each at the end, so HBM traffic is the 24 B/point
+// read plus grid x counters x 8 B; the grid is one resident wave of workgroups (1-2 per CU).  A
+// histogram larger than one LDS block takes up to HIST_MAX_PASSES passes over the points, one per
+// row block; beyond that it adds straight into the 64-bit device counters (scattered per-lane
+// device atomics run ~22 G/s on MI355X, so they only win over many passes).
+#include "gm_keys.hpp"
+
+namespace gm {
+
+constexpr int HTPB = 1024;
+constexpr int HIST_LDS_MAX = 32768;  // int32 counters per workgroup (128 KB of the 160 KB LDS)
+constexpr int HIST_MAX_PASSES = 4;
+
+struct HistArgs {
+  int64_t n;
+  int length, bin_lo, n_bins;
+  int64_t zmin, zmax;
+  double bsize;  // LongBinning.binSize = (max - min).toDouble / length
+  NDim lon, lat, tim;
+  int row_lo, row_n;  // LDS pass: the time-bin rows [row_lo, row_lo + row_n) of the window it counts
+  int tally;          // this launch reports skipped / outside features (the first pass only)
+};
+
+// LongBinning.directIndex (BinnedArray.scala:195-201); (value - min) is a Long, divided by a Double
+__device__ __forceinline__ int long_bin_index(int64_t v, const HistArgs& a) {
+  if (v < a.zmin || v > a.zmax) return -1;
+  const double q = floor((double)(int64_t)((uint64_t)v - (uint64_t)a.zmin) / a.bsize);
+  const int i = q >= 2147483647.0 ? 2147483647 : (q <= -2147483648.0 ? (-2147483647 - 1) : (int)q);
+  if (i < 0 || i > a.length) return -1;
+  return i == a.length ? a.length - 1 : i;
+}
+
+// toKey + bin lookup for one feature; returns the flat counter index, -1 to drop, and classifies
+// drops: *skip for a throwing toKey (the Scala code logs and moves on), *out for a time bin
+// outside the caller's window [bin_lo, bin_lo + n_bins)
+template <int PERIOD, bool UNOBS>
+__device__ __forceinline__ int hist_slot(double x, double y, int64_t ms, const HistArgs& a, int& rb, int& skip,
+                                         int& out) {
+  int16_t b;
+  int64_t off, z;
+  uint8_t st = binned_time<PERIOD>(ms, b, off);
+  if (st == ST_OK) st = z3_index_one<UNOBS>(x, y, off, a.lon, a.lat, a.tim, z);  // unobserve is lenient
+  if (st != ST_OK) { ++skip; return -1; }
+  rb = (int)b - a.bin_lo;
+  if (rb < 0 || rb >= a.n_bins) { ++out; return -1; }
+  const int i = long_bin_index(z, a);
+  return i < 0 ? -1 : rb * a.length + i;
+}
+
+template <int PERIOD, bool UNOBS, bool VEC>
+__global__ __launch_bounds__(HTPB) void k_z3_hist_lds(const double* __restrict__ x, const double* __restrict__ y,
+                                                      const int64_t* __restrict__ t, HistArgs a,
+                                                      uint8_t* __restrict__ present,
+                                                      unsigned long long* __restrict__ counts,
+                                                      unsigned long long* __restrict__ tally) {
+  extern __shared__ int lds[];
+  int* cnt = lds;                          // [row_n * length]
+  int* pres = lds + a.row_n * a.length;    // [row_n]: bin present (observe sets, unobserve reads)
+  __shared__ int s_skip, s_out;
+  const int total = a.row_n * a.length;
+  counts += (int64_t)a.row_lo * a.length;
+  present += a.row_lo;
+  for (int i = threadIdx.x; i < total; i += HTPB) cnt[i] = 0;
+  for (int i = threadIdx.x; i < a.row_n; i += HTPB) pres[i] = UNOBS ? (int)present[i] : 0;
+  if (threadIdx.x == 0) { s_skip = 0; s_out = 0; }
+  __syncthreads();
+  int skip = 0, out = 0;
+  auto one = [&](double xx, double yy, int64_t tt) {
+    int rb = 0;
+    int c = hist_slot<PERIOD, UNOBS>(xx, yy, tt, a, rb, skip, out);
+    rb -= a.row_lo;
+    if (c < 0 || rb < 0 || rb >= a.row_n) return;
+    c -= a.row_lo * a.length;
+    if (UNOBS) {
+      if (pres[rb]) atomicAdd(&cnt[c], -1);  // binMap.get(timeBin).foreach(_.add(z, -1))
+    } else {
+      atomicAdd(&cnt[c], 1);
+      if (!pres[rb]) pres[rb] = 1;           // binMap.getOrElseUpdate(timeBin, newBins)
+    }
+  };
+  const int64_t stride = (int64_t)gridDim.x * HTPB;
+  if (VEC) {
+    const dv2* x2 = (const dv2*)x;
+    const dv2* y2 = (const dv2*)y;
+    const lv2* t2 = (const lv2*)t;
+    const int64_t np = a.n >> 1;
+    // software-pipelined: the next HU pairs per lane are in flight while the current ones are binned
+    constexpr int HU = 2;
+    dv2 xa[HU], ya[HU];
+    lv2 ta[HU];
+    int64_t p = (int64_t)blockIdx.x * HTPB + threadIdx.x;
+#pragma unroll
+    for (int u = 0; u < HU; ++u) {
+      const int64_t q = p + u * stride;
+      if (q < np) { xa[u] = ld_stream(&x2[q]); ya[u] = ld_stream(&y2[q]); ta[u] = ld_stream(&t2[q]); }
+    }
+    while (p < np) {
+      const int64_t pn = p + HU * stride;
+      dv2 xb[HU], yb[HU];
+      lv2 tb[HU];
+#pragma unroll
+      for (int u = 0; u < HU; ++u) {
+        const int64_t q = pn + u * stride;
+        if (q < np) { xb[u] = ld_stream(&x2[q]); yb[u] = ld_stream(&y2[q]); tb[u] = ld_stream(&t2[q]); }
+      }
+#pragma unroll
+      for (int u = 0; u < HU; ++u) {
+        if (p + u * stride < np) { one(xa[u].x, ya[u].x, ta[u].x); one(xa[u].y, ya[u].y, ta[u].y); }
+        xa[u] = xb[u]; ya[u] = yb[u]; ta[u] = tb[u];
+      }
+      p = pn;
+    }
+    if ((a.n & 1) && blockIdx.x == 0 && threadIdx.x == 0) one(x[a.n - 1], y[a.n - 1], t[a.n - 1]);
+  } else {
+    for (int64_t i = (int64_t)blockIdx.x * HTPB + threadIdx.x; i < a.n; i += stride) one(x[i], y[i], t[i]);
+  }
+  if (skip) atomicAdd(&s_skip, skip);
+  if (out) atomicAdd(&s_out, out);
+  __syncthreads();
+  for (int i = threadIdx.x; i < total; i += HTPB) {
+    const int v = cnt[i];
+    if (v) atomicAdd(&counts[i], (unsigned long long)(long long)v);
+  }
+  if (!UNOBS) {
+    for (int i = threadIdx.x; i < a.row_n; i += HTPB)
+      if (pres[i] && !present[i]) present[i] = 1;
+  }
+  if (threadIdx.x == 0 && a.tally) {
+    if (s_skip) atomicAdd(&tally[0], (unsigned long long)s_skip);
+    if (s_out) atomicAdd(&tally[1], (unsigned long long)s_out);
+  }
+}
+
+// histograms too large for LDS: 64-bit device atomics per feature
+template <int PERIOD, bool UNOBS>
+__global__ __launch_bounds__(256) void k_z3_hist_global(const double* __restrict__ x, const double* __restrict__ y,
+                                                        const int64_t* __restrict__ t, HistArgs a,
+                                                        uint8_t* __restrict__ present,
+                                                        unsigned long long* __restrict__ counts,
+                                                        unsigned long long* __restrict__ tally) {
+  __shared__ int s_skip, s_out;
+  if (threadIdx.x == 0) { s_skip = 0; s_out = 0; }
+  __syncthreads();
+  int skip = 0, out = 0;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < a.n; i += (int64_t)gridDim.x * 256) {
+    int rb = 0;
+    const int c = hist_slot<PERIOD, UNOBS>(x[i], y[i], t[i], a, rb, skip, out);
+    if (c < 0) continue;
+    if (UNOBS) {
+      if (present[rb]) atomicAdd(&counts[c], ~0ull);  // += -1
+    } else {
+      atomicAdd(&counts[c], 1ull);
+      if (!present[rb]) present[rb] = 1;
+    }
+  }
+  if (skip) atomicAdd(&s_skip, skip);
+  if (out) atomicAdd(&s_out, out);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (s_skip) atomicAdd(&tally[0], (unsigned long long)s_skip);
+    if (s_out) atomicAdd(&tally[1], (unsigned long long)s_out);
+  }
+}
+
+template <int PERIOD, bool UNOBS>
+int launch_hist(gm_ctx* ctx, const double* x, const double* y, const int64_t* t, HistArgs a, uint8_t* present,
+                unsigned long long* counts, unsigned long long* tally) {
+  hipStream_t s = ctx->stream;
+  // time-bin rows per LDS pass; every pass re-reads the 24 B/point, so more than HIST_MAX_PASSES
+  // passes lose to the device-atomic kernel (measured: 2 LDS passes ~12 ms vs 45 ms atomics per 1B)
+  const int rows = (HIST_LDS_MAX) / (a.length + 1);
+  const int passes = rows > 0 ? (a.n_bins + rows - 1) / rows : 1 << 30;
+  if (passes <= HIST_MAX_PASSES) {
+    const bool vec = aligned16(x) && aligned16(y) && aligned16(t);
+    int cus = 256;
+    GM_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
+    for (int k = 0; k < passes; ++k) {
+      a.row_lo = k * rows;
+      a.row_n = std::min(rows, a.n_bins - a.row_lo);
+      a.tally = k == 0;
+      const size_t lds = (size_t)(a.row_n * a.length + a.row_n) * sizeof(int);
+      const int per_cu = lds <= 40 * 1024 ? 2 : 1;  // 2 x 1024 threads is the CU's wave limit
+      // per workgroup <= 2^31 increments so the int32 LDS counters cannot wrap
+      const int64_t need = (a.n + (int64_t)2147483647 - 1) / (int64_t)2147483647;
+      const int64_t want = (a.n + HTPB - 1) / HTPB;
+      int64_t grid = std::min<int64_t>((int64_t)cus * per_cu, std::max<int64_t>(want, 1));
+      grid = std::max(grid, need);
+      if (vec) {
+        GM_HIP(hipFuncSetAttribute((const void*)k_z3_hist_lds<PERIOD, UNOBS, true>,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        hipLaunchKernelGGL((k_z3_hist_lds<PERIOD, UNOBS, true>), dim3((unsigned)grid), dim3(HTPB), lds, s, x, y,
+                           t, a, present, counts, tally);
+      } else {
+        GM_HIP(hipFuncSetAttribute((const void*)k_z3_hist_lds<PERIOD, UNOBS, false>,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        hipLaunchKernelGGL((k_z3_hist_lds<PERIOD, UNOBS, false>), dim3((unsigned)grid), dim3(HTPB), lds, s, x,
+                           y, t, a, present, counts, tally);
+      }
+      GM_CHECK_LAUNCH();
+    }
+  } else {
+    hipLaunchKernelGGL((k_z3_hist_global<PERIOD, UNOBS>), dim3((unsigned)std::min<int64_t>((a.n + 255) / 256, 256 * 16)),
+                       dim3(256), 0, s, x, y, t, a, present, counts, tally);
+    GM_CHECK_LAUNCH();
+  }
+  return GM_OK;
+}
+
+template <int PERIOD>
+int launch_hist_p(gm_ctx* ctx, const double* x, const double* y, const int64_t* t, const HistArgs& a, bool unobs,
+                  uint8_t* present, unsigned long long* counts, unsigned long long* tally) {
+  return unobs ? launch_hist<PERIOD, true>(ctx, x, y, t, a, present, counts, tally)
+               : launch_hist<PERIOD, false>(ctx, x, y, t, a, present, counts, tally);
+}
+
+}  // namespace gm
+
+using namespace gm;
+
+extern "C" {
+
+int gm_z3_histogram(gm_ctx* ctx, const double* x, const double* y, const int64_t* t_ms, int64_t n, int period,
+                    int length, int unobserve, int bin_lo, int n_bins, uint8_t* present, int64_t* counts,
+                    int64_t* tally) {
+  if (!ctx || n < 0 || !valid_period(period) || length < 1 || n_bins < 1 || bin_lo < -32768 ||
+      bin_lo + (int64_t)n_bins > 32768 || (int64_t)n_bins * length > ((int64_t)1 << 31) - 1)
+    return GM_E_INVALID;
+  if (n == 0) return GM_OK;
+  if (!x || !y || !t_ms || !present || !counts || !tally) return GM_E_INVALID;
+  HistArgs a;
+  a.n = n;
+  a.length = length;
+  a.bin_lo = bin_lo;
+  a.n_bins = n_bins;
+  a.row_lo = 0;
+  a.row_n = n_bins;
+  a.tally = 1;
+  a.lon = lon_dim(21);
+  a.lat = lat_dim(21);
+  a.tim = time_dim(period, 21);
+  // minZ / maxZ (Z3Histogram.scala:53-54): sfc.index(-180, -90, time.min) normalizes every dimension
+  // to 0, sfc.index(180, 90, time.max) every dimension to maxIndex (x >= max, NormalizedDimension
+  // .scala:60), so for every period minZ = 0 and maxZ = Z3(2^21-1, 2^21-1, 2^21-1) = Long.MaxValue
+  a.zmin = 0;
+  a.zmax = INT64_MAX;
+  a.bsize = (double)(int64_t)((uint64_t)a.zmax - (uint64_t)a.zmin) / (double)length;
+  unsigned long long* c = (unsigned long long*)counts;
+  unsigned long long* tl = (unsigned long long*)tally;
+  const bool u = unobserve != 0;
+  switch (period) {
+    case DAY: return launch_hist_p<DAY>(ctx, x, y, t_ms, a, u, present, c, tl);
+    case WEEK: return launch_hist_p<WEEK>(ctx, x, y, t_ms, a, u, present, c, tl);
+    case MONTH: return launch_hist_p<MONTH>(ctx, x, y, t_ms, a, u, present, c, tl);
+    default: return launch_hist_p<YEAR>(ctx, x, y, t_ms, a, u, present, c, tl);
+  }
+}
+
+}  // extern "C"

@@ -382,6 +382,22 @@ int gm_key_range_scan(gm_ctx* ctx, const uint8_t* shard, const int16_t* bin, con
                       const gm_key_range* ranges, int64_t n_ranges, const uint8_t* filter_bytes, size_t filter_len,
                       const int64_t* perm, int64_t* ids, int64_t ids_cap, int64_t* n_match, int64_t* n_scanned);
 
+/* ------------------------------------------------------------------ statistics */
+/* Z3Histogram.observe / unobserve over a batch of point features (utils/stats/Z3Histogram.scala:101-128;
+   a point's safeCentroid is the point): toKey (:80-86) = BinnedTime(period) + Z3SFC(period).index,
+   lenient only for unobserve; a feature whose toKey throws is skipped (the Scala code logs a warning)
+   and counted in tally[0].  The bin is LongBinning(length, (minZ, maxZ)).directIndex
+   (utils/stats/BinnedArray.scala:185-201).  The histogram's binMap is the dense block
+   counts[(timeBin - bin_lo) * length + i] (int64) for time bins bin_lo .. bin_lo + n_bins - 1 with
+   present[timeBin - bin_lo] != 0 marking the bins binMap holds (observe sets it: getOrElseUpdate;
+   unobserve only touches present bins: binMap.get(..).foreach).  Features whose time bin lies outside
+   the window are counted in tally[1] and not added, so a caller can widen the window and re-run them.
+   counts, present and tally (int64[2]) are device arrays and are accumulated into, never cleared; the
+   call is asynchronous on the context stream. */
+int gm_z3_histogram(gm_ctx* ctx, const double* x, const double* y, const int64_t* t_ms, int64_t n, int period,
+                    int length, int unobserve, int bin_lo, int n_bins, uint8_t* present, int64_t* counts,
+                    int64_t* tally);
+
 /* ------------------------------------------------------------------ synthetic data (bench/tests) */
 /* SplitMix64 keyed by (seed, index): lon U[lon0,lon1), lat U[lat0,lat1), t_ms U[t0,t1) */
 int gm_gen_points(gm_ctx* ctx, uint64_t seed, int64_t n, int64_t index_base, double lon0, double lon1,

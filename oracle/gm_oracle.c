@@ -453,6 +453,41 @@ void gmo_z3_index_key_batch(int period, const double* x, const double* y, const 
   }
 }
 
+/* LongBinning.directIndex (utils/stats/BinnedArray.scala:185-201): binSize = (max - min).toDouble / length,
+   i = floor((value - min) / binSize).toInt; the upper bound maps to length - 1. */
+int gmo_long_binning_index(int64_t min, int64_t max, int length, int64_t v) {
+  if (v < min || v > max) return -1;
+  double bs = (double)(int64_t)((uint64_t)max - (uint64_t)min) / (double)length;
+  double q = floor((double)(int64_t)((uint64_t)v - (uint64_t)min) / bs);
+  int i = q != q ? 0 : (q >= 2147483647.0 ? 2147483647 : (q <= -2147483648.0 ? (-2147483647 - 1) : (int)q));
+  if (i < 0 || i > length) return -1;
+  return i == length ? length - 1 : i;
+}
+
+/* Z3Histogram.observe / unobserve (utils/stats/Z3Histogram.scala:101-128) over point features, one
+   feature at a time in input order.  toKey (:80-86): BinnedTime then Z3SFC(period).index(x, y, offset,
+   lenient) with lenient only for unobserve; a throwing toKey skips the feature (tally[0]).  minZ / maxZ
+   (:53-54) are the z of (-180, -90, time.min) and (180, 90, time.max).  counts is binMap as a dense
+   [n_bins][length] block for time bins bin_lo.., present[] its key set; other bins go to tally[1]. */
+void gmo_z3_histogram(int period, const double* x, const double* y, const int64_t* t_ms, int64_t n, int length,
+                      int unobserve, int bin_lo, int n_bins, uint8_t* present, int64_t* counts, int64_t* tally) {
+  int64_t zmin = 0, zmax = 0;
+  gmo_z3_index(period, 21, -180.0, -90.0, 0, 0, &zmin);
+  gmo_z3_index(period, 21, 180.0, 90.0, gmo_max_offset(period), 0, &zmax);
+  for (int64_t i = 0; i < n; i++) {
+    int16_t b; int64_t off, z = 0;
+    int st = gmo_binned_time(period, t_ms[i], &b, &off);
+    if (st == GMO_OK) st = gmo_z3_index(period, 21, x[i], y[i], off, unobserve, &z);
+    if (st != GMO_OK) { tally[0]++; continue; }
+    int rb = (int)b - bin_lo;
+    if (rb < 0 || rb >= n_bins) { tally[1]++; continue; }
+    if (unobserve && !present[rb]) continue;
+    if (!unobserve) present[rb] = 1;
+    int k = gmo_long_binning_index(zmin, zmax, length, z);
+    if (k >= 0) counts[(int64_t)rb * length + k] += unobserve ? -1 : 1;
+  }
+}
+
 void gmo_z2_index_batch(const double* x, const double* y, int64_t n, int lenient, int64_t* z, uint8_t* status) {
   for (int64_t i = 0; i < n; i++) {
     int64_t zz; int st = gmo_z2_index(31, x[i], y[i], lenient, &zz);

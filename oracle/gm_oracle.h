@@ -74,6 +74,10 @@ void    gmo_z2_invert(int precision, int64_t z, double* x, double* y);
 /* Z3IndexKeySpace.toIndexKey (bin + z), batch */
 void    gmo_z3_index_key_batch(int period, const double* x, const double* y, const int64_t* t_ms, int64_t n,
                                int lenient, int16_t* bin, int64_t* z, uint8_t* status);
+/* Z3Histogram observe / unobserve (batch) and LongBinning.directIndex */
+int     gmo_long_binning_index(int64_t min, int64_t max, int length, int64_t v);
+void    gmo_z3_histogram(int period, const double* x, const double* y, const int64_t* t_ms, int64_t n, int length,
+                         int unobserve, int bin_lo, int n_bins, uint8_t* present, int64_t* counts, int64_t* tally);
 void    gmo_z2_index_batch(const double* x, const double* y, int64_t n, int lenient, int64_t* z, uint8_t* status);
 void    gmo_z3_invert_batch(int period, const int64_t* z, int64_t n, double* x, double* y, int64_t* t);
 void    gmo_z2_invert_batch(const int64_t* z, int64_t n, double* x, double* y);

@@ -64,6 +64,9 @@ def lib():
             "gmo_z2_index": (ctypes.c_int, [ctypes.c_int, d, d, ctypes.c_int, vp]),
             "gmo_z2_invert": (None, [ctypes.c_int, i64, vp, vp]),
             "gmo_z3_index_key_batch": (None, [ctypes.c_int, vp, vp, vp, i64, ctypes.c_int, vp, vp, vp]),
+            "gmo_long_binning_index": (ctypes.c_int, [i64, i64, ctypes.c_int, i64]),
+            "gmo_z3_histogram": (None, [ctypes.c_int, vp, vp, vp, i64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                        ctypes.c_int, vp, vp, vp]),
             "gmo_z2_index_batch": (None, [vp, vp, i64, ctypes.c_int, vp, vp]),
             "gmo_z3_invert_batch": (None, [ctypes.c_int, vp, i64, vp, vp, vp]),
             "gmo_z2_invert_batch": (None, [vp, i64, vp, vp]),
@@ -216,6 +219,24 @@ def z3_index_key_batch(x, y, t_ms, lenient=False, period=WEEK):
     b = np.empty(n, np.int16); z = np.empty(n, np.int64); st = np.empty(n, np.uint8)
     lib().gmo_z3_index_key_batch(period, _p(x), _p(y), _p(t), n, int(lenient), _p(b), _p(z), _p(st))
     return b, z, st
+
+
+def z3_histogram(x, y, t_ms, length, bin_lo, n_bins, unobserve=False, period=WEEK, present=None, counts=None,
+                 tally=None):
+    """Z3Histogram observe / unobserve (utils/stats/Z3Histogram.scala:101-128); returns (present, counts
+    [n_bins, length], tally [skipped, outside window]), accumulating into the arrays passed in."""
+    x = np.ascontiguousarray(x, np.float64); y = np.ascontiguousarray(y, np.float64)
+    t = np.ascontiguousarray(t_ms, np.int64)
+    present = np.zeros(n_bins, np.uint8) if present is None else present
+    counts = np.zeros((n_bins, length), np.int64) if counts is None else counts
+    tally = np.zeros(2, np.int64) if tally is None else tally
+    lib().gmo_z3_histogram(period, _p(x), _p(y), _p(t), len(x), length, int(unobserve), bin_lo, n_bins,
+                           _p(present), _p(counts), _p(tally))
+    return present, counts, tally
+
+
+def long_binning_index(lo, hi, length, v):
+    return lib().gmo_long_binning_index(lo, hi, length, v)
 
 
 def z2_index_batch(x, y, lenient=False):

@@ -1,0 +1,130 @@
+"""GPU parity of gm_z3_histogram (Z3Histogram observe / unobserve) against the C oracle; bit-exact counts."""
+import datetime
+
+import numpy as np
+import pytest
+
+from test_gpu_parity import T2020, T2021, edge_points, random_points
+
+pytestmark = pytest.mark.gpu
+WEEK = 1
+
+
+def _dev(a, torch):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def run_hist(x, y, t, period, length, lo, nb, unobserve=False, present=None, counts=None):
+    import torch
+    from geomesa_amd import _lib
+    ctx = _lib.context()
+    X, Y, T = _dev(x, torch), _dev(y, torch), _dev(t, torch)
+    P = _dev(present if present is not None else np.zeros(nb, np.uint8), torch)
+    C = _dev(counts if counts is not None else np.zeros((nb, length), np.int64), torch)
+    tally = torch.zeros(2, dtype=torch.int64, device="cuda")
+    _lib.check(ctx.lib.gm_z3_histogram(ctx.handle, _lib.ptr(X), _lib.ptr(Y), _lib.ptr(T), len(x), period, length,
+                                       int(unobserve), lo, nb, _lib.ptr(P), _lib.ptr(C), _lib.ptr(tally)),
+               "gm_z3_histogram")
+    torch.cuda.synchronize()
+    return P.cpu().numpy(), C.cpu().numpy(), tally.cpu().numpy()
+
+
+def inputs(n):
+    x, y, t = random_points(n)
+    ex, ey, et = edge_points()
+    return np.concatenate([x, ex]), np.concatenate([y, ey]), np.concatenate([t, et])
+
+
+# LDS-private path (n_bins * length + n_bins <= 32768) and the global-atomic path
+@pytest.mark.parametrize("period,length,lo,nb", [
+    (WEEK, 512, 2600, 53), (WEEK, 1024, 2600, 53), (WEEK, 4096, 2600, 53), (WEEK, 64, 2590, 70), (0, 128, 18260, 200),
+    (2, 1000, 595, 14), (3, 10000, 48, 4), (WEEK, 1, 0, 1)])
+def test_z3_histogram_parity(gpu, oracle, period, length, lo, nb):
+    x, y, t = inputs(300_001)
+    P, C, tl = run_hist(x, y, t, period, length, lo, nb)
+    op, oc, ot = oracle.z3_histogram(x, y, t, length, lo, nb, period=period)
+    assert np.array_equal(tl, ot)
+    assert np.array_equal(P, op)
+    assert np.array_equal(C, oc)
+    # unobserve half the features on top (lenient toKey, present bins only), accumulating
+    h = len(x) // 2
+    P2, C2, tl2 = run_hist(x[:h], y[:h], t[:h], period, length, lo, nb, True, P, C)
+    oracle.z3_histogram(x[:h], y[:h], t[:h], length, lo, nb, unobserve=True, period=period, present=op, counts=oc,
+                        tally=ot)
+    assert np.array_equal(C2, oc)
+    assert np.array_equal(P2, op)
+
+
+def test_z3_histogram_unaligned_and_small(gpu, oracle):
+    import torch
+    from geomesa_amd import _lib
+    x, y, t = inputs(10_001)
+    for off, n in [(1, 5001), (3, 1), (0, 2), (1, 0)]:
+        xs, ys, ts = x[off:off + n], y[off:off + n], t[off:off + n]
+        X = _dev(x, torch)[off:off + n]; Y = _dev(y, torch)[off:off + n]; T = _dev(t, torch)[off:off + n]
+        P = torch.zeros(53, dtype=torch.uint8, device="cuda")
+        C = torch.zeros((53, 256), dtype=torch.int64, device="cuda")
+        tl = torch.zeros(2, dtype=torch.int64, device="cuda")
+        ctx = _lib.context()
+        _lib.check(ctx.lib.gm_z3_histogram(ctx.handle, _lib.ptr(X), _lib.ptr(Y), _lib.ptr(T), n, WEEK, 256, 0, 2600,
+                                           53, _lib.ptr(P), _lib.ptr(C), _lib.ptr(tl)), "gm_z3_histogram")
+        op, oc, ot = oracle.z3_histogram(xs, ys, ts, 256, 2600, 53)
+        assert np.array_equal(C.cpu().numpy(), oc) and np.array_equal(tl.cpu().numpy(), ot)
+        assert np.array_equal(P.cpu().numpy(), op)
+
+
+def test_z3_histogram_rejects_bad_args(gpu):
+    import torch
+    from geomesa_amd import _lib
+    ctx = _lib.context()
+    z = torch.zeros(4, dtype=torch.int64, device="cuda")
+    for period, length, lo, nb in [(7, 16, 0, 1), (1, 0, 0, 1), (1, 16, 0, 0), (1, 16, 32767, 2), (1, 16, -32769, 1)]:
+        rc = ctx.lib.gm_z3_histogram(ctx.handle, _lib.ptr(z), _lib.ptr(z), _lib.ptr(z), 1, period, length, 0, lo, nb,
+                                     _lib.ptr(z), _lib.ptr(z), _lib.ptr(z))
+        assert rc == _lib.GM_E_INVALID
+
+
+def ms(s):
+    return int(datetime.datetime.fromisoformat(s + "+00:00").timestamp() * 1000)
+
+
+def test_z3histogram_reference_kat(gpu):  # Z3HistogramTest.scala:44-51, 108-118 through the host mirror
+    from geomesa_amd.stats import Z3Histogram
+    i = np.arange(100)
+    x = -i.astype(np.float64); y = (i // 2).astype(np.float64)
+    t = np.array([ms("2012-01-01T%02d:00:00" % (k % 24)) for k in i], np.int64)
+    h = Z3Histogram("geom", "dtg", "week", 1024)
+    assert h.is_empty()
+    h.observe(x, y, t)
+    assert not h.is_empty()
+    for k in range(100):
+        w, idx = h.index_of(x[k], y[k], int(t[k]))
+        assert 1 <= h.count(w, idx) <= 21
+    # serialize-style equivalence: toJson of a + b equals the counts doubled
+    h2 = h + h
+    (label, body), = h2.to_json_object()[0].items()
+    assert label.startswith("week-") and sum(body["bins"]) == 200
+    h.clear()
+    assert h.is_empty()
+    for k in range(100):
+        w, idx = h.index_of(x[k], y[k], int(t[k]))
+        assert h.count(w, idx) == 0
+
+
+def test_z3histogram_window_grows(gpu, oracle):
+    from geomesa_amd.stats import Z3Histogram
+    x, y, t = random_points(50_000)
+    wk = 604800000
+    h = Z3Histogram(period="week", length=256)
+    h.observe(x[:25_000], y[:25_000], t[:25_000])
+    t2 = t[25_000:] + 30 * wk            # later weeks: the window must widen
+    h.observe(x[25_000:], y[25_000:], t2)
+    tt = np.concatenate([t[:25_000], t2])
+    lo, nb = h.bin_lo, h.n_bins
+    op, oc, ot = oracle.z3_histogram(x, y, tt, 256, lo, nb)
+    assert ot.tolist() == [0, 0]
+    assert np.array_equal(h.counts.cpu().numpy(), oc)
+    assert np.array_equal(h.present.cpu().numpy(), op)
+    parts = h.split_by_time()
+    assert sum(int(p.counts.sum()) for _, p in parts) == 50_000
+    assert T2020 < T2021

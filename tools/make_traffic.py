@@ -24,6 +24,7 @@ STREAMING = {
     "z2_invert": ("k_z2_invert<", "points", 24.0),
     "z3filter_scan": ("k_z3filter_mask_v", "points", 10.125),
     "xz2_index": ("k_xz2_index_v", "xz", 40.0),
+    "z3_histogram": ("k_z3_hist_lds<", "points", 24.0),
 }
 # join step kernels and the points per dispatch: direct = one pass per 2^31 points, partitioned =
 # hist + scan + scatter + join per 2^28-point chunk
