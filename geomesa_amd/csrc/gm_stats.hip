@@ -14,6 +14,8 @@
 // histogram larger than one LDS block takes up to HIST_MAX_PASSES passes over the points, one per
 // row block; beyond that it adds straight into the 64-bit device counters (scattered per-lane
 // device atomics run ~22 G/s on MI355X, so they only win over many passes).
+#include <cmath>
+
 #include "gm_keys.hpp"
 
 namespace gm {
@@ -27,6 +29,7 @@ struct HistArgs {
   int length, bin_lo, n_bins;
   int64_t zmin, zmax;
   double bsize;  // LongBinning.binSize = (max - min).toDouble / length
+  double inv_bsize;  // 1 / bsize when bsize is a power of two (x / 2^k == x * 2^-k exactly), else 0
   NDim lon, lat, tim;
   int row_lo, row_n;  // LDS pass: the time-bin rows [row_lo, row_lo + row_n) of the window it counts
   int tally;          // this launch reports skipped / outside features (the first pass only)
@@ -35,7 +38,8 @@ struct HistArgs {
 // LongBinning.directIndex (BinnedArray.scala:195-201); (value - min) is a Long, divided by a Double
 __device__ __forceinline__ int long_bin_index(int64_t v, const HistArgs& a) {
   if (v < a.zmin || v > a.zmax) return -1;
-  const double q = floor((double)(int64_t)((uint64_t)v - (uint64_t)a.zmin) / a.bsize);
+  const double d = (double)(int64_t)((uint64_t)v - (uint64_t)a.zmin);
+  const double q = floor(a.inv_bsize != 0.0 ? d * a.inv_bsize : d / a.bsize);
   const int i = q >= 2147483647.0 ? 2147483647 : (q <= -2147483648.0 ? (-2147483647 - 1) : (int)q);
   if (i < 0 || i > a.length) return -1;
   return i == a.length ? a.length - 1 : i;
@@ -255,6 +259,10 @@ int gm_z3_histogram(gm_ctx* ctx, const double* x, const double* y, const int64_t
   a.zmin = 0;
   a.zmax = INT64_MAX;
   a.bsize = (double)(int64_t)((uint64_t)a.zmax - (uint64_t)a.zmin) / (double)length;
+  {
+    int e;
+    a.inv_bsize = (std::frexp(a.bsize, &e) == 0.5 && e > -1000) ? std::ldexp(1.0, 1 - e) : 0.0;
+  }
   unsigned long long* c = (unsigned long long*)counts;
   unsigned long long* tl = (unsigned long long*)tally;
   const bool u = unobserve != 0;
