@@ -115,6 +115,10 @@ SIGNATURES = {
     "gm_pip_join_arrow": (cint, [vp, vp, vp, i64, i64, vp, vp, i64, vp, cint, cint]),
     "gm_pip_index_create_arrow": (cint, [vp, vp, i32, cint, vp]),
     "gm_pip_relate": (cint, [vp, vp, vp, vp, vp, i64, vp]),
+    "gm_legacy_z3_index": (cint, [vp, vp, vp, vp, i64, cint, cint, cint, vp, vp, vp]),
+    "gm_legacy_z3_invert": (cint, [vp, vp, i64, cint, cint, vp, vp, vp]),
+    "gm_legacy_z2_index": (cint, [vp, vp, vp, i64, cint, vp, vp, vp]),
+    "gm_legacy_z2_invert": (cint, [vp, vp, i64, vp, vp]),
     "gm_z3_histogram": (cint, [vp, vp, vp, vp, i64, cint, cint, cint, cint, cint, vp, vp, vp]),
     "gm_gen_points": (cint, [vp, ctypes.c_uint64, i64, i64, d, d, d, d, i64, i64, vp, vp, vp]),
 }

@@ -345,3 +345,75 @@ class XZ3SFC:
     def ranges_batch(self, queries, max_ranges=None):
         from . import ranges as R
         return R.xz3_ranges(self, queries, max_ranges)
+
+
+class _LegacyBase:
+    @staticmethod
+    def _run_index(fn, cols, n, extra, lenient, status, what):
+        torch = _torch()
+        ctx = _lib.context()
+        z = torch.empty(n, dtype=torch.int64, device=cols[0].device)
+        s = torch.empty(n, dtype=torch.uint8, device=cols[0].device) if status else None
+        st = _summary()
+        check(getattr(ctx.lib, fn)(ctx.handle, *[ptr(c) for c in cols], n, *extra, int(bool(lenient)), ptr(z), ptr(s),
+                                   ctypes.byref(st)), fn)
+        if status:
+            return z, s
+        _raise_first(st, what)
+        return z
+
+
+class LegacyZ3SFC(_LegacyBase):
+    """LegacyZ3SFC(period) (curve/LegacyZ3SFC.scala:18-49): semi-normalized dimensions, kept for old data."""
+    LEGACY_Z3, LEGACY_YEAR_Z3 = 0, 1
+
+    def __init__(self, period=TimePeriod.Week):
+        self.period = TimePeriod.of(period)
+        self.curve = self.LEGACY_Z3
+
+    def index(self, x, y, t, lenient=False, status=False):
+        torch = _torch()
+        cols = [_dev_col(x, torch.float64), _dev_col(y, torch.float64), _dev_col(t, torch.int64)]
+        return self._run_index("gm_legacy_z3_index", cols, cols[0].numel(), (self.curve, self.period), lenient,
+                               status, type(self).__name__ + ".index")
+
+    def invert(self, z):
+        torch = _torch()
+        if self.curve != self.LEGACY_Z3:
+            raise IllegalArgumentException("invert is only defined here for LegacyZ3SFC")
+        z = _dev_col(z, torch.int64)
+        n = z.numel()
+        ctx = _lib.context()
+        x = torch.empty(n, dtype=torch.float64, device=z.device)
+        y = torch.empty(n, dtype=torch.float64, device=z.device)
+        t = torch.empty(n, dtype=torch.int64, device=z.device)
+        check(ctx.lib.gm_legacy_z3_invert(ctx.handle, ptr(z), n, self.curve, self.period, ptr(x), ptr(y), ptr(t)),
+              "gm_legacy_z3_invert")
+        return x, y, t
+
+
+class LegacyYearZ3SFC(LegacyZ3SFC):
+    """LegacyYearZ3SFC (curve/LegacyYearZ3SFC.scala:17-46): 21-bit curve, legacy 52-week time max."""
+
+    def __init__(self):
+        super().__init__(TimePeriod.Year)
+        self.curve = self.LEGACY_YEAR_Z3
+
+
+class LegacyZ2SFC(_LegacyBase):
+    """LegacyZ2SFC (curve/LegacyZ2SFC.scala:14-26)."""
+
+    def index(self, x, y, lenient=False, status=False):
+        torch = _torch()
+        cols = [_dev_col(x, torch.float64), _dev_col(y, torch.float64)]
+        return self._run_index("gm_legacy_z2_index", cols, cols[0].numel(), (), lenient, status, "LegacyZ2SFC.index")
+
+    def invert(self, z):
+        torch = _torch()
+        z = _dev_col(z, torch.int64)
+        n = z.numel()
+        ctx = _lib.context()
+        x = torch.empty(n, dtype=torch.float64, device=z.device)
+        y = torch.empty(n, dtype=torch.float64, device=z.device)
+        check(ctx.lib.gm_legacy_z2_invert(ctx.handle, ptr(z), n, ptr(x), ptr(y)), "gm_legacy_z2_invert")
+        return x, y

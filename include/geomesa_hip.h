@@ -382,6 +382,23 @@ int gm_key_range_scan(gm_ctx* ctx, const uint8_t* shard, const int16_t* bin, con
                       const gm_key_range* ranges, int64_t n_ranges, const uint8_t* filter_bytes, size_t filter_len,
                       const int64_t* perm, int64_t* ids, int64_t ids_cap, int64_t* n_match, int64_t* n_scanned);
 
+/* ------------------------------------------------------------------ legacy curves (reading / deleting old data) */
+/* LegacyZ3SFC(period) (z3/curve/LegacyZ3SFC.scala:18-49): SemiNormalizedDimension lon/lat (2^21-1) and
+   time (2^20-1) (NormalizedDimension.scala:83-97), ceil-based normalize, lenientIndex clamped from
+   below only; LegacyYearZ3SFC (LegacyYearZ3SFC.scala:17-46): the 21-bit curve with the 52-week time
+   max, offsets in (52 weeks, maxOffset(Year)] indexed as the max.  Device arrays, as gm_z3_index. */
+#define GM_LEGACY_Z3 0
+#define GM_LEGACY_YEAR_Z3 1
+int gm_legacy_z3_index(gm_ctx* ctx, const double* x, const double* y, const int64_t* t, int64_t n, int curve,
+                       int period, int lenient, int64_t* z, uint8_t* status, gm_batch_status* summary);
+/* LegacyZ3SFC.invert = Z3SFC.invert with SemiNormalizedDimension.denormalize (curve GM_LEGACY_Z3 only) */
+int gm_legacy_z3_invert(gm_ctx* ctx, const int64_t* z, int64_t n, int curve, int period, double* x, double* y,
+                        int64_t* t);
+/* LegacyZ2SFC (z3/curve/LegacyZ2SFC.scala:14-26): 2^31-1 semi-normalized lon/lat */
+int gm_legacy_z2_index(gm_ctx* ctx, const double* x, const double* y, int64_t n, int lenient, int64_t* z,
+                       uint8_t* status, gm_batch_status* summary);
+int gm_legacy_z2_invert(gm_ctx* ctx, const int64_t* z, int64_t n, double* x, double* y);
+
 /* ------------------------------------------------------------------ statistics */
 /* Z3Histogram.observe / unobserve over a batch of point features (utils/stats/Z3Histogram.scala:101-128;
    a point's safeCentroid is the point): toKey (:80-86) = BinnedTime(period) + Z3SFC(period).index,

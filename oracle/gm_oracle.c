@@ -453,6 +453,70 @@ void gmo_z3_index_key_batch(int period, const double* x, const double* y, const 
   }
 }
 
+/* ---- legacy curves: LegacyZ3SFC (curve/LegacyZ3SFC.scala:18-49), LegacyZ2SFC (LegacyZ2SFC.scala:14-26),
+   LegacyYearZ3SFC (LegacyYearZ3SFC.scala:17-46); SemiNormalizedDimension (NormalizedDimension.scala:83-87) */
+static int32_t semi_norm(double mn, double mx, double prec, double x) { return gmo_d2i(ceil((x - mn) / (mx - mn) * prec)); }
+static int32_t semi_len(double mn, double mx, double prec, double x) {
+  double c = ceil((x - mn) / (mx - mn) * prec);
+  double m = (c != c) ? c : (mn >= c ? mn : c);            /* java.lang.Math.max: NaN wins */
+  return gmo_d2i(m);
+}
+static double semi_denorm(double mn, double mx, double prec, int32_t i) {
+  return i == 0 ? mn : ((double)i - 0.5) * (mx - mn) / prec + mn;
+}
+#define LZ_P21 2097151.0
+#define LZ_P20 1048575.0
+#define LZ_P31 2147483647.0
+
+int gmo_legacy_z3_index(int period, double x, double y, int64_t t, int lenient, int64_t* z) {
+  double tmax = (double)gmo_max_offset(period), td = (double)t;
+  if (x >= -180.0 && x <= 180.0 && y >= -90.0 && y <= 90.0 && td >= 0.0 && td <= tmax) {
+    *z = gmo_z3_apply(semi_norm(-180, 180, LZ_P21, x), semi_norm(-90, 90, LZ_P21, y), semi_norm(0, tmax, LZ_P20, td));
+    return GMO_OK;
+  }
+  if (!lenient) { *z = 0; return GMO_OUT_OF_BOUNDS; }
+  *z = gmo_z3_apply(semi_len(-180, 180, LZ_P21, x), semi_len(-90, 90, LZ_P21, y), semi_len(0, tmax, LZ_P20, td));
+  return GMO_OK;
+}
+
+void gmo_legacy_z3_invert(int period, int64_t z, double* x, double* y, int64_t* t) {
+  double tmax = (double)gmo_max_offset(period);
+  *x = semi_denorm(-180, 180, LZ_P21, gmo_z3_combine(z));
+  *y = semi_denorm(-90, 90, LZ_P21, gmo_z3_combine(jshr(z, 1)));
+  *t = gmo_d2l(semi_denorm(0, tmax, LZ_P20, gmo_z3_combine(jshr(z, 2))));
+}
+
+int gmo_legacy_z2_index(double x, double y, int lenient, int64_t* z) {
+  if (x >= -180.0 && x <= 180.0 && y >= -90.0 && y <= 90.0) {
+    *z = gmo_z2_apply(semi_norm(-180, 180, LZ_P31, x), semi_norm(-90, 90, LZ_P31, y));
+    return GMO_OK;
+  }
+  if (!lenient) { *z = 0; return GMO_OUT_OF_BOUNDS; }
+  *z = gmo_z2_apply(semi_len(-180, 180, LZ_P31, x), semi_len(-90, 90, LZ_P31, y));
+  return GMO_OK;
+}
+
+void gmo_legacy_z2_invert(int64_t z, double* x, double* y) {
+  *x = semi_denorm(-180, 180, LZ_P31, gmo_z2_combine(z));
+  *y = semi_denorm(-90, 90, LZ_P31, gmo_z2_combine(jshr(z, 1)));
+}
+
+/* LegacyYearZ3SFC.index: Z3SFC.index over (lon 21, lat 21, NormalizedTime(21, 52 weeks in minutes)) */
+int gmo_legacy_year_z3_index(double x, double y, int64_t t, int lenient, int64_t* z) {
+  const double tmax = 7.0 * 24 * 60 * 52;
+  if ((double)t > tmax && t <= gmo_max_offset(3)) t = (int64_t)tmax;
+  double td = (double)t;
+  if (!(x >= -180.0 && x <= 180.0 && y >= -90.0 && y <= 90.0 && td >= 0.0 && td <= tmax)) {
+    if (!lenient) { *z = 0; return GMO_OUT_OF_BOUNDS; }
+    x = x < -180.0 ? -180.0 : (x > 180.0 ? 180.0 : x);
+    y = y < -90.0 ? -90.0 : (y > 90.0 ? 90.0 : y);
+    td = td < 0.0 ? 0.0 : (td > tmax ? tmax : td);
+  }
+  *z = gmo_z3_apply(gmo_normalize(-180.0, 180.0, 21, x), gmo_normalize(-90.0, 90.0, 21, y),
+                    gmo_normalize(0.0, tmax, 21, td));
+  return GMO_OK;
+}
+
 /* LongBinning.directIndex (utils/stats/BinnedArray.scala:185-201): binSize = (max - min).toDouble / length,
    i = floor((value - min) / binSize).toInt; the upper bound maps to length - 1. */
 int gmo_long_binning_index(int64_t min, int64_t max, int length, int64_t v) {

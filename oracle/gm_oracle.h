@@ -74,6 +74,12 @@ void    gmo_z2_invert(int precision, int64_t z, double* x, double* y);
 /* Z3IndexKeySpace.toIndexKey (bin + z), batch */
 void    gmo_z3_index_key_batch(int period, const double* x, const double* y, const int64_t* t_ms, int64_t n,
                                int lenient, int16_t* bin, int64_t* z, uint8_t* status);
+/* legacy curves (LegacyZ3SFC / LegacyZ2SFC / LegacyYearZ3SFC) */
+int     gmo_legacy_z3_index(int period, double x, double y, int64_t t, int lenient, int64_t* z);
+void    gmo_legacy_z3_invert(int period, int64_t z, double* x, double* y, int64_t* t);
+int     gmo_legacy_z2_index(double x, double y, int lenient, int64_t* z);
+void    gmo_legacy_z2_invert(int64_t z, double* x, double* y);
+int     gmo_legacy_year_z3_index(double x, double y, int64_t t, int lenient, int64_t* z);
 /* Z3Histogram observe / unobserve (batch) and LongBinning.directIndex */
 int     gmo_long_binning_index(int64_t min, int64_t max, int length, int64_t v);
 void    gmo_z3_histogram(int period, const double* x, const double* y, const int64_t* t_ms, int64_t n, int length,

@@ -64,6 +64,11 @@ def lib():
             "gmo_z2_index": (ctypes.c_int, [ctypes.c_int, d, d, ctypes.c_int, vp]),
             "gmo_z2_invert": (None, [ctypes.c_int, i64, vp, vp]),
             "gmo_z3_index_key_batch": (None, [ctypes.c_int, vp, vp, vp, i64, ctypes.c_int, vp, vp, vp]),
+            "gmo_legacy_z3_index": (ctypes.c_int, [ctypes.c_int, d, d, i64, ctypes.c_int, vp]),
+            "gmo_legacy_z3_invert": (None, [ctypes.c_int, i64, vp, vp, vp]),
+            "gmo_legacy_z2_index": (ctypes.c_int, [d, d, ctypes.c_int, vp]),
+            "gmo_legacy_z2_invert": (None, [i64, vp, vp]),
+            "gmo_legacy_year_z3_index": (ctypes.c_int, [d, d, i64, ctypes.c_int, vp]),
             "gmo_long_binning_index": (ctypes.c_int, [i64, i64, ctypes.c_int, i64]),
             "gmo_z3_histogram": (None, [ctypes.c_int, vp, vp, vp, i64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                         ctypes.c_int, vp, vp, vp]),
@@ -233,6 +238,33 @@ def z3_histogram(x, y, t_ms, length, bin_lo, n_bins, unobserve=False, period=WEE
     lib().gmo_z3_histogram(period, _p(x), _p(y), _p(t), len(x), length, int(unobserve), bin_lo, n_bins,
                            _p(present), _p(counts), _p(tally))
     return present, counts, tally
+
+
+def legacy_z3_index(x, y, t, lenient=False, period=WEEK):
+    z = ctypes.c_int64()
+    return lib().gmo_legacy_z3_index(period, x, y, t, int(lenient), ctypes.byref(z)), z.value
+
+
+def legacy_year_z3_index(x, y, t, lenient=False):
+    z = ctypes.c_int64()
+    return lib().gmo_legacy_year_z3_index(x, y, t, int(lenient), ctypes.byref(z)), z.value
+
+
+def legacy_z3_invert(z, period=WEEK):
+    x, y, t = ctypes.c_double(), ctypes.c_double(), ctypes.c_int64()
+    lib().gmo_legacy_z3_invert(period, z, ctypes.byref(x), ctypes.byref(y), ctypes.byref(t))
+    return x.value, y.value, t.value
+
+
+def legacy_z2_index(x, y, lenient=False):
+    z = ctypes.c_int64()
+    return lib().gmo_legacy_z2_index(x, y, int(lenient), ctypes.byref(z)), z.value
+
+
+def legacy_z2_invert(z):
+    x, y = ctypes.c_double(), ctypes.c_double()
+    lib().gmo_legacy_z2_invert(z, ctypes.byref(x), ctypes.byref(y))
+    return x.value, y.value
 
 
 def long_binning_index(lo, hi, length, v):
