@@ -185,6 +185,14 @@ class Z3Histogram:
         out += other
         return out
 
+    def all_reduce(self, pg):
+        """Merge this rank's histogram with every other rank's (`+=` over the process group, RCCL)."""
+        from .shard import merge_histograms
+        c, p, lo = merge_histograms(pg, self.counts, self.present, self.bin_lo)
+        if c is not None:
+            self.counts, self.present, self.bin_lo, self.n_bins = c, p, lo, c.shape[0]
+        return self
+
     def split_by_time(self):
         out = []
         for b in self.time_bins():

@@ -97,3 +97,53 @@ def test_shard_bounds():
             assert max(h - l for l, h in b) - min(h - l for l, h in b) <= 1
     with pytest.raises(ValueError):
         shard_bounds(10, 2, 2)
+
+
+def _hist_worker(rank, world, port, q):
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import oracle as O
+        from geomesa_amd.shard import merge_histograms, shard_bounds
+        import torch
+        x, y, t = _hist_points()
+        lo, hi = shard_bounds(len(x), rank, world)
+        b, _, st = O.z3_index_key_batch(x[lo:hi], y[lo:hi], t[lo:hi])
+        blo, bhi = int(b[st == 0].min()), int(b[st == 0].max())   # each rank its own window
+        pres, counts, _ = O.z3_histogram(x[lo:hi], y[lo:hi], t[lo:hi], 64, blo, bhi - blo + 1)
+        c, p, mlo = merge_histograms(dist, torch.from_numpy(counts), torch.from_numpy(pres), blo)
+        if rank == 0:
+            q.put((c.numpy(), p.numpy(), mlo))
+    finally:
+        dist.destroy_process_group()
+
+
+def _hist_points():
+    rng = np.random.default_rng(5)
+    n = 40_001
+    x = rng.uniform(-180, 180, n); y = rng.uniform(-90, 90, n)
+    t = np.sort(rng.integers(1577836800000, 1609459200000, n))   # sorted: ranks see different weeks
+    x[7] = 200.0                                                  # one toKey failure
+    return x, y, t
+
+
+def test_sharded_histogram_merge_equals_global(oracle):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_hist_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    c, p, mlo = q.get(timeout=240)
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    x, y, t = _hist_points()
+    pres, counts, tally = oracle.z3_histogram(x, y, t, 64, mlo, c.shape[0])
+    assert tally.tolist() == [1, 0]
+    assert np.array_equal(c, counts) and np.array_equal(p, pres)
