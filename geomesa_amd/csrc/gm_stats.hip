@@ -62,6 +62,37 @@ __device__ __forceinline__ int hist_slot(double x, double y, int64_t ms, const H
   return i < 0 ? -1 : rb * a.length + i;
 }
 
+// Z3.split through an LDS table of the 11-bit spread (Z3.scala:73-80): two lookups per dimension
+// replace the 8-op magic-number spread of each half (the kernel is VALU-bound on the encode)
+__device__ __forceinline__ uint64_t z3_split_tab(int32_t value, const uint32_t* sp) {
+  const uint32_t v = (uint32_t)value & 0x1fffffu;
+  return ((uint64_t)sp[v >> 11] << 33) | (uint64_t)sp[v & 0x7ffu];
+}
+
+// hist_slot with the table spread; the bounds / lenient / normalize steps are z3_index_one's
+template <int PERIOD, bool UNOBS>
+__device__ __forceinline__ int hist_slot_tab(double x, double y, int64_t ms, const HistArgs& a, const uint32_t* sp,
+                                             int& rb, int& skip, int& out) {
+  int16_t b;
+  int64_t off;
+  if (binned_time<PERIOD>(ms, b, off) != ST_OK) { ++skip; return -1; }
+  double td = (double)off;
+  const bool inb = x >= a.lon.min && x <= a.lon.max && y >= a.lat.min && y <= a.lat.max && td >= a.tim.min &&
+                   td <= a.tim.max;
+  if (!inb) {
+    if (!UNOBS) { ++skip; return -1; }
+    x = x < a.lon.min ? a.lon.min : (x > a.lon.max ? a.lon.max : x);
+    y = y < a.lat.min ? a.lat.min : (y > a.lat.max ? a.lat.max : y);
+    td = td < a.tim.min ? a.tim.min : (td > a.tim.max ? a.tim.max : td);
+  }
+  const int64_t z = (int64_t)(z3_split_tab(normalize(a.lon, x), sp) | (z3_split_tab(normalize(a.lat, y), sp) << 1) |
+                              (z3_split_tab(normalize(a.tim, td), sp) << 2));
+  rb = (int)b - a.bin_lo;
+  if (rb < 0 || rb >= a.n_bins) { ++out; return -1; }
+  const int i = long_bin_index(z, a);
+  return i < 0 ? -1 : rb * a.length + i;
+}
+
 template <int PERIOD, bool UNOBS, bool VEC>
 __global__ __launch_bounds__(HTPB) void k_z3_hist_lds(const double* __restrict__ x, const double* __restrict__ y,
                                                       const int64_t* __restrict__ t, HistArgs a,
@@ -71,18 +102,20 @@ __global__ __launch_bounds__(HTPB) void k_z3_hist_lds(const double* __restrict__
   extern __shared__ int lds[];
   int* cnt = lds;                          // [row_n * length]
   int* pres = lds + a.row_n * a.length;    // [row_n]: bin present (observe sets, unobserve reads)
+  uint32_t* sp = (uint32_t*)(pres + a.row_n);  // [2048]: spread3_11 table
   __shared__ int s_skip, s_out;
   const int total = a.row_n * a.length;
   counts += (int64_t)a.row_lo * a.length;
   present += a.row_lo;
   for (int i = threadIdx.x; i < total; i += HTPB) cnt[i] = 0;
   for (int i = threadIdx.x; i < a.row_n; i += HTPB) pres[i] = UNOBS ? (int)present[i] : 0;
+  for (int i = threadIdx.x; i < 2048; i += HTPB) sp[i] = spread3_11((uint32_t)i);
   if (threadIdx.x == 0) { s_skip = 0; s_out = 0; }
   __syncthreads();
   int skip = 0, out = 0;
   auto one = [&](double xx, double yy, int64_t tt) {
     int rb = 0;
-    int c = hist_slot<PERIOD, UNOBS>(xx, yy, tt, a, rb, skip, out);
+    int c = hist_slot_tab<PERIOD, UNOBS>(xx, yy, tt, a, sp, rb, skip, out);
     rb -= a.row_lo;
     if (c < 0 || rb < 0 || rb >= a.row_n) return;
     c -= a.row_lo * a.length;
@@ -193,8 +226,8 @@ int launch_hist(gm_ctx* ctx, const double* x, const double* y, const int64_t* t,
       a.row_lo = k * rows;
       a.row_n = std::min(rows, a.n_bins - a.row_lo);
       a.tally = k == 0;
-      const size_t lds = (size_t)(a.row_n * a.length + a.row_n) * sizeof(int);
-      const int per_cu = lds <= 40 * 1024 ? 2 : 1;  // 2 x 1024 threads is the CU's wave limit
+      const size_t lds = (size_t)(a.row_n * a.length + a.row_n + 2048) * sizeof(int);
+      const int per_cu = lds <= 72 * 1024 ? 2 : 1;  // 2 x 1024 threads is the CU's wave limit
       // per workgroup <= 2^31 increments so the int32 LDS counters cannot wrap
       const int64_t need = (a.n + (int64_t)2147483647 - 1) / (int64_t)2147483647;
       const int64_t want = (a.n + HTPB - 1) / HTPB;
