@@ -21,6 +21,9 @@ __global__ __launch_bounds__(TPB) void k_z3_index_key(const dv2* __restrict__ x,
                                                       short2* __restrict__ bin, lv2* __restrict__ z,
                                                       uchar2* __restrict__ status, NDim lon, NDim lat, NDim tim,
                                                       int64_t* __restrict__ err) {
+#ifdef GM_KEY_TABLE
+  __shared__ uint32_t sp[2048];
+#endif
   const int64_t npairs = n >> 1;
   const int64_t base = (int64_t)blockIdx.x * (TPB * UNROLL) + threadIdx.x;
   dv2 xv[UNROLL], yv[UNROLL];
@@ -34,14 +37,23 @@ __global__ __launch_bounds__(TPB) void k_z3_index_key(const dv2* __restrict__ x,
       tv[u] = ld_stream(&t[p]);
     }
   }
+#ifdef GM_KEY_TABLE
+  fill_spread_table(sp, threadIdx.x, TPB);  // while the loads are in flight
+  __syncthreads();
+#endif
 #pragma unroll
   for (int u = 0; u < UNROLL; ++u) {
     const int64_t p = base + (int64_t)u * TPB;
     if (p < npairs) {
       int16_t b0, b1;
       int64_t z0, z1;
+#ifndef GM_KEY_TABLE  // default: magic-number spreads in registers (A/B with the LDS table: within noise, tools/key_ab.sh)
       uint8_t s0 = z3_key_one<PERIOD, LENIENT>(xv[u].x, yv[u].x, tv[u].x, lon, lat, tim, b0, z0);
       uint8_t s1 = z3_key_one<PERIOD, LENIENT>(xv[u].y, yv[u].y, tv[u].y, lon, lat, tim, b1, z1);
+#else
+      uint8_t s0 = z3_key_one_tab<PERIOD, LENIENT>(xv[u].x, yv[u].x, tv[u].x, lon, lat, tim, sp, b0, z0);
+      uint8_t s1 = z3_key_one_tab<PERIOD, LENIENT>(xv[u].y, yv[u].y, tv[u].y, lon, lat, tim, sp, b1, z1);
+#endif
       st_stream(lv2{z0, z1}, &z[p]);
       bin[p] = make_short2(b0, b1);
       if (STATUS) status[p] = make_uchar2(s0, s1);

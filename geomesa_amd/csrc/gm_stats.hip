@@ -62,13 +62,6 @@ __device__ __forceinline__ int hist_slot(double x, double y, int64_t ms, const H
   return i < 0 ? -1 : rb * a.length + i;
 }
 
-// Z3.split through an LDS table of the 11-bit spread (Z3.scala:73-80): two lookups per dimension
-// replace the 8-op magic-number spread of each half (the kernel is VALU-bound on the encode)
-__device__ __forceinline__ uint64_t z3_split_tab(int32_t value, const uint32_t* sp) {
-  const uint32_t v = (uint32_t)value & 0x1fffffu;
-  return ((uint64_t)sp[v >> 11] << 33) | (uint64_t)sp[v & 0x7ffu];
-}
-
 // hist_slot with the table spread; the bounds / lenient / normalize steps are z3_index_one's
 template <int PERIOD, bool UNOBS>
 __device__ __forceinline__ int hist_slot_tab(double x, double y, int64_t ms, const HistArgs& a, const uint32_t* sp,
@@ -109,7 +102,7 @@ __global__ __launch_bounds__(HTPB) void k_z3_hist_lds(const double* __restrict__
   present += a.row_lo;
   for (int i = threadIdx.x; i < total; i += HTPB) cnt[i] = 0;
   for (int i = threadIdx.x; i < a.row_n; i += HTPB) pres[i] = UNOBS ? (int)present[i] : 0;
-  for (int i = threadIdx.x; i < 2048; i += HTPB) sp[i] = spread3_11((uint32_t)i);
+  fill_spread_table(sp, threadIdx.x, HTPB);
   if (threadIdx.x == 0) { s_skip = 0; s_out = 0; }
   __syncthreads();
   int skip = 0, out = 0;
