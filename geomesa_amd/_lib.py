@@ -91,10 +91,13 @@ SIGNATURES = {
     "gm_xz3_index": (cint, [vp, vp, vp, vp, vp, vp, vp, i64, cint, cint, cint, vp, vp, vp]),
     "gm_z3_ranges": (cint, [vp, i64, vp, vp, vp, vp, cint, cint, cint, cint, cint, vp, vp, i64, vp, vp]),
     "gm_z2_ranges": (cint, [vp, i64, vp, vp, cint, cint, cint, cint, vp, vp, i64, vp, vp]),
+    "gm_zranges": (cint, [vp, cint, i64, vp, vp, cint, cint, cint, vp, vp, i64, vp, vp]),
     "gm_xz2_ranges": (cint, [vp, i64, vp, vp, cint, cint, vp, vp, i64, vp, vp]),
     "gm_xz3_ranges": (cint, [vp, i64, vp, vp, cint, cint, cint, vp, vp, i64, vp, vp]),
     "gm_z3filter_scan": (cint, [vp, vp, sz, vp, cint, vp, vp, i64, vp, vp, i64, vp]),
     "gm_z2filter_scan": (cint, [vp, vp, sz, vp, i64, vp, vp, i64, vp]),
+    "gm_z3filter_scan_rows": (cint, [vp, vp, sz, vp, vp, cint, i64, vp, vp, i64, vp, vp]),
+    "gm_z2filter_scan_rows": (cint, [vp, vp, sz, vp, vp, cint, i64, vp, vp, i64, vp, vp]),
     "gm_strict_scan": (cint, [vp, vp, vp, vp, i64, vp, cint, i64, i64, vp, vp, i64, vp]),
     "gm_query_scan": (cint, [vp, vp, vp, vp, i64, vp, cint, i64, i64, vp, cint, vp, vp, i64, vp]),
     "gm_pip_index_create": (cint, [vp, vp, vp]),

@@ -2,12 +2,13 @@
 import os
 import subprocess
 import sys
+from concurrent.futures import ThreadPoolExecutor
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 SRC = ["gm_ctx.hip", "gm_curve.hip", "gm_filter.hip", "gm_pip.hip", "gm_ranges.hip", "gm_sort.hip", "gm_arrow.hip", "gm_stats.hip", "gm_legacy.hip"]
 OUT = os.path.join(HERE, "lib", "libgeomesa_hip.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math", "-fPIC", "-shared",
+FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math", "-fPIC",
          "-Wall", "-Wno-unused-function"]
 
 
@@ -30,7 +31,23 @@ def build(force=False, verbose=True, out=OUT, defines=()):
     if out == OUT and not defines and not force and not needs_build():
         return OUT
     os.makedirs(os.path.dirname(out), exist_ok=True)
-    cmd = [HIPCC] + FLAGS + ["-D" + d for d in defines] + ["-o", out + ".tmp"] + sources()
+    # one object per unit, compiled in parallel (no device code crosses units), then one link
+    objdir = out + ".objs"
+    os.makedirs(objdir, exist_ok=True)
+    defs = ["-D" + d for d in defines]
+
+    def compile_one(src):
+        obj = os.path.join(objdir, os.path.basename(src) + ".o")
+        cmd = [HIPCC] + FLAGS + defs + ["-c", "-o", obj, src]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.check_call(cmd)
+        return obj
+
+    jobs = max(1, min(len(sources()), int(os.environ.get("MAX_JOBS", os.cpu_count() or 4))))
+    with ThreadPoolExecutor(jobs) as ex:
+        objs = list(ex.map(compile_one, sources()))
+    cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", out + ".tmp"] + objs
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.check_call(cmd)

@@ -77,7 +77,7 @@ __device__ __forceinline__ int64_t z3_apply(int32_t x, int32_t y, int32_t t) {
 }
 
 // ---------------------------------------------------------------- Z2 interleave
-// Z2.split (z3/zorder/sfcurve/Z2.scala:164-173): 31 bits -> even bits of 62. Two 16-bit halves.
+// Z2.split (z3/zorder/sfcurve/Z2.scala:58-67): 31 bits -> even bits of 62. Two 16-bit halves.
 __device__ __forceinline__ uint32_t spread2_16(uint32_t x) {
   x &= 0xffffu;
   x = (x | (x << 8)) & 0x00ff00ffu;
@@ -98,7 +98,7 @@ __device__ __forceinline__ uint32_t compact2_16(uint32_t x) {
   x = (x ^ (x >> 8)) & 0x0000ffffu;
   return x;
 }
-// Z2.combine (Z2.scala:176-184): 32 result bits (bit 62 of z lands in bit 31), then .toInt
+// Z2.combine (Z2.scala:70-78): 32 result bits (bit 62 of z lands in bit 31), then .toInt
 __device__ __forceinline__ int32_t z2_combine(int64_t z) {
   uint64_t u = (uint64_t)z;
   return (int32_t)(compact2_16((uint32_t)u) | (compact2_16((uint32_t)(u >> 32)) << 16));
@@ -108,7 +108,7 @@ __device__ __forceinline__ int64_t z2_apply(int32_t x, int32_t y) {
 }
 
 // ---------------------------------------------------------------- BitNormalizedDimension
-// z3/curve/NormalizedDimension.scala:210-226. normalizer/denormalizer are folded at compile time in
+// z3/curve/NormalizedDimension.scala:56-72. normalizer/denormalizer are folded at compile time in
 // IEEE binary64, exactly the values the JVM computes in the constructor.
 struct NDim {
   double min, max, normalizer, denormalizer;

@@ -329,6 +329,72 @@ __global__ __launch_bounds__(FTPB) void k_mask_to_ids(const uint64_t* __restrict
   }
 }
 
+// ------------------------------------------------------------------ row-key bytes (RowFilter.inBounds)
+// RowFilterIterator.findTop calls filter.inBounds(row bytes, offset) once per row
+// (geomesa-accumulo-iterators/.../RowFilterIterator.scala:52-66).  Here row i is
+// rows[row_off[i] .. row_off[i+1]): the key is read from aligned dwords covering its bytes (a dword
+// holding at least one byte of the row never crosses a page) and byte-swapped from big-endian
+// (ByteArrays.readShort / readLong).  A row too short for its key is a non-match counted in
+// *short_rows (the JVM read would throw ArrayIndexOutOfBoundsException).
+template <int KEYLEN>
+__device__ __forceinline__ bool row_key(const uint8_t* __restrict__ rows, const int64_t* __restrict__ row_off,
+                                        int64_t i, int key_offset, int16_t& epoch, int64_t& z) {
+  const int64_t a = row_off[i], len = row_off[i + 1] - a;
+  if (len < (int64_t)key_offset + KEYLEN) return false;
+  const uintptr_t p = (uintptr_t)(rows + a + key_offset);
+  const uint32_t* w = (const uint32_t*)(p & ~(uintptr_t)3);
+  const int sh = (int)(p & 3);
+  const uint32_t w0 = w[0], w1 = w[1];
+  const uint32_t w2 = (KEYLEN == 10 || sh > 0) ? w[2] : 0u;
+  const uint32_t w3 = (KEYLEN == 10 && sh == 3) ? w[3] : 0u;
+  const uint64_t lo = (uint64_t)w0 | ((uint64_t)w1 << 32), hi = (uint64_t)w2 | ((uint64_t)w3 << 32);
+  const uint64_t k0 = sh ? (lo >> (8 * sh)) | (hi << (64 - 8 * sh)) : lo;   // key bytes 0..7, little-endian
+  if (KEYLEN == 8) {
+    z = (int64_t)__builtin_bswap64(k0);
+    epoch = 0;
+  } else {
+    const uint64_t k1 = hi >> (8 * sh);                                      // key bytes 8..
+    epoch = (int16_t)(uint16_t)(((k0 & 0xffu) << 8) | ((k0 >> 8) & 0xffu));
+    z = (int64_t)__builtin_bswap64((k0 >> 16) | (k1 << 48));
+  }
+  return true;
+}
+
+template <bool Z3>
+__global__ __launch_bounds__(FTPB) void k_filter_rows_mask(const uint8_t* __restrict__ rows,
+                                                           const int64_t* __restrict__ row_off, int key_offset,
+                                                           int64_t n, const int32_t* __restrict__ fdesc, int fwords,
+                                                           uint64_t* __restrict__ mask, int32_t* __restrict__ block_counts,
+                                                           unsigned long long* __restrict__ short_rows) {
+  extern __shared__ int32_t s_f[];
+  for (int i = threadIdx.x; i < fwords; i += FTPB) s_f[i] = fdesc[i];
+  __syncthreads();
+  const int64_t base = (int64_t)blockIdx.x * FROWS;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int local = 0, nshort = 0;
+  for (int u = 0; u < FELEMS; ++u) {
+    const int64_t i = base + (int64_t)u * FTPB + threadIdx.x;
+    bool ok = false;
+    if (i < n) {
+      int16_t e;
+      int64_t zz;
+      if (row_key<Z3 ? 10 : 8>(rows, row_off, i, key_offset, e, zz)) {
+        ok = Z3 ? z3_in_bounds(s_f, e, zz) : z2_in_xy(s_f, fwords / 4, zz);   // Z3Filter.scala:26-28 / Z2Filter
+      } else {
+        ++nshort;
+      }
+    }
+    const uint64_t w = __ballot(ok);
+    if (lane == 0) {
+      const int64_t word = (base + (int64_t)u * FTPB + wave * 64) >> 6;
+      if ((word << 6) < n) mask[word] = w;
+      local += __popcll(w);
+    }
+  }
+  if (nshort && short_rows) atomicAdd(short_rows, (unsigned long long)nshort);
+  block_count(local, block_counts);
+}
+
 // ------------------------------------------------------------------ range scan of a sorted table
 // gm_key_range_scan: the seek-and-filter loop of a Z3 query against a table sorted by gm_sort_keys.
 // Each range [lo, hi] of the (shard, bin, z) key prefix (getRangeBytes, Z3IndexKeySpace.scala:196-238)
@@ -672,6 +738,67 @@ int gm_z2filter_scan(gm_ctx* ctx, const uint8_t* filter_bytes, size_t filter_len
   if (rc) return rc;
   if (n_match && ids && *n_match > ids_cap) return GM_E_CAPACITY;
   return GM_OK;
+}
+
+// shared driver of gm_z3filter_scan_rows / gm_z2filter_scan_rows
+static int filter_rows(gm_ctx* ctx, bool z3, const std::vector<int32_t>& desc, const uint8_t* rows,
+                       const int64_t* row_off, int key_offset, int64_t n, uint64_t* mask, int64_t* ids,
+                       int64_t ids_cap, int64_t* n_match, int64_t* n_short) {
+  if (n == 0) { if (n_match) *n_match = 0; if (n_short) *n_short = 0; return GM_OK; }
+  if (!rows || !row_off || key_offset < 0) return GM_E_INVALID;
+  ScanBufs b;
+  // descriptor words, then one 8-B short-row counter (16-B aligned)
+  const size_t dw = (desc.size() + 3) & ~(size_t)3;
+  int rc = alloc_scan(ctx, n, mask, dw + 4, b);
+  if (rc) return rc;
+  unsigned long long* d_short = (unsigned long long*)(b.desc + dw);
+  GM_HIP(hipMemcpyAsync(b.desc, desc.data(), desc.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+  GM_HIP(hipMemsetAsync(d_short, 0, 8, ctx->stream));
+  GM_HIP(hipStreamSynchronize(ctx->stream));  // desc is pageable host memory
+  const int64_t nblocks = (n + FROWS - 1) / FROWS;
+  const size_t lds = std::max<size_t>(desc.size() * 4, 4);
+  if (z3)
+    hipLaunchKernelGGL(k_filter_rows_mask<true>, dim3((unsigned)nblocks), dim3(FTPB), lds, ctx->stream, rows, row_off,
+                       key_offset, n, b.desc, (int)desc.size(), b.mask, b.counts, d_short);
+  else
+    hipLaunchKernelGGL(k_filter_rows_mask<false>, dim3((unsigned)nblocks), dim3(FTPB), lds, ctx->stream, rows, row_off,
+                       key_offset, n, b.desc, (int)desc.size(), b.mask, b.counts, d_short);
+  GM_CHECK_LAUNCH();
+  rc = finish_scan(ctx, n, b, ids, ids_cap, n_match);
+  if (rc) return rc;
+  if (n_short) {
+    GM_HIP(hipMemcpyAsync(ctx->h_pinned, d_short, 8, hipMemcpyDeviceToHost, ctx->stream));
+    GM_HIP(hipStreamSynchronize(ctx->stream));
+    *n_short = ctx->h_pinned[0];
+  }
+  if (n_match && ids && *n_match > ids_cap) return GM_E_CAPACITY;
+  return GM_OK;
+}
+
+int gm_z3filter_scan_rows(gm_ctx* ctx, const uint8_t* filter_bytes, size_t filter_len, const uint8_t* rows,
+                          const int64_t* row_off, int key_offset, int64_t n, uint64_t* mask, int64_t* ids,
+                          int64_t ids_cap, int64_t* n_match, int64_t* n_short) {
+  if (!ctx || !filter_bytes || n < 0) return GM_E_INVALID;
+  std::vector<int32_t> desc;
+  if (!build_z3_desc(filter_bytes, filter_len, desc)) {
+    set_error("gm_z3filter_scan_rows: malformed Z3Filter bytes");
+    return GM_E_INVALID;
+  }
+  return filter_rows(ctx, true, desc, rows, row_off, key_offset, n, mask, ids, ids_cap, n_match, n_short);
+}
+
+int gm_z2filter_scan_rows(gm_ctx* ctx, const uint8_t* filter_bytes, size_t filter_len, const uint8_t* rows,
+                          const int64_t* row_off, int key_offset, int64_t n, uint64_t* mask, int64_t* ids,
+                          int64_t ids_cap, int64_t* n_match, int64_t* n_short) {
+  if (!ctx || !filter_bytes || n < 0 || filter_len < 4) return GM_E_INVALID;
+  const int32_t nxy = be32(filter_bytes);
+  if (nxy < 0 || 4 + (size_t)nxy * 16 > filter_len) {
+    set_error("gm_z2filter_scan_rows: malformed Z2Filter bytes");
+    return GM_E_INVALID;
+  }
+  std::vector<int32_t> xy((size_t)nxy * 4);
+  for (size_t i = 0; i < xy.size(); ++i) xy[i] = be32(filter_bytes + 4 + 4 * i);
+  return filter_rows(ctx, false, xy, rows, row_off, key_offset, n, mask, ids, ids_cap, n_match, n_short);
 }
 
 int gm_strict_scan(gm_ctx* ctx, const double* x, const double* y, const int64_t* t_ms, int64_t n, const double* bbox,

@@ -68,7 +68,7 @@ __device__ __forceinline__ int32_t zdim(int64_t z, int d) {
   return D == 3 ? z3_combine(z >> d) : z2_combine(z >> d);
 }
 
-// Z3.contains / Z2.contains (Z3.scala:93-98, Z2.scala:186-189) on decoded dims
+// Z3.contains / Z2.contains (Z3.scala:93-98, Z2.scala:80-83) on decoded dims
 template <int D>
 __device__ __forceinline__ bool z_contains(const int32_t* b, int64_t v) {
 #pragma unroll
@@ -164,6 +164,8 @@ struct ZRangesArgs {
   const double* xy;         // 4 per box
   const int32_t* time_off;  // [nq + 1] (Z3 only)
   const int64_t* t;         // 2 per interval
+  const int32_t* zb_off;    // raw ZRange mode (gm_zranges): [nq + 1] bound offsets, else null
+  const int64_t* zb;        //   (min, max) per bound
   int64_t q0;               // first query of this chunk
   NDim lon, lat, tim;
   int range_precision, range_stop, recurse_stop;
@@ -199,9 +201,11 @@ __global__ __launch_bounds__(RTPB) void k_zranges(ZRangesArgs a) {
   int64_t* rhi = a.rhi + qc * a.rcap;
   uint8_t* rc = a.rc + qc * a.rcap;
 
-  const int b0 = a.box_off[q], nbx = a.box_off[q + 1] - b0;
+  const bool raw = a.zb != nullptr;
+  const int b0 = raw ? a.zb_off[q] : a.box_off[q];
+  const int nbx = (raw ? a.zb_off[q + 1] : a.box_off[q + 1]) - b0;
   int t0 = 0, ntm = 1;
-  if (D == 3) { t0 = a.time_off[q]; ntm = a.time_off[q + 1] - t0; }
+  if (D == 3 && !raw) { t0 = a.time_off[q]; ntm = a.time_off[q + 1] - t0; }
   const int nb = nbx * ntm;
   if (threadIdx.x == 0) s_err = (nb > MAXB) ? QS_TOO_MANY_BOUNDS : QS_OK;
   __syncthreads();
@@ -210,12 +214,15 @@ __global__ __launch_bounds__(RTPB) void k_zranges(ZRangesArgs a) {
     return;
   }
   // zbounds: Z3SFC.ranges builds ZRange(index(xmin, ymin, tmin), index(xmax, ymax, tmax)) for the
-  // cross product xy x t, non-lenient (Z3SFC.scala:63-65); Z2SFC.ranges likewise (Z2SFC.scala:151)
+  // cross product xy x t, non-lenient (Z3SFC.scala:63-65); Z2SFC.ranges likewise (Z2SFC.scala:50)
   for (int j = threadIdx.x; j < nb; j += RTPB) {
-    const double* bx = a.xy + 4 * (int64_t)(b0 + j / ntm);
     int64_t lo = 0, hi = 0;
-    uint8_t st;
-    if (D == 3) {
+    uint8_t st = ST_OK;
+    if (raw) {   // ZN.zranges(Array[ZRange], ...) (ZN.scala:110-113): the bounds as given
+      lo = a.zb[2 * (int64_t)(b0 + j)];
+      hi = a.zb[2 * (int64_t)(b0 + j) + 1];
+    } else if (D == 3) {
+      const double* bx = a.xy + 4 * (int64_t)(b0 + j / ntm);
       const int64_t* tt = a.t + 2 * (int64_t)(t0 + j % ntm);
       auto idx = [&](double x, double y, int64_t tv, int64_t& z) -> uint8_t {
         const double td = (double)tv;
@@ -228,6 +235,7 @@ __global__ __launch_bounds__(RTPB) void k_zranges(ZRangesArgs a) {
       st = idx(bx[0], bx[1], tt[0], lo);
       if (!st) st = idx(bx[2], bx[3], tt[1], hi);
     } else {
+      const double* bx = a.xy + 4 * (int64_t)(b0 + j);
       auto idx = [&](double x, double y, int64_t& z) -> uint8_t {
         if (!(x >= a.lon.min && x <= a.lon.max && y >= a.lat.min && y <= a.lat.max)) return ST_OUT_OF_BOUNDS;
         z = z2_apply(normalize(a.lon, x), normalize(a.lat, y));
@@ -236,7 +244,7 @@ __global__ __launch_bounds__(RTPB) void k_zranges(ZRangesArgs a) {
       st = idx(bx[0], bx[1], lo);
       if (!st) st = idx(bx[2], bx[3], hi);
     }
-    if (!st && lo > hi) st = QS_UNORDERED;  // ZRange require(min <= max) (package.scala:220)
+    if (!st && lo > hi) st = QS_UNORDERED;  // ZRange require(min <= max) (package.scala:24)
     if (st) atomicMax(&s_err, (int)st);
     s_zb[2 * j] = lo;
     s_zb[2 * j + 1] = hi;
@@ -882,6 +890,42 @@ static int xz_ranges(gm_ctx* ctx, int D, int64_t nq, const int32_t* win_off, con
                   },
                   out_off, out, cap, needed, query_status);
   (void)hipFreeAsync(dwo, s); (void)hipFreeAsync(dw, s);
+  return rc;
+}
+
+int gm_zranges(gm_ctx* ctx, int dims, int64_t nq, const int32_t* bound_off, const int64_t* zbounds,
+               int range_precision, int max_ranges, int max_recurse, int64_t* out_off, gm_range* out, int64_t cap,
+               int64_t* needed, int32_t* query_status) {
+  if (!ctx || (dims != 2 && dims != 3) || nq < 0 || !bound_off || !out_off || range_precision < 1 ||
+      range_precision > 64)
+    return GM_E_INVALID;
+  if (nq == 0) { out_off[0] = 0; if (needed) *needed = 0; return GM_OK; }
+  hipStream_t s = ctx->stream;
+  const int64_t nb = bound_off[nq];
+  if (nb > 0 && !zbounds) return GM_E_INVALID;
+  int32_t* dbo;
+  int64_t* dzb;
+  int rc = to_dev(ctx, bound_off, (size_t)nq + 1, &dbo);
+  if (!rc) rc = to_dev(ctx, zbounds, (size_t)nb * 2, &dzb);
+  if (rc) return rc;
+  ZRangesArgs a{};
+  a.zb_off = dbo; a.zb = dzb;
+  a.range_precision = range_precision;
+  a.range_stop = stop_of(max_ranges);
+  a.recurse_stop = max_recurse < 0 ? 7 : max_recurse;   // maxRecurse = Some(ZN.DefaultRecurse) (ZN.scala:113,293)
+  const int64_t zc = z_caps(max_ranges, dims, cap);
+  rc = run_ranges(ctx, nq, zc, zc, 8,
+                  [&](int64_t q0, int64_t m, int64_t fcap, int64_t rcap, char* fa, char* fb, int64_t* rlo, int64_t* rhi,
+                      uint8_t* rcb, int64_t* gkey, int32_t* gidx, gm_range* ws, int32_t* dcnt, int32_t* dst) {
+                    ZRangesArgs b = a;
+                    b.q0 = q0; b.fcap = fcap; b.rcap = rcap;
+                    b.fa = (int64_t*)fa; b.fb = (int64_t*)fb; b.rlo = rlo; b.rhi = rhi; b.rc = rcb;
+                    b.gkey = gkey; b.gidx = gidx; b.out = ws; b.out_count = dcnt; b.status = dst;
+                    if (dims == 3) hipLaunchKernelGGL(k_zranges<3>, dim3((unsigned)m), dim3(RTPB), 0, s, b);
+                    else hipLaunchKernelGGL(k_zranges<2>, dim3((unsigned)m), dim3(RTPB), 0, s, b);
+                  },
+                  out_off, out, cap, needed, query_status);
+  (void)hipFreeAsync(dbo, s); (void)hipFreeAsync(dzb, s);
   return rc;
 }
 

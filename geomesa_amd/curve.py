@@ -4,7 +4,7 @@ Mirrors the reference Scala surface (paths relative to
 geomesa-z3/src/main/scala/org/locationtech/geomesa/):
 
   * ``Z3SFC(period, precision=21)``  -- curve/Z3SFC.scala:21-100
-  * ``Z2SFC(precision=31)``          -- curve/Z2SFC.scala:115-154
+  * ``Z2SFC(precision=31)``          -- curve/Z2SFC.scala:14-53
   * ``XZ2SFC(g)`` / ``XZ3SFC(g, period)`` -- curve/XZ2SFC.scala, curve/XZ3SFC.scala
   * ``BinnedTime`` / ``TimePeriod``   -- curve/BinnedTime.scala
 
@@ -42,7 +42,7 @@ class TimePeriod:
         raise IllegalArgumentException("unknown time period %r" % (p,))
 
 
-IndexRange = namedtuple("IndexRange", ["lower", "upper", "contained"])  # package.scala:241-272
+IndexRange = namedtuple("IndexRange", ["lower", "upper", "contained"])  # package.scala:45-76
 
 
 def CoveredRange(lower, upper):
@@ -59,7 +59,7 @@ def max_offset(period):
 
 
 class NormalizedDimension:
-    """BitNormalizedDimension constants (curve/NormalizedDimension.scala:210-226)."""
+    """BitNormalizedDimension constants (curve/NormalizedDimension.scala:56-72)."""
 
     def __init__(self, mn, mx, precision):
         if not (0 < precision < 32):
@@ -86,6 +86,40 @@ class NormalizedDimension:
         if i >= self.maxIndex:
             return self.min + (self.maxIndex + 0.5) * self.denormalizer
         return self.min + (i + 0.5) * self.denormalizer
+
+
+def _jvm_to_int(v):
+    """Double.toInt: NaN -> 0, saturating at Int.MinValue / Int.MaxValue."""
+    if v != v:
+        return 0
+    if v >= 2147483647:
+        return 2147483647
+    if v <= -2147483648:
+        return -2147483648
+    return int(v)
+
+
+class SemiNormalizedDimension:
+    """Legacy SemiNormalizedDimension (curve/NormalizedDimension.scala:83-87): ceil-based, maxIndex =
+    precision (2^21 - 1 or 2^20 - 1).  Host scalar forms for query planning on legacy indices."""
+
+    def __init__(self, mn, mx, precision):
+        self.min = float(mn)
+        self.max = float(mx)
+        self.precision = int(precision)
+        self.maxIndex = int(precision)
+
+    def normalize(self, x):   # math.ceil((x - min) / (max - min) * precision).toInt   (:85)
+        import math
+        v = (float(x) - self.min) / (self.max - self.min) * float(self.precision)
+        if v != v or v in (float("inf"), float("-inf")):
+            return _jvm_to_int(v)
+        return _jvm_to_int(math.ceil(v))
+
+    def denormalize(self, i):   # :86
+        if i == 0:
+            return self.min
+        return (i - 0.5) * (self.max - self.min) / float(self.precision) + self.min
 
 
 # ------------------------------------------------------------------------------ column helpers
@@ -228,7 +262,7 @@ class Z3SFC:
 
 
 class Z2SFC:
-    """Z2 space filling curve (curve/Z2SFC.scala:115-154); Z2SFC() is the 31-bit object."""
+    """Z2 space filling curve (curve/Z2SFC.scala:14-53); Z2SFC() is the 31-bit object."""
 
     _cache = {}
 
@@ -370,6 +404,12 @@ class LegacyZ3SFC(_LegacyBase):
     def __init__(self, period=TimePeriod.Week):
         self.period = TimePeriod.of(period)
         self.curve = self.LEGACY_Z3
+        # LegacyZ3Dimensions (LegacyZ3SFC.scala:46-51): host planning forms of the dimensions
+        self.precision = 21
+        self.lon = SemiNormalizedDimension(-180.0, 180.0, (1 << 21) - 1)
+        self.lat = SemiNormalizedDimension(-90.0, 90.0, (1 << 21) - 1)
+        self.time = SemiNormalizedDimension(0.0, float(max_offset(self.period)), (1 << 20) - 1)
+        self.wholePeriod = [(int(self.time.min), int(self.time.max))]   # Z3SFC.wholePeriod (Z3SFC.scala:27)
 
     def index(self, x, y, t, lenient=False, status=False):
         torch = _torch()

@@ -188,6 +188,32 @@ def z2_deserialize_from_strings(m):
     return Z2Filter([[int(v) for v in b.split(_RS)] for b in _java_split(m[XYKey], _TS)])
 
 
+RowOffsetKey = "zo"   # RowFilterIterator.RowOffsetKey (geomesa-accumulo-iterators/.../RowFilterIterator.scala:84-86)
+
+
+def z3_iterator_options(values, offset, compatibility=None):
+    """Z3Iterator.configure's iterator options (geomesa-accumulo-iterators/.../Z3Iterator.scala:30-66).
+
+    compatibility None: the serialized Z3Filter plus the row offset; "1.3": the GeoMesa 1.3 option
+    strings -- per bounding box the normalized corners "xmin:ymin:xmax:ymax" joined by ";", per time
+    bin (ascending) "bin;t1:t2[;t1:t2...]" joined by ",", through the values' own curve (the legacy
+    SemiNormalized dimensions for a Z3IndexKeySpaceV4)."""
+    if compatibility is None:
+        opts = serialize_to_strings(Z3Filter.from_values(values))
+        opts[RowOffsetKey] = str(offset)
+        return opts
+    if compatibility != "1.3":
+        raise NotImplementedError("Unknown compatibility flag: '%s'" % compatibility)
+    sfc = values.sfc
+    xy = ["%d:%d:%d:%d" % (sfc.lon.normalize(a), sfc.lat.normalize(b), sfc.lon.normalize(c), sfc.lat.normalize(d))
+          for (a, b, c, d) in values.spatialBounds]
+    ts = []
+    for b in sorted(values.temporalBounds):
+        ts.append("%d;%s" % (b, _TS.join("%d:%d" % (sfc.time.normalize(t1), sfc.time.normalize(t2))
+                                         for (t1, t2) in values.temporalBounds[b])))
+    return {XYKey: _TS.join(xy), TKey: _ES.join(ts), RowOffsetKey: str(offset), "zl": "8"}
+
+
 # ------------------------------------------------------------------------------ GPU scans
 
 def _cols(*pairs):
@@ -248,6 +274,37 @@ def z2_scan(z2filter, z, want_ids=False, ids_cap=None):
     if rc != _lib.GM_E_CAPACITY:
         check(rc, "gm_z2filter_scan")
     return _mask_to_bool(mask, n), (ids[:min(nm.value, cap)] if want_ids else None), nm.value
+
+
+def scan_rows(row_filter, rows, row_off, key_offset=0, want_ids=False, ids_cap=None):
+    """RowFilter.inBounds(row, key_offset) for every row of a batch of row-key bytes (the loop of
+    RowFilterIterator.findTop, RowFilterIterator.scala:52-66): gm_z3filter_scan_rows for a Z3Filter
+    (or its serialized bytes with kind "z3"), gm_z2filter_scan_rows for a Z2Filter.  rows = all row
+    bytes back to back (uint8), row_off = n + 1 int64 offsets.  Returns (mask, ids, n_match, n_short)."""
+    import torch
+    if isinstance(row_filter, Z2Filter):
+        fb, fn = z2_serialize_to_bytes(row_filter), "gm_z2filter_scan_rows"
+    else:
+        fb = serialize_to_bytes(row_filter) if isinstance(row_filter, Z3Filter) else bytes(row_filter)
+        fn = "gm_z3filter_scan_rows"
+    ctx = _lib.context()
+    dev = torch.device("cuda", ctx.device)
+    rows = rows.to(dev) if isinstance(rows, torch.Tensor) else torch.from_numpy(
+        np.ascontiguousarray(np.frombuffer(bytes(rows), np.uint8) if isinstance(rows, (bytes, bytearray))
+                             else np.asarray(rows, np.uint8))).to(dev)
+    if rows.numel() == 0:
+        rows = torch.zeros(4, dtype=torch.uint8, device=dev)
+    (row_off,) = _cols((row_off, torch.int64))
+    n = row_off.numel() - 1
+    cap = n if ids_cap is None else ids_cap
+    mask, ids = _outputs(n, dev, want_ids, cap)
+    fbuf = (ctypes.c_uint8 * len(fb)).from_buffer_copy(fb)
+    nm, ns = ctypes.c_int64(), ctypes.c_int64()
+    rc = getattr(ctx.lib, fn)(ctx.handle, fbuf, len(fb), ptr(rows), ptr(row_off), int(key_offset), n, ptr(mask),
+                              ptr(ids), cap, ctypes.byref(nm), ctypes.byref(ns))
+    if rc != _lib.GM_E_CAPACITY:
+        check(rc, fn)
+    return _mask_to_bool(mask, n), (ids[:min(nm.value, cap)] if want_ids else None), nm.value, ns.value
 
 
 def strict_scan(x, y, t_ms, bbox, during=None, want_ids=False, ids_cap=None):

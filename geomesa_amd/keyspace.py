@@ -12,7 +12,7 @@ from dataclasses import dataclass, field
 
 import numpy as np
 
-from .curve import BinnedTime, IllegalArgumentException, TimePeriod, Z2SFC, Z3SFC, max_offset
+from .curve import BinnedTime, IllegalArgumentException, LegacyZ3SFC, TimePeriod, Z2SFC, Z3SFC, max_offset
 
 SHORT_MAX = 32767
 WHOLE_WORLD = (-180.0, -90.0, 180.0, 90.0)
@@ -156,9 +156,9 @@ def _clip_world(b):
 class Z3IndexKeySpace:
     """Z3 index key space for a point geometry + date attribute, no sharding by default."""
 
-    def __init__(self, period=TimePeriod.Week, shards=0):
+    def __init__(self, period=TimePeriod.Week, shards=0, sfc=None):
         self.period = TimePeriod.of(period)
-        self.sfc = Z3SFC(self.period)
+        self.sfc = Z3SFC(self.period) if sfc is None else sfc
         self.shards = shards
 
     # getIndexValues (Z3IndexKeySpace.scala:97-159) for bbox + temporal predicates
@@ -244,6 +244,14 @@ class Z3IndexKeySpace:
         out[:, off:off + 2] = bins.astype(">i2").view(np.uint8).reshape(n, 2)
         out[:, off + 2:off + 10] = z.astype(">i8").view(np.uint8).reshape(n, 8)
         return out
+
+
+class Z3IndexKeySpaceV4(Z3IndexKeySpace):
+    """Z3IndexV4.Z3IndexKeySpaceV4 (geomesa-index-api/.../index/z3/legacy/Z3IndexV4.scala:44-51): the
+    GeoMesa 1.3 key space, the same planning over LegacyZ3SFC(period)'s semi-normalized dimensions."""
+
+    def __init__(self, period=TimePeriod.Week, shards=0):
+        super().__init__(period, shards, sfc=LegacyZ3SFC(period))
 
 
 class Z2IndexKeySpace:

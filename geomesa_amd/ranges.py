@@ -138,6 +138,25 @@ def z2_ranges(sfc, queries, precision=64, max_ranges=None, max_recurse=None):
     return _run(ctx.lib.gm_z2_ranges, args, nq, cap)
 
 
+def zranges(dims, queries, precision=64, max_ranges=None, max_recurse=None):
+    """ZN.zranges(Array[ZRange], precision, maxRanges, maxRecurse) (zorder/sfcurve/ZN.scala:110-113)
+    as Z3.zranges (dims 3) / Z2.zranges (dims 2), one call per query of raw (min, max) z bounds.
+    max_recurse None = the Scala default Some(ZN.DefaultRecurse) = 7."""
+    ctx = _lib.context()
+    nq = len(queries)
+    off, zb = [0], []
+    for bounds in queries:
+        for (lo, hi) in bounds:
+            zb.extend((int(lo), int(hi)))
+        off.append(len(zb) // 2)
+    bo = np.asarray(off, np.int32)
+    za = np.asarray(zb if zb else [0], np.int64)
+    cap = nq * (max_ranges + 16 if max_ranges else 4096)
+    args = (ctx.handle, int(dims), nq, bo.ctypes.data, za.ctypes.data, int(precision), _mr(max_ranges),
+            -1 if max_recurse is None else int(max_recurse))
+    return _run(ctx.lib.gm_zranges, args, nq, cap)
+
+
 def _windows(queries, dims):
     off, w = [0], []
     for wins in queries:

@@ -70,7 +70,7 @@ typedef struct {
   int32_t reserved;
 } gm_batch_status;
 
-/* IndexRange (z3/zorder/sfcurve/package.scala:241-272): CoveredRange when contained = 1 */
+/* IndexRange (z3/zorder/sfcurve/package.scala:45-76): CoveredRange when contained = 1 */
 typedef struct {
   int64_t lower;
   int64_t upper;
@@ -115,7 +115,7 @@ int gm_z3_index_key(gm_ctx* ctx, const double* x, const double* y, const int64_t
 int gm_z3_invert(gm_ctx* ctx, const int64_t* z, int64_t n, int period, int precision, double* x, double* y,
                  int64_t* t);
 
-/* Z2SFC.index / invert (z3/curve/Z2SFC.scala:127-146); precision 1..31 (Z2SFC object uses 31) */
+/* Z2SFC.index / invert (z3/curve/Z2SFC.scala:26-45); precision 1..31 (Z2SFC object uses 31) */
 int gm_z2_index(gm_ctx* ctx, const double* x, const double* y, int64_t n, int precision, int lenient,
                 int64_t* z, uint8_t* status, gm_batch_status* summary);
 int gm_z2_invert(gm_ctx* ctx, const int64_t* z, int64_t n, int precision, double* x, double* y);
@@ -134,7 +134,7 @@ int gm_xz3_index(gm_ctx* ctx, const double* xmin, const double* ymin, const doub
 
 /* ------------------------------------------------------------------ range decomposition */
 /* Batched ZN.zranges (z3/zorder/sfcurve/ZN.scala:110-242) as reached from Z3SFC.ranges
-   (z3/curve/Z3SFC.scala:59-67) and Z2SFC.ranges (z3/curve/Z2SFC.scala:148-153).
+   (z3/curve/Z3SFC.scala:59-67) and Z2SFC.ranges (z3/curve/Z2SFC.scala:47-52).
    Host inputs, one query per entry of query_off: query q owns boxes [box_off[q], box_off[q+1]) of
    xy (host, 4 doubles each) and, for Z3, times [time_off[q], time_off[q+1]) of t (host, 2 int64
    each, offsets within the period).  The z-bounds of a query are the cross product, as in
@@ -149,6 +149,15 @@ int gm_z3_ranges(gm_ctx* ctx, int64_t n_queries, const int32_t* box_off, const d
 int gm_z2_ranges(gm_ctx* ctx, int64_t n_queries, const int32_t* box_off, const double* xy, int precision,
                  int range_precision, int max_ranges, int max_recurse, int64_t* out_off, gm_range* out,
                  int64_t cap, int64_t* needed, int32_t* query_status);
+/* ZN.zranges(zbounds: Array[ZRange], precision, maxRanges, maxRecurse) (z3/zorder/sfcurve/ZN.scala:110-242)
+   on raw z bounds, as Z3.zranges (dims = 3) / Z2.zranges (dims = 2), batched: query q owns the bounds
+   [bound_off[q], bound_off[q+1]) of zbounds (host, (min, max) int64 pairs).  max_ranges <= 0 = None;
+   max_recurse < 0 = the Scala default Some(ZN.DefaultRecurse) = 7 (ZN.scala:113).  A bound with
+   min > max gets query status GM_ST_UNORDERED (ZRange's require, z3/zorder/sfcurve/package.scala:24).
+   Outputs as gm_z3_ranges. */
+int gm_zranges(gm_ctx* ctx, int dims, int64_t n_queries, const int32_t* bound_off, const int64_t* zbounds,
+               int range_precision, int max_ranges, int max_recurse, int64_t* out_off, gm_range* out, int64_t cap,
+               int64_t* needed, int32_t* query_status);
 /* Batched XZ2SFC.ranges / XZ3SFC.ranges (z3/curve/XZ2SFC.scala:130-252, XZ3SFC.scala:139-262);
    windows as above (4 or 6 doubles each, user space). */
 int gm_xz2_ranges(gm_ctx* ctx, int64_t n_queries, const int32_t* win_off, const double* windows, int g,
@@ -174,6 +183,21 @@ int gm_z3filter_scan(gm_ctx* ctx, const uint8_t* filter_bytes, size_t filter_len
 /* Z2Filter.inBounds (idx/filters/Z2Filter.scala:20-35) */
 int gm_z2filter_scan(gm_ctx* ctx, const uint8_t* filter_bytes, size_t filter_len, const int64_t* z, int64_t n,
                      uint64_t* mask, int64_t* ids, int64_t ids_cap, int64_t* n_match);
+/* RowFilter.inBounds(buf, offset) on row-key BYTES (idx/filters/RowFilter.scala:11-13), the loop of
+   RowFilterIterator.findTop (geomesa-accumulo-iterators/.../RowFilterIterator.scala:52-66) and
+   Z3HBaseFilter as one pass: row i is rows[row_off[i] .. row_off[i+1]) (device bytes; device int64
+   offsets, n + 1 of them) and its key starts at key_offset (RowFilterIterator.RowOffsetKey, the
+   shard / table-sharing prefix length).  Z3Filter.inBounds (Z3Filter.scala:26-28) reads the
+   big-endian short epoch at key_offset and the long z at key_offset + 2; Z2Filter.inBounds
+   (Z2Filter.scala:22-35) the long at key_offset.  A row shorter than its key never matches and is
+   counted in *n_short (host, optional; the JVM read throws ArrayIndexOutOfBoundsException).
+   Outputs as gm_z3filter_scan (no bin restriction: the scan ranges already chose the rows). */
+int gm_z3filter_scan_rows(gm_ctx* ctx, const uint8_t* filter_bytes, size_t filter_len, const uint8_t* rows,
+                          const int64_t* row_off, int key_offset, int64_t n, uint64_t* mask, int64_t* ids,
+                          int64_t ids_cap, int64_t* n_match, int64_t* n_short);
+int gm_z2filter_scan_rows(gm_ctx* ctx, const uint8_t* filter_bytes, size_t filter_len, const uint8_t* rows,
+                          const int64_t* row_off, int key_offset, int64_t n, uint64_t* mask, int64_t* ids,
+                          int64_t ids_cap, int64_t* n_match, int64_t* n_short);
 /* Strict full-filter evaluation on raw columns (useFullFilter, Z3IndexKeySpace.scala:240-254):
    GeoTools BBOX on a point (geomesa-filter/.../GeometryProcessing.scala:129, inclusive) AND
    FastDuring (geomesa-filter/.../FastTemporalOperator.scala:123-126, exclusive at both ends, ms).

@@ -38,7 +38,7 @@ static inline int64_t jshr(int64_t v, int s) { return v >> (s & 63); }          
 static inline int64_t jushr(int64_t v, int s) { return (int64_t)((uint64_t)v >> (s & 63)); } /* >>> */
 
 /* ------------------------------------------------------------------ */
-/* Z3 / Z2 bit interleave  (z3/../zorder/sfcurve/Z3.scala:52-91, Z2.scala:149-184) */
+/* Z3 / Z2 bit interleave  (z3/../zorder/sfcurve/Z3.scala:52-91, Z2.scala:43-78) */
 /* ------------------------------------------------------------------ */
 
 #define Z3_MAXMASK 0x1fffffLL
@@ -70,7 +70,7 @@ int64_t gmo_z3_apply(int32_t x, int32_t y, int32_t t) {
   return gmo_z3_split(x) | jshl(gmo_z3_split(y), 1) | jshl(gmo_z3_split(t), 2);
 }
 
-/* Z2.split (Z2.scala:164-173) */
+/* Z2.split (Z2.scala:58-67) */
 int64_t gmo_z2_split(int64_t value) {
   uint64_t x = (uint64_t)(value & Z2_MAXMASK);
   x = (x ^ (x << 32)) & 0x00000000ffffffffULL;
@@ -82,7 +82,7 @@ int64_t gmo_z2_split(int64_t value) {
   return (int64_t)x;
 }
 
-/* Z2.combine (Z2.scala:176-184); final .toInt keeps the low 32 bits */
+/* Z2.combine (Z2.scala:70-78); final .toInt keeps the low 32 bits */
 int32_t gmo_z2_combine(int64_t z) {
   int64_t x = z & 0x5555555555555555LL;
   x = (x ^ (x >> 1)) & 0x3333333333333333LL;
@@ -93,16 +93,16 @@ int32_t gmo_z2_combine(int64_t z) {
   return (int32_t)(uint32_t)(uint64_t)x;
 }
 
-/* Z2.apply (Z2.scala:159) */
+/* Z2.apply (Z2.scala:53) */
 int64_t gmo_z2_apply(int32_t x, int32_t y) { return gmo_z2_split(x) | jshl(gmo_z2_split(y), 1); }
 
-/* per-dimension decode, d0/d1/d2 (Z3.scala:22-24, Z2.scala:134) */
+/* per-dimension decode, d0/d1/d2 (Z3.scala:22-24, Z2.scala:26-31) */
 static inline int32_t zdim(int dims, int64_t z, int d) {
   return dims == 3 ? gmo_z3_combine(jshr(z, d)) : gmo_z2_combine(jshr(z, d));
 }
 static inline int64_t zsplit(int dims, int64_t v) { return dims == 3 ? gmo_z3_split(v) : gmo_z2_split(v); }
 
-/* Z3.contains / Z2.contains (Z3.scala:93-98, Z2.scala:186-189) */
+/* Z3.contains / Z2.contains (Z3.scala:93-98, Z2.scala:80-83) */
 int gmo_zn_contains(int dims, int64_t rmin, int64_t rmax, int64_t value) {
   for (int d = 0; d < dims; d++) {
     int32_t v = zdim(dims, value, d);
@@ -111,7 +111,7 @@ int gmo_zn_contains(int dims, int64_t rmin, int64_t rmax, int64_t value) {
   return 1;
 }
 
-/* Z3.overlaps / Z2.overlaps (Z3.scala:100-105, Z2.scala:191-195) */
+/* Z3.overlaps / Z2.overlaps (Z3.scala:100-105, Z2.scala:85-89) */
 int gmo_zn_overlaps(int dims, int64_t rmin, int64_t rmax, int64_t vmin, int64_t vmax) {
   for (int d = 0; d < dims; d++) {
     int32_t a1 = zdim(dims, rmin, d), a2 = zdim(dims, rmax, d);
@@ -197,7 +197,7 @@ static void zq_push(zqueue* q, int64_t a, int64_t b, int term) {
 }
 static inline int64_t zq_size(const zqueue* q) { return q->tail - q->head; }
 
-/* IndexRange ordering (z3/../zorder/sfcurve/package.scala:257-265) */
+/* IndexRange ordering (z3/../zorder/sfcurve/package.scala:60-69) */
 static int range_cmp(const void* pa, const void* pb) {
   const gmo_range* a = (const gmo_range*)pa; const gmo_range* b = (const gmo_range*)pb;
   if (a->lower != b->lower) return a->lower < b->lower ? -1 : 1;
@@ -399,7 +399,7 @@ int64_t gmo_binned_to_millis(int period, int16_t bin, int64_t offset) {
 }
 
 /* ------------------------------------------------------------------ */
-/* Z3SFC / Z2SFC (z3/curve/Z3SFC.scala:37-67, Z2SFC.scala:127-153)     */
+/* Z3SFC / Z2SFC (z3/curve/Z3SFC.scala:37-67, Z2SFC.scala:26-52)     */
 /* ------------------------------------------------------------------ */
 
 int gmo_z3_index(int period, int precision, double x, double y, int64_t t, int lenient, int64_t* z) {
@@ -579,7 +579,7 @@ int64_t gmo_z3_ranges(int period, int precision, const double* xy, int nxy, cons
           gmo_z3_index(period, precision, xy[4 * i + 2], xy[4 * i + 3], t[2 * j + 1], 0, &hi)) {
         free(zb); return INT64_MIN + GMO_OUT_OF_BOUNDS;
       }
-      if (lo > hi) { free(zb); return INT64_MIN + GMO_UNORDERED; }  /* ZRange require (package.scala:220) */
+      if (lo > hi) { free(zb); return INT64_MIN + GMO_UNORDERED; }  /* ZRange require (package.scala:24) */
       zb[2 * k] = lo; zb[2 * k + 1] = hi; k++;
     }
   int64_t r = gmo_zranges(3, zb, nb, range_precision, max_ranges, INT32_MAX, out, cap);
@@ -587,7 +587,7 @@ int64_t gmo_z3_ranges(int period, int precision, const double* xy, int nxy, cons
   return r;
 }
 
-/* Z2SFC.ranges (Z2SFC.scala:148-153): Z2.zranges with default maxRecurse = Some(7) (ZN.scala:113,293) */
+/* Z2SFC.ranges (Z2SFC.scala:47-52): Z2.zranges with default maxRecurse = Some(7) (ZN.scala:113,293) */
 int64_t gmo_z2_ranges(int precision, const double* xy, int nxy, int range_precision, int max_ranges,
                       gmo_range* out, int64_t cap) {
   int64_t* zb = (int64_t*)malloc(sizeof(int64_t) * 2 * (size_t)(nxy > 0 ? nxy : 1));

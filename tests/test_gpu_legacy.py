@@ -56,3 +56,18 @@ def test_legacy_z2_index_invert(gpu, oracle, lenient):
     assert np.array_equal(f64_bits(as_np(yi)), f64_bits([r[1] for r in ref]))
     with pytest.raises(IllegalArgumentException):
         LegacyZ2SFC().index([181.0], [0.0])
+
+
+def test_z3_iterator_13_golden_gpu(gpu):
+    """Z3IteratorTest.scala:82-93 on the device: gm_legacy_z3_index of the Z3IndexKeySpaceV4 query's
+    corners decodes to the 1.3 install's golden option strings."""
+    from geomesa_amd.curve import LegacyZ3SFC
+    from geomesa_amd.keyspace import Z3IndexKeySpaceV4
+    from test_host_planning import COMPAT_13_FILTER, COMPAT_13_GOLDEN, z3_dims
+    v = Z3IndexKeySpaceV4().get_index_values(*COMPAT_13_FILTER)
+    (xmin, ymin, xmax, ymax), = v.spatialBounds
+    (t1, t2), = v.temporalBounds[2370]
+    z = as_np(LegacyZ3SFC("week").index([xmin, xmax], [ymin, ymax], [t1, t2]))
+    lo, hi = z3_dims(int(z[0])), z3_dims(int(z[1]))
+    assert "%d:%d:%d:%d" % (lo[0], lo[1], hi[0], hi[1]) == COMPAT_13_GOLDEN["zxy"]
+    assert "2370;%d:%d" % (lo[2], hi[2]) == COMPAT_13_GOLDEN["zt"]

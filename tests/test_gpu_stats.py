@@ -88,7 +88,7 @@ def ms(s):
     return int(datetime.datetime.fromisoformat(s + "+00:00").timestamp() * 1000)
 
 
-def test_z3histogram_reference_kat(gpu):  # Z3HistogramTest.scala:44-51, 108-118 through the host mirror
+def test_z3histogram_reference_kat(gpu):  # Z3HistogramTest.scala:45-52, 95-106 through the host mirror
     from geomesa_amd.stats import Z3Histogram
     i = np.arange(100)
     x = -i.astype(np.float64); y = (i // 2).astype(np.float64)

@@ -67,8 +67,40 @@ def test_z3filter_byte_layout():  # Z3Filter.scala:112-137 (big-endian, null epo
     assert s["zxy"] == "1:2:3:4" and s["zt"] == "5:6,,7:8;9:10" and s["epoch"] == "100:102"
 
 
-def test_z3_iterator_compat_values():  # geomesa-accumulo/.../iterators/Z3IteratorTest.scala:82-93 (modern curve)
-    # the 1.3 golden strings pin week bin 2370 and the during rounding to [+1 s, -1 s]
+COMPAT_13_FILTER = ([(0, -70, 50, -50)], [during(ms("2015-06-06T00:00:00.000Z"), ms("2015-06-08T00:00:00.000Z"))])
+# expected values "taken from a 1.3 install" (geomesa-accumulo/.../iterators/Z3IteratorTest.scala:90-92)
+COMPAT_13_GOLDEN = {"zl": "8", "zo": "2", "zxy": "1048576:233017:1339847:466034", "zt": "2370;299595:599184"}
+
+
+def z3_dims(z):
+    """Z3(z).decode: the three 21-bit components (zorder/sfcurve/Z3.scala:83-91)."""
+    return tuple(sum(((z >> (3 * i + d)) & 1) << i for i in range(21)) for d in range(3))
+
+
+def test_z3_iterator_13_golden():  # Z3IteratorTest.scala:82-93: Z3IndexKeySpaceV4 -> LegacyZ3SFC(week)
+    from geomesa_amd.keyspace import Z3IndexKeySpaceV4
+    v = Z3IndexKeySpaceV4().get_index_values(*COMPAT_13_FILTER)
+    assert F.z3_iterator_options(v, 2, "1.3") == COMPAT_13_GOLDEN
+    with pytest.raises(NotImplementedError):
+        F.z3_iterator_options(v, 2, "1.2")
+
+
+def test_z3_iterator_13_golden_oracle(oracle):
+    """The same strings from the C restatement's LegacyZ3SFC.index (gmo_legacy_z3_index) of the
+    query corners, decoded: pins the oracle's semi-normalized dimensions to the 1.3 golden."""
+    from geomesa_amd.keyspace import Z3IndexKeySpaceV4
+    v = Z3IndexKeySpaceV4().get_index_values(*COMPAT_13_FILTER)
+    (xmin, ymin, xmax, ymax), = v.spatialBounds
+    (t1, t2), = v.temporalBounds[2370]
+    lo = z3_dims(oracle.legacy_z3_index(xmin, ymin, t1)[1])
+    hi = z3_dims(oracle.legacy_z3_index(xmax, ymax, t2)[1])
+    assert "%d:%d:%d:%d" % (lo[0], lo[1], hi[0], hi[1]) == COMPAT_13_GOLDEN["zxy"]
+    assert "2370;%d:%d" % (lo[2], hi[2]) == COMPAT_13_GOLDEN["zt"]
+
+
+def test_z3_iterator_compat_values():  # Z3IteratorTest.scala:82-93's query through the MODERN curve
+    # derived by restatement (SURVEY section 4), not a reference golden: the golden above is the
+    # legacy curve's; these pin only that the modern Z3Filter differs from it as expected
     ks = Z3IndexKeySpace()
     v = ks.get_index_values([(0, -70, 50, -50)], [during(ms("2015-06-06T00:00:00.000Z"),
                                                            ms("2015-06-08T00:00:00.000Z"))])
@@ -76,8 +108,10 @@ def test_z3_iterator_compat_values():  # geomesa-accumulo/.../iterators/Z3Iterat
     assert v.temporalBounds[2370] == [(172801, 345599)]
     f = F.Z3Filter.from_values(v)
     s = F.serialize_to_strings(f)
-    assert s["zxy"] == "1048576:233016:1339847:466033"   # derived for the modern curve
+    assert s["zxy"] == "1048576:233016:1339847:466033"   # derived for the modern curve (not pinned)
     assert s["zt"] == "599189:1198369" and s["epoch"] == "2370:2370"
+    opts = F.z3_iterator_options(v, 0)   # compatibility None: the filter's strings + the row offset
+    assert opts["zo"] == "0" and opts["zxy"] == s["zxy"]
 
 
 # ---------------------------------------------------------------- key layout

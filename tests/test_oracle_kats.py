@@ -169,11 +169,15 @@ def test_calculate_ranges(oracle):  # curve/Z3Test.scala:169-180, curve/Z2Test.s
     assert sorted(r) == sorted([(Z2(2, 2), Z2(3, 3), True), (Z2(2, 4), Z2(3, 5), True), (Z2(2, 6), Z2(3, 6), True)])
 
 
-def z3_test_boxes(O):
-    """The 17 query boxes of curve/Z3Test.scala:188-206 (modern Z3SFC(Week))."""
+def z3_test_boxes(O, legacy=False):
+    """The 17 query boxes of curve/Z3Test.scala:186-203, for Z3SFC(Week) or LegacyZ3SFC(Week) (the
+    test iterates over both, :183)."""
     week = 604800
     day, hour = week // 7, week // 168
-    idx = lambda x, y, t: O.z3_index(float(x), float(y), int(t))[1]  # noqa: E731
+    if legacy:
+        idx = lambda x, y, t: O.legacy_z3_index(float(x), float(y), int(t))[1]  # noqa: E731
+    else:
+        idx = lambda x, y, t: O.z3_index(float(x), float(y), int(t))[1]  # noqa: E731
     b = [
         (idx(-180, -90, 0), idx(180, 90, week)), (idx(-180, -90, day), idx(180, 90, day * 2)),
         (idx(-180, -90, hour * 10), idx(180, 90, hour * 11)), (idx(-180, -90, hour * 10), idx(180, 90, hour * 64)),
@@ -188,21 +192,41 @@ def z3_test_boxes(O):
     return b
 
 
-def test_z3_nonempty_ranges(oracle):  # curve/Z3Test.scala:182-220
-    for r in z3_test_boxes(oracle):
+@pytest.mark.parametrize("legacy", [False, True])
+def test_z3_nonempty_ranges(oracle, legacy):  # curve/Z3Test.scala:182-220
+    for r in z3_test_boxes(oracle, legacy):
         ret = oracle.zranges(3, [r], max_ranges=1000)
         assert 0 < len(ret) <= 1000
 
 
-def test_z2_nonempty_ranges(oracle):  # curve/Z2Test.scala:117-143
-    O = oracle
-    idx = lambda x, y: O.z2_index(float(x), float(y))[1]  # noqa: E731
+def z2_test_boxes(O, legacy=False):
+    """The 10 query boxes of curve/Z2Test.scala:117-143 as Z2SFC (or LegacyZ2SFC) index bounds."""
+    if legacy:
+        idx = lambda x, y: O.legacy_z2_index(float(x), float(y))[1]  # noqa: E731
+    else:
+        idx = lambda x, y: O.z2_index(float(x), float(y))[1]  # noqa: E731
     boxes = [((-180, -90), (180, 90)), ((-90, -45), (90, 45)), ((35, 65), (45, 75)), ((35, 55), (45, 75)),
              ((35, 65), (37, 68)), ((35, 65), (40, 70)), ((39.999, 60.999), (40.001, 61.001)),
              ((51.0, 51.0), (51.1, 51.1)), ((51.0, 51.0), (51.001, 51.001)), ((51.0, 51.0), (51.0000001, 51.0000001))]
-    for a, b in boxes:
-        ret = O.zranges(2, [(idx(*a), idx(*b))], max_ranges=1000)
+    return [(idx(*a), idx(*b)) for a, b in boxes]
+
+
+@pytest.mark.parametrize("legacy", [False, True])
+def test_z2_nonempty_ranges(oracle, legacy):  # curve/Z2Test.scala:117-143 (Z2SFC and LegacyZ2SFC)
+    for r in z2_test_boxes(oracle, legacy):
+        ret = oracle.zranges(2, [r], max_ranges=1000)
         assert 0 < len(ret) <= 1000
+
+
+def test_ranges_wrapped_max_corner(oracle):  # SURVEY Appendix A.4, zorder/sfcurve/package.scala:24
+    """normalize(nextafter(180, 0)) = 2^21 masks to lon cell 0 in Z3.split, so index(min) > index(max)
+    and Z3SFC.ranges' ZRange(min, max) require fails (IllegalArgumentException)."""
+    import numpy as np
+    x = float(np.nextafter(180.0, 0.0))
+    assert oracle.z3_index(170.0, 0.0, 0)[1] > oracle.z3_index(x, 10.0, 100)[1]
+    with pytest.raises(ValueError, match="code 3"):
+        oracle.z3_ranges([(170.0, 0.0, x, 10.0)], [(0, 100)], 64, 2000)
+    assert oracle.z3_ranges([(170.0, 0.0, 179.0, 10.0)], [(0, 100)], 64, 2000)   # the box itself is fine
 
 
 @pytest.mark.parametrize("period", [0, 1, 2, 3])

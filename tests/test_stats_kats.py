@@ -44,7 +44,7 @@ def test_z3histogram_correctly_bins(oracle):  # Z3HistogramTest.scala:44-51
         assert 1 <= counts[0, idx] <= 21
 
 
-def test_z3histogram_clear_and_unobserve(oracle):  # Z3HistogramTest.scala:108-118 ("clear")
+def test_z3histogram_clear_and_unobserve(oracle):  # Z3HistogramTest.scala:95-106 ("clear")
     lo, pres, counts, tally = observe(oracle)
     x, y, t = stat_features()
     oracle.z3_histogram(x, y, t, 1024, lo, 1, unobserve=True, present=pres, counts=counts, tally=tally)
