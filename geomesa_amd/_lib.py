@@ -23,6 +23,8 @@ GM_ST_BAD_TIME = 2
 GM_ST_UNORDERED = 3
 GM_ST_NULL_GEOM = 4
 
+GM_PARAM_JOIN_CHUNK = 1
+
 GM_JOIN_AUTO = 0
 GM_JOIN_DIRECT = 1
 GM_JOIN_PARTITIONED = 2
@@ -75,6 +77,8 @@ SIGNATURES = {
     "gm_ctx_sync": (cint, [vp]),
     "gm_ctx_stream": (vp, [vp]),
     "gm_last_error": (ctypes.c_char_p, []),
+    "gm_ctx_set_param": (cint, [vp, cint, i64]),
+    "gm_ctx_get_param": (cint, [vp, cint, vp]),
     "gm_device_alloc": (cint, [vp, sz, vp]),
     "gm_device_free": (cint, [vp, vp]),
     "gm_copy_to_device": (cint, [vp, vp, vp, sz]),
@@ -176,6 +180,14 @@ class Context:
     @property
     def handle(self):
         return self._h
+
+    def set_param(self, param, value):
+        check(self.lib.gm_ctx_set_param(self._h, int(param), int(value)), "gm_ctx_set_param")
+
+    def get_param(self, param):
+        v = ctypes.c_int64()
+        check(self.lib.gm_ctx_get_param(self._h, int(param), ctypes.byref(v)), "gm_ctx_get_param")
+        return v.value
 
     def sync(self):
         check(self.lib.gm_ctx_sync(self._h), "gm_ctx_sync")

@@ -222,6 +222,27 @@ int gm_ctx_sync(gm_ctx* c) {
 
 void* gm_ctx_stream(gm_ctx* c) { return c ? (void*)c->stream : nullptr; }
 
+int gm_ctx_set_param(gm_ctx* c, int param, int64_t value) {
+  if (!c) return GM_E_INVALID;
+  switch (param) {
+    case GM_PARAM_JOIN_CHUNK:
+      if (value < 0) return GM_E_INVALID;
+      c->join_chunk = value;
+      return GM_OK;
+    default:
+      gm::set_error("gm_ctx_set_param: unknown parameter");
+      return GM_E_INVALID;
+  }
+}
+
+int gm_ctx_get_param(gm_ctx* c, int param, int64_t* value) {
+  if (!c || !value) return GM_E_INVALID;
+  switch (param) {
+    case GM_PARAM_JOIN_CHUNK: *value = c->join_chunk; return GM_OK;
+    default: return GM_E_INVALID;
+  }
+}
+
 int gm_device_alloc(gm_ctx* c, size_t bytes, void** ptr) {
   if (!c || !ptr) return GM_E_INVALID;
   GM_HIP(hipSetDevice(c->device));

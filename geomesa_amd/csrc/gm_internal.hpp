@@ -20,6 +20,7 @@ struct gm_ctx {
   void* ws[4] = {nullptr, nullptr, nullptr, nullptr};   // reusable device workspaces (see ctx_workspace)
   size_t ws_cap[4] = {0, 0, 0, 0};
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  int64_t join_chunk = 0;          // GM_PARAM_JOIN_CHUNK: rows per join pass (0 = each strategy's default)
 };
 
 namespace gm {

@@ -1270,6 +1270,11 @@ static unsigned resident_grid(K kernel, int device, int64_t ntiles, bool xcd_mul
   return (unsigned)g;
 }
 
+// rows per join pass: the strategy's limit, lowered by the context's GM_PARAM_JOIN_CHUNK
+static int64_t join_chunk(const gm_ctx* ctx, int64_t limit) {
+  return ctx->join_chunk > 0 ? std::min<int64_t>(limit, ctx->join_chunk) : limit;
+}
+
 template <bool WRITE, bool REC, bool SPLIT, int SRC = 0>
 static unsigned join_grid(int device, int64_t ntiles) {
   return resident_grid(k_pip_join<WRITE, REC, SPLIT, SRC>, device, ntiles, REC);
@@ -1282,7 +1287,7 @@ static int join_direct_arrow(gm_ctx* ctx, const gm_pip_index* ix, ArrowPts ap, i
   PipDev dv = ix->dev;
   dv.op = op;
   const bool write = pt_ids && poly_ids;
-  const int64_t CHUNK = (int64_t)1 << 31;
+  const int64_t CHUNK = join_chunk(ctx, (int64_t)1 << 31);
   const size_t tb = SRC == 2 ? 8 : 16;
   for (int64_t c0 = 0; c0 < n; c0 += CHUNK) {
     const int64_t m = std::min(CHUNK, n - c0);
@@ -1683,11 +1688,11 @@ int gm_pip_join_pred(gm_ctx* ctx, const gm_pip_index* ix, const double* px, cons
   GM_HIP(hipSetDevice(ctx->device));
   unsigned long long* counter = (unsigned long long*)ctx->d_scratch;
   GM_HIP(hipMemsetAsync(counter, 0, 8, ctx->stream));
-  // AUTO = DIRECT: measured on MI355X (1B CONUS points x 3,200 polygons) the direct pass takes 20 ms,
+  // AUTO = DIRECT at every size: measured on MI355X (1B CONUS points x 3,200 polygons) the direct pass takes 20 ms,
   // against 23 ms for the split pass and 39 ms for partition + join; the others stay
   // selectable
   if ((mode == GM_JOIN_AUTO || mode == GM_JOIN_DIRECT) && n > 0) {
-    const int64_t CHUNK = (int64_t)1 << 31;  // LDS staging keeps 32-bit row offsets
+    const int64_t CHUNK = join_chunk(ctx, (int64_t)1 << 31);  // LDS staging keeps 32-bit row offsets
     for (int64_t c0 = 0; c0 < n; c0 += CHUNK) {
       const int64_t m = std::min(CHUNK, n - c0);
       const int64_t ntiles = (m + JTILE - 1) / JTILE;
@@ -1716,7 +1721,8 @@ int gm_pip_join_pred(gm_ctx* ctx, const gm_pip_index* ix, const double* px, cons
 #define GM_JOIN_WS_GB 6
 #endif
     const int64_t budget = (int64_t)GM_JOIN_WS_GB << 30;
-    int64_t CHUNK = std::min<int64_t>((int64_t)1 << 31, budget / ((per_b + (write ? per_e : 0)) * (int64_t)sizeof(uint2)));
+    int64_t CHUNK = join_chunk(ctx, std::min<int64_t>((int64_t)1 << 31,
+                                                      budget / ((per_b + (write ? per_e : 0)) * (int64_t)sizeof(uint2))));
     CHUNK = std::max<int64_t>(JTILE * 8, CHUNK / (JTILE * 8) * (JTILE * 8));
     const int64_t mmax = std::min(CHUNK, n);
     const int64_t ntiles_max = (mmax + JTILE - 1) / JTILE;
@@ -1769,7 +1775,7 @@ int gm_pip_join_pred(gm_ctx* ctx, const gm_pip_index* ix, const double* px, cons
       }
     }
   } else if (n > 0) {
-    const int64_t CHUNK = (int64_t)1 << 28;  // 6 GiB of band-sorted records per pass
+    const int64_t CHUNK = join_chunk(ctx, (int64_t)1 << 28);  // 6 GiB of band-sorted records per pass
     const int rows_per_band = (ix->dev.gy + NBAND - 1) / NBAND;
     const int nb = (ix->dev.gy + rows_per_band - 1) / rows_per_band;
     const int64_t mmax = std::min(CHUNK, n);

@@ -290,7 +290,7 @@ def scan_rows(row_filter, rows, row_off, key_offset=0, want_ids=False, ids_cap=N
     ctx = _lib.context()
     dev = torch.device("cuda", ctx.device)
     rows = rows.to(dev) if isinstance(rows, torch.Tensor) else torch.from_numpy(
-        np.ascontiguousarray(np.frombuffer(bytes(rows), np.uint8) if isinstance(rows, (bytes, bytearray))
+        np.ascontiguousarray(np.frombuffer(bytes(rows), np.uint8).copy() if isinstance(rows, (bytes, bytearray))
                              else np.asarray(rows, np.uint8))).to(dev)
     if rows.numel() == 0:
         rows = torch.zeros(4, dtype=torch.uint8, device=dev)

@@ -89,6 +89,12 @@ int gm_ctx_destroy(gm_ctx* ctx);
 int gm_ctx_sync(gm_ctx* ctx);
 void* gm_ctx_stream(gm_ctx* ctx);
 const char* gm_last_error(void);
+/* per-context tuning parameters (library defaults when unset) */
+#define GM_PARAM_JOIN_CHUNK 1   /* points per pass of the join strategies (0 = defaults: direct 2^31,
+                                   partitioned 2^28, split sized to its 6 GiB workspace); smaller
+                                   values only add passes -- the pair set never changes */
+int gm_ctx_set_param(gm_ctx* ctx, int param, int64_t value);
+int gm_ctx_get_param(gm_ctx* ctx, int param, int64_t* value);
 /* device memory helpers for callers without their own allocator (e.g. a JNI shim) */
 int gm_device_alloc(gm_ctx* ctx, size_t bytes, void** ptr);
 int gm_device_free(gm_ctx* ctx, void* ptr);
@@ -246,7 +252,7 @@ int gm_pip_join(gm_ctx* ctx, const gm_pip_index* index, const double* px, const 
                 int64_t id_base, int64_t* pt_ids, int32_t* poly_ids, int64_t cap, int64_t* n_pairs);
 
 /* join strategies for gm_pip_join_ex */
-#define GM_JOIN_AUTO 0        /* the faster strategy on MI355X: currently DIRECT */
+#define GM_JOIN_AUTO 0        /* the faster strategy on MI355X: DIRECT */
 #define GM_JOIN_DIRECT 1      /* one pass over the point columns (random index reads) */
 #define GM_JOIN_PARTITIONED 2 /* counting-sort the points by grid-row band first (device temp:
                                  24 B per point, at most 2^28 points per pass), then join band by

@@ -1146,6 +1146,9 @@ typedef struct {
   int32_t* cell_off; int32_t* cell_poly;
   const double* px; const double* py; int64_t lo, hi;
   int64_t* pt; int32_t* pl; int64_t n, cap;
+  int op;                 /* 2 = contains (interior), 1 = intersects (interior or boundary) */
+  const int64_t* pedges;  /* edges per polygon, for the candidate-edge count E_c */
+  int64_t cand_edges;
 } join_task;
 
 static inline int cell_of(double v, double mn, double w, int g) {
@@ -1166,7 +1169,9 @@ static void* join_worker(void* arg) {
       int p = t->cell_poly[k];
       const double* e = t->env + 4 * p;
       if (!(x >= e[0] && x <= e[2] && y >= e[1] && y <= e[3])) continue;
-      if (gmo_locate(t->ps, p, x, y) != LOC_INTERIOR) continue;
+      t->cand_edges += t->pedges[p];
+      const int loc = gmo_locate(t->ps, p, x, y);
+      if (t->op == 1 ? loc == LOC_EXTERIOR : loc != LOC_INTERIOR) continue;
       if (t->n == t->cap) { t->cap = t->cap ? t->cap * 2 : 1024; t->pt = (int64_t*)realloc(t->pt, 8 * (size_t)t->cap); t->pl = (int32_t*)realloc(t->pl, 4 * (size_t)t->cap); }
       t->pt[t->n] = i; t->pl[t->n] = p; t->n++;
     }
@@ -1178,8 +1183,25 @@ static int cmp_i32(const void* a, const void* b) { int32_t x = *(const int32_t*)
 
 int64_t gmo_pip_join(const gmo_polyset* ps, const double* px, const double* py, int64_t n,
                      int64_t* pt_ids, int32_t* poly_ids, int64_t cap, int nthreads) {
+  return gmo_pip_join_ex(ps, px, py, n, pt_ids, poly_ids, cap, nthreads, 2, NULL);
+}
+
+/* The join with the condition's predicate (op 2 = ST_Contains, 1 = ST_Intersects,
+   SpatialRelationFunctions.scala:29-34); *cand_edges (optional) receives E_c = the edges of every
+   (point, polygon) pair whose envelope test passed, i.e. the orientation tests a JTS RayCrossingCounter
+   walk makes over the candidates (the FP64 work of SURVEY 8(d)). */
+int64_t gmo_pip_join_ex(const gmo_polyset* ps, const double* px, const double* py, int64_t n,
+                        int64_t* pt_ids, int32_t* poly_ids, int64_t cap, int nthreads, int op, int64_t* cand_edges) {
   int np = ps->n_polys;
+  if (cand_edges) *cand_edges = 0;
   if (np <= 0 || n <= 0) return 0;
+  int64_t* pedges = (int64_t*)calloc((size_t)np, sizeof(int64_t));
+  for (int p = 0; p < np; p++)
+    for (int q = ps->poly_part_off[p]; q < ps->poly_part_off[p + 1]; q++)
+      for (int r = ps->part_ring_off[q]; r < ps->part_ring_off[q + 1]; r++) {
+        const int nv = ps->ring_vert_off[r + 1] - ps->ring_vert_off[r];
+        pedges[p] += nv > 1 ? nv - 1 : 0;
+      }
   double* env = (double*)malloc(sizeof(double) * 4 * (size_t)np);
   double g[4] = {INFINITY, INFINITY, -INFINITY, -INFINITY};
   for (int p = 0; p < np; p++) {
@@ -1188,7 +1210,7 @@ int64_t gmo_pip_join(const gmo_polyset* ps, const double* px, const double* py, 
     if (env[4 * p] < g[0]) g[0] = env[4 * p]; if (env[4 * p + 1] < g[1]) g[1] = env[4 * p + 1];
     if (env[4 * p + 2] > g[2]) g[2] = env[4 * p + 2]; if (env[4 * p + 3] > g[3]) g[3] = env[4 * p + 3];
   }
-  if (!(g[0] <= g[2])) { free(env); return 0; }
+  if (!(g[0] <= g[2])) { free(env); free(pedges); return 0; }
   int gx = 1, gy = 1;
   while (gx * gy < 4 * np && gx < 1024) { gx *= 2; gy *= 2; }
   double cw = (g[2] - g[0]) / gx, ch = (g[3] - g[1]) / gy;
@@ -1219,7 +1241,7 @@ int64_t gmo_pip_join(const gmo_polyset* ps, const double* px, const double* py, 
   for (int k = 0; k < nthreads; k++) {
     join_task* t = &tasks[k];
     t->ps = ps; t->env = env; t->gx = gx; t->gy = gy; t->minx = g[0]; t->miny = g[1]; t->maxx = g[2]; t->maxy = g[3]; t->cw = cw; t->ch = ch;
-    t->cell_off = cnt; t->cell_poly = cell_poly; t->px = px; t->py = py;
+    t->cell_off = cnt; t->cell_poly = cell_poly; t->px = px; t->py = py; t->op = op; t->pedges = pedges;
     t->lo = (int64_t)k * chunk; t->hi = t->lo + chunk < n ? t->lo + chunk : n; if (t->lo > n) t->lo = n;
     if (nthreads == 1) join_worker(t); else pthread_create(&th[k], NULL, join_worker, t);
   }
@@ -1231,8 +1253,9 @@ int64_t gmo_pip_join(const gmo_polyset* ps, const double* px, const double* py, 
       if (total + j < cap) { pt_ids[total + j] = t->pt[j]; poly_ids[total + j] = t->pl[j]; }
     }
     total += t->n;
+    if (cand_edges) *cand_edges += t->cand_edges;
     free(t->pt); free(t->pl);
   }
-  free(tasks); free(th); free(cell_poly); free(fill); free(cnt); free(env);
+  free(tasks); free(th); free(cell_poly); free(fill); free(cnt); free(env); free(pedges);
   return total <= cap ? total : -total;
 }

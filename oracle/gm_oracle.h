@@ -134,6 +134,8 @@ int64_t gmo_query_scan(const double* x, const double* y, const int64_t* t_ms, in
    sorted by point then poly. returns number of pairs (or -(needed) if cap too small). */
 int64_t gmo_pip_join(const gmo_polyset* ps, const double* px, const double* py, int64_t n,
                      int64_t* pt_ids, int32_t* poly_ids, int64_t cap, int nthreads);
+int64_t gmo_pip_join_ex(const gmo_polyset* ps, const double* px, const double* py, int64_t n,
+                        int64_t* pt_ids, int32_t* poly_ids, int64_t cap, int nthreads, int op, int64_t* cand_edges);
 
 #ifdef __cplusplus
 }

@@ -93,6 +93,7 @@ def lib():
             "gmo_intersects": (ctypes.c_int, [vp, ctypes.c_int, d, d]),
             "gmo_query_scan": (i64, [vp, vp, vp, i64, vp, ctypes.c_int, i64, i64, vp, ctypes.c_int, vp]),
             "gmo_pip_join": (i64, [vp, vp, vp, i64, vp, vp, i64, ctypes.c_int]),
+            "gmo_pip_join_ex": (i64, [vp, vp, vp, i64, vp, vp, i64, ctypes.c_int, ctypes.c_int, vp]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -383,15 +384,21 @@ class OraclePolySet:
     def intersects(self, poly, x, y):
         return bool(lib().gmo_intersects(ctypes.byref(self.c), poly, x, y))
 
-    def join(self, px, py, nthreads=1):
+    def join(self, px, py, nthreads=1, predicate="st_contains", with_edges=False):
+        """(point ids, polygon ids) of the join; with_edges also returns E_c, the candidate edges."""
         px = np.ascontiguousarray(px, np.float64); py = np.ascontiguousarray(py, np.float64)
+        op = {"st_contains": 2, "st_within": 2, "st_intersects": 1, "st_covers": 1}[predicate]
         cap = max(1024, len(px) // 4)
+        ec = ctypes.c_int64()
         while True:
             pt = np.empty(cap, np.int64); pl = np.empty(cap, np.int32)
-            n = lib().gmo_pip_join(ctypes.byref(self.c), _p(px), _p(py), len(px), _p(pt), _p(pl), cap, nthreads)
+            n = lib().gmo_pip_join_ex(ctypes.byref(self.c), _p(px), _p(py), len(px), _p(pt), _p(pl), cap, nthreads,
+                                      op, ctypes.byref(ec))
             if n < 0:
                 cap = -n
                 continue
+            if with_edges:
+                return pt[:n].copy(), pl[:n].copy(), ec.value
             return pt[:n].copy(), pl[:n].copy()
 
 

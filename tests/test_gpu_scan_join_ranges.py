@@ -251,7 +251,7 @@ def test_pip_join_partitioned_edges(gpu, oracle):
 
 
 def test_pip_join_auto_large(gpu, oracle):
-    """Auto mode switches to the partitioned join at 2^22 points; results equal the oracle."""
+    """5M points x 3,200 polygons: auto (= direct at every size) and split equal the oracle."""
     from geomesa_amd.join import PolygonIndex, synthetic_counties, synthetic_points
     ps = synthetic_counties(80, 40)
     ix = PolygonIndex(ps)
