@@ -51,7 +51,7 @@ def test_states_join_parity(gpu, oracle, states, predicate):
         assert np.array_equal(_sorted_pairs(pt, pl), exp), (mode, predicate)
     # a vertex point lies on its own state's boundary: never contained by it; on shared borders it
     # intersects two states
-    n0 = len(px) - 3 * ps.n_vertices
+    n0 = len(px) - (3 * ps.n_vertices - 1)   # first vertex point (after n random points)
     on_vertex = (exp[:, 0] >= n0) & (exp[:, 0] < n0 + ps.n_vertices)
     if predicate == "st_contains":
         ring_of = np.repeat(np.arange(len(ps.ring_vert_off) - 1), np.diff(ps.ring_vert_off))
