@@ -79,33 +79,44 @@ def gather_rows(pg, cols, dst=0):
     return out if pg.get_rank() == dst else None
 
 
-def merge_histograms(pg, counts, present, bin_lo):
+def merge_histograms(pg, counts, present, bin_lo, length=None):
     """Z3Histogram `+=` across ranks (utils/stats/Z3Histogram.scala:145-160): each rank's dense block of
     time-bin rows [bin_lo, bin_lo + rows) is placed into the union window and summed (counts) / OR'd
     (present) with two all-reduces over RCCL (gloo on CPU).  A rank with no histogram passes
     counts=None.  Returns (counts [rows, length], present [rows], bin_lo) of the merged binMap on every
-    rank, or (None, None, None) when every rank is empty."""
+    rank, or (None, None, None) when every rank is empty.
+
+    The reference throws for histograms of different lengths; here every rank learns the min and the
+    max length from scalar all-reduces first and raises together, before any tensor collective (one
+    rank raising alone would leave the others waiting in the all-reduce).  With pg None the input is
+    returned as it is."""
     import torch
+    if pg is None:
+        if counts is None:
+            return None, None, None
+        return counts, present, bin_lo
     dev = _device_of(pg)
     big = float(1 << 20)
-    lo = float(bin_lo) if counts is not None else big
-    hi = float(bin_lo + counts.shape[0] - 1) if counts is not None else -big
-    lo, hi = all_reduce_scalar(pg, -lo, "max"), all_reduce_scalar(pg, hi, "max")
-    lo = -lo
+    have = counts is not None
+    lo = float(bin_lo) if have else big
+    hi = float(bin_lo + counts.shape[0] - 1) if have else -big
+    ln = float(counts.shape[1]) if have else float(length or 0)
+    lo, hi = -all_reduce_scalar(pg, -lo, "max"), all_reduce_scalar(pg, hi, "max")
+    len_max = all_reduce_scalar(pg, ln if have else -big, "max")
+    len_min = -all_reduce_scalar(pg, -ln if have else -big, "max")
     if hi < lo:
         return None, None, None
-    length = int(all_reduce_scalar(pg, counts.shape[1] if counts is not None else 0, "max"))
+    if len_max != len_min:
+        raise NotImplementedError("Can only add z3 histograms with the same length")
+    length = int(len_max)
     lo, hi = int(lo), int(hi)
     rows = hi - lo + 1
     c = torch.zeros((rows, length), dtype=torch.int64, device=dev)
     p = torch.zeros(rows, dtype=torch.int64, device=dev)   # int64: gloo has no uint8 MAX on every build
-    if counts is not None:
-        if counts.shape[1] != length:
-            raise NotImplementedError("Can only add z3 histograms with the same length")
+    if have:
         off = bin_lo - lo
         c[off:off + counts.shape[0]] = counts.to(dev) * (present.to(dev) != 0).to(torch.int64).unsqueeze(1)
         p[off:off + counts.shape[0]] = present.to(dev).to(torch.int64)
-    if pg is not None:
-        pg.all_reduce(c, op=pg.ReduceOp.SUM)
-        pg.all_reduce(p, op=pg.ReduceOp.MAX)
+    pg.all_reduce(c, op=pg.ReduceOp.SUM)
+    pg.all_reduce(p, op=pg.ReduceOp.MAX)
     return c, (p != 0).to(torch.uint8), lo

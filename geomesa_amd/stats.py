@@ -94,18 +94,27 @@ class Z3Histogram:
             self._run(x, y, t, True, self.counts, self.present, tally)
             self.skipped += int(tally[0])
             return
-        scratch = torch.zeros_like(self.counts)
-        pres = torch.zeros_like(self.present)
-        self._run(x, y, t, False, scratch, pres, tally)
-        if int(tally[1]) > 0:   # features beyond the window: widen and redo this batch
-            self._cover(t)
-            scratch = torch.zeros_like(self.counts)
-            pres = torch.zeros_like(self.present)
-            tally.zero_()
-            self._run(x, y, t, False, scratch, pres, tally)
-        self.counts += scratch
-        self.present |= pres
+        # straight into the binMap block: features of bins outside the window are left out and
+        # counted in tally[1] (no per-batch scratch block)
+        self._run(x, y, t, False, self.counts, self.present, tally)
         self.skipped += int(tally[0])
+        if int(tally[1]) > 0:
+            # widen to the batch's bins, then add only the features of the new rows: the rows below
+            # and above the old window are contiguous row blocks of the dense counts
+            lo0, hi0 = self.bin_lo, self.bin_lo + self.n_bins   # [lo0, hi0)
+            self._cover(t)
+            extra = torch.zeros(2, dtype=torch.int64, device=x.device)
+            below, above = lo0 - self.bin_lo, self.bin_lo + self.n_bins - hi0
+            if below > 0:
+                self._run_rows(x, y, t, self.bin_lo, 0, below, extra)
+            if above > 0:
+                self._run_rows(x, y, t, hi0, hi0 - self.bin_lo, above, extra)
+
+    def _run_rows(self, x, y, t, bin_lo, row0, rows, tally):
+        ctx = _lib.context(self._device)
+        check(ctx.lib.gm_z3_histogram(ctx.handle, ptr(x), ptr(y), ptr(t), x.numel(), self.period, self.length, 0,
+                                      bin_lo, rows, ptr(self.present[row0:row0 + rows]),
+                                      ptr(self.counts[row0:row0 + rows]), ptr(tally)), "gm_z3_histogram")
 
     # ------------------------------------------------------------------ Stat API
     def observe(self, x, y, t_ms):
@@ -186,11 +195,16 @@ class Z3Histogram:
         return out
 
     def all_reduce(self, pg):
-        """Merge this rank's histogram with every other rank's (`+=` over the process group, RCCL)."""
+        """Merge this rank's histogram with every other rank's (`+=` over the process group, RCCL).
+        The merged block comes back on this histogram's device whatever the backend's transport
+        device (gloo reduces on the CPU)."""
         from .shard import merge_histograms
-        c, p, lo = merge_histograms(pg, self.counts, self.present, self.bin_lo)
+        c, p, lo = merge_histograms(pg, self.counts, self.present, self.bin_lo, self.length)
         if c is not None:
-            self.counts, self.present, self.bin_lo, self.n_bins = c, p, lo, c.shape[0]
+            torch = _torch()
+            dev = torch.device("cuda", _lib.context(self._device).device)
+            self.counts, self.present = c.to(dev).contiguous(), p.to(dev).contiguous()
+            self.bin_lo, self.n_bins = lo, c.shape[0]
         return self
 
     def split_by_time(self):

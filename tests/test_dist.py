@@ -147,3 +147,57 @@ def test_sharded_histogram_merge_equals_global(oracle):
     pres, counts, tally = oracle.z3_histogram(x, y, t, 64, mlo, c.shape[0])
     assert tally.tolist() == [1, 0]
     assert np.array_equal(c, counts) and np.array_equal(p, pres)
+
+
+def _hist_mismatch_worker(rank, world, port, q):
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import torch
+        from geomesa_amd.shard import merge_histograms
+        length = 64 if rank == 0 else 32          # Z3Histogram += of different lengths throws
+        counts = torch.ones((3, length), dtype=torch.int64)
+        pres = torch.ones(3, dtype=torch.uint8)
+        try:
+            merge_histograms(dist, counts, pres, 2600 + rank)
+            q.put((rank, "no error"))
+        except NotImplementedError as e:
+            q.put((rank, str(e)))
+        # the group is still usable: no rank is left inside a collective
+        t = torch.tensor([rank + 1.0])
+        dist.all_reduce(t)
+        q.put((rank, float(t.item())))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_histogram_merge_length_mismatch_raises_on_every_rank():
+    """the length check happens on every rank before any tensor collective."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_hist_mismatch_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=240) for _ in range(2 * world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    msgs = sorted(m for m in got if isinstance(m[1], str))
+    sums = [m for m in got if not isinstance(m[1], str)]
+    assert msgs == [(0, "Can only add z3 histograms with the same length"),
+                    (1, "Can only add z3 histograms with the same length")]
+    assert sorted(s[1] for s in sums) == [3.0, 3.0]
+
+
+def test_merge_histograms_without_group():
+    import torch
+    from geomesa_amd.shard import merge_histograms
+    c, p = torch.arange(6, dtype=torch.int64).reshape(2, 3), torch.tensor([1, 0], dtype=torch.uint8)
+    rc, rp, lo = merge_histograms(None, c, p, 2600)
+    assert rc is c and rp is p and lo == 2600
+    assert merge_histograms(None, None, None, None) == (None, None, None)

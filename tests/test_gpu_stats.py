@@ -128,3 +128,46 @@ def test_z3histogram_window_grows(gpu, oracle):
     parts = h.split_by_time()
     assert sum(int(p.counts.sum()) for _, p in parts) == 50_000
     assert T2020 < T2021
+
+
+def test_z3histogram_window_grows_both_sides(gpu, oracle):
+    """A batch with features below, inside and above the window: the in-window features go straight
+    into the binMap block, the others into the rows the window gains on each side."""
+    from geomesa_amd.stats import Z3Histogram
+    x, y, t = random_points(60_000)
+    wk = 604800000
+    h = Z3Histogram(period="week", length=128)
+    h.observe(x[:20_000], y[:20_000], t[:20_000] + 20 * wk)
+    t2 = t[20_000:].copy()
+    t2[::3] += 45 * wk                     # above the window
+    t2[1::3] += 20 * wk                    # inside
+    h.observe(x[20_000:], y[20_000:], t2)  # the rest below it
+    tt = np.concatenate([t[:20_000] + 20 * wk, t2])
+    op, oc, ot = oracle.z3_histogram(x, y, tt, 128, h.bin_lo, h.n_bins)
+    assert ot.tolist() == [0, 0] and h.skipped == 0
+    assert np.array_equal(h.counts.cpu().numpy(), oc) and np.array_equal(h.present.cpu().numpy(), op)
+
+
+def test_z3histogram_all_reduce_then_observe(gpu, oracle):
+    """all_reduce over a gloo group (CPU transport) hands the merged block back on the
+    histogram's device, so the next observe runs on device memory."""
+    import os
+    import socket
+    import torch.distributed as dist
+    from geomesa_amd.stats import Z3Histogram
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = "127.0.0.1", str(port)
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        x, y, t = random_points(40_000)
+        h = Z3Histogram(period="week", length=64)
+        h.observe(x[:20_000], y[:20_000], t[:20_000])
+        h.all_reduce(dist)
+        assert h.counts.is_cuda and h.present.is_cuda
+        h.observe(x[20_000:], y[20_000:], t[20_000:])
+        op, oc, ot = oracle.z3_histogram(x, y, t, 64, h.bin_lo, h.n_bins)
+        assert np.array_equal(h.counts.cpu().numpy(), oc) and np.array_equal(h.present.cpu().numpy(), op)
+    finally:
+        dist.destroy_process_group()
