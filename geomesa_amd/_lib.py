@@ -61,6 +61,16 @@ class PolySetC(ctypes.Structure):
                 ("ring_vert_off", ctypes.c_void_p), ("vx", ctypes.c_void_p), ("vy", ctypes.c_void_p)]
 
 
+GM_PIP_INDEX_ARRAYS = 8
+GM_PIP_LAYOUT_VERSION = 1
+
+
+class PipIndexLayout(ctypes.Structure):
+    _fields_ = [("version", ctypes.c_int32), ("dims", ctypes.c_int32 * 4), ("reserved", ctypes.c_int32),
+                ("grid", ctypes.c_double * 6), ("stats", ctypes.c_int64 * 9),
+                ("bytes", ctypes.c_int64 * GM_PIP_INDEX_ARRAYS)]
+
+
 vp = ctypes.c_void_p
 i64 = ctypes.c_int64
 i32 = ctypes.c_int32
@@ -108,6 +118,9 @@ SIGNATURES = {
     "gm_pip_index_create_ex": (cint, [vp, vp, cint, vp]),
     "gm_pip_index_destroy": (cint, [vp]),
     "gm_pip_index_stats": (cint, [vp, vp]),
+    "gm_pip_index_export": (cint, [vp, vp]),
+    "gm_pip_index_copy_array": (cint, [vp, vp, cint, vp]),
+    "gm_pip_index_import": (cint, [vp, vp, vp, vp]),
     "gm_pip_join": (cint, [vp, vp, vp, vp, i64, i64, vp, vp, i64, vp]),
     "gm_pip_join_ex": (cint, [vp, vp, vp, vp, i64, i64, vp, vp, i64, vp, cint]),
     "gm_pip_join_pred": (cint, [vp, vp, vp, vp, i64, i64, vp, vp, i64, vp, cint, cint]),

@@ -28,9 +28,12 @@
 #include <string.h>
 
 #include <algorithm>
-#include <vector>
+#include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <thread>
+#include <vector>
 
 #include "gm_arrow.hpp"
 #include "gm_scan.hpp"
@@ -1200,19 +1203,41 @@ struct gm_pip_index {
   int64_t max_bnd_per_cell = 0;   // most BOUNDARY (cell, polygon) entries of any cell: work items per point
   int64_t max_ent_per_cell = 0;   // most (cell, polygon) entries of any cell: pairs per point
   const int32_t* list_poly = nullptr;   // polygon of each list_ent slot (the row-wise predicate's list search)
+  const void* arr[GM_PIP_INDEX_ARRAYS] = {};   // the device arrays in gm_pip_index_layout order
+  int64_t arr_bytes[GM_PIP_INDEX_ARRAYS] = {};
 };
 
 using namespace gm;
 
 namespace {
 
+// device array k of the index (gm_pip_index_layout order): rings, slab_off, slab_edges, cell_word,
+// coarse_word, compact, list_ent, blob
 template <class T>
-int upload(gm_pip_index* ix, const std::vector<T>& v, const T** out) {
+int upload(gm_pip_index* ix, int k, const std::vector<T>& v, const T** out) {
   void* p = nullptr;
-  GM_HIP(hipMalloc(&p, std::max<size_t>(v.size() * sizeof(T), 16)));
+  const size_t bytes = v.size() * sizeof(T);
+  GM_HIP(hipMalloc(&p, std::max<size_t>(bytes, 16)));
   ix->allocs.push_back(p);
+  ix->arr[k] = p;
+  ix->arr_bytes[k] = (int64_t)bytes;
   *out = (const T*)p;
-  return v.empty() ? GM_OK : copy_h2d(ix->ctx, p, v.data(), v.size() * sizeof(T));
+  return v.empty() ? GM_OK : copy_h2d(ix->ctx, p, v.data(), bytes);
+}
+
+// the row-wise predicate's polygon per list slot (derived on the device)
+int make_list_poly(gm_pip_index* ix) {
+  const int64_t ns = ix->arr_bytes[6] / 4;
+  void* lp = nullptr;
+  GM_HIP(hipMalloc(&lp, (size_t)std::max<int64_t>(ns, 4) * 4));
+  ix->allocs.push_back(lp);
+  ix->list_poly = (const int32_t*)lp;
+  if (ns > 0) {
+    hipLaunchKernelGGL(k_list_poly, dim3((unsigned)((ns + RTPB - 1) / RTPB)), dim3(RTPB), 0, ix->ctx->stream, ix->dev, ns,
+                       (int32_t*)lp);
+    GM_CHECK_LAUNCH();
+  }
+  return GM_OK;
 }
 
 struct BandSeg {
@@ -1249,6 +1274,21 @@ uint64_t right_parity(const std::vector<const BandSeg*>& right, double yb0,
     if (c & 1) parity |= 1ull << j;
   }
   return parity;
+}
+
+// host threads of the index build: GM_BUILD_THREADS, else OMP_NUM_THREADS (16 on the GPU boxes),
+// else the machine's, at most 64
+int build_threads() {
+  for (const char* v : {"GM_BUILD_THREADS", "OMP_NUM_THREADS"}) {
+    const char* s = getenv(v);
+    if (s && atoi(s) > 0) return std::min(64, atoi(s));
+  }
+  const unsigned hc = std::thread::hardware_concurrency();
+  return (int)std::max(1u, std::min(64u, hc ? hc : 1u));
+}
+
+double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
 }  // namespace
@@ -1317,6 +1357,7 @@ int gm_pip_index_create(gm_ctx* ctx, const gm_polyset* ps, gm_pip_index** out) {
 int gm_pip_index_create_ex(gm_ctx* ctx, const gm_polyset* ps, int cells_per_poly_in, gm_pip_index** out) {
   if (!ctx || !ps || !out || ps->n_polys < 0 || cells_per_poly_in < 0) return GM_E_INVALID;
   *out = nullptr;
+  const double t_start = now_s();
   const int P = ps->n_polys;
   if (P > 0 && (!ps->poly_part_off || !ps->part_ring_off || !ps->ring_vert_off)) return GM_E_INVALID;
   const int n_parts = P ? ps->poly_part_off[P] : 0;
@@ -1396,168 +1437,208 @@ int gm_pip_index_create_ex(gm_ctx* ctx, const gm_polyset* ps, int cells_per_poly
   const double epsx = W > 0 ? W * 1e-9 : 1e-9, epsy = H > 0 ? H * 1e-9 : 1e-9;
   const int64_t ncell = (int64_t)gx * gy;
 
-  // ---- (cell, polygon) classification + boundary blobs
+  // ---- (cell, polygon) classification + boundary blobs, in parallel over chunks of polygons.  A
+  // chunk's entries carry chunk-local blob / compact offsets; the chunks are concatenated in polygon
+  // order afterwards (so cell lists keep polygons ascending) and the offsets rebased.
   struct Ent { int64_t cell; uint32_t e; };
-  std::vector<Ent> ents;
-  std::vector<int32_t> per_cell((size_t)ncell, 0), bnd_cell((size_t)ncell, 0);
-  std::vector<double> blob;            // 8-byte words; each blob starts 16-byte aligned
-  auto put_i32x2 = [&](int32_t a, int32_t b) {
-    double w; int32_t v[2] = {a, b}; memcpy(&w, v, 8); blob.push_back(w);
+  struct ChunkOut {
+    std::vector<Ent> ents;
+    std::vector<double> blob;      // 8-byte words; each blob starts 16-byte aligned (even length kept)
+    std::vector<double> compact;   // 16-word (128-B) compact blobs
+    int64_t n_slow = 0, n_boundary = 0, n_records = 0, n_compact = 0;
   };
-  auto put_u64 = [&](uint64_t u) { double w; memcpy(&w, &u, 8); blob.push_back(w); };
-  int64_t n_slow = 0, n_boundary = 0, n_records = 0, n_compact = 0;
-  std::vector<double> compact;         // 16-word (128-B) compact blobs
-  const bool dbg = getenv("GM_PIP_DEBUG") != nullptr;
-  std::vector<int64_t> dbg_hist(16 * 64, 0);
+  constexpr int PCH = 4;   // polygons per work item
+  const int nchunks = (P + PCH - 1) / PCH;
+  std::vector<ChunkOut> outs((size_t)std::max(nchunks, 1));
+  std::atomic<int> next_chunk{0};
   struct RingRef { int32_t ring; bool shell; };
-  std::vector<RingRef> ring_list;
-  std::vector<std::vector<BandSeg>> band;  // per ring of the polygon, segments meeting the row band
-  std::vector<int32_t> a_edges;
-  std::vector<const BandSeg*> right;
-  std::vector<std::pair<double, int32_t>> bk;
-  for (int p = 0; p < P && any; ++p) {
-    const double* e = &env[4 * (size_t)p];
-    if (!(e[0] <= e[2])) continue;
-    ring_list.clear();
-    for (int q = ps->poly_part_off[p]; q < ps->poly_part_off[p + 1]; ++q)
-      for (int r = ps->part_ring_off[q]; r < ps->part_ring_off[q + 1]; ++r)
-        ring_list.push_back(RingRef{r, r == ps->part_ring_off[q]});
-    const int nr = (int)ring_list.size();
-    band.assign((size_t)nr, {});
-    const int cx0 = host::cell_of(e[0], G[0], inv_cw, gx), cx1 = host::cell_of(e[2], G[0], inv_cw, gx);
-    const int cy0 = host::cell_of(e[1], G[1], inv_ch, gy), cy1 = host::cell_of(e[3], G[1], inv_ch, gy);
-    for (int cy = cy0; cy <= cy1; ++cy) {
-      const double yb0 = degenerate ? -INFINITY : G[1] + (double)cy / inv_ch - epsy;
-      const double yb1 = degenerate ? INFINITY : G[1] + (double)(cy + 1) / inv_ch + epsy;
-      for (int k = 0; k < nr; ++k) {
-        band[k].clear();
-        const int r = ring_list[k].ring;
-        for (int i = ps->ring_vert_off[r] + 1; i < ps->ring_vert_off[r + 1]; ++i) {
-          const double ya = vy[i - 1], yb = vy[i];
-          const double ymin = std::min(ya, yb), ymax = std::max(ya, yb);
-          if (ymax < yb0 || ymin > yb1) continue;
-          band[k].push_back(BandSeg{i, std::min(vx[i - 1], vx[i]), std::max(vx[i - 1], vx[i]), ymin, ymax,
-                                    ya <= yb ? i - 1 : i, ya <= yb ? i : i - 1});
+  auto classify = [&]() {
+    std::vector<RingRef> ring_list;
+    std::vector<std::vector<BandSeg>> band;  // per ring of the polygon, segments meeting the row band
+    std::vector<int32_t> a_edges;
+    std::vector<const BandSeg*> right;
+    std::vector<std::pair<double, int32_t>> bk;
+    for (;;) {
+      const int ch = next_chunk.fetch_add(1);
+      if (ch >= nchunks || !any) break;
+      ChunkOut& o = outs[(size_t)ch];
+      std::vector<Ent>& ents = o.ents;
+      std::vector<double>& blob = o.blob;
+      std::vector<double>& compact = o.compact;
+      auto put_i32x2 = [&](int32_t a, int32_t b) {
+        double w; int32_t v[2] = {a, b}; memcpy(&w, v, 8); blob.push_back(w);
+      };
+      auto put_u64 = [&](uint64_t u) { double w; memcpy(&w, &u, 8); blob.push_back(w); };
+      for (int p = ch * PCH; p < std::min(P, (ch + 1) * PCH); ++p) {
+        const double* e = &env[4 * (size_t)p];
+        if (!(e[0] <= e[2])) continue;
+        ring_list.clear();
+        for (int q = ps->poly_part_off[p]; q < ps->poly_part_off[p + 1]; ++q)
+          for (int r = ps->part_ring_off[q]; r < ps->part_ring_off[q + 1]; ++r)
+            ring_list.push_back(RingRef{r, r == ps->part_ring_off[q]});
+        const int nr = (int)ring_list.size();
+        band.resize((size_t)nr);
+        const int cx0 = host::cell_of(e[0], G[0], inv_cw, gx), cx1 = host::cell_of(e[2], G[0], inv_cw, gx);
+        const int cy0 = host::cell_of(e[1], G[1], inv_ch, gy), cy1 = host::cell_of(e[3], G[1], inv_ch, gy);
+        for (int cy = cy0; cy <= cy1; ++cy) {
+          const double yb0 = degenerate ? -INFINITY : G[1] + (double)cy / inv_ch - epsy;
+          const double yb1 = degenerate ? INFINITY : G[1] + (double)(cy + 1) / inv_ch + epsy;
+          for (int k = 0; k < nr; ++k) {
+            band[k].clear();
+            const int r = ring_list[k].ring;
+            for (int i = ps->ring_vert_off[r] + 1; i < ps->ring_vert_off[r + 1]; ++i) {
+              const double ya = vy[i - 1], yb = vy[i];
+              const double ymin = std::min(ya, yb), ymax = std::max(ya, yb);
+              if (ymax < yb0 || ymin > yb1) continue;
+              band[k].push_back(BandSeg{i, std::min(vx[i - 1], vx[i]), std::max(vx[i - 1], vx[i]), ymin, ymax,
+                                        ya <= yb ? i - 1 : i, ya <= yb ? i : i - 1});
+            }
+          }
+          int run_loc = -1;
+          for (int cx = cx0; cx <= cx1; ++cx) {
+            const int64_t cell = (int64_t)cy * gx + cx;
+            const double xb0 = degenerate ? -INFINITY : G[0] + (double)cx / inv_cw - epsx;
+            const double xb1 = degenerate ? INFINITY : G[0] + (double)(cx + 1) / inv_cw + epsx;
+            bool bnd = degenerate;
+            for (int k = 0; k < nr && !bnd; ++k)
+              for (const BandSeg& sg : band[k])
+                if (sg.maxx >= xb0 && sg.minx <= xb1) { bnd = true; break; }
+            if (!bnd) {
+              if (run_loc < 0) {
+                // any point of the cell: its nominal centre, checked to map back to the cell
+                const double cxm = G[0] + ((double)cx + 0.5) / inv_cw;
+                const double cym = G[1] + ((double)cy + 0.5) / inv_ch;
+                if (host::cell_of(cxm, G[0], inv_cw, gx) != cx || host::cell_of(cym, G[1], inv_ch, gy) != cy) bnd = true;
+                else run_loc = host::locate_poly(ps, p, cxm, cym);
+              }
+              if (!bnd) {
+                if (run_loc == LOC_EXTERIOR) continue;
+                if (run_loc == LOC_INTERIOR) {
+                  ents.push_back(Ent{cell, (CELL_INTERIOR << 30) | (uint32_t)p});
+                  continue;
+                }
+                bnd = true;  // a boundary location cannot occur in a segment-free cell; stay exact anyway
+              }
+            }
+            run_loc = -1;
+            // ---- compact blob: single-ring polygon, <= 2 segments, <= 4 breakpoints -> one 128-B line
+            if (nr == 1 && !degenerate) {
+              a_edges.clear(); right.clear(); bk.clear();
+              for (const BandSeg& sg : band[0]) {
+                if (sg.maxx >= xb0 && sg.minx <= xb1) a_edges.push_back(sg.seg);
+                else if (sg.minx > xb1) right.push_back(&sg);
+              }
+              collect_breakpoints(right, yb0, yb1, bk);
+              if (4 * a_edges.size() + bk.size() <= 30) {
+                const int E = (int)a_edges.size(), B = (int)bk.size();
+                const int lines = (4 * E + B <= 14 && E <= 3) ? 1 : 2;
+                const uint64_t ci = compact.size() / 16;   // chunk-local line index
+                double rec[32];
+                for (double& w : rec) w = INFINITY;
+                { int32_t v[2] = {p, E | (lines << 8)}; memcpy(&rec[0], v, 8); }
+                { const uint64_t par = right_parity(right, yb0, bk); memcpy(&rec[1], &par, 8); }
+                bool used[32] = {};
+                used[0] = used[1] = true;
+                for (int j = 0; j < E; ++j) {
+                  const int32_t i = a_edges[j];
+                  double* eg = rec + cseg_word(j);
+                  eg[0] = vx[i]; eg[1] = vy[i]; eg[2] = vx[i - 1]; eg[3] = vy[i - 1];
+                  for (int q = 0; q < 4; ++q) used[cseg_word(j) + q] = true;
+                }
+                int w = 2;
+                for (int j = 0; j < B; ++j) {
+                  while (used[w]) ++w;
+                  rec[w] = bk[j].first;
+                  used[w] = true;
+                }
+                compact.insert(compact.end(), rec, rec + 16 * lines);
+                o.n_boundary++;
+                o.n_compact++;
+                ents.push_back(Ent{cell, (CELL_BOUNDARY << 30) | BLOB_COMPACT | (uint32_t)ci});
+                continue;
+              }
+            }
+            // ---- boundary blob
+            if (blob.size() & 1) blob.push_back(0.0);
+            const uint64_t boff = blob.size() / 2;   // chunk-local, 16-B units
+            put_i32x2(p, nr);
+            for (int k = 0; k < nr; ++k) {
+              a_edges.clear(); right.clear(); bk.clear();
+              for (const BandSeg& sg : band[k]) {
+                if (sg.maxx >= xb0 && sg.minx <= xb1) a_edges.push_back(sg.seg);
+                else if (sg.minx > xb1) right.push_back(&sg);
+              }
+              collect_breakpoints(right, yb0, yb1, bk);
+              const int r = ring_list[k].ring;
+              const bool slow = degenerate || a_edges.size() > 4096 || bk.size() > 63;
+              RingHdr rh{};
+              rh.flags = (int16_t)((ring_list[k].shell ? 1 : 0) | (slow ? 2 : 0));
+              rh.n_edge = slow ? 0 : (int16_t)a_edges.size();
+              rh.n_brk = slow ? 0 : (int16_t)bk.size();
+              { double w; memcpy(&w, &rh, 8); blob.push_back(w); }
+              uint64_t parity = 0;
+              if (!slow) {
+                parity = right_parity(right, yb0, bk);
+              } else {
+                o.n_slow++;
+                parity = (uint32_t)r;
+              }
+              put_u64(parity);
+              if (!slow) {
+                for (int32_t i : a_edges) {
+                  blob.push_back(vx[i]); blob.push_back(vy[i]); blob.push_back(vx[i - 1]); blob.push_back(vy[i - 1]);
+                }
+                for (auto& b : bk) blob.push_back(b.first);
+              }
+              o.n_records++;
+            }
+            o.n_boundary++;
+            ents.push_back(Ent{cell, (CELL_BOUNDARY << 30) | (uint32_t)boff});
+          }
         }
       }
-      int run_loc = -1;
-      for (int cx = cx0; cx <= cx1; ++cx) {
-        const int64_t cell = (int64_t)cy * gx + cx;
-        const double xb0 = degenerate ? -INFINITY : G[0] + (double)cx / inv_cw - epsx;
-        const double xb1 = degenerate ? INFINITY : G[0] + (double)(cx + 1) / inv_cw + epsx;
-        bool bnd = degenerate;
-        for (int k = 0; k < nr && !bnd; ++k)
-          for (const BandSeg& sg : band[k])
-            if (sg.maxx >= xb0 && sg.minx <= xb1) { bnd = true; break; }
-        if (!bnd) {
-          if (run_loc < 0) {
-            // any point of the cell: its nominal centre, checked to map back to the cell
-            const double cxm = G[0] + ((double)cx + 0.5) / inv_cw;
-            const double cym = G[1] + ((double)cy + 0.5) / inv_ch;
-            if (host::cell_of(cxm, G[0], inv_cw, gx) != cx || host::cell_of(cym, G[1], inv_ch, gy) != cy) bnd = true;
-            else run_loc = host::locate_poly(ps, p, cxm, cym);
-          }
-          if (!bnd) {
-            if (run_loc == LOC_EXTERIOR) continue;
-            if (run_loc == LOC_INTERIOR) {
-              ents.push_back(Ent{cell, (CELL_INTERIOR << 30) | (uint32_t)p});
-              per_cell[cell]++;
-              continue;
-            }
-            bnd = true;  // a boundary location cannot occur in a segment-free cell; stay exact anyway
-          }
-        }
-        run_loc = -1;
-        // ---- compact blob: single-ring polygon, <= 2 segments, <= 4 breakpoints -> one 128-B line
-        if (nr == 1 && !degenerate) {
-          a_edges.clear(); right.clear(); bk.clear();
-          for (const BandSeg& sg : band[0]) {
-            if (sg.maxx >= xb0 && sg.minx <= xb1) a_edges.push_back(sg.seg);
-            else if (sg.minx > xb1) right.push_back(&sg);
-          }
-          collect_breakpoints(right, yb0, yb1, bk);
-          if (dbg) dbg_hist[std::min<size_t>(a_edges.size(), 15) * 64 + std::min<size_t>(bk.size(), 63)]++;
-          if (4 * a_edges.size() + bk.size() <= 30) {
-            const int E = (int)a_edges.size(), B = (int)bk.size();
-            const int lines = (4 * E + B <= 14 && E <= 3) ? 1 : 2;
-            const uint64_t ci = compact.size() / 16;
-            if (ci + lines >= (1u << 29)) { gm::set_error("gm_pip_index_create: too many compact blobs"); return GM_E_CAPACITY; }
-            double rec[32];
-            for (double& w : rec) w = INFINITY;
-            { int32_t v[2] = {p, E | (lines << 8)}; memcpy(&rec[0], v, 8); }
-            { const uint64_t par = right_parity(right, yb0, bk); memcpy(&rec[1], &par, 8); }
-            bool used[32] = {};
-            used[0] = used[1] = true;
-            for (int j = 0; j < E; ++j) {
-              const int32_t i = a_edges[j];
-              double* eg = rec + cseg_word(j);
-              eg[0] = vx[i]; eg[1] = vy[i]; eg[2] = vx[i - 1]; eg[3] = vy[i - 1];
-              for (int q = 0; q < 4; ++q) used[cseg_word(j) + q] = true;
-            }
-            int w = 2;
-            for (int j = 0; j < B; ++j) {
-              while (used[w]) ++w;
-              rec[w] = bk[j].first;
-              used[w] = true;
-            }
-            if (w >= 16 * lines) { gm::set_error("gm_pip_index_create: compact layout"); return GM_E_INVALID; }
-            compact.insert(compact.end(), rec, rec + 16 * lines);
-            n_boundary++;
-            n_compact++;
-            ents.push_back(Ent{cell, (CELL_BOUNDARY << 30) | BLOB_COMPACT | (uint32_t)ci});
-            per_cell[cell]++;
-            bnd_cell[cell]++;
-            continue;
-          }
-        }
-        // ---- boundary blob
-        if (blob.size() & 1) blob.push_back(0.0);
-        const uint64_t boff = blob.size() / 2;
-        if (boff >= (1u << 30)) { gm::set_error("gm_pip_index_create: boundary blob too large"); return GM_E_CAPACITY; }
-        put_i32x2(p, nr);
-        for (int k = 0; k < nr; ++k) {
-          a_edges.clear(); right.clear(); bk.clear();
-          for (const BandSeg& sg : band[k]) {
-            if (sg.maxx >= xb0 && sg.minx <= xb1) a_edges.push_back(sg.seg);
-            else if (sg.minx > xb1) right.push_back(&sg);
-          }
-          collect_breakpoints(right, yb0, yb1, bk);
-          const int r = ring_list[k].ring;
-          const bool slow = degenerate || a_edges.size() > 4096 || bk.size() > 63;
-          RingHdr rh{};
-          rh.flags = (int16_t)((ring_list[k].shell ? 1 : 0) | (slow ? 2 : 0));
-          rh.n_edge = slow ? 0 : (int16_t)a_edges.size();
-          rh.n_brk = slow ? 0 : (int16_t)bk.size();
-          { double w; memcpy(&w, &rh, 8); blob.push_back(w); }
-          uint64_t parity = 0;
-          if (!slow) {
-            parity = right_parity(right, yb0, bk);
-          } else {
-            n_slow++;
-            parity = (uint32_t)r;
-          }
-          put_u64(parity);
-          if (!slow) {
-            for (int32_t i : a_edges) {
-              blob.push_back(vx[i]); blob.push_back(vy[i]); blob.push_back(vx[i - 1]); blob.push_back(vy[i - 1]);
-            }
-            for (auto& b : bk) blob.push_back(b.first);
-          }
-          n_records++;
-        }
-        n_boundary++;
-        ents.push_back(Ent{cell, (CELL_BOUNDARY << 30) | (uint32_t)boff});
-        per_cell[cell]++;
-        bnd_cell[cell]++;
+      if (blob.size() & 1) blob.push_back(0.0);
+    }
+  };
+  {
+    const int nth = std::max(1, std::min(build_threads(), nchunks));
+    std::vector<std::thread> th;
+    for (int t = 1; t < nth; ++t) th.emplace_back(classify);
+    classify();
+    for (auto& t : th) t.join();
+  }
+  const double t_classify = now_s();
+  // concatenate the chunks in polygon order, rebasing blob / compact offsets
+  std::vector<Ent> ents;
+  std::vector<double> blob, compact;
+  int64_t n_slow = 0, n_boundary = 0, n_records = 0, n_compact = 0;
+  {
+    size_t ne = 0, nbw = 0, ncw = 0;
+    for (const ChunkOut& o : outs) { ne += o.ents.size(); nbw += o.blob.size(); ncw += o.compact.size(); }
+    if (nbw / 2 >= (size_t)BLOB_COMPACT || ncw / 16 >= (size_t)BLOB_COMPACT) {
+      gm::set_error("gm_pip_index_create: boundary blobs too large (lower cells_per_poly)");
+      return GM_E_CAPACITY;
+    }
+    ents.reserve(ne); blob.reserve(nbw); compact.reserve(ncw);
+    for (ChunkOut& o : outs) {
+      const uint32_t bb = (uint32_t)(blob.size() / 2), cb = (uint32_t)(compact.size() / 16);
+      for (const Ent& en : o.ents) {
+        uint32_t e = en.e;
+        if ((e >> 30) == CELL_BOUNDARY) e += (e & BLOB_COMPACT) ? cb : bb;
+        ents.push_back(Ent{en.cell, e});
       }
+      blob.insert(blob.end(), o.blob.begin(), o.blob.end());
+      compact.insert(compact.end(), o.compact.begin(), o.compact.end());
+      n_slow += o.n_slow; n_boundary += o.n_boundary; n_records += o.n_records; n_compact += o.n_compact;
+      std::vector<Ent>().swap(o.ents); std::vector<double>().swap(o.blob); std::vector<double>().swap(o.compact);
     }
   }
-  if (dbg) {
-    fprintf(stderr, "[gm_pip] one-ring boundary cells by (segments, breakpoints):\n");
-    for (int e = 0; e < 16; ++e)
-      for (int b = 0; b < 64; ++b)
-        if (dbg_hist[e * 64 + b]) fprintf(stderr, "  E=%d B=%d: %lld\n", e, b, (long long)dbg_hist[e * 64 + b]);
+  std::vector<int32_t> per_cell((size_t)ncell, 0), bnd_cell((size_t)ncell, 0);
+  for (const Ent& en : ents) {
+    per_cell[en.cell]++;
+    if ((en.e >> 30) == CELL_BOUNDARY) bnd_cell[en.cell]++;
   }
+  const double t_merge = now_s();
   if (blob.empty()) blob.push_back(0.0);
   // ---- cell words: single entries inline, multi-entry cells through a list (polygons ascending)
   std::vector<uint32_t> cell_word((size_t)ncell, 0xffffffffu);
@@ -1617,28 +1698,26 @@ int gm_pip_index_create_ex(gm_ctx* ctx, const gm_polyset* ps, int cells_per_poly
   ix->blob_bytes = (int64_t)(blob.size() + compact.size()) * 8;
   int rc = GM_OK;
   GM_HIP(hipSetDevice(ctx->device));
-  if (!rc) rc = upload(ix, rings, &ix->dev.rings);
-  if (!rc) rc = upload(ix, slab_off, &ix->dev.slab_off);
-  if (!rc) rc = upload(ix, slab_edges, &ix->dev.slab_edges);
-  if (!rc) rc = upload(ix, cell_word, &ix->dev.cell_word);
-  if (!rc) rc = upload(ix, coarse_word, &ix->dev.coarse_word);
+  if (!rc) rc = upload(ix, 0, rings, &ix->dev.rings);
+  if (!rc) rc = upload(ix, 1, slab_off, &ix->dev.slab_off);
+  if (!rc) rc = upload(ix, 2, slab_edges, &ix->dev.slab_edges);
+  if (!rc) rc = upload(ix, 3, cell_word, &ix->dev.cell_word);
+  if (!rc) rc = upload(ix, 4, coarse_word, &ix->dev.coarse_word);
   if (compact.empty()) compact.assign(16, 0.0);
-  if (!rc) rc = upload(ix, compact, &ix->dev.compact);
-  if (!rc) rc = upload(ix, list_ent, &ix->dev.list_ent);
-  if (!rc) rc = upload(ix, blob, &ix->dev.blob);
+  if (!rc) rc = upload(ix, 5, compact, &ix->dev.compact);
+  if (!rc) rc = upload(ix, 6, list_ent, &ix->dev.list_ent);
+  if (!rc) rc = upload(ix, 7, blob, &ix->dev.blob);
   if (rc) { gm_pip_index_destroy(ix); return rc; }
   ix->dev.gx0 = G[0]; ix->dev.gy0 = G[1]; ix->dev.gx1 = G[2]; ix->dev.gy1 = G[3];
   ix->dev.inv_cw = inv_cw; ix->dev.inv_ch = inv_ch;
   ix->dev.gx = gx; ix->dev.gy = gy; ix->dev.gxc = gxc;
-  {
-    const int64_t ns = (int64_t)list_ent.size();
-    void* lp = nullptr;
-    if (hipMalloc(&lp, (size_t)ns * 4) != hipSuccess) { gm_pip_index_destroy(ix); return hip_fail(hipErrorOutOfMemory, "list_poly"); }
-    ix->allocs.push_back(lp);
-    ix->list_poly = (const int32_t*)lp;
-    hipLaunchKernelGGL(k_list_poly, dim3((unsigned)((ns + RTPB - 1) / RTPB)), dim3(RTPB), 0, ctx->stream, ix->dev, ns,
-                       (int32_t*)lp);
-    if (hipGetLastError() != hipSuccess) { gm_pip_index_destroy(ix); return hip_fail(hipErrorLaunchFailure, "k_list_poly"); }
+  rc = make_list_poly(ix);
+  if (rc) { gm_pip_index_destroy(ix); return rc; }
+  if (getenv("GM_PIP_DEBUG")) {
+    GM_HIP(hipStreamSynchronize(ctx->stream));
+    fprintf(stderr, "[gm_pip] build: classify %.3f s (%d threads), merge %.3f s, cell words + upload %.3f s; "
+            "%lld cells, %lld entries, %lld blob bytes\n", t_classify - t_start, build_threads(), t_merge - t_classify,
+            now_s() - t_merge, (long long)ncell, (long long)ix->n_entries, (long long)ix->blob_bytes);
   }
   *out = ix;
   return GM_OK;
@@ -1648,6 +1727,71 @@ int gm_pip_index_destroy(gm_pip_index* ix) {
   if (!ix) return GM_OK;
   for (void* p : ix->allocs) (void)hipFree(p);
   delete ix;
+  return GM_OK;
+}
+
+int gm_pip_index_export(const gm_pip_index* ix, gm_pip_index_layout* lay) {
+  if (!ix || !lay) return GM_E_INVALID;
+  memset(lay, 0, sizeof(*lay));
+  for (int k = 0; k < GM_PIP_INDEX_ARRAYS; ++k) lay->bytes[k] = ix->arr_bytes[k];
+  const PipDev& d = ix->dev;
+  const double g[6] = {d.gx0, d.gy0, d.gx1, d.gy1, d.inv_cw, d.inv_ch};
+  memcpy(lay->grid, g, sizeof g);
+  lay->dims[0] = d.gx; lay->dims[1] = d.gy; lay->dims[2] = d.gxc; lay->dims[3] = ix->n_polys;
+  const int64_t st[9] = {ix->n_cells, ix->n_entries, ix->n_boundary, ix->n_records, ix->n_slow, ix->blob_bytes,
+                         ix->n_compact, ix->max_bnd_per_cell, ix->max_ent_per_cell};
+  memcpy(lay->stats, st, sizeof st);
+  lay->version = GM_PIP_LAYOUT_VERSION;
+  return GM_OK;
+}
+
+int gm_pip_index_copy_array(gm_ctx* ctx, const gm_pip_index* ix, int k, void* dst) {
+  if (!ctx || !ix || k < 0 || k >= GM_PIP_INDEX_ARRAYS || (!dst && ix->arr_bytes[k])) return GM_E_INVALID;
+  if (ix->arr_bytes[k])
+    GM_HIP(hipMemcpyAsync(dst, ix->arr[k], (size_t)ix->arr_bytes[k], hipMemcpyDeviceToDevice, ctx->stream));
+  return GM_OK;
+}
+
+int gm_pip_index_import(gm_ctx* ctx, const gm_pip_index_layout* lay, void* const* arrays, gm_pip_index** out) {
+  if (!ctx || !lay || !arrays || !out || lay->version != GM_PIP_LAYOUT_VERSION) return GM_E_INVALID;
+  *out = nullptr;
+  for (int k = 0; k < GM_PIP_INDEX_ARRAYS; ++k)
+    if (lay->bytes[k] < 0 || (lay->bytes[k] && !arrays[k])) return GM_E_INVALID;
+  GM_HIP(hipSetDevice(ctx->device));
+  gm_pip_index* ix = new gm_pip_index();
+  ix->ctx = ctx;
+  const void** dst[GM_PIP_INDEX_ARRAYS] = {(const void**)&ix->dev.rings, (const void**)&ix->dev.slab_off,
+                                           (const void**)&ix->dev.slab_edges, (const void**)&ix->dev.cell_word,
+                                           (const void**)&ix->dev.coarse_word, (const void**)&ix->dev.compact,
+                                           (const void**)&ix->dev.list_ent, (const void**)&ix->dev.blob};
+  for (int k = 0; k < GM_PIP_INDEX_ARRAYS; ++k) {
+    void* p = nullptr;
+    if (hipMalloc(&p, (size_t)std::max<int64_t>(lay->bytes[k], 16)) != hipSuccess) {
+      gm_pip_index_destroy(ix);
+      return hip_fail(hipErrorOutOfMemory, "gm_pip_index_import");
+    }
+    ix->allocs.push_back(p);
+    ix->arr[k] = p;
+    ix->arr_bytes[k] = lay->bytes[k];
+    *dst[k] = p;
+    if (lay->bytes[k] &&
+        hipMemcpyAsync(p, arrays[k], (size_t)lay->bytes[k], hipMemcpyDeviceToDevice, ctx->stream) != hipSuccess) {
+      gm_pip_index_destroy(ix);
+      return hip_fail(hipErrorInvalidValue, "gm_pip_index_import copy");
+    }
+  }
+  PipDev& d = ix->dev;
+  d.gx0 = lay->grid[0]; d.gy0 = lay->grid[1]; d.gx1 = lay->grid[2]; d.gy1 = lay->grid[3];
+  d.inv_cw = lay->grid[4]; d.inv_ch = lay->grid[5];
+  d.gx = lay->dims[0]; d.gy = lay->dims[1]; d.gxc = lay->dims[2];
+  ix->n_polys = lay->dims[3];
+  ix->n_cells = lay->stats[0]; ix->n_entries = lay->stats[1]; ix->n_boundary = lay->stats[2];
+  ix->n_records = lay->stats[3]; ix->n_slow = lay->stats[4]; ix->blob_bytes = lay->stats[5];
+  ix->n_compact = lay->stats[6]; ix->max_bnd_per_cell = lay->stats[7]; ix->max_ent_per_cell = lay->stats[8];
+  int rc = make_list_poly(ix);
+  if (!rc && hipStreamSynchronize(ctx->stream) != hipSuccess) rc = hip_fail(hipErrorLaunchFailure, "gm_pip_index_import");
+  if (rc) { gm_pip_index_destroy(ix); return rc; }
+  *out = ix;
   return GM_OK;
 }
 

@@ -103,6 +103,33 @@ class PolygonIndex:
         check(self.ctx.lib.gm_pip_index_create_ex(self.ctx.handle, ctypes.byref(self._cs), int(cells_per_poly),
                                                   ctypes.byref(self._h)), "gm_pip_index_create_ex")
 
+    def export_arrays(self):
+        """(layout, [uint8 device tensors]) of this index: what another GPU needs to rebuild it with
+        `from_arrays` (gm_pip_index_export / gm_pip_index_copy_array)."""
+        import torch
+        lay = _lib.PipIndexLayout()
+        check(self.ctx.lib.gm_pip_index_export(self._h, ctypes.byref(lay)), "gm_pip_index_export")
+        dev = torch.device("cuda", self.ctx.device)
+        arrs = []
+        for k in range(_lib.GM_PIP_INDEX_ARRAYS):
+            t = torch.empty(max(int(lay.bytes[k]), 1), dtype=torch.uint8, device=dev)
+            check(self.ctx.lib.gm_pip_index_copy_array(self.ctx.handle, self._h, k, ptr(t)), "gm_pip_index_copy_array")
+            arrs.append(t)
+        return lay, arrs
+
+    @classmethod
+    def from_arrays(cls, layout, arrays, ctx=None, polyset=None):
+        """An index rebuilt from another GPU's export (device tensors on this rank's GPU)."""
+        self = cls.__new__(cls)
+        self.polyset = polyset
+        self.ctx = ctx or _lib.context()
+        self._cs = None
+        self._h = ctypes.c_void_p()
+        ptrs = (ctypes.c_void_p * _lib.GM_PIP_INDEX_ARRAYS)(*[a.data_ptr() for a in arrays])
+        check(self.ctx.lib.gm_pip_index_import(self.ctx.handle, ctypes.byref(layout), ptrs, ctypes.byref(self._h)),
+              "gm_pip_index_import")
+        return self
+
     def stats(self):
         """Index statistics: cells, (cell, polygon) entries, boundary entries, ring records,
         slow-walk records, blob bytes, compact blobs."""

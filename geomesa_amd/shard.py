@@ -41,6 +41,37 @@ def broadcast_polyset(pg, ps, src=0):
     return PolygonSet(*out)
 
 
+def broadcast_index(pg, index, src=0, ctx=None):
+    """Broadcast a built join index (join.PolygonIndex) from rank `src`: its device arrays go out over
+    RCCL (xGMI) and every other rank imports them (gm_pip_index_import) -- no per-rank host rebuild.
+    Other ranks pass index=None.  Over gloo the arrays travel through host memory."""
+    import ctypes
+    import torch
+    from . import _lib
+    from .join import PolygonIndex
+    dev = _device_of(pg)
+    nb = ctypes.sizeof(_lib.PipIndexLayout)
+    if pg.get_rank() == src:
+        lay, arrs = index.export_arrays()
+        hdr = torch.frombuffer(bytearray(bytes(lay)), dtype=torch.uint8).to(dev)
+    else:
+        lay, arrs = None, None
+        hdr = torch.zeros(nb, dtype=torch.uint8, device=dev)
+    pg.broadcast(hdr, src)
+    if pg.get_rank() != src:
+        lay = _lib.PipIndexLayout.from_buffer_copy(bytes(hdr.cpu().numpy().tobytes()))
+    out = []
+    cuda = torch.device("cuda", (ctx or _lib.context()).device)
+    for k in range(_lib.GM_PIP_INDEX_ARRAYS):
+        size = max(int(lay.bytes[k]), 1)
+        t = arrs[k].to(dev) if arrs is not None else torch.empty(size, dtype=torch.uint8, device=dev)
+        pg.broadcast(t, src)
+        out.append(t.to(cuda))
+    if pg.get_rank() == src:
+        return index
+    return PolygonIndex.from_arrays(lay, out, ctx)
+
+
 def all_reduce_scalar(pg, v, op="max"):
     """max / sum of one float over all ranks (identity without a process group)."""
     if pg is None:

@@ -240,6 +240,27 @@ int gm_pip_index_destroy(gm_pip_index* index);
    ring records that fall back to the slab walk, boundary blob bytes, compact (one-line) blobs */
 int gm_pip_index_stats(const gm_pip_index* index, int64_t* stats);
 
+/* A built index as device arrays, for shipping it to the other GPUs of a join (RCCL broadcast) instead
+   of rebuilding it on every rank -- the broadcast side of GeoMesaJoinRelation's join
+   (geomesa-spark-sql/.../GeoMesaJoinRelation.scala:41-91).  gm_pip_index_export fills the layout
+   (array sizes + grid scalars, plain host data); gm_pip_index_copy_array copies device array k into a
+   caller buffer of layout.bytes[k] bytes (stream-ordered); gm_pip_index_import builds an index on
+   ctx's device from the layout and device copies of the arrays (the library copies them: the caller
+   keeps ownership of `arrays`). */
+#define GM_PIP_INDEX_ARRAYS 8
+#define GM_PIP_LAYOUT_VERSION 1
+typedef struct {
+  int32_t version;                       /* GM_PIP_LAYOUT_VERSION */
+  int32_t dims[4];                       /* grid columns, rows, coarse columns, polygons */
+  int32_t reserved;
+  double grid[6];                        /* grid envelope x0 y0 x1 y1, inverse cell width / height */
+  int64_t stats[9];                      /* gm_pip_index_stats[0..6], most boundary / all entries of a cell */
+  int64_t bytes[GM_PIP_INDEX_ARRAYS];    /* device bytes of each array */
+} gm_pip_index_layout;
+int gm_pip_index_export(const gm_pip_index* index, gm_pip_index_layout* layout);
+int gm_pip_index_copy_array(gm_ctx* ctx, const gm_pip_index* index, int k, void* dst);
+int gm_pip_index_import(gm_ctx* ctx, const gm_pip_index_layout* layout, void* const* arrays, gm_pip_index** out);
+
 /* ST_Contains(polygon, point) = JTS Geometry.contains (geomesa-spark-jts/.../udf/
    SpatialRelationFunctions.scala:29), evaluated for every (point, polygon) pair -- the result of
    GeoMesaJoinRelation.sweeplineJoin + OverlapAction (geomesa-spark-sql/.../GeoMesaJoinRelation.scala:41-91,
