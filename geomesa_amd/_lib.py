@@ -61,8 +61,8 @@ class PolySetC(ctypes.Structure):
                 ("ring_vert_off", ctypes.c_void_p), ("vx", ctypes.c_void_p), ("vy", ctypes.c_void_p)]
 
 
-GM_PIP_INDEX_ARRAYS = 8
-GM_PIP_LAYOUT_VERSION = 1
+GM_PIP_INDEX_ARRAYS = 10
+GM_PIP_LAYOUT_VERSION = 2
 
 
 class PipIndexLayout(ctypes.Structure):
