@@ -61,8 +61,8 @@ class PolySetC(ctypes.Structure):
                 ("ring_vert_off", ctypes.c_void_p), ("vx", ctypes.c_void_p), ("vy", ctypes.c_void_p)]
 
 
-GM_PIP_INDEX_ARRAYS = 10
-GM_PIP_LAYOUT_VERSION = 2
+GM_PIP_INDEX_ARRAYS = 8
+GM_PIP_LAYOUT_VERSION = 1
 
 
 class PipIndexLayout(ctypes.Structure):
@@ -156,7 +156,10 @@ def load():
         raise GeomesaHipUnavailable(
             "libgeomesa_hip.so not built (%s); run `python -m geomesa_amd.build`" % LIB_PATH)
     lib = ctypes.CDLL(LIB_PATH)
+    variant = "GEOMESA_HIP_LIB" in os.environ   # an older / experimental build for A/B timing
     for name, (res, args) in SIGNATURES.items():
+        if variant and not hasattr(lib, name):
+            continue
         f = getattr(lib, name)
         f.restype = res
         f.argtypes = args

@@ -12,20 +12,15 @@
 //   * a uniform grid over the polygon set's envelope.  Every (cell, polygon) pair whose envelopes
 //     meet is INTERIOR (no segment of the polygon meets the inflated cell and the cell is inside:
 //     every point of the cell is contained, no arithmetic at all), EXTERIOR (dropped) or BOUNDARY;
-//   * a BOUNDARY pair of a single-part polygon (a Polygon, holes allowed) is located by the cell's
-//     REFERENCE POINT c (its nominal centre, never collinear with a local segment): the host knows
-//     c's location exactly, and a point p of the cell is on the boundary iff it lies on one of the
-//     ring segments meeting the inflated cell, else its location is c's, flipped once per local
-//     segment that crosses the segment pc (only local segments can: pc lies inside the cell).  The
-//     local segments are runs of consecutive ring edges kept as vertex ids into the shared vertex
-//     array; a single run of <= 4 edges is stored in the cell word itself, longer lists in a small
-//     reference blob (rblob).  Every predicate is JTS's orientation (filter + double-double), which
-//     is exact for coordinates of this magnitude, so the located set equals PointLocator's;
-//   * a BOUNDARY pair of a MultiPolygon (the Mod-2 rule needs per-part boundary counts) keeps the
-//     generic blob: per ring, the segments meeting the inflated cell (RayCrossingCounter.countSegment
-//     exactly as JTS walks them), plus the crossing parity of the segments to the RIGHT of the cell
-//     as a function of the point's y (piecewise constant with breakpoints at segment end-point y
-//     values, <= 63 breakpoints, else the record falls back to the slab walk).
+//   * a BOUNDARY pair carries one record per ring of the polygon: the ring segments that meet the
+//     inflated cell (tested exactly with RayCrossingCounter.countSegment), plus the crossing parity
+//     of all segments to the RIGHT of the cell as a function of the point's y.  Within the cell's
+//     y-band a segment that misses the inflated cell lies wholly left (never counted) or wholly
+//     right (counted iff it straddles y: ymin <= y < ymax, the half-open rule of countSegment), so
+//     that parity is piecewise constant with breakpoints at segment end-point y values; it is
+//     precomputed per interval (<= 63 breakpoints, else the record falls back to the slab walk).
+//     Geometric and JTS answers agree there: those segments are at least one cell away from the
+//     point, where the orientation filter is exact.
 //   * per ring y-slab buckets of all segments: the fallback walk (every segment whose y-range holds
 //     the point's y -- the only ones countSegment can count).
 // A point costs one cell lookup plus, in a boundary cell, ~2 exact segment tests.
@@ -63,11 +58,9 @@ struct PipDev {
   const Edge* slab_edges;
   const uint32_t* coarse_word;   // per coarse cell (CF x CF fine cells): EMPTY, INTERIOR or LIST = "look at the fine word"
   const uint32_t* cell_word;     // per cell: kind << 30 | payload (see CELL_*)
-  const dv2* vxy;                // every ring vertex (x, y), CSR order
+  const double* compact;         // compact blobs: 16 words (one 128-B line) each
   const uint32_t* list_ent;      // entries in cell-word form (kind INTERIOR or BOUNDARY)
-  const double* blob;            // generic boundary blobs (MultiPolygons), 16-byte aligned
-  const int32_t* vpoly;          // polygon of each vertex
-  const uint32_t* rblob;         // reference blobs: poly, runs | loc << 31, (first vertex, edges) per run
+  const double* blob;            // boundary blobs, 16-byte aligned
   double gx0, gy0, gx1, gy1, inv_cw, inv_ch;
   int32_t gx, gy, gxc;
   int32_t op;                    // join predicate: JOIN_CONTAINS (interior) or JOIN_INTERSECTS (not exterior)
@@ -83,15 +76,21 @@ constexpr int CF_LOG = GM_CF_LOG;   // coarse cell = 8 x 8 fine cells: the coars
 
 // cell word kinds (2 high bits; 30-bit payload)
 enum : uint32_t { CELL_INTERIOR = 0, CELL_BOUNDARY = 1, CELL_LIST = 2, CELL_EMPTY = 3 };
-// BOUNDARY payload (30 bits):
-//   bit 29 set: an inline run -- bits 27-28 = edges - 1 (1..4), bit 26 = the cell's reference point is
-//     interior, bits 0-25 = vertex j: the edges (v[j-1], v[j]), (v[j], v[j+1]), ...
-//   bit 29 clear, bit 28 set: reference blob at rblob word offset bits 0-27
-//   bits 29, 28 clear: generic blob at 16-B offset bits 0-27
-constexpr uint32_t B_EDGE = 1u << 29, B_RBLOB = 1u << 28, B_OFF = (1u << 28) - 1;
-constexpr int EDGE_VBITS = 26;
+// BOUNDARY payload: bit 29 set = compact blob index, else generic blob offset (16-B units)
+constexpr uint32_t BLOB_COMPACT = 1u << 29;
 // LIST payload: list_ent offset << 4 | count; count 15 = long list whose count is list_ent[offset]
 constexpr int LIST_LONG = 15;
+
+// Compact blob (single-ring polygon, 4 * segments + breakpoints <= 30 in the cell): one or two
+// 128-B lines of 16 words in `compact`, addressed by line index.
+//   w0: int32 polygon | int32 meta (segments | lines << 8), w1: parity bits,
+//   segment j (p1x p1y p2x p2y) at words CSEG[j] = 2, 6, 10 (line 0), 16, 20, 24, 28 (line 1);
+//   every other word of the record is a breakpoint slot (+inf when unused).
+// The breakpoint count k = #(slots <= y) does not depend on slot order, so the record is evaluated
+// with static indexing, line by line: crossings = parity bit k + segment crossings, exactly the
+// RayCrossingCounter walk of a generic one-ring blob.
+constexpr int CSEG_MAX = 7;
+__host__ __device__ constexpr int cseg_word(int j) { return j < 3 ? 2 + 4 * j : 16 + 4 * (j - 3); }
 
 struct RingHdr {
   int16_t n_edge, n_brk, flags, pad;
@@ -198,64 +197,47 @@ __device__ __forceinline__ bool blob_contains(const PipDev& d, const double* b, 
   return blob_locate(d, b, h, px, py) == LOC_INTERIOR;
 }
 
-// The cell's reference point: its nominal centre, computed identically on the host (index build)
-// and here, from the cell the point maps to.
-__device__ __forceinline__ void cell_ref(const PipDev& d, double px, double py, double& cx, double& cy) {
-  const int ix = cell_of(px, d.gx0, d.inv_cw, d.gx), iy = cell_of(py, d.gy0, d.inv_ch, d.gy);
-  cx = __dadd_rn(d.gx0, __ddiv_rn(__dadd_rn((double)ix, 0.5), d.inv_cw));
-  cy = __dadd_rn(d.gy0, __ddiv_rn(__dadd_rn((double)iy, 0.5), d.inv_ch));
+// one line (16 words, 8 independent 16-B loads) of a compact blob: breakpoint count and segments
+template <int LINE>
+__device__ __forceinline__ void compact_line(const dv2* __restrict__ c, int E, double px, double py, int& k,
+                                             int& cr, bool& on) {
+  dv2 q[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) q[i] = c[8 * LINE + i];
+  auto word = [&](int w) -> double { return (w & 1) ? q[(w & 15) >> 1].y : q[(w & 15) >> 1].x; };
+#pragma unroll
+  for (int w = 16 * LINE; w < 16 * LINE + 16; ++w) {
+    if (w < 2) continue;
+    int seg = -1;   // segment group holding word w (compile-time)
+#pragma unroll
+    for (int j = 0; j < CSEG_MAX; ++j)
+      if (w >= cseg_word(j) && w < cseg_word(j) + 4) seg = j;
+    if (seg < 0 || seg >= E) k += word(w) <= py;     // a breakpoint slot (+inf when unused)
+  }
+#pragma unroll
+  for (int j = 0; j < CSEG_MAX; ++j) {
+    if (cseg_word(j) / 16 != LINE) continue;
+    const int w0 = cseg_word(j);
+    if (j < E && !on) on = count_segment(word(w0), word(w0 + 1), word(w0 + 2), word(w0 + 3), px, py, cr);
+  }
 }
 
-// One run of consecutive ring edges (v[j-1], v[j]) ... (v[j+L-2], v[j+L-1]) against the point p and
-// the reference point c: returns true when p lies on one of them (BOUNDARY); flips `in` once per
-// edge crossing the segment pc.  An edge (a, b) crosses pc iff p and c lie strictly on opposite
-// sides of line ab and a, b on different sides of line pc, a vertex on line pc counting on the
-// negative side (the half-open rule keeps the parity right when pc passes through a vertex).
-__device__ __forceinline__ bool ref_run(const dv2* __restrict__ V, uint32_t j, int L, double cx, double cy, double px,
-                                        double py, bool& in) {
-  dv2 a = V[j - 1];
-  for (int k = 0; k < L; ++k) {
-    const dv2 b = V[j + k];
-    const int o1 = jts_orientation(a.x, a.y, b.x, b.y, px, py);
-    if (o1 == 0) {
-      if (px >= fmin(a.x, b.x) && px <= fmax(a.x, b.x) && py >= fmin(a.y, b.y) && py <= fmax(a.y, b.y)) return true;
-    } else if (o1 != jts_orientation(a.x, a.y, b.x, b.y, cx, cy)) {
-      const bool sa = jts_orientation(px, py, cx, cy, a.x, a.y) > 0;
-      const bool sb = jts_orientation(px, py, cx, cy, b.x, b.y) > 0;
-      in ^= (sa != sb);
-    }
-    a = b;
-  }
-  return false;
+__device__ __forceinline__ int compact_locate(const dv2* __restrict__ c, double px, double py, int& poly) {
+  const dv2 h = c[0];
+  const int64_t meta = __double_as_longlong(h.x);
+  poly = (int)meta;
+  const int E = (int)((meta >> 32) & 0xff), lines = (int)((meta >> 40) & 0xff);
+  int k = 0, cr = 0;
+  bool on = false;
+  compact_line<0>(c, E, px, py, k, cr, on);
+  if (lines > 1) compact_line<1>(c, E, px, py, k, cr, on);
+  if (on) return LOC_BOUNDARY;
+  cr += (int)(((uint64_t)__double_as_longlong(h.y) >> k) & 1ull);
+  return (cr & 1) ? LOC_INTERIOR : LOC_EXTERIOR;
 }
 
-// PointLocator.locate of p for a BOUNDARY entry payload; *poly gets the entry's polygon
-__device__ int boundary_locate(const PipDev& d, uint32_t ref, double px, double py, int& poly) {
-  if (ref & B_EDGE) {
-    const uint32_t j = ref & ((1u << EDGE_VBITS) - 1u);
-    poly = d.vpoly[j];
-    double cx, cy;
-    cell_ref(d, px, py, cx, cy);
-    bool in = (ref >> EDGE_VBITS) & 1u;
-    if (ref_run(d.vxy, j, (int)((ref >> 27) & 3u) + 1, cx, cy, px, py, in)) return LOC_BOUNDARY;
-    return in ? LOC_INTERIOR : LOC_EXTERIOR;
-  }
-  if (ref & B_RBLOB) {
-    const uint32_t* r = d.rblob + (ref & B_OFF);
-    poly = (int)r[0];
-    const uint32_t h = r[1];
-    double cx, cy;
-    cell_ref(d, px, py, cx, cy);
-    bool in = h >> 31;
-    const int nr = (int)(h & 0xffffu);
-    for (int k = 0; k < nr; ++k)
-      if (ref_run(d.vxy, r[2 + 2 * k], (int)r[3 + 2 * k], cx, cy, px, py, in)) return LOC_BOUNDARY;
-    return in ? LOC_INTERIOR : LOC_EXTERIOR;
-  }
-  const double* b = d.blob + 2 * (uint64_t)(ref & B_OFF);
-  const int2 h = *(const int2*)b;
-  poly = h.x;
-  return blob_locate(d, b, h, px, py);
+__device__ __forceinline__ bool compact_contains(const dv2* __restrict__ c, double px, double py, int& poly) {
+  return compact_locate(c, px, py, poly) == LOC_INTERIOR;
 }
 
 constexpr int JTPB = 256;             // 4 waves
@@ -521,7 +503,15 @@ __global__ __launch_bounds__(JTPB, GM_JOIN_WAVES) void k_pip_join(const double* 
             poly = 0; hit = false;
           } else
 #endif
-          hit = join_hit(d.op, boundary_locate(d, ref, ex, ey, poly));
+          if (ref & BLOB_COMPACT) {
+            const dv2* c = (const dv2*)(d.compact + 16 * (uint64_t)(ref & (BLOB_COMPACT - 1)));
+            hit = join_hit(d.op, compact_locate(c, ex, ey, poly));
+          } else {
+            const double* b = d.blob + 2 * (uint64_t)ref;
+            const int2 h = *(const int2*)b;
+            poly = h.x;
+            hit = join_hit(d.op, blob_locate(d, b, h, ex, ey));
+          }
         }
         wave_lds_sync();
         qn -= kq;
@@ -581,7 +571,15 @@ __global__ __launch_bounds__(JTPB) void k_pip_blobs(const double* __restrict__ p
         row = it.x;
         const uint32_t ref = it.y;
         const double ex = px[row], ey = py[row];
-        hit = join_hit(d.op, boundary_locate(d, ref, ex, ey, poly));
+        if (ref & BLOB_COMPACT) {
+          const dv2* c = (const dv2*)(d.compact + 16 * (uint64_t)(ref & (BLOB_COMPACT - 1)));
+          hit = join_hit(d.op, compact_locate(c, ex, ey, poly));
+        } else {
+          const double* b = d.blob + 2 * (uint64_t)ref;
+          const int2 h = *(const int2*)b;
+          poly = h.x;
+          hit = join_hit(d.op, blob_locate(d, b, h, ex, ey));
+        }
       }
       if (!WRITE) my_count += hit;
       if (WRITE) {
@@ -913,8 +911,15 @@ enum : int { SP_NONE = 0, SP_INTERSECTS = 1, SP_CONTAINS = 2 };
 template <int OP>
 __device__ __forceinline__ bool entry_pred(const PipDev& d, uint32_t e, double px, double py) {
   if ((e >> 30) == CELL_INTERIOR) return true;   // every point of the cell is interior
-  int poly;
-  const int loc = boundary_locate(d, e & 0x3fffffffu, px, py, poly);
+  const uint32_t ref = e & 0x3fffffffu;
+  int loc;
+  if (ref & BLOB_COMPACT) {
+    int poly;
+    loc = compact_locate((const dv2*)(d.compact + 16 * (uint64_t)(ref & (BLOB_COMPACT - 1))), px, py, poly);
+  } else {
+    const double* b = d.blob + 2 * (uint64_t)ref;
+    loc = blob_locate(d, b, *(const int2*)b, px, py);
+  }
   return OP == SP_INTERSECTS ? loc != LOC_EXTERIOR : loc == LOC_INTERIOR;
 }
 
@@ -1043,15 +1048,19 @@ constexpr uint8_t LOC_NULL = 0xff;
 __device__ __forceinline__ int entry_poly(const PipDev& d, uint32_t e) {
   const uint32_t ref = e & 0x3fffffffu;
   if ((e >> 30) == CELL_INTERIOR) return (int)ref;
-  if (ref & B_EDGE) return d.vpoly[ref & ((1u << EDGE_VBITS) - 1u)];
-  if (ref & B_RBLOB) return (int)d.rblob[ref & B_OFF];
-  return ((const int2*)(d.blob + 2 * (uint64_t)(ref & B_OFF)))->x;
+  if (ref & BLOB_COMPACT) return (int)__double_as_longlong(d.compact[16 * (uint64_t)(ref & (BLOB_COMPACT - 1))]);
+  return ((const int2*)(d.blob + 2 * (uint64_t)ref))->x;
 }
 
 __device__ __forceinline__ int entry_locate(const PipDev& d, uint32_t e, double px, double py) {
   if ((e >> 30) == CELL_INTERIOR) return LOC_INTERIOR;
-  int poly;
-  return boundary_locate(d, e & 0x3fffffffu, px, py, poly);
+  const uint32_t ref = e & 0x3fffffffu;
+  if (ref & BLOB_COMPACT) {
+    int poly;
+    return compact_locate((const dv2*)(d.compact + 16 * (uint64_t)(ref & (BLOB_COMPACT - 1))), px, py, poly);
+  }
+  const double* b = d.blob + 2 * (uint64_t)ref;
+  return blob_locate(d, b, *(const int2*)b, px, py);
 }
 
 __global__ __launch_bounds__(RTPB) void k_list_poly(PipDev d, int64_t n, int32_t* __restrict__ out) {
@@ -1146,8 +1155,15 @@ __global__ __launch_bounds__(RTPB) void k_pip_relate(const int32_t* __restrict__
       if (lane < kq) {
         const uint32_t ref = qe[slot] & 0x3fffffffu;
         const double ex = qx[slot], ey = qy[slot];
-        int pl;
-        const int l = boundary_locate(d, ref, ex, ey, pl);
+        int pl, l;
+        if (ref & BLOB_COMPACT) {
+          l = compact_locate((const dv2*)(d.compact + 16 * (uint64_t)(ref & (BLOB_COMPACT - 1))), ex, ey, pl);
+        } else {
+          const double* b = d.blob + 2 * (uint64_t)ref;
+          const int2 h = *(const int2*)b;
+          pl = h.x;
+          l = blob_locate(d, b, h, ex, ey);
+        }
         loc[qr[slot]] = (uint8_t)(pl == qp[slot] ? l : LOC_EXTERIOR);
       }
       wave_lds_sync();
@@ -1183,7 +1199,7 @@ struct gm_pip_index {
   gm::PipDev dev{};
   std::vector<void*> allocs;
   int32_t n_polys = 0;
-  int64_t n_entries = 0, n_boundary = 0, n_records = 0, n_slow = 0, n_cells = 0, blob_bytes = 0, n_inline = 0;
+  int64_t n_entries = 0, n_boundary = 0, n_records = 0, n_slow = 0, n_cells = 0, blob_bytes = 0, n_compact = 0;
   int64_t max_bnd_per_cell = 0;   // most BOUNDARY (cell, polygon) entries of any cell: work items per point
   int64_t max_ent_per_cell = 0;   // most (cell, polygon) entries of any cell: pairs per point
   const int32_t* list_poly = nullptr;   // polygon of each list_ent slot (the row-wise predicate's list search)
@@ -1196,7 +1212,7 @@ using namespace gm;
 namespace {
 
 // device array k of the index (gm_pip_index_layout order): rings, slab_off, slab_edges, cell_word,
-// coarse_word, vxy, list_ent, blob, vpoly, rblob
+// coarse_word, compact, list_ent, blob
 template <class T>
 int upload(gm_pip_index* ix, int k, const std::vector<T>& v, const T** out) {
   void* p = nullptr;
@@ -1428,8 +1444,8 @@ int gm_pip_index_create_ex(gm_ctx* ctx, const gm_polyset* ps, int cells_per_poly
   struct ChunkOut {
     std::vector<Ent> ents;
     std::vector<double> blob;      // 8-byte words; each blob starts 16-byte aligned (even length kept)
-    std::vector<uint32_t> rblob;   // reference blobs
-    int64_t n_slow = 0, n_boundary = 0, n_records = 0, n_inline = 0;
+    std::vector<double> compact;   // 16-word (128-B) compact blobs
+    int64_t n_slow = 0, n_boundary = 0, n_records = 0, n_compact = 0;
   };
   constexpr int PCH = 4;   // polygons per work item
   const int nchunks = (P + PCH - 1) / PCH;
@@ -1448,7 +1464,7 @@ int gm_pip_index_create_ex(gm_ctx* ctx, const gm_polyset* ps, int cells_per_poly
       ChunkOut& o = outs[(size_t)ch];
       std::vector<Ent>& ents = o.ents;
       std::vector<double>& blob = o.blob;
-      std::vector<uint32_t>& rblob = o.rblob;
+      std::vector<double>& compact = o.compact;
       auto put_i32x2 = [&](int32_t a, int32_t b) {
         double w; int32_t v[2] = {a, b}; memcpy(&w, v, 8); blob.push_back(w);
       };
@@ -1461,7 +1477,6 @@ int gm_pip_index_create_ex(gm_ctx* ctx, const gm_polyset* ps, int cells_per_poly
           for (int r = ps->part_ring_off[q]; r < ps->part_ring_off[q + 1]; ++r)
             ring_list.push_back(RingRef{r, r == ps->part_ring_off[q]});
         const int nr = (int)ring_list.size();
-        const bool single_part = ps->poly_part_off[p + 1] - ps->poly_part_off[p] == 1;
         band.resize((size_t)nr);
         const int cx0 = host::cell_of(e[0], G[0], inv_cw, gx), cx1 = host::cell_of(e[2], G[0], inv_cw, gx);
         const int cy0 = host::cell_of(e[1], G[1], inv_ch, gy), cy1 = host::cell_of(e[3], G[1], inv_ch, gy);
@@ -1506,63 +1521,40 @@ int gm_pip_index_create_ex(gm_ctx* ctx, const gm_polyset* ps, int cells_per_poly
               }
             }
             run_loc = -1;
-            // ---- single-part polygon: the reference-point form (runs of local edges + c's location)
-            if (single_part && !degenerate) {
-              a_edges.clear();
-              for (int k = 0; k < nr; ++k)
-                for (const BandSeg& sg : band[k])
-                  if (sg.maxx >= xb0 && sg.minx <= xb1) a_edges.push_back(sg.seg);   // ascending vertex ids
-              const double cxm = G[0] + ((double)cx + 0.5) / inv_cw;   // == cell_ref on the device
-              const double cym = G[1] + ((double)cy + 0.5) / inv_ch;
-              bool ok = host::cell_of(cxm, G[0], inv_cw, gx) == cx && host::cell_of(cym, G[1], inv_ch, gy) == cy;
-              for (size_t q = 0; q < a_edges.size() && ok; ++q) {
-                const int32_t i = a_edges[q];
-                ok = host::orientation(vx[i - 1], vy[i - 1], vx[i], vy[i], cxm, cym) != 0;
+            // ---- compact blob: single-ring polygon, <= 2 segments, <= 4 breakpoints -> one 128-B line
+            if (nr == 1 && !degenerate) {
+              a_edges.clear(); right.clear(); bk.clear();
+              for (const BandSeg& sg : band[0]) {
+                if (sg.maxx >= xb0 && sg.minx <= xb1) a_edges.push_back(sg.seg);
+                else if (sg.minx > xb1) right.push_back(&sg);
               }
-              if (ok) {
-                // c's location from the band's segments (only they can straddle cym, and c is on none):
-                // RayCrossingCounter per ring, then shell / holes (PointLocator.locateInPolygon)
-                int loc = LOC_EXTERIOR;
-                for (int k = 0; k < nr; ++k) {
-                  int crossings = 0;
-                  for (const BandSeg& sg : band[k]) {
-                    const int32_t i = sg.seg;
-                    const double p1x = vx[i], p1y = vy[i], p2x = vx[i - 1], p2y = vy[i - 1];
-                    if (p1x < cxm && p2x < cxm) continue;
-                    if (((p1y > cym) && (p2y <= cym)) || ((p2y > cym) && (p1y <= cym))) {
-                      int orient = host::orientation(p1x, p1y, p2x, p2y, cxm, cym);
-                      if (p2y < p1y) orient = -orient;
-                      if (orient == 1) crossings++;
-                    }
-                  }
-                  const bool in_ring = crossings & 1;
-                  if (k == 0) loc = in_ring ? LOC_INTERIOR : LOC_EXTERIOR;
-                  else if (in_ring && loc == LOC_INTERIOR) loc = LOC_EXTERIOR;   // inside a hole
-                  if (loc == LOC_EXTERIOR) break;
+              collect_breakpoints(right, yb0, yb1, bk);
+              if (4 * a_edges.size() + bk.size() <= 30) {
+                const int E = (int)a_edges.size(), B = (int)bk.size();
+                const int lines = (4 * E + B <= 14 && E <= 3) ? 1 : 2;
+                const uint64_t ci = compact.size() / 16;   // chunk-local line index
+                double rec[32];
+                for (double& w : rec) w = INFINITY;
+                { int32_t v[2] = {p, E | (lines << 8)}; memcpy(&rec[0], v, 8); }
+                { const uint64_t par = right_parity(right, yb0, bk); memcpy(&rec[1], &par, 8); }
+                bool used[32] = {};
+                used[0] = used[1] = true;
+                for (int j = 0; j < E; ++j) {
+                  const int32_t i = a_edges[j];
+                  double* eg = rec + cseg_word(j);
+                  eg[0] = vx[i]; eg[1] = vy[i]; eg[2] = vx[i - 1]; eg[3] = vy[i - 1];
+                  for (int q = 0; q < 4; ++q) used[cseg_word(j) + q] = true;
                 }
-                const uint32_t lc = loc == LOC_INTERIOR ? 1u : 0u;
-                // runs of consecutive edge ids (consecutive ids never span two rings)
-                size_t nrun = 0;
-                for (size_t q = 0; q < a_edges.size(); ++q) nrun += (q == 0 || a_edges[q] != a_edges[q - 1] + 1);
-                const int32_t j0 = a_edges.empty() ? 1 : a_edges[0];
-                if (nrun == 1 && a_edges.size() <= 4 && j0 < (1 << EDGE_VBITS)) {
-                  ents.push_back(Ent{cell, (CELL_BOUNDARY << 30) | B_EDGE | (uint32_t)(a_edges.size() - 1) << 27 |
-                                               lc << EDGE_VBITS | (uint32_t)j0});
-                  o.n_inline++;
-                } else {
-                  const uint32_t off = (uint32_t)rblob.size();   // chunk-local word offset
-                  rblob.push_back((uint32_t)p);
-                  rblob.push_back((uint32_t)nrun | lc << 31);
-                  for (size_t q = 0; q < a_edges.size();) {
-                    size_t e2 = q + 1;
-                    while (e2 < a_edges.size() && a_edges[e2] == a_edges[e2 - 1] + 1) ++e2;
-                    rblob.push_back((uint32_t)a_edges[q]);
-                    rblob.push_back((uint32_t)(e2 - q));
-                    q = e2;
-                  }
-                  ents.push_back(Ent{cell, (CELL_BOUNDARY << 30) | B_RBLOB | off});
+                int w = 2;
+                for (int j = 0; j < B; ++j) {
+                  while (used[w]) ++w;
+                  rec[w] = bk[j].first;
+                  used[w] = true;
                 }
+                compact.insert(compact.end(), rec, rec + 16 * lines);
                 o.n_boundary++;
+                o.n_compact++;
+                ents.push_back(Ent{cell, (CELL_BOUNDARY << 30) | BLOB_COMPACT | (uint32_t)ci});
                 continue;
               }
             }
@@ -1618,28 +1610,27 @@ int gm_pip_index_create_ex(gm_ctx* ctx, const gm_polyset* ps, int cells_per_poly
   const double t_classify = now_s();
   // concatenate the chunks in polygon order, rebasing blob / compact offsets
   std::vector<Ent> ents;
-  std::vector<double> blob;
-  std::vector<uint32_t> rblob;
-  int64_t n_slow = 0, n_boundary = 0, n_records = 0, n_inline = 0;
+  std::vector<double> blob, compact;
+  int64_t n_slow = 0, n_boundary = 0, n_records = 0, n_compact = 0;
   {
-    size_t ne = 0, nbw = 0, nrw = 0;
-    for (const ChunkOut& o : outs) { ne += o.ents.size(); nbw += o.blob.size(); nrw += o.rblob.size(); }
-    if (nbw / 2 > (size_t)B_OFF || nrw > (size_t)B_OFF) {
+    size_t ne = 0, nbw = 0, ncw = 0;
+    for (const ChunkOut& o : outs) { ne += o.ents.size(); nbw += o.blob.size(); ncw += o.compact.size(); }
+    if (nbw / 2 >= (size_t)BLOB_COMPACT || ncw / 16 >= (size_t)BLOB_COMPACT) {
       gm::set_error("gm_pip_index_create: boundary blobs too large (lower cells_per_poly)");
       return GM_E_CAPACITY;
     }
-    ents.reserve(ne); blob.reserve(nbw); rblob.reserve(nrw);
+    ents.reserve(ne); blob.reserve(nbw); compact.reserve(ncw);
     for (ChunkOut& o : outs) {
-      const uint32_t bb = (uint32_t)(blob.size() / 2), rb = (uint32_t)rblob.size();
+      const uint32_t bb = (uint32_t)(blob.size() / 2), cb = (uint32_t)(compact.size() / 16);
       for (const Ent& en : o.ents) {
         uint32_t e = en.e;
-        if ((e >> 30) == CELL_BOUNDARY && !(e & B_EDGE)) e += (e & B_RBLOB) ? rb : bb;
+        if ((e >> 30) == CELL_BOUNDARY) e += (e & BLOB_COMPACT) ? cb : bb;
         ents.push_back(Ent{en.cell, e});
       }
       blob.insert(blob.end(), o.blob.begin(), o.blob.end());
-      rblob.insert(rblob.end(), o.rblob.begin(), o.rblob.end());
-      n_slow += o.n_slow; n_boundary += o.n_boundary; n_records += o.n_records; n_inline += o.n_inline;
-      std::vector<Ent>().swap(o.ents); std::vector<double>().swap(o.blob); std::vector<uint32_t>().swap(o.rblob);
+      compact.insert(compact.end(), o.compact.begin(), o.compact.end());
+      n_slow += o.n_slow; n_boundary += o.n_boundary; n_records += o.n_records; n_compact += o.n_compact;
+      std::vector<Ent>().swap(o.ents); std::vector<double>().swap(o.blob); std::vector<double>().swap(o.compact);
     }
   }
   std::vector<int32_t> per_cell((size_t)ncell, 0), bnd_cell((size_t)ncell, 0);
@@ -1702,9 +1693,9 @@ int gm_pip_index_create_ex(gm_ctx* ctx, const gm_polyset* ps, int cells_per_poly
   ix->n_boundary = n_boundary;
   ix->n_records = n_records;
   ix->n_slow = n_slow;
-  ix->n_inline = n_inline;
+  ix->n_compact = n_compact;
   ix->n_cells = ncell;
-  ix->blob_bytes = (int64_t)blob.size() * 8 + (int64_t)rblob.size() * 4;
+  ix->blob_bytes = (int64_t)(blob.size() + compact.size()) * 8;
   int rc = GM_OK;
   GM_HIP(hipSetDevice(ctx->device));
   if (!rc) rc = upload(ix, 0, rings, &ix->dev.rings);
@@ -1712,19 +1703,10 @@ int gm_pip_index_create_ex(gm_ctx* ctx, const gm_polyset* ps, int cells_per_poly
   if (!rc) rc = upload(ix, 2, slab_edges, &ix->dev.slab_edges);
   if (!rc) rc = upload(ix, 3, cell_word, &ix->dev.cell_word);
   if (!rc) rc = upload(ix, 4, coarse_word, &ix->dev.coarse_word);
-  std::vector<dv2> vxy((size_t)std::max(n_verts, 1));
-  std::vector<int32_t> vpoly((size_t)std::max(n_verts, 1), -1);
-  for (int v = 0; v < n_verts; ++v) vxy[v] = dv2{vx[v], vy[v]};
-  for (int p = 0; p < P; ++p)
-    for (int v = ps->ring_vert_off[ps->part_ring_off[ps->poly_part_off[p]]];
-         v < ps->ring_vert_off[ps->part_ring_off[ps->poly_part_off[p + 1]]]; ++v)
-      vpoly[v] = p;
-  if (!rc) rc = upload(ix, 5, vxy, &ix->dev.vxy);
+  if (compact.empty()) compact.assign(16, 0.0);
+  if (!rc) rc = upload(ix, 5, compact, &ix->dev.compact);
   if (!rc) rc = upload(ix, 6, list_ent, &ix->dev.list_ent);
   if (!rc) rc = upload(ix, 7, blob, &ix->dev.blob);
-  if (!rc) rc = upload(ix, 8, vpoly, &ix->dev.vpoly);
-  if (rblob.empty()) rblob.assign(4, 0u);
-  if (!rc) rc = upload(ix, 9, rblob, &ix->dev.rblob);
   if (rc) { gm_pip_index_destroy(ix); return rc; }
   ix->dev.gx0 = G[0]; ix->dev.gy0 = G[1]; ix->dev.gx1 = G[2]; ix->dev.gy1 = G[3];
   ix->dev.inv_cw = inv_cw; ix->dev.inv_ch = inv_ch;
@@ -1757,7 +1739,7 @@ int gm_pip_index_export(const gm_pip_index* ix, gm_pip_index_layout* lay) {
   memcpy(lay->grid, g, sizeof g);
   lay->dims[0] = d.gx; lay->dims[1] = d.gy; lay->dims[2] = d.gxc; lay->dims[3] = ix->n_polys;
   const int64_t st[9] = {ix->n_cells, ix->n_entries, ix->n_boundary, ix->n_records, ix->n_slow, ix->blob_bytes,
-                         ix->n_inline, ix->max_bnd_per_cell, ix->max_ent_per_cell};
+                         ix->n_compact, ix->max_bnd_per_cell, ix->max_ent_per_cell};
   memcpy(lay->stats, st, sizeof st);
   lay->version = GM_PIP_LAYOUT_VERSION;
   return GM_OK;
@@ -1780,9 +1762,8 @@ int gm_pip_index_import(gm_ctx* ctx, const gm_pip_index_layout* lay, void* const
   ix->ctx = ctx;
   const void** dst[GM_PIP_INDEX_ARRAYS] = {(const void**)&ix->dev.rings, (const void**)&ix->dev.slab_off,
                                            (const void**)&ix->dev.slab_edges, (const void**)&ix->dev.cell_word,
-                                           (const void**)&ix->dev.coarse_word, (const void**)&ix->dev.vxy,
-                                           (const void**)&ix->dev.list_ent, (const void**)&ix->dev.blob,
-                                           (const void**)&ix->dev.vpoly, (const void**)&ix->dev.rblob};
+                                           (const void**)&ix->dev.coarse_word, (const void**)&ix->dev.compact,
+                                           (const void**)&ix->dev.list_ent, (const void**)&ix->dev.blob};
   for (int k = 0; k < GM_PIP_INDEX_ARRAYS; ++k) {
     void* p = nullptr;
     if (hipMalloc(&p, (size_t)std::max<int64_t>(lay->bytes[k], 16)) != hipSuccess) {
@@ -1806,7 +1787,7 @@ int gm_pip_index_import(gm_ctx* ctx, const gm_pip_index_layout* lay, void* const
   ix->n_polys = lay->dims[3];
   ix->n_cells = lay->stats[0]; ix->n_entries = lay->stats[1]; ix->n_boundary = lay->stats[2];
   ix->n_records = lay->stats[3]; ix->n_slow = lay->stats[4]; ix->blob_bytes = lay->stats[5];
-  ix->n_inline = lay->stats[6]; ix->max_bnd_per_cell = lay->stats[7]; ix->max_ent_per_cell = lay->stats[8];
+  ix->n_compact = lay->stats[6]; ix->max_bnd_per_cell = lay->stats[7]; ix->max_ent_per_cell = lay->stats[8];
   int rc = make_list_poly(ix);
   if (!rc && hipStreamSynchronize(ctx->stream) != hipSuccess) rc = hip_fail(hipErrorLaunchFailure, "gm_pip_index_import");
   if (rc) { gm_pip_index_destroy(ix); return rc; }
@@ -1822,7 +1803,7 @@ int gm_pip_index_stats(const gm_pip_index* ix, int64_t* stats) {
   stats[3] = ix->n_records;
   stats[4] = ix->n_slow;
   stats[5] = ix->blob_bytes;
-  stats[6] = ix->n_inline;
+  stats[6] = ix->n_compact;
   return GM_OK;
 }
 

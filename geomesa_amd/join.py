@@ -131,12 +131,12 @@ class PolygonIndex:
         return self
 
     def stats(self):
-        """Index statistics: cells, (cell, polygon) entries, boundary entries, generic-blob ring records
-        (MultiPolygons), slow-walk records, blob bytes, boundary entries inline in the cell word."""
+        """Index statistics: cells, (cell, polygon) entries, boundary entries, ring records,
+        slow-walk records, blob bytes, compact blobs."""
         import numpy as np
         st = np.zeros(7, np.int64)
         check(self.ctx.lib.gm_pip_index_stats(self._h, st.ctypes.data), "gm_pip_index_stats")
-        return dict(zip(["cells", "entries", "boundary", "records", "slow", "blob_bytes", "inline"], st.tolist()))
+        return dict(zip(["cells", "entries", "boundary", "records", "slow", "blob_bytes", "compact"], st.tolist()))
 
     MODES = {"auto": _lib.GM_JOIN_AUTO, "direct": _lib.GM_JOIN_DIRECT, "partitioned": _lib.GM_JOIN_PARTITIONED,
              "split": _lib.GM_JOIN_SPLIT}

@@ -236,9 +236,8 @@ int gm_pip_index_create(gm_ctx* ctx, const gm_polyset* polys, gm_pip_index** out
    L2-resident) */
 int gm_pip_index_create_ex(gm_ctx* ctx, const gm_polyset* polys, int cells_per_poly, gm_pip_index** out);
 int gm_pip_index_destroy(gm_pip_index* index);
-/* index statistics: stats[0..6] = cells, (cell, polygon) entries, boundary entries, generic-blob ring
-   records (MultiPolygons), ring records that fall back to the slab walk, blob bytes, boundary entries
-   held inline in the cell word */
+/* index statistics: stats[0..6] = cells, (cell, polygon) entries, boundary entries, ring records,
+   ring records that fall back to the slab walk, boundary blob bytes, compact (one-line) blobs */
 int gm_pip_index_stats(const gm_pip_index* index, int64_t* stats);
 
 /* A built index as device arrays, for shipping it to the other GPUs of a join (RCCL broadcast) instead
@@ -248,8 +247,8 @@ int gm_pip_index_stats(const gm_pip_index* index, int64_t* stats);
    caller buffer of layout.bytes[k] bytes (stream-ordered); gm_pip_index_import builds an index on
    ctx's device from the layout and device copies of the arrays (the library copies them: the caller
    keeps ownership of `arrays`). */
-#define GM_PIP_INDEX_ARRAYS 10
-#define GM_PIP_LAYOUT_VERSION 2
+#define GM_PIP_INDEX_ARRAYS 8
+#define GM_PIP_LAYOUT_VERSION 1
 typedef struct {
   int32_t version;                       /* GM_PIP_LAYOUT_VERSION */
   int32_t dims[4];                       /* grid columns, rows, coarse columns, polygons */
