@@ -116,6 +116,15 @@ def load_pmc(name, n):
     return None
 
 
+def load_profile(name, n):
+    """A committed per-launch PMC record (profiles/pmc_traffic.json) when it was taken at this size."""
+    try:
+        d = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))[name]
+        return d if int(d["n"]) == int(n) else None
+    except Exception:
+        return None
+
+
 def roofline(bytes_per_launch, ms, traffic=None):
     gbs = bytes_per_launch / (ms * 1e-3) / 1e9
     return {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -178,6 +187,42 @@ def cpu_join_baseline(seconds, ps):
                       "pair, %d pthreads): %.2f s, %d matches" % (n, ps.n_polys, nt, dt, len(pt))}
 
 
+def cpu_ranges_baseline(kind, q, t, max_ranges, gpu_ms, nq):
+    """The oracle's range decomposition of the same queries on the host's cores (all of them: the
+    nodes-checked total is the work measure of the GPU batch too, SURVEY 8(d) ranges() row)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    nt = cpu_threads()
+    t0 = time.time()
+    r, nodes = O.ranges_batch(kind, q, t, max_ranges=max_ranges, nthreads=nt)
+    dt = time.time() - t0
+    return {"cpu_baseline": {"value": nq / dt, "unit": "queries/s", "cores": nt, "kind": "port",
+                             "sample": "all %d queries through the C restatement (%d pthreads): %.2f s, %d ranges"
+                                       % (nq, nt, dt, r)},
+            "nodes_checked": nodes, "nodes_checked_per_s": nodes / (gpu_ms * 1e-3),
+            "cpu_ranges": r}
+
+
+def sort_bytes(b, z, n):
+    """Algorithmic bytes of gm_sort_keys over n rows: the all-digit histogram read (10 B/row), per
+    non-constant byte digit a histogram read of its column (8 B z / 2 B bin) and a scatter that reads
+    and writes z, bin and the 4-B permutation (none read on the first pass), then the 4 -> 8 B widening
+    of the permutation.  Returns (bytes, passes)."""
+    import torch
+    passes = []
+    for p in range(8):
+        d = (z >> (8 * p)) & 255
+        if int(d.min()) != int(d.max()):
+            passes.append(8)
+    bb = b.to(torch.int32) & 0xFFFF
+    for p in range(2):
+        d = (bb >> (8 * p)) & 255
+        if int(d.min()) != int(d.max()):
+            passes.append(2)
+    total = 10.0 * n + sum(h + 28.0 for h in passes) * n - (4.0 * n if passes else 0) + 12.0 * n
+    return total, len(passes)
+
+
 def gather_pairs(dist, ptids, plids, k):
     """Result gather of the join: per-rank pair counts, then every rank's
     (point id, polygon id) pairs to rank 0 over RCCL (shard.gather_rows), timed max over ranks.
@@ -220,6 +265,7 @@ def bench_table(a, dist, ctx, b, z):
     def sort_step():
         _lib.check(lib.gm_sort_keys(h, None, P(bs), P(zs), NT, None, P(ob), P(oz), P(perm)), "gm_sort_keys")
     ms_sort = timed(dist, sort_step, 3, 1)
+    sbytes, npass = sort_bytes(bs, zs, NT)
     tb = Z3Table.__new__(Z3Table)   # wrap the sorted columns without re-sorting
     tb.ks, tb.ctx, tb.n, tb.bin, tb.z, tb.perm, tb.shard, tb.shards = Z3IndexKeySpace(), ctx, NT, ob, oz, perm, None, None
     ks = tb.ks
@@ -241,8 +287,12 @@ def bench_table(a, dist, ctx, b, z):
     del ob, oz, perm, ids
     return {
         "sort_keys": {"value": NT * dist.world / (ms_sort * 1e-3), "unit": "rows/s", "ms_per_step": ms_sort,
-                      "rows_per_gpu": NT, "roofline": None,
-                      "note": "stable LSD radix sort of (bin, z) into table byte order (ingest side)"},
+                      "rows_per_gpu": NT, "digit_passes": npass,
+                      "roofline": dict(roofline(sbytes, ms_sort), bytes_per_unit=round(sbytes / NT, 2),
+                                       kernel="gm_sort_keys (all launches of one sort)"),
+                      "note": "stable LSD radix sort of (bin, z) into table byte order (ingest side); bytes = "
+                              "10 B/row digit census + per pass (digit column read + 28 B/row scatter) + 12 B/row "
+                              "permutation widening"},
         "table_query": {"value": dist.world / (ms_scan * 1e-3), "unit": "queries/s", "ms_per_step": ms_scan,
                         "rows_per_gpu": NT, "ranges": nr, "rows_scanned": ns.value, "matches": nm.value,
                         "plan_ms": round(plan_ms, 2),
@@ -419,6 +469,25 @@ def main():
                                      "ranges": int(offs[-1]),
                                      "note": "C-ABI call incl. H2D of windows and D2H of ranges (pinned host output); 100k XZ2 query "
                                              "windows (0.01-20 deg), maxRanges 2000, g = 12"}
+        if dist.rank == 0 and not a.no_cpu:
+            extra["xz2_ranges_batch"].update(cpu_ranges_baseline("xz2", win.reshape(nq, 4), None, 2000, dt * 1e3, nq))
+        # batched XZ3 ranges (configs[4]): the same windows x a time window inside the week (1 min .. 2 days)
+        tw0 = rng.uniform(0, 604800 - 172800, nq)
+        tw1 = tw0 + 10 ** rng.uniform(np.log10(60), np.log10(172800), nq)
+        win3 = np.ascontiguousarray(np.stack([win.reshape(nq, 4)[:, 0], win.reshape(nq, 4)[:, 1], tw0,
+                                              win.reshape(nq, 4)[:, 2], win.reshape(nq, 4)[:, 3], tw1], 1).reshape(-1))
+        args3 = (h, nq, woff.ctypes.data, win3.ctypes.data, 12, 1, 2000)
+        offs, rr, _ = R.call_raw(lib.gm_xz3_ranges, args3, nq, nq * 256, pinned=True)
+        t0w = time.time()
+        for _ in range(3):
+            offs, rr, _ = R.call_raw(lib.gm_xz3_ranges, args3, nq, int(offs[-1]) + 1024, pinned=True)
+        dt = (time.time() - t0w) / 3
+        extra["xz3_ranges_batch"] = {"value": nq * dist.world / dt, "unit": "queries/s", "ms_per_step": dt * 1e3,
+                                     "ranges": int(offs[-1]),
+                                     "note": "C-ABI call incl. H2D of windows and D2H of ranges (pinned host output); 100k XZ3 query "
+                                             "windows (0.01-20 deg x 1 min-2 days, week period), maxRanges 2000, g = 12"}
+        if dist.rank == 0 and not a.no_cpu:
+            extra["xz3_ranges_batch"].update(cpu_ranges_baseline("xz3", win3.reshape(nq, 6), None, 2000, dt * 1e3, nq))
         del rr
         # batched ranges (configs[4]/[0]): 4096 Z3 queries with target 2000
         rng = np.random.default_rng(1)
@@ -438,6 +507,10 @@ def main():
                                     "ms_per_step": dt * 1e3, "ranges": int(offs[-1]),
                                     "note": "C-ABI call incl. H2D of queries and D2H of ranges (pinned host output); 4096 Z3 queries "
                                             "(0.2-20 deg boxes x 1 day), maxRanges 2000 (ScanRangesTarget)"}
+        if dist.rank == 0 and not a.no_cpu:
+            qb = np.array([q[0][0] for q in qs], np.float64)
+            qt = np.array([q[1][0] for q in qs], np.int64)
+            extra["z3_ranges_batch"].update(cpu_ranges_baseline("z3", qb, qt, 2000, dt * 1e3, len(qs)))
     # ---------------------------------------------------------------- sorted table: ingest sort + seek-and-filter
     if "table" in only and not a.no_extra:
         extra.update(bench_table(a, dist, ctx, b, z))
@@ -487,6 +560,26 @@ def main():
               "workload": "st_contains(polygon, point) join, %d CONUS points/GPU x %d synthetic county polygons "
                           "(BASELINE configs[3]); polygon set broadcast over RCCL when N > 1" % (J, ps.n_polys)}
         pj["roofline"]["bytes_per_unit"] = "16 B/point + 12 B/pair"
+        # FP64 work: E_c = the edges of every (point, polygon) pair whose envelope test
+        # passes, counted by the C restatement over a prefix of the same device point stream, scaled;
+        # 7 FP64 ops per candidate edge is the reference walk's orientation arithmetic
+        if dist.rank == 0 and not a.no_cpu:
+            sys.path.insert(0, os.path.join(ROOT, "oracle"))
+            import oracle as O
+            ns = min(J, 20_000_000)
+            _, _, ec = O.OraclePolySet(*ps.to_arrays()).join(px[:ns].cpu().numpy(), py[:ns].cpu().numpy(),
+                                                            nthreads=cpu_threads(), with_edges=True)
+            ec_total = ec * (J / ns)
+            fl = 7.0 * ec_total * dist.world
+            pj["roofline"]["fp64"] = {"e_c_per_point": ec / ns, "e_c": ec_total, "flops": fl,
+                                      "achieved_tflops": fl / (jms * 1e-3) / 1e12, "peak_tflops": FP64_PEAK_TFLOPS,
+                                      "fp64_frac": fl / (jms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS,
+                                      "sample": "E_c counted by the oracle over the first %d of the %d points, scaled" % (ns, J),
+                                      "note": "the reference's per-pair RayCrossingCounter work (7 FP64 ops x E_c); the "
+                                              "grid index resolves most pairs without it, so a fraction > 1 is work avoided"}
+            fpm = load_profile("pip_join_fp64", J)
+            if fpm:
+                pj["roofline"]["fp64"]["sq_insts_valu_flops_fp64"] = fpm["sq_insts_valu_flops_fp64"]
         # row-wise st_contains (the UDF path without the join rule): row i = (its cell's county, point i)
         x0c, y0c, x1c, y1c = CONUS
         rid = (torch.clamp(((py - y0c) / (y1c - y0c) * gy).long(), 0, gy - 1) * gx +
@@ -498,9 +591,10 @@ def main():
             if rc:
                 _lib.check(rc, "gm_pip_relate")
         rms = timed(dist, relate_step, max(3, a.join_steps), 1)
+        rp = load_profile("pip_relate", J)
         pj["row_predicate"] = {"value": J * dist.world / (rms * 1e-3), "unit": "rows/s", "ms_per_step": rms,
                                "contains": int(dist.sum(int((loc == 2).sum()))),
-                               "roofline": roofline(21.0 * J, rms, load_pmc("pip_relate", J)),
+                               "roofline": roofline(21.0 * J, rms, rp["bytes_per_launch"] if rp else None),
                                "workload": "st_contains(polygon_i, point_i) row by row over the join's points, "
                                            "polygon_i = the county of the point's grid cell (21 B/row: 16 point + 4 id + 1 out)"}
         del rid, loc

@@ -231,6 +231,16 @@ static int64_t sort_merge(rvec* r, gmo_range* out, int64_t cap) {
   return m <= cap ? m : -m;
 }
 
+/* tree nodes checked by the range decompositions on this thread (ZN.checkValue calls, XZ elements
+   tested for containment / overlap): the work measure of SURVEY 8(d)'s ranges() row */
+static __thread int64_t g_nodes_checked;
+
+int64_t gmo_nodes_checked(void) {
+  const int64_t v = g_nodes_checked;
+  g_nodes_checked = 0;
+  return v;
+}
+
 /* ZN.zranges (ZN.scala:110-242) */
 int64_t gmo_zranges(int dims, const int64_t* bounds, int nb, int precision, int max_ranges,
                     int max_recurse, gmo_range* out, int64_t cap) {
@@ -250,6 +260,7 @@ int64_t gmo_zranges(int dims, const int64_t* bounds, int nb, int precision, int 
 #define IS_OVERLAPPED(mn, mx, res) do { res = 0; for (int _i = 0; _i < nb; _i++) \
     if (gmo_zn_overlaps(dims, bounds[2*_i], bounds[2*_i+1], mn, mx)) { res = 1; break; } } while (0)
 #define CHECK_VALUE(pfx, quad) do { \
+    g_nodes_checked++; \
     int64_t _mn = (pfx) | jshl((quad), offset); \
     int64_t _mx = _mn | (jshl(1, offset) - 1); \
     int _c; IS_CONTAINED(_mn, _mx, _c); \
@@ -763,6 +774,7 @@ static int64_t xz_ranges_norm(int dims, int g, const double* win, int nq, int64_
     if (next.term) {
       if ((q.tail - q.head) > 0) { level += 1; xq_push(&q, &term); }
     } else {
+      g_nodes_checked++;
       int contained = 0, overlapped = 0;
       for (int i = 0; i < nq && !contained; i++) {
         const double* w = win + 2 * dims * i;  /* mins then maxs */
@@ -1258,4 +1270,59 @@ int64_t gmo_pip_join_ex(const gmo_polyset* ps, const double* px, const double* p
   }
   free(tasks); free(th); free(cell_poly); free(fill); free(cnt); free(env); free(pedges);
   return total <= cap ? total : -total;
+}
+
+/* ---- batch timing of the range decompositions (the bench's CPU baseline): nq single-box queries on
+   nthreads pthreads, outputs discarded; totals of merged ranges and nodes checked */
+typedef struct {
+  int kind, period, g, max_ranges, pad;  /* kind 3 = Z3, 12 = XZ2, 13 = XZ3 */
+  const double* q; const int64_t* t;
+  int64_t lo, hi, ranges, nodes;
+} rbatch_task;
+
+static void* rbatch_worker(void* arg) {
+  rbatch_task* k = (rbatch_task*)arg;
+  int64_t cap = 1 << 16;
+  gmo_range* out = (gmo_range*)malloc(sizeof(gmo_range) * (size_t)cap);
+  g_nodes_checked = 0;
+  for (int64_t i = k->lo; i < k->hi; i++) {
+    int64_t m;
+    for (;;) {
+      if (k->kind == 3) m = gmo_z3_ranges(k->period, 21, k->q + 4 * i, 1, k->t + 2 * i, 1, 64, k->max_ranges, out, cap);
+      else if (k->kind == 12) m = gmo_xz2_ranges(k->g, k->q + 4 * i, 1, k->max_ranges, out, cap);
+      else m = gmo_xz3_ranges(k->g, k->period, k->q + 6 * i, 1, k->max_ranges, out, cap);
+      if (m < 0 && m > -(INT64_C(1) << 62)) {   /* capacity: grow and redo */
+        cap = -m;
+        out = (gmo_range*)realloc(out, sizeof(gmo_range) * (size_t)cap);
+        g_nodes_checked = 0;
+        continue;
+      }
+      break;
+    }
+    if (m > 0) k->ranges += m;
+  }
+  k->nodes = g_nodes_checked;
+  free(out);
+  return NULL;
+}
+
+int gmo_ranges_batch(int kind, int period, int g, const double* q, const int64_t* t, int64_t nq, int max_ranges,
+                     int nthreads, int64_t* total_ranges, int64_t* total_nodes) {
+  if (nthreads < 1) nthreads = 1;
+  rbatch_task* tasks = (rbatch_task*)calloc((size_t)nthreads, sizeof(rbatch_task));
+  pthread_t* th = (pthread_t*)calloc((size_t)nthreads, sizeof(pthread_t));
+  const int64_t chunk = (nq + nthreads - 1) / nthreads;
+  for (int k = 0; k < nthreads; k++) {
+    rbatch_task* x = &tasks[k];
+    x->kind = kind; x->period = period; x->g = g; x->max_ranges = max_ranges; x->q = q; x->t = t;
+    x->lo = (int64_t)k * chunk; x->hi = x->lo + chunk < nq ? x->lo + chunk : nq;
+    if (x->lo > nq) x->lo = nq;
+    pthread_create(&th[k], NULL, rbatch_worker, x);
+  }
+  int64_t r = 0, nd = 0;
+  for (int k = 0; k < nthreads; k++) { pthread_join(th[k], NULL); r += tasks[k].ranges; nd += tasks[k].nodes; }
+  if (total_ranges) *total_ranges = r;
+  if (total_nodes) *total_nodes = nd;
+  free(tasks); free(th);
+  return 0;
 }

@@ -137,6 +137,10 @@ int64_t gmo_pip_join(const gmo_polyset* ps, const double* px, const double* py, 
 int64_t gmo_pip_join_ex(const gmo_polyset* ps, const double* px, const double* py, int64_t n,
                         int64_t* pt_ids, int32_t* poly_ids, int64_t cap, int nthreads, int op, int64_t* cand_edges);
 
+/* range decomposition work counter (per thread, read-and-reset) and the batch timing driver */
+int64_t gmo_nodes_checked(void);
+int     gmo_ranges_batch(int kind, int period, int g, const double* q, const int64_t* t, int64_t nq, int max_ranges,
+                         int nthreads, int64_t* total_ranges, int64_t* total_nodes);
 #ifdef __cplusplus
 }
 #endif

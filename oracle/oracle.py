@@ -93,6 +93,9 @@ def lib():
             "gmo_intersects": (ctypes.c_int, [vp, ctypes.c_int, d, d]),
             "gmo_query_scan": (i64, [vp, vp, vp, i64, vp, ctypes.c_int, i64, i64, vp, ctypes.c_int, vp]),
             "gmo_pip_join": (i64, [vp, vp, vp, i64, vp, vp, i64, ctypes.c_int]),
+            "gmo_nodes_checked": (i64, []),
+            "gmo_ranges_batch": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, vp, i64, ctypes.c_int,
+                                                ctypes.c_int, vp, vp]),
             "gmo_pip_join_ex": (i64, [vp, vp, vp, i64, vp, vp, i64, ctypes.c_int, ctypes.c_int, vp]),
         }
         for name, (res, args) in sig.items():
@@ -202,6 +205,24 @@ def z2_ranges(xy, precision=64, max_ranges=None):
     a = np.ascontiguousarray(np.asarray(xy, dtype=np.float64).reshape(-1))
     mr = 2147483647 if max_ranges is None else max_ranges
     return _ranges_call(lib().gmo_z2_ranges, 31, _p(a), len(a) // 4, precision, mr)
+
+
+def nodes_checked():
+    """Tree nodes the range decompositions checked on this thread since the last call."""
+    return lib().gmo_nodes_checked()
+
+
+def ranges_batch(kind, q, t=None, max_ranges=2000, nthreads=1, g=12, period=WEEK):
+    """Times-able batch of single-box queries: kind "z3" (q = n x 4 boxes, t = n x 2 offsets), "xz2"
+    (n x 4 windows) or "xz3" (n x 6).  Returns (total merged ranges, total nodes checked)."""
+    qa = np.ascontiguousarray(np.asarray(q, np.float64))
+    ta = np.ascontiguousarray(np.asarray(t if t is not None else [0, 0], np.int64))
+    k = {"z3": 3, "xz2": 12, "xz3": 13}[kind]
+    nq = qa.shape[0]
+    r, nd = ctypes.c_int64(), ctypes.c_int64()
+    lib().gmo_ranges_batch(k, period, g, _p(qa), _p(ta), nq, 2147483647 if max_ranges is None else max_ranges,
+                           nthreads, ctypes.byref(r), ctypes.byref(nd))
+    return r.value, nd.value
 
 
 def xz2_ranges(queries, max_ranges=None, g=12):

@@ -25,11 +25,12 @@ STREAMING = {
     "z3filter_scan": ("k_z3filter_mask_v", "points", 10.125),
     "xz2_index": ("k_xz2_index_v", "xz", 40.0),
     "z3_histogram": ("k_z3_hist_lds<", "points", 24.0),
+    "pip_relate": ("k_pip_relate", "points", 21.0),
 }
 # join step kernels and the points per dispatch: direct = one pass per 2^31 points, partitioned =
 # hist + scan + scatter + join per 2^28-point chunk
-JOIN_MODES = {"direct": (["k_pip_join<true, false>"], 1 << 31),
-              "partitioned": (["k_band_hist", "k_band_scan", "k_band_scatter", "k_pip_join<true, true>"], 1 << 28)}
+JOIN_MODES = {"direct": (["k_pip_join<true, false, false"], 1 << 31),
+              "partitioned": (["k_band_hist", "k_band_scan", "k_band_scatter", "k_pip_join<true, true, false"], 1 << 28)}
 
 
 def per_dispatch(root):
@@ -81,6 +82,11 @@ def main(root, out, points=1_000_000_000, join_points=1_000_000_000):
                                "bytes_per_launch": total, "bytes_raw": total_raw,
                                "note": "whole join step; FETCH_SIZE doubled (exact for the streaming point reads, "
                                        "uncalibrated for the index gathers: raw value in bytes_raw)"}
+    # FP64 VALU work of the join (SQ_INSTS_VALU_FLOPS_FP64 pass), per launch
+    fp = mean_for(d, "k_pip_join<true, false, false", "SQ_INSTS_VALU_FLOPS_FP64")
+    if fp is not None:
+        res["pip_join_fp64"] = {"n": join_points, "sq_insts_valu_flops_fp64": fp,
+                                "note": "rocprofv3 SQ_INSTS_VALU_FLOPS_FP64 per dispatch of the direct join kernel"}
     json.dump(res, open(out, "w"), indent=1, sort_keys=True)
     for k, v in res.items():
         print("%-14s %8.2f GB/launch" % (k, v["bytes_per_launch"] / 1e9))
