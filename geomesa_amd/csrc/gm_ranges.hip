@@ -21,10 +21,13 @@
 //
 // Frontier and range lists live in per-query global workspaces (HBM is plentiful); the zbounds /
 // normalized query windows sit in LDS.
+#include <string.h>
+
 #include <algorithm>
 #include <vector>
 
 #include "gm_internal.hpp"
+#include "gm_scan.hpp"
 
 namespace gm {
 
@@ -100,22 +103,76 @@ __device__ void bitonic(K* key, I* idx, int P) {
   }
 }
 
-// sort the n ranges of this query by lower and merge adjacent ones into out (ZN.scala:221-241);
-// returns the merged count (same on every thread)
+constexpr int MAXRUNS = 64;   // sorted runs merged by rank; more fall back to the bitonic sort
+
+// rank of `key` among run [lo, hi) of keys: elements < key (or <= key when `le`)
+__device__ __forceinline__ int run_rank(const int64_t* keys, int lo, int hi, int64_t key, bool le) {
+  int a = lo, b = hi;
+  while (a < b) {
+    const int m = (a + b) >> 1;
+    const int64_t v = keys[m];
+    if (v < key || (le && v == key)) a = m + 1;
+    else b = m;
+  }
+  return a - lo;
+}
+
+// Sort the n ranges of this query by lower and merge adjacent ones into out (ZN.scala:221-241);
+// returns the merged count (same on every thread).  The walk emits each tree level in curve order
+// (children are generated in quadrant order from a curve-ordered frontier, and bottom-out appends
+// ordered frontiers), so the list is a concatenation of a few ascending runs: they are merged by
+// rank -- each range's sorted position is its offset in its run plus its rank in every other run,
+// found by binary search (stable: ties rank after earlier runs) -- with one barrier.  A list with
+// more than MAXRUNS runs takes the bitonic sort.
 __device__ int sort_merge(const int64_t* rlo, const int64_t* rhi, const uint8_t* rc, int n, int64_t* gkey,
                           int32_t* gidx, gm_range* out, int64_t* s_key, int16_t* s_idx, int64_t* s_tmp) {
+  __shared__ int s_run[MAXRUNS + 1];
+  __shared__ int s_nrun;
   if (n == 0) return 0;
-  int P = 1;
-  while (P < n) P <<= 1;
-  const bool lds = P <= LDS_SORT;
-  for (int i = threadIdx.x; i < P; i += RTPB) {
-    const int64_t k = i < n ? rlo[i] : INT64_MAX;
-    if (lds) { s_key[i] = k; s_idx[i] = (int16_t)i; }
-    else { gkey[i] = k; gidx[i] = i; }
+  const bool lds = n <= LDS_SORT;
+  // run starts: rlo[j] < rlo[j - 1]
+  if (threadIdx.x == 0) { s_run[0] = 0; s_nrun = 1; }
+  __syncthreads();
+  int64_t nrun = 1;
+  for (int c = 0; c < n && nrun <= MAXRUNS; c += RTPB) {
+    const int j = c + threadIdx.x;
+    const int f = (j > 0 && j < n && rlo[j] < rlo[j - 1]) ? 1 : 0;
+    int64_t tot;
+    const int64_t ex = block_exscan(f, s_tmp, tot);
+    if (f && nrun + ex < MAXRUNS) s_run[nrun + ex] = j;
+    nrun += tot;
+    if (lds && j < n) s_key[j] = rlo[j];
   }
   __syncthreads();
-  if (lds) bitonic(s_key, s_idx, P);
-  else bitonic(gkey, gidx, P);
+  if (nrun <= MAXRUNS) {
+    const int R = (int)nrun;
+    if (threadIdx.x == 0) s_run[R] = n;
+    __syncthreads();
+    const int64_t* keys = lds ? s_key : rlo;
+    for (int j = threadIdx.x; j < n; j += RTPB) {
+      int r = 0;
+      while (r + 1 < R && s_run[r + 1] <= j) ++r;   // R is small: linear scan
+      const int64_t key = keys[j];
+      int pos = j - s_run[r];
+      for (int r2 = 0; r2 < R; ++r2)
+        if (r2 != r) pos += run_rank(keys, s_run[r2], s_run[r2 + 1], key, r2 < r);
+      if (lds) s_idx[pos] = (int16_t)j;
+      else gidx[pos] = j;
+    }
+    __syncthreads();
+  } else {
+    int P = 1;
+    while (P < n) P <<= 1;
+    const bool lp = P <= LDS_SORT;
+    for (int i = threadIdx.x; i < P; i += RTPB) {
+      const int64_t k = i < n ? rlo[i] : INT64_MAX;
+      if (lp) { s_key[i] = k; s_idx[i] = (int16_t)i; }
+      else { gkey[i] = k; gidx[i] = i; }
+    }
+    __syncthreads();
+    if (lp) bitonic(s_key, s_idx, P);
+    else bitonic(gkey, gidx, P);
+  }
   // run starts: lower > previous upper + 1 (Java long wrap); sorted disjoint ranges have increasing
   // uppers, so the previous upper is the merged run's max (ZN.scala:228-230)
   int64_t* run_of = lds ? s_key : gkey;  // keys are dead after the sort: reuse for run ids
@@ -157,6 +214,40 @@ __device__ int sort_merge(const int64_t* rlo, const int64_t* rhi, const uint8_t*
   return total_runs;
 }
 
+// Batch output: every query's merged ranges are appended to one device buffer (one atomic per query)
+// with their (start, count) recorded by query index; the host driver then scans the counts and
+// gathers the buffer into query order.  Phase 2 re-runs the queries whose first-pass workspace
+// overflowed, through qmap.
+struct BatchOut {
+  const int32_t* qmap;           // block -> query index (phase 2), null: q0 + block
+  int64_t ocap;                  // stride of the per-block merged scratch (a.out), ranges
+  gm_range* dbuf;                // batch buffer
+  int64_t dcap;
+  unsigned long long* total;
+  int64_t* start;                // per query
+  int32_t* count;
+  int32_t* status;
+};
+
+__device__ __forceinline__ int64_t batch_query(const BatchOut& bo, int64_t q0, int64_t qc) {
+  return bo.qmap ? (int64_t)bo.qmap[qc] : q0 + qc;
+}
+
+// record a query's result (every thread of the block calls it; `ws` = its m merged ranges)
+__device__ void batch_finish(const BatchOut& bo, int64_t q, int m, int status, const gm_range* ws) {
+  __shared__ unsigned long long s_base;
+  if (threadIdx.x == 0) {
+    s_base = (status == QS_OK && m > 0) ? atomicAdd(bo.total, (unsigned long long)m) : 0ull;
+    bo.start[q] = (int64_t)s_base;
+    bo.count[q] = status == QS_OK ? m : 0;
+    bo.status[q] = status;
+  }
+  __syncthreads();
+  if (status == QS_OK)
+    for (int j = threadIdx.x; j < m; j += RTPB)
+      if ((int64_t)s_base + j < bo.dcap) bo.dbuf[s_base + j] = ws[j];
+}
+
 // ------------------------------------------------------------------ Z ranges kernel
 
 struct ZRangesArgs {
@@ -170,16 +261,14 @@ struct ZRangesArgs {
   NDim lon, lat, tim;
   int range_precision, range_stop, recurse_stop;
   int64_t fcap, rcap;
-  int64_t* fa;              // frontier ping
-  int64_t* fb;              // frontier pong
+  int64_t* fa;              // frontier ping / pong, 2 x fcap per query
   int64_t* rlo;
   int64_t* rhi;
   uint8_t* rc;
   int64_t* gkey;
   int32_t* gidx;
-  gm_range* out;            // merged ranges, rcap per query
-  int32_t* out_count;
-  int32_t* status;
+  gm_range* out;            // merged ranges scratch, bo.ocap per block
+  BatchOut bo;
 };
 
 template <int D>
@@ -194,9 +283,9 @@ __global__ __launch_bounds__(RTPB) void k_zranges(ZRangesArgs a) {
   __shared__ int16_t s_idx[LDS_SORT];
 
   const int64_t qc = blockIdx.x;            // query within the chunk
-  const int64_t q = a.q0 + qc;
-  int64_t* F = a.fa + qc * a.fcap;
-  int64_t* G = a.fb + qc * a.fcap;
+  const int64_t q = batch_query(a.bo, a.q0, qc);
+  int64_t* F = a.fa + qc * 2 * a.fcap;      // F, G adjacent per query (the merged output aliases them)
+  int64_t* G = F + a.fcap;
   int64_t* rlo = a.rlo + qc * a.rcap;
   int64_t* rhi = a.rhi + qc * a.rcap;
   uint8_t* rc = a.rc + qc * a.rcap;
@@ -210,7 +299,7 @@ __global__ __launch_bounds__(RTPB) void k_zranges(ZRangesArgs a) {
   if (threadIdx.x == 0) s_err = (nb > MAXB) ? QS_TOO_MANY_BOUNDS : QS_OK;
   __syncthreads();
   if (s_err || nb <= 0) {
-    if (threadIdx.x == 0) { a.out_count[qc] = 0; a.status[qc] = s_err; }
+    batch_finish(a.bo, q, 0, s_err, nullptr);
     return;
   }
   // zbounds: Z3SFC.ranges builds ZRange(index(xmin, ymin, tmin), index(xmax, ymax, tmax)) for the
@@ -255,7 +344,7 @@ __global__ __launch_bounds__(RTPB) void k_zranges(ZRangesArgs a) {
   }
   __syncthreads();
   if (s_err) {
-    if (threadIdx.x == 0) { a.out_count[qc] = 0; a.status[qc] = s_err; }
+    batch_finish(a.bo, q, 0, s_err, nullptr);
     return;
   }
   // longestCommonPrefix (ZN.scala:272-281)
@@ -336,18 +425,21 @@ __global__ __launch_bounds__(RTPB) void k_zranges(ZRangesArgs a) {
         }
       }
       const int cc = __popc(cmask), co = __popc(omask);
-      int64_t cct, cot;
-      const int64_t ccx = block_exscan(cc, s_tmp, cct);
-      const int64_t cox = block_exscan(co, s_tmp, cot);
-      // budget (ZN.scala:214) after node i
-      if (threadIdx.x == 0) s_stop = INT32_MAX;
-      __syncthreads();
-      if (i < K) {
-        const int64_t f = nR + cc_carry + ccx + cc + co_carry + cox + co + (K - i - 1);
-        if (f >= range_stop) atomicMin(&s_stop, (int)threadIdx.x);
+      int64_t pt;   // one scan of (contained | overlapping << 32)
+      const int64_t px = block_exscan((int64_t)cc | ((int64_t)co << 32), s_tmp, pt);
+      const int64_t ccx = px & 0xffffffff, cox = px >> 32, cct = pt & 0xffffffff, cot = pt >> 32;
+      // budget (ZN.scala:214) after node i; bounded above by the chunk totals at its first node
+      int sl = INT32_MAX;
+      if (nR + cc_carry + cct + co_carry + cot + (K - c - 1) >= range_stop) {
+        if (threadIdx.x == 0) s_stop = INT32_MAX;
+        __syncthreads();
+        if (i < K) {
+          const int64_t f = nR + cc_carry + ccx + cc + co_carry + cox + co + (K - i - 1);
+          if (f >= range_stop) atomicMin(&s_stop, (int)threadIdx.x);
+        }
+        __syncthreads();
+        sl = s_stop;
       }
-      __syncthreads();
-      const int sl = s_stop;
       const bool emit = (i < K) && (sl == INT32_MAX || (int)threadIdx.x <= sl);
       if (emit) {
         int64_t rpos = nR + cc_carry + ccx, fpos = co_carry + cox;
@@ -414,12 +506,12 @@ __global__ __launch_bounds__(RTPB) void k_zranges(ZRangesArgs a) {
   }
   __syncthreads();
   if (err) {
-    if (threadIdx.x == 0) { a.out_count[qc] = 0; a.status[qc] = err; }
+    batch_finish(a.bo, q, 0, err, nullptr);
     return;
   }
-  const int m = sort_merge(rlo, rhi, rc, (int)nR, a.gkey + qc * a.rcap, a.gidx + qc * a.rcap, a.out + qc * a.rcap,
-                           s_key, s_idx, s_tmp);
-  if (threadIdx.x == 0) { a.out_count[qc] = m; a.status[qc] = QS_OK; }
+  gm_range* ws = a.out + qc * a.bo.ocap;
+  const int m = sort_merge(rlo, rhi, rc, (int)nR, a.gkey + qc * a.rcap, a.gidx + qc * a.rcap, ws, s_key, s_idx, s_tmp);
+  batch_finish(a.bo, q, m, QS_OK, ws);
 }
 
 }  // namespace gm
@@ -436,16 +528,14 @@ struct XZRangesArgs {
   double zhi;               // XZ3 z upper bound (maxOffset(period))
   int range_stop;
   int64_t fcap, rcap;
-  uint64_t* fa;
-  uint64_t* fb;
+  uint64_t* fa;             // frontier ping / pong, 2 x fcap per query
   int64_t* rlo;
   int64_t* rhi;
   uint8_t* rc;
   int64_t* gkey;
   int32_t* gidx;
-  gm_range* out;
-  int32_t* out_count;
-  int32_t* status;
+  gm_range* out;            // merged ranges scratch, bo.ocap per block
+  BatchOut bo;
 };
 
 // element (ix, iy[, iz]) at level L packed 30 (XZ2) / 20 (XZ3) bits per coordinate
@@ -492,9 +582,9 @@ __global__ __launch_bounds__(RTPB) void k_xzranges(XZRangesArgs a) {
   __shared__ int16_t s_idx[LDS_SORT];
 
   const int64_t qc = blockIdx.x;
-  const int64_t q = a.q0 + qc;
-  uint64_t* F = a.fa + qc * a.fcap;
-  uint64_t* G = a.fb + qc * a.fcap;
+  const int64_t q = batch_query(a.bo, a.q0, qc);
+  uint64_t* F = a.fa + qc * 2 * a.fcap;
+  uint64_t* G = F + a.fcap;
   int64_t* rlo = a.rlo + qc * a.rcap;
   int64_t* rhi = a.rhi + qc * a.rcap;
   uint8_t* rc = a.rc + qc * a.rcap;
@@ -504,7 +594,7 @@ __global__ __launch_bounds__(RTPB) void k_xzranges(XZRangesArgs a) {
   if (threadIdx.x == 0) s_err = nw > MAXB ? QS_TOO_MANY_BOUNDS : QS_OK;
   __syncthreads();
   if (s_err || nw <= 0) {
-    if (threadIdx.x == 0) { a.out_count[qc] = 0; a.status[qc] = s_err; }
+    batch_finish(a.bo, q, 0, s_err, nullptr);
     return;
   }
   // normalize windows, non-lenient (XZ2SFC.scala:132-135 / XZ3SFC.scala:142-145 -> normalize)
@@ -526,7 +616,7 @@ __global__ __launch_bounds__(RTPB) void k_xzranges(XZRangesArgs a) {
   }
   __syncthreads();
   if (s_err) {
-    if (threadIdx.x == 0) { a.out_count[qc] = 0; a.status[qc] = s_err; }
+    batch_finish(a.bo, q, 0, s_err, nullptr);
     return;
   }
 
@@ -578,15 +668,19 @@ __global__ __launch_bounds__(RTPB) void k_xzranges(XZRangesArgs a) {
         kind = cont ? 1 : (ovl ? 2 : 0);
       }
       const int ai = kind != 0, co = kind == 2 ? (1 << D) : 0;
-      int64_t at, cot;
-      const int64_t ax = block_exscan(ai, s_tmp, at);
-      const int64_t cox = block_exscan(co, s_tmp, cot);
-      // budget: element i is processed only if nR + A(i-1) < rangeStop (XZ2SFC.scala:205)
-      if (threadIdx.x == 0) s_stop = INT32_MAX;
-      __syncthreads();
-      if (i < K && nR + a_carry + ax >= range_stop) atomicMin(&s_stop, (int)threadIdx.x);
-      __syncthreads();
-      const int sl = s_stop;
+      int64_t pt;   // one scan of (ranges | children << 32)
+      const int64_t px = block_exscan((int64_t)ai | ((int64_t)co << 32), s_tmp, pt);
+      const int64_t ax = px & 0xffffffff, cox = px >> 32, at = pt & 0xffffffff, cot = pt >> 32;
+      // budget: element i is processed only if nR + A(i-1) < rangeStop (XZ2SFC.scala:205); A(i-1) <= at,
+      // so a chunk that cannot reach the stop skips the search
+      int sl = INT32_MAX;
+      if (nR + a_carry + at >= range_stop) {
+        if (threadIdx.x == 0) s_stop = INT32_MAX;
+        __syncthreads();
+        if (i < K && nR + a_carry + ax >= range_stop) atomicMin(&s_stop, (int)threadIdx.x);
+        __syncthreads();
+        sl = s_stop;
+      }
       if (i < K && (sl == INT32_MAX || (int)threadIdx.x < sl) && kind) {
         const int64_t rpos = nR + a_carry + ax;
         const int64_t fpos = co_carry + cox;
@@ -649,20 +743,22 @@ __global__ __launch_bounds__(RTPB) void k_xzranges(XZRangesArgs a) {
   }
   __syncthreads();
   if (err) {
-    if (threadIdx.x == 0) { a.out_count[qc] = 0; a.status[qc] = err; }
+    batch_finish(a.bo, q, 0, err, nullptr);
     return;
   }
-  const int m = sort_merge(rlo, rhi, rc, (int)nR, a.gkey + qc * a.rcap, a.gidx + qc * a.rcap, a.out + qc * a.rcap,
-                           s_key, s_idx, s_tmp);
-  if (threadIdx.x == 0) { a.out_count[qc] = m; a.status[qc] = QS_OK; }
+  gm_range* ws = a.out + qc * a.bo.ocap;
+  const int m = sort_merge(rlo, rhi, rc, (int)nR, a.gkey + qc * a.rcap, a.gidx + qc * a.rcap, ws, s_key, s_idx, s_tmp);
+  batch_finish(a.bo, q, m, QS_OK, ws);
 }
 
-// gather each query's merged ranges into the contiguous output
-__global__ __launch_bounds__(RTPB) void k_gather_ranges(const gm_range* __restrict__ ws, int64_t rcap,
-                                                        const int64_t* __restrict__ off, gm_range* __restrict__ out) {
-  const int64_t qc = blockIdx.x;
-  const int64_t a = off[qc], n = off[qc + 1] - a;
-  for (int64_t j = threadIdx.x; j < n; j += RTPB) out[a + j] = ws[qc * rcap + j];
+// gather every query's ranges from the batch buffer into query order (one block per query)
+__global__ __launch_bounds__(RTPB) void k_gather_ranges(const gm_range* __restrict__ buf, const int64_t* __restrict__ start,
+                                                        const int64_t* __restrict__ off, int64_t nq,
+                                                        gm_range* __restrict__ out) {
+  for (int64_t q = blockIdx.x; q < nq; q += gridDim.x) {
+    const int64_t a = off[q], n = off[q + 1] - a, s = start[q];
+    for (int64_t j = threadIdx.x; j < n; j += RTPB) out[a + j] = buf[s + j];
+  }
 }
 
 // ------------------------------------------------------------------ host driver
@@ -687,82 +783,142 @@ int to_dev(gm_ctx* ctx, const T* h, size_t n, T** d) {
   return copy_h2d(ctx, *d, h, n * sizeof(T));
 }
 
-// shared driver: per chunk of queries allocate workspaces, launch, read counts, gather, copy out
+// Shared driver.  Phase 1 runs every query with small workspaces (frontier / range lists of P1CAP,
+// sorted in LDS), chunked only by a memory budget and launched back to back (the chunks reuse one
+// stream-ordered workspace, no host round trip); the merged-range scratch aliases the frontier.
+// Phase 2 re-runs the queries that overflowed it (status QS_CAPACITY) with the worst-case caps.
+// Then the counts are scanned on the device, the batch buffer is gathered into query order and the
+// result comes back in one copy.
+constexpr int64_t P1CAP = LDS_SORT;
+
 template <class LaunchFn>
 int run_ranges(gm_ctx* ctx, int64_t nq, int64_t fcap, int64_t rcap, size_t felem, LaunchFn launch, int64_t* out_off,
                gm_range* out, int64_t cap, int64_t* needed, int32_t* query_status) {
   hipStream_t s = ctx->stream;
   rcap = next_pow2(std::max<int64_t>(rcap, 16));
-  // chunk so that the workspace stays within min(4 GiB, 1/4 of free HBM): the worst-case caps per
-  // query are large but mostly untouched, and fewer chunks mean fewer launches and host syncs
-  const int64_t per_q = fcap * (int64_t)felem * 2 + rcap * (8 + 8 + 1 + 8 + 4 + (int64_t)sizeof(gm_range));
+  auto al = [](size_t v) { return (v + 15) & ~(size_t)15; };
   size_t free_b = 0, total_b = 0;
   int64_t budget = (int64_t)2 << 30;
   if (hipMemGetInfo(&free_b, &total_b) == hipSuccess)
-    budget = std::max<int64_t>(budget, std::min<int64_t>((int64_t)4 << 30, (int64_t)(free_b / 4)));
-  int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(nq, budget / std::max<int64_t>(per_q, 1)));
-  chunk = std::min<int64_t>(chunk, 65535);
-  std::vector<int32_t> counts((size_t)nq), stats((size_t)nq);
-  std::vector<int64_t> offs((size_t)nq + 1, 0);
-  out_off[0] = 0;
-  int64_t total = 0;
-  bool overflow = false;
-  for (int64_t q0 = 0; q0 < nq; q0 += chunk) {
-    const int64_t m = std::min(chunk, nq - q0);
-    char *fa, *fb;
-    int64_t *rlo, *rhi, *gkey, *doff;
-    uint8_t* rc;
-    int32_t *gidx, *dcnt, *dst;
-    gm_range *ws, *dout;
-    {  // one context-owned workspace, carved into the per-chunk arrays (16-B aligned pieces)
-      const size_t sizes[10] = {(size_t)(m * fcap) * felem, (size_t)(m * fcap) * felem, (size_t)(m * rcap) * 8,
-                                (size_t)(m * rcap) * 8,     (size_t)(m * rcap),          (size_t)(m * rcap) * 8,
-                                (size_t)(m * rcap) * 4,     (size_t)(m * rcap) * sizeof(gm_range),
-                                (size_t)m * 4,              (size_t)m * 4};
-      size_t total_b = 0, offs[10];
-      for (int i = 0; i < 10; ++i) { offs[i] = total_b; total_b += (sizes[i] + 15) & ~(size_t)15; }
+    budget = std::max<int64_t>(budget, std::min<int64_t>((int64_t)16 << 30, (int64_t)(free_b / 4)));
+  // batch buffer: sized from the largest output seen on this context (at least 64 ranges a query),
+  // bounded by the caller's capacity and the budget; a batch whose ranges overflow it but fit `cap`
+  // runs once more with the exact size
+  int64_t dcap = std::min<int64_t>(std::max<int64_t>({(int64_t)1 << 20, nq * 64, ctx->ranges_hint}),
+                                   budget / (int64_t)sizeof(gm_range));
+  dcap = std::max<int64_t>(1, std::min<int64_t>(cap, dcap));
+  std::vector<int32_t> stats((size_t)nq);
+  for (int attempt = 0;; ++attempt) {
+    // batch arrays (scan workspace): buffer | start | offsets | count | status | qmap | scan partials | total
+    gm_range* dbuf;
+    int64_t *dstart, *doff, *dparts;
+    int32_t *dcount, *dstatus, *dqmap;
+    unsigned long long* dtotal;
+    {
+      const size_t sz[8] = {al((size_t)dcap * sizeof(gm_range)), al((size_t)nq * 8), al((size_t)(nq + 1) * 8),
+                            al((size_t)nq * 4), al((size_t)nq * 4), al((size_t)nq * 4),
+                            al((size_t)scan_partials_len(nq) * 8), 16};
+      size_t tot = 0;
+      for (size_t v : sz) tot += v;
       void* base = nullptr;
-      int wrc = ctx_workspace(ctx, WS_RANGES, total_b, &base);
-      if (wrc) return wrc;
-      char* b = (char*)base;
-      fa = b + offs[0]; fb = b + offs[1]; rlo = (int64_t*)(b + offs[2]); rhi = (int64_t*)(b + offs[3]);
-      rc = (uint8_t*)(b + offs[4]); gkey = (int64_t*)(b + offs[5]); gidx = (int32_t*)(b + offs[6]);
-      ws = (gm_range*)(b + offs[7]); dcnt = (int32_t*)(b + offs[8]); dst = (int32_t*)(b + offs[9]);
+      int rc = ctx_workspace(ctx, WS_SCAN, tot, &base);
+      if (rc) return rc;
+      char* p = (char*)base;
+      dbuf = (gm_range*)p; p += sz[0];
+      dstart = (int64_t*)p; p += sz[1];
+      doff = (int64_t*)p; p += sz[2];
+      dcount = (int32_t*)p; p += sz[3];
+      dstatus = (int32_t*)p; p += sz[4];
+      dqmap = (int32_t*)p; p += sz[5];
+      dparts = (int64_t*)p; p += sz[6];
+      dtotal = (unsigned long long*)p;
     }
-    launch(q0, m, fcap, rcap, fa, fb, rlo, rhi, rc, gkey, gidx, ws, dcnt, dst);
+    GM_HIP(hipMemsetAsync(dtotal, 0, 8, s));
+    // one pass over a query list with caps (fc, rc); qmap null = queries [0, count)
+    auto pass = [&](int64_t count, const int32_t* qmap, int64_t fc, int64_t rc) -> int {
+      const bool lds_sort = rc <= LDS_SORT;
+      const bool alias = (int64_t)felem * 2 * fc >= rc * (int64_t)sizeof(gm_range);   // merged output in F|G
+      const int64_t ocap = alias ? 2 * fc * (int64_t)felem / (int64_t)sizeof(gm_range) : rc;
+      const int64_t per_q = fc * (int64_t)felem * 2 + rc * 17 + (lds_sort ? 0 : rc * 12) +
+                            (alias ? 0 : rc * (int64_t)sizeof(gm_range));
+      int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(count, budget / per_q));
+      chunk = std::min<int64_t>(chunk, (int64_t)1 << 20);
+      const int64_t m_max = std::min(chunk, count);
+      char* fa;
+      int64_t *rlo, *rhi, *gkey = nullptr;
+      uint8_t* rcb;
+      int32_t* gidx = nullptr;
+      gm_range* ws;
+      {
+        const size_t sizes[7] = {al((size_t)(m_max * fc) * felem * 2),
+                                 al((size_t)(m_max * rc) * 8),
+                                 al((size_t)(m_max * rc) * 8),
+                                 al((size_t)(m_max * rc)),
+                                 lds_sort ? 0 : al((size_t)(m_max * rc) * 8),
+                                 lds_sort ? 0 : al((size_t)(m_max * rc) * 4),
+                                 alias ? 0 : al((size_t)(m_max * rc) * sizeof(gm_range))};
+        size_t tot = 0;
+        for (size_t v : sizes) tot += v;
+        void* base = nullptr;
+        int wrc = ctx_workspace(ctx, WS_RANGES, tot, &base);
+        if (wrc) return wrc;
+        char* b = (char*)base;
+        fa = b; b += sizes[0];
+        rlo = (int64_t*)b; b += sizes[1];
+        rhi = (int64_t*)b; b += sizes[2];
+        rcb = (uint8_t*)b; b += sizes[3];
+        if (!lds_sort) { gkey = (int64_t*)b; b += sizes[4]; gidx = (int32_t*)b; b += sizes[5]; }
+        ws = alias ? (gm_range*)fa : (gm_range*)b;
+      }
+      for (int64_t q0 = 0; q0 < count; q0 += chunk) {
+        const int64_t m = std::min(chunk, count - q0);
+        const BatchOut bo{qmap ? qmap + q0 : nullptr, ocap, dbuf, dcap, dtotal, dstart, dcount, dstatus};
+        launch(qmap ? 0 : q0, m, fc, rc, fa, rlo, rhi, rcb, gkey, gidx, ws, bo);
+        GM_CHECK_LAUNCH();
+      }
+      return GM_OK;
+    };
+    int rc = pass(nq, nullptr, std::min<int64_t>(fcap, P1CAP), std::min<int64_t>(rcap, P1CAP));
+    if (rc) return rc;
+    if (fcap > P1CAP || rcap > P1CAP) {
+      rc = copy_d2h(ctx, stats.data(), dstatus, (size_t)nq * 4);
+      if (rc) return rc;
+      std::vector<int32_t> redo;
+      for (int64_t i = 0; i < nq; ++i)
+        if (stats[i] == QS_CAPACITY) redo.push_back((int32_t)i);
+      if (!redo.empty()) {
+        rc = copy_h2d(ctx, dqmap, redo.data(), redo.size() * 4);
+        if (!rc) rc = pass((int64_t)redo.size(), dqmap, fcap, rcap);
+        if (rc) return rc;
+      }
+    }
+    // device scan of the counts -> query-order offsets (total in out_off[nq])
+    launch_excl_scan(s, dcount, nq, doff, dparts, doff + nq);
     GM_CHECK_LAUNCH();
-    int crc = copy_d2h(ctx, counts.data() + q0, dcnt, (size_t)m * 4);
-    if (!crc) crc = copy_d2h(ctx, stats.data() + q0, dst, (size_t)m * 4);
-    if (crc) return crc;
-    int64_t ctotal = 0;
-    std::vector<int64_t> loff((size_t)m + 1, 0);
-    for (int64_t i = 0; i < m; ++i) {
-      loff[i + 1] = loff[i] + counts[q0 + i];
-      out_off[q0 + i + 1] = total + loff[i + 1];
+    rc = copy_d2h(ctx, out_off, doff, (size_t)(nq + 1) * 8);
+    if (!rc) rc = copy_d2h(ctx, stats.data(), dstatus, (size_t)nq * 4);
+    if (rc) return rc;
+    const int64_t total = out_off[nq];
+    ctx->ranges_hint = std::max(ctx->ranges_hint, std::min(total, cap));
+    if (total > dcap && total <= cap && attempt == 0) {
+      dcap = total;
+      continue;
     }
-    ctotal = loff[m];
-    if (total + ctotal <= cap && ctotal > 0) {
-      void* gbase = nullptr;
-      const size_t oa = ((size_t)(m + 1) * 8 + 15) & ~(size_t)15;
-      int crc = ctx_workspace(ctx, WS_SCAN, oa + (size_t)ctotal * sizeof(gm_range), &gbase);
-      if (crc) return crc;
-      doff = (int64_t*)gbase;
-      dout = (gm_range*)((char*)gbase + oa);
-      crc = copy_h2d(ctx, doff, loff.data(), (size_t)(m + 1) * 8);
-      if (crc) return crc;
-      hipLaunchKernelGGL(k_gather_ranges, dim3((unsigned)m), dim3(RTPB), 0, s, ws, rcap, doff, dout);
+    if (query_status) memcpy(query_status, stats.data(), (size_t)nq * 4);
+    if (needed) *needed = total;
+    if (total > cap) return GM_E_CAPACITY;
+    if (total > 0) {
+      void* dout = nullptr;   // the range scratch is free again
+      rc = ctx_workspace(ctx, WS_RANGES, (size_t)total * sizeof(gm_range), &dout);
+      if (rc) return rc;
+      hipLaunchKernelGGL(k_gather_ranges, dim3((unsigned)std::min<int64_t>(nq, 65536)), dim3(RTPB), 0, s, dbuf,
+                         dstart, doff, nq, (gm_range*)dout);
       GM_CHECK_LAUNCH();
-      crc = copy_d2h(ctx, out + total, dout, (size_t)ctotal * sizeof(gm_range));
-      if (crc) return crc;
-    } else if (total + ctotal > cap) {
-      overflow = true;
+      rc = copy_d2h(ctx, out, dout, (size_t)total * sizeof(gm_range));
+      if (rc) return rc;
     }
-    total += ctotal;
-    GM_HIP(hipStreamSynchronize(s));
+    return GM_OK;
   }
-  if (query_status) for (int64_t i = 0; i < nq; ++i) query_status[i] = stats[i];
-  if (needed) *needed = total;
-  return overflow ? GM_E_CAPACITY : GM_OK;
 }
 
 inline int stop_of(int max_ranges) { return max_ranges <= 0 ? INT32_MAX : max_ranges; }
@@ -804,12 +960,12 @@ int gm_z3_ranges(gm_ctx* ctx, int64_t nq, const int32_t* box_off, const double* 
   a.recurse_stop = max_recurse < 0 ? INT32_MAX : max_recurse;   // Z3SFC.MaxRecursion = Int.MaxValue
   const int64_t zc = z_caps(max_ranges, 3, cap);
   rc = run_ranges(ctx, nq, zc, zc, 8,
-                  [&](int64_t q0, int64_t m, int64_t fcap, int64_t rcap, char* fa, char* fb, int64_t* rlo, int64_t* rhi,
-                      uint8_t* rcb, int64_t* gkey, int32_t* gidx, gm_range* ws, int32_t* dcnt, int32_t* dst) {
+                  [&](int64_t q0, int64_t m, int64_t fcap, int64_t rcap, char* fa, int64_t* rlo, int64_t* rhi,
+                      uint8_t* rcb, int64_t* gkey, int32_t* gidx, gm_range* ws, const BatchOut& bo) {
                     ZRangesArgs b = a;
                     b.q0 = q0; b.fcap = fcap; b.rcap = rcap;
-                    b.fa = (int64_t*)fa; b.fb = (int64_t*)fb; b.rlo = rlo; b.rhi = rhi; b.rc = rcb;
-                    b.gkey = gkey; b.gidx = gidx; b.out = ws; b.out_count = dcnt; b.status = dst;
+                    b.fa = (int64_t*)fa; b.rlo = rlo; b.rhi = rhi; b.rc = rcb;
+                    b.gkey = gkey; b.gidx = gidx; b.out = ws; b.bo = bo;
                     hipLaunchKernelGGL(k_zranges<3>, dim3((unsigned)m), dim3(RTPB), 0, s, b);
                   },
                   out_off, out, cap, needed, query_status);
@@ -840,12 +996,12 @@ int gm_z2_ranges(gm_ctx* ctx, int64_t nq, const int32_t* box_off, const double* 
   a.recurse_stop = max_recurse < 0 ? 7 : max_recurse;   // ZN.DefaultRecurse (ZN.scala:293)
   const int64_t zc = z_caps(max_ranges, 2, cap);
   rc = run_ranges(ctx, nq, zc, zc, 8,
-                  [&](int64_t q0, int64_t m, int64_t fcap, int64_t rcap, char* fa, char* fb, int64_t* rlo, int64_t* rhi,
-                      uint8_t* rcb, int64_t* gkey, int32_t* gidx, gm_range* ws, int32_t* dcnt, int32_t* dst) {
+                  [&](int64_t q0, int64_t m, int64_t fcap, int64_t rcap, char* fa, int64_t* rlo, int64_t* rhi,
+                      uint8_t* rcb, int64_t* gkey, int32_t* gidx, gm_range* ws, const BatchOut& bo) {
                     ZRangesArgs b = a;
                     b.q0 = q0; b.fcap = fcap; b.rcap = rcap;
-                    b.fa = (int64_t*)fa; b.fb = (int64_t*)fb; b.rlo = rlo; b.rhi = rhi; b.rc = rcb;
-                    b.gkey = gkey; b.gidx = gidx; b.out = ws; b.out_count = dcnt; b.status = dst;
+                    b.fa = (int64_t*)fa; b.rlo = rlo; b.rhi = rhi; b.rc = rcb;
+                    b.gkey = gkey; b.gidx = gidx; b.out = ws; b.bo = bo;
                     hipLaunchKernelGGL(k_zranges<2>, dim3((unsigned)m), dim3(RTPB), 0, s, b);
                   },
                   out_off, out, cap, needed, query_status);
@@ -879,12 +1035,12 @@ static int xz_ranges(gm_ctx* ctx, int D, int64_t nq, const int32_t* win_off, con
     rcap = 3 * fcap;
   }
   rc = run_ranges(ctx, nq, fcap, rcap, 8,
-                  [&](int64_t q0, int64_t m, int64_t fc, int64_t rcp, char* fa, char* fb, int64_t* rlo, int64_t* rhi,
-                      uint8_t* rcb, int64_t* gkey, int32_t* gidx, gm_range* ws, int32_t* dcnt, int32_t* dst) {
+                  [&](int64_t q0, int64_t m, int64_t fc, int64_t rcp, char* fa, int64_t* rlo, int64_t* rhi,
+                      uint8_t* rcb, int64_t* gkey, int32_t* gidx, gm_range* ws, const BatchOut& bo) {
                     XZRangesArgs b = a;
                     b.q0 = q0; b.fcap = fc; b.rcap = rcp;
-                    b.fa = (uint64_t*)fa; b.fb = (uint64_t*)fb; b.rlo = rlo; b.rhi = rhi; b.rc = rcb;
-                    b.gkey = gkey; b.gidx = gidx; b.out = ws; b.out_count = dcnt; b.status = dst;
+                    b.fa = (uint64_t*)fa; b.rlo = rlo; b.rhi = rhi; b.rc = rcb;
+                    b.gkey = gkey; b.gidx = gidx; b.out = ws; b.bo = bo;
                     if (D == 2) hipLaunchKernelGGL(k_xzranges<2>, dim3((unsigned)m), dim3(RTPB), 0, s, b);
                     else hipLaunchKernelGGL(k_xzranges<3>, dim3((unsigned)m), dim3(RTPB), 0, s, b);
                   },
@@ -915,12 +1071,12 @@ int gm_zranges(gm_ctx* ctx, int dims, int64_t nq, const int32_t* bound_off, cons
   a.recurse_stop = max_recurse < 0 ? 7 : max_recurse;   // maxRecurse = Some(ZN.DefaultRecurse) (ZN.scala:113,293)
   const int64_t zc = z_caps(max_ranges, dims, cap);
   rc = run_ranges(ctx, nq, zc, zc, 8,
-                  [&](int64_t q0, int64_t m, int64_t fcap, int64_t rcap, char* fa, char* fb, int64_t* rlo, int64_t* rhi,
-                      uint8_t* rcb, int64_t* gkey, int32_t* gidx, gm_range* ws, int32_t* dcnt, int32_t* dst) {
+                  [&](int64_t q0, int64_t m, int64_t fcap, int64_t rcap, char* fa, int64_t* rlo, int64_t* rhi,
+                      uint8_t* rcb, int64_t* gkey, int32_t* gidx, gm_range* ws, const BatchOut& bo) {
                     ZRangesArgs b = a;
                     b.q0 = q0; b.fcap = fcap; b.rcap = rcap;
-                    b.fa = (int64_t*)fa; b.fb = (int64_t*)fb; b.rlo = rlo; b.rhi = rhi; b.rc = rcb;
-                    b.gkey = gkey; b.gidx = gidx; b.out = ws; b.out_count = dcnt; b.status = dst;
+                    b.fa = (int64_t*)fa; b.rlo = rlo; b.rhi = rhi; b.rc = rcb;
+                    b.gkey = gkey; b.gidx = gidx; b.out = ws; b.bo = bo;
                     if (dims == 3) hipLaunchKernelGGL(k_zranges<3>, dim3((unsigned)m), dim3(RTPB), 0, s, b);
                     else hipLaunchKernelGGL(k_zranges<2>, dim3((unsigned)m), dim3(RTPB), 0, s, b);
                   },
