@@ -550,6 +550,15 @@ __device__ __forceinline__ uint64_t xpack(const uint32_t* c) {
   return e;
 }
 
+// child k of an element, XElement.children order: bit d of k takes the upper half of dimension d
+// (XZ2SFC.scala:406-415, XZ3SFC.scala:449-464)
+template <int D>
+__device__ __forceinline__ uint64_t xchild(uint64_t p, int k) {
+  uint32_t c[3];
+  for (int d = 0; d < D; ++d) c[d] = 2 * xcoord<D>(p, d) + ((k >> d) & 1);
+  return xpack<D>(c);
+}
+
 // sequenceCode (XZ2SFC.scala:264-286, XZ3SFC.scala:275-304) of an element's lower corner: the
 // descent compares x < xCenter at every level, i.e. reads the element's coordinate bits MSB first
 template <int D>
@@ -620,20 +629,23 @@ __global__ __launch_bounds__(RTPB) void k_xzranges(XZRangesArgs a) {
     return;
   }
 
-  // LevelOneElements: the 2^D children of the unit element, in XElement.children order
-  int64_t K = 1 << D;
-  for (int k = threadIdx.x; k < K; k += RTPB) {
-    uint32_t c[3] = {(uint32_t)(k & 1), (uint32_t)((k >> 1) & 1), (uint32_t)((k >> 2) & 1)};
-    F[k] = xpack<D>(c);
-  }
+  // The frontier holds PARENTS: a level's elements are the 2^D children (XElement.children order) of
+  // each overlapping element of the level above, element i = child (i & (2^D - 1)) of parent i >> D.
+  // Level one is the children of the unit element (LevelOneElements).
+  uint64_t* P = F;   // parents of this level's elements
+  uint64_t* Q = G;   // overlapping elements of this level = parents of the next
+  constexpr int NK = 1 << D;
+  if (threadIdx.x == 0) P[0] = 0;
   __syncthreads();
+  int64_t np = 1;
   int level = 1;
   int64_t nR = 0;
   int err = QS_OK;
   const int64_t range_stop = a.range_stop;
-  bool bottom = false;   // bottom out F at `level`, children G (n_kids) at level + 1
+  bool bottom = false;   // bottom out this level's elements from first_rest, and the n_kids parents' children
   int64_t first_rest = 0, n_kids = 0;
   while (true) {
+    const int64_t K = np << D;
     if (level >= g) { bottom = true; first_rest = 0; n_kids = 0; break; }  // while (level < g ...)
     const double len = ldexp(1.0, -level);
     int64_t a_carry = 0, co_carry = 0;
@@ -643,7 +655,7 @@ __global__ __launch_bounds__(RTPB) void k_xzranges(XZRangesArgs a) {
       int kind = 0;  // 0 disjoint, 1 contained, 2 overlapping
       uint64_t e = 0;
       if (i < K) {
-        e = F[i];
+        e = xchild<D>(P[i >> D], (int)(i & (NK - 1)));
         double mn[3], ext[3];
         for (int d = 0; d < D; ++d) {
           const double ci = (double)xcoord<D>(e, d);
@@ -667,8 +679,8 @@ __global__ __launch_bounds__(RTPB) void k_xzranges(XZRangesArgs a) {
         }
         kind = cont ? 1 : (ovl ? 2 : 0);
       }
-      const int ai = kind != 0, co = kind == 2 ? (1 << D) : 0;
-      int64_t pt;   // one scan of (ranges | children << 32)
+      const int ai = kind != 0, co = kind == 2;
+      int64_t pt;   // one scan of (ranges | overlapping << 32)
       const int64_t px = block_exscan((int64_t)ai | ((int64_t)co << 32), s_tmp, pt);
       const int64_t ax = px & 0xffffffff, cox = px >> 32, at = pt & 0xffffffff, cot = pt >> 32;
       // budget: element i is processed only if nR + A(i-1) < rangeStop (XZ2SFC.scala:205); A(i-1) <= at,
@@ -690,14 +702,7 @@ __global__ __launch_bounds__(RTPB) void k_xzranges(XZRangesArgs a) {
           const int64_t cs = xseq<D>(e, level, g);
           rlo[rpos] = cs;
           if (kind == 1) { rhi[rpos] = cs + xspan<D>(level, g); rc[rpos] = 1; }
-          else {
-            rhi[rpos] = cs; rc[rpos] = 0;
-            for (int k = 0; k < (1 << D); ++k) {   // XElement.children order
-              uint32_t cc[3];
-              for (int d = 0; d < D; ++d) cc[d] = 2 * xcoord<D>(e, d) + ((k >> d) & 1);
-              G[fpos + k] = xpack<D>(cc);
-            }
-          }
+          else { rhi[rpos] = cs; rc[rpos] = 0; Q[fpos] = e; }   // children queued as their parent
         }
       }
       if (sl != INT32_MAX) {
@@ -719,24 +724,34 @@ __global__ __launch_bounds__(RTPB) void k_xzranges(XZRangesArgs a) {
     if (s_err) { err = s_err; break; }
     nR += a_carry;
     if (stop_at >= 0) { bottom = true; first_rest = stop_at; n_kids = co_carry; break; }
-    K = co_carry;
-    if (K == 0) break;
+    np = co_carry;
+    if (np == 0) break;
     level += 1;   // LevelTerminator (XZ2SFC.scala:207-212)
-    uint64_t* tmp = F; F = G; G = tmp;
+    uint64_t* tmp = P; P = Q; Q = tmp;
     __syncthreads();
   }
   if (!err && bottom) {
-    // bottom out (XZ2SFC.scala:219-227): rest of F at `level`, then G at level + 1, full intervals
-    const int64_t rest = K - first_rest;
+    // bottom out (XZ2SFC.scala:219-227): the rest of this level, then the queued children at level + 1,
+    // as full intervals.  Siblings' full intervals chain (a child's lower is its previous sibling's
+    // upper), so each parent's run of siblings is emitted as the one range the merge below would make
+    // of them: [first sibling's lower, last sibling's upper], not contained.
+    const int64_t g0 = first_rest >> D;
+    const int64_t rest = np - g0;   // sibling groups with unprocessed elements
     if (nR + rest + n_kids > a.rcap) err = QS_CAPACITY;
     else {
       for (int64_t j = threadIdx.x; j < rest; j += RTPB) {
-        const int64_t cs = xseq<D>(F[first_rest + j], level, g);
-        rlo[nR + j] = cs; rhi[nR + j] = cs + xspan<D>(level, g); rc[nR + j] = 0;
+        const int64_t grp = g0 + j;
+        const int k0 = grp == g0 ? (int)(first_rest & (NK - 1)) : 0;
+        const uint64_t par = P[grp];
+        rlo[nR + j] = xseq<D>(xchild<D>(par, k0), level, g);
+        rhi[nR + j] = xseq<D>(xchild<D>(par, NK - 1), level, g) + xspan<D>(level, g);
+        rc[nR + j] = 0;
       }
       for (int64_t j = threadIdx.x; j < n_kids; j += RTPB) {
-        const int64_t cs = xseq<D>(G[j], level + 1, g);
-        rlo[nR + rest + j] = cs; rhi[nR + rest + j] = cs + xspan<D>(level + 1, g); rc[nR + rest + j] = 0;
+        const uint64_t par = Q[j];
+        rlo[nR + rest + j] = xseq<D>(xchild<D>(par, 0), level + 1, g);
+        rhi[nR + rest + j] = xseq<D>(xchild<D>(par, NK - 1), level + 1, g) + xspan<D>(level + 1, g);
+        rc[nR + rest + j] = 0;
       }
       nR += rest + n_kids;
     }
@@ -1025,10 +1040,11 @@ static int xz_ranges(gm_ctx* ctx, int D, int64_t nq, const int32_t* win_off, con
   XZRangesArgs a{};
   a.win_off = dwo; a.win = dw; a.g = g; a.zhi = (double)max_offset(period);
   a.range_stop = stop_of(max_ranges);
-  // each processed element adds one range and at most 2^D queued children
+  // each processed element adds one range and at most one queued parent (its 2^D children); a level
+  // processes at most rangeStop elements; bottom-out adds one range per parent of either level
   int64_t fcap, rcap;
   if (max_ranges > 0) {
-    fcap = ((int64_t)max_ranges + 2) << D;
+    fcap = (int64_t)max_ranges + 2;
     rcap = (int64_t)max_ranges + 2 * fcap + 16;
   } else {
     fcap = std::max<int64_t>(cap, 1 << 16);
