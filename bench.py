@@ -21,7 +21,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from geomesa_amd.shard import all_reduce_scalar, broadcast_polyset, shard_bounds  # noqa: E402
+from geomesa_amd.shard import all_reduce_scalar, broadcast_polyset, gather_rows, shard_bounds  # noqa: E402
 
 METRIC = "points/sec Z3 encode + point-in-polygon join pairs/sec at 1/2/4/8 MI355X"
 SEED = 0x67656F6D65736121
@@ -203,6 +203,29 @@ def cpu_ranges_baseline(kind, q, t, max_ranges, gpu_ms, nq):
             "cpu_ranges": r}
 
 
+def ranges_batch(dist, fn, args, n_local, nq, reps=3):
+    """One batched-ranges entry point over this rank's block of queries, then the gather of every
+    rank's offsets + ranges to rank 0; wall time per batch (barrier on both sides, max over ranks)."""
+    from geomesa_amd import ranges as R
+    from geomesa_amd.shard import gather_ranges
+    offs, rr, _ = R.call_raw(fn, args, n_local, max(n_local, 1) * 256, pinned=True)
+    cap = int(offs[-1]) + 1024
+    res = {}
+
+    def step():
+        o, r, _ = R.call_raw(fn, args, n_local, cap, pinned=True)
+        g = gather_ranges(dist.pg, o, r[:int(o[-1])])
+        res["n"] = int(g[0][-1]) if g is not None else -1
+    step()
+    dist.barrier()
+    t0 = time.time()
+    for _ in range(reps):
+        step()
+    dist.barrier()
+    dt = dist.max((time.time() - t0) / reps)
+    return {"value": nq / dt, "unit": "queries/s", "ms_per_step": dt * 1e3, "ranges": res["n"]}
+
+
 def sort_bytes(b, z, n):
     """Algorithmic bytes of gm_sort_keys over n rows: the all-digit histogram read (10 B/row), per
     non-constant byte digit a histogram read of its column (8 B z / 2 B bin) and a scatter that reads
@@ -246,16 +269,16 @@ def gather_pairs(dist, ptids, plids, k):
 
 
 def bench_table(a, dist, ctx, b, z):
-    """configs[2]: the rank's slice of a range-sharded Z3 table (2B rows over 8 GPUs = 250M per GPU):
-    gm_sort_keys into table order (ingest), then the configs[2] bbox + during query as ranges +
-    gm_key_range_scan (seek + Z3Filter).  Reported: sort rows/s and queries/s, with the rows the
-    seeks touched."""
-    import ctypes
+    """configs[2]: a Z3 table range-sharded over the GPUs (2B rows over 8 GPUs = 250M per GPU).
+    sort_keys: one gm_sort_keys of the rank's rows into table order.  table_ingest: the partitioned
+    table built from the rank's rows (local sort, splitters, all-to-all by key range, slice sort).
+    table_query: the configs[2] bbox + during query over the whole table -- ranges clipped to each
+    slice, gm_key_range_scan (seek + Z3Filter), global ids gathered to rank 0."""
     import torch
     from geomesa_amd import _lib
     from geomesa_amd import filters as F
     from geomesa_amd.keyspace import Z3IndexKeySpace, during
-    from geomesa_amd.table import Z3Table, key_ranges
+    from geomesa_amd.table import key_ranges
     NT = min(a.table_rows, b.numel())
     lib, h, P = ctx.lib, ctx.handle, _lib.ptr
     bs, zs = b[:NT], z[:NT]
@@ -266,25 +289,36 @@ def bench_table(a, dist, ctx, b, z):
         _lib.check(lib.gm_sort_keys(h, None, P(bs), P(zs), NT, None, P(ob), P(oz), P(perm)), "gm_sort_keys")
     ms_sort = timed(dist, sort_step, 3, 1)
     sbytes, npass = sort_bytes(bs, zs, NT)
-    tb = Z3Table.__new__(Z3Table)   # wrap the sorted columns without re-sorting
-    tb.ks, tb.ctx, tb.n, tb.bin, tb.z, tb.perm, tb.shard, tb.shards = Z3IndexKeySpace(), ctx, NT, ob, oz, perm, None, None
-    ks = tb.ks
+    del ob, oz, perm
+    # the key-range partitioned table (configs[2]): every rank keys its own rows, the ranks sample
+    # splitters and exchange rows by key range (one all-to-all over RCCL), each sorts its slice
+    from geomesa_amd.table import PartitionedZ3Table
+    ks = Z3IndexKeySpace()
+    gids = torch.arange(NT, dtype=torch.int64, device=zs.device) + dist.rank * NT
+    holder = {}
+
+    def ingest_step():
+        holder.pop("t", None)
+        holder["t"] = PartitionedZ3Table(dist.pg, bs, zs, gids)
+    ms_ingest = timed(dist, ingest_step, 1, 1)
+    pt = holder["t"]
+    del gids
+    slice_rows = [int(v) for v in (all_gather_ints(dist, pt.n))]
     v = ks.get_index_values([(-10, 35, 30, 60)], [during(1590969600000, 1591617600000)])
     t0 = time.time()
     sr = ks.get_ranges(v)
     plan_ms = (time.time() - t0) * 1e3
     arr, nr = key_ranges(sr)
     fb = F.serialize_to_bytes(F.Z3Filter.from_values(v))
-    fbuf = (ctypes.c_uint8 * len(fb)).from_buffer_copy(fb)
-    cap = NT // 100
-    ids = torch.empty(cap, dtype=torch.int64, device=zs.device)
-    nm, ns = ctypes.c_int64(), ctypes.c_int64()
+    res = {}
 
-    def scan_step():
-        _lib.check(lib.gm_key_range_scan(h, None, P(ob), P(oz), NT, arr, nr, fbuf, len(fb), P(perm), P(ids), cap,
-                                         ctypes.byref(nm), ctypes.byref(ns)), "gm_key_range_scan")
-    ms_scan = timed(dist, scan_step, 10, 2)
-    del ob, oz, perm, ids
+    def query_step():
+        ids, nm, ns, ncl = pt.scan(sr, fb)       # clip to the slice, seek + Z3Filter, global ids
+        g = gather_rows(dist.pg, [ids])           # results to rank 0
+        res.update(nm=nm, ns=ns, ncl=ncl, n0=int(g[0].numel()) if g is not None else -1)
+    ms_scan = timed(dist, query_step, 10, 2)
+    matches, scanned = dist.sum(res["nm"]), dist.sum(res["ns"])
+    del holder, pt
     return {
         "sort_keys": {"value": NT * dist.world / (ms_sort * 1e-3), "unit": "rows/s", "ms_per_step": ms_sort,
                       "rows_per_gpu": NT, "digit_passes": npass,
@@ -293,14 +327,29 @@ def bench_table(a, dist, ctx, b, z):
                       "note": "stable LSD radix sort of (bin, z) into table byte order (ingest side); bytes = "
                               "10 B/row digit census + per pass (digit column read + 28 B/row scatter) + 12 B/row "
                               "permutation widening"},
-        "table_query": {"value": dist.world / (ms_scan * 1e-3), "unit": "queries/s", "ms_per_step": ms_scan,
-                        "rows_per_gpu": NT, "ranges": nr, "rows_scanned": ns.value, "matches": nm.value,
-                        "plan_ms": round(plan_ms, 2),
+        "table_ingest": {"value": NT * dist.world / (ms_ingest * 1e-3), "unit": "rows/s", "ms_per_step": ms_ingest,
+                         "rows_per_gpu": NT, "slice_rows": slice_rows,
+                         "note": "key-range partitioned table: local sort, splitter sampling (1024 keys per rank), "
+                                 "all-to-all of the rows by key range (24 B/row), sort of the received slice"},
+        "table_query": {"value": 1.0 / (ms_scan * 1e-3), "unit": "queries/s", "ms_per_step": ms_scan,
+                        "table_rows": NT * dist.world, "ranges": nr, "ranges_scanned_rank0": res["ncl"],
+                        "rows_scanned": int(scanned), "matches": int(matches), "plan_ms": round(plan_ms, 2),
                         "equivalent_scan_rate": NT * dist.world / (ms_scan * 1e-3),
-                        "note": "configs[2] query bbox(-10,35,30,60) during 2020-06-01/06-08T12 on a sorted "
-                                "table slice: binary-searched ranges + Z3Filter on the rows inside (ranges "
-                                "planned on the GPU once, plan_ms, not in ms_per_step)"},
+                        "note": "configs[2] query bbox(-10,35,30,60) during 2020-06-01/06-08T12 over the whole "
+                                "partitioned table: each rank clips the ranges to its key slice, seeks + Z3Filter, "
+                                "maps to global ids, ids gathered to rank 0 (ranges planned once, plan_ms, not in "
+                                "ms_per_step)"},
     }
+
+
+def all_gather_ints(dist, v):
+    if dist.pg is None:
+        return [v]
+    import torch
+    t = torch.tensor([int(v)], dtype=torch.int64, device="cuda")
+    parts = [torch.zeros_like(t) for _ in range(dist.world)]
+    dist.pg.all_gather(parts, t)
+    return [int(p.item()) for p in parts]
 
 
 def query_polygon():
@@ -451,66 +500,50 @@ def main():
         rec("xz3_index", lambda: lib.gm_xz3_index(h, P(x), P(y), P(zmin), P(xmax), P(ymax), P(zmax), NX, 12, 1, 0, P(xo),
                                                  None, None), 56, NX, unit="envelopes/s")
         del xmax, ymax, xo, zmin, zmax
-        # batched XZ2 ranges (configs[4]): 100k query windows, log-uniform 0.01..20 deg, maxRanges 2000
+        # batched ranges (configs[4]): the queries sharded over the ranks (contiguous blocks), every
+        # rank decomposes its block, offsets + ranges gathered to rank 0 (shard.gather_ranges)
+        from geomesa_amd import ranges as R
         rng = np.random.default_rng(2)
         nq = 100_000
         wq = 10 ** rng.uniform(-2, np.log10(20), (nq, 2)) / 2
         cq = np.stack([rng.uniform(-180 + wq[:, 0], 180 - wq[:, 0]), rng.uniform(-90 + wq[:, 1], 90 - wq[:, 1])], 1)
-        win = np.ascontiguousarray(np.concatenate([cq - wq, cq + wq], 1).reshape(-1))
-        woff = np.arange(nq + 1, dtype=np.int32)
-        from geomesa_amd import ranges as R
-        args = (h, nq, woff.ctypes.data, win.ctypes.data, 12, 2000)
-        offs, rr, _ = R.call_raw(lib.gm_xz2_ranges, args, nq, nq * 256, pinned=True)
-        t0w = time.time()
-        for _ in range(3):
-            offs, rr, _ = R.call_raw(lib.gm_xz2_ranges, args, nq, int(offs[-1]) + 1024, pinned=True)
-        dt = (time.time() - t0w) / 3
-        extra["xz2_ranges_batch"] = {"value": nq * dist.world / dt, "unit": "queries/s", "ms_per_step": dt * 1e3,
-                                     "ranges": int(offs[-1]),
-                                     "note": "C-ABI call incl. H2D of windows and D2H of ranges (pinned host output); 100k XZ2 query "
-                                             "windows (0.01-20 deg), maxRanges 2000, g = 12"}
-        if dist.rank == 0 and not a.no_cpu:
-            extra["xz2_ranges_batch"].update(cpu_ranges_baseline("xz2", win.reshape(nq, 4), None, 2000, dt * 1e3, nq))
-        # batched XZ3 ranges (configs[4]): the same windows x a time window inside the week (1 min .. 2 days)
+        win = np.ascontiguousarray(np.concatenate([cq - wq, cq + wq], 1))
         tw0 = rng.uniform(0, 604800 - 172800, nq)
         tw1 = tw0 + 10 ** rng.uniform(np.log10(60), np.log10(172800), nq)
-        win3 = np.ascontiguousarray(np.stack([win.reshape(nq, 4)[:, 0], win.reshape(nq, 4)[:, 1], tw0,
-                                              win.reshape(nq, 4)[:, 2], win.reshape(nq, 4)[:, 3], tw1], 1).reshape(-1))
-        args3 = (h, nq, woff.ctypes.data, win3.ctypes.data, 12, 1, 2000)
-        offs, rr, _ = R.call_raw(lib.gm_xz3_ranges, args3, nq, nq * 256, pinned=True)
-        t0w = time.time()
-        for _ in range(3):
-            offs, rr, _ = R.call_raw(lib.gm_xz3_ranges, args3, nq, int(offs[-1]) + 1024, pinned=True)
-        dt = (time.time() - t0w) / 3
-        extra["xz3_ranges_batch"] = {"value": nq * dist.world / dt, "unit": "queries/s", "ms_per_step": dt * 1e3,
-                                     "ranges": int(offs[-1]),
-                                     "note": "C-ABI call incl. H2D of windows and D2H of ranges (pinned host output); 100k XZ3 query "
-                                             "windows (0.01-20 deg x 1 min-2 days, week period), maxRanges 2000, g = 12"}
+        win3 = np.ascontiguousarray(np.stack([win[:, 0], win[:, 1], tw0, win[:, 2], win[:, 3], tw1], 1))
+        qlo, qhi = shard_bounds(nq, dist.rank, dist.world)
+        wl, wl3 = np.ascontiguousarray(win[qlo:qhi]), np.ascontiguousarray(win3[qlo:qhi])
+        woff = np.arange(qhi - qlo + 1, dtype=np.int32)
+        note = ("C-ABI call incl. H2D of the windows and D2H of the ranges (pinned host output), queries "
+                "sharded over the ranks with offsets + ranges gathered to rank 0; 100k %s query windows "
+                "(0.01-20 deg%s), maxRanges 2000, g = 12")
+        m = ranges_batch(dist, lib.gm_xz2_ranges, (h, qhi - qlo, woff.ctypes.data, wl.ctypes.data, 12, 2000),
+                         qhi - qlo, nq)
+        extra["xz2_ranges_batch"] = dict(m, note=note % ("XZ2", ""))
         if dist.rank == 0 and not a.no_cpu:
-            extra["xz3_ranges_batch"].update(cpu_ranges_baseline("xz3", win3.reshape(nq, 6), None, 2000, dt * 1e3, nq))
-        del rr
-        # batched ranges (configs[4]/[0]): 4096 Z3 queries with target 2000
+            extra["xz2_ranges_batch"].update(cpu_ranges_baseline("xz2", win, None, 2000, m["ms_per_step"], nq))
+        m = ranges_batch(dist, lib.gm_xz3_ranges, (h, qhi - qlo, woff.ctypes.data, wl3.ctypes.data, 12, 1, 2000),
+                         qhi - qlo, nq)
+        extra["xz3_ranges_batch"] = dict(m, note=note % ("XZ3", " x 1 min-2 days, week period"))
+        if dist.rank == 0 and not a.no_cpu:
+            extra["xz3_ranges_batch"].update(cpu_ranges_baseline("xz3", win3, None, 2000, m["ms_per_step"], nq))
+        # batched Z3 ranges (configs[4]/[0]): 4096 queries with target 2000
         rng = np.random.default_rng(1)
         qs = []
         for _ in range(4096):
             w = 10 ** rng.uniform(-1, 1); hh = 10 ** rng.uniform(-1, 1)
             cx = rng.uniform(-170, 170); cy = rng.uniform(-80, 80); t0 = int(rng.integers(0, 500000))
             qs.append(([(cx - w, cy - hh, cx + w, cy + hh)], [(t0, t0 + 86400)]))
-        from geomesa_amd import ranges as R
-        fn, args, nq, cap = R.prepare_z3(sfc, qs, 64, 2000)
-        offs, rr, _ = R.call_raw(fn, args, nq, cap, pinned=True)
-        t0w = time.time()
-        for _ in range(3):
-            R.call_raw(fn, args, nq, cap, pinned=True)
-        dt = (time.time() - t0w) / 3
-        extra["z3_ranges_batch"] = {"value": len(qs) * dist.world / dt, "unit": "queries/s",
-                                    "ms_per_step": dt * 1e3, "ranges": int(offs[-1]),
-                                    "note": "C-ABI call incl. H2D of queries and D2H of ranges (pinned host output); 4096 Z3 queries "
-                                            "(0.2-20 deg boxes x 1 day), maxRanges 2000 (ScanRangesTarget)"}
+        qlo, qhi = shard_bounds(len(qs), dist.rank, dist.world)
+        fn, args, n3, _ = R.prepare_z3(sfc, qs[qlo:qhi], 64, 2000)
+        m = ranges_batch(dist, fn, args, n3, len(qs))
+        extra["z3_ranges_batch"] = dict(m, note="C-ABI call incl. H2D of queries and D2H of ranges (pinned host "
+                                                "output), sharded over the ranks + gather to rank 0; 4096 Z3 queries "
+                                                "(0.2-20 deg boxes x 1 day), maxRanges 2000 (ScanRangesTarget)")
         if dist.rank == 0 and not a.no_cpu:
             qb = np.array([q[0][0] for q in qs], np.float64)
             qt = np.array([q[1][0] for q in qs], np.int64)
-            extra["z3_ranges_batch"].update(cpu_ranges_baseline("z3", qb, qt, 2000, dt * 1e3, len(qs)))
+            extra["z3_ranges_batch"].update(cpu_ranges_baseline("z3", qb, qt, 2000, m["ms_per_step"], len(qs)))
     # ---------------------------------------------------------------- sorted table: ingest sort + seek-and-filter
     if "table" in only and not a.no_extra:
         extra.update(bench_table(a, dist, ctx, b, z))

@@ -6,6 +6,8 @@ no GPU is visible, every compute entry point raises GeomesaHipUnavailable.
 import ctypes
 import os
 
+import numpy as np
+
 HERE = os.path.dirname(os.path.abspath(__file__))
 # GEOMESA_HIP_LIB selects another in-tree build of the same library (variant builds for profiling)
 LIB_PATH = os.environ.get("GEOMESA_HIP_LIB", os.path.join(HERE, "lib", "libgeomesa_hip.so"))
@@ -53,6 +55,11 @@ class Range(ctypes.Structure):
 class KeyRange(ctypes.Structure):
     _fields_ = [("z_lo", ctypes.c_int64), ("z_hi", ctypes.c_int64), ("bin_lo", ctypes.c_int16),
                 ("bin_hi", ctypes.c_int16), ("shard", ctypes.c_uint8), ("reserved", ctypes.c_uint8 * 3)]
+
+
+# numpy view of gm_key_range rows (24 B, the KeyRange layout)
+KEY_RANGE_DTYPE = np.dtype([("z_lo", "<i8"), ("z_hi", "<i8"), ("bin_lo", "<i2"), ("bin_hi", "<i2"), ("shard", "u1"),
+                            ("reserved", "u1", (3,))])
 
 
 class PolySetC(ctypes.Structure):

@@ -151,3 +151,157 @@ def merge_histograms(pg, counts, present, bin_lo, length=None):
     pg.all_reduce(c, op=pg.ReduceOp.SUM)
     pg.all_reduce(p, op=pg.ReduceOp.MAX)
     return c, (p != 0).to(torch.uint8), lo
+
+
+# ---------------------------------------------------------------- key-range partitioned table
+# configs[2]: the table's rows are split into `world` contiguous key ranges, one per GPU, the way a
+# sorted store splits a table into tablets / regions; a query's scan ranges are clipped to each
+# slice (what the client's range binning does per tablet) and every GPU scans only its part.
+# Keys compare as the row bytes do: [shard][bin BE16][z BE64], unsigned.  In torch they are carried
+# as two int64 columns with the same lexicographic order:
+#   hi = shard << 16 | bin as unsigned short       lo = z with the sign bit flipped
+
+_SIGN = -(1 << 63)
+
+
+def table_key(shard, bin, z):
+    """(hi, lo) int64 key columns (torch) of (shard uint8 or None, bin int16, z int64) columns."""
+    import torch
+    hi = bin.to(torch.int64) & 0xffff
+    if shard is not None:
+        hi = hi | (shard.to(torch.int64) << 16)
+    return hi, z.to(torch.int64) ^ _SIGN
+
+
+def key_columns(hi, lo, sharded):
+    """Inverse of table_key: (shard uint8 or None, bin int16, z int64)."""
+    import torch
+    b = (((hi & 0xffff) ^ 0x8000) - 0x8000).to(torch.int16)
+    return ((hi >> 16).to(torch.uint8) if sharded else None), b, lo ^ _SIGN
+
+
+def sample_splitters(pg, hi, lo, samples=1024):
+    """world - 1 splitter keys (numpy int64 (hi, lo) arrays, identical on every rank) from `samples`
+    evenly spaced keys of each rank's SORTED local columns, weighted by the rank's row count, so each
+    key range holds about 1/world of all rows.  One all_gather of samples x 2 int64 per rank."""
+    import torch
+    world = pg.get_world_size() if pg is not None else 1
+    n = int(hi.numel())
+    if world == 1:
+        return np.zeros(0, np.int64), np.zeros(0, np.int64)
+    dev = _device_of(pg)
+    s = torch.zeros((samples, 3), dtype=torch.int64)
+    if n:
+        pos = ((torch.arange(samples, dtype=torch.float64) + 0.5) * (n / samples)).to(torch.int64).clamp_(0, n - 1)
+        pos = pos.to(hi.device)
+        s[:, 0] = hi[pos].cpu()
+        s[:, 1] = lo[pos].cpu()
+        s[:, 2] = n
+    parts = [torch.zeros_like(s).to(dev) for _ in range(world)]
+    pg.all_gather(parts, s.to(dev))
+    allv = torch.cat([p.cpu() for p in parts]).numpy()
+    w = allv[:, 2].astype(np.float64) / samples       # rows each sample stands for
+    keep = w > 0
+    allv, w = allv[keep], w[keep]
+    if len(allv) == 0:
+        return np.zeros(world - 1, np.int64), np.zeros(world - 1, np.int64)
+    order = np.lexsort((allv[:, 1], allv[:, 0]))
+    allv, cw = allv[order], np.cumsum(w[order])
+    total = cw[-1]
+    idx = np.minimum(np.searchsorted(cw, total * np.arange(1, world) / world, side="left"), len(allv) - 1)
+    return allv[idx, 0].copy(), allv[idx, 1].copy()
+
+
+def split_positions(hi, lo, s_hi, s_lo):
+    """Row positions of the splitters in SORTED local (hi, lo) columns: p[k] = rows with key below
+    splitter k - 1 (p[0] = 0, p[world] = n); a key equal to a splitter goes to the upper range."""
+    import torch
+    n = int(hi.numel())
+    pos = [0]
+    for sh, sl in zip(s_hi.tolist(), s_lo.tolist()):
+        t = torch.tensor([sh], dtype=torch.int64, device=hi.device)
+        a = int(torch.searchsorted(hi, t, right=False).item())
+        b = int(torch.searchsorted(hi, t, right=True).item())
+        c = a
+        if b > a:
+            c = a + int(torch.searchsorted(lo[a:b].contiguous(), torch.tensor([sl], dtype=torch.int64,
+                                                                               device=hi.device)).item())
+        pos.append(max(c, pos[-1]))
+    pos.append(max(n, pos[-1]))
+    return pos
+
+
+def exchange_by_key_range(pg, hi, lo, cols=(), samples=1024):
+    """All-to-all of SORTED local rows by key range: rank r receives every row whose key falls in
+    [splitter r-1, splitter r).  hi / lo / cols are 1-D int64 tensors of one length.  One all_to_all
+    of the counts, then one of the rows packed as (hi, lo, cols...) int64 records -- over RCCL a
+    grouped send / recv on every xGMI link at once.  Returns (hi, lo, cols, (s_hi, s_lo)) of the
+    received rows: `world` sorted runs, one per sender, in rank order (the caller re-sorts)."""
+    import torch
+    s_hi, s_lo = sample_splitters(pg, hi, lo, samples)
+    if pg is None or pg.get_world_size() == 1:
+        return hi, lo, list(cols), (s_hi, s_lo)
+    world = pg.get_world_size()
+    dev = _device_of(pg)
+    home = hi.device
+    pos = split_positions(hi, lo, s_hi, s_lo)
+    send = [pos[k + 1] - pos[k] for k in range(world)]
+    sc = torch.tensor(send, dtype=torch.int64, device=dev)
+    rc = torch.empty(world, dtype=torch.int64, device=dev)
+    pg.all_to_all_single(rc, sc)
+    recv = [int(v) for v in rc.cpu().tolist()]
+    rec = torch.stack([hi, lo] + [c.to(torch.int64) for c in cols], 1).to(dev).contiguous()
+    out = torch.empty((sum(recv), rec.shape[1]), dtype=torch.int64, device=dev)
+    pg.all_to_all_single(out, rec, recv, send)
+    del rec
+    out = out.to(home)
+    return out[:, 0].contiguous(), out[:, 1].contiguous(), [out[:, 2 + k].contiguous() for k in range(len(cols))], \
+        (s_hi, s_lo)
+
+
+def clip_key_ranges(ranges, kmin, kmax):
+    """Clip gm_key_range rows (numpy KEY_RANGE_DTYPE array) to the key slice [kmin, kmax] (each an
+    (hi, lo) key pair, inclusive): ranges outside are dropped, the rest narrowed.  A range lies in
+    one shard and the slice bounds are keys of that ordering, so a clipped range stays in its shard."""
+    r = np.asarray(ranges)
+    if kmin is None or len(r) == 0:
+        return r[:0].copy()
+    sh = r["shard"].astype(np.int64) << 16
+    l_hi = sh | (r["bin_lo"].astype(np.int64) & 0xffff)
+    h_hi = sh | (r["bin_hi"].astype(np.int64) & 0xffff)
+    l_lo = r["z_lo"] ^ np.int64(_SIGN)
+    h_lo = r["z_hi"] ^ np.int64(_SIGN)
+
+    def less(ah, al, bh, bl):
+        return (ah < bh) | ((ah == bh) & (al < bl))
+    # new lower = max(L, kmin), new upper = min(H, kmax)
+    up = less(l_hi, l_lo, kmin[0], kmin[1])
+    n_hi, n_lo = np.where(up, kmin[0], l_hi), np.where(up, kmin[1], l_lo)
+    dn = less(kmax[0], kmax[1], h_hi, h_lo)
+    x_hi, x_lo = np.where(dn, kmax[0], h_hi), np.where(dn, kmax[1], h_lo)
+    keep = ~less(x_hi, x_lo, n_hi, n_lo)
+    out = r[keep].copy()
+
+    def s16(v):
+        return (((v & 0xffff) ^ 0x8000) - 0x8000).astype(np.int16)
+    out["bin_lo"], out["z_lo"] = s16(n_hi[keep]), n_lo[keep] ^ np.int64(_SIGN)
+    out["bin_hi"], out["z_hi"] = s16(x_hi[keep]), x_lo[keep] ^ np.int64(_SIGN)
+    return out
+
+
+def gather_ranges(pg, out_off, ranges, dst=0):
+    """Gather per-rank batched-ranges results (out_off [nq_r + 1] int64, ranges numpy RANGE_DTYPE) of
+    contiguous query shards to rank `dst`: (out_off, ranges) over all queries in rank order there,
+    None elsewhere; with pg None the input."""
+    if pg is None:
+        return out_off, ranges
+    import torch
+    from .ranges import RANGE_DTYPE
+    cnt = torch.from_numpy(np.diff(np.asarray(out_off, np.int64)))
+    rr = torch.from_numpy(np.ascontiguousarray(ranges).view(np.int64).reshape(-1).copy())
+    g = gather_rows(pg, [cnt])
+    gr = gather_rows(pg, [rr])
+    if g is None:
+        return None
+    offs = np.concatenate([[0], np.cumsum(g[0].cpu().numpy())]).astype(np.int64)
+    return offs, gr[0].cpu().numpy().view(RANGE_DTYPE)

@@ -26,8 +26,8 @@ _ALL64 = -1  # 0xFFFF... as int64
 
 
 def key_ranges(scan_ranges, shards=None):
-    """getRangeBytes (Z3IndexKeySpace.scala:196-238) as gm_key_range rows: one per scan range and
-    shard.  scan_ranges are Z3IndexKeySpace.get_ranges tuples."""
+    """getRangeBytes (Z3IndexKeySpace.scala:196-238) as gm_key_range rows (numpy KEY_RANGE_DTYPE): one
+    per scan range and shard.  scan_ranges are Z3IndexKeySpace.get_ranges tuples."""
     out = []
     for kind, lo, hi in scan_ranges:
         if kind == "bounded":
@@ -40,9 +40,9 @@ def key_ranges(scan_ranges, shards=None):
             r = (0, _ALL64, 0, -1)
         for s in (range(shards) if shards else [0]):
             out.append(r + (s,))
-    arr = (_lib.KeyRange * max(1, len(out)))()
+    arr = np.zeros(len(out), _lib.KEY_RANGE_DTYPE)
     for i, (zl, zh, bl, bh, s) in enumerate(out):
-        arr[i].z_lo, arr[i].z_hi, arr[i].bin_lo, arr[i].bin_hi, arr[i].shard = zl, zh, bl, bh, s
+        arr[i]["z_lo"], arr[i]["z_hi"], arr[i]["bin_lo"], arr[i]["bin_hi"], arr[i]["shard"] = zl, zh, bl, bh, s
     return arr, len(out)
 
 
@@ -90,8 +90,13 @@ class Z3Table:
         """Rows in any scan range that pass `z3filter` (a Z3Filter, its bytes, or None).
 
         Returns (ids tensor, n_match, n_scanned); ids are input rows (map_rows) or table rows."""
+        arr, _ = key_ranges(scan_ranges, self.shards)
+        return self.scan_key_ranges(arr, z3filter, map_rows, ids_cap)
+
+    def scan_key_ranges(self, arr, z3filter=None, map_rows=True, ids_cap=None):
+        """scan() over gm_key_range rows (numpy KEY_RANGE_DTYPE), e.g. ranges clipped to a slice."""
         import torch
-        arr, nr = key_ranges(scan_ranges, self.shards)
+        arr = np.ascontiguousarray(arr, _lib.KEY_RANGE_DTYPE)
         fb = None
         if z3filter is not None:
             fb = F.serialize_to_bytes(z3filter) if not isinstance(z3filter, (bytes, bytearray)) else bytes(z3filter)
@@ -100,7 +105,8 @@ class Z3Table:
         ids = torch.empty(max(cap, 1), dtype=torch.int64, device=self.z.device)
         nm, ns = ctypes.c_int64(), ctypes.c_int64()
         rc = self.ctx.lib.gm_key_range_scan(self.ctx.handle, ptr(self.shard), ptr(self.bin), ptr(self.z), self.n,
-                                            arr, nr, fbuf, len(fb) if fb else 0, ptr(self.perm) if map_rows else None,
+                                            arr.ctypes.data if len(arr) else None, len(arr), fbuf,
+                                            len(fb) if fb else 0, ptr(self.perm) if map_rows else None,
                                             ptr(ids), cap, ctypes.byref(nm), ctypes.byref(ns))
         if rc != _lib.GM_E_CAPACITY:
             check(rc, "gm_key_range_scan")
@@ -114,3 +120,70 @@ class Z3Table:
             return torch.zeros(0, dtype=torch.int64, device=self.z.device), 0, 0
         sr = self.ks.get_ranges(v, target=target)
         return self.scan(sr, F.Z3Filter.from_values(v))
+
+
+class PartitionedZ3Table:
+    """configs[2]: a Z3 table range-partitioned over the GPUs of a process group, one slice per rank.
+
+    Every rank starts from its own rows (any split), keys them, sorts them (gm_sort_keys), and the
+    ranks agree on world - 1 splitter keys sampled from the sorted slices; one all-to-all moves every
+    row to the rank owning its key range (shard.exchange_by_key_range), which sorts what it received.
+    Afterwards rank r holds the rows of keys [splitter r-1, splitter r) in table order -- a sorted
+    store's table split into tablets / regions (the shard prefix of ShardStrategy.scala:75-80 stays
+    the key's first byte).  A query's scan ranges (getRangeBytes, Z3IndexKeySpace.scala:196-238) are
+    clipped to the slice's first and last key (the per-tablet range binning of a batch scanner) and
+    each rank scans only those; the ids that come back are global row ids, so the union over ranks
+    equals the scan of one unpartitioned table.  pg None = a single unpartitioned slice."""
+
+    def __init__(self, pg, bins, z, ids, shard=None, shards=None, period="week", samples=1024):
+        import torch
+        from . import shard as S
+        self.pg = pg
+        local = Z3Table(bins, z, shard, period)
+        sharded = shard is not None
+        hi, lo = S.table_key(local.shard, local.bin, local.z)
+        gid = torch.as_tensor(ids).to(local.z.device, torch.int64)[local.perm]
+        del local
+        hi, lo, (gid,), self.splitters = S.exchange_by_key_range(pg, hi, lo, [gid], samples)
+        sh, b, zz = S.key_columns(hi, lo, sharded)
+        del hi, lo
+        self.table = Z3Table(b, zz, sh, period)
+        if sharded:
+            self.table.shards = int(shards) if shards else (
+                int(S.all_reduce_scalar(pg, float(self.table.shards or 0), "max")))
+        self.gid = gid[self.table.perm]   # global row id of each table row
+        self.n = self.table.n
+        if self.n:
+            t = self.table
+            ends = torch.tensor([0, self.n - 1], device=t.z.device)
+            k_hi, k_lo = S.table_key(None if t.shard is None else t.shard[ends], t.bin[ends], t.z[ends])
+            k_hi, k_lo = k_hi.cpu().tolist(), k_lo.cpu().tolist()
+            self.kmin, self.kmax = (k_hi[0], k_lo[0]), (k_hi[1], k_lo[1])
+        else:
+            self.kmin = self.kmax = None
+
+    @classmethod
+    def from_points(cls, pg, x, y, t_ms, ids, shard=None, shards=None, period="week", lenient=False, samples=1024):
+        bins, z = Z3IndexKeySpace(period).sfc.index_keys(x, y, t_ms, lenient=lenient)
+        return cls(pg, bins, z, ids, shard, shards, period, samples)
+
+    def clip(self, arr):
+        """gm_key_range rows clipped to this rank's slice."""
+        from .shard import clip_key_ranges
+        return clip_key_ranges(arr, self.kmin, self.kmax)
+
+    def scan(self, scan_ranges, z3filter=None):
+        """(global row ids of this slice's matches, n_match, n_scanned, n_ranges scanned)."""
+        arr, _ = key_ranges(scan_ranges, self.table.shards)
+        arr = self.clip(arr)
+        ids, nm, ns = self.table.scan_key_ranges(arr, z3filter, map_rows=False)
+        return self.gid[ids], nm, ns, len(arr)
+
+    def query(self, bboxes=None, intervals=None, target=2000):
+        """bbox + during query (Z3Filter on the rows of the clipped ranges) on this rank's slice."""
+        ks = self.table.ks
+        v = ks.get_index_values(bboxes, intervals)
+        if v.disjoint:
+            import torch
+            return torch.zeros(0, dtype=torch.int64, device=self.table.z.device), 0, 0, 0
+        return self.scan(ks.get_ranges(v, target=target), F.Z3Filter.from_values(v))

@@ -201,3 +201,165 @@ def test_merge_histograms_without_group():
     rc, rp, lo = merge_histograms(None, c, p, 2600)
     assert rc is c and rp is p and lo == 2600
     assert merge_histograms(None, None, None, None) == (None, None, None)
+
+
+# ---------------------------------------------------------------- key-range partitioned table (configs[2])
+
+def _rand_keys(rng, n):
+    """(shard, bin, z) rows with shards 0-3, bins on both sides of the unsigned-short sign flip and z
+    spanning the whole unsigned range."""
+    sh = rng.integers(0, 4, n).astype(np.uint8)
+    b = rng.choice(np.array([0, 1, 2, 2600, 32767, -32768, -2], np.int16), n)
+    z = rng.integers(-(1 << 63), (1 << 63) - 1, n, dtype=np.int64, endpoint=True)
+    z[rng.random(n) < 0.3] = rng.integers(0, 50, int((rng.random(n) < 0.3).sum()) or 1)[0]
+    return sh, b, z
+
+
+def _order_key(sh, b, z):
+    """Python tuple ordering = row-byte ordering (bin and z unsigned)."""
+    return list(zip(sh.astype(int).tolist(), (b.astype(np.int64) & 0xffff).tolist(),
+                    (z.astype(np.int64).view(np.uint64)).tolist()))
+
+
+def test_clip_key_ranges_matches_brute_force():
+    from geomesa_amd import _lib
+    from geomesa_amd.shard import clip_key_ranges, table_key
+    import torch
+    rng = np.random.default_rng(3)
+    sh, b, z = _rand_keys(rng, 3000)
+    keys = _order_key(sh, b, z)
+    skeys = sorted(keys)
+    for trial in range(40):
+        nr = 30
+        arr = np.zeros(nr, _lib.KEY_RANGE_DTYPE)
+        i = rng.integers(0, len(keys), (nr, 2))
+        for k in range(nr):
+            a, c = sorted([keys[i[k, 0]], keys[i[k, 1]]])
+            if a[0] != c[0]:
+                c = (a[0], 0xffff, (1 << 64) - 1)   # ranges stay inside one shard
+            arr[k]["shard"] = a[0]
+            arr[k]["bin_lo"], arr[k]["bin_hi"] = np.int64(a[1]).astype(np.int16), np.int64(c[1]).astype(np.int16)
+            arr[k]["z_lo"], arr[k]["z_hi"] = np.uint64(a[2]).view(np.int64), np.uint64(c[2]).view(np.int64)
+        lo_i, hi_i = sorted(rng.integers(0, len(skeys), 2))
+        smin, smax = skeys[lo_i], skeys[hi_i]
+
+        def tk(k):
+            h, l_ = table_key(torch.tensor([k[0]], dtype=torch.uint8), torch.tensor([np.int64(k[1]).astype(np.int16)]),
+                              torch.tensor([np.uint64(k[2]).view(np.int64)]))
+            return int(h.item()), int(l_.item())
+        out = clip_key_ranges(arr, tk(smin), tk(smax))
+
+        def inside(rows, k):
+            for r in rows:
+                lo = (int(r["shard"]), int(r["bin_lo"]) & 0xffff, int(np.int64(r["z_lo"]).view(np.uint64)))
+                hi = (int(r["shard"]), int(r["bin_hi"]) & 0xffff, int(np.int64(r["z_hi"]).view(np.uint64)))
+                if lo <= k <= hi:
+                    return True
+            return False
+        for k in keys:
+            assert inside(out, k) == (inside(arr, k) and smin <= k <= smax), (trial, k)
+        assert all(r["shard"] == r["shard"] for r in out)
+    assert len(clip_key_ranges(arr, None, None)) == 0
+
+
+def _xchg_worker(rank, world, port, sizes, q):
+    sys.path.insert(0, ROOT)
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from geomesa_amd.shard import exchange_by_key_range, key_columns, table_key
+        rng = np.random.default_rng(100 + rank)
+        sh, b, z = _rand_keys(rng, sizes[rank])
+        hi, lo = table_key(torch.from_numpy(sh), torch.from_numpy(b), torch.from_numpy(z))
+        o = np.lexsort((lo.numpy(), hi.numpy()))
+        hi, lo = hi[o].contiguous(), lo[o].contiguous()
+        gid = torch.from_numpy(o.astype(np.int64) + rank * 10**6)
+        rh, rl, (rg,), spl = exchange_by_key_range(dist, hi, lo, [gid], samples=64)
+        s2, b2, z2 = key_columns(rh, rl, True)
+        q.put((rank, s2.numpy(), b2.numpy(), z2.numpy(), rg.numpy(), spl[0], spl[1]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,sizes", [(2, (5000, 3001)), (3, (4000, 0, 2500))])
+def test_exchange_by_key_range(world, sizes):
+    """Every row lands on the rank owning its key range, nothing is lost or duplicated, the ranges
+    are ordered, and the split is balanced (an empty rank included)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_xchg_worker, args=(r, world, port, sizes, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = sorted([q.get(timeout=240) for _ in range(world)], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    spl = [(int(h), int(l)) for h, l in zip(got[0][5], got[0][6])]
+    assert all(np.array_equal(g[5], got[0][5]) for g in got)       # same splitters everywhere
+    sent = []
+    for r in range(world):
+        rng = np.random.default_rng(100 + r)
+        sh, b, z = _rand_keys(rng, sizes[r])
+        sent += [(k, i + r * 10**6) for i, k in enumerate(_order_key(sh, b, z))]
+    recv = []
+    bounds = []
+    for r, s2, b2, z2, rg, _, _ in got:
+        ks = _order_key(s2, b2, z2)
+        recv += list(zip(ks, rg.tolist()))
+        bounds.append((min(ks), max(ks)) if ks else None)
+        for k in ks:   # key range of rank r: [splitter r-1, splitter r)
+            kk = (k[0] << 16 | k[1], k[2] ^ (1 << 63))
+            kk = (kk[0], kk[1] - (1 << 64) if kk[1] >= (1 << 63) else kk[1])
+            assert r == 0 or kk >= spl[r - 1]
+            assert r == world - 1 or kk < spl[r]
+    assert sorted(recv) == sorted(sent)
+    nz = [bd for bd in bounds if bd]
+    assert all(nz[i][1] <= nz[i + 1][0] for i in range(len(nz) - 1))
+    n = sum(sizes)
+    assert max(len(g[1]) for g in got) <= 1.35 * n / world
+
+
+def _granges_worker(rank, world, port, q):
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from geomesa_amd.ranges import RANGE_DTYPE
+        from geomesa_amd.shard import gather_ranges
+        nq = 3 + rank
+        cnt = np.arange(nq) % 3 + rank
+        off = np.concatenate([[0], np.cumsum(cnt)]).astype(np.int64)
+        rr = np.zeros(int(off[-1]), RANGE_DTYPE)
+        rr["lower"] = np.arange(len(rr)) + 1000 * rank
+        rr["upper"] = rr["lower"] + 1
+        rr["contained"] = rank
+        g = gather_ranges(dist, off, rr)
+        q.put((rank, g))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gather_ranges():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_granges_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert got[1] is None
+    off, rr = got[0]
+    c0, c1 = np.arange(3) % 3, np.arange(4) % 3 + 1
+    assert off.tolist() == np.concatenate([[0], np.cumsum(np.concatenate([c0, c1]))]).tolist()
+    assert rr["lower"].tolist() == list(range(c0.sum())) + [1000 + i for i in range(c1.sum())]
+    assert rr["contained"].tolist() == [0] * c0.sum() + [1] * c1.sum()

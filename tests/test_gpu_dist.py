@@ -79,3 +79,82 @@ def test_broadcast_index_sharded_join(gpu, oracle):
     got = got[np.lexsort((got[:, 1], got[:, 0]))]
     exp = exp[np.lexsort((exp[:, 1], exp[:, 0]))]
     assert np.array_equal(got, exp)
+
+
+# ---------------------------------------------------------------- key-range partitioned table (configs[2])
+
+def _table_points(n=600_001, seed=4):
+    rng = np.random.default_rng(seed)
+    x = rng.uniform(-180, 180, n)
+    y = rng.uniform(-90, 90, n)
+    t = rng.integers(1590969600000, 1590969600000 + 5 * 604800000, n)   # five weeks from 2020-06-01
+    sh = (np.arange(n) * 2654435761 % 4).astype(np.uint8)               # a 4-way shard byte
+    return x, y, t, sh
+
+
+TABLE_QUERIES = [([(-10, 35, 30, 60)], [(1590969600000, 1591617600000)]),
+                 ([(100, -40, 160, 0)], [(1591500000000, 1592900000000)]),
+                 ([(-180, -90, 180, 90)], [(1590969600000, 1593000000000)]),
+                 ([(0, 0, 0.5, 0.5)], [(1590969600000, 1594000000000)])]
+
+
+def _table_worker(rank, world, port, sharded, q):
+    sys.path.insert(0, ROOT)
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from geomesa_amd.keyspace import during
+        from geomesa_amd.shard import gather_rows, shard_bounds
+        from geomesa_amd.table import PartitionedZ3Table
+        torch.cuda.set_device(0)
+        x, y, t, sh = _table_points()
+        lo, hi = shard_bounds(len(x), rank, world)
+        tb = PartitionedZ3Table.from_points(dist, x[lo:hi], y[lo:hi], t[lo:hi], np.arange(lo, hi),
+                                            shard=sh[lo:hi] if sharded else None, shards=4 if sharded else None,
+                                            samples=256)
+        res = [tb.n]
+        for bxs, ts in TABLE_QUERIES:
+            ids, nm, ns, nr = tb.query(bxs, [during(a, b) for a, b in ts])
+            g = gather_rows(dist, [ids.cpu()])
+            if rank == 0:
+                res.append(np.sort(g[0].numpy()))
+        if rank == 0:
+            q.put(res)
+        else:
+            q.put(res[:1])
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("sharded", [False, True])
+def test_partitioned_table_equals_global_scan(gpu, sharded):
+    """2 ranks on the box's GPU (gloo): rows exchanged by key range, each rank scans the query
+    ranges clipped to its slice; the gathered ids equal one unpartitioned table's scan."""
+    from geomesa_amd.keyspace import during
+    from geomesa_amd.table import Z3Table
+    world = 2
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_table_worker, args=(r, world, port, sharded, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    full = max(got, key=len)
+    sizes = sorted(g[0] for g in got)
+    x, y, t, sh = _table_points()
+    assert sum(sizes) == len(x) and sizes[0] > 0.4 * len(x)   # balanced key ranges
+    tb = Z3Table.from_points(x, y, t, shard=sh if sharded else None)
+    for k, (bxs, ts) in enumerate(TABLE_QUERIES):
+        ids, nm, ns = tb.query(bxs, [during(a, b) for a, b in ts])
+        exp = np.sort(ids.cpu().numpy())
+        assert len(exp) > 0 or k == 3
+        assert np.array_equal(full[1 + k], exp), k
