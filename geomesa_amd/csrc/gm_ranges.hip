@@ -127,11 +127,10 @@ __device__ __forceinline__ int run_rank(const int64_t* keys, int lo, int hi, int
 __device__ int sort_merge(const int64_t* rlo, const int64_t* rhi, const uint8_t* rc, int n, int64_t* gkey,
                           int32_t* gidx, gm_range* out, int64_t* s_key, int16_t* s_idx, int64_t* s_tmp) {
   __shared__ int s_run[MAXRUNS + 1];
-  __shared__ int s_nrun;
   if (n == 0) return 0;
   const bool lds = n <= LDS_SORT;
   // run starts: rlo[j] < rlo[j - 1]
-  if (threadIdx.x == 0) { s_run[0] = 0; s_nrun = 1; }
+  if (threadIdx.x == 0) s_run[0] = 0;
   __syncthreads();
   int64_t nrun = 1;
   for (int c = 0; c < n && nrun <= MAXRUNS; c += RTPB) {

@@ -8,7 +8,7 @@
 //   * gm_z3_key_bytes  -- the row-key prefix bytes, staged through LDS so the stores are 16-B wide;
 //   * gm_sort_keys     -- a stable LSD radix sort of (shard u8, bin u16, z u64) in that byte order,
 //                         8-bit digits, per-block segments: histogram -> one-block scan -> stable
-//                         scatter (wave ballots rank equal digits, LDS reorders each 2048-row tile so
+//                         scatter (wave ballots rank equal digits, LDS reorders each 8192-row tile so
 //                         the global writes are digit runs).  Passes on which every key has the same
 //                         digit are skipped (one extra read computes all 11 digit histograms);
 // The range scan over a sorted table (gm_key_range_scan) lives with the other row-filter scans in
@@ -23,9 +23,6 @@
 namespace gm {
 
 constexpr int STPB = 256;               // sort / scan threads per block
-constexpr int SPER = 8;                 // rows per thread per tile
-constexpr int STILE = STPB * SPER;      // 2048 rows per tile
-constexpr int SNW = STPB / 64;          // waves per block
 constexpr int NPASS = 11;               // digit positions: z bytes 0..7, bin bytes 0..1, shard
 
 __device__ __forceinline__ uint32_t key_digit(uint8_t sh, uint16_t b, uint64_t z, int pass) {
@@ -59,110 +56,177 @@ __global__ __launch_bounds__(STPB) void k_sort_hist_all(const uint8_t* __restric
     if (h[i]) atomicAdd(&ghist[i], h[i]);
 }
 
-// per-block segment histogram of one digit, digit-major: hist[d * gridDim.x + block]
-__global__ __launch_bounds__(STPB) void k_sort_hist(const uint8_t* __restrict__ sh, const uint16_t* __restrict__ bin,
-                                                    const uint64_t* __restrict__ z, int64_t n, int64_t per_block,
-                                                    int pass, uint32_t* __restrict__ hist) {
-  __shared__ uint32_t h[256];
-  h[threadIdx.x] = 0;
+// per-block segment histogram of one digit, digit-major: hist[d * gridDim.x + block].  1024 threads,
+// two rows per lane (16-B z loads), per-wave LDS counters summed at the end.
+constexpr int HT = 1024;
+__global__ __launch_bounds__(HT) void k_sort_hist(const uint8_t* __restrict__ sh, const uint16_t* __restrict__ bin,
+                                                  const uint64_t* __restrict__ z, int64_t n, int64_t per_block,
+                                                  int pass, uint32_t* __restrict__ hist) {
+  __shared__ uint32_t h[HT / 64][256];
+  const int wave = threadIdx.x >> 6;
+  for (int i = threadIdx.x; i < (HT / 64) * 256; i += HT) (&h[0][0])[i] = 0;
   __syncthreads();
   const int64_t b0 = (int64_t)blockIdx.x * per_block, b1 = min(n, b0 + per_block);
-  for (int64_t i = b0 + threadIdx.x; i < b1; i += STPB) {
-    const uint32_t d = pass < 8 ? (uint32_t)(z[i] >> (8 * pass)) & 255u
-                                : pass < 10 ? (uint32_t)(bin[i] >> (8 * (pass - 8))) & 255u : (uint32_t)sh[i];
-    atomicAdd(&h[d], 1u);
+  auto digit = [&](int64_t i) -> uint32_t {
+    return pass < 8 ? (uint32_t)(z[i] >> (8 * pass)) & 255u
+                    : pass < 10 ? (uint32_t)(bin[i] >> (8 * (pass - 8))) & 255u : (uint32_t)sh[i];
+  };
+  for (int64_t i = b0 + 2 * threadIdx.x; i < b1; i += 2 * HT) {   // b0 is even (tile multiple)
+    if (i + 1 < b1) {
+      uint32_t d0, d1;
+      if (pass < 8) {
+        const ulonglong2 zz = *(const ulonglong2*)(z + i);
+        d0 = (uint32_t)(zz.x >> (8 * pass)) & 255u;
+        d1 = (uint32_t)(zz.y >> (8 * pass)) & 255u;
+      } else if (pass < 10) {
+        const ushort2 bb = *(const ushort2*)(bin + i);
+        d0 = (uint32_t)(bb.x >> (8 * (pass - 8))) & 255u;
+        d1 = (uint32_t)(bb.y >> (8 * (pass - 8))) & 255u;
+      } else {
+        const uchar2 ss = *(const uchar2*)(sh + i);
+        d0 = ss.x; d1 = ss.y;
+      }
+      atomicAdd(&h[wave][d0], 1u);
+      atomicAdd(&h[wave][d1], 1u);
+    } else {
+      atomicAdd(&h[wave][digit(i)], 1u);
+    }
   }
   __syncthreads();
-  hist[(int64_t)threadIdx.x * gridDim.x + blockIdx.x] = h[threadIdx.x];
+  if (threadIdx.x < 256) {
+    uint32_t c = 0;
+#pragma unroll
+    for (int w = 0; w < HT / 64; ++w) c += h[w][threadIdx.x];
+    hist[(int64_t)threadIdx.x * gridDim.x + blockIdx.x] = c;
+  }
 }
 
-// Stable scatter of one digit pass.  Each block walks its segment in tiles of 2048 rows laid out
-// slot-major (row = tile + k*256 + thread), which is also the order ranks are assigned in:
-// within a wave, lanes holding the same digit find each other with 8 ballots (one per digit bit);
-// per (slot, wave) digit counts are turned into running offsets per digit; the tile is written to
-// LDS in digit order and streamed out as digit runs at the block's cursor for each digit.
-__global__ __launch_bounds__(STPB) void k_sort_scatter(const uint8_t* __restrict__ sh_in, const uint16_t* __restrict__ bin_in,
-                                                       const uint64_t* __restrict__ z_in,
-                                                       const uint32_t* __restrict__ perm_in, uint8_t* __restrict__ sh_out,
-                                                       uint16_t* __restrict__ bin_out, uint64_t* __restrict__ z_out,
-                                                       uint32_t* __restrict__ perm_out, int64_t n, int64_t per_block,
-                                                       int pass, const uint32_t* __restrict__ off) {
-  __shared__ uint64_t s_z[STILE];
-  __shared__ uint32_t s_perm[STILE];
-  __shared__ uint16_t s_bin[STILE];
-  __shared__ uint8_t s_sh[STILE];
-  __shared__ uint16_t s_cnt[SPER * SNW][256];
-  __shared__ uint32_t s_gcur[256], s_tot[256], s_dstart[256], s_wsum[SNW];
+// Stable scatter of one digit pass, one 1024-thread workgroup per CU.  Each block walks its segment
+// in 8192-row tiles; wave w owns rows [512 w, 512 w + 512) of a tile and reads them in 4 slots of
+// 128 rows, 2 per lane (16-B z loads).  Within a slot, lanes holding the same digit find each other
+// with 16 ballots (8 digit bits x even / odd row); a per-wave LDS counter per digit turns slot ranks
+// into wave ranks, a scan over the waves into block ranks, so a row's place in the tile is (digit,
+// wave, slot, lane, even/odd) = stable.  The tile is reordered in LDS and leaves as digit runs at
+// the block's cursor for each digit (runs average 32 rows for uniform digits: 256-B z segments).
+constexpr int BT = 1024;            // scatter threads per block
+constexpr int BW = BT / 64;         // waves
+constexpr int BSLOT = 4;            // slots of 2 rows per lane
+constexpr int BTILE = BT * 2 * BSLOT;   // 8192 rows per tile
+
+__device__ __forceinline__ uint64_t digit_mask(const uint64_t* bal, uint32_t d) {
+  uint64_t m = ~0ull;
+#pragma unroll
+  for (int bit = 0; bit < 8; ++bit) m &= ((d >> bit) & 1u) ? bal[bit] : ~bal[bit];
+  return m;
+}
+
+__global__ __launch_bounds__(BT) void k_sort_scatter(const uint8_t* __restrict__ sh_in, const uint16_t* __restrict__ bin_in,
+                                                     const uint64_t* __restrict__ z_in,
+                                                     const uint32_t* __restrict__ perm_in, uint8_t* __restrict__ sh_out,
+                                                     uint16_t* __restrict__ bin_out, uint64_t* __restrict__ z_out,
+                                                     uint32_t* __restrict__ perm_out, int64_t n, int64_t per_block,
+                                                     int pass, const uint32_t* __restrict__ off) {
+  __shared__ uint64_t s_z[BTILE];
+  __shared__ uint32_t s_perm[BTILE];
+  __shared__ uint16_t s_bin[BTILE];
+  __shared__ uint8_t s_sh[BTILE];
+  __shared__ uint8_t s_dg[BTILE];
+  __shared__ uint16_t s_wcnt[BW][256];      // per wave: rows of each digit so far (then: wave offsets)
+  __shared__ uint32_t s_gcur[256], s_tot[256], s_dstart[256], s_wsum[4];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  s_gcur[t] = off[(int64_t)t * gridDim.x + blockIdx.x];
+  if (t < 256) s_gcur[t] = off[(int64_t)t * gridDim.x + blockIdx.x];
   const int64_t b0 = (int64_t)blockIdx.x * per_block, b1 = min(n, b0 + per_block);
   const uint64_t lt = lanemask_lt();
-  for (int64_t t0 = b0; t0 < b1; t0 += STILE) {
-    {
-      uint4* c4 = (uint4*)&s_cnt[0][0];
-      for (int i = t; i < SPER * SNW * 256 * 2 / 16; i += STPB) c4[i] = make_uint4(0, 0, 0, 0);
-    }
+  for (int64_t t0 = b0; t0 < b1; t0 += BTILE) {
+    for (int i = t; i < BW * 256 / 2; i += BT) ((uint32_t*)&s_wcnt[0][0])[i] = 0u;
     __syncthreads();
-    uint64_t zv[SPER];
-    uint32_t pv[SPER], dg[SPER];
-    uint16_t bv[SPER];
-    uint8_t sv[SPER];
-    int rk[SPER];
+    uint64_t zv[BSLOT][2];
+    uint32_t pv[BSLOT][2];
+    uint32_t bs[BSLOT][2];   // bin | shard << 16
+    uint32_t rd[BSLOT][2];   // wave rank | digit << 16; rank 0xffff = no row
 #pragma unroll
-    for (int k = 0; k < SPER; ++k) {
-      const int64_t i = t0 + k * STPB + t;
-      const bool ok = i < b1;
-      zv[k] = 0; bv[k] = 0; sv[k] = 0; pv[k] = 0; dg[k] = 0;
-      if (ok) {
-        zv[k] = z_in[i];
-        bv[k] = bin_in[i];
-        sv[k] = sh_in ? sh_in[i] : 0;
-        pv[k] = perm_in ? perm_in[i] : (uint32_t)i;
-        dg[k] = key_digit(sv[k], bv[k], zv[k], pass);
+    for (int k = 0; k < BSLOT; ++k) {
+      const int64_t i = t0 + wave * (2 * 64 * BSLOT) + k * 128 + 2 * lane;
+      const bool ok0 = i < b1, ok1 = i + 1 < b1;
+      if (ok1) {   // both rows: vector loads (i is even and segments start on tile boundaries)
+        const ulonglong2 zz = *(const ulonglong2*)(z_in + i);
+        zv[k][0] = zz.x; zv[k][1] = zz.y;
+        const ushort2 bb = *(const ushort2*)(bin_in + i);
+        uint32_t s0 = 0, s1 = 0;
+        if (sh_in) { const uchar2 ss = *(const uchar2*)(sh_in + i); s0 = ss.x; s1 = ss.y; }
+        bs[k][0] = bb.x | (s0 << 16); bs[k][1] = bb.y | (s1 << 16);
+        if (perm_in) { const uint2 pp = *(const uint2*)(perm_in + i); pv[k][0] = pp.x; pv[k][1] = pp.y; }
+        else { pv[k][0] = (uint32_t)i; pv[k][1] = (uint32_t)(i + 1); }
+      } else {
+        zv[k][0] = ok0 ? z_in[i] : 0; zv[k][1] = 0;
+        bs[k][0] = ok0 ? ((uint32_t)bin_in[i] | ((sh_in ? (uint32_t)sh_in[i] : 0u) << 16)) : 0; bs[k][1] = 0;
+        pv[k][0] = ok0 ? (perm_in ? perm_in[i] : (uint32_t)i) : 0; pv[k][1] = 0;
       }
-      uint64_t m = __ballot(ok);
+      const uint32_t d0 = key_digit((uint8_t)(bs[k][0] >> 16), (uint16_t)bs[k][0], zv[k][0], pass);
+      const uint32_t d1 = key_digit((uint8_t)(bs[k][1] >> 16), (uint16_t)bs[k][1], zv[k][1], pass);
+      uint64_t bal0[8], bal1[8];
 #pragma unroll
       for (int bit = 0; bit < 8; ++bit) {
-        const uint64_t bb = __ballot(ok && ((dg[k] >> bit) & 1u));
-        m &= ((dg[k] >> bit) & 1u) ? bb : ~bb;
+        bal0[bit] = __ballot((d0 >> bit) & 1u);
+        bal1[bit] = __ballot((d1 >> bit) & 1u);
       }
-      const uint64_t below = m & lt;
-      rk[k] = ok ? __popcll(below) : -1;
-      if (ok && below == 0) s_cnt[k * SNW + wave][dg[k]] = (uint16_t)__popcll(m);
+      const uint64_t okm0 = __ballot(ok0), okm1 = __ballot(ok1);
+      // masks of lanes whose even / odd row holds my even / odd row's digit
+      const uint64_t m00 = digit_mask(bal0, d0) & okm0, m01 = digit_mask(bal1, d0) & okm1;
+      const uint64_t m10 = digit_mask(bal0, d1) & okm0, m11 = digit_mask(bal1, d1) & okm1;
+      const uint64_t le = lt | (1ull << lane);
+      const int r0 = __popcll(m00 & lt) + __popcll(m01 & lt);
+      const int r1 = __popcll(m10 & le) + __popcll(m11 & lt);
+      // wave counters: read before this slot's increments, then the first row of each digit adds
+      const uint32_t c0 = s_wcnt[wave][d0], c1 = s_wcnt[wave][d1];
+      rd[k][0] = (ok0 ? c0 + r0 : 0xffffu) | (d0 << 16);
+      rd[k][1] = (ok1 ? c1 + r1 : 0xffffu) | (d1 << 16);
+      __builtin_amdgcn_wave_barrier();
+      if (ok0 && r0 == 0) s_wcnt[wave][d0] = (uint16_t)(c0 + __popcll(m00) + __popcll(m01));
+      if (ok1 && r1 == 0) s_wcnt[wave][d1] = (uint16_t)(c1 + __popcll(m10) + __popcll(m11));
+      __builtin_amdgcn_wave_barrier();
     }
     __syncthreads();
-    {  // running offsets per digit over the (slot, wave) order
-      uint32_t run = 0;
-      for (int s = 0; s < SPER * SNW; ++s) {
-        const uint32_t c = s_cnt[s][t];
-        s_cnt[s][t] = (uint16_t)run;
+    uint32_t run = 0, x = 0;
+    if (t < 256) {   // per digit: exclusive offsets over the waves, and the digit's tile total
+#pragma unroll
+      for (int w = 0; w < BW; ++w) {
+        const uint32_t c = s_wcnt[w][t];
+        s_wcnt[w][t] = (uint16_t)run;
         run += c;
       }
       s_tot[t] = run;
-      // exclusive scan of the digit totals across the block
-      uint32_t x = run;
+      x = run;   // inclusive scan of the digit totals within the wave (waves 0-3 hold the 256 digits)
 #pragma unroll
       for (int o = 1; o < 64; o <<= 1) {
         const uint32_t y = __shfl_up(x, o, 64);
         if (lane >= o) x += y;
       }
       if (lane == 63) s_wsum[wave] = x;
-      __syncthreads();
+    }
+    __syncthreads();
+    if (t < 256) {
       uint32_t pre = 0;
       for (int w = 0; w < wave; ++w) pre += s_wsum[w];
       s_dstart[t] = pre + x - run;
     }
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < SPER; ++k) {
-      if (rk[k] < 0) continue;
-      const uint32_t pos = s_dstart[dg[k]] + s_cnt[k * SNW + wave][dg[k]] + (uint32_t)rk[k];
-      s_z[pos] = zv[k]; s_bin[pos] = bv[k]; s_sh[pos] = sv[k]; s_perm[pos] = pv[k];
+    for (int k = 0; k < BSLOT; ++k) {
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const uint32_t r = rd[k][e] & 0xffffu, d = rd[k][e] >> 16;
+        if (r == 0xffffu) continue;
+        const uint32_t pos = s_dstart[d] + s_wcnt[wave][d] + r;
+        s_z[pos] = zv[k][e]; s_bin[pos] = (uint16_t)bs[k][e]; s_sh[pos] = (uint8_t)(bs[k][e] >> 16);
+        s_perm[pos] = pv[k][e];
+        s_dg[pos] = (uint8_t)d;
+      }
     }
     __syncthreads();
-    const int cnt = (int)min((int64_t)STILE, b1 - t0);
-    for (int q = t; q < cnt; q += STPB) {
-      const uint32_t d = key_digit(s_sh[q], s_bin[q], s_z[q], pass);
+    const int cnt = (int)min((int64_t)BTILE, b1 - t0);
+    for (int q = t; q < cnt; q += BT) {
+      const uint32_t d = s_dg[q];
       const int64_t g = (int64_t)s_gcur[d] + (q - (int)s_dstart[d]);
       z_out[g] = s_z[q];
       bin_out[g] = s_bin[q];
@@ -170,7 +234,7 @@ __global__ __launch_bounds__(STPB) void k_sort_scatter(const uint8_t* __restrict
       perm_out[g] = s_perm[q];
     }
     __syncthreads();
-    s_gcur[t] += s_tot[t];
+    if (t < 256) s_gcur[t] += s_tot[t];
     __syncthreads();
   }
 }
@@ -263,18 +327,17 @@ int gm_sort_keys(gm_ctx* ctx, const uint8_t* shard, const int16_t* bin, const in
     GM_CHECK_LAUNCH();
     return GM_OK;
   }
-  // one resident wave of blocks: the scatter's LDS (~47 KiB) allows 3 blocks per CU, and a grid of
-  // 1024 blocks ran as 768 + a second round of 256
+  // one resident wave of blocks: the scatter's LDS (~139 KiB) allows one 1024-thread block per CU
   static int resident = 0;
   if (!resident) {
     int b = 0, cus = 256;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_sort_scatter, STPB, 0) != hipSuccess || b < 1) b = 2;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_sort_scatter, BT, 0) != hipSuccess || b < 1) b = 1;
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, ctx->device) == hipSuccess) cus = prop.multiProcessorCount;
     resident = b * cus;
   }
-  const int nblk = (int)std::max<int64_t>(1, std::min<int64_t>(resident, (n + STILE - 1) / STILE));
-  const int64_t per = ((n + nblk - 1) / nblk + STILE - 1) / STILE * STILE;
+  const int nblk = (int)std::max<int64_t>(1, std::min<int64_t>(resident, (n + BTILE - 1) / BTILE));
+  const int64_t per = ((n + nblk - 1) / nblk + BTILE - 1) / BTILE * BTILE;
   const int grid = (int)((n + per - 1) / per);
   // ping-pong: the user outputs and one temp set; the last pass lands in the user outputs
   uint8_t* tsh = nullptr;
@@ -310,9 +373,9 @@ int gm_sort_keys(gm_ctx* ctx, const uint8_t* shard, const int16_t* bin, const in
     uint16_t* obin = to_user ? (uint16_t*)bin_out : tbin;
     uint64_t* oz = to_user ? (uint64_t*)z_out : tz;
     uint32_t* operm = (k % 2) ? p1 : p0;
-    hipLaunchKernelGGL(k_sort_hist, dim3(grid), dim3(STPB), 0, s, ish, ibin, iz, n, per, passes[k], hist);
+    hipLaunchKernelGGL(k_sort_hist, dim3(grid), dim3(HT), 0, s, ish, ibin, iz, n, per, passes[k], hist);
     launch_excl_scan(s, hist, (int64_t)256 * grid, hist, hpart, (int64_t*)nullptr);
-    hipLaunchKernelGGL(k_sort_scatter, dim3(grid), dim3(STPB), 0, s, ish, ibin, iz, iperm, osh, obin, oz, operm, n, per,
+    hipLaunchKernelGGL(k_sort_scatter, dim3(grid), dim3(BT), 0, s, ish, ibin, iz, iperm, osh, obin, oz, operm, n, per,
                        passes[k], hist);
     if (hipGetLastError() != hipSuccess) rc = hip_fail(hipErrorLaunchFailure, "k_sort_scatter");
     ish = osh; ibin = obin; iz = oz; iperm = operm;
