@@ -11,9 +11,11 @@
 // time-bin rows of the [n_bins][length] counters in LDS (<= 32768 int32 = 128 KB) and flushes the
 // nonzero counters with one 64-bit device atomic each at the end, so HBM traffic is the 24 B/point
 // read plus grid x counters x 8 B; the grid is one resident wave of workgroups (1-2 per CU).  A
-// histogram larger than one LDS block takes up to HIST_MAX_PASSES passes over the points, one per
-// row block; beyond that it adds straight into the 64-bit device counters (scattered per-lane
-// device atomics run ~22 G/s on MI355X, so they only win over many passes).
+// histogram larger than one LDS block of int32 counters keeps biased 16-bit counters instead (two
+// per word, NARROW below: 1024 x 54 week bins fit one pass), and beyond that takes up to
+// HIST_MAX_PASSES passes over the points, one per row block; beyond that it adds straight into the
+// 64-bit device counters (scattered per-lane device atomics run ~22 G/s on MI355X, so they only win
+// over many passes).
 #include <cmath>
 
 #include "gm_keys.hpp"
@@ -86,21 +88,43 @@ __device__ __forceinline__ int hist_slot_tab(double x, double y, int64_t ms, con
   return i < 0 ? -1 : rb * a.length + i;
 }
 
-template <int PERIOD, bool UNOBS, bool VEC>
+// NARROW: two biased 16-bit counters per 32-bit LDS word (twice the time-bin rows per pass).  A half
+// starts at NB; the thread whose increment lifts it to NB + NS moves NS to the device counter (the
+// decrement that drops it to NB - NS moves -NS), so a half stays within NB +- NS plus the increments
+// in flight and never carries into its neighbour.  The final flush adds half - NB.
+constexpr uint32_t NB = 0x8000u, NS = 0x4000u;
+
+__device__ __forceinline__ void narrow_inc(uint32_t* w, int sh, unsigned long long* g) {
+  const uint32_t old = atomicAdd(w, 1u << sh);
+  if (((old >> sh) & 0xFFFFu) == NB + NS - 1) {
+    atomicSub(w, NS << sh);
+    atomicAdd(g, (unsigned long long)NS);
+  }
+}
+__device__ __forceinline__ void narrow_dec(uint32_t* w, int sh, unsigned long long* g) {
+  const uint32_t old = atomicSub(w, 1u << sh);
+  if (((old >> sh) & 0xFFFFu) == NB - NS + 1) {
+    atomicAdd(w, NS << sh);
+    atomicAdd(g, (unsigned long long)(-(long long)NS));
+  }
+}
+
+template <int PERIOD, bool UNOBS, bool VEC, bool NARROW>
 __global__ __launch_bounds__(HTPB) void k_z3_hist_lds(const double* __restrict__ x, const double* __restrict__ y,
                                                       const int64_t* __restrict__ t, HistArgs a,
                                                       uint8_t* __restrict__ present,
                                                       unsigned long long* __restrict__ counts,
                                                       unsigned long long* __restrict__ tally) {
   extern __shared__ int lds[];
-  int* cnt = lds;                          // [row_n * length]
-  int* pres = lds + a.row_n * a.length;    // [row_n]: bin present (observe sets, unobserve reads)
+  const int total = a.row_n * a.length;
+  const int cwords = NARROW ? (total + 1) / 2 : total;
+  int* cnt = lds;                          // [row_n * length] (NARROW: 16-bit halves)
+  int* pres = lds + cwords;                // [row_n]: bin present (observe sets, unobserve reads)
   uint32_t* sp = (uint32_t*)(pres + a.row_n);  // [2048]: spread3_11 table
   __shared__ int s_skip, s_out;
-  const int total = a.row_n * a.length;
   counts += (int64_t)a.row_lo * a.length;
   present += a.row_lo;
-  for (int i = threadIdx.x; i < total; i += HTPB) cnt[i] = 0;
+  for (int i = threadIdx.x; i < cwords; i += HTPB) cnt[i] = NARROW ? (int)(NB | (NB << 16)) : 0;
   for (int i = threadIdx.x; i < a.row_n; i += HTPB) pres[i] = UNOBS ? (int)present[i] : 0;
   fill_spread_table(sp, threadIdx.x, HTPB);
   if (threadIdx.x == 0) { s_skip = 0; s_out = 0; }
@@ -113,9 +137,13 @@ __global__ __launch_bounds__(HTPB) void k_z3_hist_lds(const double* __restrict__
     if (c < 0 || rb < 0 || rb >= a.row_n) return;
     c -= a.row_lo * a.length;
     if (UNOBS) {
-      if (pres[rb]) atomicAdd(&cnt[c], -1);  // binMap.get(timeBin).foreach(_.add(z, -1))
+      if (pres[rb]) {                        // binMap.get(timeBin).foreach(_.add(z, -1))
+        if (NARROW) narrow_dec((uint32_t*)&cnt[c >> 1], (c & 1) * 16, &counts[c]);
+        else atomicAdd(&cnt[c], -1);
+      }
     } else {
-      atomicAdd(&cnt[c], 1);
+      if (NARROW) narrow_inc((uint32_t*)&cnt[c >> 1], (c & 1) * 16, &counts[c]);
+      else atomicAdd(&cnt[c], 1);
       if (!pres[rb]) pres[rb] = 1;           // binMap.getOrElseUpdate(timeBin, newBins)
     }
   };
@@ -159,7 +187,7 @@ __global__ __launch_bounds__(HTPB) void k_z3_hist_lds(const double* __restrict__
   if (out) atomicAdd(&s_out, out);
   __syncthreads();
   for (int i = threadIdx.x; i < total; i += HTPB) {
-    const int v = cnt[i];
+    const int v = NARROW ? (int)((((uint32_t)cnt[i >> 1]) >> ((i & 1) * 16)) & 0xFFFFu) - (int)NB : cnt[i];
     if (v) atomicAdd(&counts[i], (unsigned long long)(long long)v);
   }
   if (!UNOBS) {
@@ -209,7 +237,10 @@ int launch_hist(gm_ctx* ctx, const double* x, const double* y, const int64_t* t,
   hipStream_t s = ctx->stream;
   // time-bin rows per LDS pass; every pass re-reads the 24 B/point, so more than HIST_MAX_PASSES
   // passes lose to the device-atomic kernel (measured: 2 LDS passes ~12 ms vs 45 ms atomics per 1B)
-  const int rows = (HIST_LDS_MAX) / (a.length + 1);
+  // 32-bit LDS counters when every time-bin row fits one pass, else 16-bit halves (NARROW)
+  const int rows32 = (HIST_LDS_MAX) / (a.length + 1);
+  const bool narrow = rows32 < a.n_bins;
+  const int rows = narrow ? (int)((2 * (int64_t)HIST_LDS_MAX - 2) / (a.length + 2)) : rows32;
   const int passes = rows > 0 ? (a.n_bins + rows - 1) / rows : 1 << 30;
   if (passes <= HIST_MAX_PASSES) {
     const bool vec = aligned16(x) && aligned16(y) && aligned16(t);
@@ -219,25 +250,24 @@ int launch_hist(gm_ctx* ctx, const double* x, const double* y, const int64_t* t,
       a.row_lo = k * rows;
       a.row_n = std::min(rows, a.n_bins - a.row_lo);
       a.tally = k == 0;
-      const size_t lds = (size_t)(a.row_n * a.length + a.row_n + 2048) * sizeof(int);
+      const int64_t cwords = narrow ? ((int64_t)a.row_n * a.length + 1) / 2 : (int64_t)a.row_n * a.length;
+      const size_t lds = (size_t)(cwords + a.row_n + 2048) * sizeof(int);
       const int per_cu = lds <= 72 * 1024 ? 2 : 1;  // 2 x 1024 threads is the CU's wave limit
       // per workgroup <= 2^31 increments so the int32 LDS counters cannot wrap
       const int64_t need = (a.n + (int64_t)2147483647 - 1) / (int64_t)2147483647;
       const int64_t want = (a.n + HTPB - 1) / HTPB;
       int64_t grid = std::min<int64_t>((int64_t)cus * per_cu, std::max<int64_t>(want, 1));
       grid = std::max(grid, need);
-      if (vec) {
-        GM_HIP(hipFuncSetAttribute((const void*)k_z3_hist_lds<PERIOD, UNOBS, true>,
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        hipLaunchKernelGGL((k_z3_hist_lds<PERIOD, UNOBS, true>), dim3((unsigned)grid), dim3(HTPB), lds, s, x, y,
-                           t, a, present, counts, tally);
-      } else {
-        GM_HIP(hipFuncSetAttribute((const void*)k_z3_hist_lds<PERIOD, UNOBS, false>,
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        hipLaunchKernelGGL((k_z3_hist_lds<PERIOD, UNOBS, false>), dim3((unsigned)grid), dim3(HTPB), lds, s, x,
-                           y, t, a, present, counts, tally);
-      }
-      GM_CHECK_LAUNCH();
+      auto go = [&](auto kern) -> int {
+        GM_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(HTPB), lds, s, x, y, t, a, present, counts, tally);
+        GM_CHECK_LAUNCH();
+        return GM_OK;
+      };
+      int rc;
+      if (vec) rc = narrow ? go(k_z3_hist_lds<PERIOD, UNOBS, true, true>) : go(k_z3_hist_lds<PERIOD, UNOBS, true, false>);
+      else rc = narrow ? go(k_z3_hist_lds<PERIOD, UNOBS, false, true>) : go(k_z3_hist_lds<PERIOD, UNOBS, false, false>);
+      if (rc) return rc;
     }
   } else {
     hipLaunchKernelGGL((k_z3_hist_global<PERIOD, UNOBS>), dim3((unsigned)std::min<int64_t>((a.n + 255) / 256, 256 * 16)),

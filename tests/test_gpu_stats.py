@@ -55,6 +55,27 @@ def test_z3_histogram_parity(gpu, oracle, period, length, lo, nb):
     assert np.array_equal(P2, op)
 
 
+@pytest.mark.parametrize("length,lo,nb", [(1024, 2600, 53), (64, 2607, 4)])
+def test_z3_histogram_hot_counters(gpu, oracle, length, lo, nb):
+    """8M features on 3 positions: tens of thousands of increments per counter per workgroup, past the
+    16-bit counters' spill threshold (length 1024 x 53 runs the NARROW path) and the int32 path."""
+    rng = np.random.default_rng(9)
+    n = 8_000_000
+    k = rng.integers(0, 3, n)
+    x = np.array([10.0, -75.5, 139.7])[k]
+    y = np.array([47.0, 40.1, 35.6])[k]
+    t = np.array([T2020 + 5 * 86400000, T2020 + 5 * 86400000 + 1, T2020 + 9 * 86400000])[k]
+    P, C, tl = run_hist(x, y, t, WEEK, length, lo, nb)
+    op, oc, ot = oracle.z3_histogram(x, y, t, length, lo, nb, period=WEEK)
+    assert np.array_equal(C, oc) and np.array_equal(P, op) and np.array_equal(tl, ot)
+    assert C.max() > 2_000_000
+    h = 6_000_000
+    P2, C2, _ = run_hist(x[:h], y[:h], t[:h], WEEK, length, lo, nb, True, P, C)
+    oracle.z3_histogram(x[:h], y[:h], t[:h], length, lo, nb, unobserve=True, period=WEEK, present=op, counts=oc,
+                        tally=ot)
+    assert np.array_equal(C2, oc) and np.array_equal(P2, op)
+
+
 def test_z3_histogram_unaligned_and_small(gpu, oracle):
     import torch
     from geomesa_amd import _lib
