@@ -227,10 +227,10 @@ def ranges_batch(dist, fn, args, n_local, nq, reps=3):
 
 
 def sort_bytes(b, z, n):
-    """Algorithmic bytes of gm_sort_keys over n rows: the all-digit histogram read (10 B/row), per
-    non-constant byte digit a histogram read of its column (8 B z / 2 B bin) and a scatter that reads
-    and writes z, bin and the 4-B permutation (none read on the first pass), then the 4 -> 8 B widening
-    of the permutation.  Returns (bytes, passes)."""
+    """Algorithmic bytes of gm_sort_keys over n rows: the OR/AND read of the key columns that finds
+    the constant digits (10 B/row), then per non-constant byte digit a histogram read of its column
+    (8 B z / 2 B bin) and a scatter that reads and writes z, bin and the 4-B permutation (none read on
+    the first pass; the last pass writes it as 8 B).  Returns (bytes, passes)."""
     import torch
     passes = []
     for p in range(8):
@@ -242,7 +242,7 @@ def sort_bytes(b, z, n):
         d = (bb >> (8 * p)) & 255
         if int(d.min()) != int(d.max()):
             passes.append(2)
-    total = 10.0 * n + sum(h + 28.0 for h in passes) * n - (4.0 * n if passes else 0) + 12.0 * n
+    total = 10.0 * n + sum(h + 28.0 for h in passes) * n - (4.0 * n if passes else 0) + (4.0 * n if passes else 0)
     return total, len(passes)
 
 
@@ -325,8 +325,8 @@ def bench_table(a, dist, ctx, b, z):
                       "roofline": dict(roofline(sbytes, ms_sort), bytes_per_unit=round(sbytes / NT, 2),
                                        kernel="gm_sort_keys (all launches of one sort)"),
                       "note": "stable LSD radix sort of (bin, z) into table byte order (ingest side); bytes = "
-                              "10 B/row digit census + per pass (digit column read + 28 B/row scatter) + 12 B/row "
-                              "permutation widening"},
+                              "10 B/row OR/AND read + per pass (digit column read + 28 B/row scatter; no permutation "
+                              "read on the first pass, an 8-B permutation written on the last)"},
         "table_ingest": {"value": NT * dist.world / (ms_ingest * 1e-3), "unit": "rows/s", "ms_per_step": ms_ingest,
                          "rows_per_gpu": NT, "slice_rows": slice_rows,
                          "note": "key-range partitioned table: local sort, splitter sampling (1024 keys per rank), "

@@ -36,24 +36,46 @@ __device__ __forceinline__ uint64_t lanemask_lt() {
   return lane ? (~0ull >> (64 - lane)) : 0ull;
 }
 
-// all 11 digit histograms in one read: a pass whose histogram has one bucket holding every key is
-// skipped (its scatter would be the identity)
-__global__ __launch_bounds__(STPB) void k_sort_hist_all(const uint8_t* __restrict__ sh, const uint16_t* __restrict__ bin,
-                                                        const uint64_t* __restrict__ z, int64_t n,
-                                                        uint32_t* __restrict__ ghist) {
-  __shared__ uint32_t h[NPASS * 256];
-  for (int i = threadIdx.x; i < NPASS * 256; i += STPB) h[i] = 0;
-  __syncthreads();
-  for (int64_t i = (int64_t)blockIdx.x * STPB + threadIdx.x; i < n; i += (int64_t)gridDim.x * STPB) {
-    const uint64_t zz = z[i];
-    const uint16_t b = bin[i];
-    const uint8_t s = sh ? sh[i] : 0;
+// which digit passes carry information: the OR and the AND of every key column (a digit on which
+// OR == AND is the same for every key, so its pass would be the identity and is skipped).
+// acc[0] = OR z, acc[1] = OR (bin | shard << 16), acc[2] = AND z, acc[3] = AND (bin | shard << 16).
+__device__ __forceinline__ uint64_t wave_or(uint64_t v) {
 #pragma unroll
-    for (int p = 0; p < NPASS; ++p) atomicAdd(&h[p * 256 + key_digit(s, b, zz, p)], 1u);
+  for (int o = 32; o > 0; o >>= 1) v |= __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ uint64_t wave_and(uint64_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v &= __shfl_xor(v, o, 64);
+  return v;
+}
+__global__ __launch_bounds__(STPB) void k_key_or_and(const uint8_t* __restrict__ sh, const uint16_t* __restrict__ bin,
+                                                     const uint64_t* __restrict__ z, int64_t n,
+                                                     unsigned long long* __restrict__ acc, int vec) {
+  uint64_t zo = 0, za = ~0ull, bo = 0, ba = ~0ull;
+  const int64_t np = n >> 1;   // pairs: 16-B z loads
+  for (int64_t p = (int64_t)blockIdx.x * STPB + threadIdx.x; p < np; p += (int64_t)gridDim.x * STPB) {
+    uint64_t z0, z1, b0, b1;
+    if (vec) {
+      const ulonglong2 zz = *(const ulonglong2*)(z + 2 * p);
+      const ushort2 bb = *(const ushort2*)(bin + 2 * p);
+      z0 = zz.x; z1 = zz.y; b0 = bb.x; b1 = bb.y;
+      if (sh) { const uchar2 ss = *(const uchar2*)(sh + 2 * p); b0 |= (uint64_t)ss.x << 16; b1 |= (uint64_t)ss.y << 16; }
+    } else {
+      z0 = z[2 * p]; z1 = z[2 * p + 1]; b0 = bin[2 * p]; b1 = bin[2 * p + 1];
+      if (sh) { b0 |= (uint64_t)sh[2 * p] << 16; b1 |= (uint64_t)sh[2 * p + 1] << 16; }
+    }
+    zo |= z0 | z1; za &= z0 & z1;
+    bo |= b0 | b1; ba &= b0 & b1;
   }
-  __syncthreads();
-  for (int i = threadIdx.x; i < NPASS * 256; i += STPB)
-    if (h[i]) atomicAdd(&ghist[i], h[i]);
+  if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
+    const uint64_t b0 = (uint64_t)bin[n - 1] | (sh ? (uint64_t)sh[n - 1] << 16 : 0);
+    zo |= z[n - 1]; za &= z[n - 1]; bo |= b0; ba &= b0;
+  }
+  zo = wave_or(zo); za = wave_and(za); bo = wave_or(bo); ba = wave_and(ba);
+  if ((threadIdx.x & 63) == 0) {
+    atomicOr(&acc[0], zo); atomicOr(&acc[1], bo); atomicAnd(&acc[2], za); atomicAnd(&acc[3], ba);
+  }
 }
 
 // per-block segment histogram of one digit, digit-major: hist[d * gridDim.x + block].  1024 threads,
@@ -61,7 +83,7 @@ __global__ __launch_bounds__(STPB) void k_sort_hist_all(const uint8_t* __restric
 constexpr int HT = 1024;
 __global__ __launch_bounds__(HT) void k_sort_hist(const uint8_t* __restrict__ sh, const uint16_t* __restrict__ bin,
                                                   const uint64_t* __restrict__ z, int64_t n, int64_t per_block,
-                                                  int pass, uint32_t* __restrict__ hist) {
+                                                  int pass, uint32_t* __restrict__ hist, int vec) {
   __shared__ uint32_t h[HT / 64][256];
   const int wave = threadIdx.x >> 6;
   for (int i = threadIdx.x; i < (HT / 64) * 256; i += HT) (&h[0][0])[i] = 0;
@@ -72,7 +94,7 @@ __global__ __launch_bounds__(HT) void k_sort_hist(const uint8_t* __restrict__ sh
                     : pass < 10 ? (uint32_t)(bin[i] >> (8 * (pass - 8))) & 255u : (uint32_t)sh[i];
   };
   for (int64_t i = b0 + 2 * threadIdx.x; i < b1; i += 2 * HT) {   // b0 is even (tile multiple)
-    if (i + 1 < b1) {
+    if (vec && i + 1 < b1) {
       uint32_t d0, d1;
       if (pass < 8) {
         const ulonglong2 zz = *(const ulonglong2*)(z + i);
@@ -90,6 +112,7 @@ __global__ __launch_bounds__(HT) void k_sort_hist(const uint8_t* __restrict__ sh
       atomicAdd(&h[wave][d1], 1u);
     } else {
       atomicAdd(&h[wave][digit(i)], 1u);
+      if (i + 1 < b1) atomicAdd(&h[wave][digit(i + 1)], 1u);
     }
   }
   __syncthreads();
@@ -124,8 +147,9 @@ __global__ __launch_bounds__(BT) void k_sort_scatter(const uint8_t* __restrict__
                                                      const uint64_t* __restrict__ z_in,
                                                      const uint32_t* __restrict__ perm_in, uint8_t* __restrict__ sh_out,
                                                      uint16_t* __restrict__ bin_out, uint64_t* __restrict__ z_out,
-                                                     uint32_t* __restrict__ perm_out, int64_t n, int64_t per_block,
-                                                     int pass, const uint32_t* __restrict__ off) {
+                                                     uint32_t* __restrict__ perm_out, int64_t* __restrict__ perm64_out,
+                                                     int64_t n, int64_t per_block, int pass,
+                                                     const uint32_t* __restrict__ off, int vec) {
   __shared__ uint64_t s_z[BTILE];
   __shared__ uint32_t s_perm[BTILE];
   __shared__ uint16_t s_bin[BTILE];
@@ -137,18 +161,16 @@ __global__ __launch_bounds__(BT) void k_sort_scatter(const uint8_t* __restrict__
   if (t < 256) s_gcur[t] = off[(int64_t)t * gridDim.x + blockIdx.x];
   const int64_t b0 = (int64_t)blockIdx.x * per_block, b1 = min(n, b0 + per_block);
   const uint64_t lt = lanemask_lt();
-  for (int64_t t0 = b0; t0 < b1; t0 += BTILE) {
-    for (int i = t; i < BW * 256 / 2; i += BT) ((uint32_t*)&s_wcnt[0][0])[i] = 0u;
-    __syncthreads();
-    uint64_t zv[BSLOT][2];
-    uint32_t pv[BSLOT][2];
-    uint32_t bs[BSLOT][2];   // bin | shard << 16
-    uint32_t rd[BSLOT][2];   // wave rank | digit << 16; rank 0xffff = no row
+  uint64_t zv[BSLOT][2];
+  uint32_t pv[BSLOT][2];
+  uint32_t bs[BSLOT][2];   // bin | shard << 16
+  // this lane's rows of the tile at t0 into registers (the next tile's loads are issued before the
+  // current tile leaves LDS, so they overlap its global writes)
+  auto load = [&](int64_t t0) {
 #pragma unroll
     for (int k = 0; k < BSLOT; ++k) {
       const int64_t i = t0 + wave * (2 * 64 * BSLOT) + k * 128 + 2 * lane;
-      const bool ok0 = i < b1, ok1 = i + 1 < b1;
-      if (ok1) {   // both rows: vector loads (i is even and segments start on tile boundaries)
+      if (vec && i + 1 < b1) {   // both rows: vector loads (i is even: segments start on tile boundaries)
         const ulonglong2 zz = *(const ulonglong2*)(z_in + i);
         zv[k][0] = zz.x; zv[k][1] = zz.y;
         const ushort2 bb = *(const ushort2*)(bin_in + i);
@@ -158,10 +180,25 @@ __global__ __launch_bounds__(BT) void k_sort_scatter(const uint8_t* __restrict__
         if (perm_in) { const uint2 pp = *(const uint2*)(perm_in + i); pv[k][0] = pp.x; pv[k][1] = pp.y; }
         else { pv[k][0] = (uint32_t)i; pv[k][1] = (uint32_t)(i + 1); }
       } else {
-        zv[k][0] = ok0 ? z_in[i] : 0; zv[k][1] = 0;
-        bs[k][0] = ok0 ? ((uint32_t)bin_in[i] | ((sh_in ? (uint32_t)sh_in[i] : 0u) << 16)) : 0; bs[k][1] = 0;
-        pv[k][0] = ok0 ? (perm_in ? perm_in[i] : (uint32_t)i) : 0; pv[k][1] = 0;
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const bool ok = i + e < b1;
+          zv[k][e] = ok ? z_in[i + e] : 0;
+          bs[k][e] = ok ? ((uint32_t)bin_in[i + e] | ((sh_in ? (uint32_t)sh_in[i + e] : 0u) << 16)) : 0;
+          pv[k][e] = ok ? (perm_in ? perm_in[i + e] : (uint32_t)(i + e)) : 0;
+        }
       }
+    }
+  };
+  if (b0 < b1) load(b0);
+  for (int64_t t0 = b0; t0 < b1; t0 += BTILE) {
+    for (int i = t; i < BW * 256 / 2; i += BT) ((uint32_t*)&s_wcnt[0][0])[i] = 0u;
+    __syncthreads();
+    uint32_t rd[BSLOT][2];   // wave rank | digit << 16; rank 0xffff = no row
+#pragma unroll
+    for (int k = 0; k < BSLOT; ++k) {
+      const int64_t i = t0 + wave * (2 * 64 * BSLOT) + k * 128 + 2 * lane;
+      const bool ok0 = i < b1, ok1 = i + 1 < b1;
       const uint32_t d0 = key_digit((uint8_t)(bs[k][0] >> 16), (uint16_t)bs[k][0], zv[k][0], pass);
       const uint32_t d1 = key_digit((uint8_t)(bs[k][1] >> 16), (uint16_t)bs[k][1], zv[k][1], pass);
       uint64_t bal0[8], bal1[8];
@@ -224,6 +261,7 @@ __global__ __launch_bounds__(BT) void k_sort_scatter(const uint8_t* __restrict__
       }
     }
     __syncthreads();
+    if (t0 + BTILE < b1) load(t0 + BTILE);
     const int cnt = (int)min((int64_t)BTILE, b1 - t0);
     for (int q = t; q < cnt; q += BT) {
       const uint32_t d = s_dg[q];
@@ -231,11 +269,11 @@ __global__ __launch_bounds__(BT) void k_sort_scatter(const uint8_t* __restrict__
       z_out[g] = s_z[q];
       bin_out[g] = s_bin[q];
       if (sh_out) sh_out[g] = s_sh[q];
-      perm_out[g] = s_perm[q];
+      if (perm64_out) perm64_out[g] = s_perm[q];
+      else perm_out[g] = s_perm[q];
     }
     __syncthreads();
     if (t < 256) s_gcur[t] += s_tot[t];
-    __syncthreads();
   }
 }
 
@@ -301,21 +339,26 @@ int gm_sort_keys(gm_ctx* ctx, const uint8_t* shard, const int16_t* bin, const in
     return GM_E_INVALID;
   hipStream_t s = ctx->stream;
   const uint8_t* sh = shard;
-  // which digit passes carry information
-  uint32_t* ghist = nullptr;
-  GM_HIP(hipMallocAsync((void**)&ghist, NPASS * 256 * 4, s));
-  GM_HIP(hipMemsetAsync(ghist, 0, NPASS * 256 * 4, s));
-  hipLaunchKernelGGL(k_sort_hist_all, dim3((unsigned)std::min<int64_t>(2048, (n + STPB - 1) / STPB)), dim3(STPB), 0, s, sh,
-                     (const uint16_t*)bin, (const uint64_t*)z, n, ghist);
+  // 16-B z / 4-B bin / 2-B shard pair loads need aligned caller columns (the workspaces are)
+  const bool user_vec = ((uintptr_t)z % 16) == 0 && ((uintptr_t)bin % 4) == 0 && (!sh || ((uintptr_t)sh % 2) == 0);
+  const bool out_vec = ((uintptr_t)z_out % 16) == 0 && ((uintptr_t)bin_out % 4) == 0 &&
+                       (!sh || ((uintptr_t)shard_out % 2) == 0);
+  // which digit passes carry information (k_key_or_and)
+  unsigned long long* acc = (unsigned long long*)ctx->d_scratch;
+  GM_HIP(hipMemsetAsync(acc, 0, 16, s));
+  GM_HIP(hipMemsetAsync(acc + 2, 0xff, 16, s));
+  hipLaunchKernelGGL(k_key_or_and, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(2048, (n / 2 + STPB - 1) / STPB))),
+                     dim3(STPB), 0, s, sh, (const uint16_t*)bin, (const uint64_t*)z, n, acc, (int)user_vec);
   GM_CHECK_LAUNCH();
-  std::vector<uint32_t> h(NPASS * 256);
-  GM_HIP(hipMemcpyAsync(h.data(), ghist, NPASS * 256 * 4, hipMemcpyDeviceToHost, s));
+  unsigned long long hacc[4];
+  GM_HIP(hipMemcpyAsync(hacc, acc, sizeof(hacc), hipMemcpyDeviceToHost, s));
   GM_HIP(hipStreamSynchronize(s));
-  GM_HIP(hipFreeAsync(ghist, s));
   std::vector<int> passes;
   for (int p = 0; p < NPASS; ++p) {
     if (p == 10 && !sh) continue;
-    if (*std::max_element(h.begin() + p * 256, h.begin() + (p + 1) * 256) != (uint32_t)n) passes.push_back(p);
+    const uint64_t o = p < 8 ? hacc[0] >> (8 * p) : hacc[1] >> (8 * (p - 8));
+    const uint64_t a = p < 8 ? hacc[2] >> (8 * p) : hacc[3] >> (8 * (p - 8));
+    if (((o ^ a) & 255u) != 0) passes.push_back(p);
   }
   const int np = (int)passes.size();
   if (np == 0) {  // every key equal: table order = input order
@@ -373,17 +416,15 @@ int gm_sort_keys(gm_ctx* ctx, const uint8_t* shard, const int16_t* bin, const in
     uint16_t* obin = to_user ? (uint16_t*)bin_out : tbin;
     uint64_t* oz = to_user ? (uint64_t*)z_out : tz;
     uint32_t* operm = (k % 2) ? p1 : p0;
-    hipLaunchKernelGGL(k_sort_hist, dim3(grid), dim3(HT), 0, s, ish, ibin, iz, n, per, passes[k], hist);
+    // pass 0 reads the caller's columns, a later pass reads the caller's outputs or the workspace
+    const int vec = k == 0 ? (int)user_vec : (((np - k) % 2) == 0 ? (int)out_vec : 1);
+    hipLaunchKernelGGL(k_sort_hist, dim3(grid), dim3(HT), 0, s, ish, ibin, iz, n, per, passes[k], hist, vec);
     launch_excl_scan(s, hist, (int64_t)256 * grid, hist, hpart, (int64_t*)nullptr);
-    hipLaunchKernelGGL(k_sort_scatter, dim3(grid), dim3(BT), 0, s, ish, ibin, iz, iperm, osh, obin, oz, operm, n, per,
-                       passes[k], hist);
+    const bool last = k == np - 1;   // the last pass writes the 64-bit permutation itself
+    hipLaunchKernelGGL(k_sort_scatter, dim3(grid), dim3(BT), 0, s, ish, ibin, iz, iperm, osh, obin, oz,
+                       last ? nullptr : operm, last ? perm_out : nullptr, n, per, passes[k], hist, vec);
     if (hipGetLastError() != hipSuccess) rc = hip_fail(hipErrorLaunchFailure, "k_sort_scatter");
     ish = osh; ibin = obin; iz = oz; iperm = operm;
-  }
-  if (!rc) {
-    hipLaunchKernelGGL(k_widen_perm, dim3((unsigned)std::min<int64_t>(4096, (n + STPB - 1) / STPB)), dim3(STPB), 0, s,
-                       iperm, n, perm_out);
-    if (hipGetLastError() != hipSuccess) rc = hip_fail(hipErrorLaunchFailure, "k_widen_perm");
   }
   return rc;
 }

@@ -60,6 +60,31 @@ def test_sort_keys_parity(gpu, n, kind, sharded):
         assert np.array_equal(as_np(os_), shard[order])
 
 
+@pytest.mark.parametrize("in_off,out_off", [(1, 0), (0, 1), (1, 3)])
+def test_sort_keys_unaligned_columns(gpu, in_off, out_off):
+    """Caller columns off the 16-B grid (slices): the pair-load paths must not be taken for them."""
+    import torch
+    from geomesa_amd import _lib
+    n = 150_001
+    rng = np.random.default_rng(11)
+    bins = rng.integers(-2**15, 2**15, n).astype(np.int16)
+    z = rng.integers(-2**63, 2**63 - 1, n, dtype=np.int64, endpoint=True)
+    shard = rng.integers(0, 3, n).astype(np.uint8)
+    pad = lambda a, o: torch.from_numpy(np.concatenate([np.zeros(o, a.dtype), a])).cuda()[o:]
+    db, dz, ds = pad(bins, in_off), pad(z, in_off), pad(shard, in_off)
+    ob = torch.empty(n + out_off, dtype=torch.int16, device="cuda")[out_off:]
+    oz = torch.empty(n + out_off, dtype=torch.int64, device="cuda")[out_off:]
+    os_ = torch.empty(n + out_off, dtype=torch.uint8, device="cuda")[out_off:]
+    op = torch.empty(n, dtype=torch.int64, device="cuda")
+    ctx = _lib.context()
+    _lib.check(ctx.lib.gm_sort_keys(ctx.handle, _lib.ptr(ds), _lib.ptr(db), _lib.ptr(dz), n, _lib.ptr(os_),
+                                    _lib.ptr(ob), _lib.ptr(oz), _lib.ptr(op)), "sort")
+    order = expected_order(bins, z, shard)
+    assert np.array_equal(as_np(op), order)
+    assert np.array_equal(as_np(ob), bins[order]) and np.array_equal(as_np(oz), z[order])
+    assert np.array_equal(as_np(os_), shard[order])
+
+
 @pytest.mark.parametrize("sharded", [False, True])
 def test_key_bytes(gpu, sharded):
     from geomesa_amd.table import Z3Table
