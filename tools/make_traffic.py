@@ -1,6 +1,6 @@
 """Per-launch HBM traffic from rocprofv3 FETCH_SIZE / WRITE_SIZE passes -> profiles/pmc_traffic.json.
 
-usage: python tools/make_traffic.py PMC_DIR OUT_JSON [points] [join_points]
+usage: python tools/make_traffic.py PMC_DIR OUT_JSON [points] [join_points] [table_rows]
 
 FETCH_SIZE and WRITE_SIZE are in KiB per dispatch.  MI355X_MICROARCH.md (HBM section): on gfx950
 FETCH_SIZE reports exactly half of the bytes of a wide coalesced streaming read (16 B per lane), so
@@ -26,6 +26,7 @@ STREAMING = {
     "xz2_index": ("k_xz2_index_v", "xz", 40.0),
     "z3_histogram": ("k_z3_hist_lds<", "points", 24.0),
     "pip_relate": ("k_pip_relate", "points", 21.0),
+    "sort_scatter": ("k_sort_scatter", "rows", 28.0),
 }
 # join step kernels and the points per dispatch: direct = one pass per 2^31 points, partitioned =
 # hist + scan + scatter + join per 2^28-point chunk
@@ -54,14 +55,14 @@ def mean_for(d, sub, counter):
     return sum(vals) / len(vals) if vals else None
 
 
-def main(root, out, points=1_000_000_000, join_points=1_000_000_000):
+def main(root, out, points=1_000_000_000, join_points=1_000_000_000, table_rows=250_000_000):
     d = per_dispatch(root)
     res = {}
     for name, (sub, unit, alg) in STREAMING.items():
         f, w = mean_for(d, sub, "FETCH_SIZE"), mean_for(d, sub, "WRITE_SIZE")
         if f is None or w is None:
             continue
-        n = points if unit == "points" else min(points, 200_000_000)
+        n = points if unit == "points" else (table_rows if unit == "rows" else min(points, 200_000_000))
         fb, wb = 2.0 * f * 1024, w * 1024
         res[name] = {"n": n, "kernel": sub, "bytes_per_launch": fb + wb, "fetch_bytes": fb, "write_bytes": wb,
                      "fetch_size_raw_kib": f, "write_size_kib": w, "algorithmic_bytes": alg * n,
@@ -89,7 +90,8 @@ def main(root, out, points=1_000_000_000, join_points=1_000_000_000):
                                 "note": "rocprofv3 SQ_INSTS_VALU_FLOPS_FP64 per dispatch of the direct join kernel"}
     json.dump(res, open(out, "w"), indent=1, sort_keys=True)
     for k, v in res.items():
-        print("%-14s %8.2f GB/launch" % (k, v["bytes_per_launch"] / 1e9))
+        if "bytes_per_launch" in v:
+            print("%-14s %8.2f GB/launch" % (k, v["bytes_per_launch"] / 1e9))
 
 
 if __name__ == "__main__":
