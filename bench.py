@@ -620,8 +620,14 @@ def main():
                                       "note": "the reference's per-pair RayCrossingCounter work (7 FP64 ops x E_c); the "
                                               "grid index resolves most pairs without it, so a fraction > 1 is work avoided"}
             fpm = load_profile("pip_join_fp64", J)
-            if fpm:
-                pj["roofline"]["fp64"]["sq_insts_valu_flops_fp64"] = fpm["sq_insts_valu_flops_fp64"]
+            if fpm:   # what the kernel itself executes: SQ_INSTS_VALU_FLOPS_FP64 (FLOPs per wave
+                # instruction, gfx950) x 64 lanes, an upper bound (inactive lanes counted)
+                kf = 64.0 * fpm["sq_insts_valu_flops_fp64"] * dist.world
+                pj["roofline"]["fp64"].update(
+                    sq_insts_valu_flops_fp64=fpm["sq_insts_valu_flops_fp64"], kernel_flops_max=kf,
+                    kernel_fp64_frac_max=kf / (jms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS,
+                    kernel_note="profiles/pmc_traffic.json pip_join_fp64: the grid kernel's own FP64 work is "
+                                "far below the FP64 peak; the join is bound by dependent index loads")
         # row-wise st_contains (the UDF path without the join rule): row i = (its cell's county, point i)
         x0c, y0c, x1c, y1c = CONUS
         rid = (torch.clamp(((py - y0c) / (y1c - y0c) * gy).long(), 0, gy - 1) * gx +

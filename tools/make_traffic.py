@@ -62,7 +62,7 @@ def main(root, out, points=1_000_000_000, join_points=1_000_000_000, table_rows=
         f, w = mean_for(d, sub, "FETCH_SIZE"), mean_for(d, sub, "WRITE_SIZE")
         if f is None or w is None:
             continue
-        n = points if unit == "points" else (table_rows if unit == "rows" else min(points, 200_000_000))
+        n = points if unit == "points" else (table_rows if unit == "rows" else min(points, 100_000_000))
         fb, wb = 2.0 * f * 1024, w * 1024
         res[name] = {"n": n, "kernel": sub, "bytes_per_launch": fb + wb, "fetch_bytes": fb, "write_bytes": wb,
                      "fetch_size_raw_kib": f, "write_size_kib": w, "algorithmic_bytes": alg * n,
