@@ -229,6 +229,10 @@ int gm_ctx_set_param(gm_ctx* c, int param, int64_t value) {
       if (value < 0) return GM_E_INVALID;
       c->join_chunk = value;
       return GM_OK;
+    case GM_PARAM_INDEX_BUILD:
+      if (value != 0 && value != 1) return GM_E_INVALID;
+      c->index_build = value;
+      return GM_OK;
     default:
       gm::set_error("gm_ctx_set_param: unknown parameter");
       return GM_E_INVALID;
@@ -239,6 +243,7 @@ int gm_ctx_get_param(gm_ctx* c, int param, int64_t* value) {
   if (!c || !value) return GM_E_INVALID;
   switch (param) {
     case GM_PARAM_JOIN_CHUNK: *value = c->join_chunk; return GM_OK;
+    case GM_PARAM_INDEX_BUILD: *value = c->index_build; return GM_OK;
     default: return GM_E_INVALID;
   }
 }

@@ -21,6 +21,7 @@ struct gm_ctx {
   size_t ws_cap[4] = {0, 0, 0, 0};
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   int64_t join_chunk = 0;          // GM_PARAM_JOIN_CHUNK: rows per join pass (0 = each strategy's default)
+  int64_t index_build = 0;         // GM_PARAM_INDEX_BUILD: 0 = device build of the join index, 1 = host build
   int64_t ranges_hint = 0;         // largest batched-ranges output seen (sizes the device batch buffer)
 };
 

@@ -1194,6 +1194,455 @@ void launch_query(hipStream_t s, unsigned grid, int op, const double* x, const d
 
 }  // namespace gm
 
+// ------------------------------------------------------------------ index build on the device
+// The same classification as the host build below (gm_pip_index_create_ex), one workgroup per task
+// = (polygon, grid row): the row band's ring segments are gathered in ring / vertex order (LDS, or a
+// global slice for polygons with more edges than BAND_LDS), then every cell of the row is tested
+// against them in parallel; the cells that no segment meets take the location of their run's first
+// cell centre (PointLocator, probed once per run as on the host); boundary cells get a compact or a
+// generic blob.  A count pass sizes every slot (cell of a task), a scan turns the sizes into offsets
+// in slot order -- the host build's polygon / row / column order -- and the write pass fills the
+// blobs, so the arrays are byte-identical to the host build's.
+namespace gm {
+
+constexpr int BT_TPB = 256;
+constexpr int BAND_LDS = 1024;   // band segments kept in LDS; larger polygons use a global slice
+constexpr int BUILD_MAXR = 512;  // rings per polygon handled on the device
+constexpr int BUILD_MAXBK = 64;  // breakpoints collected per (cell, ring): more = slow ring
+
+struct BandView {
+  int32_t* seg;      // global vertex id of the segment end
+  int32_t* ring;     // ring list index k
+  double* minx;
+  double* maxx;
+  double* ymin;
+  double* ymax;
+};
+
+struct BuildArgs {
+  const int32_t* poly_part_off;
+  const int32_t* part_ring_off;
+  const int32_t* ring_vert_off;
+  const double* vx;
+  const double* vy;
+  const RingDev* rings;
+  const double* env;            // 4 per polygon
+  const int32_t* task_poly;
+  const int32_t* task_cy;
+  const int64_t* task_slot;     // [ntask + 1]
+  const int64_t* band_off;      // per task: global band slice offset, -1 = LDS
+  BandView band_g;
+  double G0, G1, inv_cw, inv_ch, epsx, epsy;
+  int gx, gy;
+  int write;
+  int32_t* gen_words;           // count pass: generic blob words (even) per slot
+  int32_t* cmp_lines;           // count pass: compact lines per slot
+  const int64_t* gen_off;       // write pass: word offset per slot
+  const int64_t* cmp_off;       // write pass: line offset per slot
+  uint32_t* ent_word;           // write pass: entry word per slot (0xffffffff = none)
+  int32_t* ent_cell;
+  double* blob;
+  double* compact;
+  unsigned long long* stat;     // count pass: [0] slow rings, [1] ring records, [2] boundary, [3] compact
+};
+
+__device__ __forceinline__ int ring_locate_dev(const BuildArgs& a, int r, double px, double py) {
+  const RingDev rd = a.rings[r];
+  const int v0 = a.ring_vert_off[r], v1 = a.ring_vert_off[r + 1];
+  if (v1 - v0 < 1) return LOC_EXTERIOR;
+  if (!(px >= rd.minx && px <= rd.maxx && py >= rd.miny && py <= rd.maxy)) return LOC_EXTERIOR;
+  int crossings = 0;
+  for (int i = v0 + 1; i < v1; ++i)
+    if (count_segment(a.vx[i], a.vy[i], a.vx[i - 1], a.vy[i - 1], px, py, crossings)) return LOC_BOUNDARY;
+  return (crossings & 1) ? LOC_INTERIOR : LOC_EXTERIOR;
+}
+
+// PointLocator.locate(point, polygon): parts (shell, then holes) with the Mod-2 rule across parts
+__device__ int poly_locate_dev(const BuildArgs& a, int poly, double px, double py) {
+  bool is_in = false;
+  int nb = 0;
+  for (int q = a.poly_part_off[poly]; q < a.poly_part_off[poly + 1]; ++q) {
+    const int r0 = a.part_ring_off[q], r1 = a.part_ring_off[q + 1];
+    if (r1 <= r0) continue;
+    int loc = ring_locate_dev(a, r0, px, py);
+    if (loc == LOC_INTERIOR) {
+      for (int r = r0 + 1; r < r1; ++r) {
+        const int hl = ring_locate_dev(a, r, px, py);
+        if (hl == LOC_INTERIOR) { loc = LOC_EXTERIOR; break; }
+        if (hl == LOC_BOUNDARY) { loc = LOC_BOUNDARY; break; }
+      }
+    }
+    if (loc == LOC_INTERIOR) is_in = true;
+    if (loc == LOC_BOUNDARY) nb++;
+  }
+  if (nb & 1) return LOC_BOUNDARY;
+  if (nb > 0 || is_in) return LOC_INTERIOR;
+  return LOC_EXTERIOR;
+}
+
+// breakpoints of (cell, ring k): y of right-of-cell segment end points in (yb0, yb1], ascending,
+// unique (host collect_breakpoints); returns the count, > BUILD_MAXBK - 1 when there are more
+__device__ int cell_breakpoints(const BandView& b, int s0, int s1, double xb1, double yb0, double yb1, double* bk) {
+  int n = 0;
+  for (int s = s0; s < s1; ++s) {
+    if (!(b.minx[s] > xb1)) continue;
+    const double ys[2] = {b.ymin[s], b.ymax[s]};
+    for (int e = 0; e < 2; ++e) {
+      const double y = ys[e];
+      if (!(y > yb0 && y <= yb1)) continue;
+      int j = 0;   // insertion into the sorted unique list
+      while (j < n && bk[j] < y) ++j;
+      if (j < n && bk[j] == y) continue;
+      if (n >= BUILD_MAXBK) return BUILD_MAXBK;   // too many: the ring is slow
+      for (int m = n; m > j; --m) bk[m] = bk[m - 1];
+      bk[j] = y;
+      ++n;
+    }
+  }
+  return n;
+}
+
+// parity of right-of-cell segments straddling y (ymin <= y < ymax) at each breakpoint interval's
+// left end (host right_parity)
+__device__ uint64_t cell_parity(const BandView& b, int s0, int s1, double xb1, double yb0, const double* bk, int nbk) {
+  uint64_t parity = 0;
+  for (int j = 0; j <= nbk; ++j) {
+    const double yk = j == 0 ? yb0 : bk[j - 1];
+    int c = 0;
+    for (int s = s0; s < s1; ++s)
+      if (b.minx[s] > xb1) c += (b.ymin[s] <= yk && yk < b.ymax[s]);
+    if (c & 1) parity |= 1ull << j;
+  }
+  return parity;
+}
+
+__device__ __forceinline__ double i32x2_word(int32_t lo, int32_t hi) {
+  return __longlong_as_double((long long)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo));
+}
+
+__global__ __launch_bounds__(BT_TPB) void k_build_rows(BuildArgs a) {
+  __shared__ int32_t l_seg[BAND_LDS], l_ring[BAND_LDS];
+  __shared__ double l_minx[BAND_LDS], l_maxx[BAND_LDS], l_ymin[BAND_LDS], l_ymax[BAND_LDS];
+  __shared__ int32_t s_ring_id[BUILD_MAXR], s_bstart[BUILD_MAXR + 1];
+  __shared__ uint8_t s_shell[BUILD_MAXR];
+  __shared__ int32_t s_wcnt[BT_TPB / 64];
+  __shared__ int s_nr, s_changed;
+  __shared__ uint8_t s_bnd[BT_TPB];
+  __shared__ int32_t s_probe[BT_TPB];
+  __shared__ int8_t s_loc[BT_TPB];
+  const int task = blockIdx.x;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int p = a.task_poly[task], cy = a.task_cy[task];
+  const double* e = a.env + 4 * (int64_t)p;
+  const int cx0 = cell_of(e[0], a.G0, a.inv_cw, a.gx), cx1 = cell_of(e[2], a.G0, a.inv_cw, a.gx);
+  const double yb0 = __dsub_rn(__dadd_rn(a.G1, __ddiv_rn((double)cy, a.inv_ch)), a.epsy);
+  const double yb1 = __dadd_rn(__dadd_rn(a.G1, __ddiv_rn((double)(cy + 1), a.inv_ch)), a.epsy);
+  const int64_t slot0 = a.task_slot[task];
+  BandView b;
+  if (a.band_off[task] < 0) {
+    b = BandView{l_seg, l_ring, l_minx, l_maxx, l_ymin, l_ymax};
+  } else {
+    const int64_t o = a.band_off[task];
+    b = BandView{a.band_g.seg + o, a.band_g.ring + o, a.band_g.minx + o, a.band_g.maxx + o, a.band_g.ymin + o,
+                 a.band_g.ymax + o};
+  }
+  // ring list of the polygon (RingRef order of the host build)
+  if (t == 0) {
+    int nr = 0;
+    for (int q = a.poly_part_off[p]; q < a.poly_part_off[p + 1]; ++q)
+      for (int r = a.part_ring_off[q]; r < a.part_ring_off[q + 1]; ++r) {
+        if (nr < BUILD_MAXR) { s_ring_id[nr] = r; s_shell[nr] = r == a.part_ring_off[q]; }
+        ++nr;
+      }
+    s_nr = nr;
+  }
+  __syncthreads();
+  const int nr = s_nr;   // <= BUILD_MAXR (the host checks)
+  // band: per ring, the segments whose y-range meets the row band, in vertex order
+  int nb = 0;
+  for (int k = 0; k < nr; ++k) {
+    if (t == 0) s_bstart[k] = nb;
+    const int r = s_ring_id[k];
+    const int v0 = a.ring_vert_off[r], v1 = a.ring_vert_off[r + 1];
+    for (int c = v0 + 1; c < v1; c += BT_TPB) {
+      const int i = c + t;
+      bool in = false;
+      double ya = 0, yb = 0;
+      if (i < v1) {
+        ya = a.vy[i - 1]; yb = a.vy[i];
+        const double ymn = ya < yb ? ya : yb, ymx = ya < yb ? yb : ya;
+        in = !(ymx < yb0 || ymn > yb1);
+      }
+      const uint64_t m = __ballot(in);
+      if (lane == 0) s_wcnt[wave] = __popcll(m);
+      __syncthreads();
+      int pre = 0, tot = 0;
+      for (int w = 0; w < BT_TPB / 64; ++w) { if (w < wave) pre += s_wcnt[w]; tot += s_wcnt[w]; }
+      if (in) {
+        const int pos = nb + pre + __popcll(m & ((1ull << lane) - 1));
+        const double xa = a.vx[i - 1], xb = a.vx[i];
+        b.seg[pos] = i; b.ring[pos] = k;
+        b.minx[pos] = xa < xb ? xa : xb; b.maxx[pos] = xa < xb ? xb : xa;
+        b.ymin[pos] = ya < yb ? ya : yb; b.ymax[pos] = ya < yb ? yb : ya;
+      }
+      nb += tot;
+      __syncthreads();
+    }
+  }
+  if (t == 0) s_bstart[nr] = nb;
+  __syncthreads();
+  // the row's cells in segments of BT_TPB, with the run location carried between segments
+  int carried = -1;   // run_loc of the host loop after the previous segment
+  for (int c0 = cx0; c0 <= cx1; c0 += BT_TPB) {
+    const int cx = c0 + t;
+    const bool valid = cx <= cx1;
+    const double xb0 = __dsub_rn(__dadd_rn(a.G0, __ddiv_rn((double)cx, a.inv_cw)), a.epsx);
+    const double xb1 = __dadd_rn(__dadd_rn(a.G0, __ddiv_rn((double)(cx + 1), a.inv_cw)), a.epsx);
+    bool bnd = false;
+    if (valid)
+      for (int s = 0; s < nb && !bnd; ++s) bnd = b.maxx[s] >= xb0 && b.minx[s] <= xb1;
+    s_bnd[t] = valid ? (uint8_t)bnd : 1;
+    __syncthreads();
+    // probes: non-boundary cells after a boundary cell (or starting a run) locate their centre (the
+    // host's run_loc < 0 case).  A probe whose centre falls outside its cell, or lands on the
+    // boundary, becomes a boundary cell, which makes its successor a probe: iterate to a fixpoint
+    bool probe = false, evaluated = false;
+    int ploc = -1;
+    for (;;) {
+      if (t == 0) s_changed = 0;
+      __syncthreads();
+      const bool prev_bnd = t == 0 ? (carried < 0) : (s_bnd[t - 1] != 0);
+      probe = valid && !s_bnd[t] && prev_bnd;
+      bool fail = false;
+      if (probe && !evaluated) {
+        evaluated = true;
+        const double cxm = __dadd_rn(a.G0, __ddiv_rn((double)cx + 0.5, a.inv_cw));
+        const double cym = __dadd_rn(a.G1, __ddiv_rn((double)cy + 0.5, a.inv_ch));
+        if (cell_of(cxm, a.G0, a.inv_cw, a.gx) != cx || cell_of(cym, a.G1, a.inv_ch, a.gy) != cy) fail = true;
+        else {
+          ploc = poly_locate_dev(a, p, cxm, cym);
+          fail = ploc == LOC_BOUNDARY;
+        }
+      }
+      __syncthreads();
+      if (fail) { s_bnd[t] = 1; s_changed = 1; }
+      __syncthreads();
+      const int ch = s_changed;
+      __syncthreads();
+      if (!ch) break;
+    }
+    bnd = valid && s_bnd[t];
+    s_loc[t] = probe ? (int8_t)ploc : (int8_t)-1;
+    s_probe[t] = probe ? t : -1;
+    __syncthreads();
+    // last probe at or before each cell (inclusive max scan)
+    for (int o = 1; o < BT_TPB; o <<= 1) {
+      const int v = t >= o ? s_probe[t - o] : -1;
+      __syncthreads();
+      if (v > s_probe[t]) s_probe[t] = v;
+      __syncthreads();
+    }
+    int loc = -1;
+    if (valid && !bnd) loc = s_probe[t] >= 0 ? s_loc[s_probe[t]] : carried;
+    // this cell's output
+    const int64_t slot = slot0 + (cx - cx0);
+    if (valid) {
+      int gw = 0, cl = 0;
+      uint32_t word = 0xffffffffu;
+      const int32_t cell = cy * a.gx + cx;
+      if (!bnd && loc == LOC_INTERIOR) word = (CELL_INTERIOR << 30) | (uint32_t)p;
+      if (bnd) {
+        double bk[BUILD_MAXBK];
+        bool compact = false;
+        if (nr == 1) {
+          int E = 0;
+          for (int s = 0; s < nb; ++s) E += (b.maxx[s] >= xb0 && b.minx[s] <= xb1);
+          if (4 * E <= 30) {
+            const int B = cell_breakpoints(b, 0, nb, xb1, yb0, yb1, bk);
+            if (4 * E + B <= 30) {
+              compact = true;
+              cl = (4 * E + B <= 14 && E <= 3) ? 1 : 2;
+              if (a.write) {
+                double* rec = a.compact + 16 * a.cmp_off[slot];
+                for (int w = 0; w < 16 * cl; ++w) rec[w] = INFINITY;
+                rec[0] = i32x2_word(p, E | (cl << 8));
+                rec[1] = __longlong_as_double((long long)cell_parity(b, 0, nb, xb1, yb0, bk, B));
+                uint32_t used = 3u;   // word bits of the record in use
+                int j = 0;
+                for (int s = 0; s < nb; ++s) {
+                  if (!(b.maxx[s] >= xb0 && b.minx[s] <= xb1)) continue;
+                  const int i = b.seg[s], w0 = cseg_word(j);
+                  rec[w0] = a.vx[i]; rec[w0 + 1] = a.vy[i]; rec[w0 + 2] = a.vx[i - 1]; rec[w0 + 3] = a.vy[i - 1];
+                  used |= 15u << w0;
+                  ++j;
+                }
+                int w = 2;
+                for (int m = 0; m < B; ++m) {
+                  while ((used >> w) & 1u) ++w;
+                  rec[w] = bk[m];
+                  used |= 1u << w;
+                }
+                word = (CELL_BOUNDARY << 30) | BLOB_COMPACT | (uint32_t)a.cmp_off[slot];
+              } else {
+                atomicAdd(&a.stat[2], 1ull);
+                atomicAdd(&a.stat[3], 1ull);
+              }
+            }
+          }
+        }
+        if (!compact) {
+          double* out = a.write ? a.blob + a.gen_off[slot] : nullptr;
+          int w = 0;
+          if (out) out[w] = i32x2_word(p, nr);
+          ++w;
+          for (int k = 0; k < nr; ++k) {
+            const int s0 = s_bstart[k], s1 = s_bstart[k + 1];
+            int E = 0;
+            for (int s = s0; s < s1; ++s) E += (b.maxx[s] >= xb0 && b.minx[s] <= xb1);
+            const int B = cell_breakpoints(b, s0, s1, xb1, yb0, yb1, bk);
+            const bool slow = E > 4096 || B > 63;
+            if (out) {
+              RingHdr rh{};
+              rh.flags = (int16_t)((s_shell[k] ? 1 : 0) | (slow ? 2 : 0));
+              rh.n_edge = slow ? 0 : (int16_t)E;
+              rh.n_brk = slow ? 0 : (int16_t)B;
+              double hw;
+              memcpy(&hw, &rh, 8);
+              out[w] = hw;
+              const uint64_t par = slow ? (uint64_t)(uint32_t)s_ring_id[k] : cell_parity(b, s0, s1, xb1, yb0, bk, B);
+              out[w + 1] = __longlong_as_double((long long)par);
+              int q = w + 2;
+              if (!slow) {
+                for (int s = s0; s < s1; ++s) {
+                  if (!(b.maxx[s] >= xb0 && b.minx[s] <= xb1)) continue;
+                  const int i = b.seg[s];
+                  out[q] = a.vx[i]; out[q + 1] = a.vy[i]; out[q + 2] = a.vx[i - 1]; out[q + 3] = a.vy[i - 1];
+                  q += 4;
+                }
+                for (int m = 0; m < B; ++m) out[q++] = bk[m];
+              }
+            } else {
+              if (slow) atomicAdd(&a.stat[0], 1ull);
+              atomicAdd(&a.stat[1], 1ull);
+            }
+            w += 2 + (slow ? 0 : 4 * E + B);
+          }
+          gw = (w + 1) & ~1;
+          if (out) {
+            if (w & 1) out[w] = 0.0;
+            word = (CELL_BOUNDARY << 30) | (uint32_t)(a.gen_off[slot] / 2);
+          } else {
+            atomicAdd(&a.stat[2], 1ull);
+          }
+        }
+      }
+      if (a.write) { a.ent_word[slot] = word; a.ent_cell[slot] = cell; }
+      else { a.gen_words[slot] = gw; a.cmp_lines[slot] = cl; }
+    }
+    // run location after this segment's last cell
+    __syncthreads();
+    const int last = cx1 - c0 < BT_TPB - 1 ? cx1 - c0 : BT_TPB - 1;
+    if (t == last) s_probe[0] = (valid && !bnd) ? loc : -1;   // reuse: carried run location
+    __syncthreads();
+    carried = s_probe[0];
+    __syncthreads();
+  }
+}
+
+// entries per cell (count pass over the slots)
+__global__ void k_build_cell_count(const uint32_t* __restrict__ ent_word, const int32_t* __restrict__ ent_cell,
+                                   int64_t nslot, int32_t* __restrict__ per_cell, int32_t* __restrict__ bnd_cell) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nslot; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t w = ent_word[i];
+    if (w == 0xffffffffu) continue;
+    atomicAdd(&per_cell[ent_cell[i]], 1);
+    if ((w >> 30) == CELL_BOUNDARY) atomicAdd(&bnd_cell[ent_cell[i]], 1);
+  }
+}
+
+// scatter the entries into per-cell buckets (any order; sorted by polygon per cell afterwards)
+__global__ void k_build_cell_scatter(const uint32_t* __restrict__ ent_word, const int32_t* __restrict__ ent_cell,
+                                     int64_t nslot, const int64_t* __restrict__ cell_start, int32_t* __restrict__ fill,
+                                     uint32_t* __restrict__ bucket, const int32_t* __restrict__ slot_poly) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nslot; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t w = ent_word[i];
+    if (w == 0xffffffffu) continue;
+    const int c = ent_cell[i];
+    const int64_t pos = cell_start[c] + atomicAdd(&fill[c], 1);
+    bucket[2 * pos] = w;
+    bucket[2 * pos + 1] = (uint32_t)slot_poly[i];
+  }
+}
+
+// list slot count of a cell: (long-list count slot) + entries, padded to 4 (16-B aligned lists)
+__device__ __forceinline__ int list_len(int k) { return k > 1 ? ((k + (k >= LIST_LONG ? 1 : 0) + 3) & ~3) : 0; }
+
+__global__ void k_build_list_len(const int32_t* __restrict__ per_cell, int64_t ncell, int32_t* __restrict__ len) {
+  for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < ncell; c += (int64_t)gridDim.x * blockDim.x)
+    len[c] = list_len(per_cell[c]);
+}
+
+// cell words and lists: each cell's entries sorted by polygon (the host order), single entries inline
+__global__ void k_build_cells(const int32_t* __restrict__ per_cell, const int64_t* __restrict__ cell_start,
+                              uint32_t* __restrict__ bucket, const int64_t* __restrict__ list_off, int64_t ncell,
+                              uint32_t* __restrict__ cell_word, uint32_t* __restrict__ list_ent) {
+  for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < ncell; c += (int64_t)gridDim.x * blockDim.x) {
+    const int k = per_cell[c];
+    uint32_t* bk = bucket + 2 * cell_start[c];
+    for (int i = 1; i < k; ++i) {   // insertion sort by polygon
+      const uint32_t w = bk[2 * i], pl = bk[2 * i + 1];
+      int j = i - 1;
+      while (j >= 0 && bk[2 * j + 1] > pl) { bk[2 * (j + 1)] = bk[2 * j]; bk[2 * (j + 1) + 1] = bk[2 * j + 1]; --j; }
+      bk[2 * (j + 1)] = w; bk[2 * (j + 1) + 1] = pl;
+    }
+    if (k == 0) { cell_word[c] = 0xffffffffu; continue; }
+    if (k == 1) { cell_word[c] = bk[0]; continue; }
+    const int64_t off = list_off[c];
+    cell_word[c] = (CELL_LIST << 30) | (uint32_t)((off / 4) << 4) | (uint32_t)(k < LIST_LONG ? k : LIST_LONG);
+    int64_t q = off;
+    if (k >= LIST_LONG) list_ent[q++] = (uint32_t)k;
+    for (int j = 0; j < k; ++j) list_ent[q++] = bk[2 * j];
+    const int64_t end = off + list_len(k);
+    while (q < end) list_ent[q++] = 0u;
+  }
+}
+
+// coarse words: the fine word when every fine cell carries the same EMPTY or INTERIOR word, else LIST
+__global__ void k_build_coarse(const uint32_t* __restrict__ cell_word, int gx, int gy, int gxc, int gyc,
+                               uint32_t* __restrict__ coarse_word) {
+  const int64_t n = (int64_t)gxc * gyc;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int yc = (int)(i / gxc), xc = (int)(i % gxc);
+    uint32_t w = 0xffffffffu;
+    bool first = true, mixed = false;
+    for (int yy = yc << CF_LOG; yy < min(gy, (yc + 1) << CF_LOG) && !mixed; ++yy)
+      for (int xx = xc << CF_LOG; xx < min(gx, (xc + 1) << CF_LOG); ++xx) {
+        const uint32_t f = cell_word[(int64_t)yy * gx + xx];
+        if (first) { w = f; first = false; }
+        else if (f != w) { mixed = true; break; }
+      }
+    const uint32_t kind = w >> 30;
+    coarse_word[i] = (!mixed && (kind == CELL_EMPTY || kind == CELL_INTERIOR)) ? w : (CELL_LIST << 30);
+  }
+}
+
+__global__ void k_build_max(const int32_t* __restrict__ v, int64_t n, int* __restrict__ out) {
+  int m = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    m = max(m, v[i]);
+  for (int o = 32; o > 0; o >>= 1) m = max(m, __shfl_xor(m, o, 64));
+  if ((threadIdx.x & 63) == 0) atomicMax(out, m);
+}
+
+__global__ void k_build_slot_poly(const int32_t* __restrict__ task_poly, const int64_t* __restrict__ task_slot,
+                                  int ntask, int32_t* __restrict__ slot_poly) {
+  const int task = blockIdx.x;
+  if (task >= ntask) return;
+  for (int64_t i = task_slot[task] + threadIdx.x; i < task_slot[task + 1]; i += blockDim.x) slot_poly[i] = task_poly[task];
+}
+
+}  // namespace gm
+
 struct gm_pip_index {
   gm_ctx* ctx = nullptr;
   gm::PipDev dev{};
@@ -1287,8 +1736,239 @@ int build_threads() {
   return (int)std::max(1u, std::min(64u, hc ? hc : 1u));
 }
 
+// fn(i) for i in [0, n) over the build threads (contiguous blocks of items per thread)
+template <class F>
+void parallel_for(int n, F fn) {
+  const int nth = std::max(1, std::min(build_threads(), n / 64));
+  if (nth <= 1) { for (int i = 0; i < n; ++i) fn(i); return; }
+  std::atomic<int> next{0};
+  auto work = [&]() {
+    for (;;) {
+      const int b = next.fetch_add(64);
+      if (b >= n) break;
+      for (int i = b; i < std::min(n, b + 64); ++i) fn(i);
+    }
+  };
+  std::vector<std::thread> th;
+  for (int t = 1; t < nth; ++t) th.emplace_back(work);
+  work();
+  for (auto& t : th) t.join();
+}
+
 double now_s() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// Device build of the cell words, coarse words, lists and blobs (k_build_rows and friends); the
+// rings / slab arrays stay host-built.  Returns GM_OK, an error, or 1 = "not handled here" (the
+// caller then runs the host classification).  Fills ix arrays 3-7 and the counters.
+int build_cells_device(gm_ctx* ctx, gm_pip_index* ix, const gm_polyset* ps, const std::vector<double>& env,
+                       const double* G, double inv_cw, double inv_ch, double epsx, double epsy, int gx, int gy,
+                       const RingDev* d_rings) {
+  hipStream_t s = ctx->stream;
+  const int P = ps->n_polys;
+  const int n_parts = P ? ps->poly_part_off[P] : 0;
+  const int n_rings = n_parts ? ps->part_ring_off[n_parts] : 0;
+  const int n_verts = n_rings ? ps->ring_vert_off[n_rings] : 0;
+  // tasks = (polygon, row); slots = cells of a task's row
+  std::vector<int32_t> task_poly, task_cy;
+  std::vector<int64_t> task_slot{0}, band_off;
+  int64_t band_total = 0;
+  for (int p = 0; p < P; ++p) {
+    const double* e = &env[4 * (size_t)p];
+    if (!(e[0] <= e[2])) continue;
+    int nr = 0, ne = 0;
+    for (int q = ps->poly_part_off[p]; q < ps->poly_part_off[p + 1]; ++q)
+      for (int r = ps->part_ring_off[q]; r < ps->part_ring_off[q + 1]; ++r) {
+        ++nr;
+        ne += std::max(0, ps->ring_vert_off[r + 1] - ps->ring_vert_off[r] - 1);
+      }
+    if (nr > BUILD_MAXR) return 1;
+    const int cx0 = host::cell_of(e[0], G[0], inv_cw, gx), cx1 = host::cell_of(e[2], G[0], inv_cw, gx);
+    const int cy0 = host::cell_of(e[1], G[1], inv_ch, gy), cy1 = host::cell_of(e[3], G[1], inv_ch, gy);
+    for (int cy = cy0; cy <= cy1; ++cy) {
+      task_poly.push_back(p);
+      task_cy.push_back(cy);
+      task_slot.push_back(task_slot.back() + (cx1 - cx0 + 1));
+      if (ne > BAND_LDS) { band_off.push_back(band_total); band_total += ne; }
+      else band_off.push_back(-1);
+    }
+  }
+  const int64_t ntask = (int64_t)task_poly.size(), nslot = task_slot.back();
+  if (ntask == 0 || ntask > INT32_MAX) return 1;
+  const int64_t ncell = (int64_t)gx * gy;
+  std::vector<void*> tmp;
+  auto dalloc = [&](size_t bytes, void** p) -> int {
+    GM_HIP(hipMalloc(p, std::max<size_t>(bytes, 16)));
+    tmp.push_back(*p);
+    return GM_OK;
+  };
+  auto cleanup = [&]() { for (void* p : tmp) (void)hipFree(p); tmp.clear(); };
+  auto up = [&](const void* h, size_t bytes, void** d) -> int {
+    int rc = dalloc(bytes, d);
+    if (!rc && bytes) rc = copy_h2d(ctx, *d, h, bytes);
+    return rc;
+  };
+  BuildArgs a{};
+  int rc = GM_OK;
+  void *d_ppo, *d_pro, *d_rvo, *d_vx, *d_vy, *d_env, *d_tp, *d_tc, *d_ts, *d_bo;
+  rc = up(ps->poly_part_off, (size_t)(P + 1) * 4, &d_ppo);
+  if (!rc) rc = up(ps->part_ring_off, (size_t)(n_parts + 1) * 4, &d_pro);
+  if (!rc) rc = up(ps->ring_vert_off, (size_t)(n_rings + 1) * 4, &d_rvo);
+  if (!rc) rc = up(ps->vx, (size_t)n_verts * 8, &d_vx);
+  if (!rc) rc = up(ps->vy, (size_t)n_verts * 8, &d_vy);
+  if (!rc) rc = up(env.data(), env.size() * 8, &d_env);
+  if (!rc) rc = up(task_poly.data(), (size_t)ntask * 4, &d_tp);
+  if (!rc) rc = up(task_cy.data(), (size_t)ntask * 4, &d_tc);
+  if (!rc) rc = up(task_slot.data(), (size_t)(ntask + 1) * 8, &d_ts);
+  if (!rc) rc = up(band_off.data(), (size_t)ntask * 8, &d_bo);
+  void *d_bseg = nullptr, *d_bring = nullptr, *d_bmnx = nullptr, *d_bmxx = nullptr, *d_bmny = nullptr, *d_bmxy = nullptr;
+  if (!rc) rc = dalloc((size_t)band_total * 4, &d_bseg);
+  if (!rc) rc = dalloc((size_t)band_total * 4, &d_bring);
+  if (!rc) rc = dalloc((size_t)band_total * 8, &d_bmnx);
+  if (!rc) rc = dalloc((size_t)band_total * 8, &d_bmxx);
+  if (!rc) rc = dalloc((size_t)band_total * 8, &d_bmny);
+  if (!rc) rc = dalloc((size_t)band_total * 8, &d_bmxy);
+  void *d_gw, *d_cl, *d_goff, *d_coff, *d_part, *d_stat;
+  const int64_t np = scan_partials_len(nslot);
+  if (!rc) rc = dalloc((size_t)nslot * 4, &d_gw);
+  if (!rc) rc = dalloc((size_t)nslot * 4, &d_cl);
+  if (!rc) rc = dalloc((size_t)(nslot + 1) * 8, &d_goff);
+  if (!rc) rc = dalloc((size_t)(nslot + 1) * 8, &d_coff);
+  if (!rc) rc = dalloc((size_t)std::max(np, scan_partials_len(ncell)) * 8, &d_part);
+  if (!rc) rc = dalloc(8 * 8, &d_stat);
+  if (rc) { cleanup(); return rc; }
+  GM_HIP(hipMemsetAsync(d_stat, 0, 64, s));
+  a.poly_part_off = (const int32_t*)d_ppo; a.part_ring_off = (const int32_t*)d_pro;
+  a.ring_vert_off = (const int32_t*)d_rvo; a.vx = (const double*)d_vx; a.vy = (const double*)d_vy;
+  a.rings = d_rings; a.env = (const double*)d_env;
+  a.task_poly = (const int32_t*)d_tp; a.task_cy = (const int32_t*)d_tc; a.task_slot = (const int64_t*)d_ts;
+  a.band_off = (const int64_t*)d_bo;
+  a.band_g = BandView{(int32_t*)d_bseg, (int32_t*)d_bring, (double*)d_bmnx, (double*)d_bmxx, (double*)d_bmny,
+                      (double*)d_bmxy};
+  a.G0 = G[0]; a.G1 = G[1]; a.inv_cw = inv_cw; a.inv_ch = inv_ch; a.epsx = epsx; a.epsy = epsy;
+  a.gx = gx; a.gy = gy;
+  a.gen_words = (int32_t*)d_gw; a.cmp_lines = (int32_t*)d_cl;
+  a.stat = (unsigned long long*)d_stat;
+  // count pass -> slot offsets
+  a.write = 0;
+  hipLaunchKernelGGL(k_build_rows, dim3((unsigned)ntask), dim3(BT_TPB), 0, s, a);
+  GM_CHECK_LAUNCH();
+  launch_excl_scan(s, (const int32_t*)d_gw, nslot, (int64_t*)d_goff, (int64_t*)d_part, (int64_t*)d_goff + nslot);
+  launch_excl_scan(s, (const int32_t*)d_cl, nslot, (int64_t*)d_coff, (int64_t*)d_part, (int64_t*)d_coff + nslot);
+  GM_CHECK_LAUNCH();
+  int64_t tot_words = 0, tot_lines = 0;
+  unsigned long long st[4];
+  rc = copy_d2h(ctx, &tot_words, (int64_t*)d_goff + nslot, 8);
+  if (!rc) rc = copy_d2h(ctx, &tot_lines, (int64_t*)d_coff + nslot, 8);
+  if (!rc) rc = copy_d2h(ctx, st, d_stat, sizeof st);
+  if (rc) { cleanup(); return rc; }
+  if (tot_words / 2 >= (int64_t)BLOB_COMPACT || tot_lines >= (int64_t)BLOB_COMPACT) {
+    cleanup();
+    gm::set_error("gm_pip_index_create: boundary blobs too large (lower cells_per_poly)");
+    return GM_E_CAPACITY;
+  }
+  // the index arrays this build produces
+  void *d_blob, *d_cmp, *d_cw, *d_coarse, *d_list;
+  const int64_t blob_words = std::max<int64_t>(tot_words, 1), cmp_words = std::max<int64_t>(tot_lines, 1) * 16;
+  auto own = [&](int k, size_t bytes, void** p) -> int {
+    GM_HIP(hipMalloc(p, std::max<size_t>(bytes, 16)));
+    ix->allocs.push_back(*p);
+    ix->arr[k] = *p;
+    ix->arr_bytes[k] = (int64_t)bytes;
+    return GM_OK;
+  };
+  rc = own(7, (size_t)blob_words * 8, &d_blob);
+  if (!rc) rc = own(5, (size_t)cmp_words * 8, &d_cmp);
+  if (!rc) rc = own(3, (size_t)ncell * 4, &d_cw);
+  if (rc) { cleanup(); return rc; }
+  GM_HIP(hipMemsetAsync(d_blob, 0, (size_t)blob_words * 8, s));
+  GM_HIP(hipMemsetAsync(d_cmp, 0, (size_t)cmp_words * 8, s));
+  void *d_ew, *d_ec;
+  rc = dalloc((size_t)nslot * 4, &d_ew);
+  if (!rc) rc = dalloc((size_t)nslot * 4, &d_ec);
+  if (rc) { cleanup(); return rc; }
+  a.write = 1;
+  a.gen_off = (const int64_t*)d_goff; a.cmp_off = (const int64_t*)d_coff;
+  a.ent_word = (uint32_t*)d_ew; a.ent_cell = (int32_t*)d_ec;
+  a.blob = (double*)d_blob; a.compact = (double*)d_cmp;
+  hipLaunchKernelGGL(k_build_rows, dim3((unsigned)ntask), dim3(BT_TPB), 0, s, a);
+  GM_CHECK_LAUNCH();
+  // entries per cell -> buckets -> cell words and lists
+  void *d_pc, *d_bc, *d_cs, *d_fill, *d_sp, *d_ll, *d_lo, *d_max;
+  rc = dalloc((size_t)ncell * 4, &d_pc);
+  if (!rc) rc = dalloc((size_t)ncell * 4, &d_bc);
+  if (!rc) rc = dalloc((size_t)(ncell + 1) * 8, &d_cs);
+  if (!rc) rc = dalloc((size_t)ncell * 4, &d_fill);
+  if (!rc) rc = dalloc((size_t)nslot * 4, &d_sp);
+  if (!rc) rc = dalloc((size_t)ncell * 4, &d_ll);
+  if (!rc) rc = dalloc((size_t)(ncell + 1) * 8, &d_lo);
+  if (!rc) rc = dalloc(16, &d_max);
+  if (rc) { cleanup(); return rc; }
+  GM_HIP(hipMemsetAsync(d_pc, 0, (size_t)ncell * 4, s));
+  GM_HIP(hipMemsetAsync(d_bc, 0, (size_t)ncell * 4, s));
+  GM_HIP(hipMemsetAsync(d_fill, 0, (size_t)ncell * 4, s));
+  GM_HIP(hipMemsetAsync(d_max, 0, 16, s));
+  const unsigned g1 = (unsigned)std::min<int64_t>(65536, (std::max(nslot, ncell) + 255) / 256);
+  hipLaunchKernelGGL(k_build_cell_count, dim3(g1), dim3(256), 0, s, (const uint32_t*)d_ew, (const int32_t*)d_ec, nslot,
+                     (int32_t*)d_pc, (int32_t*)d_bc);
+  launch_excl_scan(s, (const int32_t*)d_pc, ncell, (int64_t*)d_cs, (int64_t*)d_part, (int64_t*)d_cs + ncell);
+  hipLaunchKernelGGL(k_build_slot_poly, dim3((unsigned)ntask), dim3(256), 0, s, (const int32_t*)d_tp,
+                     (const int64_t*)d_ts, (int)ntask, (int32_t*)d_sp);
+  GM_CHECK_LAUNCH();
+  int64_t n_ent = 0;
+  rc = copy_d2h(ctx, &n_ent, (int64_t*)d_cs + ncell, 8);
+  if (rc) { cleanup(); return rc; }
+  void* d_bucket;
+  rc = dalloc((size_t)std::max<int64_t>(n_ent, 1) * 8, &d_bucket);
+  if (rc) { cleanup(); return rc; }
+  hipLaunchKernelGGL(k_build_cell_scatter, dim3(g1), dim3(256), 0, s, (const uint32_t*)d_ew, (const int32_t*)d_ec, nslot,
+                     (const int64_t*)d_cs, (int32_t*)d_fill, (uint32_t*)d_bucket, (const int32_t*)d_sp);
+  hipLaunchKernelGGL(k_build_list_len, dim3(g1), dim3(256), 0, s, (const int32_t*)d_pc, ncell, (int32_t*)d_ll);
+  launch_excl_scan(s, (const int32_t*)d_ll, ncell, (int64_t*)d_lo, (int64_t*)d_part, (int64_t*)d_lo + ncell);
+  GM_CHECK_LAUNCH();
+  int64_t n_list = 0;
+  rc = copy_d2h(ctx, &n_list, (int64_t*)d_lo + ncell, 8);
+  if (rc) { cleanup(); return rc; }
+  if (n_list / 4 + 1 >= ((int64_t)1 << 26)) {
+    cleanup();
+    gm::set_error("gm_pip_index_create: cell lists too large");
+    return GM_E_CAPACITY;
+  }
+  const int64_t list_slots = std::max<int64_t>(n_list, 4);
+  rc = own(6, (size_t)list_slots * 4, &d_list);
+  if (rc) { cleanup(); return rc; }
+  GM_HIP(hipMemsetAsync(d_list, 0, (size_t)list_slots * 4, s));
+  hipLaunchKernelGGL(k_build_cells, dim3(g1), dim3(256), 0, s, (const int32_t*)d_pc, (const int64_t*)d_cs,
+                     (uint32_t*)d_bucket, (const int64_t*)d_lo, ncell, (uint32_t*)d_cw, (uint32_t*)d_list);
+  GM_CHECK_LAUNCH();
+  const int gxc = (gx + (1 << CF_LOG) - 1) >> CF_LOG, gyc = (gy + (1 << CF_LOG) - 1) >> CF_LOG;
+  rc = own(4, (size_t)gxc * gyc * 4, &d_coarse);
+  if (rc) { cleanup(); return rc; }
+  hipLaunchKernelGGL(k_build_coarse, dim3((unsigned)std::min<int64_t>(65536, ((int64_t)gxc * gyc + 255) / 256)),
+                     dim3(256), 0, s, (const uint32_t*)d_cw, gx, gy, gxc, gyc, (uint32_t*)d_coarse);
+  hipLaunchKernelGGL(k_build_max, dim3(g1), dim3(256), 0, s, (const int32_t*)d_pc, ncell, (int*)d_max);
+  hipLaunchKernelGGL(k_build_max, dim3(g1), dim3(256), 0, s, (const int32_t*)d_bc, ncell, (int*)d_max + 1);
+  GM_CHECK_LAUNCH();
+  int mx[2] = {0, 0};
+  rc = copy_d2h(ctx, mx, d_max, 8);
+  cleanup();
+  if (rc) return rc;
+  ix->dev.cell_word = (const uint32_t*)d_cw;
+  ix->dev.coarse_word = (const uint32_t*)d_coarse;
+  ix->dev.compact = (const double*)d_cmp;
+  ix->dev.list_ent = (const uint32_t*)d_list;
+  ix->dev.blob = (const double*)d_blob;
+  ix->dev.gxc = gxc;
+  ix->max_ent_per_cell = mx[0];
+  ix->max_bnd_per_cell = mx[1];
+  ix->n_entries = n_ent;
+  ix->n_slow = (int64_t)st[0];
+  ix->n_records = (int64_t)st[1];
+  ix->n_boundary = (int64_t)st[2];
+  ix->n_compact = (int64_t)st[3];
+  ix->blob_bytes = (std::max<int64_t>(tot_words, 1) + tot_lines * 16) * 8;   // the host build pads an empty blob array to one word
+  return GM_OK;
 }
 
 }  // namespace
@@ -1371,36 +2051,67 @@ int gm_pip_index_create_ex(gm_ctx* ctx, const gm_polyset* ps, int cells_per_poly
   std::vector<RingDev> rings((size_t)n_rings);
   std::vector<int32_t> slab_off;
   std::vector<Edge> slab_edges, segs((size_t)std::max(n_verts, 1));  // segs: segment ending at vertex i
-  for (int r = 0; r < n_rings; ++r) {
-    const int v0 = ps->ring_vert_off[r], v1 = ps->ring_vert_off[r + 1];
-    RingDev& rd = rings[r];
-    rd.minx = rd.miny = INFINITY;
-    rd.maxx = rd.maxy = -INFINITY;
-    for (int v = v0; v < v1; ++v) {
-      rd.minx = std::min(rd.minx, vx[v]); rd.maxx = std::max(rd.maxx, vx[v]);
-      rd.miny = std::min(rd.miny, vy[v]); rd.maxy = std::max(rd.maxy, vy[v]);
+  // per ring: envelope and slab count (parallel over rings), then flat counting-sort of the
+  // segments into their slabs (two passes over each ring, no per-slab vectors)
+  std::vector<int64_t> ring_slab_base((size_t)n_rings + 1, 0), ring_edge_base((size_t)n_rings + 1, 0);
+  {
+    auto ring_env = [&](int r) {
+      const int v0 = ps->ring_vert_off[r], v1 = ps->ring_vert_off[r + 1];
+      RingDev& rd = rings[r];
+      rd.minx = rd.miny = INFINITY;
+      rd.maxx = rd.maxy = -INFINITY;
+      for (int v = v0; v < v1; ++v) {
+        rd.minx = std::min(rd.minx, vx[v]); rd.maxx = std::max(rd.maxx, vx[v]);
+        rd.miny = std::min(rd.miny, vy[v]); rd.maxy = std::max(rd.maxy, vy[v]);
+      }
+      for (int i = v0 + 1; i < v1; ++i) segs[i] = Edge{vx[i], vy[i], vx[i - 1], vy[i - 1]};
+      const int nseg = std::max(0, v1 - v0 - 1);
+      int ns = std::max(1, std::min(4096, nseg / 2));
+      const double hgt = rd.maxy - rd.miny;
+      if (!(hgt > 0.0) || nseg == 0) ns = 1;
+      rd.y0 = nseg ? rd.miny : 0.0;
+      rd.inv_h = (ns > 1) ? (double)ns / hgt : 0.0;
+      rd.ns = ns;
+      int64_t ne = 0;   // (segment, slab) pairs of the ring
+      for (int i = v0 + 1; i < v1; ++i) {
+        const int s0 = host::cell_of(std::min(vy[i], vy[i - 1]), rd.y0, rd.inv_h, ns);
+        const int s1 = host::cell_of(std::max(vy[i], vy[i - 1]), rd.y0, rd.inv_h, ns);
+        ne += s1 - s0 + 1;
+      }
+      ring_edge_base[r + 1] = ne;
+      ring_slab_base[r + 1] = ns;
+    };
+    parallel_for(n_rings, ring_env);
+    for (int r = 0; r < n_rings; ++r) {
+      ring_slab_base[r + 1] += ring_slab_base[r];
+      ring_edge_base[r + 1] += ring_edge_base[r];
+      rings[r].slab_base = (int32_t)ring_slab_base[r];
     }
-    for (int i = v0 + 1; i < v1; ++i) segs[i] = Edge{vx[i], vy[i], vx[i - 1], vy[i - 1]};
-    const int nseg = std::max(0, v1 - v0 - 1);
-    int ns = std::max(1, std::min(4096, nseg / 2));
-    const double hgt = rd.maxy - rd.miny;
-    if (!(hgt > 0.0) || nseg == 0) ns = 1;
-    rd.y0 = nseg ? rd.miny : 0.0;
-    rd.inv_h = (ns > 1) ? (double)ns / hgt : 0.0;
-    rd.ns = ns;
-    rd.slab_base = (int32_t)slab_off.size();
-    std::vector<std::vector<int32_t>> buckets((size_t)ns);
-    for (int i = v0 + 1; i < v1; ++i) {
-      const int s0 = host::cell_of(std::min(vy[i], vy[i - 1]), rd.y0, rd.inv_h, ns);
-      const int s1 = host::cell_of(std::max(vy[i], vy[i - 1]), rd.y0, rd.inv_h, ns);
-      for (int k = s0; k <= s1; ++k) buckets[k].push_back(i);
-    }
-    for (int k = 0; k < ns; ++k) {
-      slab_off.push_back((int32_t)slab_edges.size());
-      for (int32_t i : buckets[k]) slab_edges.push_back(segs[i]);
-    }
+    slab_off.assign((size_t)ring_slab_base[n_rings] + 1, 0);
+    slab_edges.resize((size_t)ring_edge_base[n_rings]);
+    auto ring_fill = [&](int r) {
+      const int v0 = ps->ring_vert_off[r], v1 = ps->ring_vert_off[r + 1];
+      const RingDev& rd = rings[r];
+      const int ns = rd.ns;
+      int32_t* so = slab_off.data() + ring_slab_base[r];
+      std::vector<int32_t> cnt((size_t)ns + 1, 0);
+      for (int i = v0 + 1; i < v1; ++i) {
+        const int s0 = host::cell_of(std::min(vy[i], vy[i - 1]), rd.y0, rd.inv_h, ns);
+        const int s1 = host::cell_of(std::max(vy[i], vy[i - 1]), rd.y0, rd.inv_h, ns);
+        for (int k = s0; k <= s1; ++k) cnt[k + 1]++;
+      }
+      for (int k = 0; k < ns; ++k) cnt[k + 1] += cnt[k];
+      for (int k = 0; k < ns; ++k) so[k] = (int32_t)(ring_edge_base[r] + cnt[k]);
+      Edge* out = slab_edges.data() + ring_edge_base[r];
+      for (int i = v0 + 1; i < v1; ++i) {   // segments in vertex order within each slab
+        const int s0 = host::cell_of(std::min(vy[i], vy[i - 1]), rd.y0, rd.inv_h, ns);
+        const int s1 = host::cell_of(std::max(vy[i], vy[i - 1]), rd.y0, rd.inv_h, ns);
+        for (int k = s0; k <= s1; ++k) out[cnt[k]++] = segs[i];
+      }
+    };
+    parallel_for(n_rings, ring_fill);
+    slab_off[(size_t)ring_slab_base[n_rings]] = (int32_t)slab_edges.size();
   }
-  slab_off.push_back((int32_t)slab_edges.size());
 
   // ---- polygon envelopes (JTS: Polygon envelope = shell envelope; MultiPolygon = union)
   std::vector<double> env((size_t)std::max(P, 1) * 4);
@@ -1436,6 +2147,41 @@ int gm_pip_index_create_ex(gm_ctx* ctx, const gm_polyset* ps, int cells_per_poly
   const double inv_cw = degenerate ? 0.0 : (double)gx / W, inv_ch = degenerate ? 0.0 : (double)gy / H;
   const double epsx = W > 0 ? W * 1e-9 : 1e-9, epsy = H > 0 ? H * 1e-9 : 1e-9;
   const int64_t ncell = (int64_t)gx * gy;
+
+  // ---- device build (default): cell words, lists and blobs built on the GPU from the polygon CSR
+  if (!degenerate && any && ctx->index_build == 0) {
+    gm_pip_index* ix = new gm_pip_index();
+    ix->ctx = ctx;
+    int rc = GM_OK;
+    GM_HIP(hipSetDevice(ctx->device));
+    rc = upload(ix, 0, rings, &ix->dev.rings);
+    if (!rc) rc = upload(ix, 1, slab_off, &ix->dev.slab_off);
+    if (!rc) rc = upload(ix, 2, slab_edges, &ix->dev.slab_edges);
+    const double t_prep = now_s();
+    if (!rc) rc = build_cells_device(ctx, ix, ps, env, G, inv_cw, inv_ch, epsx, epsy, gx, gy, ix->dev.rings);
+    if (rc == 1) {
+      gm_pip_index_destroy(ix);   // not handled on the device: the host classification below
+    } else if (rc) {
+      gm_pip_index_destroy(ix);
+      return rc;
+    } else {
+      ix->n_polys = P;
+      ix->n_cells = ncell;
+      ix->dev.gx0 = G[0]; ix->dev.gy0 = G[1]; ix->dev.gx1 = G[2]; ix->dev.gy1 = G[3];
+      ix->dev.inv_cw = inv_cw; ix->dev.inv_ch = inv_ch;
+      ix->dev.gx = gx; ix->dev.gy = gy;
+      rc = make_list_poly(ix);
+      if (rc) { gm_pip_index_destroy(ix); return rc; }
+      if (getenv("GM_PIP_DEBUG")) {
+        GM_HIP(hipStreamSynchronize(ctx->stream));
+        fprintf(stderr, "[gm_pip] device build: rings + slabs %.3f s, cells %.3f s; %lld cells, %lld entries, "
+                "%lld blob bytes\n", t_prep - t_start, now_s() - t_prep, (long long)ncell, (long long)ix->n_entries,
+                (long long)ix->blob_bytes);
+      }
+      *out = ix;
+      return GM_OK;
+    }
+  }
 
   // ---- (cell, polygon) classification + boundary blobs, in parallel over chunks of polygons.  A
   // chunk's entries carry chunk-local blob / compact offsets; the chunks are concatenated in polygon

@@ -28,22 +28,22 @@ _ALL64 = -1  # 0xFFFF... as int64
 def key_ranges(scan_ranges, shards=None):
     """getRangeBytes (Z3IndexKeySpace.scala:196-238) as gm_key_range rows (numpy KEY_RANGE_DTYPE): one
     per scan range and shard.  scan_ranges are Z3IndexKeySpace.get_ranges tuples."""
-    out = []
-    for kind, lo, hi in scan_ranges:
+    k = len(scan_ranges)
+    zl, zh = np.zeros(k, np.int64), np.full(k, _ALL64, np.int64)
+    bl, bh = np.zeros(k, np.int16), np.full(k, -1, np.int16)
+    for i, (kind, lo, hi) in enumerate(scan_ranges):
         if kind == "bounded":
-            r = (lo[1], hi[1], lo[0], hi[0])
+            zl[i], zh[i], bl[i], bh[i] = lo[1], hi[1], lo[0], hi[0]
         elif kind == "lower":
-            r = (lo[1], _ALL64, lo[0], -1)
+            zl[i], bl[i] = lo[1], lo[0]
         elif kind == "upper":
-            r = (0, hi[1], 0, hi[0])
-        else:  # unbounded
-            r = (0, _ALL64, 0, -1)
-        for s in (range(shards) if shards else [0]):
-            out.append(r + (s,))
-    arr = np.zeros(len(out), _lib.KEY_RANGE_DTYPE)
-    for i, (zl, zh, bl, bh, s) in enumerate(out):
-        arr[i]["z_lo"], arr[i]["z_hi"], arr[i]["bin_lo"], arr[i]["bin_hi"], arr[i]["shard"] = zl, zh, bl, bh, s
-    return arr, len(out)
+            zh[i], bh[i] = hi[1], hi[0]
+    ns = shards if shards else 1
+    arr = np.zeros(k * ns, _lib.KEY_RANGE_DTYPE)   # range-major, then shard (getRangeBytes order)
+    arr["z_lo"], arr["z_hi"] = np.repeat(zl, ns), np.repeat(zh, ns)
+    arr["bin_lo"], arr["bin_hi"] = np.repeat(bl, ns), np.repeat(bh, ns)
+    arr["shard"] = np.tile(np.arange(ns, dtype=np.uint8), k)
+    return arr, len(arr)
 
 
 class Z3Table:

@@ -93,6 +93,8 @@ const char* gm_last_error(void);
 #define GM_PARAM_JOIN_CHUNK 1   /* points per pass of the join strategies (0 = defaults: direct 2^31,
                                    partitioned 2^28, split sized to its 6 GiB workspace); smaller
                                    values only add passes -- the pair set never changes */
+#define GM_PARAM_INDEX_BUILD 2  /* where gm_pip_index_create builds the join index: 0 (default) = on the
+                                   device (same arrays, byte for byte), 1 = on the host */
 int gm_ctx_set_param(gm_ctx* ctx, int param, int64_t value);
 int gm_ctx_get_param(gm_ctx* ctx, int param, int64_t* value);
 /* device memory helpers for callers without their own allocator (e.g. a JNI shim) */

@@ -1,4 +1,4 @@
-"""Times PolygonIndex construction (host build + upload) for the bench's 3,200 synthetic counties and
+"""Times PolygonIndex construction (device build, then the host build) for the bench's 3,200 synthetic counties and
 the US states, with GM_PIP_DEBUG phase timings on stderr.  Usage: python tools/index_build_probe.py"""
 import os
 import sys
@@ -14,13 +14,16 @@ from geomesa_amd.join import PolygonIndex, synthetic_counties  # noqa: E402
 
 ctx = _lib.context(0)
 ps = synthetic_counties(80, 40)
-for cpp in (8192, 0):
-    for rep in range(2):
+for mode in (0, 1):   # GM_PARAM_INDEX_BUILD: device, host
+    ctx.set_param(_lib.GM_PARAM_INDEX_BUILD, mode)
+    for rep in range(3):
         t0 = time.time()
-        ix = PolygonIndex(ps, ctx, cpp)
+        ix = PolygonIndex(ps, ctx, 0)
         torch.cuda.synchronize()
-        print("counties cells_per_poly=%d: %.3f s  %s" % (cpp, time.time() - t0, ix.stats()), flush=True)
+        print("counties %s build: %.3f s  %s" % ("device" if mode == 0 else "host", time.time() - t0, ix.stats()),
+              flush=True)
         del ix
+ctx.set_param(_lib.GM_PARAM_INDEX_BUILD, 0)
 from shapefile import us_states  # noqa: E402
 st, _ = us_states()
 t0 = time.time()
