@@ -131,7 +131,10 @@ __global__ __launch_bounds__(HT) void k_sort_hist(const uint8_t* __restrict__ sh
 // into wave ranks, a scan over the waves into block ranks, so a row's place in the tile is (digit,
 // wave, slot, lane, even/odd) = stable.  The tile is reordered in LDS and leaves as digit runs at
 // the block's cursor for each digit (runs average 32 rows for uniform digits: 256-B z segments).
-constexpr int BT = 1024;            // scatter threads per block
+#ifndef GM_SORT_BT
+#define GM_SORT_BT 1024
+#endif
+constexpr int BT = GM_SORT_BT;      // scatter threads per block
 constexpr int BW = BT / 64;         // waves
 constexpr int BSLOT = 4;            // slots of 2 rows per lane
 constexpr int BTILE = BT * 2 * BSLOT;   // 8192 rows per tile
@@ -154,7 +157,6 @@ __global__ __launch_bounds__(BT) void k_sort_scatter(const uint8_t* __restrict__
   __shared__ uint32_t s_perm[BTILE];
   __shared__ uint16_t s_bin[BTILE];
   __shared__ uint8_t s_sh[BTILE];
-  __shared__ uint8_t s_dg[BTILE];
   __shared__ uint16_t s_wcnt[BW][256];      // per wave: rows of each digit so far (then: wave offsets)
   __shared__ uint32_t s_gcur[256], s_tot[256], s_dstart[256], s_wsum[4];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -255,16 +257,16 @@ __global__ __launch_bounds__(BT) void k_sort_scatter(const uint8_t* __restrict__
         const uint32_t r = rd[k][e] & 0xffffu, d = rd[k][e] >> 16;
         if (r == 0xffffu) continue;
         const uint32_t pos = s_dstart[d] + s_wcnt[wave][d] + r;
-        s_z[pos] = zv[k][e]; s_bin[pos] = (uint16_t)bs[k][e]; s_sh[pos] = (uint8_t)(bs[k][e] >> 16);
+        s_z[pos] = zv[k][e]; s_bin[pos] = (uint16_t)bs[k][e];
+        if (sh_in) s_sh[pos] = (uint8_t)(bs[k][e] >> 16);
         s_perm[pos] = pv[k][e];
-        s_dg[pos] = (uint8_t)d;
       }
     }
     __syncthreads();
     if (t0 + BTILE < b1) load(t0 + BTILE);
     const int cnt = (int)min((int64_t)BTILE, b1 - t0);
     for (int q = t; q < cnt; q += BT) {
-      const uint32_t d = s_dg[q];
+      const uint32_t d = key_digit(sh_in ? s_sh[q] : (uint8_t)0, s_bin[q], s_z[q], pass);
       const int64_t g = (int64_t)s_gcur[d] + (q - (int)s_dstart[d]);
       z_out[g] = s_z[q];
       bin_out[g] = s_bin[q];
