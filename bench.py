@@ -59,12 +59,21 @@ class Dist:
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        # rehearsal knobs (never used by the driver's runs): GM_BENCH_DEVICE puts every rank on one GPU,
+        # GM_BENCH_BACKEND=gloo runs the collectives through host memory, so the N > 1 paths can be
+        # exercised on a one-GPU box
+        if os.environ.get("GM_BENCH_DEVICE"):
+            self.local = int(os.environ["GM_BENCH_DEVICE"])
+        backend = os.environ.get("GM_BENCH_BACKEND", "nccl")
         torch.cuda.set_device(self.local)
         self.pg = None
         if self.world > 1:
             import torch.distributed as dist
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            dist.init_process_group("nccl", device_id=torch.device("cuda", self.local))
+            if backend == "nccl":
+                dist.init_process_group("nccl", device_id=torch.device("cuda", self.local))
+            else:
+                dist.init_process_group(backend)
             self.pg = dist
 
     def barrier(self):
@@ -137,14 +146,16 @@ def cpu_threads():
     return max(1, min(16, os.cpu_count() or 1))
 
 
-def cpu_z3_baseline(seconds):
+def cpu_z3_baseline(seconds, sample):
+    """The oracle on the host cores, over a strided sample of the GPU run's own points; the sample's
+    keys are also compared with what the GPU wrote for them (full-size parity, strided)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     nt = cpu_threads()
-    per = 4_000_000
-    rng = np.random.default_rng(7)
-    x = rng.uniform(-180, 180, per); y = rng.uniform(-90, 90, per); t = rng.integers(T2020, T2021, per)
-    O.z3_index_key_batch(x[:8], y[:8], t[:8])
+    x, y, t, gb, gz, stride = sample
+    per = len(x)
+    ob, oz, ost = O.z3_index_key_batch(x, y, t)
+    bad = int(((ob != gb) | (oz != gz) | (ost != 0)).sum())
     done = [0] * nt
     stop = time.time() + seconds
 
@@ -160,16 +171,31 @@ def cpu_z3_baseline(seconds):
         h.join()
     dt = time.time() - t0
     return {"value": sum(done) / dt, "unit": "points/s", "cores": nt, "kind": "port",
-            "sample": "%d threads x repeated 4M-point batches of the C restatement (oracle/gm_oracle.c "
-                      "gmo_z3_index_key_batch, week) for %.1f s: %d points" % (nt, dt, sum(done))}
+            "sample": "%d threads x repeated batches of the C restatement (oracle/gm_oracle.c gmo_z3_index_key_batch, "
+                      "week) over every %d-th point of the GPU run (%d points) for %.1f s: %d points"
+                      % (nt, stride, per, dt, sum(done)),
+            "parity_sample": {"points": per, "stride": stride, "mismatches": bad,
+                              "note": "bin / z of the strided sample of the 1B-point GPU run against the oracle"}}
 
 
-def cpu_join_baseline(seconds, ps):
+def cpu_join_baseline(seconds, ps, sample=None):
+    """The oracle's join on the host cores; with `sample` (every stride-th point of the GPU run and the
+    GPU's pairs for those points) it also reports full-size parity of the strided sample."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     from geomesa_amd.join import synthetic_points
     nt = cpu_threads()
     op = O.OraclePolySet(*ps.to_arrays())
+    parity = None
+    if sample is not None:
+        sx, sy, stride, gpu_pairs = sample
+        opt, opl = op.join(sx, sy, nthreads=nt)
+        exp = np.stack([opt.astype(np.int64), opl.astype(np.int64)], 1)
+        exp = exp[np.lexsort((exp[:, 1], exp[:, 0]))]
+        got = gpu_pairs[np.lexsort((gpu_pairs[:, 1], gpu_pairs[:, 0]))]
+        parity = {"points": len(sx), "stride": stride, "pairs": len(exp), "gpu_pairs": len(got),
+                  "equal": bool(len(exp) == len(got) and np.array_equal(exp, got)),
+                  "note": "(point, polygon) pairs of every stride-th point of the 1B-point GPU join against the oracle"}
     n = 200_000
     px, py = synthetic_points(n, seed=SEED + 5)
     t0 = time.time()
@@ -182,9 +208,12 @@ def cpu_join_baseline(seconds, ps):
     t0 = time.time()
     pt, _ = op.join(px, py, nthreads=nt)
     dt = time.time() - t0
-    return {"value": n * ps.n_polys / dt, "unit": "pairs/s", "cores": nt, "kind": "port",
-            "sample": "%d CONUS points x %d polygons, C restatement (grid candidates + JTS contains per "
-                      "pair, %d pthreads): %.2f s, %d matches" % (n, ps.n_polys, nt, dt, len(pt))}
+    out = {"value": n * ps.n_polys / dt, "unit": "pairs/s", "cores": nt, "kind": "port",
+           "sample": "%d CONUS points x %d polygons, C restatement (grid candidates + JTS contains per "
+                     "pair, %d pthreads): %.2f s, %d matches" % (n, ps.n_polys, nt, dt, len(pt))}
+    if parity is not None:
+        out["parity_sample"] = parity
+    return out
 
 
 def cpu_ranges_baseline(kind, q, t, max_ranges, gpu_ms, nq):
@@ -403,7 +432,8 @@ def all_gather_ints(dist, v):
     if dist.pg is None:
         return [v]
     import torch
-    t = torch.tensor([int(v)], dtype=torch.int64, device="cuda")
+    from geomesa_amd.shard import _device_of
+    t = torch.tensor([int(v)], dtype=torch.int64, device=_device_of(dist.pg))
     parts = [torch.zeros_like(t) for _ in range(dist.world)]
     dist.pg.all_gather(parts, t)
     return [int(p.item()) for p in parts]
@@ -464,6 +494,9 @@ def main():
         _lib.check(lib.gm_z3_index_key(h, P(x), P(y), P(t), N, 1, 0, P(b), P(z), None, __import__("ctypes").byref(st)),
                    "z3")
         assert st.n_errors == 0
+        if dist.rank == 0 and not a.no_cpu:   # strided sample of this run for the CPU leg
+            stride = max(1, N // 4_000_000)
+            z3_sample = tuple(v[::stride].cpu().numpy() for v in (x, y, t, b, z)) + (stride,)
         total = N * dist.world
         out.update({"value": total / (ms * 1e-3), "ms_per_step": ms})
         out["roofline"] = roofline(34.0 * N, ms, load_pmc("z3_index_key", N))
@@ -708,17 +741,25 @@ def main():
                                            "polygon_i = the county of the point's grid cell (21 B/row: 16 point + 4 id + 1 out)"}
         del rid, loc
 
+        join_sample = None
+        if dist.rank == 0 and not a.no_cpu:   # every stride-th point of this run and the GPU's pairs for them
+            stride = max(1, J // 2_000_000)
+            npv = int(npairs.value)
+            sel = ((ptids[:npv] - jlo) % stride) == 0
+            join_sample = (px[::stride].cpu().numpy(), py[::stride].cpu().numpy(), stride,
+                           torch.stack([(ptids[:npv][sel] - jlo) // stride, plids[:npv][sel].to(torch.int64)], 1).cpu().numpy())
+            del sel
         del px, py
         torch.cuda.empty_cache()
         if not a.no_gather:
             pj["gather"] = gather_pairs(dist, ptids, plids, int(npairs.value))
         if dist.rank == 0 and not a.no_cpu:
-            pj["cpu_baseline"] = cpu_join_baseline(a.cpu_seconds, ps)
+            pj["cpu_baseline"] = cpu_join_baseline(a.cpu_seconds, ps, join_sample)
         out["pip_join"] = pj
         del ptids, plids, ix
 
     if dist.rank == 0 and not a.no_cpu and "z3" in only:
-        out["cpu_baseline"] = cpu_z3_baseline(a.cpu_seconds)
+        out["cpu_baseline"] = cpu_z3_baseline(a.cpu_seconds, z3_sample)
     if extra:
         out["extra"] = extra
     if dist.rank == 0:
