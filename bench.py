@@ -688,9 +688,13 @@ def main():
                                       __import__("ctypes").byref(npairs), jmode), "join")
         matches = int(dist.sum(npairs.value))
         pairs = J * n_polys * dist.world
-        pj = {"value": pairs / (jms * 1e-3), "unit": "pairs/s", "ms_per_step": jms, "points_per_gpu": J,
+        pj = {"value": pairs / (jms * 1e-3), "unit": "pairs/s",
+              "points_per_s": J * dist.world / (jms * 1e-3), "matches_per_s": matches / (jms * 1e-3),
+              "value_note": "value = logical (point, polygon) pairs resolved per second, N_points x N_polygons / t "
+                            "(SURVEY 8(d)); the work-based rates are points_per_s and matches_per_s",
+              "ms_per_step": jms, "points_per_gpu": J,
               "polygons": n_polys, "vertices": n_verts, "matches": matches,
-              "matches_per_s": matches / (jms * 1e-3), "index_build_s": round(t_build, 3), "index_ready_s": round(t_ix, 3), "index": ix.stats(), "mode": a.join_mode,
+              "index_build_s": round(t_build, 3), "index_ready_s": round(t_ix, 3), "index": ix.stats(), "mode": a.join_mode,
               "roofline": roofline(16.0 * J + 12.0 * npairs.value, jms, load_pmc("pip_join", J)),
               "workload": "st_contains(polygon, point) join, %d CONUS points/GPU x %d synthetic county polygons "
                           "(BASELINE configs[3]); index built on rank 0, broadcast over RCCL when N > 1"
