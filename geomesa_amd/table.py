@@ -141,6 +141,14 @@ class PartitionedZ3Table:
         self.pg = pg
         local = Z3Table(bins, z, shard, period)
         sharded = shard is not None
+        if pg is None or pg.get_world_size() == 1:   # one slice: the local table is the table
+            self.table, self.splitters = local, (np.zeros(0, np.int64), np.zeros(0, np.int64))
+            if sharded and shards:
+                self.table.shards = int(shards)
+            self.gid = torch.as_tensor(ids).to(local.z.device, torch.int64)[local.perm]
+            self.n = local.n
+            self._bounds()
+            return
         hi, lo = S.table_key(local.shard, local.bin, local.z)
         gid = torch.as_tensor(ids).to(local.z.device, torch.int64)[local.perm]
         del local
@@ -153,6 +161,12 @@ class PartitionedZ3Table:
                 int(S.all_reduce_scalar(pg, float(self.table.shards or 0), "max")))
         self.gid = gid[self.table.perm]   # global row id of each table row
         self.n = self.table.n
+        self._bounds()
+
+    def _bounds(self):
+        """The slice's first and last key (the clipping bounds)."""
+        import torch
+        from . import shard as S
         if self.n:
             t = self.table
             ends = torch.tensor([0, self.n - 1], device=t.z.device)

@@ -158,3 +158,17 @@ def test_partitioned_table_equals_global_scan(gpu, sharded):
         exp = np.sort(ids.cpu().numpy())
         assert len(exp) > 0 or k == 3
         assert np.array_equal(full[1 + k], exp), k
+
+
+def test_partitioned_table_single_slice(gpu):
+    """pg None: one slice, no exchange; the query ids equal the plain table's."""
+    from geomesa_amd.keyspace import during
+    from geomesa_amd.table import PartitionedZ3Table, Z3Table
+    x, y, t, sh = _table_points(200_001, seed=9)
+    ids = np.arange(len(x)) + 1000
+    pt = PartitionedZ3Table.from_points(None, x, y, t, ids, shard=sh, shards=4)
+    tb = Z3Table.from_points(x, y, t, shard=sh)
+    for bxs, ts in TABLE_QUERIES:
+        got, nm, ns, nr = pt.query(bxs, [during(a, b) for a, b in ts])
+        exp, _, _ = tb.query(bxs, [during(a, b) for a, b in ts])
+        assert np.array_equal(np.sort(got.cpu().numpy()), np.sort(exp.cpu().numpy()) + 1000)
