@@ -1796,6 +1796,9 @@ int build_cells_device(gm_ctx* ctx, gm_pip_index* ix, const gm_polyset* ps, cons
   }
   const int64_t ntask = (int64_t)task_poly.size(), nslot = task_slot.back();
   if (ntask == 0 || ntask > INT32_MAX) return 1;
+  // very large rings spanning many rows would need a huge global band scratch (a slice of the
+  // polygon's edge count per row task): those sets are left to the host build
+  if (band_total > ((int64_t)1 << 27)) return 1;
   const int64_t ncell = (int64_t)gx * gy;
   std::vector<void*> tmp;
   auto dalloc = [&](size_t bytes, void** p) -> int {
