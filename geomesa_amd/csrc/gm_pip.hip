@@ -658,26 +658,66 @@ constexpr int NBAND = 256;          // max bands (band id fits LDS histograms of
 constexpr int PTPB = 256;           // partition block
 constexpr int PTILE = 2048;         // scatter tile: 8 points per thread, sorted by band in LDS
 
-__device__ __forceinline__ int band_of(double y, const PipDev& d, int rows_per_band, int nb) {
-  if (!(y >= d.gy0 && y <= d.gy1)) return nb;   // drop bin
+// Coarse triage (the partition pass resolves what the coarse table already decides): a point
+// outside the grid or in an EMPTY coarse cell is dropped (band nb), a point in an INTERIOR coarse
+// cell is a final pair with the cell's polygon (band nb, *w = the coarse word), and only points in
+// mixed (LIST) coarse cells become records of their row band for the join pass.
+__device__ __forceinline__ int triage_band(double x, double y, uint32_t w, const PipDev& d, int rows_per_band, int nb) {
+  if ((w >> 30) != CELL_LIST) return nb;
   return cell_of(y, d.gy0, d.inv_ch, d.gy) / rows_per_band;
 }
 
-// per-block band histogram, band-major: hist[band * gridDim.x + block]
-__global__ __launch_bounds__(PTPB) void k_band_hist(const double* __restrict__ py, int64_t n, int64_t per_block,
-                                                    PipDev d, int rows_per_band, int nb, uint32_t* __restrict__ hist) {
-  __shared__ uint32_t h[NBAND + 1];
-  for (int b = threadIdx.x; b <= nb; b += PTPB) h[b] = 0;
-  __syncthreads();
-  const int64_t b0 = (int64_t)blockIdx.x * per_block, b1 = min(n, b0 + per_block);
-  for (int64_t j = b0 + threadIdx.x; j < b1; j += PTPB)
-    atomicAdd(&h[band_of(__builtin_nontemporal_load(&py[j]), d, rows_per_band, nb)], 1u);
-  __syncthreads();
-  for (int b = threadIdx.x; b < nb; b += PTPB) hist[(int64_t)b * gridDim.x + blockIdx.x] = h[b];
+// the coarse word of a point (EMPTY outside the grid / NaN)
+__device__ __forceinline__ uint32_t coarse_of(double x, double y, const PipDev& d) {
+  if (!(x >= d.gx0 && x <= d.gx1 && y >= d.gy0 && y <= d.gy1)) return CELL_EMPTY << 30;
+  const int cx = cell_of(x, d.gx0, d.inv_cw, d.gx), cy = cell_of(y, d.gy0, d.inv_ch, d.gy);
+  return d.coarse_word[(int64_t)(cy >> CF_LOG) * d.gxc + (cx >> CF_LOG)];
 }
 
-// in-place exclusive scan of hist[0, len) by one 1024-thread block; hist[len] = total kept points
-__global__ __launch_bounds__(1024) void k_band_scan(uint32_t* __restrict__ hist, int64_t len) {
+// per-block band histogram of the triaged points, band-major: hist[band * gridDim.x + block], and
+// the block's count of coarse-INTERIOR pairs: pcount[block]
+__global__ __launch_bounds__(PTPB) void k_band_hist(const double* __restrict__ px, const double* __restrict__ py,
+                                                    int64_t n, int64_t per_block, PipDev d, int rows_per_band, int nb,
+                                                    uint32_t* __restrict__ hist, uint32_t* __restrict__ pcount) {
+  constexpr int U = PTILE / PTPB;
+  __shared__ uint32_t h[NBAND + 1];
+  __shared__ uint32_t s_pairs;
+  for (int b = threadIdx.x; b <= nb; b += PTPB) h[b] = 0;
+  if (threadIdx.x == 0) s_pairs = 0;
+  __syncthreads();
+  uint32_t pairs = 0;
+  const int64_t b0 = (int64_t)blockIdx.x * per_block, b1 = min(n, b0 + per_block);
+  for (int64_t t0 = b0; t0 < b1; t0 += PTILE) {
+    double x[U], y[U];
+    uint32_t w[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const int64_t j = t0 + k * PTPB + threadIdx.x;
+      x[k] = y[k] = NAN;
+      if (j < b1) { x[k] = __builtin_nontemporal_load(&px[j]); y[k] = __builtin_nontemporal_load(&py[j]); }
+    }
+#pragma unroll
+    for (int k = 0; k < U; ++k) w[k] = coarse_of(x[k], y[k], d);
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const int b = triage_band(x[k], y[k], w[k], d, rows_per_band, nb);
+      if (b < nb) atomicAdd(&h[b], 1u);
+      pairs += (w[k] >> 30) == CELL_INTERIOR;
+    }
+  }
+  for (int off = 32; off > 0; off >>= 1) pairs += __shfl_down(pairs, off, 64);
+  if ((threadIdx.x & 63) == 0 && pairs) atomicAdd(&s_pairs, pairs);
+  __syncthreads();
+  for (int b = threadIdx.x; b < nb; b += PTPB) hist[(int64_t)b * gridDim.x + blockIdx.x] = h[b];
+  if (threadIdx.x == 0) pcount[blockIdx.x] = s_pairs;
+}
+
+// in-place exclusive scan of hist[0, len) by one 1024-thread block; hist[len] = total kept points.
+// The blocks' coarse-INTERIOR pair counts pcount[0, nblk) become their output slots after the pairs
+// already counted (*counter), and *counter moves past them (the join pass appends after).
+__global__ __launch_bounds__(1024) void k_band_scan(uint32_t* __restrict__ hist, int64_t len, uint32_t* __restrict__ pcount,
+                                                    int nblk, int64_t* __restrict__ poff,
+                                                    unsigned long long* __restrict__ counter) {
   __shared__ uint32_t part[1024];
   const int t = threadIdx.x;
   const int64_t per = (len + 1023) / 1024, a = t * per, b = min(len, a + per);
@@ -694,40 +734,72 @@ __global__ __launch_bounds__(1024) void k_band_scan(uint32_t* __restrict__ hist,
   uint32_t run = part[t] - s;
   for (int64_t k = a; k < b; ++k) { const uint32_t c = hist[k]; hist[k] = run; run += c; }
   if (t == 1023) hist[len] = part[1023];
+  __syncthreads();
+  if (t < 64) {   // nblk is small (one resident wave of partition blocks): one wave scans it
+    const unsigned long long base = *counter;
+    unsigned long long run2 = 0;
+    for (int c0 = 0; c0 < nblk; c0 += 64) {
+      const int j = c0 + t;
+      const unsigned long long v = j < nblk ? pcount[j] : 0ull;
+      unsigned long long inc = v;
+      for (int o = 1; o < 64; o <<= 1) { const unsigned long long u = __shfl_up(inc, o, 64); if (t >= o) inc += u; }
+      if (j < nblk) poff[j] = (int64_t)(base + run2 + inc - v);
+      run2 += __shfl(inc, 63, 64);
+    }
+    if (t == 0) *counter = base + run2;
+  }
 }
 
-// Scatter: tile of PTILE points -> LDS counting sort by band -> each band's run written as
-// consecutive 24-B records at the block's running cursor for that band.
+// Scatter: tile of PTILE points -> coarse triage -> coarse-INTERIOR pairs written at the block's
+// pair slots, LIST points counting-sorted by band in LDS -> each band's run written as consecutive
+// 24-B records at the block's running cursor for that band.
+template <bool WRITE>
 __global__ __launch_bounds__(PTPB) void k_band_scatter(const double* __restrict__ px, const double* __restrict__ py,
                                                        int64_t n, int64_t per_block, PipDev d, int rows_per_band,
                                                        int nb, const uint32_t* __restrict__ off,
-                                                       PtRec* __restrict__ rec) {
+                                                       PtRec* __restrict__ rec, const int64_t* __restrict__ poff,
+                                                       int64_t id_base, int64_t* __restrict__ pt_ids,
+                                                       int32_t* __restrict__ poly_ids, int64_t cap) {
   constexpr int PER_T = PTILE / PTPB;
   __shared__ uint32_t cnt[NBAND + 1], loff[NBAND + 2], gcur[NBAND];
   __shared__ double sx[PTILE], sy[PTILE];
   __shared__ uint32_t sid[PTILE];
   __shared__ uint16_t sband[PTILE];
+  __shared__ uint32_t s_np;
   const int t = threadIdx.x;
   for (int b = t; b <= nb; b += PTPB) cnt[b] = 0;
   for (int b = t; b < nb; b += PTPB) gcur[b] = off[(int64_t)b * gridDim.x + blockIdx.x];
+  if (t == 0) s_np = 0;
+  int64_t pbase = WRITE ? poff[blockIdx.x] : 0;
   __syncthreads();
   const int64_t b0 = (int64_t)blockIdx.x * per_block, b1 = min(n, b0 + per_block);
   for (int64_t t0 = b0; t0 < b1; t0 += PTILE) {
     double x[PER_T], y[PER_T];
     int band[PER_T];
-    uint32_t r[PER_T];
+    uint32_t r[PER_T], w[PER_T];
+#pragma unroll
+    for (int k = 0; k < PER_T; ++k) {
+      const int64_t j = t0 + k * PTPB + t;
+      x[k] = y[k] = NAN;
+      if (j < b1) { x[k] = __builtin_nontemporal_load(&px[j]); y[k] = __builtin_nontemporal_load(&py[j]); }
+    }
+#pragma unroll
+    for (int k = 0; k < PER_T; ++k) w[k] = coarse_of(x[k], y[k], d);
 #pragma unroll
     for (int k = 0; k < PER_T; ++k) {
       const int64_t j = t0 + k * PTPB + t;
       band[k] = -1;
       if (j < b1) {
-        x[k] = __builtin_nontemporal_load(&px[j]);
-        y[k] = __builtin_nontemporal_load(&py[j]);
-        band[k] = band_of(y[k], d, rows_per_band, nb);
+        band[k] = triage_band(x[k], y[k], w[k], d, rows_per_band, nb);
         r[k] = atomicAdd(&cnt[band[k]], 1u);
+        if (WRITE && (w[k] >> 30) == CELL_INTERIOR) {
+          const int64_t slot = pbase + atomicAdd(&s_np, 1u);
+          if (slot < cap) { pt_ids[slot] = id_base + j; poly_ids[slot] = (int32_t)(w[k] & 0x3fffffffu); }
+        }
       }
     }
     __syncthreads();
+    if (WRITE) pbase += s_np;
     if (t < 64) {   // exclusive scan of cnt[0..nb] by one wave
       constexpr int PER_L = (NBAND + 1 + 63) / 64;
       uint32_t v[PER_L], s = 0;
@@ -743,7 +815,7 @@ __global__ __launch_bounds__(PTPB) void k_band_scatter(const double* __restrict_
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < PER_T; ++k) {
-      if (band[k] < 0) continue;
+      if (band[k] < 0 || band[k] == nb) continue;   // dropped or resolved by the triage
       const uint32_t pos = loff[band[k]] + r[k];
       sx[pos] = x[k]; sy[pos] = y[k];
       sid[pos] = (uint32_t)(t0 + k * PTPB + t);
@@ -754,13 +826,15 @@ __global__ __launch_bounds__(PTPB) void k_band_scatter(const double* __restrict_
     for (int q = t; q < kept; q += PTPB) {
       const int b = sband[q];
       PtRec* o = rec + gcur[b] + (q - loff[b]);
-      o->x = sx[q]; o->y = sy[q]; o->idx = sid[q]; o->pad = 0;
+      o->x = sx[q]; o->y = sy[q];
+      *(uint2*)&o->idx = make_uint2(sid[q], 0u);
     }
     __syncthreads();
     for (int b = t; b <= nb; b += PTPB) {
       if (b < nb) gcur[b] += cnt[b];
       cnt[b] = 0;
     }
+    if (t == 0) s_np = 0;
     __syncthreads();
   }
 }
@@ -2672,28 +2746,40 @@ int gm_pip_join_pred(gm_ctx* ctx, const gm_pip_index* ix, const double* px, cons
     const int rows_per_band = (ix->dev.gy + NBAND - 1) / NBAND;
     const int nb = (ix->dev.gy + rows_per_band - 1) / rows_per_band;
     const int64_t mmax = std::min(CHUNK, n);
-    const int nblk = (int)std::max<int64_t>(1, std::min<int64_t>(512, (mmax + PTILE - 1) / PTILE));
+    // one resident wave of partition blocks (each walks a contiguous slice of the chunk)
+    const int nblk = (int)std::max<int64_t>(1, std::min<int64_t>(resident_grid(k_band_scatter<true>, ctx->device, 1 << 20, false),
+                                                                 (mmax + PTILE - 1) / PTILE));
     const int64_t hlen = (int64_t)nb * nblk;
     uint32_t* hist = nullptr;
+    uint32_t* pcount = nullptr;
+    int64_t* poff = nullptr;
     PtRec* rec = nullptr;
-    {  // context-owned workspace: records | histogram
-      const size_t a_rec = (size_t)mmax * sizeof(PtRec), a_h = (size_t)(hlen + 1) * 4;
+    {  // context-owned workspace: records | histogram | per-block pair counts | pair slots
+      const size_t a_rec = (size_t)mmax * sizeof(PtRec), a_h = ((size_t)(hlen + 1) * 4 + 15) & ~(size_t)15;
+      const size_t a_pc = ((size_t)nblk * 4 + 15) & ~(size_t)15;
       void* base = nullptr;
-      int wrc = ctx_workspace(ctx, WS_JOIN, a_rec + a_h, &base);
+      int wrc = ctx_workspace(ctx, WS_JOIN, a_rec + a_h + a_pc + (size_t)nblk * 8, &base);
       if (wrc) return wrc;
       rec = (PtRec*)base;
       hist = (uint32_t*)((char*)base + a_rec);
+      pcount = (uint32_t*)((char*)base + a_rec + a_h);
+      poff = (int64_t*)((char*)base + a_rec + a_h + a_pc);
     }
     int rc = GM_OK;
     for (int64_t c0 = 0; c0 < n && rc == GM_OK; c0 += CHUNK) {
       const int64_t m = std::min(CHUNK, n - c0);
       const int64_t per = ((m + nblk - 1) / nblk + PTILE - 1) / PTILE * PTILE;
       const unsigned pgrid = (unsigned)((m + per - 1) / per);   // <= nblk
-      hipLaunchKernelGGL(k_band_hist, dim3(pgrid), dim3(PTPB), 0, ctx->stream, py + c0, m, per, ix->dev,
-                         rows_per_band, nb, hist);
-      hipLaunchKernelGGL(k_band_scan, dim3(1), dim3(1024), 0, ctx->stream, hist, (int64_t)nb * pgrid);
-      hipLaunchKernelGGL(k_band_scatter, dim3(pgrid), dim3(PTPB), 0, ctx->stream, px + c0, py + c0, m, per, ix->dev,
-                         rows_per_band, nb, hist, rec);
+      hipLaunchKernelGGL(k_band_hist, dim3(pgrid), dim3(PTPB), 0, ctx->stream, px + c0, py + c0, m, per, dv,
+                         rows_per_band, nb, hist, pcount);
+      hipLaunchKernelGGL(k_band_scan, dim3(1), dim3(1024), 0, ctx->stream, hist, (int64_t)nb * pgrid, pcount, (int)pgrid,
+                         poff, counter);
+      if (write)
+        hipLaunchKernelGGL(k_band_scatter<true>, dim3(pgrid), dim3(PTPB), 0, ctx->stream, px + c0, py + c0, m, per, dv,
+                           rows_per_band, nb, hist, rec, poff, id_base + c0, pt_ids, poly_ids, cap);
+      else
+        hipLaunchKernelGGL(k_band_scatter<false>, dim3(pgrid), dim3(PTPB), 0, ctx->stream, px + c0, py + c0, m, per, dv,
+                           rows_per_band, nb, hist, rec, poff, id_base + c0, pt_ids, poly_ids, cap);
       const uint32_t* n_rec = hist + (int64_t)nb * pgrid;
       const int64_t ntiles = (m + JTILE - 1) / JTILE;
       const unsigned grid = write ? join_grid<true, true, false>(ctx->device, ntiles)
