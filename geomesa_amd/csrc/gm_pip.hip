@@ -61,6 +61,8 @@ struct PipDev {
   const double* compact;         // compact blobs: 16 words (one 128-B line) each
   const uint32_t* list_ent;      // entries in cell-word form (kind INTERIOR or BOUNDARY)
   const double* blob;            // boundary blobs, 16-byte aligned
+  const uint32_t* cell_sc;       // per cell: the cell word with the boundary shortcuts applied (k_build_shortcut)
+  const uint4* line_ent;         // line shortcuts: {cell word, polygon, A | B << 16, C | sides << 24}
   double gx0, gy0, gx1, gy1, inv_cw, inv_ch;
   int32_t gx, gy, gxc;
   int32_t op;                    // join predicate: JOIN_CONTAINS (interior) or JOIN_INTERSECTS (not exterior)
@@ -204,6 +206,15 @@ __device__ __forceinline__ void compact_line(const dv2* __restrict__ c, int E, d
   dv2 q[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) q[i] = c[8 * LINE + i];
+#ifdef GM_JX_BLOBUNI   // timing experiment only: pieces 1-7 of the line from one wave-uniform address
+#pragma unroll
+  for (int i = 1; i < 8; ++i) {
+    const uint64_t a = (uint64_t)(c + 8 * LINE + i);
+    const uint64_t u = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(a >> 32)) << 32) |
+                       (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)a);
+    q[i] = *(const dv2*)u;
+  }
+#endif
   auto word = [&](int w) -> double { return (w & 1) ? q[(w & 15) >> 1].y : q[(w & 15) >> 1].x; };
 #pragma unroll
   for (int w = 16 * LINE; w < 16 * LINE + 16; ++w) {
@@ -238,6 +249,61 @@ __device__ __forceinline__ int compact_locate(const dv2* __restrict__ c, double 
 
 __device__ __forceinline__ bool compact_contains(const dv2* __restrict__ c, double px, double py, int& poly) {
   return compact_locate(c, px, py, poly) == LOC_INTERIOR;
+}
+
+// Boundary shortcuts.  A BOUNDARY (cell, polygon) word stands for every ring segment whose bounding
+// box meets the cell; the segments that actually cross the cell are found once, on the device
+// (k_build_shortcut), and the join walks cell_sc, a copy of the cell words where
+//  * a cell crossed by none of them has one location (no boundary inside it): its word becomes
+//    INTERIOR(polygon) or EMPTY;
+//  * a cell crossed by exactly one segment is cut into two regions, each of one location: its word
+//    becomes LINE | entry, and line_ent holds the polygon, the segment's line in cell units,
+//    f(u, v) = A u + B v - C (int16 A, B with max |A|, |B| = 2^14, int24 C, |f - f_exact| <= SC_DEV over
+//    the cell), and each side's location, found by locating test points of that side from the blob.
+//    A point with f > SC_T or f < -SC_T takes its side's location; a point near the line (and so every
+//    boundary point) takes the exact blob walk from the entry's original word.
+// Every location comes from the blob's own PointLocator walk, so results are those of the blob.
+constexpr double SC_DEV = 4.0;   // quantization deviation allowed over the cell (units of 2^-14 cell)
+constexpr double SC_T = 6.0;     // decision threshold: SC_DEV plus ample room for FP64 rounding
+enum : uint32_t { SC_POS = 1, SC_POS_IN = 2, SC_NEG = 4, SC_NEG_IN = 8 };
+// LINE words: BOUNDARY | BLOB_COMPACT | SC_LINE | entry (compact blob indices stay below SC_LINE)
+constexpr uint32_t SC_LINE = 1u << 28;
+
+// f(u, v) of a point, with u, v its position in cell units inside cell (cx, cy) (cell_of's arithmetic)
+__device__ __forceinline__ double shortcut_f(const uint4 f, double x, double y, const PipDev& d, int cx, int cy) {
+  const double u = __dsub_rn(__dmul_rn(__dsub_rn(x, d.gx0), d.inv_cw), (double)cx);
+  const double v = __dsub_rn(__dmul_rn(__dsub_rn(y, d.gy0), d.inv_ch), (double)cy);
+  const double A = (double)(int16_t)(f.z & 0xffffu), B = (double)(int16_t)(f.z >> 16);
+  const double C = (double)((int32_t)(f.w << 8) >> 8);
+  return __dsub_rn(__dadd_rn(__dmul_rn(A, u), __dmul_rn(B, v)), C);
+}
+
+// the side of a line entry a point is on: LOC_INTERIOR / LOC_EXTERIOR, or -1 (near the line, or a
+// side without a location: the blob decides)
+__device__ __forceinline__ int line_locate(const uint4 f, double x, double y, const PipDev& d) {
+  const uint32_t fl = f.w >> 24;
+  const double g = shortcut_f(f, x, y, d, cell_of(x, d.gx0, d.inv_cw, d.gx), cell_of(y, d.gy0, d.inv_ch, d.gy));
+  if (g > SC_T && (fl & SC_POS)) return (fl & SC_POS_IN) ? LOC_INTERIOR : LOC_EXTERIOR;
+  if (g < -SC_T && (fl & SC_NEG)) return (fl & SC_NEG_IN) ? LOC_INTERIOR : LOC_EXTERIOR;
+  return -1;
+}
+
+// PointLocator's location of a point for one BOUNDARY item (ref = the word's payload): a line
+// shortcut (near the line: the entry's own blob), a compact blob or a generic blob
+__device__ __forceinline__ int item_locate(const PipDev& d, uint32_t ref, double x, double y, int& poly) {
+  int loc = -1;
+  if ((ref & BLOB_COMPACT) && d.line_ent && (ref & SC_LINE)) {
+    const uint4 f = d.line_ent[ref & (SC_LINE - 1)];
+    poly = (int)f.y;
+    loc = line_locate(f, x, y, d);
+    ref = f.x & 0x3fffffffu;
+  }
+  if (loc >= 0) return loc;
+  if (ref & BLOB_COMPACT) return compact_locate((const dv2*)(d.compact + 16 * (uint64_t)(ref & (BLOB_COMPACT - 1))), x, y, poly);
+  const double* b = d.blob + 2 * (uint64_t)ref;
+  const int2 h = *(const int2*)b;
+  poly = h.x;
+  return blob_locate(d, b, h, x, y);
 }
 
 constexpr int JTPB = 256;             // 4 waves
@@ -358,7 +424,7 @@ __global__ __launch_bounds__(JTPB, GM_JOIN_WAVES) void k_pip_join(const double* 
   uint2* wpp = s_pp + (WRITE && SPLIT ? wv * WC : 0);
   const int64_t seg = (int64_t)blockIdx.x * NW + wv;   // split: this wave's private segments
   int64_t icur = 0, pcur = 0;
-  int wn = 0, qn = 0;   // wave-uniform fills of the pair staging and the blob queue
+  int wn = 0, qn = 0, qg = 0;   // wave-uniform fills of the pair staging and the blob queue (compact / generic)
   int my_count = 0;
   if (REC) n = *n_rec;
   const int64_t ntiles = (n + JTILE - 1) / JTILE;
@@ -413,7 +479,7 @@ __global__ __launch_bounds__(JTPB, GM_JOIN_WAVES) void k_pip_join(const double* 
 #ifdef GM_JX_NOFINE   // timing experiment only: stop at the coarse level
         cw[u] = CELL_EMPTY << 30;
 #else
-        cw[u] = d.cell_word[(int64_t)cys[u] * d.gx + cxs[u]];
+        cw[u] = d.cell_sc[(int64_t)cys[u] * d.gx + cxs[u]];
 #endif
       }
 #pragma unroll
@@ -445,7 +511,7 @@ __global__ __launch_bounds__(JTPB, GM_JOIN_WAVES) void k_pip_join(const double* 
     for (int k = 0;; ++k) {
       const bool act = k < ntot;
       const bool any = __ballot(act) != 0;
-      if (!any && (have ? qn < (SPLIT ? QCAP_S - 64 : 64) : qn == 0)) break;
+      if (!any && (have ? qn + qg < (SPLIT ? QCAP_S - 64 : 64) : qn + qg == 0)) break;   // split: qg = 0
       if (any) {
         // item k belongs to the last point u with pre[u] <= k (static selects, no register indexing)
         double ex = x[0], ey = y[0];
@@ -471,26 +537,35 @@ __global__ __launch_bounds__(JTPB, GM_JOIN_WAVES) void k_pip_join(const double* 
           }
           wn += __popcll(m);
         }
-        const uint64_t mq = __ballot(blob);
-        if (blob) {
-          const int o = qn + lanes_below(mq);
-          if (SPLIT) {
-            qi[o] = make_uint2(eid, e & 0x3fffffffu);
-          } else {
+        if (SPLIT) {
+          const uint64_t mq = __ballot(blob);
+          if (blob) qi[qn + lanes_below(mq)] = make_uint2(eid, e & 0x3fffffffu);
+          qn += __popcll(mq);
+        } else {
+          // compact blobs stack up from slot 0, generic blobs down from slot QCAP - 1, so every
+          // evaluation round below runs one kind of blob code on all its lanes
+          const bool cmp = (e & BLOB_COMPACT) != 0;
+          const uint64_t mc = __ballot(blob && cmp), mg = __ballot(blob && !cmp);
+          if (blob) {
+            const int o = cmp ? qn + lanes_below(mc) : QCAP - 1 - qg - lanes_below(mg);
             qx[o] = ex; qy[o] = ey; qid[o] = eid; qb[o] = e & 0x3fffffffu;
           }
+          qn += __popcll(mc);
+          qg += __popcll(mg);
         }
-        qn += __popcll(mq);
       }
       if (SPLIT) {
         if (qn >= QCAP_S - 64 || (!have && !any && qn > 0)) {   // hand the wave's items to the work list
           append_seg(qi, qn, lane, sp.items + seg * sp.ipw, icur, sp.ipw);
           qn = 0;
         }
-      } else if (qn >= 64 || (!have && !any && qn > 0)) {   // evaluate the newest min(qn, 64) queued items
+      } else if (qn + qg >= 64 || (!have && !any && qn + qg > 0)) {
+        // evaluate the newest min(count, 64) items of the fuller kind: the queue then holds < 64
+        // items again, whatever the mix (qn + qg < 128 here, so the fuller kind holds at least half)
         wave_lds_sync();
-        const int kq = qn < 64 ? qn : 64;
-        const int slot = qn - kq + lane;
+        const bool cmp = qn >= qg;
+        const int kq = min(cmp ? qn : qg, 64);
+        const int slot = cmp ? qn - kq + lane : QCAP - qg + lane;
         bool hit = false;
         int poly = 0;
         uint32_t eid = 0;
@@ -503,9 +578,18 @@ __global__ __launch_bounds__(JTPB, GM_JOIN_WAVES) void k_pip_join(const double* 
             poly = 0; hit = false;
           } else
 #endif
-          if (ref & BLOB_COMPACT) {
-            const dv2* c = (const dv2*)(d.compact + 16 * (uint64_t)(ref & (BLOB_COMPACT - 1)));
-            hit = join_hit(d.op, compact_locate(c, ex, ey, poly));
+#ifdef GM_JX_NOGEN    // timing experiment only: generic blobs not evaluated
+          if (!cmp) {
+            poly = 0; hit = false;
+          } else
+#endif
+#ifdef GM_JX_NOCMP    // timing experiment only: compact blobs not evaluated
+          if (cmp) {
+            poly = 0; hit = false;
+          } else
+#endif
+          if (cmp) {
+            hit = join_hit(d.op, item_locate(d, ref, ex, ey, poly));
           } else {
             const double* b = d.blob + 2 * (uint64_t)ref;
             const int2 h = *(const int2*)b;
@@ -514,7 +598,8 @@ __global__ __launch_bounds__(JTPB, GM_JOIN_WAVES) void k_pip_join(const double* 
           }
         }
         wave_lds_sync();
-        qn -= kq;
+        if (cmp) qn -= kq;
+        else qg -= kq;
         if (!WRITE) my_count += hit;
         if (WRITE) {
           const uint64_t m = __ballot(hit);
@@ -570,16 +655,7 @@ __global__ __launch_bounds__(JTPB) void k_pip_blobs(const double* __restrict__ p
         const uint2 it = items[i];
         row = it.x;
         const uint32_t ref = it.y;
-        const double ex = px[row], ey = py[row];
-        if (ref & BLOB_COMPACT) {
-          const dv2* c = (const dv2*)(d.compact + 16 * (uint64_t)(ref & (BLOB_COMPACT - 1)));
-          hit = join_hit(d.op, compact_locate(c, ex, ey, poly));
-        } else {
-          const double* b = d.blob + 2 * (uint64_t)ref;
-          const int2 h = *(const int2*)b;
-          poly = h.x;
-          hit = join_hit(d.op, blob_locate(d, b, h, ex, ey));
-        }
+        hit = join_hit(d.op, item_locate(d, ref, px[row], py[row], poly));
       }
       if (!WRITE) my_count += hit;
       if (WRITE) {
@@ -1700,6 +1776,148 @@ __global__ void k_build_coarse(const uint32_t* __restrict__ cell_word, int gx, i
   }
 }
 
+// does segment (u1, v1)-(u2, v2) meet the box [lo, hi]^2 (cell units)?  Liang-Barsky clipping; the
+// caller's box is the cell enlarged by 1% of a cell, far beyond the builder's inflation and the
+// rounding of the cell-unit mapping, so "no" is certain.
+__device__ __forceinline__ bool seg_meets_box(double u1, double v1, double u2, double v2, double lo, double hi) {
+  double t0 = 0.0, t1 = 1.0;
+  const double du = u2 - u1, dv = v2 - v1;
+  const double p[4] = {-du, du, -dv, dv}, q[4] = {u1 - lo, hi - u1, v1 - lo, hi - v1};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    if (p[k] == 0.0) {
+      if (q[k] < 0.0) return false;
+    } else {
+      const double r = q[k] / p[k];
+      if (p[k] < 0.0) t0 = fmax(t0, r);
+      else t1 = fmin(t1, r);
+    }
+  }
+  return t0 <= t1;
+}
+
+// One cell's shortcut (see "Boundary shortcuts"): 0 = none, 1 = *word resolved to INTERIOR / EMPTY,
+// 2 = a line entry in *ent.  Compact and generic blobs alike; rings left to the slab walk have no
+// segment list here, so their cells keep the blob.
+__device__ int analyze_cell(const PipDev& d, int64_t c, uint32_t w, uint32_t* word, uint4* ent) {
+  if ((w >> 30) != CELL_BOUNDARY) return 0;
+  if (!(isfinite(d.inv_cw) && isfinite(d.inv_ch) && d.inv_cw > 0 && d.inv_ch > 0)) return 0;
+  const bool cmp = (w & BLOB_COMPACT) != 0;
+  const dv2* cb = (const dv2*)(d.compact + 16 * (uint64_t)(w & (BLOB_COMPACT - 1)));
+  const double* gb = d.blob + 2 * (uint64_t)(w & 0x3fffffffu);
+  int poly, nseg_or_rings;
+  if (cmp) {
+    const int64_t meta = __double_as_longlong(cb[0].x);
+    poly = (int)meta;
+    nseg_or_rings = (int)((meta >> 32) & 0xff);
+  } else {
+    const int2 h = *(const int2*)gb;
+    poly = h.x;
+    nseg_or_rings = h.y;
+  }
+  const int cx = (int)(c % d.gx), cy = (int)(c / d.gx);
+  auto cu = [&](double x) { return (x - d.gx0) * d.inv_cw - cx; };
+  auto cv = [&](double y) { return (y - d.gy0) * d.inv_ch - cy; };
+  // the segments crossing the enlarged cell: how many, and the last one
+  int ncross = 0;
+  double l1x = 0, l1y = 0, l2x = 0, l2y = 0;
+  auto visit = [&](double p1x, double p1y, double p2x, double p2y) -> bool {
+    const double u1 = cu(p1x), v1 = cv(p1y), u2 = cu(p2x), v2 = cv(p2y);
+    if (!(isfinite(u1) && isfinite(v1) && isfinite(u2) && isfinite(v2))) return false;
+    if (seg_meets_box(u1, v1, u2, v2, -0.01, 1.01)) { ++ncross; l1x = p1x; l1y = p1y; l2x = p2x; l2y = p2y; }
+    return true;
+  };
+  if (cmp) {
+    for (int j = 0; j < nseg_or_rings; ++j) {
+      const dv2 s0 = cb[cseg_word(j) / 2], s1 = cb[cseg_word(j) / 2 + 1];   // p1x p1y, p2x p2y
+      if (!visit(s0.x, s0.y, s1.x, s1.y)) return 0;
+    }
+  } else {
+    const double* q = gb + 1;
+    for (int r = 0; r < nseg_or_rings; ++r) {
+      const RingHdr rh = *(const RingHdr*)q;
+      if (rh.flags & 2) return 0;   // slab-walk ring: its segments are not in the blob
+      const double* eg = q + 2;
+      for (int j = 0; j < rh.n_edge; ++j)
+        if (!visit(eg[4 * j], eg[4 * j + 1], eg[4 * j + 2], eg[4 * j + 3])) return 0;
+      q = eg + 4 * rh.n_edge + rh.n_brk;
+    }
+  }
+  auto locate = [&](double X, double Y) -> int {
+    if (cmp) { int pp; return compact_locate(cb, X, Y, pp); }
+    return blob_locate(d, gb, *(const int2*)gb, X, Y);
+  };
+  if (ncross == 0) {
+    const double X0 = d.gx0 + (cx + 0.5) / d.inv_cw, Y0 = d.gy0 + (cy + 0.5) / d.inv_ch;
+    if (cell_of(X0, d.gx0, d.inv_cw, d.gx) != cx || cell_of(Y0, d.gy0, d.inv_ch, d.gy) != cy) return 0;
+    const int loc = locate(X0, Y0);   // the cell's one location
+    if (loc == LOC_INTERIOR) { *word = (CELL_INTERIOR << 30) | (uint32_t)poly; return 1; }
+    if (loc == LOC_EXTERIOR) { *word = CELL_EMPTY << 30; return 1; }
+    return 0;
+  }
+  if (ncross != 1) return 0;
+  const double u1 = cu(l1x), v1 = cv(l1y), u2 = cu(l2x), v2 = cv(l2y);
+  double at = v2 - v1, bt = u1 - u2;
+  const double mx = fmax(fabs(at), fabs(bt));
+  if (!(mx > 0)) return 0;
+  at *= 16384.0 / mx;
+  bt *= 16384.0 / mx;
+  const double ct = at * u1 + bt * v1;
+  const double A = rint(at), B = rint(bt), C = rint(ct);
+  if (!(fabs(C) < 8.0e6)) return 0;
+  double dev = 0.0;
+  for (int k = 0; k < 4; ++k) {
+    const double uc = (k & 1) ? 1.01 : -0.01, vc = (k & 2) ? 1.01 : -0.01;
+    dev = fmax(dev, fabs((A - at) * uc + (B - bt) * vc - (C - ct)));
+  }
+  if (!(dev <= SC_DEV)) return 0;
+  uint4 f = make_uint4(w, (uint32_t)poly, ((uint32_t)(int32_t)A & 0xffffu) | ((uint32_t)(int32_t)B << 16),
+                       (uint32_t)(int32_t)C & 0xffffffu);
+  uint32_t fl = 0, bad = 0;
+  for (int t = 0; t < 9; ++t) {   // test points of a 3 x 3 pattern inside the cell
+    const double tu = 0.05 + 0.45 * (t % 3), tv = 0.05 + 0.45 * (t / 3);
+    const double X = d.gx0 + (cx + tu) / d.inv_cw, Y = d.gy0 + (cy + tv) / d.inv_ch;
+    if (cell_of(X, d.gx0, d.inv_cw, d.gx) != cx || cell_of(Y, d.gy0, d.inv_ch, d.gy) != cy) continue;
+    const double g = shortcut_f(f, X, Y, d, cx, cy);
+    const int side = g > 2 * SC_T ? 0 : g < -2 * SC_T ? 1 : -1;
+    if (side < 0) continue;
+    const int loc = locate(X, Y);
+    const uint32_t has = side ? SC_NEG : SC_POS, in = side ? SC_NEG_IN : SC_POS_IN;
+    if (loc == LOC_BOUNDARY) { bad |= has; continue; }
+    const uint32_t want = loc == LOC_INTERIOR ? in : 0u;
+    if ((fl & has) && (fl & in) != want) bad |= has;   // inconsistent: no shortcut for that side
+    fl |= has | want;
+  }
+  if (bad & SC_POS) fl &= ~(SC_POS | SC_POS_IN);
+  if (bad & SC_NEG) fl &= ~(SC_NEG | SC_NEG_IN);
+  if (!fl) return 0;
+  f.w |= fl << 24;
+  *ent = f;
+  return 2;
+}
+
+// pass 0 (ent == nullptr): cell_sc = resolved words, is_line[c] = 1 for line cells;
+// pass 1: the line entries at their scanned slots, and the LINE words
+template <bool LINES>
+__global__ __launch_bounds__(256) void k_build_shortcut(PipDev d, int64_t ncell, uint32_t* __restrict__ cell_sc,
+                                                        int32_t* __restrict__ is_line, const int64_t* __restrict__ slot,
+                                                        uint4* __restrict__ ent) {
+  for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < ncell; c += (int64_t)gridDim.x * blockDim.x) {
+    if (LINES && !is_line[c]) continue;
+    const uint32_t w = d.cell_word[c];
+    uint32_t word = w;
+    uint4 e;
+    const int k = analyze_cell(d, c, w, &word, &e);
+    if (!LINES) {
+      cell_sc[c] = k == 1 ? word : w;
+      is_line[c] = k == 2;
+    } else if (k == 2) {
+      ent[slot[c]] = e;
+      cell_sc[c] = (CELL_BOUNDARY << 30) | BLOB_COMPACT | SC_LINE | (uint32_t)slot[c];
+    }
+  }
+}
+
 __global__ void k_build_max(const int32_t* __restrict__ v, int64_t n, int* __restrict__ out) {
   int m = 0;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
@@ -1725,6 +1943,7 @@ struct gm_pip_index {
   int64_t n_entries = 0, n_boundary = 0, n_records = 0, n_slow = 0, n_cells = 0, blob_bytes = 0, n_compact = 0;
   int64_t max_bnd_per_cell = 0;   // most BOUNDARY (cell, polygon) entries of any cell: work items per point
   int64_t max_ent_per_cell = 0;   // most (cell, polygon) entries of any cell: pairs per point
+  int64_t n_lines = 0;            // line shortcut entries (make_shortcut)
   const int32_t* list_poly = nullptr;   // polygon of each list_ent slot (the row-wise predicate's list search)
   const void* arr[GM_PIP_INDEX_ARRAYS] = {};   // the device arrays in gm_pip_index_layout order
   int64_t arr_bytes[GM_PIP_INDEX_ARRAYS] = {};
@@ -1761,6 +1980,60 @@ int make_list_poly(gm_pip_index* ix) {
     GM_CHECK_LAUNCH();
   }
   return GM_OK;
+}
+
+// the shortcut tables of a built or imported index (device-derived, not part of the exported layout)
+int make_shortcut(gm_pip_index* ix) {
+  const int64_t ncell = ix->arr_bytes[3] / 4;
+  hipStream_t s = ix->ctx->stream;
+  void* p = nullptr;
+  GM_HIP(hipMalloc(&p, (size_t)std::max<int64_t>(ncell, 1) * 4));
+  ix->allocs.push_back(p);
+  ix->dev.cell_sc = (const uint32_t*)p;
+  ix->dev.line_ent = nullptr;
+  ix->n_lines = 0;
+  if (ncell == 0) return GM_OK;
+  const bool lines_ok = ix->arr_bytes[5] / 128 < (int64_t)SC_LINE;   // compact indices below the LINE bit
+  void *fl = nullptr, *sl = nullptr, *part = nullptr;
+  auto cleanup = [&]() { (void)hipFree(fl); (void)hipFree(sl); (void)hipFree(part); };
+  if (hipMalloc(&fl, (size_t)ncell * 4) != hipSuccess || hipMalloc(&sl, (size_t)(ncell + 1) * 8) != hipSuccess ||
+      hipMalloc(&part, (size_t)scan_partials_len(ncell) * 8) != hipSuccess) {
+    cleanup();
+    return hip_fail(hipErrorOutOfMemory, "gm_pip_index shortcut");
+  }
+  const unsigned g = (unsigned)std::min<int64_t>(65536, (ncell + 255) / 256);
+  hipLaunchKernelGGL(k_build_shortcut<false>, dim3(g), dim3(256), 0, s, ix->dev, ncell, (uint32_t*)p, (int32_t*)fl,
+                     nullptr, nullptr);
+  launch_excl_scan(s, (const int32_t*)fl, ncell, (int64_t*)sl, (int64_t*)part, (int64_t*)sl + ncell);
+  int64_t nl = 0;
+  int rc = copy_d2h(ix->ctx, &nl, (int64_t*)sl + ncell, 8);
+  if (!rc && nl > 0 && lines_ok && nl < (int64_t)SC_LINE) {
+    void* e = nullptr;
+    if (hipMalloc(&e, (size_t)nl * sizeof(uint4)) != hipSuccess) { cleanup(); return hip_fail(hipErrorOutOfMemory, "gm_pip_index lines"); }
+    ix->allocs.push_back(e);
+    ix->dev.line_ent = (const uint4*)e;
+    ix->n_lines = nl;
+    hipLaunchKernelGGL(k_build_shortcut<true>, dim3(g), dim3(256), 0, s, ix->dev, ncell, (uint32_t*)p, (int32_t*)fl,
+                       (const int64_t*)sl, (uint4*)e);
+  }
+  if (!rc && hipStreamSynchronize(s) != hipSuccess) rc = hip_fail(hipErrorLaunchFailure, "k_build_shortcut");
+  cleanup();
+  if (!rc && getenv("GM_PIP_DEBUG")) {   // coverage (diagnostic copies)
+    std::vector<uint32_t> cw((size_t)ncell), sc((size_t)ncell);
+    GM_HIP(hipMemcpy(cw.data(), ix->dev.cell_word, (size_t)ncell * 4, hipMemcpyDeviceToHost));
+    GM_HIP(hipMemcpy(sc.data(), p, (size_t)ncell * 4, hipMemcpyDeviceToHost));
+    int64_t nb = 0, nc = 0, nu = 0, ns = 0;
+    for (int64_t c = 0; c < ncell; ++c) {
+      if ((cw[(size_t)c] >> 30) != CELL_BOUNDARY) continue;
+      ++nb;
+      nc += (cw[(size_t)c] & BLOB_COMPACT) != 0;
+      nu += (sc[(size_t)c] >> 30) != CELL_BOUNDARY;
+      ns += (sc[(size_t)c] & (BLOB_COMPACT | SC_LINE)) == (BLOB_COMPACT | SC_LINE) && (sc[(size_t)c] >> 30) == CELL_BOUNDARY;
+    }
+    fprintf(stderr, "[gm_pip] shortcut: %lld boundary cell words (%lld compact), %lld uncrossed (one location), "
+            "%lld line shortcuts\n", (long long)nb, (long long)nc, (long long)nu, (long long)ns);
+  }
+  return rc;
 }
 
 struct BandSeg {
@@ -2248,6 +2521,7 @@ int gm_pip_index_create_ex(gm_ctx* ctx, const gm_polyset* ps, int cells_per_poly
       ix->dev.inv_cw = inv_cw; ix->dev.inv_ch = inv_ch;
       ix->dev.gx = gx; ix->dev.gy = gy;
       rc = make_list_poly(ix);
+      if (!rc) rc = make_shortcut(ix);
       if (rc) { gm_pip_index_destroy(ix); return rc; }
       if (getenv("GM_PIP_DEBUG")) {
         GM_HIP(hipStreamSynchronize(ctx->stream));
@@ -2535,6 +2809,7 @@ int gm_pip_index_create_ex(gm_ctx* ctx, const gm_polyset* ps, int cells_per_poly
   ix->dev.inv_cw = inv_cw; ix->dev.inv_ch = inv_ch;
   ix->dev.gx = gx; ix->dev.gy = gy; ix->dev.gxc = gxc;
   rc = make_list_poly(ix);
+  if (!rc) rc = make_shortcut(ix);
   if (rc) { gm_pip_index_destroy(ix); return rc; }
   if (getenv("GM_PIP_DEBUG")) {
     GM_HIP(hipStreamSynchronize(ctx->stream));
@@ -2612,6 +2887,7 @@ int gm_pip_index_import(gm_ctx* ctx, const gm_pip_index_layout* lay, void* const
   ix->n_records = lay->stats[3]; ix->n_slow = lay->stats[4]; ix->blob_bytes = lay->stats[5];
   ix->n_compact = lay->stats[6]; ix->max_bnd_per_cell = lay->stats[7]; ix->max_ent_per_cell = lay->stats[8];
   int rc = make_list_poly(ix);
+  if (!rc) rc = make_shortcut(ix);
   if (!rc && hipStreamSynchronize(ctx->stream) != hipSuccess) rc = hip_fail(hipErrorLaunchFailure, "gm_pip_index_import");
   if (rc) { gm_pip_index_destroy(ix); return rc; }
   *out = ix;

@@ -41,6 +41,39 @@ __global__ __launch_bounds__(256) void k_gather16(const uint4* __restrict__ tab,
   if (acc == 0x12345678u) atomicAdd(out, 1ull);
 }
 
+// 8 lanes per 128-B line: lanes 8k..8k+7 read the 16-B pieces of one random line (coalesced per group)
+template <int U>
+__global__ __launch_bounds__(256) void k_line8(const uint4* __restrict__ tab, uint32_t lmask, int64_t n,
+                                               unsigned long long* __restrict__ out) {
+  uint32_t acc = 0;
+  const int sub = threadIdx.x & 7;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x * U;
+  for (int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * U; i < n; i += stride) {
+    uint4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = tab[(uint64_t)(mix((i >> 3) * U + u) & lmask) * 8 + sub];
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc += v[u].x ^ v[u].w;
+  }
+  if (acc == 0x12345678u) atomicAdd(out, 1ull);
+}
+
+// every lane of a wave reads the same 16 B (uniform address, random per wave and step)
+template <int U>
+__global__ __launch_bounds__(256) void k_uniform16(const uint4* __restrict__ tab, uint32_t mask, int64_t n,
+                                                   unsigned long long* __restrict__ out) {
+  uint32_t acc = 0;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x * U;
+  for (int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * U; i < n; i += stride) {
+    uint4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = tab[mix((i >> 6) * U + u) & mask];
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc += v[u].x ^ v[u].w;
+  }
+  if (acc == 0x12345678u) atomicAdd(out, 1ull);
+}
+
 // dependent chain: each gather's address depends on the previous value (latency, not throughput)
 __global__ __launch_bounds__(256) void k_chain4(const uint32_t* __restrict__ tab, uint32_t mask, int64_t n,
                                                 unsigned long long* __restrict__ out) {
@@ -97,28 +130,22 @@ float timeit(F f) {
 }
 
 int main() {
-  const int64_t N = 1ll << 30;   // gathers per launch
+  const int64_t N = 1ll << 30;   // lane loads per launch
   const size_t big = (size_t)1 << 30;
   uint32_t* tab = nullptr;
   unsigned long long* out = nullptr;
   CK(hipMalloc(&tab, big));
   CK(hipMalloc(&out, 8));
   CK(hipMemset(tab, 1, big));
-  const int grids[] = {1024, 2048, 4096};
-  for (int g : grids) {
-    for (size_t tb : {(size_t)1 << 20, (size_t)1 << 22, (size_t)64 << 20, (size_t)1 << 30}) {
-      const uint32_t m4 = (uint32_t)(tb / 4 - 1), m16 = (uint32_t)(tb / 16 - 1);
-      float a = timeit([&] { hipLaunchKernelGGL(k_gather4<8>, dim3(g), dim3(256), 0, 0, tab, m4, N, out); });
-      float b = timeit([&] { hipLaunchKernelGGL(k_gather16<4>, dim3(g), dim3(256), 0, 0, (const uint4*)tab, m16, N, out); });
-      float c = timeit([&] { hipLaunchKernelGGL(k_chain4, dim3(g), dim3(256), 0, 0, tab, m4, N, out); });
-      printf("grid %5d table %8zu KB: gather4 %.3f ms (%.1f G/s)  gather16 %.3f ms (%.1f G/s, %.0f GB/s)  chain4 %.3f ms (%.1f G/s)\n",
-             g, tb >> 10, a, N / a / 1e6, b, N / b / 1e6, N * 16.0 / b / 1e6, c, N / c / 1e6);
-      fflush(stdout);
-    }
-    float l = timeit([&] { hipLaunchKernelGGL(k_lds4<8>, dim3(g), dim3(256), 0, 0, N, out); });
-    printf("grid %5d lds random dword: %.3f ms (%.1f G/s)\n", g, l, N / l / 1e6);
+  const int g = 2048;
+  for (size_t tb : {(size_t)1 << 20, (size_t)64 << 20, (size_t)1 << 30}) {
+    const uint32_t m16 = (uint32_t)(tb / 16 - 1), ml = (uint32_t)(tb / 128 - 1);
+    float b = timeit([&] { hipLaunchKernelGGL(k_gather16<4>, dim3(g), dim3(256), 0, 0, (const uint4*)tab, m16, N, out); });
+    float c = timeit([&] { hipLaunchKernelGGL(k_line8<4>, dim3(g), dim3(256), 0, 0, (const uint4*)tab, ml, N, out); });
+    float d = timeit([&] { hipLaunchKernelGGL(k_uniform16<4>, dim3(g), dim3(256), 0, 0, (const uint4*)tab, m16, N, out); });
+    printf("table %8zu KB (16-B lane loads): divergent %.3f ms (%.0f GB/s)  8-lane lines %.3f ms (%.0f GB/s)  uniform %.3f ms (%.0f GB/s)\n",
+           tb >> 10, b, N * 16.0 / b / 1e6, c, N * 16.0 / c / 1e6, d, N * 16.0 / d / 1e6);
+    fflush(stdout);
   }
-  float s = timeit([&] { hipLaunchKernelGGL(k_stream, dim3(8192), dim3(256), 0, 0, (const double2*)tab, (int64_t)(big / 16), out); });
-  printf("stream 1 GB: %.3f ms (%.0f GB/s)\n", s, big / s / 1e6);
   return 0;
 }
