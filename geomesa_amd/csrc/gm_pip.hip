@@ -62,7 +62,7 @@ struct PipDev {
   const uint32_t* list_ent;      // entries in cell-word form (kind INTERIOR or BOUNDARY)
   const double* blob;            // boundary blobs, 16-byte aligned
   const uint32_t* cell_sc;       // per cell: the cell word with the boundary shortcuts applied (k_build_shortcut)
-  const uint4* line_ent;         // line shortcuts: {cell word, polygon, A | B << 16, C | sides << 24}
+  const uint4* line_ent;         // line shortcuts, two uint4 each (see "Boundary shortcuts")
   double gx0, gy0, gx1, gy1, inv_cw, inv_ch;
   int32_t gx, gy, gxc;
   int32_t op;                    // join predicate: JOIN_CONTAINS (interior) or JOIN_INTERSECTS (not exterior)
@@ -256,36 +256,54 @@ __device__ __forceinline__ bool compact_contains(const dv2* __restrict__ c, doub
 // (k_build_shortcut), and the join walks cell_sc, a copy of the cell words where
 //  * a cell crossed by none of them has one location (no boundary inside it): its word becomes
 //    INTERIOR(polygon) or EMPTY;
-//  * a cell crossed by exactly one segment is cut into two regions, each of one location: its word
-//    becomes LINE | entry, and line_ent holds the polygon, the segment's line in cell units,
-//    f(u, v) = A u + B v - C (int16 A, B with max |A|, |B| = 2^14, int24 C, |f - f_exact| <= SC_DEV over
-//    the cell), and each side's location, found by locating test points of that side from the blob.
-//    A point with f > SC_T or f < -SC_T takes its side's location; a point near the line (and so every
-//    boundary point) takes the exact blob walk from the entry's original word.
+//  * a cell crossed by one or two segments gets a LINE word and a line entry: the segments' lines in
+//    cell units, f(u, v) = A u + B v - C (int16 A, B with max |A|, |B| = 2^14, int24 C, |f - f_exact| <=
+//    SC_DEV over the cell), and a location for each combination of sides.  Each combination of
+//    open half-planes meets the (convex) cell in a convex region that no boundary crosses, so the
+//    location is constant there; it is found by locating test points of that region from the blob.
+//    A point at least SC_T from every line takes its region's location; a point nearer a line (and
+//    so every boundary point) or in a region without a test point takes the exact blob walk from
+//    the entry's original word.
 // Every location comes from the blob's own PointLocator walk, so results are those of the blob.
+// Entry = two uint4: {cell word, polygon, A1 | B1 << 16, C1 | region flags << 24},
+// {A2 | B2 << 16, C2 | lines << 24, 0, 0}; region r = side1 + 2 side2 (side 0: f > 0) has flag bits
+// 2r (located) and 2r + 1 (interior).
 constexpr double SC_DEV = 4.0;   // quantization deviation allowed over the cell (units of 2^-14 cell)
 constexpr double SC_T = 6.0;     // decision threshold: SC_DEV plus ample room for FP64 rounding
-enum : uint32_t { SC_POS = 1, SC_POS_IN = 2, SC_NEG = 4, SC_NEG_IN = 8 };
 // LINE words: BOUNDARY | BLOB_COMPACT | SC_LINE | entry (compact blob indices stay below SC_LINE)
 constexpr uint32_t SC_LINE = 1u << 28;
 
-// f(u, v) of a point, with u, v its position in cell units inside cell (cx, cy) (cell_of's arithmetic)
-__device__ __forceinline__ double shortcut_f(const uint4 f, double x, double y, const PipDev& d, int cx, int cy) {
+// f(u, v) of a point on one quantized line (ab = A | B << 16, c = C in the low 24 bits), with u, v
+// its position in cell units inside cell (cx, cy) (cell_of's arithmetic)
+__device__ __forceinline__ double shortcut_f(uint32_t ab, uint32_t c, double x, double y, const PipDev& d, int cx, int cy) {
   const double u = __dsub_rn(__dmul_rn(__dsub_rn(x, d.gx0), d.inv_cw), (double)cx);
   const double v = __dsub_rn(__dmul_rn(__dsub_rn(y, d.gy0), d.inv_ch), (double)cy);
-  const double A = (double)(int16_t)(f.z & 0xffffu), B = (double)(int16_t)(f.z >> 16);
-  const double C = (double)((int32_t)(f.w << 8) >> 8);
+  const double A = (double)(int16_t)(ab & 0xffffu), B = (double)(int16_t)(ab >> 16);
+  const double C = (double)((int32_t)(c << 8) >> 8);
   return __dsub_rn(__dadd_rn(__dmul_rn(A, u), __dmul_rn(B, v)), C);
 }
 
-// the side of a line entry a point is on: LOC_INTERIOR / LOC_EXTERIOR, or -1 (near the line, or a
-// side without a location: the blob decides)
-__device__ __forceinline__ int line_locate(const uint4 f, double x, double y, const PipDev& d) {
-  const uint32_t fl = f.w >> 24;
-  const double g = shortcut_f(f, x, y, d, cell_of(x, d.gx0, d.inv_cw, d.gx), cell_of(y, d.gy0, d.inv_ch, d.gy));
-  if (g > SC_T && (fl & SC_POS)) return (fl & SC_POS_IN) ? LOC_INTERIOR : LOC_EXTERIOR;
-  if (g < -SC_T && (fl & SC_NEG)) return (fl & SC_NEG_IN) ? LOC_INTERIOR : LOC_EXTERIOR;
-  return -1;
+// the region of a point (side bits), or -1 within SC_T of a line
+__device__ __forceinline__ int line_region(const uint4 e0, const uint4 e1, double x, double y, const PipDev& d, int cx,
+                                           int cy, double t) {
+  const double g1 = shortcut_f(e0.z, e0.w, x, y, d, cx, cy);
+  if (!(g1 > t || g1 < -t)) return -1;
+  int r = g1 > t ? 0 : 1;
+  if ((e1.y >> 24) > 1) {
+    const double g2 = shortcut_f(e1.x, e1.y, x, y, d, cx, cy);
+    if (!(g2 > t || g2 < -t)) return -1;
+    r |= g2 > t ? 0 : 2;
+  }
+  return r;
+}
+
+// a point's location from a line entry: LOC_INTERIOR / LOC_EXTERIOR, or -1 (the blob decides)
+__device__ __forceinline__ int line_locate(const uint4 e0, const uint4 e1, double x, double y, const PipDev& d) {
+  const int r = line_region(e0, e1, x, y, d, cell_of(x, d.gx0, d.inv_cw, d.gx), cell_of(y, d.gy0, d.inv_ch, d.gy), SC_T);
+  if (r < 0) return -1;
+  const uint32_t fl = e0.w >> 24;
+  if (!((fl >> (2 * r)) & 1u)) return -1;
+  return ((fl >> (2 * r + 1)) & 1u) ? LOC_INTERIOR : LOC_EXTERIOR;
 }
 
 // PointLocator's location of a point for one BOUNDARY item (ref = the word's payload): a line
@@ -293,10 +311,10 @@ __device__ __forceinline__ int line_locate(const uint4 f, double x, double y, co
 __device__ __forceinline__ int item_locate(const PipDev& d, uint32_t ref, double x, double y, int& poly) {
   int loc = -1;
   if ((ref & BLOB_COMPACT) && d.line_ent && (ref & SC_LINE)) {
-    const uint4 f = d.line_ent[ref & (SC_LINE - 1)];
-    poly = (int)f.y;
-    loc = line_locate(f, x, y, d);
-    ref = f.x & 0x3fffffffu;
+    const uint4 e0 = d.line_ent[2 * (uint64_t)(ref & (SC_LINE - 1))], e1 = d.line_ent[2 * (uint64_t)(ref & (SC_LINE - 1)) + 1];
+    poly = (int)e0.y;
+    loc = line_locate(e0, e1, x, y, d);
+    ref = e0.x & 0x3fffffffu;
   }
   if (loc >= 0) return loc;
   if (ref & BLOB_COMPACT) return compact_locate((const dv2*)(d.compact + 16 * (uint64_t)(ref & (BLOB_COMPACT - 1))), x, y, poly);
@@ -1818,13 +1836,16 @@ __device__ int analyze_cell(const PipDev& d, int64_t c, uint32_t w, uint32_t* wo
   const int cx = (int)(c % d.gx), cy = (int)(c / d.gx);
   auto cu = [&](double x) { return (x - d.gx0) * d.inv_cw - cx; };
   auto cv = [&](double y) { return (y - d.gy0) * d.inv_ch - cy; };
-  // the segments crossing the enlarged cell: how many, and the last one
+  // the segments crossing the enlarged cell: how many, and the first two
   int ncross = 0;
-  double l1x = 0, l1y = 0, l2x = 0, l2y = 0;
+  double sg[2][4];
   auto visit = [&](double p1x, double p1y, double p2x, double p2y) -> bool {
     const double u1 = cu(p1x), v1 = cv(p1y), u2 = cu(p2x), v2 = cv(p2y);
     if (!(isfinite(u1) && isfinite(v1) && isfinite(u2) && isfinite(v2))) return false;
-    if (seg_meets_box(u1, v1, u2, v2, -0.01, 1.01)) { ++ncross; l1x = p1x; l1y = p1y; l2x = p2x; l2y = p2y; }
+    if (seg_meets_box(u1, v1, u2, v2, -0.01, 1.01)) {
+      if (ncross < 2) { sg[ncross][0] = u1; sg[ncross][1] = v1; sg[ncross][2] = u2; sg[ncross][3] = v2; }
+      ++ncross;
+    }
     return true;
   };
   if (cmp) {
@@ -1855,44 +1876,48 @@ __device__ int analyze_cell(const PipDev& d, int64_t c, uint32_t w, uint32_t* wo
     if (loc == LOC_EXTERIOR) { *word = CELL_EMPTY << 30; return 1; }
     return 0;
   }
-  if (ncross != 1) return 0;
-  const double u1 = cu(l1x), v1 = cv(l1y), u2 = cu(l2x), v2 = cv(l2y);
-  double at = v2 - v1, bt = u1 - u2;
-  const double mx = fmax(fabs(at), fabs(bt));
-  if (!(mx > 0)) return 0;
-  at *= 16384.0 / mx;
-  bt *= 16384.0 / mx;
-  const double ct = at * u1 + bt * v1;
-  const double A = rint(at), B = rint(bt), C = rint(ct);
-  if (!(fabs(C) < 8.0e6)) return 0;
-  double dev = 0.0;
-  for (int k = 0; k < 4; ++k) {
-    const double uc = (k & 1) ? 1.01 : -0.01, vc = (k & 2) ? 1.01 : -0.01;
-    dev = fmax(dev, fabs((A - at) * uc + (B - bt) * vc - (C - ct)));
+  if (ncross > 2) return 0;
+  uint32_t ab[2] = {0u, 0u}, cc[2] = {0u, 0u};
+  for (int k = 0; k < ncross; ++k) {   // quantized line of each crossing segment
+    const double u1 = sg[k][0], v1 = sg[k][1], u2 = sg[k][2], v2 = sg[k][3];
+    double at = v2 - v1, bt = u1 - u2;
+    const double mx = fmax(fabs(at), fabs(bt));
+    if (!(mx > 0)) return 0;
+    at *= 16384.0 / mx;
+    bt *= 16384.0 / mx;
+    const double ct = at * u1 + bt * v1;
+    const double A = rint(at), B = rint(bt), C = rint(ct);
+    if (!(fabs(C) < 8.0e6)) return 0;
+    double dev = 0.0;
+    for (int q = 0; q < 4; ++q) {
+      const double uc = (q & 1) ? 1.01 : -0.01, vc = (q & 2) ? 1.01 : -0.01;
+      dev = fmax(dev, fabs((A - at) * uc + (B - bt) * vc - (C - ct)));
+    }
+    if (!(dev <= SC_DEV)) return 0;
+    ab[k] = ((uint32_t)(int32_t)A & 0xffffu) | ((uint32_t)(int32_t)B << 16);
+    cc[k] = (uint32_t)(int32_t)C & 0xffffffu;
   }
-  if (!(dev <= SC_DEV)) return 0;
-  uint4 f = make_uint4(w, (uint32_t)poly, ((uint32_t)(int32_t)A & 0xffffu) | ((uint32_t)(int32_t)B << 16),
-                       (uint32_t)(int32_t)C & 0xffffffu);
+  const uint4 e0 = make_uint4(w, (uint32_t)poly, ab[0], cc[0]);
+  const uint4 e1 = make_uint4(ab[1], cc[1] | ((uint32_t)ncross << 24), 0u, 0u);
   uint32_t fl = 0, bad = 0;
-  for (int t = 0; t < 9; ++t) {   // test points of a 3 x 3 pattern inside the cell
-    const double tu = 0.05 + 0.45 * (t % 3), tv = 0.05 + 0.45 * (t / 3);
+  for (int t = 0; t < 25; ++t) {   // test points of a 5 x 5 pattern inside the cell
+    const double tu = 0.04 + 0.23 * (t % 5), tv = 0.04 + 0.23 * (t / 5);
     const double X = d.gx0 + (cx + tu) / d.inv_cw, Y = d.gy0 + (cy + tv) / d.inv_ch;
     if (cell_of(X, d.gx0, d.inv_cw, d.gx) != cx || cell_of(Y, d.gy0, d.inv_ch, d.gy) != cy) continue;
-    const double g = shortcut_f(f, X, Y, d, cx, cy);
-    const int side = g > 2 * SC_T ? 0 : g < -2 * SC_T ? 1 : -1;
-    if (side < 0) continue;
+    const int r = line_region(e0, e1, X, Y, d, cx, cy, 2 * SC_T);
+    if (r < 0) continue;
     const int loc = locate(X, Y);
-    const uint32_t has = side ? SC_NEG : SC_POS, in = side ? SC_NEG_IN : SC_POS_IN;
+    const uint32_t has = 1u << (2 * r), in = 2u << (2 * r);
     if (loc == LOC_BOUNDARY) { bad |= has; continue; }
     const uint32_t want = loc == LOC_INTERIOR ? in : 0u;
-    if ((fl & has) && (fl & in) != want) bad |= has;   // inconsistent: no shortcut for that side
+    if ((fl & has) && (fl & in) != want) bad |= has;   // inconsistent: no shortcut for that region
     fl |= has | want;
   }
-  if (bad & SC_POS) fl &= ~(SC_POS | SC_POS_IN);
-  if (bad & SC_NEG) fl &= ~(SC_NEG | SC_NEG_IN);
+  for (int r = 0; r < 4; ++r)
+    if (bad & (1u << (2 * r))) fl &= ~(3u << (2 * r));
   if (!fl) return 0;
-  f.w |= fl << 24;
-  *ent = f;
+  ent[0] = make_uint4(e0.x, e0.y, e0.z, e0.w | (fl << 24));
+  ent[1] = e1;
   return 2;
 }
 
@@ -1906,13 +1931,14 @@ __global__ __launch_bounds__(256) void k_build_shortcut(PipDev d, int64_t ncell,
     if (LINES && !is_line[c]) continue;
     const uint32_t w = d.cell_word[c];
     uint32_t word = w;
-    uint4 e;
-    const int k = analyze_cell(d, c, w, &word, &e);
+    uint4 e[2];
+    const int k = analyze_cell(d, c, w, &word, e);
     if (!LINES) {
       cell_sc[c] = k == 1 ? word : w;
       is_line[c] = k == 2;
     } else if (k == 2) {
-      ent[slot[c]] = e;
+      ent[2 * slot[c]] = e[0];
+      ent[2 * slot[c] + 1] = e[1];
       cell_sc[c] = (CELL_BOUNDARY << 30) | BLOB_COMPACT | SC_LINE | (uint32_t)slot[c];
     }
   }
@@ -2009,7 +2035,7 @@ int make_shortcut(gm_pip_index* ix) {
   int rc = copy_d2h(ix->ctx, &nl, (int64_t*)sl + ncell, 8);
   if (!rc && nl > 0 && lines_ok && nl < (int64_t)SC_LINE) {
     void* e = nullptr;
-    if (hipMalloc(&e, (size_t)nl * sizeof(uint4)) != hipSuccess) { cleanup(); return hip_fail(hipErrorOutOfMemory, "gm_pip_index lines"); }
+    if (hipMalloc(&e, (size_t)nl * 2 * sizeof(uint4)) != hipSuccess) { cleanup(); return hip_fail(hipErrorOutOfMemory, "gm_pip_index lines"); }
     ix->allocs.push_back(e);
     ix->dev.line_ent = (const uint4*)e;
     ix->n_lines = nl;
