@@ -1282,7 +1282,7 @@ __global__ __launch_bounds__(RTPB) void k_pip_relate(const int32_t* __restrict__
       }
 #pragma unroll
       for (int u = 0; u < RILP; ++u)
-        if ((w[u] >> 30) == CELL_LIST) w[u] = d.cell_word[(int64_t)cy[u] * d.gx + cx[u]];
+        if ((w[u] >> 30) == CELL_LIST) w[u] = d.cell_sc[(int64_t)cy[u] * d.gx + cx[u]];   // boundary shortcuts applied
 #pragma unroll
       for (int u = 0; u < RILP; ++u) {
         uint8_t r = LOC_EXTERIOR;
@@ -1323,15 +1323,8 @@ __global__ __launch_bounds__(RTPB) void k_pip_relate(const int32_t* __restrict__
       if (lane < kq) {
         const uint32_t ref = qe[slot] & 0x3fffffffu;
         const double ex = qx[slot], ey = qy[slot];
-        int pl, l;
-        if (ref & BLOB_COMPACT) {
-          l = compact_locate((const dv2*)(d.compact + 16 * (uint64_t)(ref & (BLOB_COMPACT - 1))), ex, ey, pl);
-        } else {
-          const double* b = d.blob + 2 * (uint64_t)ref;
-          const int2 h = *(const int2*)b;
-          pl = h.x;
-          l = blob_locate(d, b, h, ex, ey);
-        }
+        int pl = -1;
+        const int l = item_locate(d, ref, ex, ey, pl);
         loc[qr[slot]] = (uint8_t)(pl == qp[slot] ? l : LOC_EXTERIOR);
       }
       wave_lds_sync();
