@@ -488,7 +488,11 @@ __global__ __launch_bounds__(JTPB, GM_JOIN_WAVES) void k_pip_join(const double* 
       if (x[u] >= d.gx0 && x[u] <= d.gx1 && y[u] >= d.gy0 && y[u] <= d.gy1) {
         cxs[u] = cell_of(x[u], d.gx0, d.inv_cw, d.gx);
         cys[u] = cell_of(y[u], d.gy0, d.inv_ch, d.gy);
+#ifdef GM_JX_NOCOARSE   // timing experiment only: no coarse lookup (every point EMPTY)
+        cw[u] = CELL_EMPTY << 30;
+#else
         cw[u] = d.coarse_word[(int64_t)(cys[u] >> CF_LOG) * d.gxc + (cxs[u] >> CF_LOG)];
+#endif
       }
     }
 #pragma unroll
