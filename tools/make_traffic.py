@@ -50,8 +50,14 @@ def per_dispatch(root):
     return out
 
 
-def mean_for(d, sub, counter):
+def mean_for(d, sub, counter, largest=False):
+    """Mean per dispatch of kernels whose name holds `sub`; largest=True keeps only the dispatches of
+    the largest launches (e.g. the 1B-point encode, not the PCIe leg's 8M-point chunks of the same
+    kernel): those within half of the largest value."""
     vals = [v for k, cs in d.items() if sub in k for v in cs.get(counter, [])]
+    if largest and vals:
+        top = max(vals)
+        vals = [v for v in vals if v >= 0.5 * top]
     return sum(vals) / len(vals) if vals else None
 
 
@@ -59,7 +65,7 @@ def main(root, out, points=1_000_000_000, join_points=1_000_000_000, table_rows=
     d = per_dispatch(root)
     res = {}
     for name, (sub, unit, alg) in STREAMING.items():
-        f, w = mean_for(d, sub, "FETCH_SIZE"), mean_for(d, sub, "WRITE_SIZE")
+        f, w = mean_for(d, sub, "FETCH_SIZE", True), mean_for(d, sub, "WRITE_SIZE", True)
         if f is None or w is None:
             continue
         n = points if unit == "points" else (table_rows if unit == "rows" else min(points, 100_000_000))
