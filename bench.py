@@ -349,7 +349,7 @@ def gather_pairs(dist, ptids, plids, k):
         del g
         torch.cuda.empty_cache()
         return {"ms": ms, "pairs_on_rank0": n if dist.rank == 0 else None, "bytes": 12 * n,
-                "how": "all_gather of counts + padded gather to rank 0 (grouped send/recv over xGMI)"}
+                "how": "all_gather of counts, then batched point-to-point receives of exact sizes into rank 0's output slices (RCCL send/recv over xGMI)"}
     except Exception as e:  # noqa: BLE001 -- reported in the JSON line
         return {"error": repr(e)[:200]}
 

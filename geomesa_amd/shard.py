@@ -86,28 +86,41 @@ def gather_rows(pg, cols, dst=0):
     """Gather variable-length per-rank result columns (1-D tensors of equal length per rank: ids,
     or point ids + polygon ids) to rank `dst`, in rank order.
 
-    One all_gather of the per-rank counts (8 B each), then one gather of each column padded to the
-    largest count: over RCCL a gather is a grouped send/recv, so rank `dst` receives from every
-    peer at once over its own xGMI link (padding costs at most the imbalance between ranks).
-    Returns the concatenated columns on `dst` and None elsewhere; with pg None, `cols`."""
+    One all_gather of the per-rank counts (8 B each); then rank `dst` allocates each column once at
+    its exact total and receives every peer's rows straight into that peer's slice (point-to-point,
+    batched: over RCCL a group of sends / receives, so `dst` takes every peer's rows at once over its
+    own xGMI link), and copies its own rows in.  No padding and no concatenation copy: rank `dst`
+    holds the result and nothing else.  Returns the columns on `dst` and None elsewhere; with pg None,
+    `cols`."""
     if pg is None:
         return list(cols)
     import torch
     dev = _device_of(pg)
-    world = pg.get_world_size()
+    world, rank = pg.get_world_size(), pg.get_rank()
     n = torch.tensor([int(cols[0].numel())], dtype=torch.int64, device=dev)
     counts = [torch.zeros_like(n) for _ in range(world)]
     pg.all_gather(counts, n)
     counts = [int(c.item()) for c in counts]
-    mx = max(counts)
-    out = []
+    offs = [0]
+    for c in counts:
+        offs.append(offs[-1] + c)
+    out, ops, keep = [], [], []
     for c in cols:
-        buf = torch.zeros(mx, dtype=c.dtype, device=dev)
-        buf[:c.numel()] = c.to(dev)
-        parts = [torch.empty_like(buf) for _ in range(world)] if pg.get_rank() == dst else None
-        pg.gather(buf, parts, dst=dst)
-        out.append(torch.cat([p[:k] for p, k in zip(parts, counts)]) if pg.get_rank() == dst else None)
-    return out if pg.get_rank() == dst else None
+        if rank == dst:
+            o = torch.empty(offs[-1], dtype=c.dtype, device=dev)
+            o[offs[dst]:offs[dst + 1]] = c.to(dev)
+            for r in range(world):
+                if r != dst and counts[r] > 0:
+                    ops.append(pg.P2POp(pg.irecv, o[offs[r]:offs[r + 1]], r))
+            out.append(o)
+        elif counts[rank] > 0:
+            src = c.to(dev).contiguous()
+            keep.append(src)
+            ops.append(pg.P2POp(pg.isend, src, dst))
+    if ops:
+        for req in pg.batch_isend_irecv(ops):
+            req.wait()
+    return out if rank == dst else None
 
 
 def merge_histograms(pg, counts, present, bin_lo, length=None):

@@ -363,3 +363,44 @@ def test_gather_ranges():
     assert off.tolist() == np.concatenate([[0], np.cumsum(np.concatenate([c0, c1]))]).tolist()
     assert rr["lower"].tolist() == list(range(c0.sum())) + [1000 + i for i in range(c1.sum())]
     assert rr["contained"].tolist() == [0] * c0.sum() + [1] * c1.sum()
+
+
+def _grows_worker(rank, world, port, sizes, dst, q):
+    sys.path.insert(0, ROOT)
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from geomesa_amd.shard import gather_rows
+        k = sizes[rank]
+        ids = torch.arange(k, dtype=torch.int64) + 1000 * rank
+        pl = torch.full((k,), rank, dtype=torch.int32)
+        g = gather_rows(dist, [ids, pl], dst=dst)
+        q.put((rank, None if g is None else (g[0].numpy(), g[1].numpy())))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("sizes,dst", [((5, 0, 3), 0), ((0, 4, 2), 0), ((2, 7, 0), 1), ((0, 0, 0), 2)])
+def test_gather_rows_exact_sizes(sizes, dst):
+    """gather_rows: rank order, exact per-rank counts (empty ranks included, also the destination),
+    nothing on the other ranks (shard.py gather_rows)."""
+    world = len(sizes)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_grows_worker, args=(r, world, port, sizes, dst, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(world):
+        assert (got[r] is None) == (r != dst)
+    ids, pl = got[dst]
+    assert ids.tolist() == [1000 * r + i for r in range(world) for i in range(sizes[r])]
+    assert pl.tolist() == [r for r in range(world) for _ in range(sizes[r])]
+    assert ids.dtype == np.int64 and pl.dtype == np.int32
