@@ -101,6 +101,8 @@ template <int PERIOD, bool LENIENT, bool F32, bool TIME, int UNROLL>
 __global__ __launch_bounds__(ATPB) void k_z3_key_arrow_v(ArrowPts g, ArrowTime tc, int64_t n, NDim lon, NDim lat,
                                                          NDim tim, short2* __restrict__ bin, lv2* __restrict__ z,
                                                          uchar2* __restrict__ status, int64_t* __restrict__ err) {
+  static_assert(UNROLL == 4, "staged bins: 4 pairs per lane");
+  __shared__ uint32_t s_bin[ATPB * UNROLL];   // the block's bins, stored 16 B per lane at the end
   const int64_t npairs = n >> 1;
   const int64_t base = (int64_t)blockIdx.x * (ATPB * UNROLL) + threadIdx.x;
   dv2 a[UNROLL], b[UNROLL];
@@ -130,11 +132,12 @@ __global__ __launch_bounds__(ATPB) void k_z3_key_arrow_v(ArrowPts g, ArrowTime t
     if (arrow_valid(g.valid, g.voff, 2 * p)) s0 = z3_key_one<PERIOD, LENIENT>(x0, y0, tv[u].x, lon, lat, tim, b0, z0);
     if (arrow_valid(g.valid, g.voff, 2 * p + 1)) s1 = z3_key_one<PERIOD, LENIENT>(x1, y1, tv[u].y, lon, lat, tim, b1, z1);
     st_stream(lv2{z0, z1}, &z[p]);
-    bin[p] = make_short2(b0, b1);
+    s_bin[u * ATPB + threadIdx.x] = bin_pair(b0, b1);
     if (status) status[p] = make_uchar2(s0, s1);
     if (s0) report_error(err, 2 * p, s0);
     if (s1) report_error(err, 2 * p + 1, s1);
   }
+  store_staged_bins<ATPB>(s_bin, bin, npairs);
   if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {   // the odd last row
     const int64_t i = n - 1;
     int16_t bb = 0;

@@ -27,6 +27,27 @@ __device__ __forceinline__ void st_stream(T v, T* p) {
 #endif
 }
 
+// Bins of a key kernel's block leave as one 16-B store per lane: pair j of the block (pairs
+// [block * TPB * 4, +TPB * 4)) sits at s_bin[j] as bin0 | bin1 << 16, and lane l stores pairs
+// 4l .. 4l + 3 (a 4-B store per pair otherwise; bin columns are only 4-B aligned).  Every thread of
+// the block calls it (one barrier).
+template <int TPB>
+__device__ __forceinline__ void store_staged_bins(const uint32_t* s_bin, short2* __restrict__ bin, int64_t npairs) {
+  typedef unsigned int uv4 __attribute__((ext_vector_type(4)));
+  __syncthreads();
+  const int64_t q = (int64_t)blockIdx.x * (TPB * 4) + 4 * (int64_t)threadIdx.x;
+  if (q + 3 < npairs && ((uintptr_t)bin & 15u) == 0) {
+    __builtin_nontemporal_store(*(const uv4*)&s_bin[4 * threadIdx.x], (uv4*)&bin[q]);
+  } else {
+    for (int k = 0; k < 4; ++k)
+      if (q + k < npairs) ((uint32_t*)bin)[q + k] = s_bin[4 * threadIdx.x + k];
+  }
+}
+
+__device__ __forceinline__ uint32_t bin_pair(int16_t b0, int16_t b1) {
+  return (uint32_t)(uint16_t)b0 | ((uint32_t)(uint16_t)b1 << 16);
+}
+
 // ------------------------------------------------------------------ per-element bodies
 
 // Z3SFC.index (z3/curve/Z3SFC.scala:37-52); t is the offset within the period (Long)
