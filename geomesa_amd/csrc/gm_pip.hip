@@ -62,6 +62,7 @@ struct PipDev {
   const uint32_t* list_ent;      // entries in cell-word form (kind INTERIOR or BOUNDARY)
   const double* blob;            // boundary blobs, 16-byte aligned
   const uint32_t* cell_sc;       // per cell: the cell word with the boundary shortcuts applied (k_build_shortcut)
+  const uint32_t* coarse_sc;     // the join's coarse words over cell_sc; LIST words carry a sub-block EMPTY mask
   const uint4* line_ent;         // line shortcuts, two uint4 each (see "Boundary shortcuts")
   double gx0, gy0, gx1, gy1, inv_cw, inv_ch;
   int32_t gx, gy, gxc;
@@ -306,6 +307,19 @@ __device__ __forceinline__ int line_locate(const uint4 e0, const uint4 e1, doubl
   return ((fl >> (2 * r + 1)) & 1u) ? LOC_INTERIOR : LOC_EXTERIOR;
 }
 
+// The join's coarse table (coarse_sc, 4 B per coarse cell like coarse_word, so it stays L2-resident)
+// is built over cell_sc: EMPTY / INTERIOR(p) when all its fine cells carry that word, else LIST with
+// bit s of the payload set when all fine cells of sub-block s (4 x 4 sub-blocks of 2 x 2 fine
+// cells) are EMPTY: a point there needs no fine lookup.
+constexpr int SUB_LOG = CF_LOG - 2;
+static_assert(CF_LOG >= 2, "sub-block masks need at least 4 x 4 fine cells per coarse cell");
+
+__device__ __forceinline__ uint32_t coarse_mask(uint32_t w, int cx, int cy) {
+  if ((w >> 30) != CELL_LIST) return w;
+  const int sub = (((cy & ((1 << CF_LOG) - 1)) >> SUB_LOG) << 2) | ((cx & ((1 << CF_LOG) - 1)) >> SUB_LOG);
+  return ((w >> sub) & 1u) ? (CELL_EMPTY << 30) : w;
+}
+
 // PointLocator's location of a point for one BOUNDARY item (ref = the word's payload): a line
 // shortcut (near the line: the entry's own blob), a compact blob or a generic blob
 __device__ __forceinline__ int item_locate(const PipDev& d, uint32_t ref, double x, double y, int& poly) {
@@ -491,7 +505,7 @@ __global__ __launch_bounds__(JTPB, GM_JOIN_WAVES) void k_pip_join(const double* 
 #ifdef GM_JX_NOCOARSE   // timing experiment only: no coarse lookup (every point EMPTY)
         cw[u] = CELL_EMPTY << 30;
 #else
-        cw[u] = d.coarse_word[(int64_t)(cys[u] >> CF_LOG) * d.gxc + (cxs[u] >> CF_LOG)];
+        cw[u] = coarse_mask(d.coarse_sc[(int64_t)(cys[u] >> CF_LOG) * d.gxc + (cxs[u] >> CF_LOG)], cxs[u], cys[u]);
 #endif
       }
     }
@@ -769,7 +783,7 @@ __device__ __forceinline__ int triage_band(double x, double y, uint32_t w, const
 __device__ __forceinline__ uint32_t coarse_of(double x, double y, const PipDev& d) {
   if (!(x >= d.gx0 && x <= d.gx1 && y >= d.gy0 && y <= d.gy1)) return CELL_EMPTY << 30;
   const int cx = cell_of(x, d.gx0, d.inv_cw, d.gx), cy = cell_of(y, d.gy0, d.inv_ch, d.gy);
-  return d.coarse_word[(int64_t)(cy >> CF_LOG) * d.gxc + (cx >> CF_LOG)];
+  return coarse_mask(d.coarse_sc[(int64_t)(cy >> CF_LOG) * d.gxc + (cx >> CF_LOG)], cx, cy);
 }
 
 // per-block band histogram of the triaged points, band-major: hist[band * gridDim.x + block], and
@@ -1918,6 +1932,32 @@ __device__ int analyze_cell(const PipDev& d, int64_t c, uint32_t w, uint32_t* wo
   return 2;
 }
 
+// coarse_sc (see coarse_mask) over the resolved words cell_sc
+__global__ __launch_bounds__(256) void k_build_coarse_sc(const uint32_t* __restrict__ cell_sc, int gx, int gy, int gxc,
+                                                         int gyc, uint32_t* __restrict__ out) {
+  const int64_t n = (int64_t)gxc * gyc;
+  constexpr int CF = 1 << CF_LOG, SB = 1 << SUB_LOG;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int yc = (int)(i / gxc), xc = (int)(i % gxc);
+    uint32_t w0 = 0xffffffffu, mask = 0;
+    bool mixed = false;
+    for (int sb = 0; sb < 16; ++sb) {
+      const int x0 = xc * CF + (sb & 3) * SB, y0 = yc * CF + (sb >> 2) * SB;
+      bool empty = true;
+      for (int yy = y0; yy < min(gy, y0 + SB); ++yy)
+        for (int xx = x0; xx < min(gx, x0 + SB); ++xx) {
+          const uint32_t f = cell_sc[(int64_t)yy * gx + xx];
+          if (w0 == 0xffffffffu) w0 = f;
+          else if (f != w0) mixed = true;
+          empty &= (f >> 30) == CELL_EMPTY;
+        }
+      if (empty) mask |= 1u << sb;   // (a sub-block without cells is never reached)
+    }
+    const uint32_t kind = w0 >> 30;
+    out[i] = (!mixed && (kind == CELL_EMPTY || kind == CELL_INTERIOR)) ? w0 : ((CELL_LIST << 30) | mask);
+  }
+}
+
 // pass 0 (ent == nullptr): cell_sc = resolved words, is_line[c] = 1 for line cells;
 // pass 1: the line entries at their scanned slots, and the LINE words
 template <bool LINES>
@@ -2015,6 +2055,14 @@ int make_shortcut(gm_pip_index* ix) {
   ix->dev.cell_sc = (const uint32_t*)p;
   ix->dev.line_ent = nullptr;
   ix->n_lines = 0;
+  {   // the join's coarse table: EMPTY until k_build_coarse_sc fills it
+    const int64_t nh = std::max<int64_t>(1, (int64_t)ix->dev.gxc * ((ix->dev.gy + (1 << CF_LOG) - 1) >> CF_LOG));
+    void* cp = nullptr;
+    GM_HIP(hipMalloc(&cp, (size_t)nh * 4));
+    ix->allocs.push_back(cp);
+    ix->dev.coarse_sc = (const uint32_t*)cp;
+    GM_HIP(hipMemsetD32Async((hipDeviceptr_t)cp, CELL_EMPTY << 30, (size_t)nh, s));
+  }
   if (ncell == 0) return GM_OK;
   const bool lines_ok = ix->arr_bytes[5] / 128 < (int64_t)SC_LINE;   // compact indices below the LINE bit
   void *fl = nullptr, *sl = nullptr, *part = nullptr;
@@ -2038,6 +2086,11 @@ int make_shortcut(gm_pip_index* ix) {
     ix->n_lines = nl;
     hipLaunchKernelGGL(k_build_shortcut<true>, dim3(g), dim3(256), 0, s, ix->dev, ncell, (uint32_t*)p, (int32_t*)fl,
                        (const int64_t*)sl, (uint4*)e);
+  }
+  if (!rc) {
+    const int gxc = ix->dev.gxc, gyc = (ix->dev.gy + (1 << CF_LOG) - 1) >> CF_LOG;
+    hipLaunchKernelGGL(k_build_coarse_sc, dim3((unsigned)std::min<int64_t>(65536, ((int64_t)gxc * gyc + 255) / 256)), dim3(256),
+                       0, s, (const uint32_t*)p, ix->dev.gx, ix->dev.gy, gxc, gyc, (uint32_t*)ix->dev.coarse_sc);
   }
   if (!rc && hipStreamSynchronize(s) != hipSuccess) rc = hip_fail(hipErrorLaunchFailure, "k_build_shortcut");
   cleanup();
