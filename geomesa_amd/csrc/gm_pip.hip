@@ -62,7 +62,8 @@ struct PipDev {
   const uint32_t* list_ent;      // entries in cell-word form (kind INTERIOR or BOUNDARY)
   const double* blob;            // boundary blobs, 16-byte aligned
   const uint32_t* cell_sc;       // per cell: the cell word with the boundary shortcuts applied (k_build_shortcut)
-  const uint32_t* coarse_sc;     // the join's coarse words over cell_sc; LIST words carry a sub-block EMPTY mask
+  const uint32_t* coarse_sc;     // the join's coarse words over cell_sc; LIST words carry sub-block masks
+  int32_t coarse_fmt;            // COARSE_EMPTY_MASK / COARSE_MAIN (see coarse_mask)
   const uint4* line_ent;         // line shortcuts, two uint4 each (see "Boundary shortcuts")
   double gx0, gy0, gx1, gy1, inv_cw, inv_ch;
   int32_t gx, gy, gxc;
@@ -311,12 +312,23 @@ __device__ __forceinline__ int line_locate(const uint4 e0, const uint4 e1, doubl
 // is built over cell_sc: EMPTY / INTERIOR(p) when all its fine cells carry that word, else LIST with
 // bit s of the payload set when all fine cells of sub-block s (4 x 4 sub-blocks of 2 x 2 fine
 // cells) are EMPTY: a point there needs no fine lookup.
+// With fewer than 2^14 polygons (COARSE_MAIN) the payload instead holds 8 sub-blocks of 4 x 2 fine
+// cells with an EMPTY bit and an INTERIOR-of-"main" bit each, main being the polygon of the coarse
+// cell's first INTERIOR fine cell (14 bits): 13.46 -> 13.27 ms on the counties.
 constexpr int SUB_LOG = CF_LOG - 2;
 static_assert(CF_LOG >= 2, "sub-block masks need at least 4 x 4 fine cells per coarse cell");
+enum : int32_t { COARSE_EMPTY_MASK = 0, COARSE_MAIN = 1 };
 
-__device__ __forceinline__ uint32_t coarse_mask(uint32_t w, int cx, int cy) {
+__device__ __forceinline__ uint32_t coarse_mask(uint32_t w, int cx, int cy, int32_t fmt) {
   if ((w >> 30) != CELL_LIST) return w;
-  const int sub = (((cy & ((1 << CF_LOG) - 1)) >> SUB_LOG) << 2) | ((cx & ((1 << CF_LOG) - 1)) >> SUB_LOG);
+  constexpr int CM = (1 << CF_LOG) - 1;
+  if (fmt == COARSE_MAIN) {   // 8 sub-blocks of 4 x 2: EMPTY mask | INTERIOR(main) mask << 8 | main << 16
+    const int sub = (((cy & CM) >> (CF_LOG - 2)) << 1) | ((cx & CM) >> (CF_LOG - 1));
+    if ((w >> sub) & 1u) return CELL_EMPTY << 30;
+    if ((w >> (8 + sub)) & 1u) return (CELL_INTERIOR << 30) | ((w >> 16) & 0x3fffu);
+    return w;
+  }
+  const int sub = (((cy & CM) >> SUB_LOG) << 2) | ((cx & CM) >> SUB_LOG);   // 16 sub-blocks of 2 x 2: EMPTY mask
   return ((w >> sub) & 1u) ? (CELL_EMPTY << 30) : w;
 }
 
@@ -505,7 +517,7 @@ __global__ __launch_bounds__(JTPB, GM_JOIN_WAVES) void k_pip_join(const double* 
 #ifdef GM_JX_NOCOARSE   // timing experiment only: no coarse lookup (every point EMPTY)
         cw[u] = CELL_EMPTY << 30;
 #else
-        cw[u] = coarse_mask(d.coarse_sc[(int64_t)(cys[u] >> CF_LOG) * d.gxc + (cxs[u] >> CF_LOG)], cxs[u], cys[u]);
+        cw[u] = coarse_mask(d.coarse_sc[(int64_t)(cys[u] >> CF_LOG) * d.gxc + (cxs[u] >> CF_LOG)], cxs[u], cys[u], d.coarse_fmt);
 #endif
       }
     }
@@ -783,7 +795,7 @@ __device__ __forceinline__ int triage_band(double x, double y, uint32_t w, const
 __device__ __forceinline__ uint32_t coarse_of(double x, double y, const PipDev& d) {
   if (!(x >= d.gx0 && x <= d.gx1 && y >= d.gy0 && y <= d.gy1)) return CELL_EMPTY << 30;
   const int cx = cell_of(x, d.gx0, d.inv_cw, d.gx), cy = cell_of(y, d.gy0, d.inv_ch, d.gy);
-  return coarse_mask(d.coarse_sc[(int64_t)(cy >> CF_LOG) * d.gxc + (cx >> CF_LOG)], cx, cy);
+  return coarse_mask(d.coarse_sc[(int64_t)(cy >> CF_LOG) * d.gxc + (cx >> CF_LOG)], cx, cy, d.coarse_fmt);
 }
 
 // per-block band histogram of the triaged points, band-major: hist[band * gridDim.x + block], and
@@ -1295,7 +1307,7 @@ __global__ __launch_bounds__(RTPB) void k_pip_relate(const int32_t* __restrict__
         if (p[u] >= 0 && p[u] < n_polys && x[u] >= d.gx0 && x[u] <= d.gx1 && y[u] >= d.gy0 && y[u] <= d.gy1) {
           cx[u] = cell_of(x[u], d.gx0, d.inv_cw, d.gx);
           cy[u] = cell_of(y[u], d.gy0, d.inv_ch, d.gy);
-          w[u] = d.coarse_word[(int64_t)(cy[u] >> CF_LOG) * d.gxc + (cx[u] >> CF_LOG)];
+          w[u] = coarse_mask(d.coarse_sc[(int64_t)(cy[u] >> CF_LOG) * d.gxc + (cx[u] >> CF_LOG)], cx[u], cy[u], d.coarse_fmt);
         }
       }
 #pragma unroll
@@ -1934,7 +1946,7 @@ __device__ int analyze_cell(const PipDev& d, int64_t c, uint32_t w, uint32_t* wo
 
 // coarse_sc (see coarse_mask) over the resolved words cell_sc
 __global__ __launch_bounds__(256) void k_build_coarse_sc(const uint32_t* __restrict__ cell_sc, int gx, int gy, int gxc,
-                                                         int gyc, uint32_t* __restrict__ out) {
+                                                         int gyc, int32_t fmt, uint32_t* __restrict__ out) {
   const int64_t n = (int64_t)gxc * gyc;
   constexpr int CF = 1 << CF_LOG, SB = 1 << SUB_LOG;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
@@ -1954,6 +1966,27 @@ __global__ __launch_bounds__(256) void k_build_coarse_sc(const uint32_t* __restr
       if (empty) mask |= 1u << sb;   // (a sub-block without cells is never reached)
     }
     const uint32_t kind = w0 >> 30;
+    if (fmt == COARSE_MAIN) {   // 8 sub-blocks of 4 x 2: EMPTY and INTERIOR(main) masks, main = first INTERIOR polygon
+      uint32_t em = 0, im = 0, main = 0xffffffffu;
+      for (int yy = yc * CF; yy < min(gy, (yc + 1) * CF) && main == 0xffffffffu; ++yy)
+        for (int xx = xc * CF; xx < min(gx, (xc + 1) * CF); ++xx) {
+          const uint32_t f = cell_sc[(int64_t)yy * gx + xx];
+          if ((f >> 30) == CELL_INTERIOR) { main = f & 0x3fffffffu; break; }
+        }
+      for (int sb = 0; sb < 8; ++sb) {
+        const int x0 = xc * CF + (sb & 1) * (CF / 2), y0 = yc * CF + (sb >> 1) * (CF / 4);
+        bool empty = true, inner = main < (1u << 14);
+        for (int yy = y0; yy < min(gy, y0 + CF / 4); ++yy)
+          for (int xx = x0; xx < min(gx, x0 + CF / 2); ++xx) {
+            const uint32_t f = cell_sc[(int64_t)yy * gx + xx];
+            empty &= (f >> 30) == CELL_EMPTY;
+            inner &= f == ((CELL_INTERIOR << 30) | main);
+          }
+        if (empty) em |= 1u << sb;
+        else if (inner) im |= 1u << sb;
+      }
+      mask = em | (im << 8) | ((main < (1u << 14) ? main : 0u) << 16);
+    }
     out[i] = (!mixed && (kind == CELL_EMPTY || kind == CELL_INTERIOR)) ? w0 : ((CELL_LIST << 30) | mask);
   }
 }
@@ -2055,6 +2088,9 @@ int make_shortcut(gm_pip_index* ix) {
   ix->dev.cell_sc = (const uint32_t*)p;
   ix->dev.line_ent = nullptr;
   ix->n_lines = 0;
+  ix->dev.coarse_fmt = ix->n_polys < (1 << 14) ? COARSE_MAIN : COARSE_EMPTY_MASK;
+  if (const char* f = getenv("GM_PIP_COARSE_FMT")) ix->dev.coarse_fmt = atoi(f) ? COARSE_MAIN : COARSE_EMPTY_MASK;   // tests
+  if (ix->n_polys >= (1 << 14)) ix->dev.coarse_fmt = COARSE_EMPTY_MASK;   // main ids need 14 bits
   {   // the join's coarse table: EMPTY until k_build_coarse_sc fills it
     const int64_t nh = std::max<int64_t>(1, (int64_t)ix->dev.gxc * ((ix->dev.gy + (1 << CF_LOG) - 1) >> CF_LOG));
     void* cp = nullptr;
@@ -2090,7 +2126,8 @@ int make_shortcut(gm_pip_index* ix) {
   if (!rc) {
     const int gxc = ix->dev.gxc, gyc = (ix->dev.gy + (1 << CF_LOG) - 1) >> CF_LOG;
     hipLaunchKernelGGL(k_build_coarse_sc, dim3((unsigned)std::min<int64_t>(65536, ((int64_t)gxc * gyc + 255) / 256)), dim3(256),
-                       0, s, (const uint32_t*)p, ix->dev.gx, ix->dev.gy, gxc, gyc, (uint32_t*)ix->dev.coarse_sc);
+                       0, s, (const uint32_t*)p, ix->dev.gx, ix->dev.gy, gxc, gyc, ix->dev.coarse_fmt,
+                       (uint32_t*)ix->dev.coarse_sc);
   }
   if (!rc && hipStreamSynchronize(s) != hipSuccess) rc = hip_fail(hipErrorLaunchFailure, "k_build_shortcut");
   cleanup();

@@ -73,3 +73,23 @@ def test_relate_at_shortcut_thresholds(gpu, oracle):
     exp = np.array([ops.locate(int(p), x, y) for p, x, y in zip(near, px, py)], np.uint8)
     assert np.array_equal(loc, exp)
     assert (exp == 1).sum() > 0 and (exp == 2).sum() > 0 and (exp == 0).sum() > 0
+
+
+@pytest.mark.parametrize("fmt", ["0", "1"])
+def test_join_coarse_mask_formats(gpu, oracle, fmt, monkeypatch):
+    """Both layouts of the join's coarse sub-block masks (gm_pip.hip coarse_mask): EMPTY bits of 16
+    sub-blocks (any polygon count) and EMPTY / INTERIOR(main) bits of 8 (fewer than 2^14 polygons),
+    forced through GM_PIP_COARSE_FMT at index build, against the oracle on random and boundary points."""
+    from geomesa_amd.join import PolygonIndex, synthetic_counties, synthetic_points
+    monkeypatch.setenv("GM_PIP_COARSE_FMT", fmt)
+    ps = synthetic_counties(20, 10)
+    px, py = synthetic_points(300_000, seed=9)
+    tx, ty = threshold_points(ps, stride=5)
+    px, py = np.concatenate([px, tx]), np.concatenate([py, ty])
+    opt, opl = oracle.OraclePolySet(*ps.to_arrays()).join(px, py, nthreads=16)
+    exp = np.stack([opt, opl.astype(np.int64)], 1)
+    exp = exp[np.lexsort((exp[:, 1], exp[:, 0]))]
+    ix = PolygonIndex(ps)
+    for mode in ("direct", "partitioned"):
+        pt, pl = ix.join(px, py, mode=mode)
+        assert np.array_equal(_sorted_pairs(pt, pl), exp), (fmt, mode)
