@@ -56,6 +56,19 @@ int copy_d2h(gm_ctx* ctx, void* host, const void* dev, size_t bytes) {
   return GM_OK;
 }
 
+bool host_pinned(const void* p) { return is_pinned(p); }
+
+int ctx_copy_stream(gm_ctx* ctx) {
+  if (ctx->copy_stream) return GM_OK;
+  GM_HIP(hipSetDevice(ctx->device));
+  GM_HIP(hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking));
+  for (int k = 0; k < 2; ++k) {
+    GM_HIP(hipEventCreateWithFlags(&ctx->ev_ready[k], hipEventDisableTiming));
+    GM_HIP(hipEventCreateWithFlags(&ctx->ev_copied[k], hipEventDisableTiming));
+  }
+  return GM_OK;
+}
+
 int ctx_workspace(gm_ctx* ctx, int slot, size_t bytes, void** p) {
   if (ctx->ws_cap[slot] < bytes) {
     GM_HIP(hipStreamSynchronize(ctx->stream));
@@ -209,6 +222,12 @@ int gm_ctx_destroy(gm_ctx* c) {
     if (w) (void)hipFree(w);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
+  if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
+  for (int k = 0; k < 2; ++k) {
+    if (c->ev_ready[k]) (void)hipEventDestroy(c->ev_ready[k]);
+    if (c->ev_copied[k]) (void)hipEventDestroy(c->ev_copied[k]);
+  }
+  if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
   if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
   return GM_OK;
@@ -233,6 +252,10 @@ int gm_ctx_set_param(gm_ctx* c, int param, int64_t value) {
       if (value != 0 && value != 1) return GM_E_INVALID;
       c->index_build = value;
       return GM_OK;
+    case GM_PARAM_RANGES_CHUNK:
+      if (value < 0) return GM_E_INVALID;
+      c->ranges_chunk = value;
+      return GM_OK;
     default:
       gm::set_error("gm_ctx_set_param: unknown parameter");
       return GM_E_INVALID;
@@ -244,6 +267,7 @@ int gm_ctx_get_param(gm_ctx* c, int param, int64_t* value) {
   switch (param) {
     case GM_PARAM_JOIN_CHUNK: *value = c->join_chunk; return GM_OK;
     case GM_PARAM_INDEX_BUILD: *value = c->index_build; return GM_OK;
+    case GM_PARAM_RANGES_CHUNK: *value = c->ranges_chunk; return GM_OK;
     default: return GM_E_INVALID;
   }
 }

@@ -23,6 +23,9 @@ struct gm_ctx {
   int64_t join_chunk = 0;          // GM_PARAM_JOIN_CHUNK: rows per join pass (0 = each strategy's default)
   int64_t index_build = 0;         // GM_PARAM_INDEX_BUILD: 0 = device build of the join index, 1 = host build
   int64_t ranges_hint = 0;         // largest batched-ranges output seen (sizes the device batch buffer)
+  int64_t ranges_chunk = 0;        // GM_PARAM_RANGES_CHUNK: queries per pipelined chunk (0 = default)
+  hipStream_t copy_stream = nullptr;   // result copies overlapping the next chunk's kernels (lazy)
+  hipEvent_t ev_ready[2] = {nullptr, nullptr}, ev_copied[2] = {nullptr, nullptr};
 };
 
 namespace gm {
@@ -58,6 +61,8 @@ int copy_h2d(gm_ctx* ctx, void* dev, const void* host, size_t bytes);
 // (0.7-6 s stalls between launches).  slot: 0 = range batches, 1 = sort, 2 = scans, 3 = join.
 enum : int { WS_RANGES = 0, WS_SORT = 1, WS_SCAN = 2, WS_JOIN = 3 };
 int ctx_workspace(gm_ctx* ctx, int slot, size_t bytes, void** p);
+bool host_pinned(const void* p);
+int ctx_copy_stream(gm_ctx* ctx);   // creates copy_stream and its events on first use
 
 // reset the error summary before a call that reports one
 int begin_summary(gm_ctx* ctx, gm_batch_status* summary);

@@ -801,13 +801,15 @@ int to_dev(gm_ctx* ctx, const T* h, size_t n, T** d) {
 // sorted in LDS), chunked only by a memory budget and launched back to back (the chunks reuse one
 // stream-ordered workspace, no host round trip); the merged-range scratch aliases the frontier.
 // Phase 2 re-runs the queries that overflowed it (status QS_CAPACITY) with the worst-case caps.
-// Then the counts are scanned on the device, the batch buffer is gathered into query order and the
-// result comes back in one copy.
+// Then the counts are scanned on the device, the batch buffer is gathered into query order and
+// `finish` takes the result.  run_batch does this for queries [q_base, q_base + nq); the per-query
+// arrays are indexed by absolute query id in the kernels (their base pointers are offset).
 constexpr int64_t P1CAP = LDS_SORT;
 
-template <class LaunchFn>
-int run_ranges(gm_ctx* ctx, int64_t nq, int64_t fcap, int64_t rcap, size_t felem, LaunchFn launch, int64_t* out_off,
-               gm_range* out, int64_t cap, int64_t* needed, int32_t* query_status) {
+// finish(total, dbuf, dstart, doff): query-order gather of the batch buffer and the copy out
+template <class LaunchFn, class FinishFn>
+int run_batch(gm_ctx* ctx, int64_t q_base, int64_t nq, int64_t fcap, int64_t rcap, size_t felem, LaunchFn& launch,
+              int64_t* out_off, int64_t cap, int64_t* needed, int32_t* query_status, FinishFn finish) {
   hipStream_t s = ctx->stream;
   rcap = next_pow2(std::max<int64_t>(rcap, 16));
   auto al = [](size_t v) { return (v + 15) & ~(size_t)15; };
@@ -848,7 +850,7 @@ int run_ranges(gm_ctx* ctx, int64_t nq, int64_t fcap, int64_t rcap, size_t felem
       dtotal = (unsigned long long*)p;
     }
     GM_HIP(hipMemsetAsync(dtotal, 0, 8, s));
-    // one pass over a query list with caps (fc, rc); qmap null = queries [0, count)
+    // one pass over a query list with caps (fc, rc); qmap null = queries [q_base, q_base + count)
     auto pass = [&](int64_t count, const int32_t* qmap, int64_t fc, int64_t rc) -> int {
       const bool lds_sort = rc <= LDS_SORT;
       const bool alias = (int64_t)felem * 2 * fc >= rc * (int64_t)sizeof(gm_range);   // merged output in F|G
@@ -886,8 +888,10 @@ int run_ranges(gm_ctx* ctx, int64_t nq, int64_t fcap, int64_t rcap, size_t felem
       }
       for (int64_t q0 = 0; q0 < count; q0 += chunk) {
         const int64_t m = std::min(chunk, count - q0);
-        const BatchOut bo{qmap ? qmap + q0 : nullptr, ocap, dbuf, dcap, dtotal, dstart, dcount, dstatus};
-        launch(qmap ? 0 : q0, m, fc, rc, fa, rlo, rhi, rcb, gkey, gidx, ws, bo);
+        // per-query arrays offset so that the kernels index them by absolute query id
+        const BatchOut bo{qmap ? qmap + q0 : nullptr, ocap, dbuf, dcap, dtotal, dstart - q_base, dcount - q_base,
+                          dstatus - q_base};
+        launch(qmap ? 0 : q_base + q0, m, fc, rc, fa, rlo, rhi, rcb, gkey, gidx, ws, bo);
         GM_CHECK_LAUNCH();
       }
       return GM_OK;
@@ -899,7 +903,7 @@ int run_ranges(gm_ctx* ctx, int64_t nq, int64_t fcap, int64_t rcap, size_t felem
       if (rc) return rc;
       std::vector<int32_t> redo;
       for (int64_t i = 0; i < nq; ++i)
-        if (stats[i] == QS_CAPACITY) redo.push_back((int32_t)i);
+        if (stats[i] == QS_CAPACITY) redo.push_back((int32_t)(q_base + i));
       if (!redo.empty()) {
         rc = copy_h2d(ctx, dqmap, redo.data(), redo.size() * 4);
         if (!rc) rc = pass((int64_t)redo.size(), dqmap, fcap, rcap);
@@ -921,18 +925,80 @@ int run_ranges(gm_ctx* ctx, int64_t nq, int64_t fcap, int64_t rcap, size_t felem
     if (query_status) memcpy(query_status, stats.data(), (size_t)nq * 4);
     if (needed) *needed = total;
     if (total > cap) return GM_E_CAPACITY;
-    if (total > 0) {
-      void* dout = nullptr;   // the range scratch is free again
-      rc = ctx_workspace(ctx, WS_RANGES, (size_t)total * sizeof(gm_range), &dout);
-      if (rc) return rc;
-      hipLaunchKernelGGL(k_gather_ranges, dim3((unsigned)std::min<int64_t>(nq, 65536)), dim3(RTPB), 0, s, dbuf,
-                         dstart, doff, nq, (gm_range*)dout);
-      GM_CHECK_LAUNCH();
-      rc = copy_d2h(ctx, out, dout, (size_t)total * sizeof(gm_range));
-      if (rc) return rc;
-    }
-    return GM_OK;
+    return total > 0 ? finish(total, dbuf, (const int64_t*)dstart, (const int64_t*)doff, nq) : GM_OK;
   }
+}
+
+// Batched ranges.  With pinned host output and enough queries, the queries run in chunks and chunk
+// k's result copy (a second stream) overlaps chunk k + 1's kernels: the copy back of 10^7-10^8
+// ranges costs as much as their computation.  The output is identical either way.
+template <class LaunchFn>
+int run_ranges(gm_ctx* ctx, int64_t nq, int64_t fcap, int64_t rcap, size_t felem, LaunchFn launch, int64_t* out_off,
+               gm_range* out, int64_t cap, int64_t* needed, int32_t* query_status) {
+  hipStream_t s = ctx->stream;
+  int64_t qc = ctx->ranges_chunk > 0 ? ctx->ranges_chunk : (nq < 16384 ? nq : std::max<int64_t>(8192, (nq + 7) / 8));
+  if (qc >= nq || !out || !host_pinned(out)) {   // one batch: gather into scratch, one copy
+    return run_batch(ctx, 0, nq, fcap, rcap, felem, launch, out_off, cap, needed, query_status,
+                     [&](int64_t total, const gm_range* dbuf, const int64_t* dstart, const int64_t* doff, int64_t n) -> int {
+                       void* dout = nullptr;   // the range scratch is free again
+                       int rc = ctx_workspace(ctx, WS_RANGES, (size_t)total * sizeof(gm_range), &dout);
+                       if (rc) return rc;
+                       hipLaunchKernelGGL(k_gather_ranges, dim3((unsigned)std::min<int64_t>(n, 65536)), dim3(RTPB), 0, s,
+                                          dbuf, dstart, doff, n, (gm_range*)dout);
+                       GM_CHECK_LAUNCH();
+                       return copy_d2h(ctx, out, dout, (size_t)total * sizeof(gm_range));
+                     });
+  }
+  int rc = ctx_copy_stream(ctx);
+  if (rc) return rc;
+  // two device result buffers, reused every other chunk once their copy is done (ev_copied)
+  gm_range* dres[2] = {nullptr, nullptr};
+  int64_t dres_cap[2] = {0, 0};
+  bool used[2] = {false, false};
+  auto release = [&]() {
+    (void)hipStreamSynchronize(ctx->copy_stream);
+    for (int k = 0; k < 2; ++k) if (dres[k]) (void)hipFree(dres[k]);
+  };
+  int64_t base = 0;
+  bool over = false;
+  int k = 0;
+  std::vector<int64_t> off_c;
+  for (int64_t c0 = 0; c0 < nq; c0 += qc, k ^= 1) {
+    const int64_t m = std::min(qc, nq - c0);
+    off_c.assign((size_t)m + 1, 0);
+    int64_t tot = 0;
+    rc = run_batch(ctx, c0, m, fcap, rcap, felem, launch, off_c.data(), INT64_MAX / 32, &tot,
+                   query_status ? query_status + c0 : nullptr,
+                   [&](int64_t total, const gm_range* dbuf, const int64_t* dstart, const int64_t* doff, int64_t n) -> int {
+                     if (over || base + total > cap) { over = true; return GM_OK; }   // capacity: counting only
+                     if (used[k]) GM_HIP(hipStreamWaitEvent(s, ctx->ev_copied[k], 0));   // its last copy is done
+                     if (dres_cap[k] < total) {
+                       GM_HIP(hipStreamSynchronize(s));
+                       if (dres[k]) (void)hipFree(dres[k]);
+                       dres[k] = nullptr;
+                       GM_HIP(hipMalloc(&dres[k], (size_t)total * sizeof(gm_range)));
+                       dres_cap[k] = total;
+                     }
+                     hipLaunchKernelGGL(k_gather_ranges, dim3((unsigned)std::min<int64_t>(n, 65536)), dim3(RTPB), 0, s,
+                                        dbuf, dstart, doff, n, dres[k]);
+                     GM_CHECK_LAUNCH();
+                     GM_HIP(hipEventRecord(ctx->ev_ready[k], s));
+                     GM_HIP(hipStreamWaitEvent(ctx->copy_stream, ctx->ev_ready[k], 0));
+                     GM_HIP(hipMemcpyAsync(out + base, dres[k], (size_t)total * sizeof(gm_range), hipMemcpyDeviceToHost,
+                                           ctx->copy_stream));
+                     GM_HIP(hipEventRecord(ctx->ev_copied[k], ctx->copy_stream));
+                     used[k] = true;
+                     return GM_OK;
+                   });
+    if (rc) { release(); return rc; }
+    for (int64_t i = 0; i <= m; ++i) out_off[c0 + i] = base + off_c[(size_t)i];
+    base += tot;
+  }
+  release();
+  if (hipGetLastError() != hipSuccess) return hip_fail(hipErrorLaunchFailure, "batched ranges copy");
+  if (needed) *needed = base;
+  ctx->ranges_hint = std::max(ctx->ranges_hint, std::min(base, cap) / std::max<int64_t>(1, (nq + qc - 1) / qc));
+  return base > cap ? GM_E_CAPACITY : GM_OK;
 }
 
 inline int stop_of(int max_ranges) { return max_ranges <= 0 ? INT32_MAX : max_ranges; }

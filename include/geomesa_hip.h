@@ -95,6 +95,10 @@ const char* gm_last_error(void);
                                    values only add passes -- the pair set never changes */
 #define GM_PARAM_INDEX_BUILD 2  /* where gm_pip_index_create builds the join index: 0 (default) = on the
                                    device (same arrays, byte for byte), 1 = on the host */
+#define GM_PARAM_RANGES_CHUNK 3 /* queries per chunk of a batched ranges call whose output is pinned host
+                                   memory: chunk k's result copy runs while chunk k + 1 computes (0 =
+                                   default: one batch below 16384 queries, else about nq / 8 per chunk);
+                                   the output never changes */
 int gm_ctx_set_param(gm_ctx* ctx, int param, int64_t value);
 int gm_ctx_get_param(gm_ctx* ctx, int param, int64_t* value);
 /* device memory helpers for callers without their own allocator (e.g. a JNI shim) */

@@ -357,3 +357,44 @@ def test_xz2_kats_gpu(gpu):  # geomesa-z3/src/test/.../curve/XZ2SFCTest.scala:24
     idx = as_np(sfc.index(g[:, 0], g[:, 1], g[:, 2], g[:, 3]))
     rr = sfc.ranges([(45.0, 23.0, 48.0, 27.0)])
     assert all(hit(rr, int(v)) for v in idx)
+
+
+@pytest.mark.parametrize("kind", ["xz2", "xz3", "z3"])
+def test_ranges_pipelined_chunks(gpu, oracle, kind):
+    """Batched ranges into pinned host memory in pipelined query chunks (GM_PARAM_RANGES_CHUNK): the
+    chunk results copied back on a second stream while the next chunk runs give exactly the
+    one-batch offsets, ranges and statuses, also through a capacity retry (gm_ranges.hip run_ranges)."""
+    import ctypes
+    from geomesa_amd import _lib
+    from geomesa_amd import ranges as R
+    from geomesa_amd.curve import XZ2SFC, XZ3SFC, Z3SFC
+    ctx = _lib.context()
+    if kind == "z3":
+        qs = [([b], [(int(t[0]), int(t[1]))]) for b, t in ranges_queries(70, seed=29)]
+        fn, args, nq, cap = R.prepare_z3(Z3SFC("week"), qs, 64, 300)
+    else:
+        d = 2 if kind == "xz2" else 3
+        sfc = XZ2SFC(12) if d == 2 else XZ3SFC(12, "week")
+        qs = [[b] if d == 2 else [(b[0], b[1], float(t[0]), b[2], b[3], float(t[1]))]
+              for b, t in ranges_queries(70, seed=31)]
+        off, w = R._windows(qs, d)
+        nq, cap = len(qs), len(qs) * 4096
+        fn = ctx.lib.gm_xz2_ranges if d == 2 else ctx.lib.gm_xz3_ranges
+        args = (ctx.handle, nq, off.ctypes.data, w.ctypes.data, 12, 300) if d == 2 else \
+            (ctx.handle, nq, off.ctypes.data, w.ctypes.data, 12, sfc.period, 300)
+    o1, r1, s1 = R.call_raw(fn, args, nq, cap)                       # pageable output: one batch
+    r1 = r1[:int(o1[-1])].copy()
+    try:
+        for chunk in (1, 7, 64):
+            ctx.set_param(_lib.GM_PARAM_RANGES_CHUNK, chunk)
+            o2, r2, s2 = R.call_raw(fn, args, nq, cap, pinned=True)
+            assert np.array_equal(o1, o2) and np.array_equal(s1, s2), chunk
+            assert np.array_equal(r1, r2[:int(o2[-1])]), chunk
+            # a capacity below the total: GM_E_CAPACITY with the exact need, then the retry
+            o3, r3, _ = R.call_raw(fn, args, nq, max(1, int(o1[-1]) // 3), pinned=True)
+            assert np.array_equal(o1, o3) and np.array_equal(r1, r3[:int(o3[-1])]), chunk
+    finally:
+        ctx.set_param(_lib.GM_PARAM_RANGES_CHUNK, 0)
+    if kind == "xz2":   # and the oracle, for one query
+        got = [(int(r["lower"]), int(r["upper"]), bool(r["contained"])) for r in r1[int(o1[0]):int(o1[1])]]
+        assert got == [(int(a), int(b), bool(c)) for a, b, c in oracle.xz2_ranges(qs[0], max_ranges=300)]
