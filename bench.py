@@ -608,7 +608,8 @@ def main():
         qlo, qhi = shard_bounds(nq, dist.rank, dist.world)
         wl, wl3 = np.ascontiguousarray(win[qlo:qhi]), np.ascontiguousarray(win3[qlo:qhi])
         woff = np.arange(qhi - qlo + 1, dtype=np.int32)
-        note = ("C-ABI call incl. H2D of the windows and D2H of the ranges (pinned host output), queries "
+        note = ("C-ABI call incl. H2D of the windows and D2H of the ranges (pinned host output: query chunks "
+                "pipelined with their result copies), queries "
                 "sharded over the ranks with offsets + ranges gathered to rank 0; 100k %s query windows "
                 "(0.01-20 deg%s), maxRanges 2000, g = 12")
         m = ranges_batch(dist, lib.gm_xz2_ranges, (h, qhi - qlo, woff.ctypes.data, wl.ctypes.data, 12, 2000),
