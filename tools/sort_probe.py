@@ -43,6 +43,9 @@ def main(n=250_000_000, sharded=False):
         e1.record()
         torch.cuda.synchronize()
         ts.append(e0.elapsed_time(e1))
+    if os.environ.get("GM_SORT_PROBE_NOCHECK"):   # timing-only library variants write partial output
+        print("sort %d rows: best %.2f ms, mean %.2f ms, unchecked" % (n, min(ts), sum(ts) / len(ts)), flush=True)
+        return
     # checks: output = input[perm], keys nondecreasing in (shard, bin unsigned, z unsigned) order
     ok = bool(torch.equal(ob, b[perm])) and bool(torch.equal(oz, z[perm]))
     hi = (ob.to(torch.int64) & 0xffff) | ((osh.to(torch.int64) << 16) if sharded else 0)
