@@ -42,6 +42,8 @@ def timed(name, fn, args, nq, reps=3):
 
 def main(nq=100_000):
     ctx = _lib.context()
+    if os.environ.get("GM_RANGES_CHUNK"):   # pipelined chunk size (GM_PARAM_RANGES_CHUNK) for sweeps
+        ctx.set_param(_lib.GM_PARAM_RANGES_CHUNK, int(os.environ["GM_RANGES_CHUNK"]))
     lib, h = ctx.lib, ctx.handle
     win, win3 = windows(nq)
     woff = np.arange(nq + 1, dtype=np.int32)
