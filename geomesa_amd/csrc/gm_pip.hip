@@ -1285,7 +1285,7 @@ __global__ __launch_bounds__(RTPB) void k_pip_relate(const int32_t* __restrict__
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   double* qx = s_x[wave]; double* qy = s_y[wave];
   int64_t* qr = s_row[wave]; uint32_t* qe = s_e[wave]; int32_t* qp = s_p[wave];
-  int qn = 0;
+  int qn = 0, qg = 0;   // queued line-entry items (from slot 0 up) and blob items (from RQCAP - 1 down)
   const int64_t wstep = (int64_t)gridDim.x * NW * (64 * RILP);
   for (int64_t w0 = ((int64_t)blockIdx.x * NW + wave) * (64 * RILP);; w0 += wstep) {
     const bool have = w0 < n;   // uniform per wave
@@ -1337,19 +1337,26 @@ __global__ __launch_bounds__(RTPB) void k_pip_relate(const int32_t* __restrict__
           }
         }
         if (row[u] < n && !queue) loc[row[u]] = r;
-        const uint64_t m = __ballot(queue && row[u] < n);
-        if (queue && row[u] < n) {
-          const int o = qn + lanes_below(m);
+        // line-entry items and blob items on separate ends, so an evaluation round runs one kind
+        const bool ln = (e & (BLOB_COMPACT | SC_LINE)) == (BLOB_COMPACT | SC_LINE) && d.line_ent;
+        const bool qv = queue && row[u] < n;
+        const uint64_t ml = __ballot(qv && ln), mb = __ballot(qv && !ln);
+        if (qv) {
+          const int o = ln ? qn + lanes_below(ml) : RQCAP - 1 - qg - lanes_below(mb);
           qx[o] = x[u]; qy[o] = y[u]; qr[o] = row[u]; qe[o] = e; qp[o] = p[u];
         }
-        qn += __popcll(m);
+        qn += __popcll(ml);
+        qg += __popcll(mb);
       }
     }
     // walk min(qn, 64) queued blobs when the queue holds a full wave, and drain it at the end
-    while (qn >= 64 || (!have && qn > 0)) {
+    // (< 64 queued before a step's <= 64 * RILP rows, so both ends fit RQCAP; the fuller kind goes
+    // first, which leaves < 64 again)
+    while (qn + qg >= 64 || (!have && qn + qg > 0)) {
       wave_lds_sync();
-      const int kq = qn < 64 ? qn : 64;
-      const int slot = qn - kq + lane;
+      const bool lines = qn >= qg;
+      const int kq = min(lines ? qn : qg, 64);
+      const int slot = lines ? qn - kq + lane : RQCAP - qg + lane;
       if (lane < kq) {
         const uint32_t ref = qe[slot] & 0x3fffffffu;
         const double ex = qx[slot], ey = qy[slot];
@@ -1358,7 +1365,8 @@ __global__ __launch_bounds__(RTPB) void k_pip_relate(const int32_t* __restrict__
         loc[qr[slot]] = (uint8_t)(pl == qp[slot] ? l : LOC_EXTERIOR);
       }
       wave_lds_sync();
-      qn -= kq;
+      if (lines) qn -= kq;
+      else qg -= kq;
     }
     if (!have) break;
   }
