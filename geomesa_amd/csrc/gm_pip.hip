@@ -590,9 +590,9 @@ __global__ __launch_bounds__(JTPB, GM_JOIN_WAVES) void k_pip_join(const double* 
           if (blob) qi[qn + lanes_below(mq)] = make_uint2(eid, e & 0x3fffffffu);
           qn += __popcll(mq);
         } else {
-          // compact blobs stack up from slot 0, generic blobs down from slot QCAP - 1, so every
-          // evaluation round below runs one kind of blob code on all its lanes
-          const bool cmp = (e & BLOB_COMPACT) != 0;
+          // line-entry items stack up from slot 0, blob items (compact and generic, rare once the
+          // shortcuts apply) down from slot QCAP - 1, so an evaluation round runs one kind of code
+          const bool cmp = (e & (BLOB_COMPACT | SC_LINE)) == (BLOB_COMPACT | SC_LINE) && d.line_ent;
           const uint64_t mc = __ballot(blob && cmp), mg = __ballot(blob && !cmp);
           if (blob) {
             const int o = cmp ? qn + lanes_below(mc) : QCAP - 1 - qg - lanes_below(mg);
@@ -626,23 +626,8 @@ __global__ __launch_bounds__(JTPB, GM_JOIN_WAVES) void k_pip_join(const double* 
             poly = 0; hit = false;
           } else
 #endif
-#ifdef GM_JX_NOGEN    // timing experiment only: generic blobs not evaluated
-          if (!cmp) {
-            poly = 0; hit = false;
-          } else
-#endif
-#ifdef GM_JX_NOCMP    // timing experiment only: compact blobs not evaluated
-          if (cmp) {
-            poly = 0; hit = false;
-          } else
-#endif
-          if (cmp) {
+          {   // one kind per round (cmp: line entries, else compact / generic blobs); item_locate takes any ref
             hit = join_hit(d.op, item_locate(d, ref, ex, ey, poly));
-          } else {
-            const double* b = d.blob + 2 * (uint64_t)ref;
-            const int2 h = *(const int2*)b;
-            poly = h.x;
-            hit = join_hit(d.op, blob_locate(d, b, h, ex, ey));
           }
         }
         wave_lds_sync();
