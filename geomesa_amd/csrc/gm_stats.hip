@@ -154,7 +154,10 @@ __global__ __launch_bounds__(HTPB) void k_z3_hist_lds(const double* __restrict__
     const lv2* t2 = (const lv2*)t;
     const int64_t np = a.n >> 1;
     // software-pipelined: the next HU pairs per lane are in flight while the current ones are binned
-    constexpr int HU = 2;
+#ifndef GM_HIST_HU
+#define GM_HIST_HU 2
+#endif
+    constexpr int HU = GM_HIST_HU;
     dv2 xa[HU], ya[HU];
     lv2 ta[HU];
     int64_t p = (int64_t)blockIdx.x * HTPB + threadIdx.x;
