@@ -1255,7 +1255,10 @@ __global__ __launch_bounds__(RTPB) void k_list_poly(PipDev d, int64_t n, int32_t
 // a list without polygon poly[i] (list_poly search); a boundary entry of the row's polygon is queued
 // in LDS and the wave walks 64 queued blobs at a time (one per lane), as the join does -- every row
 // writes its location exactly once.
-constexpr int RILP = 2;
+#ifndef GM_RILP
+#define GM_RILP 2
+#endif
+constexpr int RILP = GM_RILP;
 constexpr int RQCAP = 64 * (RILP + 1);
 
 __global__ __launch_bounds__(RTPB) void k_pip_relate(const int32_t* __restrict__ poly, const double* __restrict__ px,
