@@ -7,8 +7,12 @@
 namespace gm {
 
 constexpr int FTPB = 256;             // threads per block
-constexpr int FELEMS = 8;             // rows per thread per block
-constexpr int FROWS = FTPB * FELEMS;  // rows per block (2048) -> 64 mask words
+#ifndef GM_FELEMS
+#define GM_FELEMS 16  // sweep (tools/filter_ab.sh, z3filter_scan ms per 1B rows): 4 2.27, 8 1.81-1.94, 16 1.68-1.80, 32 1.92-1.94
+#endif
+constexpr int FELEMS = GM_FELEMS;     // rows per thread per block
+static_assert(FELEMS % 2 == 0 && FELEMS >= 2, "pair layout");
+constexpr int FROWS = FTPB * FELEMS;  // rows per block (4096) -> 64 mask words
 
 // ------------------------------------------------------------------ vectorised pass A
 // The scalar kernels of gm_filter.hip move 2 B (bin) and 8 B (z) per lane per load instruction; on gfx950 narrow
@@ -17,7 +21,7 @@ constexpr int FROWS = FTPB * FELEMS;  // rows per block (2048) -> 64 mask words
 // (z, x, y, t) and one 4-B load of the two bins, and pair p of lane l in step u sits at
 // block_base + u*256 + l, so every wave instruction reads one contiguous 1 KiB run.  A wave step
 // covers 128 rows: ballot(row 2l) and ballot(row 2l+1) interleave bit by bit into the two 64-bit
-// mask words of those rows.  A block still covers FROWS = 2048 rows (4 steps), so block_counts,
+// mask words of those rows.  A block still covers FROWS = 4096 rows (8 steps), so block_counts,
 // the count scan and k_mask_to_ids are shared with the scalar kernels.
 typedef short sv2 __attribute__((ext_vector_type(2)));
 constexpr int FPAIRS = FELEMS / 2;   // pair steps per lane
