@@ -391,9 +391,20 @@ __global__ __launch_bounds__(TPB) void k_xz3_index_v(const dv2* __restrict__ xmi
 
 // ------------------------------------------------------------------ host-side launchers
 
-constexpr int UNROLL_KEY = 4;
-constexpr int UNROLL_INV = 4;
-constexpr int UNROLL_XZ = 2;
+// pairs per lane; tuning sweeps build variants with -DGM_UNROLL_INV=... (tools/jx_build.sh, tools/curve_ab.sh).
+// The key kernel's LDS bin staging fixes UNROLL_KEY at 4; XZ 1 / 2 / 4 were within noise.
+#ifndef GM_UNROLL_KEY
+#define GM_UNROLL_KEY 4
+#endif
+#ifndef GM_UNROLL_INV
+#define GM_UNROLL_INV 2   // 1 / 2 / 4 / 8: profiles/r2_curve_unroll_sweep.txt (2 beat 4 in every same-box pair)
+#endif
+#ifndef GM_UNROLL_XZ
+#define GM_UNROLL_XZ 2
+#endif
+constexpr int UNROLL_KEY = GM_UNROLL_KEY;
+constexpr int UNROLL_INV = GM_UNROLL_INV;
+constexpr int UNROLL_XZ = GM_UNROLL_XZ;
 
 inline unsigned stride_grid(int64_t n) {
   int64_t b = (n + TPB - 1) / TPB;
