@@ -405,6 +405,10 @@ __global__ __launch_bounds__(TPB) void k_xz3_index_v(const dv2* __restrict__ xmi
 constexpr int UNROLL_KEY = GM_UNROLL_KEY;
 constexpr int UNROLL_INV = GM_UNROLL_INV;
 constexpr int UNROLL_XZ = GM_UNROLL_XZ;
+#ifndef GM_UNROLL_Z2
+#define GM_UNROLL_Z2 2   // 2 / 4 / 8: 3.91 / 3.94-3.98 / 4.09-4.11 ms per 1B points (profiles/r2_curve_unroll_sweep.txt)
+#endif
+constexpr int UNROLL_Z2 = GM_UNROLL_Z2;
 
 inline unsigned stride_grid(int64_t n) {
   int64_t b = (n + TPB - 1) / TPB;
@@ -513,15 +517,15 @@ int gm_z2_index(gm_ctx* ctx, const double* x, const double* y, int64_t n, int pr
   const bool vec = aligned16(x) && aligned16(y) && aligned16(z) && (((uintptr_t)status & 1u) == 0);
   hipStream_t s = ctx->stream;
   if (vec) {
-    unsigned grid = grid_for((n >> 1) > 0 ? (n >> 1) : 1, (int64_t)TPB * UNROLL_KEY);
+    unsigned grid = grid_for((n >> 1) > 0 ? (n >> 1) : 1, (int64_t)TPB * UNROLL_Z2);
     const dv2* x2 = (const dv2*)x; const dv2* y2 = (const dv2*)y;
     lv2* z2 = (lv2*)z; uchar2* s2 = (uchar2*)status;
     if (lenient) {
-      if (status) hipLaunchKernelGGL((k_z2_index<true, true, UNROLL_KEY>), dim3(grid), dim3(TPB), 0, s, x2, y2, n, z2, s2, lon, lat, ctx->d_err);
-      else hipLaunchKernelGGL((k_z2_index<true, false, UNROLL_KEY>), dim3(grid), dim3(TPB), 0, s, x2, y2, n, z2, s2, lon, lat, ctx->d_err);
+      if (status) hipLaunchKernelGGL((k_z2_index<true, true, UNROLL_Z2>), dim3(grid), dim3(TPB), 0, s, x2, y2, n, z2, s2, lon, lat, ctx->d_err);
+      else hipLaunchKernelGGL((k_z2_index<true, false, UNROLL_Z2>), dim3(grid), dim3(TPB), 0, s, x2, y2, n, z2, s2, lon, lat, ctx->d_err);
     } else {
-      if (status) hipLaunchKernelGGL((k_z2_index<false, true, UNROLL_KEY>), dim3(grid), dim3(TPB), 0, s, x2, y2, n, z2, s2, lon, lat, ctx->d_err);
-      else hipLaunchKernelGGL((k_z2_index<false, false, UNROLL_KEY>), dim3(grid), dim3(TPB), 0, s, x2, y2, n, z2, s2, lon, lat, ctx->d_err);
+      if (status) hipLaunchKernelGGL((k_z2_index<false, true, UNROLL_Z2>), dim3(grid), dim3(TPB), 0, s, x2, y2, n, z2, s2, lon, lat, ctx->d_err);
+      else hipLaunchKernelGGL((k_z2_index<false, false, UNROLL_Z2>), dim3(grid), dim3(TPB), 0, s, x2, y2, n, z2, s2, lon, lat, ctx->d_err);
     }
   } else {
     unsigned grid = stride_grid(n);
