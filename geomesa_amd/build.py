@@ -30,6 +30,11 @@ def build(force=False, verbose=True, out=OUT, defines=()):
     GM_JILP=8) to another path for side-by-side measurement."""
     if out == OUT and not defines and not force and not needs_build():
         return OUT
+    if out == OUT and any(d.startswith("GM_JX_") for d in defines):
+        # GM_JX_* are wrong-result timing hooks (stage ablations): never in the shipped library
+        raise ValueError("GM_JX_* timing hooks cannot be built into %s; pass --out=<other path>" % OUT)
+    if out == OUT:
+        defines = tuple(defines) + ("GM_PRODUCT_BUILD",)
     os.makedirs(os.path.dirname(out), exist_ok=True)
     # one object per unit, compiled in parallel (no device code crosses units), then one link
     objdir = out + ".objs"

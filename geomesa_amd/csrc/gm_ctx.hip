@@ -2,8 +2,10 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <map>
 #include <mutex>
 #include <string>
+#include <utility>
 
 #include "gm_internal.hpp"
 
@@ -22,6 +24,28 @@ static bool is_pinned(const void* p) {
     return false;
   }
   return a.type == hipMemoryTypeHost || a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged;
+}
+
+int resident_blocks(const void* kernel, int device, int block, int fallback_per_cu) {
+  static std::mutex mu;
+  static std::map<std::pair<const void*, int>, int> cache;
+  std::lock_guard<std::mutex> lk(mu);
+  const auto key = std::make_pair(kernel, device);
+  auto it = cache.find(key);
+  if (it != cache.end()) return it->second;
+  int b = 0, cus = 256, prev = 0;
+  (void)hipGetDevice(&prev);
+  (void)hipSetDevice(device);
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kernel, block, 0) != hipSuccess || b < 1) {
+    (void)hipGetLastError();
+    b = fallback_per_cu;
+  }
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) == hipSuccess) cus = prop.multiProcessorCount;
+  (void)hipSetDevice(prev);
+  const int r = std::max(1, b * cus);
+  cache[key] = r;
+  return r;
 }
 
 static int stage(gm_ctx* ctx) {

@@ -69,6 +69,11 @@ int begin_summary(gm_ctx* ctx, gm_batch_status* summary);
 // read the summary back (synchronises the stream); maps to GM_OK / per-element semantics
 int end_summary(gm_ctx* ctx, gm_batch_status* summary);
 
+// Resident block count of `kernel` at `block` threads per block on `device`: occupancy x CUs,
+// computed once per (kernel, device) under a lock (contexts on different devices and concurrent
+// callers are safe); `fallback_per_cu` when the occupancy query fails.
+int resident_blocks(const void* kernel, int device, int block, int fallback_per_cu);
+
 inline bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
 inline unsigned grid_for(int64_t n, int64_t per_block) {

@@ -38,6 +38,13 @@
 #include "gm_arrow.hpp"
 #include "gm_scan.hpp"
 
+// GM_JX_* macros are stage-ablation timing hooks that give wrong results; geomesa_amd/build.py
+// refuses them for the shipped library and defines GM_PRODUCT_BUILD there, so this guard holds
+#if defined(GM_PRODUCT_BUILD) && (defined(GM_JX_BLOBUNI) || defined(GM_JX_CAPS) || defined(GM_JX_NOATOMIC) || \
+                                  defined(GM_JX_NOCOARSE) || defined(GM_JX_NOFINE) || defined(GM_JX_NOBLOB))
+#error "GM_JX_* timing hooks are not allowed in the product build"
+#endif
+
 namespace gm {
 
 enum : int { LOC_EXTERIOR = 0, LOC_BOUNDARY = 1, LOC_INTERIOR = 2 };
@@ -2436,14 +2443,7 @@ int build_cells_device(gm_ctx* ctx, gm_pip_index* ix, const gm_polyset* ps, cons
 // the XCD-aware mapping), so no partial second round of blocks forms a tail
 template <class K>
 static unsigned resident_grid(K kernel, int device, int64_t ntiles, bool xcd_multiple) {
-  static int resident = 0;   // per kernel instantiation; every device of the node is the same MI355X
-  if (!resident) {
-    int b = 0, n = 256;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kernel, JTPB, 0) != hipSuccess || b < 1) b = 4;
-    hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, device) == hipSuccess) n = prop.multiProcessorCount;
-    resident = b * n;
-  }
+  const int resident = resident_blocks((const void*)kernel, device, JTPB, 4);
   int64_t g = std::min<int64_t>(resident, std::max<int64_t>(ntiles, 1));
   if (xcd_multiple) g = (g + 7) / 8 * 8;
   return (unsigned)g;

@@ -1009,6 +1009,17 @@ inline int64_t z_caps(int max_ranges, int D, int64_t cap_hint) {
   return std::max<int64_t>(cap_hint, 1 << 16);
 }
 
+// frees the stream-ordered input copies of one entry point on every return path
+struct StreamFrees {
+  hipStream_t s;
+  void* p[4] = {nullptr, nullptr, nullptr, nullptr};
+  explicit StreamFrees(hipStream_t st) : s(st) {}
+  ~StreamFrees() {
+    for (void* q : p)
+      if (q) (void)hipFreeAsync(q, s);
+  }
+};
+
 }  // namespace
 
 extern "C" {
@@ -1022,13 +1033,15 @@ int gm_z3_ranges(gm_ctx* ctx, int64_t nq, const int32_t* box_off, const double* 
   if (nq == 0) { out_off[0] = 0; if (needed) *needed = 0; return GM_OK; }
   hipStream_t s = ctx->stream;
   const int64_t nbox = box_off[nq], ntim = time_off[nq];
-  int32_t *dbo, *dto;
-  double* dxy;
-  int64_t* dt;
+  int32_t *dbo = nullptr, *dto = nullptr;
+  double* dxy = nullptr;
+  int64_t* dt = nullptr;
+  StreamFrees fr(s);
   int rc = to_dev(ctx, box_off, (size_t)nq + 1, &dbo);
-  if (!rc) rc = to_dev(ctx, time_off, (size_t)nq + 1, &dto);
-  if (!rc) rc = to_dev(ctx, xy, (size_t)nbox * 4, &dxy);
-  if (!rc) rc = to_dev(ctx, t, (size_t)ntim * 2, &dt);
+  fr.p[0] = dbo;
+  if (!rc) { rc = to_dev(ctx, time_off, (size_t)nq + 1, &dto); fr.p[1] = dto; }
+  if (!rc) { rc = to_dev(ctx, xy, (size_t)nbox * 4, &dxy); fr.p[2] = dxy; }
+  if (!rc) { rc = to_dev(ctx, t, (size_t)ntim * 2, &dt); fr.p[3] = dt; }
   if (rc) return rc;
   ZRangesArgs a{};
   a.box_off = dbo; a.xy = dxy; a.time_off = dto; a.t = dt;
@@ -1049,7 +1062,6 @@ int gm_z3_ranges(gm_ctx* ctx, int64_t nq, const int32_t* box_off, const double* 
                     hipLaunchKernelGGL(k_zranges<3>, dim3((unsigned)m), dim3(RTPB), 0, s, b);
                   },
                   out_off, out, cap, needed, query_status);
-  (void)hipFreeAsync(dbo, s); (void)hipFreeAsync(dto, s); (void)hipFreeAsync(dxy, s); (void)hipFreeAsync(dt, s);
   return rc;
 }
 
@@ -1062,10 +1074,12 @@ int gm_z2_ranges(gm_ctx* ctx, int64_t nq, const int32_t* box_off, const double* 
   if (nq == 0) { out_off[0] = 0; if (needed) *needed = 0; return GM_OK; }
   hipStream_t s = ctx->stream;
   const int64_t nbox = box_off[nq];
-  int32_t* dbo;
-  double* dxy;
+  int32_t* dbo = nullptr;
+  double* dxy = nullptr;
+  StreamFrees fr(s);
   int rc = to_dev(ctx, box_off, (size_t)nq + 1, &dbo);
-  if (!rc) rc = to_dev(ctx, xy, (size_t)nbox * 4, &dxy);
+  fr.p[0] = dbo;
+  if (!rc) { rc = to_dev(ctx, xy, (size_t)nbox * 4, &dxy); fr.p[1] = dxy; }
   if (rc) return rc;
   ZRangesArgs a{};
   a.box_off = dbo; a.xy = dxy; a.time_off = nullptr; a.t = nullptr;
@@ -1085,7 +1099,6 @@ int gm_z2_ranges(gm_ctx* ctx, int64_t nq, const int32_t* box_off, const double* 
                     hipLaunchKernelGGL(k_zranges<2>, dim3((unsigned)m), dim3(RTPB), 0, s, b);
                   },
                   out_off, out, cap, needed, query_status);
-  (void)hipFreeAsync(dbo, s); (void)hipFreeAsync(dxy, s);
   return rc;
 }
 
@@ -1097,10 +1110,12 @@ static int xz_ranges(gm_ctx* ctx, int D, int64_t nq, const int32_t* win_off, con
   if (nq == 0) { out_off[0] = 0; if (needed) *needed = 0; return GM_OK; }
   hipStream_t s = ctx->stream;
   const int64_t nw = win_off[nq];
-  int32_t* dwo;
-  double* dw;
+  int32_t* dwo = nullptr;
+  double* dw = nullptr;
+  StreamFrees fr(s);
   int rc = to_dev(ctx, win_off, (size_t)nq + 1, &dwo);
-  if (!rc) rc = to_dev(ctx, windows, (size_t)nw * 2 * D, &dw);
+  fr.p[0] = dwo;
+  if (!rc) { rc = to_dev(ctx, windows, (size_t)nw * 2 * D, &dw); fr.p[1] = dw; }
   if (rc) return rc;
   XZRangesArgs a{};
   a.win_off = dwo; a.win = dw; a.g = g; a.zhi = (double)max_offset(period);
@@ -1126,7 +1141,6 @@ static int xz_ranges(gm_ctx* ctx, int D, int64_t nq, const int32_t* win_off, con
                     else hipLaunchKernelGGL(k_xzranges<3>, dim3((unsigned)m), dim3(RTPB), 0, s, b);
                   },
                   out_off, out, cap, needed, query_status);
-  (void)hipFreeAsync(dwo, s); (void)hipFreeAsync(dw, s);
   return rc;
 }
 
@@ -1140,10 +1154,12 @@ int gm_zranges(gm_ctx* ctx, int dims, int64_t nq, const int32_t* bound_off, cons
   hipStream_t s = ctx->stream;
   const int64_t nb = bound_off[nq];
   if (nb > 0 && !zbounds) return GM_E_INVALID;
-  int32_t* dbo;
-  int64_t* dzb;
+  int32_t* dbo = nullptr;
+  int64_t* dzb = nullptr;
+  StreamFrees fr(s);
   int rc = to_dev(ctx, bound_off, (size_t)nq + 1, &dbo);
-  if (!rc) rc = to_dev(ctx, zbounds, (size_t)nb * 2, &dzb);
+  fr.p[0] = dbo;
+  if (!rc) { rc = to_dev(ctx, zbounds, (size_t)nb * 2, &dzb); fr.p[1] = dzb; }
   if (rc) return rc;
   ZRangesArgs a{};
   a.zb_off = dbo; a.zb = dzb;
@@ -1162,7 +1178,6 @@ int gm_zranges(gm_ctx* ctx, int dims, int64_t nq, const int32_t* bound_off, cons
                     else hipLaunchKernelGGL(k_zranges<2>, dim3((unsigned)m), dim3(RTPB), 0, s, b);
                   },
                   out_off, out, cap, needed, query_status);
-  (void)hipFreeAsync(dbo, s); (void)hipFreeAsync(dzb, s);
   return rc;
 }
 

@@ -373,14 +373,7 @@ int gm_sort_keys(gm_ctx* ctx, const uint8_t* shard, const int16_t* bin, const in
     return GM_OK;
   }
   // one resident wave of blocks: the scatter's LDS (~139 KiB) allows one 1024-thread block per CU
-  static int resident = 0;
-  if (!resident) {
-    int b = 0, cus = 256;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_sort_scatter, BT, 0) != hipSuccess || b < 1) b = 1;
-    hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, ctx->device) == hipSuccess) cus = prop.multiProcessorCount;
-    resident = b * cus;
-  }
+  const int resident = resident_blocks((const void*)k_sort_scatter, ctx->device, BT, 1);
   const int nblk = (int)std::max<int64_t>(1, std::min<int64_t>(resident, (n + BTILE - 1) / BTILE));
   const int64_t per = ((n + nblk - 1) / nblk + BTILE - 1) / BTILE * BTILE;
   const int grid = (int)((n + per - 1) / per);

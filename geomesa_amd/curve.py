@@ -417,6 +417,43 @@ class LegacyZ3SFC(_LegacyBase):
         return self._run_index("gm_legacy_z3_index", cols, cols[0].numel(), (self.curve, self.period), lenient,
                                status, type(self).__name__ + ".index")
 
+    def index_keys(self, x, y, t_ms, lenient=False, status=False):
+        """Z3IndexKeySpaceV4's (bin, z) (legacy/Z3IndexV4.scala:44-51 over Z3IndexKeySpace.scala:71-76):
+        BinnedTime (raises for out-of-range dates even when lenient), then this curve's index."""
+        if status:
+            raise IllegalArgumentException("per-element status is not offered for the legacy key space")
+        bins, off = BinnedTime.time_to_binned_time(self.period, t_ms)
+        return bins, self.index(x, y, off, lenient=lenient)
+
+    def ranges(self, xy, t, precision=64, max_ranges=None):
+        """Z3SFC.ranges (Z3SFC.scala:59-67), which LegacyZ3SFC inherits, for one query."""
+        return self.ranges_batch([(xy, t)], precision, max_ranges)[0]
+
+    def ranges_batch(self, queries, precision=64, max_ranges=None, max_recurse=None):
+        """Z3SFC.ranges as LegacyZ3SFC inherits it (Z3SFC.scala:59-67): per (box, interval) a
+        ZRange(index(xmin, ymin, tmin), index(xmax, ymax, tmax)) through THIS curve's (legacy,
+        non-lenient) index, then Z3.zranges with Z3SFC.MaxRecursion = Int.MaxValue (Z3SFC.scala:72).
+        Corners are keyed on the device (gm_legacy_z3_index), the walk is gm_zranges."""
+        from . import ranges as R
+        lo_x, lo_y, lo_t, hi_x, hi_y, hi_t, counts = [], [], [], [], [], [], []
+        for (bxs, ts) in queries:
+            k = 0
+            for (xmin, ymin, xmax, ymax) in bxs:
+                for (tmin, tmax) in ts:
+                    lo_x.append(float(xmin)); lo_y.append(float(ymin)); lo_t.append(int(tmin))
+                    hi_x.append(float(xmax)); hi_y.append(float(ymax)); hi_t.append(int(tmax))
+                    k += 1
+            counts.append(k)
+        bounds = [[] for _ in queries]
+        if lo_x:
+            zlo = self.index(lo_x, lo_y, lo_t).cpu().tolist()   # require(...) raises like the Scala index
+            zhi = self.index(hi_x, hi_y, hi_t).cpu().tolist()
+            k = 0
+            for q, c in enumerate(counts):
+                bounds[q] = list(zip(zlo[k:k + c], zhi[k:k + c]))
+                k += c
+        return R.zranges(3, bounds, precision, max_ranges, (1 << 31) - 1 if max_recurse is None else max_recurse)
+
     def invert(self, z):
         torch = _torch()
         if self.curve != self.LEGACY_Z3:

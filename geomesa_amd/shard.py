@@ -312,8 +312,8 @@ def gather_ranges(pg, out_off, ranges, dst=0):
     from .ranges import RANGE_DTYPE
     cnt = torch.from_numpy(np.diff(np.asarray(out_off, np.int64)))
     rr = torch.from_numpy(np.ascontiguousarray(ranges).view(np.int64).reshape(-1).copy())
-    g = gather_rows(pg, [cnt])
-    gr = gather_rows(pg, [rr])
+    g = gather_rows(pg, [cnt], dst=dst)
+    gr = gather_rows(pg, [rr], dst=dst)
     if g is None:
         return None
     offs = np.concatenate([[0], np.cumsum(g[0].cpu().numpy())]).astype(np.int64)

@@ -5,6 +5,8 @@ import re
 
 from geomesa_amd import _lib
 
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
 
 def declared_symbols():
     src = open(_lib.HEADER).read()
@@ -45,3 +47,17 @@ def test_load_without_gpu_fails_loudly():
         pytest.skip("GPU present")
     with pytest.raises(_lib.GeomesaHipUnavailable):
         _lib.context()
+
+
+def test_product_build_refuses_timing_hooks():
+    """The GM_JX_* stage-ablation hooks (wrong results by design) cannot reach the shipped library:
+    build.py refuses them for its output path (no compile runs), and the product build defines
+    GM_PRODUCT_BUILD, under which gm_pip.hip #errors on any of them."""
+    import pytest
+    from geomesa_amd import build as B
+    with pytest.raises(ValueError):
+        B.build(defines=("GM_JX_NOBLOB",), verbose=False)
+    src = open(os.path.join(ROOT, "geomesa_amd", "csrc", "gm_pip.hip")).read()
+    hooks = set(re.findall(r"GM_JX_[A-Z0-9]+", src))
+    guard = src[src.index("#if defined(GM_PRODUCT_BUILD)"):src.index("#error")]
+    assert hooks and all(h in guard for h in hooks), hooks

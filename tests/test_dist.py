@@ -323,7 +323,7 @@ def test_exchange_by_key_range(world, sizes):
     assert max(len(g[1]) for g in got) <= 1.35 * n / world
 
 
-def _granges_worker(rank, world, port, q):
+def _granges_worker(rank, world, port, q, dst=0):
     sys.path.insert(0, ROOT)
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -339,26 +339,27 @@ def _granges_worker(rank, world, port, q):
         rr["lower"] = np.arange(len(rr)) + 1000 * rank
         rr["upper"] = rr["lower"] + 1
         rr["contained"] = rank
-        g = gather_ranges(dist, off, rr)
+        g = gather_ranges(dist, off, rr, dst=dst)
         q.put((rank, g))
     finally:
         dist.destroy_process_group()
 
 
-def test_gather_ranges():
+@pytest.mark.parametrize("dst", [0, 1])
+def test_gather_ranges(dst):
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_granges_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_granges_worker, args=(r, world, port, q, dst)) for r in range(world)]
     for p in procs:
         p.start()
     got = dict(q.get(timeout=240) for _ in range(world))
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    assert got[1] is None
-    off, rr = got[0]
+    assert got[1 - dst] is None
+    off, rr = got[dst]
     c0, c1 = np.arange(3) % 3, np.arange(4) % 3 + 1
     assert off.tolist() == np.concatenate([[0], np.cumsum(np.concatenate([c0, c1]))]).tolist()
     assert rr["lower"].tolist() == list(range(c0.sum())) + [1000 + i for i in range(c1.sum())]

@@ -71,3 +71,37 @@ def test_z3_iterator_13_golden_gpu(gpu):
     lo, hi = z3_dims(int(z[0])), z3_dims(int(z[1]))
     assert "%d:%d:%d:%d" % (lo[0], lo[1], hi[0], hi[1]) == COMPAT_13_GOLDEN["zxy"]
     assert "2370;%d:%d" % (lo[2], hi[2]) == COMPAT_13_GOLDEN["zt"]
+
+
+@pytest.mark.parametrize("target", [None, 2000, 40])
+def test_key_space_v4_ranges_and_keys(gpu, oracle, target):
+    """Z3IndexKeySpaceV4 query planning over LegacyZ3SFC (legacy/Z3IndexV4.scala:44-51): getRanges runs
+    Z3SFC.ranges as LegacyZ3SFC inherits it (Z3SFC.scala:59-67) -- ZRanges of the legacy index of each
+    (box, interval)'s corners, Z3.zranges with Int.MaxValue recursion -- and toIndexKey is BinnedTime +
+    the legacy index.  Checked against the oracle's legacy index and ZN.zranges."""
+    from geomesa_amd.keyspace import Z3IndexKeySpaceV4
+    from test_host_planning import COMPAT_13_FILTER
+    ks = Z3IndexKeySpaceV4()
+    v = ks.get_index_values(*COMPAT_13_FILTER)
+    (xmin, ymin, xmax, ymax), = v.spatialBounds
+    got = ks.sfc.ranges_batch([(v.spatialBounds, v.temporalBounds[b]) for b in sorted(v.temporalBounds)], 64, target)
+    for b, rr in zip(sorted(v.temporalBounds), got):
+        bounds = []
+        for (t1, t2) in v.temporalBounds[b]:
+            s0, lo = oracle.legacy_z3_index(xmin, ymin, int(t1))
+            s1, hi = oracle.legacy_z3_index(xmax, ymax, int(t2))
+            assert s0 == 0 and s1 == 0
+            bounds.append((lo, hi))
+        exp = oracle.zranges(3, bounds, 64, target, None)
+        assert [(r.lower, r.upper, r.contained) for r in rr] == exp
+    # get_ranges goes through the same call: [bin][z] ranges, one per IndexRange
+    assert len(ks.get_ranges(v)) == sum(len(r) for r in ks.sfc.ranges_batch(
+        [(v.spatialBounds, v.temporalBounds[b]) for b in sorted(v.temporalBounds)], 64, 2000 // len(v.temporalBounds)))
+    # toIndexKey: BinnedTime(week) + LegacyZ3SFC.index
+    x, y, t = random_points(5_001)
+    bins, z = ks.to_index_keys(x, y, t)
+    bins, z = as_np(bins), as_np(z)
+    for i in range(0, len(x), 97):
+        _, ob, off = oracle.binned_time(1, int(t[i]))
+        st, oz = oracle.legacy_z3_index(float(x[i]), float(y[i]), int(off))
+        assert (bins[i], z[i]) == (ob, oz), i

@@ -91,6 +91,24 @@ def test_relate_box_kats(gpu):
     assert as_np(null).tolist() == [False] * 6 + [True]
 
 
+@pytest.mark.parametrize("mode", ["auto", "split", "partitioned"])
+def test_st_covers_box_kats(gpu, mode):
+    """SpatialRelationFunctionsTest.scala:113-139: st_covers(POLYGON((0 0,0 10,10 10,10 0,0 0)), p) is true
+    for POINT(5 5), POINT(0 5) (edge) and POINT(0 0) (corner), false for POINT(-5 0) -- as the join
+    condition (every strategy) and row by row."""
+    from geomesa_amd.join import PolygonIndex, PolygonSet
+    ps = PolygonSet.from_polygons([[[[(0, 0), (0, 10), (10, 10), (10, 0), (0, 0)]]]])
+    ix = PolygonIndex(ps)
+    px, py = [5.0, 0.0, 0.0, -5.0], [5.0, 5.0, 0.0, 0.0]
+    pt, pl = ix.join(px, py, mode=mode, predicate="st_covers")
+    assert sorted(as_np(pt).tolist()) == [0, 1, 2] and set(as_np(pl).tolist()) == {0}
+    cov, null = ix.predicate("st_covers", [0, 0, 0, 0], px, py)
+    assert as_np(cov).tolist() == [True, True, True, False]
+    assert not as_np(null).any()
+    pt, _ = ix.join(px, py, mode=mode, predicate="st_contains")   # :96-99, the same points under st_contains
+    assert as_np(pt).tolist() == [0]
+
+
 def _envelopes(ps):
     ppo, pro, rvo, vx, vy = ps.to_arrays()
     env = []

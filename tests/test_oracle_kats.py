@@ -432,6 +432,22 @@ def test_st_intersects_within_box(oracle):  # SpatialRelationFunctionsTest.scala
     assert [k for k, (x, y) in pts.items() if ps.contains(0, x, y)] == ["int"]
 
 
+def test_st_covers_box(oracle):  # SpatialRelationFunctionsTest.scala:113-139 (st_covers pt1-pt4)
+    """st_covers(box, point): every point of the point lies in the box (interior or boundary), so
+    int / edge / corner are covered and ext is not (:115-118 select, :131-134 pt1-pt4)."""
+    box = [[[[(0, 0), (0, 10), (10, 10), (10, 0), (0, 0)]]]]
+    ps = _polyset(box)
+    pts = {"int": (5.0, 5.0), "edge": (0.0, 5.0), "corner": (0.0, 0.0), "ext": (-5.0, 0.0)}
+    import oracle as O
+    covered = [k for k, (x, y) in pts.items() if ps.locate(0, x, y) != 0]   # LOC_EXTERIOR = 0
+    assert covered == ["int", "edge", "corner"]
+    import numpy as np
+    px = np.array([v[0] for v in pts.values()]); py = np.array([v[1] for v in pts.values()])
+    pt, pl = ps.join(px, py, predicate="st_covers")
+    assert sorted(pt.tolist()) == [0, 1, 2] and set(pl.tolist()) == {0}
+    assert O is not None
+
+
 def test_query_scan_oracle_terms(oracle):
     """bbox AND during AND OR-over-polygons, each term optional (gmo_query_scan)."""
     import numpy as np
