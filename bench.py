@@ -857,6 +857,7 @@ def main():
         _lib.check(lib.gm_pip_join_ex(h, ix._h, P(px), P(py), J, jlo, P(ptids), P(plids), cap,
                                       __import__("ctypes").byref(npairs), jmode), "join")
         matches = int(dist.sum(npairs.value))
+        census = ix.census(px, py)   # how the lookup chain resolves these points (diagnostic, untimed)
         pairs = J * n_polys * dist.world
         pj = {"value": pairs / (jms * 1e-3), "unit": "pairs/s",
               "points_per_s": J * dist.world / (jms * 1e-3), "matches_per_s": matches / (jms * 1e-3),
@@ -865,6 +866,7 @@ def main():
               "ms_per_step": jms, "points_per_gpu": J,
               "polygons": n_polys, "vertices": n_verts, "matches": matches,
               "index_build_s": round(t_build, 3), "index_ready_s": round(t_ix, 3), "index": ix.stats(), "mode": a.join_mode,
+              "census": census,
               "roofline": roofline(16.0 * J + 12.0 * npairs.value, jms, load_pmc("pip_join", J)),
               "workload": "st_contains(polygon, point) join, %d CONUS points/GPU x %d synthetic county polygons "
                           "(BASELINE configs[3]); index built on rank 0, broadcast over RCCL when N > 1"

@@ -1224,6 +1224,68 @@ __global__ __launch_bounds__(FTPB, GM_QUERY_WAVES) void k_query_mask(const doubl
   block_count_waves(cnt, block_counts);
 }
 
+// ------------------------------------------------------------------ lookup census (diagnostic)
+// How the join's lookup chain resolves a batch of points, stage by stage (gm_pip_join_census): the
+// design numbers behind its gather costs.  Counters (JC_*) are summed per block in LDS.
+enum : int {
+  JC_POINTS = 0, JC_OUTSIDE, JC_COARSE_EMPTY, JC_COARSE_INTERIOR, JC_COARSE_RAW_MIXED, JC_FINE, JC_FINE_EMPTY,
+  JC_FINE_INTERIOR, JC_FINE_LINE, JC_FINE_COMPACT, JC_FINE_GENERIC, JC_FINE_LIST, JC_LIST_ENTRIES,
+  JC_LIST_BLOBS, JC_LINE_RESOLVED, JC_LINE_FALLBACK, JC_N
+};
+
+__global__ __launch_bounds__(256) void k_pip_census(const double* __restrict__ px, const double* __restrict__ py, int64_t n,
+                                                    PipDev d, unsigned long long* __restrict__ out) {
+  __shared__ unsigned long long s_c[JC_N];
+  if (threadIdx.x < JC_N) s_c[threadIdx.x] = 0;
+  __syncthreads();
+  int c[JC_N];
+#pragma unroll
+  for (int k = 0; k < JC_N; ++k) c[k] = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const double x = px[i], y = py[i];
+    c[JC_POINTS]++;
+    if (!(x >= d.gx0 && x <= d.gx1 && y >= d.gy0 && y <= d.gy1)) { c[JC_OUTSIDE]++; continue; }
+    const int cx = cell_of(x, d.gx0, d.inv_cw, d.gx), cy = cell_of(y, d.gy0, d.inv_ch, d.gy);
+    const uint32_t raw = d.coarse_sc[(int64_t)(cy >> CF_LOG) * d.gxc + (cx >> CF_LOG)];
+    if ((raw >> 30) == CELL_LIST) c[JC_COARSE_RAW_MIXED]++;
+    uint32_t w = coarse_mask(raw, cx, cy, d.coarse_fmt);
+    if ((w >> 30) == CELL_EMPTY) { c[JC_COARSE_EMPTY]++; continue; }
+    if ((w >> 30) == CELL_INTERIOR) { c[JC_COARSE_INTERIOR]++; continue; }
+    c[JC_FINE]++;
+    w = d.cell_sc[(int64_t)cy * d.gx + cx];
+    const uint32_t kind = w >> 30, ref = w & 0x3fffffffu;
+    if (kind == CELL_EMPTY) { c[JC_FINE_EMPTY]++; continue; }
+    if (kind == CELL_INTERIOR) { c[JC_FINE_INTERIOR]++; continue; }
+    if (kind == CELL_BOUNDARY) {
+      if ((ref & BLOB_COMPACT) && (ref & SC_LINE) && d.line_ent) {
+        c[JC_FINE_LINE]++;
+        const uint64_t li = ref & (SC_LINE - 1);
+        const int l = line_locate(d.line_ent[2 * li], d.line_ent[2 * li + 1], x, y, d);
+        if (l >= 0) c[JC_LINE_RESOLVED]++;
+        else c[JC_LINE_FALLBACK]++;
+      } else if (ref & BLOB_COMPACT) {
+        c[JC_FINE_COMPACT]++;
+      } else {
+        c[JC_FINE_GENERIC]++;
+      }
+      continue;
+    }
+    c[JC_FINE_LIST]++;
+    int l0 = 4 * (int)(ref >> 4), ni = (int)(w & 15u);
+    if (ni == LIST_LONG) { ni = (int)d.list_ent[l0]; l0 += 1; }
+    c[JC_LIST_ENTRIES] += ni;
+    for (int j = 0; j < ni; ++j) c[JC_LIST_BLOBS] += (d.list_ent[l0 + j] >> 30) != CELL_INTERIOR;
+  }
+#pragma unroll
+  for (int k = 0; k < JC_N; ++k) {
+    unsigned long long v = (unsigned long long)c[k];
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if ((threadIdx.x & 63) == 0 && v) atomicAdd(&s_c[k], v);
+  }
+  __syncthreads();
+  if (threadIdx.x < JC_N && s_c[threadIdx.x]) atomicAdd(&out[threadIdx.x], s_c[threadIdx.x]);
+}
+
 // ------------------------------------------------------------------ row-wise predicate (UDF path)
 // st_contains / st_covers / st_intersects / ... evaluated row by row, as Spark SQL runs the UDF when
 // the join rule does not apply (SpatialRelationFunctions.scala:29-37 over nullableUDF,
@@ -3252,6 +3314,21 @@ int gm_query_scan(gm_ctx* ctx, const double* x, const double* y, const int64_t* 
   if (rc) return rc;
   if (n_match && ids && *n_match > ids_cap) return GM_E_CAPACITY;
   return GM_OK;
+}
+
+int gm_pip_join_census(gm_ctx* ctx, const gm_pip_index* ix, const double* px, const double* py, int64_t n,
+                       int64_t* counters) {
+  if (!ctx || !ix || n < 0 || !counters || (n > 0 && (!px || !py))) return GM_E_INVALID;
+  GM_HIP(hipSetDevice(ctx->device));
+  unsigned long long* d = (unsigned long long*)ctx->d_scratch;
+  static_assert(JC_N <= 16, "census counters exceed the context scratch");
+  GM_HIP(hipMemsetAsync(d, 0, JC_N * 8, ctx->stream));
+  if (n > 0) {
+    hipLaunchKernelGGL(k_pip_census, dim3((unsigned)std::min<int64_t>(8192, (n + 255) / 256)), dim3(256), 0, ctx->stream,
+                       px, py, n, ix->dev, d);
+    GM_CHECK_LAUNCH();
+  }
+  return copy_d2h(ctx, counters, d, JC_N * 8);
 }
 
 int gm_pip_relate(gm_ctx* ctx, const gm_pip_index* ix, const int32_t* poly, const double* px, const double* py,

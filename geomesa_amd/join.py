@@ -138,6 +138,22 @@ class PolygonIndex:
         check(self.ctx.lib.gm_pip_index_stats(self._h, st.ctypes.data), "gm_pip_index_stats")
         return dict(zip(["cells", "entries", "boundary", "records", "slow", "blob_bytes", "compact"], st.tolist()))
 
+    CENSUS = ["points", "outside", "coarse_empty", "coarse_interior", "coarse_raw_mixed", "fine", "fine_empty",
+              "fine_interior", "fine_line", "fine_compact", "fine_generic", "fine_list", "list_entries",
+              "list_blobs", "line_resolved", "line_fallback"]
+
+    def census(self, px, py):
+        """Diagnostic: how the lookup chain resolves these points, stage by stage (gm_pip_join_census)."""
+        import numpy as np
+        import torch
+        dev = torch.device("cuda", self.ctx.device)
+        x = torch.as_tensor(px, dtype=torch.float64, device=dev).contiguous()
+        y = torch.as_tensor(py, dtype=torch.float64, device=dev).contiguous()
+        c = np.zeros(16, np.int64)
+        check(self.ctx.lib.gm_pip_join_census(self.ctx.handle, self._h, ptr(x), ptr(y), x.numel(), c.ctypes.data),
+              "gm_pip_join_census")
+        return dict(zip(self.CENSUS, c.tolist()))
+
     MODES = {"auto": _lib.GM_JOIN_AUTO, "direct": _lib.GM_JOIN_DIRECT, "partitioned": _lib.GM_JOIN_PARTITIONED,
              "split": _lib.GM_JOIN_SPLIT}
 

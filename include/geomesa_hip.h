@@ -245,6 +245,13 @@ int gm_pip_index_destroy(gm_pip_index* index);
 /* index statistics: stats[0..6] = cells, (cell, polygon) entries, boundary entries, ring records,
    ring records that fall back to the slab walk, boundary blob bytes, compact (one-line) blobs */
 int gm_pip_index_stats(const gm_pip_index* index, int64_t* stats);
+/* Diagnostic (no reference counterpart): how the join's lookup chain resolves the device points
+   px / py, stage by stage -- counters[16] = points, outside the grid, coarse EMPTY, coarse INTERIOR,
+   points in mixed coarse cells before the sub-block masks, fine lookups, fine EMPTY, fine INTERIOR,
+   fine line entries, fine compact blobs, fine generic blobs, fine lists, list entries, list entries
+   that are blobs, line entries that decide, line entries that fall back to the blob. */
+int gm_pip_join_census(gm_ctx* ctx, const gm_pip_index* index, const double* px, const double* py, int64_t n,
+                       int64_t* counters);
 
 /* A built index as device arrays, for shipping it to the other GPUs of a join (RCCL broadcast) instead
    of rebuilding it on every rank -- the broadcast side of GeoMesaJoinRelation's join

@@ -93,3 +93,18 @@ def test_join_coarse_mask_formats(gpu, oracle, fmt, monkeypatch):
     for mode in ("direct", "partitioned"):
         pt, pl = ix.join(px, py, mode=mode)
         assert np.array_equal(_sorted_pairs(pt, pl), exp), (fmt, mode)
+
+
+def test_join_census_accounts_for_every_point(gpu):
+    """gm_pip_join_census (diagnostic): every point ends at exactly one stage of the lookup chain."""
+    from geomesa_amd.join import PolygonIndex, synthetic_counties, synthetic_points
+    ps = synthetic_counties(20, 10)
+    px, py = synthetic_points(300_000)
+    px = np.concatenate([px, [np.nan, 0.0, -200.0]]); py = np.concatenate([py, [30.0, np.nan, 30.0]])
+    c = PolygonIndex(ps).census(px, py)
+    assert c["points"] == len(px)
+    assert c["points"] == c["outside"] + c["coarse_empty"] + c["coarse_interior"] + c["fine"]
+    assert c["fine"] == (c["fine_empty"] + c["fine_interior"] + c["fine_line"] + c["fine_compact"] + c["fine_generic"]
+                         + c["fine_list"])
+    assert c["fine_line"] == c["line_resolved"] + c["line_fallback"]
+    assert c["outside"] >= 3 and c["fine"] > 0 and c["coarse_interior"] > 0
