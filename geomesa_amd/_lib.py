@@ -18,6 +18,7 @@ GM_E_INVALID = -1
 GM_E_HIP = -2
 GM_E_CAPACITY = -3
 GM_E_ELEMENT = -4
+GM_E_INDEX = -5
 
 GM_ST_OK = 0
 GM_ST_OUT_OF_BOUNDS = 1

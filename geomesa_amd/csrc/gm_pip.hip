@@ -75,7 +75,19 @@ struct PipDev {
   double gx0, gy0, gx1, gy1, inv_cw, inv_ch;
   int32_t gx, gy, gxc;
   int32_t op;                    // join predicate: JOIN_CONTAINS (interior) or JOIN_INTERSECTS (not exterior)
+  // reference checks: every blob / line / list reference a kernel follows is bounded by these sizes
+  // (make_shortcut); a reference beyond them sets a PIP_FAULT_* bit in *fault (the call's scratch
+  // word, null = not checked by this caller) and is treated as EXTERIOR, never dereferenced
+  uint32_t* fault;
+  int64_t n_line, n_compact_lines, n_blob16, n_list;
 };
+
+enum : uint32_t { PIP_FAULT_LINE = 1, PIP_FAULT_COMPACT = 2, PIP_FAULT_BLOB = 4, PIP_FAULT_LIST = 8, PIP_FAULT_QUEUE = 16 };
+
+__device__ __forceinline__ void pip_fault(const PipDev& d, uint32_t code) {
+  if (d.fault) atomicOr(d.fault, code);
+}
+
 
 #ifndef GM_CF_LOG
 #define GM_CF_LOG 3
@@ -91,6 +103,12 @@ enum : uint32_t { CELL_INTERIOR = 0, CELL_BOUNDARY = 1, CELL_LIST = 2, CELL_EMPT
 constexpr uint32_t BLOB_COMPACT = 1u << 29;
 // LIST payload: list_ent offset << 4 | count; count 15 = long list whose count is list_ent[offset]
 constexpr int LIST_LONG = 15;
+
+// is the blob reference of a BOUNDARY entry (payload `ref`, LINE words excluded) inside the index?
+__device__ __forceinline__ bool blob_ref_ok(const PipDev& d, uint32_t ref) {
+  if (ref & BLOB_COMPACT) return (uint64_t)(ref & (BLOB_COMPACT - 1)) < (uint64_t)d.n_compact_lines;
+  return (uint64_t)ref < (uint64_t)d.n_blob16;
+}
 
 // Compact blob (single-ring polygon, 4 * segments + breakpoints <= 30 in the cell): one or two
 // 128-B lines of 16 words in `compact`, addressed by line index.
@@ -344,13 +362,20 @@ __device__ __forceinline__ uint32_t coarse_mask(uint32_t w, int cx, int cy, int3
 __device__ __forceinline__ int item_locate(const PipDev& d, uint32_t ref, double x, double y, int& poly) {
   int loc = -1;
   if ((ref & BLOB_COMPACT) && d.line_ent && (ref & SC_LINE)) {
-    const uint4 e0 = d.line_ent[2 * (uint64_t)(ref & (SC_LINE - 1))], e1 = d.line_ent[2 * (uint64_t)(ref & (SC_LINE - 1)) + 1];
+    const uint64_t li = ref & (SC_LINE - 1);
+    if (li >= (uint64_t)d.n_line) { pip_fault(d, PIP_FAULT_LINE); poly = -1; return LOC_EXTERIOR; }
+    const uint4 e0 = d.line_ent[2 * li], e1 = d.line_ent[2 * li + 1];
     poly = (int)e0.y;
     loc = line_locate(e0, e1, x, y, d);
     ref = e0.x & 0x3fffffffu;
   }
   if (loc >= 0) return loc;
-  if (ref & BLOB_COMPACT) return compact_locate((const dv2*)(d.compact + 16 * (uint64_t)(ref & (BLOB_COMPACT - 1))), x, y, poly);
+  if (ref & BLOB_COMPACT) {
+    const uint64_t ci = ref & (BLOB_COMPACT - 1);
+    if (ci >= (uint64_t)d.n_compact_lines) { pip_fault(d, PIP_FAULT_COMPACT); poly = -1; return LOC_EXTERIOR; }
+    return compact_locate((const dv2*)(d.compact + 16 * ci), x, y, poly);
+  }
+  if ((uint64_t)ref >= (uint64_t)d.n_blob16) { pip_fault(d, PIP_FAULT_BLOB); poly = -1; return LOC_EXTERIOR; }
   const double* b = d.blob + 2 * (uint64_t)ref;
   const int2 h = *(const int2*)b;
   poly = h.x;
@@ -546,7 +571,8 @@ __global__ __launch_bounds__(JTPB, GM_JOIN_WAVES) void k_pip_join(const double* 
       if (kind == CELL_LIST) {
         lo[u] = 4 * (int)((cw[u] & 0x3fffffffu) >> 4);
         ni[u] = (int)(cw[u] & 15u);
-        lq[u] = *(const uint4*)(d.list_ent + lo[u]);   // the first four slots, all points at once
+        if ((int64_t)lo[u] + 4 > d.n_list) { pip_fault(d, PIP_FAULT_LIST); ni[u] = 0; cw[u] = CELL_EMPTY << 30; }
+        else lq[u] = *(const uint4*)(d.list_ent + lo[u]);   // the first four slots, all points at once
       }
     }
 #pragma unroll
@@ -555,6 +581,7 @@ __global__ __launch_bounds__(JTPB, GM_JOIN_WAVES) void k_pip_join(const double* 
         ni[u] = (int)lq[u].x;
         lo[u] += 1;
         lq[u] = make_uint4(lq[u].y, lq[u].z, lq[u].w, 0u);
+        if (ni[u] < 0 || (int64_t)lo[u] + ni[u] > d.n_list) { pip_fault(d, PIP_FAULT_LIST); ni[u] = 0; }
       }
     }
     // item walk; after the last tile the same loop drains the queue and ends
@@ -594,19 +621,27 @@ __global__ __launch_bounds__(JTPB, GM_JOIN_WAVES) void k_pip_join(const double* 
         }
         if (SPLIT) {
           const uint64_t mq = __ballot(blob);
-          if (blob) qi[qn + lanes_below(mq)] = make_uint2(eid, e & 0x3fffffffu);
-          qn += __popcll(mq);
+          if (qn + 64 > QCAP_S) { if (lane == 0 && mq) pip_fault(d, PIP_FAULT_QUEUE); }   // cannot happen: qn < QCAP_S - 64 here
+          else {
+            if (blob) qi[qn + lanes_below(mq)] = make_uint2(eid, e & 0x3fffffffu);
+            qn += __popcll(mq);
+          }
         } else {
           // line-entry items stack up from slot 0, blob items (compact and generic, rare once the
           // shortcuts apply) down from slot QCAP - 1, so an evaluation round runs one kind of code
           const bool cmp = (e & (BLOB_COMPACT | SC_LINE)) == (BLOB_COMPACT | SC_LINE) && d.line_ent;
           const uint64_t mc = __ballot(blob && cmp), mg = __ballot(blob && !cmp);
-          if (blob) {
-            const int o = cmp ? qn + lanes_below(mc) : QCAP - 1 - qg - lanes_below(mg);
-            qx[o] = ex; qy[o] = ey; qid[o] = eid; qb[o] = e & 0x3fffffffu;
+          // invariant: qn + qg < 64 before a step (the evaluation below restores it), so this step's
+          // <= 64 items fit the QCAP = 128 slots from both ends without meeting
+          if (qn + qg + 64 > QCAP) { if (lane == 0 && (mc | mg)) pip_fault(d, PIP_FAULT_QUEUE); }
+          else {
+            if (blob) {
+              const int o = cmp ? qn + lanes_below(mc) : QCAP - 1 - qg - lanes_below(mg);
+              qx[o] = ex; qy[o] = ey; qid[o] = eid; qb[o] = e & 0x3fffffffu;
+            }
+            qn += __popcll(mc);
+            qg += __popcll(mg);
           }
-          qn += __popcll(mc);
-          qg += __popcll(mg);
         }
       }
       if (SPLIT) {
@@ -1102,6 +1137,7 @@ template <int OP>
 __device__ __forceinline__ bool entry_pred(const PipDev& d, uint32_t e, double px, double py) {
   if ((e >> 30) == CELL_INTERIOR) return true;   // every point of the cell is interior
   const uint32_t ref = e & 0x3fffffffu;
+  if (!blob_ref_ok(d, ref)) { pip_fault(d, PIP_FAULT_BLOB); return false; }
   int loc;
   if (ref & BLOB_COMPACT) {
     int poly;
@@ -1205,7 +1241,9 @@ __global__ __launch_bounds__(FTPB, GM_QUERY_WAVES) void k_query_mask(const doubl
       bool hit;
       if ((w >> 30) == CELL_LIST) {
         int l0 = 4 * (int)((w & 0x3fffffffu) >> 4), ni = (int)(w & 15u);
-        if (ni == LIST_LONG) { ni = (int)d.list_ent[l0]; l0 += 1; }
+        if ((int64_t)l0 + 4 > d.n_list) { pip_fault(d, PIP_FAULT_LIST); ni = 0; }
+        else if (ni == LIST_LONG) { ni = (int)d.list_ent[l0]; l0 += 1; }
+        if (ni < 0 || (int64_t)l0 + ni > d.n_list) { pip_fault(d, PIP_FAULT_LIST); ni = 0; }
         hit = false;
         for (int j = 0; j < ni && !hit; ++j) hit = entry_pred<OP>(d, d.list_ent[l0 + j], px, py);
       } else {
@@ -1257,7 +1295,7 @@ __global__ __launch_bounds__(256) void k_pip_census(const double* __restrict__ p
     if (kind == CELL_EMPTY) { c[JC_FINE_EMPTY]++; continue; }
     if (kind == CELL_INTERIOR) { c[JC_FINE_INTERIOR]++; continue; }
     if (kind == CELL_BOUNDARY) {
-      if ((ref & BLOB_COMPACT) && (ref & SC_LINE) && d.line_ent) {
+      if ((ref & BLOB_COMPACT) && (ref & SC_LINE) && d.line_ent && (uint64_t)(ref & (SC_LINE - 1)) < (uint64_t)d.n_line) {
         c[JC_FINE_LINE]++;
         const uint64_t li = ref & (SC_LINE - 1);
         const int l = line_locate(d.line_ent[2 * li], d.line_ent[2 * li + 1], x, y, d);
@@ -1272,7 +1310,9 @@ __global__ __launch_bounds__(256) void k_pip_census(const double* __restrict__ p
     }
     c[JC_FINE_LIST]++;
     int l0 = 4 * (int)(ref >> 4), ni = (int)(w & 15u);
-    if (ni == LIST_LONG) { ni = (int)d.list_ent[l0]; l0 += 1; }
+    if ((int64_t)l0 + 4 > d.n_list) ni = 0;
+    else if (ni == LIST_LONG) { ni = (int)d.list_ent[l0]; l0 += 1; }
+    if (ni < 0 || (int64_t)l0 + ni > d.n_list) ni = 0;
     c[JC_LIST_ENTRIES] += ni;
     for (int j = 0; j < ni; ++j) c[JC_LIST_BLOBS] += (d.list_ent[l0 + j] >> 30) != CELL_INTERIOR;
   }
@@ -1300,6 +1340,7 @@ constexpr uint8_t LOC_NULL = 0xff;
 __device__ __forceinline__ int entry_poly(const PipDev& d, uint32_t e) {
   const uint32_t ref = e & 0x3fffffffu;
   if ((e >> 30) == CELL_INTERIOR) return (int)ref;
+  if (!blob_ref_ok(d, ref)) return -1;
   if (ref & BLOB_COMPACT) return (int)__double_as_longlong(d.compact[16 * (uint64_t)(ref & (BLOB_COMPACT - 1))]);
   return ((const int2*)(d.blob + 2 * (uint64_t)ref))->x;
 }
@@ -1307,6 +1348,7 @@ __device__ __forceinline__ int entry_poly(const PipDev& d, uint32_t e) {
 __device__ __forceinline__ int entry_locate(const PipDev& d, uint32_t e, double px, double py) {
   if ((e >> 30) == CELL_INTERIOR) return LOC_INTERIOR;
   const uint32_t ref = e & 0x3fffffffu;
+  if (!blob_ref_ok(d, ref)) { pip_fault(d, PIP_FAULT_BLOB); return LOC_EXTERIOR; }
   if (ref & BLOB_COMPACT) {
     int poly;
     return compact_locate((const dv2*)(d.compact + 16 * (uint64_t)(ref & (BLOB_COMPACT - 1))), px, py, poly);
@@ -1384,7 +1426,9 @@ __global__ __launch_bounds__(RTPB) void k_pip_relate(const int32_t* __restrict__
           queue = true;   // the blob's polygon is checked when it is walked
         } else if (kind == CELL_LIST) {
           int l0 = 4 * (int)((e & 0x3fffffffu) >> 4), ni = (int)(e & 15u);
-          if (ni == LIST_LONG) { ni = (int)d.list_ent[l0]; l0 += 1; }
+          if ((int64_t)l0 + 4 > d.n_list) { pip_fault(d, PIP_FAULT_LIST); ni = 0; }
+          else if (ni == LIST_LONG) { ni = (int)d.list_ent[l0]; l0 += 1; }
+          if (ni < 0 || (int64_t)l0 + ni > d.n_list) { pip_fault(d, PIP_FAULT_LIST); ni = 0; }
           int j = 0;
           while (j < ni && list_poly[l0 + j] != p[u]) ++j;
           if (j < ni) {
@@ -1907,6 +1951,7 @@ __device__ __forceinline__ bool seg_meets_box(double u1, double v1, double u2, d
 // segment list here, so their cells keep the blob.
 __device__ int analyze_cell(const PipDev& d, int64_t c, uint32_t w, uint32_t* word, uint4* ent) {
   if ((w >> 30) != CELL_BOUNDARY) return 0;
+  if (!blob_ref_ok(d, w & 0x3fffffffu)) return 0;   // an out-of-range reference stays for the join to report
   if (!(isfinite(d.inv_cw) && isfinite(d.inv_ch) && d.inv_cw > 0 && d.inv_ch > 0)) return 0;
   const bool cmp = (w & BLOB_COMPACT) != 0;
   const dv2* cb = (const dv2*)(d.compact + 16 * (uint64_t)(w & (BLOB_COMPACT - 1)));
@@ -2153,6 +2198,11 @@ int make_shortcut(gm_pip_index* ix) {
   ix->dev.cell_sc = (const uint32_t*)p;
   ix->dev.line_ent = nullptr;
   ix->n_lines = 0;
+  ix->dev.fault = nullptr;   // set per call (the call's scratch word)
+  ix->dev.n_line = 0;
+  ix->dev.n_compact_lines = ix->arr_bytes[5] / 128;
+  ix->dev.n_blob16 = ix->arr_bytes[7] / 16;
+  ix->dev.n_list = ix->arr_bytes[6] / 4;
   ix->dev.coarse_fmt = ix->n_polys < (1 << 14) ? COARSE_MAIN : COARSE_EMPTY_MASK;
   if (const char* f = getenv("GM_PIP_COARSE_FMT")) ix->dev.coarse_fmt = atoi(f) ? COARSE_MAIN : COARSE_EMPTY_MASK;   // tests
   if (ix->n_polys >= (1 << 14)) ix->dev.coarse_fmt = COARSE_EMPTY_MASK;   // main ids need 14 bits
@@ -2185,6 +2235,7 @@ int make_shortcut(gm_pip_index* ix) {
     ix->allocs.push_back(e);
     ix->dev.line_ent = (const uint4*)e;
     ix->n_lines = nl;
+    ix->dev.n_line = nl;
     hipLaunchKernelGGL(k_build_shortcut<true>, dim3(g), dim3(256), 0, s, ix->dev, ncell, (uint32_t*)p, (int32_t*)fl,
                        (const int64_t*)sl, (uint4*)e);
   }
@@ -2503,6 +2554,16 @@ int build_cells_device(gm_ctx* ctx, gm_pip_index* ix, const gm_polyset* ps, cons
 
 // persistent grid: exactly the resident block count of this kernel (a rounded multiple of 8 for
 // the XCD-aware mapping), so no partial second round of blocks forms a tail
+// a reference check of the join failed on the device (PIP_FAULT_* bits): nothing of the call's
+// output is trusted
+static int index_fault(const char* what, uint32_t bits) {
+  char msg[160];
+  snprintf(msg, sizeof msg, "%s: device reference check failed (PIP_FAULT bits 0x%x): corrupt index or internal "
+           "queue invariant", what, bits);
+  set_error(msg);
+  return GM_E_INDEX;
+}
+
 template <class K>
 static unsigned resident_grid(K kernel, int device, int64_t ntiles, bool xcd_multiple) {
   const int resident = resident_blocks((const void*)kernel, device, JTPB, 4);
@@ -2527,6 +2588,7 @@ static int join_direct_arrow(gm_ctx* ctx, const gm_pip_index* ix, ArrowPts ap, i
                              int64_t* pt_ids, int32_t* poly_ids, int64_t cap, unsigned long long* counter, int32_t op) {
   PipDev dv = ix->dev;
   dv.op = op;
+  dv.fault = (uint32_t*)(counter + 1);
   const bool write = pt_ids && poly_ids;
   const int64_t CHUNK = join_chunk(ctx, (int64_t)1 << 31);
   const size_t tb = SRC == 2 ? 8 : 16;
@@ -3101,7 +3163,8 @@ int gm_pip_join_pred(gm_ctx* ctx, const gm_pip_index* ix, const double* px, cons
   if (n > 0 && (!px || !py)) return GM_E_INVALID;
   GM_HIP(hipSetDevice(ctx->device));
   unsigned long long* counter = (unsigned long long*)ctx->d_scratch;
-  GM_HIP(hipMemsetAsync(counter, 0, 8, ctx->stream));
+  dv.fault = (uint32_t*)(counter + 1);   // reference-check bits (PIP_FAULT_*), read back with the pair count
+  GM_HIP(hipMemsetAsync(counter, 0, 16, ctx->stream));
   // AUTO = DIRECT at every size: measured on MI355X (1B CONUS points x 3,200 polygons) the direct pass takes 20 ms,
   // against 23 ms for the split pass and 39 ms for partition + join; the others stay
   // selectable
@@ -3242,9 +3305,10 @@ int gm_pip_join_pred(gm_ctx* ctx, const gm_pip_index* ix, const double* px, cons
     if (rc) return rc;
   }
   if (n_pairs) {
-    GM_HIP(hipMemcpyAsync(ctx->h_pinned, counter, 8, hipMemcpyDeviceToHost, ctx->stream));
+    GM_HIP(hipMemcpyAsync(ctx->h_pinned, counter, 16, hipMemcpyDeviceToHost, ctx->stream));
     GM_HIP(hipStreamSynchronize(ctx->stream));
     *n_pairs = ctx->h_pinned[0];
+    if (ctx->h_pinned[1]) return index_fault("gm_pip_join", (uint32_t)ctx->h_pinned[1]);
     if (write && *n_pairs > cap) return GM_E_CAPACITY;
   }
   return GM_OK;
@@ -3264,13 +3328,14 @@ int gm_pip_join_arrow(gm_ctx* ctx, const gm_pip_index* ix, const gm_geom_column*
   const ArrowPts ap{pts->coords, pts->validity, pts->validity_offset, pts->flip_axis, pts->ordinal_bits == 32};
   if (mode == GM_JOIN_AUTO || mode == GM_JOIN_DIRECT) {
     unsigned long long* counter = (unsigned long long*)ctx->d_scratch;
-    GM_HIP(hipMemsetAsync(counter, 0, 8, ctx->stream));
+    GM_HIP(hipMemsetAsync(counter, 0, 16, ctx->stream));
     int rc = n == 0 ? GM_OK
              : ap.f32 ? join_direct_arrow<2>(ctx, ix, ap, n, id_base, pt_ids, poly_ids, cap, counter, op)
                       : join_direct_arrow<1>(ctx, ix, ap, n, id_base, pt_ids, poly_ids, cap, counter, op);
     if (rc) return rc;
-    GM_HIP(hipMemcpyAsync(ctx->h_pinned, counter, 8, hipMemcpyDeviceToHost, ctx->stream));
+    GM_HIP(hipMemcpyAsync(ctx->h_pinned, counter, 16, hipMemcpyDeviceToHost, ctx->stream));
     GM_HIP(hipStreamSynchronize(ctx->stream));
+    if (ctx->h_pinned[1]) return index_fault("gm_pip_join_arrow", (uint32_t)ctx->h_pinned[1]);
     const int64_t total = ctx->h_pinned[0];
     if (n_pairs) *n_pairs = total;
     return (pt_ids && total > cap) ? GM_E_CAPACITY : GM_OK;

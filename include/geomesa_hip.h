@@ -41,6 +41,8 @@ extern "C" {
 #define GM_E_HIP (-2)         /* HIP runtime failure; see gm_last_error() */
 #define GM_E_CAPACITY (-3)    /* output capacity too small; the needed size is reported */
 #define GM_E_ELEMENT (-4)     /* at least one element failed (only when no status[] and no summary) */
+#define GM_E_INDEX (-5)       /* a device-side reference check of a join failed (corrupt or mismatched index,
+                                 or a broken internal invariant); the call's output is not valid */
 
 /* per-element status codes */
 /* BinnedTime periods (TimePeriod, z3/curve/BinnedTime.scala:283-291) */
