@@ -705,6 +705,244 @@ __global__ __launch_bounds__(JTPB, GM_JOIN_WAVES) void k_pip_join(const double* 
   }
 }
 
+// ---------------------------------------------------------------- the direct pass, stage queues
+// The direct join as three stages joined by per-wave LDS queues, so that every gather beyond L2 is
+// issued by a full wave (64 independent addresses) and many are in flight at once:
+//   1. stream: a step is 128 consecutive points of the wave's stream, 2 per lane (16-B pair loads
+//      of x and y; the next step's loads are issued while this one is processed).  Their coarse
+//      words (L2-resident) decide INTERIOR / EMPTY coarse cells (after the sub-block masks); the
+//      other points go to the fine queue F.
+//   2. fine: whenever F holds 128 points, 2 per lane take their fine words (cell_sc) in one go and
+//      resolve them one after the other: INTERIOR / EMPTY decide; a LINE word or a blob word becomes
+//      an item; a LIST word walks its entries (INTERIOR: a pair; a blob: an item), one per lane per
+//      loop trip.
+//   3. items: line-entry items stack up from slot 0 of the item queue, blob items down from slot
+//      ICAP - 1; whenever 64 are queued, one kind runs on all lanes: a line entry decides from its
+//      quantized lines or hands its blob over as a blob item, a blob is walked (PointLocator).
+// One loop runs the stages by priority (items, list walks, pending fine words, fine rounds, the
+// stream), so each stage's code exists once and the queues stay bounded: the item queue holds < 64
+// before any push of <= 64 (and a line round hands over at most the items it took), F < 128 before
+// a stream step pushes <= 128.  Both are checked (PIP_FAULT_QUEUE).  Pairs are staged per wave and
+// flushed with one atomic per flush.
+constexpr int QTPB = 256;           // 4 waves per block
+constexpr int FCAP = 256;           // fine queue (< 128 + one step's 128)
+constexpr int FBATCH = 128;         // fine words per round (2 per lane)
+constexpr int ICAP = 128;           // item queue (two ends)
+constexpr int PCAP = 192;           // pair staging
+
+template <bool WRITE, int SRC, bool VEC>
+__global__ __launch_bounds__(QTPB) void k_pip_join_q(const double* __restrict__ px, const double* __restrict__ py,
+                                                     int64_t n, int64_t id_base, PipDev d,
+                                                     int64_t* __restrict__ pt_ids, int32_t* __restrict__ poly_ids,
+                                                     int64_t cap, unsigned long long* __restrict__ counter, ArrowPts ap) {
+  constexpr int NW = QTPB / 64;
+  __shared__ double s_fx[NW][FCAP], s_fy[NW][FCAP];
+  __shared__ uint32_t s_fid[NW][FCAP];
+  __shared__ double s_ix[NW][ICAP], s_iy[NW][ICAP];
+  __shared__ uint32_t s_iid[NW][ICAP], s_iref[NW][ICAP];
+  __shared__ uint32_t s_pid[WRITE ? NW : 1][WRITE ? PCAP : 1];
+  __shared__ int32_t s_ppl[WRITE ? NW : 1][WRITE ? PCAP : 1];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  double* fx = s_fx[wv]; double* fy = s_fy[wv]; uint32_t* fid = s_fid[wv];
+  double* qx = s_ix[wv]; double* qy = s_iy[wv]; uint32_t* qid = s_iid[wv]; uint32_t* qref = s_iref[wv];
+  uint32_t* wpt = s_pid[WRITE ? wv : 0];
+  int32_t* wpl = s_ppl[WRITE ? wv : 0];
+  int fn = 0, qn = 0, qg = 0, wn = 0;   // wave-uniform fills: fine queue, line items, blob items, pairs
+  int my_count = 0;
+  const bool lines_on = d.line_ent != nullptr;
+
+  auto pair_push = [&](bool hit, uint32_t id, int poly) __attribute__((always_inline)) {
+    if (!WRITE) { my_count += hit; return; }
+    const uint64_t m = __ballot(hit);
+    if (!m) return;
+    if (wn + 64 > PCAP) { flush_pairs(wpt, wpl, wn, lane, id_base, pt_ids, poly_ids, cap, counter); wn = 0; }
+    if (hit) { const int o = wn + lanes_below(m); wpt[o] = id; wpl[o] = poly; }
+    wn += __popcll(m);
+  };
+  auto item_push = [&](bool valid, bool is_line, double x, double y, uint32_t id, uint32_t ref) __attribute__((always_inline)) {
+    const uint64_t ml = __ballot(valid && is_line), mb = __ballot(valid && !is_line);
+    if (!(ml | mb)) return;
+    if (qn + qg + 64 > ICAP) { if (lane == 0) pip_fault(d, PIP_FAULT_QUEUE); return; }   // cannot happen: < 64 here
+    if (valid) {
+      const int o = is_line ? qn + lanes_below(ml) : ICAP - 1 - qg - lanes_below(mb);
+      qx[o] = x; qy[o] = y; qid[o] = id; qref[o] = ref;
+    }
+    qn += __popcll(ml);
+    qg += __popcll(mb);
+  };
+
+  // stream: step k of this wave covers pairs [k * 64, k * 64 + 64) of its share, 2 points per lane
+  const int64_t npair = (n + 1) >> 1;
+  const int64_t nstep = (npair + 63) >> 6;
+  const int64_t wstride = (int64_t)gridDim.x * NW;
+  int64_t step = (int64_t)blockIdx.x * NW + wv;
+  auto load_pair = [&](int64_t k, double& x0, double& x1, double& y0, double& y1) __attribute__((always_inline)) {
+    const int64_t i = 2 * (k * 64 + lane);
+    x0 = x1 = y0 = y1 = NAN;
+    if (k >= nstep) return;
+    if (SRC == 0) {
+      if (VEC && i + 1 < n) {
+        const dv2 a = __builtin_nontemporal_load((const dv2*)(px + i));
+        const dv2 b = __builtin_nontemporal_load((const dv2*)(py + i));
+        x0 = a.x; x1 = a.y; y0 = b.x; y1 = b.y;
+      } else {
+        if (i < n) { x0 = px[i]; y0 = py[i]; }
+        if (i + 1 < n) { x1 = px[i + 1]; y1 = py[i + 1]; }
+      }
+    } else {   // Arrow tuples; null slots keep NaN (no cell, no pair)
+      if (i < n && arrow_valid(ap.valid, ap.voff, i)) arrow_tuple<SRC == 2>(ap.c, i, ap.flip, x0, y0);
+      if (i + 1 < n && arrow_valid(ap.valid, ap.voff, i + 1)) arrow_tuple<SRC == 2>(ap.c, i + 1, ap.flip, x1, y1);
+    }
+  };
+  double X0, X1, Y0, Y1, NX0, NX1, NY0, NY1;
+  load_pair(step, X0, X1, Y0, Y1);
+  load_pair(step + wstride, NX0, NX1, NY0, NY1);
+
+  // pending fine words (fine round -> resolve), and the list walk of the one being resolved
+  int pend = 0;                      // wave-uniform: pending words left (slot a then slot b)
+  uint32_t wa = 0, wb = 0, ia = 0, ib = 0;
+  double xa = 0.0, ya = 0.0, xb = 0.0, yb = 0.0;
+  bool list_on = false;              // wave-uniform: some lane walks a list
+  int l_lo = 0, l_n = 0, l_j = 0;
+  double lx = 0.0, ly = 0.0;
+  uint32_t lid = 0;
+
+  for (;;) {
+    // every other stage idle: the item stage drains what is left (a line round may hand blobs over)
+    const bool idle = !list_on && pend == 0 && fn == 0 && step >= nstep;
+    if (qn + qg >= 64 || (idle && qn + qg > 0)) {   // ---- items: one round of the fuller kind
+      wave_lds_sync();
+      const bool lines = qn >= qg;
+      const int kq = min(lines ? qn : qg, 64);
+      const int slot = lines ? qn - kq + lane : ICAP - qg + lane;
+      const bool act = lane < kq;
+      double x = 0.0, y = 0.0;
+      uint32_t id = 0, ref = 0;
+      if (act) { x = qx[slot]; y = qy[slot]; id = qid[slot]; ref = qref[slot]; }
+      wave_lds_sync();
+      if (lines) qn -= kq;
+      else qg -= kq;
+      int poly = 0;
+      if (lines) {
+        int loc = -1;
+        uint32_t blob = 0;
+        if (act) {
+          const uint64_t li = ref & (SC_LINE - 1);
+          if (li >= (uint64_t)d.n_line) { pip_fault(d, PIP_FAULT_LINE); loc = LOC_EXTERIOR; }
+          else {
+            const uint4 e0 = d.line_ent[2 * li], e1 = d.line_ent[2 * li + 1];
+            poly = (int)e0.y;
+            loc = line_locate(e0, e1, x, y, d);
+            blob = e0.x & 0x3fffffffu;
+          }
+        }
+        pair_push(act && loc >= 0 && join_hit(d.op, loc), id, poly);
+        // near a line: the entry's own blob, as a blob item (fits: at most kq were taken)
+        const bool fb = act && loc < 0;
+        const uint64_t mb = __ballot(fb);
+        if (fb) {
+          const int o = ICAP - 1 - qg - lanes_below(mb);
+          qx[o] = x; qy[o] = y; qid[o] = id; qref[o] = blob;
+        }
+        qg += __popcll(mb);
+      } else {
+        const int loc = act ? item_locate(d, ref, x, y, poly) : LOC_EXTERIOR;
+        pair_push(act && join_hit(d.op, loc), id, poly);
+      }
+      continue;
+    }
+    if (list_on) {   // ---- one entry of each walking lane's list
+      const bool act = l_j < l_n;
+      const uint32_t e = act ? d.list_ent[l_lo + l_j] : (CELL_EMPTY << 30);
+      pair_push(act && (e >> 30) == CELL_INTERIOR, lid, (int)(e & 0x3fffffffu));
+      item_push(act && (e >> 30) == CELL_BOUNDARY, false, lx, ly, lid, e & 0x3fffffffu);
+      ++l_j;
+      list_on = __ballot(l_j < l_n) != 0;
+      continue;
+    }
+    if (pend > 0) {   // ---- resolve one pending fine word per lane (slot a, then slot b)
+      const bool sa = pend == 2;
+      const uint32_t w = sa ? wa : wb, id = sa ? ia : ib;
+      const double x = sa ? xa : xb, y = sa ? ya : yb;
+      --pend;
+      const uint32_t kind = w >> 30, ref = w & 0x3fffffffu;
+      pair_push(kind == CELL_INTERIOR, id, (int)ref);
+      const bool item = kind == CELL_BOUNDARY;
+      item_push(item, item && lines_on && (ref & (BLOB_COMPACT | SC_LINE)) == (BLOB_COMPACT | SC_LINE), x, y, id, ref);
+      const bool is_list = kind == CELL_LIST;
+      l_j = 0;
+      l_n = 0;
+      if (is_list) {
+        l_lo = 4 * (int)(ref >> 4);
+        l_n = (int)(w & 15u);
+        if ((int64_t)l_lo + 4 > d.n_list) { pip_fault(d, PIP_FAULT_LIST); l_n = 0; }
+        else if (l_n == LIST_LONG) { l_n = (int)d.list_ent[l_lo]; l_lo += 1; }
+        if (l_n < 0 || (int64_t)l_lo + l_n > d.n_list) { pip_fault(d, PIP_FAULT_LIST); l_n = 0; }
+        lx = x; ly = y; lid = id;
+      }
+      list_on = __ballot(l_j < l_n) != 0;
+      continue;
+    }
+    const bool streaming = step < nstep;
+    if (fn >= FBATCH || (!streaming && fn > 0)) {   // ---- fine round: the newest min(fn, 128) points
+      wave_lds_sync();
+      const int cnt = min(fn, FBATCH);
+      const int a = fn - cnt + lane, b = a + 64;
+      const bool act_a = lane < cnt, act_b = lane + 64 < cnt;
+      xa = ya = xb = yb = 0.0;
+      ia = ib = 0;
+      if (act_a) { xa = fx[a]; ya = fy[a]; ia = fid[a]; }
+      if (act_b) { xb = fx[b]; yb = fy[b]; ib = fid[b]; }
+      wave_lds_sync();
+      fn -= cnt;
+      wa = wb = CELL_EMPTY << 30;
+      if (act_a) wa = d.cell_sc[(int64_t)cell_of(ya, d.gy0, d.inv_ch, d.gy) * d.gx + cell_of(xa, d.gx0, d.inv_cw, d.gx)];
+      if (act_b) wb = d.cell_sc[(int64_t)cell_of(yb, d.gy0, d.inv_ch, d.gy) * d.gx + cell_of(xb, d.gx0, d.inv_cw, d.gx)];
+      pend = cnt > 64 ? 2 : 1;
+      if (pend == 1) { wb = wa; xb = xa; yb = ya; ib = ia; }   // one slot: it is "b" (pend 1 resolves b)
+      continue;
+    }
+    if (streaming) {   // ---- stream step: 2 points per lane, their coarse words together
+      uint32_t c0 = CELL_EMPTY << 30, c1 = CELL_EMPTY << 30;
+      int cx0 = 0, cy0 = 0, cx1 = 0, cy1 = 0;
+      const bool g0 = X0 >= d.gx0 && X0 <= d.gx1 && Y0 >= d.gy0 && Y0 <= d.gy1;   // NaN fails
+      const bool g1 = X1 >= d.gx0 && X1 <= d.gx1 && Y1 >= d.gy0 && Y1 <= d.gy1;
+      if (g0) {
+        cx0 = cell_of(X0, d.gx0, d.inv_cw, d.gx); cy0 = cell_of(Y0, d.gy0, d.inv_ch, d.gy);
+        c0 = d.coarse_sc[(int64_t)(cy0 >> CF_LOG) * d.gxc + (cx0 >> CF_LOG)];
+      }
+      if (g1) {
+        cx1 = cell_of(X1, d.gx0, d.inv_cw, d.gx); cy1 = cell_of(Y1, d.gy0, d.inv_ch, d.gy);
+        c1 = d.coarse_sc[(int64_t)(cy1 >> CF_LOG) * d.gxc + (cx1 >> CF_LOG)];
+      }
+      c0 = coarse_mask(c0, cx0, cy0, d.coarse_fmt);
+      c1 = coarse_mask(c1, cx1, cy1, d.coarse_fmt);
+      const uint32_t id0 = (uint32_t)(2 * (step * 64 + lane)), id1 = id0 + 1;
+      pair_push((c0 >> 30) == CELL_INTERIOR, id0, (int)(c0 & 0x3fffffffu));
+      pair_push((c1 >> 30) == CELL_INTERIOR, id1, (int)(c1 & 0x3fffffffu));
+      const bool f0 = (c0 >> 30) == CELL_LIST, f1 = (c1 >> 30) == CELL_LIST;
+      const uint64_t m0 = __ballot(f0), m1 = __ballot(f1);
+      if (fn + 128 > FCAP) { if (lane == 0 && (m0 | m1)) pip_fault(d, PIP_FAULT_QUEUE); }   // cannot happen: fn < 128
+      else {
+        if (f0) { const int o = fn + lanes_below(m0); fx[o] = X0; fy[o] = Y0; fid[o] = id0; }
+        fn += __popcll(m0);
+        if (f1) { const int o = fn + lanes_below(m1); fx[o] = X1; fy[o] = Y1; fid[o] = id1; }
+        fn += __popcll(m1);
+      }
+      step += wstride;
+      X0 = NX0; X1 = NX1; Y0 = NY0; Y1 = NY1;
+      load_pair(step + wstride, NX0, NX1, NY0, NY1);
+      continue;
+    }
+    break;   // every stage idle and the item queue empty (the item stage drains it once nothing else runs)
+  }
+  if (WRITE && wn > 0) flush_pairs(wpt, wpl, wn, lane, id_base, pt_ids, poly_ids, cap, counter);
+  if (!WRITE) {
+    for (int off = 32; off > 0; off >>= 1) my_count += __shfl_down(my_count, off, 64);
+    if (lane == 0 && my_count) atomicAdd(counter, (unsigned long long)my_count);
+  }
+}
+
 // Evaluation of the split pass's work list: one (row, blob) item per lane, every lane busy with
 // the same kind of work (JTS RayCrossingCounter over the blob's segments, compact or generic).
 // The row's coordinates are re-read from the point columns; items come in roughly ascending row
@@ -2582,6 +2820,24 @@ static unsigned join_grid(int device, int64_t ntiles) {
   return resident_grid(k_pip_join<WRITE, REC, SPLIT, SRC>, device, ntiles, REC);
 }
 
+// the staged direct pass (k_pip_join_q) over rows [0, m) of one chunk; GM_PIP_JOIN_LEGACY=1 selects
+// the round-2 single-stage kernel (k_pip_join) for A/B measurement
+static bool join_legacy() {
+  const char* e = getenv("GM_PIP_JOIN_LEGACY");
+  return e && atoi(e) != 0;
+}
+
+template <bool WRITE, int SRC, bool VEC>
+static void launch_join_q(gm_ctx* ctx, const double* px, const double* py, int64_t m, int64_t id_base, const PipDev& dv,
+                          int64_t* pt_ids, int32_t* poly_ids, int64_t cap, unsigned long long* counter, ArrowPts ap) {
+  const int64_t wsteps = ((m + 1) / 2 + 63) / 64;   // 128-point stream steps, one wave each
+  const int64_t blocks = (wsteps + QTPB / 64 - 1) / (QTPB / 64);
+  const int resident = resident_blocks((const void*)k_pip_join_q<WRITE, SRC, VEC>, ctx->device, QTPB, 4);
+  const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(resident, blocks));
+  hipLaunchKernelGGL((k_pip_join_q<WRITE, SRC, VEC>), dim3(grid), dim3(QTPB), 0, ctx->stream, px, py, m, id_base, dv,
+                     pt_ids, poly_ids, cap, counter, ap);
+}
+
 // the direct pass over an Arrow point column (tuples read in place)
 template <int SRC>
 static int join_direct_arrow(gm_ctx* ctx, const gm_pip_index* ix, ArrowPts ap, int64_t n, int64_t id_base,
@@ -2598,7 +2854,10 @@ static int join_direct_arrow(gm_ctx* ctx, const gm_pip_index* ix, ArrowPts ap, i
     ArrowPts a = ap;
     a.c = (const char*)ap.c + (size_t)c0 * tb;
     a.voff = ap.voff + c0;
-    if (write)
+    if (!join_legacy()) {
+      if (write) launch_join_q<true, SRC, false>(ctx, nullptr, nullptr, m, id_base + c0, dv, pt_ids, poly_ids, cap, counter, a);
+      else launch_join_q<false, SRC, false>(ctx, nullptr, nullptr, m, id_base + c0, dv, pt_ids, poly_ids, cap, counter, a);
+    } else if (write)
       hipLaunchKernelGGL((k_pip_join<true, false, false, SRC>), dim3(join_grid<true, false, false, SRC>(ctx->device, ntiles)),
                          dim3(JTPB), 0, ctx->stream, nullptr, nullptr, nullptr, nullptr, m, id_base + c0, dv,
                          pt_ids, poly_ids, cap, counter, SplitArgs{}, a);
@@ -3170,9 +3429,18 @@ int gm_pip_join_pred(gm_ctx* ctx, const gm_pip_index* ix, const double* px, cons
   // selectable
   if ((mode == GM_JOIN_AUTO || mode == GM_JOIN_DIRECT) && n > 0) {
     const int64_t CHUNK = join_chunk(ctx, (int64_t)1 << 31);  // LDS staging keeps 32-bit row offsets
+    const bool vec = aligned16(px) && aligned16(py);   // chunk starts stay 16-B aligned (CHUNK is even)
     for (int64_t c0 = 0; c0 < n; c0 += CHUNK) {
       const int64_t m = std::min(CHUNK, n - c0);
       const int64_t ntiles = (m + JTILE - 1) / JTILE;
+      if (!join_legacy()) {
+        if (write && vec) launch_join_q<true, 0, true>(ctx, px + c0, py + c0, m, id_base + c0, dv, pt_ids, poly_ids, cap, counter, ArrowPts{});
+        else if (write) launch_join_q<true, 0, false>(ctx, px + c0, py + c0, m, id_base + c0, dv, pt_ids, poly_ids, cap, counter, ArrowPts{});
+        else if (vec) launch_join_q<false, 0, true>(ctx, px + c0, py + c0, m, id_base + c0, dv, pt_ids, poly_ids, cap, counter, ArrowPts{});
+        else launch_join_q<false, 0, false>(ctx, px + c0, py + c0, m, id_base + c0, dv, pt_ids, poly_ids, cap, counter, ArrowPts{});
+        GM_CHECK_LAUNCH();
+        continue;
+      }
       const unsigned grid = write ? join_grid<true, false, false>(ctx->device, ntiles)
                                   : join_grid<false, false, false>(ctx->device, ntiles);
       if (write)
