@@ -75,8 +75,8 @@ def test_queue_both_kinds_interleaved(gpu, oracle, block):
     ps = synthetic_counties(20, 10)
     rng = np.random.default_rng(block)
     ppo, pro, rvo, vx, vy = ps.to_arrays()
-    ex, ey = _edge_points(ps, 1e-4, rng, 24 * JTILE)
-    k = rng.choice(len(vx), 24 * JTILE)
+    ex, ey = _edge_points(ps, 1e-4, rng, 48 * JTILE)
+    k = rng.choice(len(vx), 48 * JTILE)
     bx, by = vx[k], vy[k]
     px = np.empty(48 * JTILE); py = np.empty(48 * JTILE)
     idx = np.arange(48 * JTILE)
