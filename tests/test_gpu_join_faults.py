@@ -106,7 +106,7 @@ def test_arrow_nulls_at_tile_ends(gpu, oracle, f32):
         nulls[t] = True
         nulls[min(n - 1, t + JTILE - 1)] = True
     nulls[-1] = True
-    idx = arrow.ArrowPolygonIndex(polyset_to_arrow(ps, f32=f32), kind="multipolygon")
+    idx = arrow.ArrowPolygonIndex(polyset_to_arrow(ps), kind="multipolygon")   # polygons stay Float8
     pt, pl = idx.join(point_array(px, py, nulls, f32=f32), mode="auto")
     got = set(zip(as_np(pt).tolist(), as_np(pl).tolist()))
     opt, opl = oracle.OraclePolySet(*ps.to_arrays()).join(px, py, nthreads=8)
