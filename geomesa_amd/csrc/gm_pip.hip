@@ -724,20 +724,26 @@ __global__ __launch_bounds__(JTPB, GM_JOIN_WAVES) void k_pip_join(const double* 
 // before any push of <= 64 (and a line round hands over at most the items it took), F < 128 before
 // a stream step pushes <= 128.  Both are checked (PIP_FAULT_QUEUE).  Pairs are staged per wave and
 // flushed with one atomic per flush.
+#ifndef GM_JQ_WAVES
+#define GM_JQ_WAVES 4               // blocks per CU (= waves per SIMD) the register allocation targets
+#endif
 constexpr int QTPB = 256;           // 4 waves per block
-constexpr int FCAP = 256;           // fine queue (< 128 + one step's 128)
-constexpr int FBATCH = 128;         // fine words per round (2 per lane)
+#ifndef GM_JQ_FBATCH
+#define GM_JQ_FBATCH 128
+#endif
+constexpr int FBATCH = GM_JQ_FBATCH;   // fine words per round (64: 1 per lane, 128: 2 per lane)
+constexpr int FCAP = FBATCH + 128;     // fine queue (< FBATCH + one step's 128)
 constexpr int ICAP = 128;           // item queue (two ends)
 constexpr int PCAP = 192;           // pair staging
 
 template <bool WRITE, int SRC, bool VEC>
-__global__ __launch_bounds__(QTPB) void k_pip_join_q(const double* __restrict__ px, const double* __restrict__ py,
+__global__ __launch_bounds__(QTPB, GM_JQ_WAVES) void k_pip_join_q(const double* __restrict__ px, const double* __restrict__ py,
                                                      int64_t n, int64_t id_base, PipDev d,
                                                      int64_t* __restrict__ pt_ids, int32_t* __restrict__ poly_ids,
                                                      int64_t cap, unsigned long long* __restrict__ counter, ArrowPts ap) {
   constexpr int NW = QTPB / 64;
   __shared__ double s_fx[NW][FCAP], s_fy[NW][FCAP];
-  __shared__ uint32_t s_fid[NW][FCAP];
+  __shared__ uint32_t s_fid[NW][FCAP], s_fw[NW][FCAP];
   __shared__ double s_ix[NW][ICAP], s_iy[NW][ICAP];
   __shared__ uint32_t s_iid[NW][ICAP], s_iref[NW][ICAP];
   __shared__ uint32_t s_pid[WRITE ? NW : 1][WRITE ? PCAP : 1];
@@ -751,11 +757,13 @@ __global__ __launch_bounds__(QTPB) void k_pip_join_q(const double* __restrict__ 
   int my_count = 0;
   const bool lines_on = d.line_ent != nullptr;
 
+  // pairs are staged without a flush here: the loop flushes at its top while wn > PCAP - 128, and one
+  // trip pushes at most 128 (a stream step's two points per lane)
   auto pair_push = [&](bool hit, uint32_t id, int poly) __attribute__((always_inline)) {
     if (!WRITE) { my_count += hit; return; }
     const uint64_t m = __ballot(hit);
     if (!m) return;
-    if (wn + 64 > PCAP) { flush_pairs(wpt, wpl, wn, lane, id_base, pt_ids, poly_ids, cap, counter); wn = 0; }
+    if (wn + __popcll(m) > PCAP) { if (lane == 0) pip_fault(d, PIP_FAULT_QUEUE); return; }   // cannot happen
     if (hit) { const int o = wn + lanes_below(m); wpt[o] = id; wpl[o] = poly; }
     wn += __popcll(m);
   };
@@ -798,18 +806,18 @@ __global__ __launch_bounds__(QTPB) void k_pip_join_q(const double* __restrict__ 
   load_pair(step, X0, X1, Y0, Y1);
   load_pair(step + wstride, NX0, NX1, NY0, NY1);
 
-  // pending fine words (fine round -> resolve), and the list walk of the one being resolved
-  int pend = 0;                      // wave-uniform: pending words left (slot a then slot b)
-  uint32_t wa = 0, wb = 0, ia = 0, ib = 0;
-  double xa = 0.0, ya = 0.0, xb = 0.0, yb = 0.0;
+  // pending fine words: a fine round leaves its window [pb, pb + pc) of the fine queue in place and
+  // stores each point's word beside it (s_fw); the window is resolved in two halves of 64 and only
+  // then released.  The list walk of a half reads its point back from the window.
+  int pb = 0, pc = 0, hn = 0, hd = 0;   // wave-uniform: window base and size, next half, halves
   bool list_on = false;              // wave-uniform: some lane walks a list
-  int l_lo = 0, l_n = 0, l_j = 0;
-  double lx = 0.0, ly = 0.0;
-  uint32_t lid = 0;
+  int l_slot = 0, l_lo = 0, l_n = 0, l_j = 0;
+  uint32_t* fw = s_fw[wv];
 
   for (;;) {
+    if (WRITE && wn > PCAP - 128) { flush_pairs(wpt, wpl, wn, lane, id_base, pt_ids, poly_ids, cap, counter); wn = 0; }
     // every other stage idle: the item stage drains what is left (a line round may hand blobs over)
-    const bool idle = !list_on && pend == 0 && fn == 0 && step >= nstep;
+    const bool idle = !list_on && hn == hd && fn == 0 && step >= nstep;
     if (qn + qg >= 64 || (idle && qn + qg > 0)) {   // ---- items: one round of the fuller kind
       wave_lds_sync();
       const bool lines = qn >= qg;
@@ -854,33 +862,39 @@ __global__ __launch_bounds__(QTPB) void k_pip_join_q(const double* __restrict__ 
     if (list_on) {   // ---- one entry of each walking lane's list
       const bool act = l_j < l_n;
       const uint32_t e = act ? d.list_ent[l_lo + l_j] : (CELL_EMPTY << 30);
-      pair_push(act && (e >> 30) == CELL_INTERIOR, lid, (int)(e & 0x3fffffffu));
-      item_push(act && (e >> 30) == CELL_BOUNDARY, false, lx, ly, lid, e & 0x3fffffffu);
+      double x = 0.0, y = 0.0;
+      uint32_t id = 0;
+      if (act) { x = fx[l_slot]; y = fy[l_slot]; id = fid[l_slot]; }
+      pair_push(act && (e >> 30) == CELL_INTERIOR, id, (int)(e & 0x3fffffffu));
+      item_push(act && (e >> 30) == CELL_BOUNDARY, false, x, y, id, e & 0x3fffffffu);
       ++l_j;
       list_on = __ballot(l_j < l_n) != 0;
       continue;
     }
-    if (pend > 0) {   // ---- resolve one pending fine word per lane (slot a, then slot b)
-      const bool sa = pend == 2;
-      const uint32_t w = sa ? wa : wb, id = sa ? ia : ib;
-      const double x = sa ? xa : xb, y = sa ? ya : yb;
-      --pend;
+    if (hn < hd) {   // ---- resolve one half of the pending window
+      const int slot = pb + hn * 64 + lane;
+      const bool act = slot < pb + pc;
+      ++hn;
+      uint32_t w = CELL_EMPTY << 30, id = 0;
+      double x = 0.0, y = 0.0;
+      if (act) { w = fw[slot]; x = fx[slot]; y = fy[slot]; id = fid[slot]; }
       const uint32_t kind = w >> 30, ref = w & 0x3fffffffu;
       pair_push(kind == CELL_INTERIOR, id, (int)ref);
       const bool item = kind == CELL_BOUNDARY;
       item_push(item, item && lines_on && (ref & (BLOB_COMPACT | SC_LINE)) == (BLOB_COMPACT | SC_LINE), x, y, id, ref);
-      const bool is_list = kind == CELL_LIST;
       l_j = 0;
       l_n = 0;
-      if (is_list) {
+      if (kind == CELL_LIST) {
+        l_slot = slot;
         l_lo = 4 * (int)(ref >> 4);
         l_n = (int)(w & 15u);
         if ((int64_t)l_lo + 4 > d.n_list) { pip_fault(d, PIP_FAULT_LIST); l_n = 0; }
         else if (l_n == LIST_LONG) { l_n = (int)d.list_ent[l_lo]; l_lo += 1; }
         if (l_n < 0 || (int64_t)l_lo + l_n > d.n_list) { pip_fault(d, PIP_FAULT_LIST); l_n = 0; }
-        lx = x; ly = y; lid = id;
       }
       list_on = __ballot(l_j < l_n) != 0;
+      if (hn == hd) fn = pb;  // the window is released once its last half is resolved (list walks
+                              // of that half run next, before anything can push to the queue)
       continue;
     }
     const bool streaming = step < nstep;
@@ -888,18 +902,17 @@ __global__ __launch_bounds__(QTPB) void k_pip_join_q(const double* __restrict__ 
       wave_lds_sync();
       const int cnt = min(fn, FBATCH);
       const int a = fn - cnt + lane, b = a + 64;
-      const bool act_a = lane < cnt, act_b = lane + 64 < cnt;
-      xa = ya = xb = yb = 0.0;
-      ia = ib = 0;
-      if (act_a) { xa = fx[a]; ya = fy[a]; ia = fid[a]; }
-      if (act_b) { xb = fx[b]; yb = fy[b]; ib = fid[b]; }
+      const bool act_a = lane < cnt, act_b = FBATCH > 64 && lane + 64 < cnt;
+      uint32_t wa = CELL_EMPTY << 30, wb = CELL_EMPTY << 30;
+      if (act_a) wa = d.cell_sc[(int64_t)cell_of(fy[a], d.gy0, d.inv_ch, d.gy) * d.gx + cell_of(fx[a], d.gx0, d.inv_cw, d.gx)];
+      if (act_b) wb = d.cell_sc[(int64_t)cell_of(fy[b], d.gy0, d.inv_ch, d.gy) * d.gx + cell_of(fx[b], d.gx0, d.inv_cw, d.gx)];
+      if (act_a) fw[a] = wa;
+      if (act_b) fw[b] = wb;
       wave_lds_sync();
-      fn -= cnt;
-      wa = wb = CELL_EMPTY << 30;
-      if (act_a) wa = d.cell_sc[(int64_t)cell_of(ya, d.gy0, d.inv_ch, d.gy) * d.gx + cell_of(xa, d.gx0, d.inv_cw, d.gx)];
-      if (act_b) wb = d.cell_sc[(int64_t)cell_of(yb, d.gy0, d.inv_ch, d.gy) * d.gx + cell_of(xb, d.gx0, d.inv_cw, d.gx)];
-      pend = cnt > 64 ? 2 : 1;
-      if (pend == 1) { wb = wa; xb = xa; yb = ya; ib = ia; }   // one slot: it is "b" (pend 1 resolves b)
+      pb = fn - cnt;
+      pc = cnt;
+      hn = 0;
+      hd = cnt > 64 ? 2 : 1;
       continue;
     }
     if (streaming) {   // ---- stream step: 2 points per lane, their coarse words together
