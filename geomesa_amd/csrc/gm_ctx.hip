@@ -82,6 +82,15 @@ int copy_d2h(gm_ctx* ctx, void* host, const void* dev, size_t bytes) {
 
 bool host_pinned(const void* p) { return is_pinned(p); }
 
+bool device_memory(const void* p) {
+  hipPointerAttribute_t a;
+  if (!p || hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return a.type == hipMemoryTypeDevice;
+}
+
 int ctx_copy_stream(gm_ctx* ctx) {
   if (ctx->copy_stream) return GM_OK;
   GM_HIP(hipSetDevice(ctx->device));

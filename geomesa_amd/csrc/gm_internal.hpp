@@ -62,6 +62,7 @@ int copy_h2d(gm_ctx* ctx, void* dev, const void* host, size_t bytes);
 enum : int { WS_RANGES = 0, WS_SORT = 1, WS_SCAN = 2, WS_JOIN = 3 };
 int ctx_workspace(gm_ctx* ctx, int slot, size_t bytes, void** p);
 bool host_pinned(const void* p);
+bool device_memory(const void* p);   // device (hipMalloc) memory, as opposed to host memory
 int ctx_copy_stream(gm_ctx* ctx);   // creates copy_stream and its events on first use
 
 // reset the error summary before a call that reports one

@@ -937,6 +937,16 @@ int run_ranges(gm_ctx* ctx, int64_t nq, int64_t fcap, int64_t rcap, size_t felem
                gm_range* out, int64_t cap, int64_t* needed, int32_t* query_status) {
   hipStream_t s = ctx->stream;
   int64_t qc = ctx->ranges_chunk > 0 ? ctx->ranges_chunk : (nq < 16384 ? nq : std::max<int64_t>(8192, (nq + 7) / 8));
+  if (out && device_memory(out)) {   // device output (ranges consumed on the device): gathered in place
+    return run_batch(ctx, 0, nq, fcap, rcap, felem, launch, out_off, cap, needed, query_status,
+                     [&](int64_t total, const gm_range* dbuf, const int64_t* dstart, const int64_t* doff, int64_t n) -> int {
+                       hipLaunchKernelGGL(k_gather_ranges, dim3((unsigned)std::min<int64_t>(n, 65536)), dim3(RTPB), 0, s,
+                                          dbuf, dstart, doff, n, out);
+                       GM_CHECK_LAUNCH();
+                       GM_HIP(hipStreamSynchronize(s));
+                       return GM_OK;
+                     });
+  }
   if (qc >= nq || !out || !host_pinned(out)) {   // one batch: gather into scratch, one copy
     return run_batch(ctx, 0, nq, fcap, rcap, felem, launch, out_off, cap, needed, query_status,
                      [&](int64_t total, const gm_range* dbuf, const int64_t* dstart, const int64_t* doff, int64_t n) -> int {

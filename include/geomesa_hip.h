@@ -153,9 +153,12 @@ int gm_xz3_index(gm_ctx* ctx, const double* xmin, const double* ymin, const doub
    xy (host, 4 doubles each) and, for Z3, times [time_off[q], time_off[q+1]) of t (host, 2 int64
    each, offsets within the period).  The z-bounds of a query are the cross product, as in
    Z3SFC.ranges.  max_ranges <= 0 means None; max_recurse < 0 means the default (Z3:
-   Int.MaxValue, Z2: ZN.DefaultRecurse = 7).  Output (host): ranges of query q are
-   out[out_off[q] .. out_off[q+1]); capacity in ranges.  Returns GM_E_CAPACITY with
-   *needed set when cap is too small. */
+   Int.MaxValue, Z2: ZN.DefaultRecurse = 7).  Output: ranges of query q are
+   out[out_off[q] .. out_off[q+1]) (out_off host); capacity in ranges.  `out` is host memory
+   (pageable or pinned; pinned output is copied back chunk by chunk, overlapping the next chunk's
+   kernels) or device memory (the ranges stay in HBM for a device-side consumer: no copy).  Returns
+   GM_E_CAPACITY with *needed set when cap is too small.  The same output rules hold for
+   gm_z2_ranges, gm_zranges, gm_xz2_ranges and gm_xz3_ranges. */
 int gm_z3_ranges(gm_ctx* ctx, int64_t n_queries, const int32_t* box_off, const double* xy,
                  const int32_t* time_off, const int64_t* t, int period, int precision, int range_precision,
                  int max_ranges, int max_recurse, int64_t* out_off, gm_range* out, int64_t cap,

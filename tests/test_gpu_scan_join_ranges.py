@@ -398,3 +398,37 @@ def test_ranges_pipelined_chunks(gpu, oracle, kind):
     if kind == "xz2":   # and the oracle, for one query
         got = [(int(r["lower"]), int(r["upper"]), bool(r["contained"])) for r in r1[int(o1[0]):int(o1[1])]]
         assert got == [(int(a), int(b), bool(c)) for a, b, c in oracle.xz2_ranges(qs[0], max_ranges=300)]
+
+
+@pytest.mark.parametrize("kind", ["z3", "xz2", "xz3"])
+def test_ranges_device_output(gpu, kind):
+    """Batched ranges written straight into device memory (ranges for a device-side consumer: no copy
+    back) equal the host-output batch: offsets, ranges and statuses."""
+    import ctypes
+    import torch
+    from geomesa_amd import _lib
+    from geomesa_amd import ranges as R
+    from geomesa_amd.curve import XZ3SFC, Z3SFC
+    ctx = _lib.context()
+    if kind == "z3":
+        qs = [([b], [(int(t[0]), int(t[1]))]) for b, t in ranges_queries(50, seed=37)]
+        fn, args, nq, cap = R.prepare_z3(Z3SFC("week"), qs, 64, 500)
+    else:
+        d = 2 if kind == "xz2" else 3
+        qs = [[b] if d == 2 else [(b[0], b[1], float(t[0]), b[2], b[3], float(t[1]))]
+              for b, t in ranges_queries(50, seed=41)]
+        off, w = R._windows(qs, d)
+        nq, cap = len(qs), len(qs) * 4096
+        fn = ctx.lib.gm_xz2_ranges if d == 2 else ctx.lib.gm_xz3_ranges
+        args = (ctx.handle, nq, off.ctypes.data, w.ctypes.data, 12, 500) if d == 2 else \
+            (ctx.handle, nq, off.ctypes.data, w.ctypes.data, 12, XZ3SFC(12, "week").period, 500)
+    o1, r1, s1 = R.call_raw(fn, args, nq, cap)
+    total = int(o1[-1])
+    dev = torch.empty(max(total, 1) * R.RANGE_DTYPE.itemsize, dtype=torch.uint8, device="cuda")
+    o2 = np.zeros(nq + 1, np.int64)
+    s2 = np.zeros(nq, np.int32)
+    need = ctypes.c_int64()
+    _lib.check(fn(*args, o2.ctypes.data, dev.data_ptr(), max(total, 1), ctypes.byref(need), s2.ctypes.data), "ranges")
+    assert np.array_equal(o1, o2) and np.array_equal(s1, s2) and need.value == total
+    r2 = dev[:total * R.RANGE_DTYPE.itemsize].cpu().numpy().view(R.RANGE_DTYPE)
+    assert np.array_equal(r1[:total], r2)
