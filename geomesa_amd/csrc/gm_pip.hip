@@ -705,6 +705,119 @@ __global__ __launch_bounds__(JTPB, GM_JOIN_WAVES) void k_pip_join(const double* 
   }
 }
 
+// ---------------------------------------------------------------- pair output by slabs
+// One returning atomic on one output counter saturates near 88 per us chip-wide (MI355X_MICROARCH.md,
+// "dequeue"): a flush of a few hundred staged pairs each was ~0.8M atomics per 1B-point join, several
+// ms of serialised counter traffic.  Instead each wave reserves SLAB pairs at a time (one atomic per
+// 4096 pairs) and writes its pairs straight into its slab, 64 at a time, no LDS staging.  Only each
+// wave's last slab can be partly filled; the waves record (slab base, fill) and, after the join,
+// k_pair_plan lists the holes below the pair count and the pairs at or above it, and k_pair_move
+// moves those into these (at most waves x SLAB pairs): the caller gets [0, n_pairs) contiguous.
+// Slab positions at or past the caller's capacity land in a context overflow area (waves x SLAB
+// pairs), so nothing below n_pairs is lost when reservations run past cap while n_pairs fits.
+constexpr int SLAB = 4096;
+constexpr int PLAN_MAX = 8192;       // wave descriptors one plan handles
+
+struct PairOut {
+  int64_t* pt; int32_t* pl; int64_t cap;       // caller arrays
+  int64_t* opt; int32_t* opl; int64_t ocap;    // overflow area: positions [cap, cap + ocap)
+  unsigned long long* counter;                 // slab reservations (pairs), then the pair count
+  longlong2* desc;                             // per wave: (last slab base or -1, its fill)
+};
+
+__device__ __forceinline__ void pair_store(const PairOut& o, int64_t pos, int64_t id, int32_t poly) {
+  if (pos < o.cap) { o.pt[pos] = id; o.pl[pos] = poly; }
+  else if (pos - o.cap < o.ocap) { o.opt[pos - o.cap] = id; o.opl[pos - o.cap] = poly; }
+}
+
+struct PairPlan {
+  int64_t n_pairs, moves, n_src, n_dst;
+  int64_t src[PLAN_MAX + 1], src_pre[PLAN_MAX + 2];   // source runs (start) and their exclusive prefix
+  int64_t dst[PLAN_MAX + 1], dst_pre[PLAN_MAX + 2];   // hole runs below n_pairs
+};
+
+// one block: sort the waves' last slabs by base, then (thread 0) the hole runs below the pair count
+// and the pair runs at or above it; counter[0] becomes the pair count
+__global__ __launch_bounds__(1024) void k_pair_plan(const longlong2* __restrict__ desc, int nd,
+                                                    unsigned long long* __restrict__ counter, PairPlan* __restrict__ plan) {
+  __shared__ int64_t key[PLAN_MAX];
+  __shared__ int32_t fil[PLAN_MAX];
+  int P = 1;
+  while (P < nd) P <<= 1;
+  for (int i = threadIdx.x; i < P; i += blockDim.x) {
+    const bool ok = i < nd && desc[i].x >= 0 && desc[i].y < SLAB;   // a slab with a hole
+    key[i] = ok ? desc[i].x : INT64_MAX;
+    fil[i] = ok ? (int32_t)desc[i].y : SLAB;
+  }
+  __syncthreads();
+  for (int k = 2; k <= P; k <<= 1)
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = threadIdx.x; i < P; i += blockDim.x) {
+        const int l = i ^ j;
+        if (l > i) {
+          const bool up = (i & k) == 0;
+          if ((key[i] > key[l]) == up) {
+            const int64_t t = key[i]; key[i] = key[l]; key[l] = t;
+            const int32_t f = fil[i]; fil[i] = fil[l]; fil[l] = f;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  if (threadIdx.x == 0) {
+    const int64_t T = (int64_t)*counter;
+    int64_t H = 0;
+    int nh = 0;
+    while (nh < P && key[nh] != INT64_MAX) { H += SLAB - fil[nh]; ++nh; }
+    const int64_t np = T - H;
+    int64_t nd2 = 0, ns = 0, dacc = 0, sacc = 0, cur = np;
+    for (int i = 0; i < nh; ++i) {
+      const int64_t hs = key[i] + fil[i], he = key[i] + SLAB;
+      if (hs < np) {   // the part of this hole below the pair count
+        const int64_t len = min(he, np) - hs;
+        plan->dst[nd2] = hs; plan->dst_pre[nd2] = dacc; dacc += len; ++nd2;
+      }
+      if (he > np) {   // pairs between the previous hole and this one, at or above the pair count
+        const int64_t a = cur, b = max(cur, hs);
+        if (b > a) { plan->src[ns] = a; plan->src_pre[ns] = sacc; sacc += b - a; ++ns; }
+        cur = max(cur, he);
+      }
+    }
+    if (T > cur) { plan->src[ns] = cur; plan->src_pre[ns] = sacc; sacc += T - cur; ++ns; }
+    plan->dst_pre[nd2] = dacc;
+    plan->src_pre[ns] = sacc;
+    plan->n_dst = nd2; plan->n_src = ns;
+    plan->moves = min(dacc, sacc);   // equal by construction
+    plan->n_pairs = np;
+    *counter = (unsigned long long)np;
+  }
+}
+
+__device__ __forceinline__ int64_t run_of(const int64_t* pre, int64_t n, int64_t k) {   // last r with pre[r] <= k
+  int64_t a = 0, b = n - 1;
+  while (a < b) {
+    const int64_t m = (a + b + 1) >> 1;
+    if (pre[m] <= k) a = m;
+    else b = m - 1;
+  }
+  return a;
+}
+
+__global__ __launch_bounds__(256) void k_pair_move(PairOut o, const PairPlan* __restrict__ plan) {
+  const int64_t L = plan->moves, np = plan->n_pairs;
+  if (np > o.cap) return;   // GM_E_CAPACITY: nothing to deliver
+  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < L; k += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t rs = run_of(plan->src_pre, plan->n_src, k), rd = run_of(plan->dst_pre, plan->n_dst, k);
+    const int64_t sp = plan->src[rs] + (k - plan->src_pre[rs]), dp = plan->dst[rd] + (k - plan->dst_pre[rd]);
+    int64_t id;
+    int32_t pl;
+    if (sp < o.cap) { id = o.pt[sp]; pl = o.pl[sp]; }
+    else { id = o.opt[sp - o.cap]; pl = o.opl[sp - o.cap]; }
+    o.pt[dp] = id;
+    o.pl[dp] = pl;
+  }
+}
+
 // ---------------------------------------------------------------- the direct pass, stage queues
 // The direct join as three stages joined by per-wave LDS queues, so that every gather beyond L2 is
 // issued by a full wave (64 independent addresses) and many are in flight at once:
@@ -734,38 +847,42 @@ constexpr int QTPB = 256;           // 4 waves per block
 constexpr int FBATCH = GM_JQ_FBATCH;   // fine words per round (64: 1 per lane, 128: 2 per lane)
 constexpr int FCAP = FBATCH + 128;     // fine queue (< FBATCH + one step's 128)
 constexpr int ICAP = 128;           // item queue (two ends)
-constexpr int PCAP = 192;           // pair staging
 
 template <bool WRITE, int SRC, bool VEC>
 __global__ __launch_bounds__(QTPB, GM_JQ_WAVES) void k_pip_join_q(const double* __restrict__ px, const double* __restrict__ py,
-                                                     int64_t n, int64_t id_base, PipDev d,
-                                                     int64_t* __restrict__ pt_ids, int32_t* __restrict__ poly_ids,
-                                                     int64_t cap, unsigned long long* __restrict__ counter, ArrowPts ap) {
+                                                     int64_t n, int64_t id_base, PipDev d, PairOut po,
+                                                     int64_t desc_base, ArrowPts ap) {
   constexpr int NW = QTPB / 64;
   __shared__ double s_fx[NW][FCAP], s_fy[NW][FCAP];
   __shared__ uint32_t s_fid[NW][FCAP], s_fw[NW][FCAP];
   __shared__ double s_ix[NW][ICAP], s_iy[NW][ICAP];
   __shared__ uint32_t s_iid[NW][ICAP], s_iref[NW][ICAP];
-  __shared__ uint32_t s_pid[WRITE ? NW : 1][WRITE ? PCAP : 1];
-  __shared__ int32_t s_ppl[WRITE ? NW : 1][WRITE ? PCAP : 1];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   double* fx = s_fx[wv]; double* fy = s_fy[wv]; uint32_t* fid = s_fid[wv];
   double* qx = s_ix[wv]; double* qy = s_iy[wv]; uint32_t* qid = s_iid[wv]; uint32_t* qref = s_iref[wv];
-  uint32_t* wpt = s_pid[WRITE ? wv : 0];
-  int32_t* wpl = s_ppl[WRITE ? wv : 0];
-  int fn = 0, qn = 0, qg = 0, wn = 0;   // wave-uniform fills: fine queue, line items, blob items, pairs
+  int fn = 0, qn = 0, qg = 0;   // wave-uniform fills: fine queue, line items, blob items
+  int64_t sbase = -1;           // wave-uniform: this wave's current output slab and its fill
+  int sfill = SLAB;
   int my_count = 0;
   const bool lines_on = d.line_ent != nullptr;
 
-  // pairs are staged without a flush here: the loop flushes at its top while wn > PCAP - 128, and one
-  // trip pushes at most 128 (a stream step's two points per lane)
+  // a wave's pairs go straight into its slab (see "pair output by slabs"); a full slab takes the
+  // next one with one atomic
   auto pair_push = [&](bool hit, uint32_t id, int poly) __attribute__((always_inline)) {
     if (!WRITE) { my_count += hit; return; }
     const uint64_t m = __ballot(hit);
     if (!m) return;
-    if (wn + __popcll(m) > PCAP) { if (lane == 0) pip_fault(d, PIP_FAULT_QUEUE); return; }   // cannot happen
-    if (hit) { const int o = wn + lanes_below(m); wpt[o] = id; wpl[o] = poly; }
-    wn += __popcll(m);
+    const int c = __popcll(m), off = lanes_below(m), room = SLAB - sfill;
+    if (hit && off < room) pair_store(po, sbase + sfill + off, id_base + id, poly);
+    if (c > room) {
+      unsigned long long b = 0;
+      if (lane == 0) b = atomicAdd(po.counter, (unsigned long long)SLAB);
+      sbase = (int64_t)__shfl(b, 0, 64);
+      if (hit && off >= room) pair_store(po, sbase + (off - room), id_base + id, poly);
+      sfill = c - room;
+    } else {
+      sfill += c;
+    }
   };
   auto item_push = [&](bool valid, bool is_line, double x, double y, uint32_t id, uint32_t ref) __attribute__((always_inline)) {
     const uint64_t ml = __ballot(valid && is_line), mb = __ballot(valid && !is_line);
@@ -815,7 +932,6 @@ __global__ __launch_bounds__(QTPB, GM_JQ_WAVES) void k_pip_join_q(const double* 
   uint32_t* fw = s_fw[wv];
 
   for (;;) {
-    if (WRITE && wn > PCAP - 128) { flush_pairs(wpt, wpl, wn, lane, id_base, pt_ids, poly_ids, cap, counter); wn = 0; }
     // every other stage idle: the item stage drains what is left (a line round may hand blobs over)
     const bool idle = !list_on && hn == hd && fn == 0 && step >= nstep;
     if (qn + qg >= 64 || (idle && qn + qg > 0)) {   // ---- items: one round of the fuller kind
@@ -949,10 +1065,11 @@ __global__ __launch_bounds__(QTPB, GM_JQ_WAVES) void k_pip_join_q(const double* 
     }
     break;   // every stage idle and the item queue empty (the item stage drains it once nothing else runs)
   }
-  if (WRITE && wn > 0) flush_pairs(wpt, wpl, wn, lane, id_base, pt_ids, poly_ids, cap, counter);
-  if (!WRITE) {
+  if (WRITE) {
+    if (lane == 0) po.desc[desc_base + (int64_t)blockIdx.x * NW + wv] = make_longlong2(sbase, sfill);
+  } else {
     for (int off = 32; off > 0; off >>= 1) my_count += __shfl_down(my_count, off, 64);
-    if (lane == 0 && my_count) atomicAdd(counter, (unsigned long long)my_count);
+    if (lane == 0 && my_count) atomicAdd(po.counter, (unsigned long long)my_count);
   }
 }
 
@@ -2840,15 +2957,58 @@ static bool join_legacy() {
   return e && atoi(e) != 0;
 }
 
-template <bool WRITE, int SRC, bool VEC>
-static void launch_join_q(gm_ctx* ctx, const double* px, const double* py, int64_t m, int64_t id_base, const PipDev& dv,
-                          int64_t* pt_ids, int32_t* poly_ids, int64_t cap, unsigned long long* counter, ArrowPts ap) {
-  const int64_t wsteps = ((m + 1) / 2 + 63) / 64;   // 128-point stream steps, one wave each
-  const int64_t blocks = (wsteps + QTPB / 64 - 1) / (QTPB / 64);
-  const int resident = resident_blocks((const void*)k_pip_join_q<WRITE, SRC, VEC>, ctx->device, QTPB, 4);
-  const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(resident, blocks));
-  hipLaunchKernelGGL((k_pip_join_q<WRITE, SRC, VEC>), dim3(grid), dim3(QTPB), 0, ctx->stream, px, py, m, id_base, dv,
-                     pt_ids, poly_ids, cap, counter, ap);
+// The staged direct pass over n rows in chunks of at most 2^31 (32-bit row ids in the queues).  With
+// outputs, each chunk's waves write slabs, then k_pair_plan / k_pair_move close the holes, so
+// [0, counter[0]) is contiguous before the next chunk reserves past it.  SRC / VEC as k_pip_join_q;
+// `ap` is the Arrow column (tuple bytes `tb`) when SRC != 0.
+template <int SRC, bool VEC>
+static int join_staged(gm_ctx* ctx, const double* px, const double* py, ArrowPts ap, size_t tb, int64_t n,
+                       int64_t id_base, const PipDev& dv, int64_t* pt_ids, int32_t* poly_ids, int64_t cap,
+                       unsigned long long* counter) {
+  const bool write = pt_ids && poly_ids;
+  const int64_t CHUNK = join_chunk(ctx, (int64_t)1 << 31);
+  const int resident = write ? resident_blocks((const void*)k_pip_join_q<true, SRC, VEC>, ctx->device, QTPB, 4)
+                             : resident_blocks((const void*)k_pip_join_q<false, SRC, VEC>, ctx->device, QTPB, 4);
+  const int64_t wmax = (int64_t)resident * (QTPB / 64);
+  if (write && wmax > PLAN_MAX) return hip_fail(hipErrorInvalidValue, "join: more waves than the pair plan holds");
+  PairOut po{pt_ids, poly_ids, cap, nullptr, nullptr, 0, counter, nullptr};
+  PairPlan* plan = nullptr;
+  if (write) {   // context workspace: overflow ids | overflow polygons | wave descriptors | plan
+    auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
+    const int64_t ocap = wmax * SLAB;
+    const size_t a_id = al((size_t)ocap * 8), a_pl = al((size_t)ocap * 4), a_d = al((size_t)wmax * sizeof(longlong2));
+    void* base = nullptr;
+    int rc = ctx_workspace(ctx, WS_JOIN, a_id + a_pl + a_d + sizeof(PairPlan), &base);
+    if (rc) return rc;
+    char* q = (char*)base;
+    po.opt = (int64_t*)q; q += a_id;
+    po.opl = (int32_t*)q; q += a_pl;
+    po.desc = (longlong2*)q; q += a_d;
+    po.ocap = ocap;
+    plan = (PairPlan*)q;
+  }
+  for (int64_t c0 = 0; c0 < n; c0 += CHUNK) {
+    const int64_t m = std::min(CHUNK, n - c0);
+    const int64_t wsteps = ((m + 1) / 2 + 63) / 64;   // 128-point stream steps, one wave each
+    const int64_t blocks = (wsteps + QTPB / 64 - 1) / (QTPB / 64);
+    const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(resident, blocks));
+    ArrowPts a = ap;
+    if (SRC != 0) { a.c = (const char*)ap.c + (size_t)c0 * tb; a.voff = ap.voff + c0; }
+    const double* cx = SRC == 0 ? px + c0 : nullptr;
+    const double* cy = SRC == 0 ? py + c0 : nullptr;
+    if (write) {
+      hipLaunchKernelGGL((k_pip_join_q<true, SRC, VEC>), dim3(grid), dim3(QTPB), 0, ctx->stream, cx, cy, m, id_base + c0,
+                         dv, po, (int64_t)0, a);
+      hipLaunchKernelGGL(k_pair_plan, dim3(1), dim3(1024), 0, ctx->stream, (const longlong2*)po.desc,
+                         (int)(grid * (QTPB / 64)), counter, plan);
+      hipLaunchKernelGGL(k_pair_move, dim3(1024), dim3(256), 0, ctx->stream, po, (const PairPlan*)plan);
+    } else {
+      hipLaunchKernelGGL((k_pip_join_q<false, SRC, VEC>), dim3(grid), dim3(QTPB), 0, ctx->stream, cx, cy, m,
+                         id_base + c0, dv, po, (int64_t)0, a);
+    }
+    GM_CHECK_LAUNCH();
+  }
+  return GM_OK;
 }
 
 // the direct pass over an Arrow point column (tuples read in place)
@@ -2868,8 +3028,11 @@ static int join_direct_arrow(gm_ctx* ctx, const gm_pip_index* ix, ArrowPts ap, i
     a.c = (const char*)ap.c + (size_t)c0 * tb;
     a.voff = ap.voff + c0;
     if (!join_legacy()) {
-      if (write) launch_join_q<true, SRC, false>(ctx, nullptr, nullptr, m, id_base + c0, dv, pt_ids, poly_ids, cap, counter, a);
-      else launch_join_q<false, SRC, false>(ctx, nullptr, nullptr, m, id_base + c0, dv, pt_ids, poly_ids, cap, counter, a);
+      if (c0 == 0) {
+        const int rc = join_staged<SRC, false>(ctx, nullptr, nullptr, ap, tb, n, id_base, dv, pt_ids, poly_ids, cap, counter);
+        if (rc) return rc;
+      }
+      continue;
     } else if (write)
       hipLaunchKernelGGL((k_pip_join<true, false, false, SRC>), dim3(join_grid<true, false, false, SRC>(ctx->device, ntiles)),
                          dim3(JTPB), 0, ctx->stream, nullptr, nullptr, nullptr, nullptr, m, id_base + c0, dv,
@@ -3447,11 +3610,11 @@ int gm_pip_join_pred(gm_ctx* ctx, const gm_pip_index* ix, const double* px, cons
       const int64_t m = std::min(CHUNK, n - c0);
       const int64_t ntiles = (m + JTILE - 1) / JTILE;
       if (!join_legacy()) {
-        if (write && vec) launch_join_q<true, 0, true>(ctx, px + c0, py + c0, m, id_base + c0, dv, pt_ids, poly_ids, cap, counter, ArrowPts{});
-        else if (write) launch_join_q<true, 0, false>(ctx, px + c0, py + c0, m, id_base + c0, dv, pt_ids, poly_ids, cap, counter, ArrowPts{});
-        else if (vec) launch_join_q<false, 0, true>(ctx, px + c0, py + c0, m, id_base + c0, dv, pt_ids, poly_ids, cap, counter, ArrowPts{});
-        else launch_join_q<false, 0, false>(ctx, px + c0, py + c0, m, id_base + c0, dv, pt_ids, poly_ids, cap, counter, ArrowPts{});
-        GM_CHECK_LAUNCH();
+        if (c0 == 0) {
+          const int rc = vec ? join_staged<0, true>(ctx, px, py, ArrowPts{}, 16, n, id_base, dv, pt_ids, poly_ids, cap, counter)
+                             : join_staged<0, false>(ctx, px, py, ArrowPts{}, 16, n, id_base, dv, pt_ids, poly_ids, cap, counter);
+          if (rc) return rc;
+        }
         continue;
       }
       const unsigned grid = write ? join_grid<true, false, false>(ctx->device, ntiles)
