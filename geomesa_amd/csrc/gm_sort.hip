@@ -93,7 +93,42 @@ __global__ __launch_bounds__(HT) void k_sort_hist(const uint8_t* __restrict__ sh
     return pass < 8 ? (uint32_t)(z[i] >> (8 * pass)) & 255u
                     : pass < 10 ? (uint32_t)(bin[i] >> (8 * (pass - 8))) & 255u : (uint32_t)sh[i];
   };
-  for (int64_t i = b0 + 2 * threadIdx.x; i < b1; i += 2 * HT) {   // b0 is even (tile multiple)
+  // full stretches: 4 pairs per lane, loads issued together (a digit extraction between loads made
+  // the compiler wait for each pair before the next load)
+  constexpr int HU = 4;
+  int64_t i = b0 + 2 * threadIdx.x;
+  if (vec)
+    for (; i + 2 * HT * (HU - 1) + 1 < b1; i += 2 * HT * HU) {
+      uint32_t d[2 * HU];
+      if (pass < 8) {
+        ulonglong2 zz[HU];
+#pragma unroll
+        for (int u = 0; u < HU; ++u) zz[u] = *(const ulonglong2*)(z + i + 2 * HT * u);
+#pragma unroll
+        for (int u = 0; u < HU; ++u) {
+          d[2 * u] = (uint32_t)(zz[u].x >> (8 * pass)) & 255u;
+          d[2 * u + 1] = (uint32_t)(zz[u].y >> (8 * pass)) & 255u;
+        }
+      } else if (pass < 10) {
+        uint32_t bb[HU];
+#pragma unroll
+        for (int u = 0; u < HU; ++u) bb[u] = *(const uint32_t*)(bin + i + 2 * HT * u);
+#pragma unroll
+        for (int u = 0; u < HU; ++u) {
+          d[2 * u] = (bb[u] >> (8 * (pass - 8))) & 255u;
+          d[2 * u + 1] = (bb[u] >> (16 + 8 * (pass - 8))) & 255u;
+        }
+      } else {
+        uint32_t ss[HU];
+#pragma unroll
+        for (int u = 0; u < HU; ++u) ss[u] = *(const uint16_t*)(sh + i + 2 * HT * u);
+#pragma unroll
+        for (int u = 0; u < HU; ++u) { d[2 * u] = ss[u] & 255u; d[2 * u + 1] = (ss[u] >> 8) & 255u; }
+      }
+#pragma unroll
+      for (int k = 0; k < 2 * HU; ++k) atomicAdd(&h[wave][d[k]], 1u);
+    }
+  for (; i < b1; i += 2 * HT) {   // b0 is even (tile multiple)
     if (vec && i + 1 < b1) {
       uint32_t d0, d1;
       if (pass < 8) {
@@ -146,6 +181,11 @@ __device__ __forceinline__ uint64_t digit_mask(const uint64_t* bal, uint32_t d) 
   return m;
 }
 
+// SH: a shard column; PIN: a permutation input (else the row index).  The next tile's loads only issue
+// into raw registers (z pair, bin pair, shard pair, permutation pair) and are combined when ranked:
+// a combine (or a column test) between loads made the compiler wait for each slot's loads before
+// issuing the next ones, which serialised the "prefetch" into four round trips per tile.
+template <bool SH, bool PIN>
 __global__ __launch_bounds__(BT) void k_sort_scatter(const uint8_t* __restrict__ sh_in, const uint16_t* __restrict__ bin_in,
                                                      const uint64_t* __restrict__ z_in,
                                                      const uint32_t* __restrict__ perm_in, uint8_t* __restrict__ sh_out,
@@ -156,44 +196,56 @@ __global__ __launch_bounds__(BT) void k_sort_scatter(const uint8_t* __restrict__
   __shared__ uint64_t s_z[BTILE];
   __shared__ uint32_t s_perm[BTILE];
   __shared__ uint16_t s_bin[BTILE];
-  __shared__ uint8_t s_sh[BTILE];
+  __shared__ uint8_t s_sh[SH ? BTILE : 1];
   __shared__ uint16_t s_wcnt[BW][256];      // per wave: rows of each digit so far (then: wave offsets)
   __shared__ uint32_t s_gcur[256], s_tot[256], s_dstart[256], s_wsum[4];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   if (t < 256) s_gcur[t] = off[(int64_t)t * gridDim.x + blockIdx.x];
   const int64_t b0 = (int64_t)blockIdx.x * per_block, b1 = min(n, b0 + per_block);
   const uint64_t lt = lanemask_lt();
-  uint64_t zv[BSLOT][2];
-  uint32_t pv[BSLOT][2];
-  uint32_t bs[BSLOT][2];   // bin | shard << 16
-  // this lane's rows of the tile at t0 into registers (the next tile's loads are issued before the
-  // current tile leaves LDS, so they overlap its global writes)
-  auto load = [&](int64_t t0) {
+  // raw loads of this lane's rows of a tile (2 rows per slot)
+  ulonglong2 rz[BSLOT];
+  uint32_t rb[BSLOT];    // bin pair (ushort2 bits)
+  uint32_t rs[BSLOT];    // shard pair (uchar2 bits)
+  uint2 rp[BSLOT];       // permutation pair
+  auto load = [&](int64_t t0) __attribute__((always_inline)) {
+    const bool full = vec && t0 + BTILE <= b1;   // block-uniform: every slot holds two rows
+    if (full) {
 #pragma unroll
-    for (int k = 0; k < BSLOT; ++k) {
-      const int64_t i = t0 + wave * (2 * 64 * BSLOT) + k * 128 + 2 * lane;
-      if (vec && i + 1 < b1) {   // both rows: vector loads (i is even: segments start on tile boundaries)
-        const ulonglong2 zz = *(const ulonglong2*)(z_in + i);
-        zv[k][0] = zz.x; zv[k][1] = zz.y;
-        const ushort2 bb = *(const ushort2*)(bin_in + i);
-        uint32_t s0 = 0, s1 = 0;
-        if (sh_in) { const uchar2 ss = *(const uchar2*)(sh_in + i); s0 = ss.x; s1 = ss.y; }
-        bs[k][0] = bb.x | (s0 << 16); bs[k][1] = bb.y | (s1 << 16);
-        if (perm_in) { const uint2 pp = *(const uint2*)(perm_in + i); pv[k][0] = pp.x; pv[k][1] = pp.y; }
-        else { pv[k][0] = (uint32_t)i; pv[k][1] = (uint32_t)(i + 1); }
-      } else {
+      for (int k = 0; k < BSLOT; ++k) {
+        const int64_t i = t0 + wave * (2 * 64 * BSLOT) + k * 128 + 2 * lane;
+        rz[k] = *(const ulonglong2*)(z_in + i);
+        rb[k] = *(const uint32_t*)(bin_in + i);
+        if (SH) rs[k] = *(const uint16_t*)(sh_in + i);
+        if (PIN) rp[k] = *(const uint2*)(perm_in + i);
+      }
+    } else {
 #pragma unroll
-        for (int e = 0; e < 2; ++e) {
-          const bool ok = i + e < b1;
-          zv[k][e] = ok ? z_in[i + e] : 0;
-          bs[k][e] = ok ? ((uint32_t)bin_in[i + e] | ((sh_in ? (uint32_t)sh_in[i + e] : 0u) << 16)) : 0;
-          pv[k][e] = ok ? (perm_in ? perm_in[i + e] : (uint32_t)(i + e)) : 0;
-        }
+      for (int k = 0; k < BSLOT; ++k) {
+        const int64_t i = t0 + wave * (2 * 64 * BSLOT) + k * 128 + 2 * lane;
+        const bool ok0 = i < b1, ok1 = i + 1 < b1;
+        rz[k].x = ok0 ? z_in[i] : 0; rz[k].y = ok1 ? z_in[i + 1] : 0;
+        rb[k] = (ok0 ? (uint32_t)bin_in[i] : 0u) | ((ok1 ? (uint32_t)bin_in[i + 1] : 0u) << 16);
+        if (SH) rs[k] = (ok0 ? (uint32_t)sh_in[i] : 0u) | ((ok1 ? (uint32_t)sh_in[i + 1] : 0u) << 8);
+        if (PIN) rp[k] = make_uint2(ok0 ? perm_in[i] : 0u, ok1 ? perm_in[i + 1] : 0u);
       }
     }
   };
   if (b0 < b1) load(b0);
   for (int64_t t0 = b0; t0 < b1; t0 += BTILE) {
+    // this tile's rows out of the raw registers
+    uint64_t zv[BSLOT][2];
+    uint32_t pv[BSLOT][2];
+    uint32_t bs[BSLOT][2];   // bin | shard << 16
+#pragma unroll
+    for (int k = 0; k < BSLOT; ++k) {
+      const int64_t i = t0 + wave * (2 * 64 * BSLOT) + k * 128 + 2 * lane;
+      zv[k][0] = rz[k].x; zv[k][1] = rz[k].y;
+      bs[k][0] = (rb[k] & 0xffffu) | (SH ? (rs[k] & 0xffu) << 16 : 0u);
+      bs[k][1] = (rb[k] >> 16) | (SH ? ((rs[k] >> 8) & 0xffu) << 16 : 0u);
+      if (PIN) { pv[k][0] = rp[k].x; pv[k][1] = rp[k].y; }
+      else { pv[k][0] = (uint32_t)i; pv[k][1] = (uint32_t)(i + 1); }
+    }
     for (int i = t; i < BW * 256 / 2; i += BT) ((uint32_t*)&s_wcnt[0][0])[i] = 0u;
     __syncthreads();
     uint32_t rd[BSLOT][2];   // wave rank | digit << 16; rank 0xffff = no row
@@ -258,19 +310,19 @@ __global__ __launch_bounds__(BT) void k_sort_scatter(const uint8_t* __restrict__
         if (r == 0xffffu) continue;
         const uint32_t pos = s_dstart[d] + s_wcnt[wave][d] + r;
         s_z[pos] = zv[k][e]; s_bin[pos] = (uint16_t)bs[k][e];
-        if (sh_in) s_sh[pos] = (uint8_t)(bs[k][e] >> 16);
+        if (SH) s_sh[pos] = (uint8_t)(bs[k][e] >> 16);
         s_perm[pos] = pv[k][e];
       }
     }
     __syncthreads();
-    if (t0 + BTILE < b1) load(t0 + BTILE);
+    if (t0 + BTILE < b1) load(t0 + BTILE);   // issued before the write-out: in flight during it
     const int cnt = (int)min((int64_t)BTILE, b1 - t0);
     for (int q = t; q < cnt; q += BT) {
-      const uint32_t d = key_digit(sh_in ? s_sh[q] : (uint8_t)0, s_bin[q], s_z[q], pass);
+      const uint32_t d = key_digit(SH ? s_sh[q] : (uint8_t)0, s_bin[q], s_z[q], pass);
       const int64_t g = (int64_t)s_gcur[d] + (q - (int)s_dstart[d]);
       z_out[g] = s_z[q];
       bin_out[g] = s_bin[q];
-      if (sh_out) sh_out[g] = s_sh[q];
+      if (SH) sh_out[g] = s_sh[q];
       if (perm64_out) perm64_out[g] = s_perm[q];
       else perm_out[g] = s_perm[q];
     }
@@ -373,7 +425,7 @@ int gm_sort_keys(gm_ctx* ctx, const uint8_t* shard, const int16_t* bin, const in
     return GM_OK;
   }
   // one resident wave of blocks: the scatter's LDS (~139 KiB) allows one 1024-thread block per CU
-  const int resident = resident_blocks((const void*)k_sort_scatter, ctx->device, BT, 1);
+  const int resident = resident_blocks((const void*)k_sort_scatter<false, true>, ctx->device, BT, 1);
   const int nblk = (int)std::max<int64_t>(1, std::min<int64_t>(resident, (n + BTILE - 1) / BTILE));
   const int64_t per = ((n + nblk - 1) / nblk + BTILE - 1) / BTILE * BTILE;
   const int grid = (int)((n + per - 1) / per);
@@ -416,7 +468,9 @@ int gm_sort_keys(gm_ctx* ctx, const uint8_t* shard, const int16_t* bin, const in
     hipLaunchKernelGGL(k_sort_hist, dim3(grid), dim3(HT), 0, s, ish, ibin, iz, n, per, passes[k], hist, vec);
     launch_excl_scan(s, hist, (int64_t)256 * grid, hist, hpart, (int64_t*)nullptr);
     const bool last = k == np - 1;   // the last pass writes the 64-bit permutation itself
-    hipLaunchKernelGGL(k_sort_scatter, dim3(grid), dim3(BT), 0, s, ish, ibin, iz, iperm, osh, obin, oz,
+    auto scatter = sh ? (iperm ? k_sort_scatter<true, true> : k_sort_scatter<true, false>)
+                      : (iperm ? k_sort_scatter<false, true> : k_sort_scatter<false, false>);
+    hipLaunchKernelGGL(scatter, dim3(grid), dim3(BT), 0, s, ish, ibin, iz, iperm, osh, obin, oz,
                        last ? nullptr : operm, last ? perm_out : nullptr, n, per, passes[k], hist, vec);
     if (hipGetLastError() != hipSuccess) rc = hip_fail(hipErrorLaunchFailure, "k_sort_scatter");
     ish = osh; ibin = obin; iz = oz; iperm = operm;

@@ -20,5 +20,5 @@ for g in "${groups[@]}"; do
     > gpurun_out/${tag}_jpmc/p$i.log 2>&1
   i=$((i+1))
 done
-python3 tools/pmc_summary.py gpurun_out/${tag}_jpmc "k_pip_join<true" > gpurun_out/${tag}_jpmc/join.txt
+python3 tools/pmc_summary.py gpurun_out/${tag}_jpmc "k_pip_join_q<true" > gpurun_out/${tag}_jpmc/join.txt
 python3 tools/pmc_summary.py gpurun_out/${tag}_jpmc "k_pip_relate" > gpurun_out/${tag}_jpmc/relate.txt
