@@ -361,12 +361,37 @@ def ranges_batch(dist, fn, args, n_local, nq, reps=3):
     return {"value": nq / dt, "unit": "queries/s", "ms_per_step": dt * 1e3, "ranges": res["n"]}
 
 
-def sort_bytes(b, z, n):
-    """Algorithmic bytes of gm_sort_keys over n rows: the OR/AND read of the key columns that finds
-    the constant digits (10 B/row), then per non-constant byte digit a histogram read of its column
-    (8 B z / 2 B bin) and a scatter that reads and writes z, bin and the 4-B permutation (none read on
-    the first pass; the last pass writes it as 8 B).  Returns (bytes, passes)."""
+def sort_bytes(b, z, n, last):
+    """Algorithmic bytes of gm_sort_keys over n rows, for the path the library reports
+    (GM_PARAM_SORT_LAST: digit passes, + 256 when the runs of equal prefixes were ranked locally):
+    the OR/AND read of the key columns that finds the varying bits (10 B/row); per digit pass a
+    histogram read of the columns its 8 bits touch (8 B z and/or 2 B bin) and a scatter that reads and
+    writes z, bin and the 4-B permutation (none read on the first pass); then either the local ranking
+    (reads z, bin, the 4-B permutation; writes z, bin, an 8-B permutation: 32 B/row) or, for the plain
+    digit passes, the last pass writing the permutation as 8 B.  Returns (bytes, passes, path)."""
     import torch
+    local = last >= 256
+    npass = last - 256 if local else last
+    total = 10.0 * n
+    if local:   # npass digit passes over the top varying bits of K = bin:z (the library's greedy choice:
+        # each digit ends at the highest varying bit below the previous one)
+        bb = b.to(torch.int64) & 0xFFFF
+
+        def varies(bit):
+            col, sh = (z, bit) if bit < 64 else (bb, bit - 64)
+            v = (col >> sh) & 1
+            return int(v.min()) != int(v.max())
+        offs, bit = [], 79
+        for _ in range(npass):
+            while bit >= 0 and not varies(bit):
+                bit -= 1
+            offs.append(max(0, bit - 7))
+            bit = offs[-1] - 1
+        for k, off in enumerate(reversed(offs)):
+            h = (8 if off < 64 else 0) + (2 if off + 8 > 64 else 0)
+            total += (h + 28.0 - (4.0 if k == 0 else 0.0)) * n
+        total += 32.0 * n
+        return total, npass, "prefix passes + local ranks"
     passes = []
     for p in range(8):
         d = (z >> (8 * p)) & 255
@@ -377,8 +402,8 @@ def sort_bytes(b, z, n):
         d = (bb >> (8 * p)) & 255
         if int(d.min()) != int(d.max()):
             passes.append(2)
-    total = 10.0 * n + sum(h + 28.0 for h in passes) * n - (4.0 * n if passes else 0) + (4.0 * n if passes else 0)
-    return total, len(passes)
+    total += sum(h + 28.0 for h in passes) * n - (4.0 * n if passes else 0) + (4.0 * n if passes else 0)
+    return total, len(passes), "digit passes"
 
 
 def gather_pairs(dist, ptids, plids, k):
@@ -425,7 +450,7 @@ def bench_table(a, dist, ctx, b, z):
     def sort_step():
         _lib.check(lib.gm_sort_keys(h, None, P(bs), P(zs), NT, None, P(ob), P(oz), P(perm)), "gm_sort_keys")
     ms_sort = timed(dist, sort_step, 3, 1)
-    sbytes, npass = sort_bytes(bs, zs, NT)
+    sbytes, npass, spath = sort_bytes(bs, zs, NT, ctx.get_param(_lib.GM_PARAM_SORT_LAST))
     del ob, oz, perm
     # the key-range partitioned table (configs[2]): every rank keys its own rows, the ranks sample
     # splitters and exchange rows by key range (one all-to-all over RCCL), each sorts its slice
@@ -458,12 +483,14 @@ def bench_table(a, dist, ctx, b, z):
     del holder, pt
     return {
         "sort_keys": {"value": NT * dist.world / (ms_sort * 1e-3), "unit": "rows/s", "ms_per_step": ms_sort,
-                      "rows_per_gpu": NT, "digit_passes": npass,
+                      "rows_per_gpu": NT, "digit_passes": npass, "path": spath,
                       "roofline": dict(roofline(sbytes, ms_sort), bytes_per_unit=round(sbytes / NT, 2),
                                        kernel="gm_sort_keys (all launches of one sort)"),
-                      "note": "stable LSD radix sort of (bin, z) into table byte order (ingest side); bytes = "
-                              "10 B/row OR/AND read + per pass (digit column read + 28 B/row scatter; no permutation "
-                              "read on the first pass, an 8-B permutation written on the last)"},
+                      "note": "stable sort of (bin, z) into table byte order (ingest side): digit passes over the top "
+                              "~log2(n) + 3 varying key bits, then every run of equal prefixes ranked by full key in LDS "
+                              "(digit passes over every varying byte when a run exceeds 256 rows); bytes = 10 B/row "
+                              "OR/AND read + per pass (digit column read + 28 B/row scatter, no permutation read on the "
+                              "first) + 32 B/row local ranking (see sort_bytes)"},
         "table_ingest": {"value": NT * dist.world / (ms_ingest * 1e-3), "unit": "rows/s", "ms_per_step": ms_ingest,
                          "rows_per_gpu": NT, "slice_rows": slice_rows,
                          "note": "key-range partitioned table: local sort, splitter sampling (1024 keys per rank), "

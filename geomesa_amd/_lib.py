@@ -29,6 +29,8 @@ GM_ST_NULL_GEOM = 4
 GM_PARAM_JOIN_CHUNK = 1
 GM_PARAM_INDEX_BUILD = 2
 GM_PARAM_RANGES_CHUNK = 3
+GM_PARAM_SORT_MODE = 4
+GM_PARAM_SORT_LAST = 5
 
 GM_JOIN_AUTO = 0
 GM_JOIN_DIRECT = 1

@@ -24,6 +24,8 @@ struct gm_ctx {
   int64_t index_build = 0;         // GM_PARAM_INDEX_BUILD: 0 = device build of the join index, 1 = host build
   int64_t ranges_hint = 0;         // largest batched-ranges output seen (sizes the device batch buffer)
   int64_t ranges_chunk = 0;        // GM_PARAM_RANGES_CHUNK: queries per pipelined chunk (0 = default)
+  int64_t sort_last = 0;           // GM_PARAM_SORT_LAST (read-only): the last sort's digit passes | 256 if ranked locally
+  int64_t sort_mode = 0;           // GM_PARAM_SORT_MODE: 0 = auto (prefix passes + local ranks), 1 = digit passes only
   hipStream_t copy_stream = nullptr;   // result copies overlapping the next chunk's kernels (lazy)
   hipEvent_t ev_ready[2] = {nullptr, nullptr}, ev_copied[2] = {nullptr, nullptr};
 };

@@ -80,6 +80,12 @@ struct PipDev {
   // word, null = not checked by this caller) and is treated as EXTERIOR, never dereferenced
   uint32_t* fault;
   int64_t n_line, n_compact_lines, n_blob16, n_list;
+  // coarse EMPTY bitmap (make_shortcut; staged in LDS by the direct join): bit (by * cm_w + bx) set when
+  // every coarse cell of block (bx, by) = coarse cells [bx << cm_shift, (bx + 1) << cm_shift) x (same
+  // in y) is EMPTY; cm_words = 0: no bitmap
+  const uint32_t* cm;
+  int32_t cm_shift, cm_w;
+  int64_t cm_words;
 };
 
 enum : uint32_t { PIP_FAULT_LINE = 1, PIP_FAULT_COMPACT = 2, PIP_FAULT_BLOB = 4, PIP_FAULT_LIST = 8, PIP_FAULT_QUEUE = 16 };
@@ -837,10 +843,16 @@ __global__ __launch_bounds__(256) void k_pair_move(PairOut o, const PairPlan* __
 // before any push of <= 64 (and a line round hands over at most the items it took), F < 128 before
 // a stream step pushes <= 128.  Both are checked (PIP_FAULT_QUEUE).  Pairs are staged per wave and
 // flushed with one atomic per flush.
-#ifndef GM_JQ_WAVES
-#define GM_JQ_WAVES 4               // blocks per CU (= waves per SIMD) the register allocation targets
+// One 768-thread block per CU (12 waves, 9 KiB of queues each) leaves 52 KiB of LDS for the coarse
+// EMPTY bitmap: a point whose coarse block is EMPTY costs no gather at all.  The join is bound by the
+// vector-memory path (TD busy 97%, the L1 stalled on its outstanding misses 83% of the kernel, r3
+// PMC), and the coarse lookups were 70% of its L1 misses; 55% of the bench's points sit in EMPTY
+// coarse cells.
+#ifndef GM_JQ_TPB
+#define GM_JQ_TPB 768
 #endif
-constexpr int QTPB = 256;           // 4 waves per block
+constexpr int QTPB = GM_JQ_TPB;
+constexpr int CM_WORDS_MAX = 13248;   // 52,992 B: 160 KiB minus 12 waves x 9,216 B of queues
 #ifndef GM_JQ_FBATCH
 #define GM_JQ_FBATCH 128
 #endif
@@ -849,7 +861,7 @@ constexpr int FCAP = FBATCH + 128;     // fine queue (< FBATCH + one step's 128)
 constexpr int ICAP = 128;           // item queue (two ends)
 
 template <bool WRITE, int SRC, bool VEC>
-__global__ __launch_bounds__(QTPB, GM_JQ_WAVES) void k_pip_join_q(const double* __restrict__ px, const double* __restrict__ py,
+__global__ __launch_bounds__(QTPB) void k_pip_join_q(const double* __restrict__ px, const double* __restrict__ py,
                                                      int64_t n, int64_t id_base, PipDev d, PairOut po,
                                                      int64_t desc_base, ArrowPts ap) {
   constexpr int NW = QTPB / 64;
@@ -857,6 +869,10 @@ __global__ __launch_bounds__(QTPB, GM_JQ_WAVES) void k_pip_join_q(const double* 
   __shared__ uint32_t s_fid[NW][FCAP], s_fw[NW][FCAP];
   __shared__ double s_ix[NW][ICAP], s_iy[NW][ICAP];
   __shared__ uint32_t s_iid[NW][ICAP], s_iref[NW][ICAP];
+  __shared__ uint32_t s_cm[CM_WORDS_MAX];
+  const int64_t cm_words = d.cm_words <= CM_WORDS_MAX ? d.cm_words : 0;
+  for (int64_t i = threadIdx.x; i < cm_words; i += QTPB) s_cm[i] = d.cm[i];
+  __syncthreads();
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   double* fx = s_fx[wv]; double* fy = s_fy[wv]; uint32_t* fid = s_fid[wv];
   double* qx = s_ix[wv]; double* qy = s_iy[wv]; uint32_t* qid = s_iid[wv]; uint32_t* qref = s_iref[wv];
@@ -1034,16 +1050,19 @@ __global__ __launch_bounds__(QTPB, GM_JQ_WAVES) void k_pip_join_q(const double* 
     if (streaming) {   // ---- stream step: 2 points per lane, their coarse words together
       uint32_t c0 = CELL_EMPTY << 30, c1 = CELL_EMPTY << 30;
       int cx0 = 0, cy0 = 0, cx1 = 0, cy1 = 0;
-      const bool g0 = X0 >= d.gx0 && X0 <= d.gx1 && Y0 >= d.gy0 && Y0 <= d.gy1;   // NaN fails
-      const bool g1 = X1 >= d.gx0 && X1 <= d.gx1 && Y1 >= d.gy0 && Y1 <= d.gy1;
-      if (g0) {
-        cx0 = cell_of(X0, d.gx0, d.inv_cw, d.gx); cy0 = cell_of(Y0, d.gy0, d.inv_ch, d.gy);
-        c0 = d.coarse_sc[(int64_t)(cy0 >> CF_LOG) * d.gxc + (cx0 >> CF_LOG)];
+      bool g0 = X0 >= d.gx0 && X0 <= d.gx1 && Y0 >= d.gy0 && Y0 <= d.gy1;   // NaN fails
+      bool g1 = X1 >= d.gx0 && X1 <= d.gx1 && Y1 >= d.gy0 && Y1 <= d.gy1;
+      if (g0) { cx0 = cell_of(X0, d.gx0, d.inv_cw, d.gx); cy0 = cell_of(Y0, d.gy0, d.inv_ch, d.gy); }
+      if (g1) { cx1 = cell_of(X1, d.gx0, d.inv_cw, d.gx); cy1 = cell_of(Y1, d.gy0, d.inv_ch, d.gy); }
+      if (cm_words) {   // EMPTY coarse blocks from the LDS bitmap: no gather
+        const int b0 = ((cy0 >> CF_LOG) >> d.cm_shift) * d.cm_w + ((cx0 >> CF_LOG) >> d.cm_shift);
+        const int b1 = ((cy1 >> CF_LOG) >> d.cm_shift) * d.cm_w + ((cx1 >> CF_LOG) >> d.cm_shift);
+        const bool e0 = (s_cm[b0 >> 5] >> (b0 & 31)) & 1u, e1 = (s_cm[b1 >> 5] >> (b1 & 31)) & 1u;
+        g0 = g0 && !e0;
+        g1 = g1 && !e1;
       }
-      if (g1) {
-        cx1 = cell_of(X1, d.gx0, d.inv_cw, d.gx); cy1 = cell_of(Y1, d.gy0, d.inv_ch, d.gy);
-        c1 = d.coarse_sc[(int64_t)(cy1 >> CF_LOG) * d.gxc + (cx1 >> CF_LOG)];
-      }
+      if (g0) c0 = d.coarse_sc[(int64_t)(cy0 >> CF_LOG) * d.gxc + (cx0 >> CF_LOG)];
+      if (g1) c1 = d.coarse_sc[(int64_t)(cy1 >> CF_LOG) * d.gxc + (cx1 >> CF_LOG)];
       c0 = coarse_mask(c0, cx0, cy0, d.coarse_fmt);
       c1 = coarse_mask(c1, cx1, cy1, d.coarse_fmt);
       const uint32_t id0 = (uint32_t)(2 * (step * 64 + lane)), id1 = id0 + 1;
@@ -2469,6 +2488,25 @@ __global__ __launch_bounds__(256) void k_build_coarse_sc(const uint32_t* __restr
   }
 }
 
+// the coarse EMPTY bitmap over coarse_sc: one thread per 32-bit word
+__global__ __launch_bounds__(256) void k_build_cmask(const uint32_t* __restrict__ coarse_sc, int gxc, int gyc, int shift,
+                                                     int cw, int ch, int64_t nwords, uint32_t* __restrict__ out) {
+  for (int64_t wi = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; wi < nwords; wi += (int64_t)gridDim.x * blockDim.x) {
+    uint32_t w = 0;
+    for (int k = 0; k < 32; ++k) {
+      const int64_t b = wi * 32 + k;
+      if (b >= (int64_t)cw * ch) break;
+      const int by = (int)(b / cw), bx = (int)(b % cw);
+      bool empty = true;
+      for (int y = by << shift; empty && y < min(gyc, (by + 1) << shift); ++y)
+        for (int x = bx << shift; x < min(gxc, (bx + 1) << shift); ++x)
+          if ((coarse_sc[(int64_t)y * gxc + x] >> 30) != CELL_EMPTY) { empty = false; break; }
+      if (empty) w |= 1u << k;
+    }
+    out[wi] = w;
+  }
+}
+
 // pass 0 (ent == nullptr): cell_sc = resolved words, is_line[c] = 1 for line cells;
 // pass 1: the line entries at their scanned slots, and the LINE words
 template <bool LINES>
@@ -2567,6 +2605,8 @@ int make_shortcut(gm_pip_index* ix) {
   ix->dev.line_ent = nullptr;
   ix->n_lines = 0;
   ix->dev.fault = nullptr;   // set per call (the call's scratch word)
+  ix->dev.cm = nullptr;      // the coarse EMPTY bitmap, built after coarse_sc
+  ix->dev.cm_words = 0;
   ix->dev.n_line = 0;
   ix->dev.n_compact_lines = ix->arr_bytes[5] / 128;
   ix->dev.n_blob16 = ix->arr_bytes[7] / 16;
@@ -2612,6 +2652,20 @@ int make_shortcut(gm_pip_index* ix) {
     hipLaunchKernelGGL(k_build_coarse_sc, dim3((unsigned)std::min<int64_t>(65536, ((int64_t)gxc * gyc + 255) / 256)), dim3(256),
                        0, s, (const uint32_t*)p, ix->dev.gx, ix->dev.gy, gxc, gyc, ix->dev.coarse_fmt,
                        (uint32_t*)ix->dev.coarse_sc);
+    // the coarse EMPTY bitmap: the finest block size whose bitmap fits the join's LDS budget
+    int sh = 0;
+    while ((int64_t)((gxc + (1 << sh) - 1) >> sh) * ((gyc + (1 << sh) - 1) >> sh) > (int64_t)CM_WORDS_MAX * 32) ++sh;
+    const int cw = (gxc + (1 << sh) - 1) >> sh, ch = (gyc + (1 << sh) - 1) >> sh;
+    const int64_t nw = ((int64_t)cw * ch + 31) / 32;
+    void* cm = nullptr;
+    if (hipMalloc(&cm, (size_t)nw * 4) != hipSuccess) { cleanup(); return hip_fail(hipErrorOutOfMemory, "gm_pip_index bitmap"); }
+    ix->allocs.push_back(cm);
+    hipLaunchKernelGGL(k_build_cmask, dim3((unsigned)std::min<int64_t>(4096, (nw + 255) / 256)), dim3(256), 0, s,
+                       (const uint32_t*)ix->dev.coarse_sc, gxc, gyc, sh, cw, ch, nw, (uint32_t*)cm);
+    ix->dev.cm = (const uint32_t*)cm;
+    ix->dev.cm_shift = sh;
+    ix->dev.cm_w = cw;
+    ix->dev.cm_words = nw;
   }
   if (!rc && hipStreamSynchronize(s) != hipSuccess) rc = hip_fail(hipErrorLaunchFailure, "k_build_shortcut");
   cleanup();
@@ -2967,8 +3021,8 @@ static int join_staged(gm_ctx* ctx, const double* px, const double* py, ArrowPts
                        unsigned long long* counter) {
   const bool write = pt_ids && poly_ids;
   const int64_t CHUNK = join_chunk(ctx, (int64_t)1 << 31);
-  const int resident = write ? resident_blocks((const void*)k_pip_join_q<true, SRC, VEC>, ctx->device, QTPB, 4)
-                             : resident_blocks((const void*)k_pip_join_q<false, SRC, VEC>, ctx->device, QTPB, 4);
+  const int resident = write ? resident_blocks((const void*)k_pip_join_q<true, SRC, VEC>, ctx->device, QTPB, 1)
+                             : resident_blocks((const void*)k_pip_join_q<false, SRC, VEC>, ctx->device, QTPB, 1);
   const int64_t wmax = (int64_t)resident * (QTPB / 64);
   if (write && wmax > PLAN_MAX) return hip_fail(hipErrorInvalidValue, "join: more waves than the pair plan holds");
   PairOut po{pt_ids, poly_ids, cap, nullptr, nullptr, 0, counter, nullptr};

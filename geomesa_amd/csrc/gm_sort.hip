@@ -6,11 +6,16 @@
 // getRangeBytes produces (Z3IndexKeySpace.scala:196-238) and the tablet server runs the Z3Filter on
 // every row inside (RowFilterIterator.scala:52-66).  Here the table is columnar and resident in HBM:
 //   * gm_z3_key_bytes  -- the row-key prefix bytes, staged through LDS so the stores are 16-B wide;
-//   * gm_sort_keys     -- a stable LSD radix sort of (shard u8, bin u16, z u64) in that byte order,
-//                         8-bit digits, per-block segments: histogram -> one-block scan -> stable
-//                         scatter (wave ballots rank equal digits, LDS reorders each 8192-row tile so
-//                         the global writes are digit runs).  Passes on which every key has the same
-//                         digit are skipped (one extra read computes all 11 digit histograms);
+//   * gm_sort_keys     -- a stable sort of (shard u8, bin u16, z u64) in that byte order.  The key
+//                         K = shard:bin:z is an 88-bit integer; one read finds its varying bits (OR /
+//                         AND).  Three stable digit passes (8-bit digits, per-block segments:
+//                         histogram -> one-block scan -> scatter, wave ballots rank equal digits, LDS
+//                         reorders each 8192-row tile so the global writes are digit runs) order the
+//                         rows by the top 24 varying bits; then k_sort_local ranks every run of
+//                         equal 24-bit prefixes (~15 rows for 250M uniform keys) by full key in LDS
+//                         and writes the rows to their final places.  A run longer than 1024 rows
+//                         (skewed keys) sends the call to digit passes over every varying byte (LSD,
+//                         the same kernels), which is also GM_PARAM_SORT_MODE 1;
 // The range scan over a sorted table (gm_key_range_scan) lives with the other row-filter scans in
 // gm_filter.hip.
 #include <string.h>
@@ -25,11 +30,17 @@ namespace gm {
 constexpr int STPB = 256;               // sort / scan threads per block
 constexpr int NPASS = 11;               // digit positions: z bytes 0..7, bin bytes 0..1, shard
 
-__device__ __forceinline__ uint32_t key_digit(uint8_t sh, uint16_t b, uint64_t z, int pass) {
-  if (pass < 8) return (uint32_t)(z >> (8 * pass)) & 255u;
-  if (pass < 10) return (uint32_t)(b >> (8 * (pass - 8))) & 255u;
-  return sh;
+// 24 bits of K = bs:z (bs = bin | shard << 16) from bit `off` (0 <= off < 88) up; a digit is the low 8
+__device__ __forceinline__ uint32_t key_bits(uint32_t bs, uint64_t z, int off) {
+  uint64_t v;
+  if (off >= 64) v = (uint64_t)bs >> (off - 64);
+  else {
+    v = z >> off;
+    if (off > 0) v |= (uint64_t)bs << (64 - off);
+  }
+  return (uint32_t)v & 0xffffffu;
 }
+__device__ __forceinline__ uint32_t key_digit(uint32_t bs, uint64_t z, int off) { return key_bits(bs, z, off) & 255u; }
 
 __device__ __forceinline__ uint64_t lanemask_lt() {
   const int lane = threadIdx.x & 63;
@@ -78,76 +89,46 @@ __global__ __launch_bounds__(STPB) void k_key_or_and(const uint8_t* __restrict__
   }
 }
 
-// per-block segment histogram of one digit, digit-major: hist[d * gridDim.x + block].  1024 threads,
-// two rows per lane (16-B z loads), per-wave LDS counters summed at the end.
+// per-block segment histogram of one digit (bits [off, off + 8) of K), digit-major:
+// hist[d * gridDim.x + block].  1024 threads, two rows per lane (16-B z loads), only the columns the
+// digit touches are read, per-wave LDS counters summed at the end.
 constexpr int HT = 1024;
 __global__ __launch_bounds__(HT) void k_sort_hist(const uint8_t* __restrict__ sh, const uint16_t* __restrict__ bin,
                                                   const uint64_t* __restrict__ z, int64_t n, int64_t per_block,
-                                                  int pass, uint32_t* __restrict__ hist, int vec) {
+                                                  int off, uint32_t* __restrict__ hist, int vec) {
   __shared__ uint32_t h[HT / 64][256];
   const int wave = threadIdx.x >> 6;
   for (int i = threadIdx.x; i < (HT / 64) * 256; i += HT) (&h[0][0])[i] = 0;
   __syncthreads();
   const int64_t b0 = (int64_t)blockIdx.x * per_block, b1 = min(n, b0 + per_block);
-  auto digit = [&](int64_t i) -> uint32_t {
-    return pass < 8 ? (uint32_t)(z[i] >> (8 * pass)) & 255u
-                    : pass < 10 ? (uint32_t)(bin[i] >> (8 * (pass - 8))) & 255u : (uint32_t)sh[i];
-  };
+  const bool nz = off < 64, nb = off + 8 > 64 && off < 80, ns = sh != nullptr && off + 8 > 80;
   // full stretches: 4 pairs per lane, loads issued together (a digit extraction between loads made
   // the compiler wait for each pair before the next load)
   constexpr int HU = 4;
   int64_t i = b0 + 2 * threadIdx.x;
   if (vec)
     for (; i + 2 * HT * (HU - 1) + 1 < b1; i += 2 * HT * HU) {
-      uint32_t d[2 * HU];
-      if (pass < 8) {
-        ulonglong2 zz[HU];
+      ulonglong2 zz[HU];
+      uint32_t bb[HU], ss[HU];
 #pragma unroll
-        for (int u = 0; u < HU; ++u) zz[u] = *(const ulonglong2*)(z + i + 2 * HT * u);
-#pragma unroll
-        for (int u = 0; u < HU; ++u) {
-          d[2 * u] = (uint32_t)(zz[u].x >> (8 * pass)) & 255u;
-          d[2 * u + 1] = (uint32_t)(zz[u].y >> (8 * pass)) & 255u;
-        }
-      } else if (pass < 10) {
-        uint32_t bb[HU];
-#pragma unroll
-        for (int u = 0; u < HU; ++u) bb[u] = *(const uint32_t*)(bin + i + 2 * HT * u);
-#pragma unroll
-        for (int u = 0; u < HU; ++u) {
-          d[2 * u] = (bb[u] >> (8 * (pass - 8))) & 255u;
-          d[2 * u + 1] = (bb[u] >> (16 + 8 * (pass - 8))) & 255u;
-        }
-      } else {
-        uint32_t ss[HU];
-#pragma unroll
-        for (int u = 0; u < HU; ++u) ss[u] = *(const uint16_t*)(sh + i + 2 * HT * u);
-#pragma unroll
-        for (int u = 0; u < HU; ++u) { d[2 * u] = ss[u] & 255u; d[2 * u + 1] = (ss[u] >> 8) & 255u; }
+      for (int u = 0; u < HU; ++u) {
+        zz[u] = nz ? *(const ulonglong2*)(z + i + 2 * HT * u) : make_ulonglong2(0ull, 0ull);
+        bb[u] = nb ? *(const uint32_t*)(bin + i + 2 * HT * u) : 0u;
+        ss[u] = ns ? (uint32_t)*(const uint16_t*)(sh + i + 2 * HT * u) : 0u;
       }
 #pragma unroll
-      for (int k = 0; k < 2 * HU; ++k) atomicAdd(&h[wave][d[k]], 1u);
+      for (int u = 0; u < HU; ++u) {
+        atomicAdd(&h[wave][key_digit((bb[u] & 0xffffu) | ((ss[u] & 0xffu) << 16), zz[u].x, off)], 1u);
+        atomicAdd(&h[wave][key_digit((bb[u] >> 16) | ((ss[u] >> 8) << 16), zz[u].y, off)], 1u);
+      }
     }
   for (; i < b1; i += 2 * HT) {   // b0 is even (tile multiple)
-    if (vec && i + 1 < b1) {
-      uint32_t d0, d1;
-      if (pass < 8) {
-        const ulonglong2 zz = *(const ulonglong2*)(z + i);
-        d0 = (uint32_t)(zz.x >> (8 * pass)) & 255u;
-        d1 = (uint32_t)(zz.y >> (8 * pass)) & 255u;
-      } else if (pass < 10) {
-        const ushort2 bb = *(const ushort2*)(bin + i);
-        d0 = (uint32_t)(bb.x >> (8 * (pass - 8))) & 255u;
-        d1 = (uint32_t)(bb.y >> (8 * (pass - 8))) & 255u;
-      } else {
-        const uchar2 ss = *(const uchar2*)(sh + i);
-        d0 = ss.x; d1 = ss.y;
-      }
-      atomicAdd(&h[wave][d0], 1u);
-      atomicAdd(&h[wave][d1], 1u);
-    } else {
-      atomicAdd(&h[wave][digit(i)], 1u);
-      if (i + 1 < b1) atomicAdd(&h[wave][digit(i + 1)], 1u);
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int64_t r = i + e;
+      if (r >= b1) continue;
+      const uint32_t bs = (nb ? (uint32_t)bin[r] : 0u) | (ns ? (uint32_t)sh[r] << 16 : 0u);
+      atomicAdd(&h[wave][key_digit(bs, nz ? z[r] : 0ull, off)], 1u);
     }
   }
   __syncthreads();
@@ -191,7 +172,7 @@ __global__ __launch_bounds__(BT) void k_sort_scatter(const uint8_t* __restrict__
                                                      const uint32_t* __restrict__ perm_in, uint8_t* __restrict__ sh_out,
                                                      uint16_t* __restrict__ bin_out, uint64_t* __restrict__ z_out,
                                                      uint32_t* __restrict__ perm_out, int64_t* __restrict__ perm64_out,
-                                                     int64_t n, int64_t per_block, int pass,
+                                                     int64_t n, int64_t per_block, int doff,
                                                      const uint32_t* __restrict__ off, int vec) {
   __shared__ uint64_t s_z[BTILE];
   __shared__ uint32_t s_perm[BTILE];
@@ -253,8 +234,8 @@ __global__ __launch_bounds__(BT) void k_sort_scatter(const uint8_t* __restrict__
     for (int k = 0; k < BSLOT; ++k) {
       const int64_t i = t0 + wave * (2 * 64 * BSLOT) + k * 128 + 2 * lane;
       const bool ok0 = i < b1, ok1 = i + 1 < b1;
-      const uint32_t d0 = key_digit((uint8_t)(bs[k][0] >> 16), (uint16_t)bs[k][0], zv[k][0], pass);
-      const uint32_t d1 = key_digit((uint8_t)(bs[k][1] >> 16), (uint16_t)bs[k][1], zv[k][1], pass);
+      const uint32_t d0 = key_digit(bs[k][0], zv[k][0], doff);
+      const uint32_t d1 = key_digit(bs[k][1], zv[k][1], doff);
       uint64_t bal0[8], bal1[8];
 #pragma unroll
       for (int bit = 0; bit < 8; ++bit) {
@@ -318,7 +299,7 @@ __global__ __launch_bounds__(BT) void k_sort_scatter(const uint8_t* __restrict__
     if (t0 + BTILE < b1) load(t0 + BTILE);   // issued before the write-out: in flight during it
     const int cnt = (int)min((int64_t)BTILE, b1 - t0);
     for (int q = t; q < cnt; q += BT) {
-      const uint32_t d = key_digit(SH ? s_sh[q] : (uint8_t)0, s_bin[q], s_z[q], pass);
+      const uint32_t d = key_digit((uint32_t)s_bin[q] | (SH ? (uint32_t)s_sh[q] << 16 : 0u), s_z[q], doff);
       const int64_t g = (int64_t)s_gcur[d] + (q - (int)s_dstart[d]);
       z_out[g] = s_z[q];
       bin_out[g] = s_bin[q];
@@ -328,6 +309,129 @@ __global__ __launch_bounds__(BT) void k_sort_scatter(const uint8_t* __restrict__
     }
     __syncthreads();
     if (t < 256) s_gcur[t] += s_tot[t];
+  }
+}
+
+// Final placement after the prefix passes: the digit passes at bit offsets o1 > o2 > ... (each digit
+// ends at a varying bit, and only constant bits lie between them) leave the rows grouped, stably, by
+// P = digit(o1) : digit(o2) : ... -- the key's top varying bits, ~log2(n) + 3 of them, so that runs
+// of equal P are short (Poisson(n / 2^bits) for uniform keys).  Tile k covers the runs of
+// equal P that start in [k LSTEP, (k + 1) LSTEP); its rows are staged in LDS, a block scan marks each
+// row's run (start, and at the start its end), each row counts the rows of its run with a smaller key
+// (ties by position: stable) and goes to run start + rank: O(run length) LDS reads per row.  A run
+// longer than RUN_MAX rows (skewed or repeated keys) sets *flag and the host sorts with digit passes
+// over every varying byte instead.
+constexpr int LT = 512, LCAP = 4096, LPT = LCAP / LT, RUN_MAX = 256, LSTEP = LCAP - RUN_MAX;
+
+// the prefix digits (offsets o.x > o.y > ...; an offset < 0: no digit)
+__device__ __forceinline__ uint32_t prefix3(uint32_t bs, uint64_t z, int4 o) {
+  uint32_t p = 0;
+  p = (p << 8) | (o.x >= 0 ? key_digit(bs, z, o.x) : 0u);
+  p = (p << 8) | (o.y >= 0 ? key_digit(bs, z, o.y) : 0u);
+  p = (p << 8) | (o.z >= 0 ? key_digit(bs, z, o.z) : 0u);
+  p = (p << 8) | (o.w >= 0 ? key_digit(bs, z, o.w) : 0u);
+  return p;
+}
+
+template <bool SH>
+__global__ __launch_bounds__(LT) void k_sort_local(const uint8_t* __restrict__ sh_in, const uint16_t* __restrict__ bin_in,
+                                                   const uint64_t* __restrict__ z_in, const uint32_t* __restrict__ perm_in,
+                                                   uint8_t* __restrict__ sh_out, uint16_t* __restrict__ bin_out,
+                                                   uint64_t* __restrict__ z_out, int64_t* __restrict__ perm_out,
+                                                   int64_t n, int4 po, uint32_t* __restrict__ flag) {
+  __shared__ uint64_t s_z[LCAP];
+  __shared__ uint32_t s_bs[LCAP];
+  __shared__ uint32_t s_run[LCAP];   // prefix; then run start (low 16) | at a run start, its end << 16
+  __shared__ int64_t s_ab[2];
+  __shared__ uint32_t s_wmax[LT / 64];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  auto gbs = [&](int64_t r) -> uint32_t { return (uint32_t)bin_in[r] | (SH ? (uint32_t)sh_in[r] << 16 : 0u); };
+  const int64_t ntile = (n + LSTEP - 1) / LSTEP;
+  for (int64_t tk = blockIdx.x; tk < ntile; tk += gridDim.x) {   // block-uniform
+    if (wave < 2) {   // waves 0 / 1: the first run start at or after p (none within RUN_MAX rows: flag)
+      int64_t p = min(n, (tk + wave) * LSTEP);
+      if (p > 0 && p < n) {
+        const uint32_t pp = prefix3(gbs(p - 1), z_in[p - 1], po);
+        int64_t found = -1;
+        for (int c = 0; c <= RUN_MAX / 64 && found < 0; ++c) {   // wave-uniform
+          const int64_t r = p + c * 64 + lane;
+          const bool diff = r >= n || prefix3(gbs(r), z_in[r], po) != pp;
+          const uint64_t bal = __ballot(diff);
+          if (bal) found = p + c * 64 + __builtin_ctzll(bal);
+        }
+        p = (found < 0 || found - p > RUN_MAX) ? -1 : found;
+        if (p < 0 && lane == 0) *flag = 1u;
+      }
+      if (lane == 0) s_ab[wave] = p;
+    }
+    __syncthreads();
+    const int64_t a = s_ab[0], b = s_ab[1];
+    __syncthreads();
+    if (a < 0 || b < 0) continue;   // flagged: the host redoes the sort
+    const int m = (int)(b - a);     // <= LSTEP + RUN_MAX = LCAP
+    for (int i = t; i < m; i += LT) {
+      const uint64_t zz = z_in[a + i];
+      const uint32_t bb = gbs(a + i);
+      s_z[i] = zz; s_bs[i] = bb; s_run[i] = prefix3(bb, zz, po);
+    }
+    __syncthreads();
+    // run starts: a block max-scan of (row starts a run ? row : 0) over rows [LPT t, LPT t + LPT)
+    uint32_t st[LPT];
+    uint32_t run = 0;
+#pragma unroll
+    for (int k = 0; k < LPT; ++k) {
+      const int i = LPT * t + k;
+      if (i < m && (i == 0 || s_run[i] != s_run[i - 1])) run = (uint32_t)i;
+      st[k] = run;
+    }
+    uint32_t x = run;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(x, o, 64);
+      if (lane >= o) x = max(x, y);
+    }
+    if (lane == 63) s_wmax[wave] = x;
+    __syncthreads();
+    uint32_t carry = 0;
+    for (int w = 0; w < wave; ++w) carry = max(carry, s_wmax[w]);
+    const uint32_t prev = __shfl_up(x, 1, 64);
+    if (lane > 0) carry = max(carry, prev);
+#pragma unroll
+    for (int k = 0; k < LPT; ++k) st[k] = max(st[k], carry);
+    __syncthreads();   // every prefix read before s_run is overwritten
+#pragma unroll
+    for (int k = 0; k < LPT; ++k)
+      if (LPT * t + k < m) s_run[LPT * t + k] = st[k];
+    __syncthreads();
+    // a run's end, stored at its start: written by the next run's first row (or the tile's last row)
+#pragma unroll
+    for (int k = 0; k < LPT; ++k) {
+      const int i = LPT * t + k;
+      if (i < m && i > 0 && st[k] == (uint32_t)i) {
+        const uint32_t ps = s_run[i - 1] & 0xffffu;
+        s_run[ps] = ps | ((uint32_t)i << 16);
+      }
+      if (i == m - 1) s_run[st[k]] = st[k] | ((uint32_t)m << 16);
+    }
+    __syncthreads();
+    for (int i = t; i < m; i += LT) {
+      const int s0 = (int)(s_run[i] & 0xffffu), e0 = (int)(s_run[s0] >> 16);
+      if (e0 - s0 > RUN_MAX) { *flag = 1u; continue; }
+      const uint64_t zi = s_z[i];
+      const uint32_t bi = s_bs[i];
+      int r = 0;
+      for (int j = s0; j < e0; ++j) {
+        const uint32_t bj = s_bs[j];
+        const uint64_t zj = s_z[j];
+        r += (bj < bi) || (bj == bi && (zj < zi || (zj == zi && j < i)));
+      }
+      const int64_t dst = a + s0 + r;
+      z_out[dst] = zi;
+      bin_out[dst] = (uint16_t)bi;
+      if (SH) sh_out[dst] = (uint8_t)(bi >> 16);
+      perm_out[dst] = perm_in ? (int64_t)perm_in[a + i] : a + i;
+    }
+    __syncthreads();
   }
 }
 
@@ -397,39 +501,62 @@ int gm_sort_keys(gm_ctx* ctx, const uint8_t* shard, const int16_t* bin, const in
   const bool user_vec = ((uintptr_t)z % 16) == 0 && ((uintptr_t)bin % 4) == 0 && (!sh || ((uintptr_t)sh % 2) == 0);
   const bool out_vec = ((uintptr_t)z_out % 16) == 0 && ((uintptr_t)bin_out % 4) == 0 &&
                        (!sh || ((uintptr_t)shard_out % 2) == 0);
-  // which digit passes carry information (k_key_or_and)
+  // which key bits vary (k_key_or_and): acc = OR z, OR bs, AND z, AND bs (bs = bin | shard << 16)
   unsigned long long* acc = (unsigned long long*)ctx->d_scratch;
   GM_HIP(hipMemsetAsync(acc, 0, 16, s));
   GM_HIP(hipMemsetAsync(acc + 2, 0xff, 16, s));
+  GM_HIP(hipMemsetAsync(acc + 4, 0, 8, s));   // k_sort_local's flag
   hipLaunchKernelGGL(k_key_or_and, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(2048, (n / 2 + STPB - 1) / STPB))),
                      dim3(STPB), 0, s, sh, (const uint16_t*)bin, (const uint64_t*)z, n, acc, (int)user_vec);
   GM_CHECK_LAUNCH();
   unsigned long long hacc[4];
   GM_HIP(hipMemcpyAsync(hacc, acc, sizeof(hacc), hipMemcpyDeviceToHost, s));
   GM_HIP(hipStreamSynchronize(s));
-  std::vector<int> passes;
+  // LSD digit offsets: every byte on which some keys differ
+  std::vector<int> lsd;
   for (int p = 0; p < NPASS; ++p) {
     if (p == 10 && !sh) continue;
     const uint64_t o = p < 8 ? hacc[0] >> (8 * p) : hacc[1] >> (8 * (p - 8));
     const uint64_t a = p < 8 ? hacc[2] >> (8 * p) : hacc[3] >> (8 * (p - 8));
-    if (((o ^ a) & 255u) != 0) passes.push_back(p);
+    if (((o ^ a) & 255u) != 0) lsd.push_back(8 * p);
   }
-  const int np = (int)passes.size();
-  if (np == 0) {  // every key equal: table order = input order
+  if (lsd.empty()) {  // every key equal: table order = input order
     if (sh) GM_HIP(hipMemcpyAsync(shard_out, sh, (size_t)n, hipMemcpyDeviceToDevice, s));
     GM_HIP(hipMemcpyAsync(bin_out, bin, (size_t)n * 2, hipMemcpyDeviceToDevice, s));
     GM_HIP(hipMemcpyAsync(z_out, z, (size_t)n * 8, hipMemcpyDeviceToDevice, s));
     hipLaunchKernelGGL(k_widen_perm, dim3((unsigned)std::min<int64_t>(4096, (n + STPB - 1) / STPB)), dim3(STPB), 0, s,
                        nullptr, n, perm_out);
     GM_CHECK_LAUNCH();
+    ctx->sort_last = 0;
     return GM_OK;
   }
+  // prefix passes: digits each ending at the highest varying bit below the previous one (only constant
+  // bits are skipped), ceil((log2 n + 3) / 8) of them (at most 4), when that is fewer than the
+  // varying bytes
+  const uint64_t vz = hacc[0] ^ hacc[2], vb = (hacc[1] ^ hacc[3]) & 0xffffffull;
+  auto varying = [&](int bit) -> bool { return bit < 64 ? ((vz >> bit) & 1u) : ((vb >> (bit - 64)) & 1u); };
+  int lg = 0;
+  while (((int64_t)1 << lg) < n) ++lg;
+  const int npre = std::min(4, (lg + 3 + 7) / 8);
+  int pofs[4] = {-1, -1, -1, -1};
+  int nfound = 0;
+  {
+    int bit = 87;
+    for (int k = 0; k < npre; ++k) {
+      while (bit >= 0 && !varying(bit)) --bit;
+      if (bit < 0) break;
+      pofs[k] = std::max(0, bit - 7);
+      bit = pofs[k] - 1;
+      ++nfound;
+    }
+  }
+  const bool prefix_mode = ctx->sort_mode == 0 && (int)lsd.size() > npre && nfound == npre;
   // one resident wave of blocks: the scatter's LDS (~139 KiB) allows one 1024-thread block per CU
   const int resident = resident_blocks((const void*)k_sort_scatter<false, true>, ctx->device, BT, 1);
   const int nblk = (int)std::max<int64_t>(1, std::min<int64_t>(resident, (n + BTILE - 1) / BTILE));
   const int64_t per = ((n + nblk - 1) / nblk + BTILE - 1) / BTILE * BTILE;
   const int grid = (int)((n + per - 1) / per);
-  // ping-pong: the user outputs and one temp set; the last pass lands in the user outputs
+  // ping-pong: the user outputs and one temp set
   uint8_t* tsh = nullptr;
   uint16_t* tbin = nullptr;
   uint64_t* tz = nullptr;
@@ -452,30 +579,65 @@ int gm_sort_keys(gm_ctx* ctx, const uint8_t* shard, const int16_t* bin, const in
     hpart = (int64_t*)q; q += a_pt;
     if (sh) tsh = (uint8_t*)q;
   }
-  const uint8_t* ish = sh;
-  const uint16_t* ibin = (const uint16_t*)bin;
-  const uint64_t* iz = (const uint64_t*)z;
-  const uint32_t* iperm = nullptr;
-  int rc = GM_OK;
-  for (int k = 0; k < np && !rc; ++k) {
-    const bool to_user = ((np - 1 - k) % 2) == 0;
-    uint8_t* osh = sh ? (to_user ? shard_out : tsh) : nullptr;
-    uint16_t* obin = to_user ? (uint16_t*)bin_out : tbin;
-    uint64_t* oz = to_user ? (uint64_t*)z_out : tz;
-    uint32_t* operm = (k % 2) ? p1 : p0;
-    // pass 0 reads the caller's columns, a later pass reads the caller's outputs or the workspace
-    const int vec = k == 0 ? (int)user_vec : (((np - k) % 2) == 0 ? (int)out_vec : 1);
-    hipLaunchKernelGGL(k_sort_hist, dim3(grid), dim3(HT), 0, s, ish, ibin, iz, n, per, passes[k], hist, vec);
-    launch_excl_scan(s, hist, (int64_t)256 * grid, hist, hpart, (int64_t*)nullptr);
-    const bool last = k == np - 1;   // the last pass writes the 64-bit permutation itself
-    auto scatter = sh ? (iperm ? k_sort_scatter<true, true> : k_sort_scatter<true, false>)
-                      : (iperm ? k_sort_scatter<false, true> : k_sort_scatter<false, false>);
-    hipLaunchKernelGGL(scatter, dim3(grid), dim3(BT), 0, s, ish, ibin, iz, iperm, osh, obin, oz,
-                       last ? nullptr : operm, last ? perm_out : nullptr, n, per, passes[k], hist, vec);
-    if (hipGetLastError() != hipSuccess) rc = hip_fail(hipErrorLaunchFailure, "k_sort_scatter");
-    ish = osh; ibin = obin; iz = oz; iperm = operm;
+  // digit passes at bit offsets `offs` (LSD order) from the caller's columns; the last pass lands in
+  // the user outputs when `to_user_last`, else in the workspace (read by k_sort_local); `perm64`:
+  // the last pass writes the 64-bit permutation
+  const uint8_t *rsh = nullptr;
+  const uint16_t* rbin = nullptr;
+  const uint64_t* rz = nullptr;
+  const uint32_t* rperm = nullptr;
+  auto passes = [&](const std::vector<int>& offs, bool to_user_last) -> int {
+    const int np = (int)offs.size();
+    const uint8_t* ish = sh;
+    const uint16_t* ibin = (const uint16_t*)bin;
+    const uint64_t* iz = (const uint64_t*)z;
+    const uint32_t* iperm = nullptr;
+    for (int k = 0; k < np; ++k) {
+      const bool to_user = ((np - 1 - k) % 2 == 0) == to_user_last;
+      uint8_t* osh = sh ? (to_user ? shard_out : tsh) : nullptr;
+      uint16_t* obin = to_user ? (uint16_t*)bin_out : tbin;
+      uint64_t* oz = to_user ? (uint64_t*)z_out : tz;
+      uint32_t* operm = (k % 2) ? p1 : p0;
+      // pass 0 reads the caller's columns, a later pass reads the caller's outputs or the workspace
+      const int vec = k == 0 ? (int)user_vec : (ibin == (const uint16_t*)bin_out ? (int)out_vec : 1);
+      hipLaunchKernelGGL(k_sort_hist, dim3(grid), dim3(HT), 0, s, ish, ibin, iz, n, per, offs[k], hist, vec);
+      launch_excl_scan(s, hist, (int64_t)256 * grid, hist, hpart, (int64_t*)nullptr);
+      const bool last64 = to_user_last && k == np - 1;   // the last pass writes the 64-bit permutation itself
+      auto scatter = sh ? (iperm ? k_sort_scatter<true, true> : k_sort_scatter<true, false>)
+                        : (iperm ? k_sort_scatter<false, true> : k_sort_scatter<false, false>);
+      hipLaunchKernelGGL(scatter, dim3(grid), dim3(BT), 0, s, ish, ibin, iz, iperm, osh, obin, oz,
+                         last64 ? nullptr : operm, last64 ? perm_out : nullptr, n, per, offs[k], hist, vec);
+      if (hipGetLastError() != hipSuccess) return hip_fail(hipErrorLaunchFailure, "k_sort_scatter");
+      ish = osh; ibin = obin; iz = oz; iperm = operm;
+    }
+    rsh = ish; rbin = ibin; rz = iz; rperm = iperm;
+    return GM_OK;
+  };
+  if (prefix_mode) {
+    std::vector<int> offs(pofs, pofs + npre);
+    std::reverse(offs.begin(), offs.end());   // LSD order: lowest digit first
+    int rc = passes(offs, false);
+    if (rc) return rc;
+    const int4 po = make_int4(pofs[0], pofs[1], pofs[2], pofs[3]);
+    const int lgrid = resident_blocks((const void*)k_sort_local<false>, ctx->device, LT, 2);
+    if (sh)
+      hipLaunchKernelGGL(k_sort_local<true>, dim3(lgrid), dim3(LT), 0, s, rsh, rbin, rz, rperm, shard_out,
+                         (uint16_t*)bin_out, (uint64_t*)z_out, perm_out, n, po, (uint32_t*)(acc + 4));
+    else
+      hipLaunchKernelGGL(k_sort_local<false>, dim3(lgrid), dim3(LT), 0, s, rsh, rbin, rz, rperm, nullptr,
+                         (uint16_t*)bin_out, (uint64_t*)z_out, perm_out, n, po, (uint32_t*)(acc + 4));
+    GM_CHECK_LAUNCH();
+    uint32_t flag = 0;
+    GM_HIP(hipMemcpyAsync(&flag, acc + 4, 4, hipMemcpyDeviceToHost, s));
+    GM_HIP(hipStreamSynchronize(s));
+    if (!flag) {
+      ctx->sort_last = 256 + npre;
+      return GM_OK;
+    }
+    // a run of equal prefixes longer than RUN_MAX: digit passes over every varying byte
   }
-  return rc;
+  ctx->sort_last = (int64_t)lsd.size() + (prefix_mode ? npre : 0);   // (a failed prefix attempt included)
+  return passes(lsd, true);
 }
 
 }  // extern "C"

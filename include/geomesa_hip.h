@@ -101,6 +101,12 @@ const char* gm_last_error(void);
                                    memory: chunk k's result copy runs while chunk k + 1 computes (0 =
                                    default: one batch below 16384 queries, else about nq / 8 per chunk);
                                    the output never changes */
+#define GM_PARAM_SORT_MODE 4    /* gm_sort_keys: 0 (default) = three digit passes over the top 24 varying
+                                   key bits, then every run of equal prefixes ranked in LDS (digit passes
+                                   over every varying byte when a run exceeds 1024 rows); 1 = digit passes
+                                   over every varying byte.  The output never changes */
+#define GM_PARAM_SORT_LAST 5    /* read-only (gm_ctx_get_param): how the context's last gm_sort_keys ran:
+                                   digit passes, plus 256 when the runs were ranked locally */
 int gm_ctx_set_param(gm_ctx* ctx, int param, int64_t value);
 int gm_ctx_get_param(gm_ctx* ctx, int param, int64_t* value);
 /* device memory helpers for callers without their own allocator (e.g. a JNI shim) */

@@ -28,9 +28,13 @@ def expected_order(bins, z, shard=None):
 
 
 @pytest.mark.parametrize("n,kind", [(1, "rand"), (2, "rand"), (2047, "rand"), (2049, "rand"), (300_001, "rand"),
-                                    (100_000, "equal"), (100_000, "few"), (1_000_003, "keys")])
+                                    (100_000, "equal"), (100_000, "few"), (1_000_003, "keys"), (399_900, "dups"),
+                                    (600_000, "narrow"), (200_000, "runs")])
 @pytest.mark.parametrize("sharded", [False, True])
-def test_sort_keys_parity(gpu, n, kind, sharded):
+@pytest.mark.parametrize("mode", [0, 1])
+def test_sort_keys_parity(gpu, n, kind, sharded, mode):
+    """mode 0: prefix passes + local ranks (digit passes when a run of equal 24-bit prefixes exceeds
+    256 rows: "dups"); mode 1: digit passes over every varying byte (GM_PARAM_SORT_MODE)."""
     import torch
     from geomesa_amd import _lib
     rng = np.random.default_rng(n + sharded)
@@ -41,12 +45,25 @@ def test_sort_keys_parity(gpu, n, kind, sharded):
         bins = np.full(n, 2610, np.int16); z = np.full(n, 123456789, np.int64)
     elif kind == "few":    # heavy duplicates: stability decides the permutation
         bins = rng.integers(2608, 2611, n).astype(np.int16); z = rng.integers(0, 5, n).astype(np.int64)
+    elif kind == "dups":   # real keys, each repeated 300 times: runs longer than 256 rows
+        x = rng.uniform(-180, 180, n // 300); y = rng.uniform(-90, 90, n // 300); t = rng.integers(T2020, T2021, n // 300)
+        b, zz = Z3IndexKeySpace().sfc.index_keys(x, y, t)
+        idx = rng.permutation(np.repeat(np.arange(n // 300), 300))
+        bins, z = as_np(b)[idx], as_np(zz)[idx]
+    elif kind == "narrow":  # one bin, 40 varying z bits: the prefix window straddles no column
+        bins = np.full(n, -7, np.int16); z = rng.integers(0, 2**40, n, dtype=np.int64)
+    elif kind == "runs":   # runs of 1-48 equal prefixes with distinct low bits (ranked locally, ties included)
+        pre = np.repeat(rng.choice(2**24, 12000, replace=False), rng.integers(1, 49, 12000))[:n].astype(np.int64)
+        rng.shuffle(pre)
+        bins = (pre >> 12).astype(np.int16)
+        z = ((pre & 0xfff) << 52) | rng.integers(0, 8, n, dtype=np.int64)   # bits 52-63 (negative z included)
     else:                  # real keys
         x = rng.uniform(-180, 180, n); y = rng.uniform(-90, 90, n); t = rng.integers(T2020, T2021, n)
         b, zz = Z3IndexKeySpace().sfc.index_keys(x, y, t)
         bins, z = as_np(b), as_np(zz)
     shard = rng.integers(0, 4, n).astype(np.uint8) if sharded else None
     ctx = _lib.context()
+    ctx.set_param(_lib.GM_PARAM_SORT_MODE, mode)
     db, dz = torch.from_numpy(bins).cuda(), torch.from_numpy(z).cuda()
     ds = torch.from_numpy(shard).cuda() if sharded else None
     ob, oz, op = torch.empty_like(db), torch.empty_like(dz), torch.empty(n, dtype=torch.int64, device="cuda")
@@ -58,6 +75,14 @@ def test_sort_keys_parity(gpu, n, kind, sharded):
     assert np.array_equal(as_np(ob), bins[order]) and np.array_equal(as_np(oz), z[order])
     if sharded:
         assert np.array_equal(as_np(os_), shard[order])
+    last = ctx.get_param(_lib.GM_PARAM_SORT_LAST)
+    ctx.set_param(_lib.GM_PARAM_SORT_MODE, 0)
+    if mode == 1:
+        assert last < 256
+    elif kind in ("rand", "keys", "narrow", "runs") and n > 100_000:
+        assert last >= 256 + 3, last          # prefix passes + local ranks
+    elif kind == "dups":
+        assert last < 256 and last > 3, last  # runs > 256 rows: digit passes
 
 
 @pytest.mark.parametrize("in_off,out_off", [(1, 0), (0, 1), (1, 3)])

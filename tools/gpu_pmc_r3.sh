@@ -14,17 +14,22 @@ groups=(
   "TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum"
 )
 if [ -n "$PMC_GROUPS" ]; then IFS=";" read -ra groups <<< "$PMC_GROUPS"; fi
+cmd="python3 bench.py"
 if [ "$leg" = join ]; then args="--only join --no-cpu --no-gather --steps 1 --warmup 0 --join-steps 1"
+elif [ "$leg" = ranges ]; then cmd="python3 tools/ranges_probe.py"; args="100000"
 else args="--only z3,table --no-cpu --steps 1 --warmup 0"; fi
 i=0
 for g in "${groups[@]}"; do
   timeout -s KILL 120 rocprofv3 --kernel-trace --output-format csv --pmc $g -d $out/p$i -o run -- \
-    python3 bench.py $args > $out/p$i.log 2>&1 || { echo "pass $i ($g) failed: $?" >> $out/failed.txt; break; }
+    $cmd $args > $out/p$i.log 2>&1 || { echo "pass $i ($g) failed: $?" >> $out/failed.txt; break; }
   i=$((i+1))
 done
 if [ "$leg" = join ]; then
   python3 tools/pmc_summary.py $out "k_pip_join_q<true" > $out/join.txt
   python3 tools/pmc_summary.py $out "k_pip_relate" > $out/relate.txt
+elif [ "$leg" = ranges ]; then
+  python3 tools/pmc_summary.py $out "k_xzranges<3>" > $out/xz3.txt
+  python3 tools/pmc_summary.py $out "k_xzranges<2>" > $out/xz2.txt
 else
   python3 tools/pmc_summary.py $out "k_sort_scatter" > $out/scatter.txt
   python3 tools/pmc_summary.py $out "k_sort_hist" > $out/hist.txt

@@ -3,6 +3,7 @@ of each result (so two library builds, picked with GEOMESA_HIP_LIB, can be compa
 
     python tools/ranges_probe.py [n_queries]
 """
+import ctypes
 import hashlib
 import os
 import sys
@@ -40,6 +41,29 @@ def timed(name, fn, args, nq, reps=3):
           % (name, nq, n, min(ts), sum(ts) / len(ts), dig), flush=True)
 
 
+def timed_dev(name, fn, args, nq, cap, reps=3):
+    """The same entry point writing into device memory (the ranges stay in HBM for a device-side
+    consumer such as gm_key_range_scan): no copy back; the digest must equal the host-output run's."""
+    import torch
+    out = torch.empty(int(cap) * R.RANGE_DTYPE.itemsize, dtype=torch.uint8, device="cuda")
+    ts = []
+    for _ in range(reps + 1):
+        offs = np.zeros(nq + 1, np.int64)
+        needed = ctypes.c_int64()
+        qst = np.zeros(nq, np.int32)
+        torch.cuda.synchronize()
+        t0 = time.time()
+        _lib.check(fn(*args, offs.ctypes.data, out.data_ptr(), int(cap), ctypes.byref(needed), qst.ctypes.data), name)
+        torch.cuda.synchronize()
+        ts.append((time.time() - t0) * 1e3)
+    ts = ts[1:]
+    n = int(offs[-1])
+    rr = out[:n * R.RANGE_DTYPE.itemsize].cpu().numpy().view(R.RANGE_DTYPE)
+    dig = hashlib.sha1(offs.tobytes() + np.asarray(rr[:n]).tobytes() + qst.tobytes()).hexdigest()[:12]
+    print("%-4s %d queries %10d ranges  best %8.2f ms  mean %8.2f ms  digest %s  (device output)"
+          % (name, nq, n, min(ts), sum(ts) / len(ts), dig), flush=True)
+
+
 def main(nq=100_000):
     ctx = _lib.context()
     if os.environ.get("GM_RANGES_CHUNK"):   # pipelined chunk size (GM_PARAM_RANGES_CHUNK) for sweeps
@@ -49,6 +73,9 @@ def main(nq=100_000):
     woff = np.arange(nq + 1, dtype=np.int32)
     timed("xz2", lib.gm_xz2_ranges, (h, nq, woff.ctypes.data, win.ctypes.data, 12, 2000), nq)
     timed("xz3", lib.gm_xz3_ranges, (h, nq, woff.ctypes.data, win3.ctypes.data, 12, 1, 2000), nq)
+    if os.environ.get("GM_RANGES_DEV", "1") == "1":
+        timed_dev("xz2", lib.gm_xz2_ranges, (h, nq, woff.ctypes.data, win.ctypes.data, 12, 2000), nq, nq * 256)
+        timed_dev("xz3", lib.gm_xz3_ranges, (h, nq, woff.ctypes.data, win3.ctypes.data, 12, 1, 2000), nq, nq * 1024)
     rng = np.random.default_rng(1)
     qs = []
     for _ in range(4096):
