@@ -10,6 +10,7 @@ hot-path kernels are reported under "extra".  Inputs are generated on the device
 the timed region; the CPU restatement (oracle/) is timed on a bounded sample as cpu_baseline.
 """
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -338,6 +339,11 @@ def pcie_encode(dist, ctx, x, y, t, z_ref, n=64 << 20, chunk=8 << 20, reps=3):
                     "8M-point chunks double-buffered over a copy stream); never `value`"}
 
 
+def _lib_check(rc):
+    from geomesa_amd import _lib
+    _lib.check(rc, "batched ranges (device output)")
+
+
 def ranges_batch(dist, fn, args, n_local, nq, reps=3):
     """One batched-ranges entry point over this rank's block of queries, then the gather of every
     rank's offsets + ranges to rank 0; wall time per batch (barrier on both sides, max over ranks)."""
@@ -358,7 +364,30 @@ def ranges_batch(dist, fn, args, n_local, nq, reps=3):
         step()
     dist.barrier()
     dt = dist.max((time.time() - t0) / reps)
-    return {"value": nq / dt, "unit": "queries/s", "ms_per_step": dt * 1e3, "ranges": res["n"]}
+    # the same call writing into HBM (the ranges feed a device-side seek such as gm_key_range_scan):
+    # no D2H copy of the ranges, no gather; per rank, max over ranks
+    import torch
+    dout = torch.empty(max(cap, 1) * R.RANGE_DTYPE.itemsize, dtype=torch.uint8, device="cuda")
+    offd = np.zeros(n_local + 1, np.int64)
+    qst = np.zeros(max(n_local, 1), np.int32)
+    needed = ctypes.c_int64()
+
+    def dev_step():
+        _lib_check(fn(*args, offd.ctypes.data, dout.data_ptr(), cap, ctypes.byref(needed), qst.ctypes.data))
+    dev_step()
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.time()
+    for _ in range(reps):
+        dev_step()
+    torch.cuda.synchronize()
+    dist.barrier()
+    ddt = dist.max((time.time() - t0) / reps)
+    same = bool(np.array_equal(offd, offs)) if dist.world == 1 else None
+    del dout
+    return {"value": nq / dt, "unit": "queries/s", "ms_per_step": dt * 1e3, "ranges": res["n"],
+            "device_output": {"ms_per_step": ddt * 1e3, "queries_per_s": nq / ddt, "offsets_equal": same,
+                              "note": "ranges written into HBM (device-side consumer), windows H2D included"}}
 
 
 def sort_bytes(b, z, n, last):
