@@ -31,7 +31,10 @@
 
 namespace gm {
 
-constexpr int RTPB = 256;
+#ifndef GM_RTPB
+#define GM_RTPB 256
+#endif
+constexpr int RTPB = GM_RTPB;   // threads per query (one workgroup each)
 constexpr int RNW = RTPB / 64;
 constexpr int MAXB = 256;       // zbounds / windows per query
 constexpr int LDS_SORT = 4096;  // ranges sorted in LDS; larger lists sort in global memory
