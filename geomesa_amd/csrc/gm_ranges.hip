@@ -32,7 +32,7 @@
 namespace gm {
 
 #ifndef GM_RTPB
-#define GM_RTPB 256
+#define GM_RTPB 512
 #endif
 constexpr int RTPB = GM_RTPB;   // threads per query (one workgroup each)
 constexpr int RNW = RTPB / 64;

@@ -27,10 +27,11 @@ STREAMING = {
     "z3_histogram": ("k_z3_hist_lds<", "points", 24.0),
     "pip_relate": ("k_pip_relate", "points", 21.0),
     "sort_scatter": ("k_sort_scatter", "rows", 28.0),
+    "sort_local": ("k_sort_local", "rows", 32.0),
 }
 # join step kernels and the points per dispatch: direct = one pass per 2^31 points, partitioned =
 # hist + scan + scatter + join per 2^28-point chunk
-JOIN_MODES = {"direct": (["k_pip_join<true, false, false"], 1 << 31),
+JOIN_MODES = {"direct": (["k_pip_join_q<true", "k_pair_plan", "k_pair_move"], 1 << 31),
               "partitioned": (["k_band_hist", "k_band_scan", "k_band_scatter", "k_pip_join<true, true, false"], 1 << 28)}
 
 
@@ -90,7 +91,7 @@ def main(root, out, points=1_000_000_000, join_points=1_000_000_000, table_rows=
                                "note": "whole join step; FETCH_SIZE doubled (exact for the streaming point reads, "
                                        "uncalibrated for the index gathers: raw value in bytes_raw)"}
     # FP64 VALU work of the join (SQ_INSTS_VALU_FLOPS_FP64 pass), per launch
-    fp = mean_for(d, "k_pip_join<true, false, false", "SQ_INSTS_VALU_FLOPS_FP64")
+    fp = mean_for(d, "k_pip_join_q<true", "SQ_INSTS_VALU_FLOPS_FP64")
     if fp is not None:
         res["pip_join_fp64"] = {"n": join_points, "sq_insts_valu_flops_fp64": fp,
                                 "note": "rocprofv3 SQ_INSTS_VALU_FLOPS_FP64 per dispatch of the direct join kernel"}
