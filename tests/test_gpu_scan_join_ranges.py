@@ -334,6 +334,32 @@ def test_xz2_ranges_batch_parity(gpu, oracle, max_ranges):
         assert [tuple(r) for r in g] == oracle.xz2_ranges(q, max_ranges=max_ranges)
 
 
+@pytest.mark.parametrize("dims", [2, 3])
+def test_xz_ranges_many_windows(gpu, oracle, dims):
+    """Queries with more windows than the first pass stages in LDS (16) run again in the second pass
+    with every window in LDS; batched with one-window queries, the output equals the oracle's."""
+    from geomesa_amd.curve import XZ2SFC, XZ3SFC
+    rng = np.random.default_rng(31 + dims)
+    qs = []
+    for k in range(40):
+        nw = [1, 15, 16, 17, 40, 256][k % 6]
+        ws = []
+        for _ in range(nw):
+            x0, y0 = rng.uniform(-170, 160), rng.uniform(-80, 70)
+            w, h = rng.uniform(0.01, 8), rng.uniform(0.01, 8)
+            if dims == 2:
+                ws.append((x0, y0, x0 + w, y0 + h))
+            else:
+                t0 = rng.uniform(0, 500000)
+                ws.append((x0, y0, t0, x0 + w, y0 + h, t0 + rng.uniform(60, 90000)))
+        qs.append(ws)
+    sfc = XZ2SFC(12) if dims == 2 else XZ3SFC(12, "week")
+    got = sfc.ranges_batch(qs, 2000)
+    for q, g in zip(qs, got):
+        exp = oracle.xz2_ranges(q, max_ranges=2000) if dims == 2 else oracle.xz3_ranges(q, max_ranges=2000)
+        assert [tuple(r) for r in g] == exp
+
+
 @pytest.mark.parametrize("max_ranges", [10000, 2000, 50])
 def test_xz3_ranges_batch_parity(gpu, oracle, max_ranges):
     from geomesa_amd.curve import XZ3SFC
