@@ -1721,7 +1721,10 @@ __global__ __launch_bounds__(256) void k_pip_census(const double* __restrict__ p
 // (PointLocator.locate), so the kernel writes that location (LOC_*) and the host maps it.
 // The lookup is the join's: cell word chain, then only the entry of polygon poly[i] -- INTERIOR
 // decides at once, a blob is walked; no entry means the cell misses the polygon (exterior).
-constexpr int RTPB = 256;
+#ifndef GM_RELATE_TPB
+#define GM_RELATE_TPB 256
+#endif
+constexpr int RTPB = GM_RELATE_TPB;   // row-predicate threads per block
 constexpr uint8_t LOC_NULL = 0xff;
 
 __device__ __forceinline__ int entry_poly(const PipDev& d, uint32_t e) {
@@ -3900,7 +3903,8 @@ int gm_pip_relate(gm_ctx* ctx, const gm_pip_index* ix, const int32_t* poly, cons
   if (n == 0) return GM_OK;
   if (!poly || !px || !py || !loc) return GM_E_INVALID;
   GM_HIP(hipSetDevice(ctx->device));
-  const unsigned grid = resident_grid(k_pip_relate, ctx->device, (n + RTPB * RILP - 1) / (RTPB * RILP), false);
+  const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(resident_blocks((const void*)k_pip_relate, ctx->device, RTPB, 1),
+                                                                          (n + RTPB * RILP - 1) / (RTPB * RILP)));
   hipLaunchKernelGGL(k_pip_relate, dim3(grid), dim3(RTPB), 0, ctx->stream, poly, px, py, n, ix->n_polys, ix->dev,
                      ix->list_poly, loc);
   GM_CHECK_LAUNCH();
