@@ -144,7 +144,10 @@ __global__ __launch_bounds__(HTPB) void k_z3_hist_lds(const double* __restrict__
     } else {
       if (NARROW) narrow_inc((uint32_t*)&cnt[c >> 1], (c & 1) * 16, &counts[c]);
       else atomicAdd(&cnt[c], 1);
-      if (!pres[rb]) pres[rb] = 1;           // binMap.getOrElseUpdate(timeBin, newBins)
+      // binMap.getOrElseUpdate(timeBin, newBins): a row is present iff one of its features was
+      // counted; int32 counters only grow here, so the flush derives it from the row (no per-point
+      // LDS read); biased 16-bit halves move to the device counters and cannot tell, so they mark it
+      if (NARROW && !pres[rb]) pres[rb] = 1;
     }
   };
   const int64_t stride = (int64_t)gridDim.x * HTPB;
@@ -192,6 +195,11 @@ __global__ __launch_bounds__(HTPB) void k_z3_hist_lds(const double* __restrict__
   for (int i = threadIdx.x; i < total; i += HTPB) {
     const int v = NARROW ? (int)((((uint32_t)cnt[i >> 1]) >> ((i & 1) * 16)) & 0xFFFFu) - (int)NB : cnt[i];
     if (v) atomicAdd(&counts[i], (unsigned long long)(long long)v);
+  }
+  if (!UNOBS && !NARROW) {   // a row with a nonzero counter was seen by this workgroup
+    for (int i = threadIdx.x; i < total; i += HTPB)
+      if (cnt[i] && !pres[i / a.length]) pres[i / a.length] = 1;
+    __syncthreads();
   }
   if (!UNOBS) {
     for (int i = threadIdx.x; i < a.row_n; i += HTPB)
