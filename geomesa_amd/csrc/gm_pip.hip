@@ -894,16 +894,18 @@ __global__ __launch_bounds__(256) void k_pair_move(PairOut o, const PairPlan* __
 // before any push of <= 64 (and a line round hands over at most the items it took), F < 128 before
 // a stream step pushes <= 128.  Both are checked (PIP_FAULT_QUEUE).  Pairs are staged per wave and
 // flushed with one atomic per flush.
-// One 768-thread block per CU (12 waves, 9 KiB of queues each) leaves 52 KiB of LDS for the coarse
-// EMPTY bitmap: a point whose coarse block is EMPTY costs no gather at all.  The join is bound by the
+// One 1024-thread block per CU (16 waves, 9 KiB of queues each) leaves 16 KiB of LDS for the coarse
+// EMPTY bitmap (one bit per 2 x 2 coarse cells on the bench's index; 768 threads left 52 KiB for one
+// bit per coarse cell, but 16 waves hide more: 11.45 -> 10.88 ms): a point whose coarse block is
+// EMPTY costs no gather at all.  The join is bound by the
 // vector-memory path (TD busy 97%, the L1 stalled on its outstanding misses 83% of the kernel, r3
 // PMC), and the coarse lookups were 70% of its L1 misses; 55% of the bench's points sit in EMPTY
 // coarse cells.
 #ifndef GM_JQ_TPB
-#define GM_JQ_TPB 768
+#define GM_JQ_TPB 1024
 #endif
 constexpr int QTPB = GM_JQ_TPB;
-constexpr int CM_WORDS_MAX = 13248;   // 52,992 B: 160 KiB minus 12 waves x 9,216 B of queues
+constexpr int CM_WORDS_MAX = (163840 - (QTPB / 64) * 9216 - 256) / 4;   // 160 KiB minus the waves' queues (9,216 B each): 13,248 words at 768 threads
 #ifndef GM_JQ_FBATCH
 #define GM_JQ_FBATCH 128
 #endif
