@@ -905,7 +905,7 @@ __global__ __launch_bounds__(256) void k_pair_move(PairOut o, const PairPlan* __
 #define GM_JQ_TPB 1024
 #endif
 constexpr int QTPB = GM_JQ_TPB;
-constexpr int CM_WORDS_MAX = (163840 - (QTPB / 64) * 9216 - 256) / 4;   // 160 KiB minus the waves' queues (9,216 B each): 13,248 words at 768 threads
+constexpr int CM_WORDS_MAX = (163840 - (QTPB / 64) * 9216 - 256) / 4;   // 160 KiB minus the waves' queues (9,216 B each): 4,032 words at 1024 threads
 #ifndef GM_JQ_FBATCH
 #define GM_JQ_FBATCH 128
 #endif
@@ -1824,6 +1824,12 @@ __global__ __launch_bounds__(RTPB) void k_pip_relate(const int32_t* __restrict__
   __shared__ int64_t s_row[NW][RQCAP];
   __shared__ uint32_t s_e[NW][RQCAP];
   __shared__ int32_t s_p[NW][RQCAP];
+  // the join's coarse EMPTY bitmap (d.cm, staged in LDS like k_pip_join_q): rows in EMPTY coarse
+  // blocks skip the coarse gather
+  __shared__ uint32_t s_cm[CM_WORDS_MAX];
+  const int64_t cm_words = d.cm_words <= CM_WORDS_MAX ? d.cm_words : 0;
+  for (int64_t i = threadIdx.x; i < cm_words; i += RTPB) s_cm[i] = d.cm[i];
+  __syncthreads();
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   double* qx = s_x[wave]; double* qy = s_y[wave];
   int64_t* qr = s_row[wave]; uint32_t* qe = s_e[wave]; int32_t* qp = s_p[wave];
@@ -1849,7 +1855,13 @@ __global__ __launch_bounds__(RTPB) void k_pip_relate(const int32_t* __restrict__
         if (p[u] >= 0 && p[u] < n_polys && x[u] >= d.gx0 && x[u] <= d.gx1 && y[u] >= d.gy0 && y[u] <= d.gy1) {
           cx[u] = cell_of(x[u], d.gx0, d.inv_cw, d.gx);
           cy[u] = cell_of(y[u], d.gy0, d.inv_ch, d.gy);
-          w[u] = coarse_mask(d.coarse_sc[(int64_t)(cy[u] >> CF_LOG) * d.gxc + (cx[u] >> CF_LOG)], cx[u], cy[u], d.coarse_fmt);
+          bool empty = false;
+          if (cm_words) {
+            const int b = ((cy[u] >> CF_LOG) >> d.cm_shift) * d.cm_w + ((cx[u] >> CF_LOG) >> d.cm_shift);
+            empty = (s_cm[b >> 5] >> (b & 31)) & 1u;
+          }
+          if (!empty)
+            w[u] = coarse_mask(d.coarse_sc[(int64_t)(cy[u] >> CF_LOG) * d.gxc + (cx[u] >> CF_LOG)], cx[u], cy[u], d.coarse_fmt);
         }
       }
 #pragma unroll

@@ -17,6 +17,7 @@ if [ -n "$PMC_GROUPS" ]; then IFS=";" read -ra groups <<< "$PMC_GROUPS"; fi
 cmd="python3 bench.py"
 if [ "$leg" = join ]; then args="--only join --no-cpu --no-gather --steps 1 --warmup 0 --join-steps 1"
 elif [ "$leg" = ranges ]; then cmd="python3 tools/ranges_probe.py"; args="100000"
+elif [ "$leg" = hist ]; then cmd="python3 tools/hist_probe.py"; args=""
 else args="--only z3,table --no-cpu --steps 1 --warmup 0"; fi
 i=0
 for g in "${groups[@]}"; do
@@ -27,6 +28,8 @@ done
 if [ "$leg" = join ]; then
   python3 tools/pmc_summary.py $out "k_pip_join_q<true" > $out/join.txt
   python3 tools/pmc_summary.py $out "k_pip_relate" > $out/relate.txt
+elif [ "$leg" = hist ]; then
+  python3 tools/pmc_summary.py $out "k_z3_hist_lds<1, false, true, false>" > $out/hist.txt
 elif [ "$leg" = ranges ]; then
   python3 tools/pmc_summary.py $out "k_xzranges<3>" > $out/xz3.txt
   python3 tools/pmc_summary.py $out "k_xzranges<2>" > $out/xz2.txt
