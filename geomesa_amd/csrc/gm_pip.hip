@@ -905,13 +905,16 @@ __global__ __launch_bounds__(256) void k_pair_move(PairOut o, const PairPlan* __
 #define GM_JQ_TPB 1024
 #endif
 constexpr int QTPB = GM_JQ_TPB;
-constexpr int CM_WORDS_MAX = (163840 - (QTPB / 64) * 9216 - 256) / 4;   // 160 KiB minus the waves' queues (9,216 B each): 4,032 words at 1024 threads
 #ifndef GM_JQ_FBATCH
 #define GM_JQ_FBATCH 128
 #endif
 constexpr int FBATCH = GM_JQ_FBATCH;   // fine words per round (64: 1 per lane, 128: 2 per lane)
 constexpr int FCAP = FBATCH + 128;     // fine queue (< FBATCH + one step's 128)
 constexpr int ICAP = 128;           // item queue (two ends)
+// per wave: the fine queue (x, y, row; plus each point's fine word when a round resolves two halves)
+// and the item queue (x, y, row, reference)
+constexpr int JQ_WAVE_LDS = FCAP * (FBATCH > 64 ? 24 : 20) + ICAP * 24;
+constexpr int CM_WORDS_MAX = (163840 - (QTPB / 64) * JQ_WAVE_LDS - 256) / 4;   // the rest of the 160 KiB: 4,032 words at 1024 threads
 
 template <bool WRITE, int SRC, bool VEC>
 __global__ __launch_bounds__(QTPB) void k_pip_join_q(const double* __restrict__ px, const double* __restrict__ py,
@@ -919,7 +922,7 @@ __global__ __launch_bounds__(QTPB) void k_pip_join_q(const double* __restrict__ 
                                                      int64_t desc_base, ArrowPts ap) {
   constexpr int NW = QTPB / 64;
   __shared__ double s_fx[NW][FCAP], s_fy[NW][FCAP];
-  __shared__ uint32_t s_fid[NW][FCAP], s_fw[NW][FCAP];
+  __shared__ uint32_t s_fid[NW][FCAP], s_fw[NW][FBATCH > 64 ? FCAP : 1];   // one half per round: its words stay in registers
   __shared__ double s_ix[NW][ICAP], s_iy[NW][ICAP];
   __shared__ uint32_t s_iid[NW][ICAP], s_iref[NW][ICAP];
   __shared__ uint32_t s_cm[CM_WORDS_MAX];
@@ -999,6 +1002,7 @@ __global__ __launch_bounds__(QTPB) void k_pip_join_q(const double* __restrict__ 
   bool list_on = false;              // wave-uniform: some lane walks a list
   int l_slot = 0, l_lo = 0, l_n = 0, l_j = 0;
   uint32_t* fw = s_fw[wv];
+  uint32_t pend_w = CELL_EMPTY << 30;   // FBATCH == 64: the pending window's word of this lane
 
   for (;;) {
     // every other stage idle: the item stage drains what is left (a line round may hand blobs over)
@@ -1062,7 +1066,7 @@ __global__ __launch_bounds__(QTPB) void k_pip_join_q(const double* __restrict__ 
       ++hn;
       uint32_t w = CELL_EMPTY << 30, id = 0;
       double x = 0.0, y = 0.0;
-      if (act) { w = fw[slot]; x = fx[slot]; y = fy[slot]; id = fid[slot]; }
+      if (act) { w = FBATCH > 64 ? fw[slot] : pend_w; x = fx[slot]; y = fy[slot]; id = fid[slot]; }
       const uint32_t kind = w >> 30, ref = w & 0x3fffffffu;
       pair_push(kind == CELL_INTERIOR, id, (int)ref);
       const bool item = kind == CELL_BOUNDARY;
@@ -1091,8 +1095,12 @@ __global__ __launch_bounds__(QTPB) void k_pip_join_q(const double* __restrict__ 
       uint32_t wa = CELL_EMPTY << 30, wb = CELL_EMPTY << 30;
       if (act_a) wa = d.cell_sc[(int64_t)cell_of(fy[a], d.gy0, d.inv_ch, d.gy) * d.gx + cell_of(fx[a], d.gx0, d.inv_cw, d.gx)];
       if (act_b) wb = d.cell_sc[(int64_t)cell_of(fy[b], d.gy0, d.inv_ch, d.gy) * d.gx + cell_of(fx[b], d.gx0, d.inv_cw, d.gx)];
-      if (act_a) fw[a] = wa;
-      if (act_b) fw[b] = wb;
+      if (FBATCH > 64) {
+        if (act_a) fw[a] = wa;
+        if (act_b) fw[b] = wb;
+      } else {
+        pend_w = wa;
+      }
       wave_lds_sync();
       pb = fn - cnt;
       pc = cnt;
