@@ -86,6 +86,10 @@ struct PipDev {
   const uint32_t* cm;
   int32_t cm_shift, cm_w;
   int64_t cm_words;
+  // the same bitmap at the row predicate's smaller LDS budget (RELATE_CM_WORDS)
+  const uint32_t* cm2;
+  int32_t cm2_shift, cm2_w;
+  int64_t cm2_words;
 };
 
 enum : uint32_t { PIP_FAULT_LINE = 1, PIP_FAULT_COMPACT = 2, PIP_FAULT_BLOB = 4, PIP_FAULT_LIST = 8, PIP_FAULT_QUEUE = 16 };
@@ -906,7 +910,7 @@ __global__ __launch_bounds__(256) void k_pair_move(PairOut o, const PairPlan* __
 #endif
 constexpr int QTPB = GM_JQ_TPB;
 #ifndef GM_JQ_FBATCH
-#define GM_JQ_FBATCH 128
+#define GM_JQ_FBATCH 64
 #endif
 constexpr int FBATCH = GM_JQ_FBATCH;   // fine words per round (64: 1 per lane, 128: 2 per lane)
 constexpr int FCAP = FBATCH + 128;     // fine queue (< FBATCH + one step's 128)
@@ -1822,6 +1826,7 @@ __global__ __launch_bounds__(RTPB) void k_list_poly(PipDev d, int64_t n, int32_t
 #endif
 constexpr int RILP = GM_RILP;
 constexpr int RQCAP = 64 * (RILP + 1);
+constexpr int RELATE_CM_WORDS = 4032;   // the row predicate's bitmap budget (16 KiB)
 
 __global__ __launch_bounds__(RTPB) void k_pip_relate(const int32_t* __restrict__ poly, const double* __restrict__ px,
                                                      const double* __restrict__ py, int64_t n, int32_t n_polys,
@@ -1832,11 +1837,11 @@ __global__ __launch_bounds__(RTPB) void k_pip_relate(const int32_t* __restrict__
   __shared__ int64_t s_row[NW][RQCAP];
   __shared__ uint32_t s_e[NW][RQCAP];
   __shared__ int32_t s_p[NW][RQCAP];
-  // the join's coarse EMPTY bitmap (d.cm, staged in LDS like k_pip_join_q): rows in EMPTY coarse
-  // blocks skip the coarse gather
-  __shared__ uint32_t s_cm[CM_WORDS_MAX];
-  const int64_t cm_words = d.cm_words <= CM_WORDS_MAX ? d.cm_words : 0;
-  for (int64_t i = threadIdx.x; i < cm_words; i += RTPB) s_cm[i] = d.cm[i];
+  // the coarse EMPTY bitmap at this kernel's budget (d.cm2, 16 KiB: three 256-thread blocks per CU),
+  // staged in LDS like k_pip_join_q's: rows in EMPTY coarse blocks skip the coarse gather
+  __shared__ uint32_t s_cm[RELATE_CM_WORDS];
+  const int64_t cm_words = d.cm2_words <= RELATE_CM_WORDS ? d.cm2_words : 0;
+  for (int64_t i = threadIdx.x; i < cm_words; i += RTPB) s_cm[i] = d.cm2[i];
   __syncthreads();
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   double* qx = s_x[wave]; double* qy = s_y[wave];
@@ -1865,7 +1870,7 @@ __global__ __launch_bounds__(RTPB) void k_pip_relate(const int32_t* __restrict__
           cy[u] = cell_of(y[u], d.gy0, d.inv_ch, d.gy);
           bool empty = false;
           if (cm_words) {
-            const int b = ((cy[u] >> CF_LOG) >> d.cm_shift) * d.cm_w + ((cx[u] >> CF_LOG) >> d.cm_shift);
+            const int b = ((cy[u] >> CF_LOG) >> d.cm2_shift) * d.cm2_w + ((cx[u] >> CF_LOG) >> d.cm2_shift);
             empty = (s_cm[b >> 5] >> (b & 31)) & 1u;
           }
           if (!empty)
@@ -2681,8 +2686,10 @@ int make_shortcut(gm_pip_index* ix) {
   ix->dev.line_ent = nullptr;
   ix->n_lines = 0;
   ix->dev.fault = nullptr;   // set per call (the call's scratch word)
-  ix->dev.cm = nullptr;      // the coarse EMPTY bitmap, built after coarse_sc
+  ix->dev.cm = nullptr;      // the coarse EMPTY bitmaps, built after coarse_sc
   ix->dev.cm_words = 0;
+  ix->dev.cm2 = nullptr;
+  ix->dev.cm2_words = 0;
   ix->dev.n_line = 0;
   ix->dev.n_compact_lines = ix->arr_bytes[5] / 128;
   ix->dev.n_blob16 = ix->arr_bytes[7] / 16;
@@ -2728,20 +2735,24 @@ int make_shortcut(gm_pip_index* ix) {
     hipLaunchKernelGGL(k_build_coarse_sc, dim3((unsigned)std::min<int64_t>(65536, ((int64_t)gxc * gyc + 255) / 256)), dim3(256),
                        0, s, (const uint32_t*)p, ix->dev.gx, ix->dev.gy, gxc, gyc, ix->dev.coarse_fmt,
                        (uint32_t*)ix->dev.coarse_sc);
-    // the coarse EMPTY bitmap: the finest block size whose bitmap fits the join's LDS budget
-    int sh = 0;
-    while ((int64_t)((gxc + (1 << sh) - 1) >> sh) * ((gyc + (1 << sh) - 1) >> sh) > (int64_t)CM_WORDS_MAX * 32) ++sh;
-    const int cw = (gxc + (1 << sh) - 1) >> sh, ch = (gyc + (1 << sh) - 1) >> sh;
-    const int64_t nw = ((int64_t)cw * ch + 31) / 32;
-    void* cm = nullptr;
-    if (hipMalloc(&cm, (size_t)nw * 4) != hipSuccess) { cleanup(); return hip_fail(hipErrorOutOfMemory, "gm_pip_index bitmap"); }
-    ix->allocs.push_back(cm);
-    hipLaunchKernelGGL(k_build_cmask, dim3((unsigned)std::min<int64_t>(4096, (nw + 255) / 256)), dim3(256), 0, s,
-                       (const uint32_t*)ix->dev.coarse_sc, gxc, gyc, sh, cw, ch, nw, (uint32_t*)cm);
-    ix->dev.cm = (const uint32_t*)cm;
-    ix->dev.cm_shift = sh;
-    ix->dev.cm_w = cw;
-    ix->dev.cm_words = nw;
+    // the coarse EMPTY bitmaps: the finest block size whose bitmap fits each kernel's LDS budget
+    // (the join's, the row predicate's)
+    auto bitmap = [&](int64_t budget_words, const uint32_t** out, int32_t* shift, int32_t* w, int64_t* words) -> int {
+      int sh = 0;
+      while ((int64_t)((gxc + (1 << sh) - 1) >> sh) * ((gyc + (1 << sh) - 1) >> sh) > budget_words * 32) ++sh;
+      const int cw = (gxc + (1 << sh) - 1) >> sh, ch = (gyc + (1 << sh) - 1) >> sh;
+      const int64_t nw = ((int64_t)cw * ch + 31) / 32;
+      void* cm = nullptr;
+      if (hipMalloc(&cm, (size_t)nw * 4) != hipSuccess) return hip_fail(hipErrorOutOfMemory, "gm_pip_index bitmap");
+      ix->allocs.push_back(cm);
+      hipLaunchKernelGGL(k_build_cmask, dim3((unsigned)std::min<int64_t>(4096, (nw + 255) / 256)), dim3(256), 0, s,
+                         (const uint32_t*)ix->dev.coarse_sc, gxc, gyc, sh, cw, ch, nw, (uint32_t*)cm);
+      *out = (const uint32_t*)cm; *shift = sh; *w = cw; *words = nw;
+      return GM_OK;
+    };
+    rc = bitmap(CM_WORDS_MAX, &ix->dev.cm, &ix->dev.cm_shift, &ix->dev.cm_w, &ix->dev.cm_words);
+    if (!rc) rc = bitmap(RELATE_CM_WORDS, &ix->dev.cm2, &ix->dev.cm2_shift, &ix->dev.cm2_w, &ix->dev.cm2_words);
+    if (rc) { cleanup(); return rc; }
   }
   if (!rc && hipStreamSynchronize(s) != hipSuccess) rc = hip_fail(hipErrorLaunchFailure, "k_build_shortcut");
   cleanup();
