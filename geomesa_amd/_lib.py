@@ -130,6 +130,7 @@ SIGNATURES = {
     "gm_pip_index_create_ex": (cint, [vp, vp, cint, vp]),
     "gm_pip_index_destroy": (cint, [vp]),
     "gm_pip_index_stats": (cint, [vp, vp]),
+    "gm_pip_index_core": (cint, [vp, vp, vp, vp]),
     "gm_pip_join_census": (cint, [vp, vp, vp, vp, i64, vp]),
     "gm_pip_index_export": (cint, [vp, vp]),
     "gm_pip_index_copy_array": (cint, [vp, vp, cint, vp]),

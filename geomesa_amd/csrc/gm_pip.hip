@@ -90,6 +90,11 @@ struct PipDev {
   const uint32_t* cm2;
   int32_t cm2_shift, cm2_w;
   int64_t cm2_words;
+  // per polygon p, a rectangle of fine cells (x0, y0, x1, y1 inclusive; x0 > x1 = none) whose words
+  // are all INTERIOR(p) (make_shortcut, k_core_*): the row predicate answers a row of polygon p inside
+  // it from LDS, without the coarse and fine gathers.  n_core = 0: no table
+  const ushort4* core;
+  int32_t n_core;
 };
 
 enum : uint32_t { PIP_FAULT_LINE = 1, PIP_FAULT_COMPACT = 2, PIP_FAULT_BLOB = 4, PIP_FAULT_LIST = 8, PIP_FAULT_QUEUE = 16 };
@@ -1787,7 +1792,7 @@ __global__ __launch_bounds__(256) void k_pip_census(const double* __restrict__ p
 // The lookup is the join's: cell word chain, then only the entry of polygon poly[i] -- INTERIOR
 // decides at once, a blob is walked; no entry means the cell misses the polygon (exterior).
 #ifndef GM_RELATE_TPB
-#define GM_RELATE_TPB 256
+#define GM_RELATE_TPB 1024
 #endif
 constexpr int RTPB = GM_RELATE_TPB;   // row-predicate threads per block
 constexpr uint8_t LOC_NULL = 0xff;
@@ -1827,21 +1832,39 @@ __global__ __launch_bounds__(RTPB) void k_list_poly(PipDev d, int64_t n, int32_t
 constexpr int RILP = GM_RILP;
 constexpr int RQCAP = 64 * (RILP + 1);
 constexpr int RELATE_CM_WORDS = 4032;   // the row predicate's bitmap budget (16 KiB)
+#ifndef GM_RELATE_CORE_MAX
+#define GM_RELATE_CORE_MAX 4096
+#endif
+constexpr int RELATE_CORE_MAX = GM_RELATE_CORE_MAX;   // polygons whose core rectangle fits LDS (8 B each)
+#ifndef GM_RELATE_SPEC
+#define GM_RELATE_SPEC 0
+#endif
+// rows that the LDS tests leave load their fine word beside the coarse word (one round trip instead
+// of two for rows in mixed coarse cells, a wasted fine load for the others)
+constexpr bool RELATE_SPEC = GM_RELATE_SPEC;
 
+// VEC: a lane's RILP = 2 rows are adjacent (one 16-B load per coordinate column, one 8-B id load, one
+// 2-B location store when both resolve at once); the host picks it when the columns are aligned
+template <bool VEC>
 __global__ __launch_bounds__(RTPB) void k_pip_relate(const int32_t* __restrict__ poly, const double* __restrict__ px,
                                                      const double* __restrict__ py, int64_t n, int32_t n_polys,
                                                      PipDev d, const int32_t* __restrict__ list_poly,
                                                      uint8_t* __restrict__ loc) {
+  static_assert(!VEC || RILP == 2, "adjacent rows per lane are written for RILP = 2");
   constexpr int NW = RTPB / 64;
   __shared__ double s_x[NW][RQCAP], s_y[NW][RQCAP];
   __shared__ int64_t s_row[NW][RQCAP];
   __shared__ uint32_t s_e[NW][RQCAP];
   __shared__ int32_t s_p[NW][RQCAP];
-  // the coarse EMPTY bitmap at this kernel's budget (d.cm2, 16 KiB: three 256-thread blocks per CU),
-  // staged in LDS like k_pip_join_q's: rows in EMPTY coarse blocks skip the coarse gather
+  // the coarse EMPTY bitmap at this kernel's budget (d.cm2, 16 KiB), staged in LDS like
+  // k_pip_join_q's: rows in EMPTY coarse blocks skip the coarse gather
   __shared__ uint32_t s_cm[RELATE_CM_WORDS];
+  // each polygon's core rectangle (d.core): a row inside its own polygon's core is INTERIOR at once
+  __shared__ ushort4 s_core[RELATE_CORE_MAX > 0 ? RELATE_CORE_MAX : 1];
   const int64_t cm_words = d.cm2_words <= RELATE_CM_WORDS ? d.cm2_words : 0;
   for (int64_t i = threadIdx.x; i < cm_words; i += RTPB) s_cm[i] = d.cm2[i];
+  const int n_core = d.core && d.n_core == n_polys && d.n_core <= RELATE_CORE_MAX ? d.n_core : 0;
+  for (int i = threadIdx.x; i < n_core; i += RTPB) s_core[i] = d.core[i];
   __syncthreads();
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   double* qx = s_x[wave]; double* qy = s_y[wave];
@@ -1854,13 +1877,22 @@ __global__ __launch_bounds__(RTPB) void k_pip_relate(const int32_t* __restrict__
       int64_t row[RILP];
       int p[RILP];
       double x[RILP], y[RILP];
-      uint32_t w[RILP];
+      uint32_t w[RILP], fw[RILP];
       int cx[RILP], cy[RILP];
 #pragma unroll
       for (int u = 0; u < RILP; ++u) {
-        row[u] = w0 + u * 64 + lane;
+        row[u] = VEC ? w0 + RILP * lane + u : w0 + u * 64 + lane;
         p[u] = -1; x[u] = y[u] = 0.0;
-        if (row[u] < n) { p[u] = poly[row[u]]; x[u] = px[row[u]]; y[u] = py[row[u]]; }
+      }
+      if (VEC && row[1] < n) {
+        const uint64_t pp = __builtin_nontemporal_load((const uint64_t*)(poly + row[0]));
+        const dv2 a = __builtin_nontemporal_load((const dv2*)(px + row[0]));
+        const dv2 b = __builtin_nontemporal_load((const dv2*)(py + row[0]));
+        p[0] = (int)(uint32_t)pp; p[1] = (int)(uint32_t)(pp >> 32); x[0] = a.x; x[1] = a.y; y[0] = b.x; y[1] = b.y;
+      } else {
+#pragma unroll
+        for (int u = 0; u < RILP; ++u)
+          if (row[u] < n) { p[u] = poly[row[u]]; x[u] = px[row[u]]; y[u] = py[row[u]]; }
       }
 #pragma unroll
       for (int u = 0; u < RILP; ++u) {
@@ -1868,18 +1900,29 @@ __global__ __launch_bounds__(RTPB) void k_pip_relate(const int32_t* __restrict__
         if (p[u] >= 0 && p[u] < n_polys && x[u] >= d.gx0 && x[u] <= d.gx1 && y[u] >= d.gy0 && y[u] <= d.gy1) {
           cx[u] = cell_of(x[u], d.gx0, d.inv_cw, d.gx);
           cy[u] = cell_of(y[u], d.gy0, d.inv_ch, d.gy);
-          bool empty = false;
-          if (cm_words) {
+          bool empty = false, core = false;
+          if (n_core) {
+            const ushort4 b = s_core[p[u]];
+            core = cx[u] >= b.x && cx[u] <= b.z && cy[u] >= b.y && cy[u] <= b.w;
+          }
+          if (cm_words && !core) {
             const int b = ((cy[u] >> CF_LOG) >> d.cm2_shift) * d.cm2_w + ((cx[u] >> CF_LOG) >> d.cm2_shift);
             empty = (s_cm[b >> 5] >> (b & 31)) & 1u;
           }
-          if (!empty)
-            w[u] = coarse_mask(d.coarse_sc[(int64_t)(cy[u] >> CF_LOG) * d.gxc + (cx[u] >> CF_LOG)], cx[u], cy[u], d.coarse_fmt);
+          if (core)
+            w[u] = (CELL_INTERIOR << 30) | (uint32_t)p[u];   // what the coarse word of a core cell says
+          else if (!empty) {
+            const uint32_t craw = d.coarse_sc[(int64_t)(cy[u] >> CF_LOG) * d.gxc + (cx[u] >> CF_LOG)];
+            if (RELATE_SPEC) fw[u] = d.cell_sc[(int64_t)cy[u] * d.gx + cx[u]];   // in flight beside the coarse word
+            w[u] = coarse_mask(craw, cx[u], cy[u], d.coarse_fmt);
+          }
         }
       }
 #pragma unroll
       for (int u = 0; u < RILP; ++u)
-        if ((w[u] >> 30) == CELL_LIST) w[u] = d.cell_sc[(int64_t)cy[u] * d.gx + cx[u]];   // boundary shortcuts applied
+        if ((w[u] >> 30) == CELL_LIST) w[u] = RELATE_SPEC ? fw[u] : d.cell_sc[(int64_t)cy[u] * d.gx + cx[u]];   // boundary shortcuts applied
+      uint8_t rv[RILP];
+      bool dir[RILP];
 #pragma unroll
       for (int u = 0; u < RILP; ++u) {
         uint8_t r = LOC_EXTERIOR;
@@ -1894,18 +1937,34 @@ __global__ __launch_bounds__(RTPB) void k_pip_relate(const int32_t* __restrict__
           queue = true;   // the blob's polygon is checked when it is walked
         } else if (kind == CELL_LIST) {
           int l0 = 4 * (int)((e & 0x3fffffffu) >> 4), ni = (int)(e & 15u);
+          bool found = false;
           if ((int64_t)l0 + 4 > d.n_list) { pip_fault(d, PIP_FAULT_LIST); ni = 0; }
-          else if (ni == LIST_LONG) { ni = (int)d.list_ent[l0]; l0 += 1; }
+          else if (ni <= 4) {
+            // a short list is one 16-B group (lists start at multiples of 4 slots): its polygon ids
+            // and entries in two independent loads instead of a serial search
+            const int4 lp = *(const int4*)(list_poly + l0);
+            const uint4 le = *(const uint4*)(d.list_ent + l0);
+            const int pv = p[u];
+            found = true;
+            if (ni > 0 && lp.x == pv) e = le.x;
+            else if (ni > 1 && lp.y == pv) e = le.y;
+            else if (ni > 2 && lp.z == pv) e = le.z;
+            else if (ni > 3 && lp.w == pv) e = le.w;
+            else found = false;
+            ni = 0;
+          } else if (ni == LIST_LONG) { ni = (int)d.list_ent[l0]; l0 += 1; }
           if (ni < 0 || (int64_t)l0 + ni > d.n_list) { pip_fault(d, PIP_FAULT_LIST); ni = 0; }
           int j = 0;
           while (j < ni && list_poly[l0 + j] != p[u]) ++j;
-          if (j < ni) {
-            e = d.list_ent[l0 + j];
+          if (j < ni) { e = d.list_ent[l0 + j]; found = true; }
+          if (found) {
             if ((e >> 30) == CELL_INTERIOR) r = LOC_INTERIOR;
             else queue = true;
           }
         }
-        if (row[u] < n && !queue) loc[row[u]] = r;
+        rv[u] = r;
+        dir[u] = row[u] < n && !queue;
+        if (!VEC && dir[u]) loc[row[u]] = r;
         // line-entry items and blob items on separate ends, so an evaluation round runs one kind
         const bool ln = (e & (BLOB_COMPACT | SC_LINE)) == (BLOB_COMPACT | SC_LINE) && d.line_ent;
         const bool qv = queue && row[u] < n;
@@ -1916,6 +1975,13 @@ __global__ __launch_bounds__(RTPB) void k_pip_relate(const int32_t* __restrict__
         }
         qn += __popcll(ml);
         qg += __popcll(mb);
+      }
+      if (VEC) {
+        if (dir[0] && dir[1]) *(uint16_t*)(loc + row[0]) = (uint16_t)(rv[0] | (rv[1] << 8));
+        else {
+          if (dir[0]) loc[row[0]] = rv[0];
+          if (dir[1]) loc[row[1]] = rv[1];
+        }
       }
     }
     // walk min(qn, 64) queued blobs when the queue holds a full wave, and drain it at the end
@@ -2588,6 +2654,99 @@ __global__ __launch_bounds__(256) void k_build_cmask(const uint32_t* __restrict_
   }
 }
 
+// The row predicate's core rectangles (PipDev::core): for every polygon, a large rectangle of fine
+// cells whose words are all INTERIOR(p).  Any such rectangle is exact (a row in it gets the answer its
+// cell word gives).  The search runs on the coarse grid -- the largest rectangle of INTERIOR(p) coarse
+// cells with its top-left corner on any cell, extents capped at CORE_CAP coarse cells so the build
+// stays linear in the coarse grid -- and k_core_write widens it over the fine cells.
+constexpr int CORE_CAP = 256;
+
+// run[i] = how many coarse cells from i rightwards (<= CORE_CAP) carry i's INTERIOR word; 0 otherwise
+__global__ __launch_bounds__(256) void k_core_run(const uint32_t* __restrict__ coarse_sc, int gxc, int64_t n,
+                                                  int32_t n_polys, int32_t* __restrict__ run) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t w = coarse_sc[i];
+    int r = 0;
+    if ((w >> 30) == CELL_INTERIOR && (int64_t)(w & 0x3fffffffu) < n_polys) {
+      const int xc = (int)(i % gxc);
+      r = 1;
+      while (r < CORE_CAP && xc + r < gxc && coarse_sc[i + r] == w) ++r;
+    }
+    run[i] = r;
+  }
+}
+
+// the largest rectangle with its top-left corner on coarse cell i (first maximum scanning down)
+__device__ __forceinline__ int core_rect(const uint32_t* coarse_sc, const int32_t* run, int gxc, int gyc, int64_t i,
+                                         int& bw, int& bh) {
+  const uint32_t w = coarse_sc[i];
+  const int yc = (int)(i / gxc);
+  int best = 0, wmin = run[i];
+  bw = bh = 0;
+  for (int h = 1; h <= CORE_CAP && yc + h - 1 < gyc && wmin > 0; ++h) {
+    const int64_t j = i + (int64_t)(h - 1) * gxc;
+    wmin = coarse_sc[j] == w ? min(wmin, (int)run[j]) : 0;
+    if (wmin * h > best) { best = wmin * h; bw = wmin; bh = h; }
+  }
+  return best;
+}
+
+// best[p] = max over p's cells of (area << 40 | cell): deterministic (ties go to the larger cell index)
+__global__ __launch_bounds__(256) void k_core_best(const uint32_t* __restrict__ coarse_sc, const int32_t* __restrict__ run,
+                                                   int gxc, int gyc, unsigned long long* __restrict__ best) {
+  const int64_t n = (int64_t)gxc * gyc;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    if (run[i] == 0) continue;
+    int bw, bh;
+    const int a = core_rect(coarse_sc, run, gxc, gyc, i, bw, bh);
+    if (a > 0) atomicMax(&best[coarse_sc[i] & 0x3fffffffu], ((unsigned long long)a << 40) | (unsigned long long)i);
+  }
+}
+
+// core[p] in fine cells: the coarse rectangle widened cell by cell (at most one coarse cell per side)
+// while the new column / row of fine cells still carries INTERIOR(p) -- the fine cells of the mixed
+// coarse ring around it that are interior too
+__global__ __launch_bounds__(256) void k_core_write(const uint32_t* __restrict__ coarse_sc, const uint32_t* __restrict__ cell_sc,
+                                                    const int32_t* __restrict__ run, int gx, int gy, int gxc, int gyc,
+                                                    const unsigned long long* __restrict__ best, int32_t n_polys,
+                                                    ushort4* __restrict__ core) {
+  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < n_polys; p += gridDim.x * blockDim.x) {
+    const unsigned long long v = best[p];
+    ushort4 r = make_ushort4(1, 1, 0, 0);   // none
+    if (v) {
+      const int64_t i = (int64_t)(v & ((1ull << 40) - 1));
+      int bw, bh;
+      core_rect(coarse_sc, run, gxc, gyc, i, bw, bh);
+      const int xc = (int)(i % gxc), yc = (int)(i / gxc);
+      const uint32_t w = coarse_sc[i];
+      int X0 = xc << CF_LOG, Y0 = yc << CF_LOG;
+      int X1 = min(gx, (xc + bw) << CF_LOG) - 1, Y1 = min(gy, (yc + bh) << CF_LOG) - 1;
+      auto col_ok = [&](int X) {
+        if (X < 0 || X >= gx) return false;
+        for (int Y = Y0; Y <= Y1; ++Y)
+          if (cell_sc[(int64_t)Y * gx + X] != w) return false;
+        return true;
+      };
+      auto row_ok = [&](int Y) {
+        if (Y < 0 || Y >= gy) return false;
+        for (int X = X0; X <= X1; ++X)
+          if (cell_sc[(int64_t)Y * gx + X] != w) return false;
+        return true;
+      };
+      for (int k = 0; k < (1 << CF_LOG); ++k) {
+        bool grew = false;
+        if (col_ok(X0 - 1)) { --X0; grew = true; }
+        if (col_ok(X1 + 1)) { ++X1; grew = true; }
+        if (row_ok(Y0 - 1)) { --Y0; grew = true; }
+        if (row_ok(Y1 + 1)) { ++Y1; grew = true; }
+        if (!grew) break;
+      }
+      r = make_ushort4((unsigned short)X0, (unsigned short)Y0, (unsigned short)X1, (unsigned short)Y1);
+    }
+    core[p] = r;
+  }
+}
+
 // pass 0 (ent == nullptr): cell_sc = resolved words, is_line[c] = 1 for line cells;
 // pass 1: the line entries at their scanned slots, and the LINE words
 template <bool LINES>
@@ -2690,6 +2849,8 @@ int make_shortcut(gm_pip_index* ix) {
   ix->dev.cm_words = 0;
   ix->dev.cm2 = nullptr;
   ix->dev.cm2_words = 0;
+  ix->dev.core = nullptr;    // the row predicate's core rectangles, built after the bitmaps
+  ix->dev.n_core = 0;
   ix->dev.n_line = 0;
   ix->dev.n_compact_lines = ix->arr_bytes[5] / 128;
   ix->dev.n_blob16 = ix->arr_bytes[7] / 16;
@@ -2752,6 +2913,32 @@ int make_shortcut(gm_pip_index* ix) {
     };
     rc = bitmap(CM_WORDS_MAX, &ix->dev.cm, &ix->dev.cm_shift, &ix->dev.cm_w, &ix->dev.cm_words);
     if (!rc) rc = bitmap(RELATE_CM_WORDS, &ix->dev.cm2, &ix->dev.cm2_shift, &ix->dev.cm2_w, &ix->dev.cm2_words);
+    // the row predicate's core rectangles (fine-cell coordinates in 16 bits; polygon count within its LDS table)
+    if (!rc && ix->n_polys > 0 && ix->n_polys <= RELATE_CORE_MAX && ix->dev.gx < 65535 && ix->dev.gy < 65535 &&
+        !getenv("GM_PIP_NO_CORE")) {
+      const int64_t nc = (int64_t)gxc * gyc;
+      void *run = nullptr, *best = nullptr, *core = nullptr;
+      if (hipMalloc(&run, (size_t)nc * 4) != hipSuccess || hipMalloc(&best, (size_t)ix->n_polys * 8) != hipSuccess ||
+          hipMalloc(&core, (size_t)ix->n_polys * 8) != hipSuccess) {
+        (void)hipFree(run); (void)hipFree(best); (void)hipFree(core);
+        cleanup();
+        return hip_fail(hipErrorOutOfMemory, "gm_pip_index core");
+      }
+      ix->allocs.push_back(core);
+      const unsigned gc = (unsigned)std::min<int64_t>(65536, (nc + 255) / 256);
+      hipLaunchKernelGGL(k_core_run, dim3(gc), dim3(256), 0, s, ix->dev.coarse_sc, gxc, nc, ix->n_polys, (int32_t*)run);
+      GM_HIP(hipMemsetAsync(best, 0, (size_t)ix->n_polys * 8, s));
+      hipLaunchKernelGGL(k_core_best, dim3(gc), dim3(256), 0, s, ix->dev.coarse_sc, (const int32_t*)run, gxc, gyc,
+                         (unsigned long long*)best);
+      hipLaunchKernelGGL(k_core_write, dim3((unsigned)((ix->n_polys + 255) / 256)), dim3(256), 0, s, ix->dev.coarse_sc,
+                         ix->dev.cell_sc, (const int32_t*)run, ix->dev.gx, ix->dev.gy, gxc, gyc,
+                         (const unsigned long long*)best, ix->n_polys, (ushort4*)core);
+      const bool ok = hipStreamSynchronize(s) == hipSuccess;
+      (void)hipFree(run); (void)hipFree(best);
+      if (!ok) { cleanup(); return hip_fail(hipErrorLaunchFailure, "k_core_*"); }
+      ix->dev.core = (const ushort4*)core;
+      ix->dev.n_core = ix->n_polys;
+    }
     if (rc) { cleanup(); return rc; }
   }
   if (!rc && hipStreamSynchronize(s) != hipSuccess) rc = hip_fail(hipErrorLaunchFailure, "k_build_shortcut");
@@ -3715,6 +3902,14 @@ int gm_pip_index_stats(const gm_pip_index* ix, int64_t* stats) {
   return GM_OK;
 }
 
+int gm_pip_index_core(gm_ctx* ctx, const gm_pip_index* ix, uint16_t* rects, int32_t* n_core) {
+  if (!ctx || !ix || !n_core) return GM_E_INVALID;
+  *n_core = ix->dev.core ? ix->dev.n_core : 0;
+  if (!rects || *n_core == 0) return GM_OK;
+  GM_HIP(hipSetDevice(ctx->device));
+  return copy_d2h(ctx, rects, ix->dev.core, (size_t)*n_core * 8);
+}
+
 int gm_pip_join(gm_ctx* ctx, const gm_pip_index* ix, const double* px, const double* py, int64_t n, int64_t id_base,
                 int64_t* pt_ids, int32_t* poly_ids, int64_t cap, int64_t* n_pairs) {
   return gm_pip_join_ex(ctx, ix, px, py, n, id_base, pt_ids, poly_ids, cap, n_pairs, GM_JOIN_AUTO);
@@ -3987,9 +4182,12 @@ int gm_pip_relate(gm_ctx* ctx, const gm_pip_index* ix, const int32_t* poly, cons
   if (n == 0) return GM_OK;
   if (!poly || !px || !py || !loc) return GM_E_INVALID;
   GM_HIP(hipSetDevice(ctx->device));
-  const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(resident_blocks((const void*)k_pip_relate, ctx->device, RTPB, 1),
+  const bool vec = RILP == 2 && ((uintptr_t)px | (uintptr_t)py) % 16 == 0 && (uintptr_t)poly % 8 == 0 &&
+                   (uintptr_t)loc % 2 == 0 && !getenv("GM_PIP_RELATE_SCALAR");
+  auto* kern = vec ? k_pip_relate<RILP == 2> : k_pip_relate<false>;
+  const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(resident_blocks((const void*)kern, ctx->device, RTPB, 1),
                                                                           (n + RTPB * RILP - 1) / (RTPB * RILP)));
-  hipLaunchKernelGGL(k_pip_relate, dim3(grid), dim3(RTPB), 0, ctx->stream, poly, px, py, n, ix->n_polys, ix->dev,
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(RTPB), 0, ctx->stream, poly, px, py, n, ix->n_polys, ix->dev,
                      ix->list_poly, loc);
   GM_CHECK_LAUNCH();
   return GM_OK;

@@ -37,7 +37,15 @@ namespace gm {
 constexpr int RTPB = GM_RTPB;   // threads per query (one workgroup each)
 constexpr int RNW = RTPB / 64;
 constexpr int MAXB = 256;       // zbounds / windows per query
-constexpr int LDS_SORT = 4096;  // ranges sorted in LDS; larger lists sort in global memory
+#ifndef GM_LDS_SORT
+#define GM_LDS_SORT 4096
+#endif
+constexpr int LDS_SORT = GM_LDS_SORT;  // ranges sorted in LDS; larger lists sort in global memory
+#ifdef GM_RANGES_MINW   // tuning: minimum waves per SIMD for the XZ walk (caps its VGPRs)
+#define GM_XZ_BOUNDS __launch_bounds__(RTPB, GM_RANGES_MINW)
+#else
+#define GM_XZ_BOUNDS __launch_bounds__(RTPB)
+#endif
 
 enum : int32_t { QS_OK = 0, QS_OUT_OF_BOUNDS = 1, QS_UNORDERED = 3, QS_CAPACITY = 4, QS_TOO_MANY_BOUNDS = 5 };
 
@@ -585,7 +593,7 @@ __device__ __forceinline__ int64_t xspan(int L, int g) {
 }
 
 template <int D>
-__global__ __launch_bounds__(RTPB) void k_xzranges(XZRangesArgs a) {
+__global__ GM_XZ_BOUNDS void k_xzranges(XZRangesArgs a) {
   __shared__ double s_w[2 * D * MAXB];
   __shared__ int64_t s_tmp[RNW];
   __shared__ int s_err, s_stop;

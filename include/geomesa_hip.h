@@ -256,6 +256,11 @@ int gm_pip_index_destroy(gm_pip_index* index);
 /* index statistics: stats[0..6] = cells, (cell, polygon) entries, boundary entries, ring records,
    ring records that fall back to the slab walk, boundary blob bytes, compact (one-line) blobs */
 int gm_pip_index_stats(const gm_pip_index* index, int64_t* stats);
+/* Diagnostic (no reference counterpart): the row predicate's per-polygon core rectangles, grid
+   cells (x0, y0, x1, y1) inclusive whose cell words are all INTERIOR(p); x0 > x1 = none.  *n_core =
+   polygons with a table (0: none built, e.g. more polygons than gm_pip_relate's LDS table holds);
+   rects (4 * *n_core uint16, host memory) may be null. */
+int gm_pip_index_core(gm_ctx* ctx, const gm_pip_index* index, uint16_t* rects, int32_t* n_core);
 /* Diagnostic (no reference counterpart): how the join's lookup chain resolves the device points
    px / py, stage by stage -- counters[16] = points, outside the grid, coarse EMPTY, coarse INTERIOR,
    points in mixed coarse cells before the sub-block masks, fine lookups, fine EMPTY, fine INTERIOR,

@@ -155,3 +155,49 @@ def test_arrow_join_intersects(gpu, oracle):
     ix = arrow.ArrowPolygonIndex(polyset_to_arrow(ps), kind="multipolygon")
     pt, pl = ix.join(point_array(px, py), predicate="st_intersects")
     assert set(zip(as_np(pt).tolist(), as_np(pl).tolist())) == oracle_pairs(oracle, ps, px, py, "st_intersects")
+
+
+def test_relate_core_rectangles(gpu, oracle):
+    """The row predicate's per-polygon core rectangles (grid cells all INTERIOR(p), answered from LDS):
+    every county has one, points sampled inside it are INTERIOR of that county by the oracle and by
+    gm_pip_relate, and the same points against a neighbouring county match the oracle."""
+    from geomesa_amd.join import PolygonIndex, synthetic_counties
+    ps = synthetic_counties(NX, NY)
+    ix = PolygonIndex(ps)
+    core = ix.core_rects().astype(np.int64)
+    assert core.shape == (ps.n_polys, 4)
+    has = core[:, 0] <= core[:, 2]
+    assert has.mean() > 0.9
+    lay, _ = ix.export_arrays()
+    gx0, gy0, _, _, icw, ich = list(lay.grid)
+    rng = np.random.default_rng(7)
+    poly, px, py = [], [], []
+    for p in np.flatnonzero(has):
+        a, b, c, d = core[p]
+        u = rng.uniform(a + 0.01, c + 1 - 0.01, 16)   # grid-cell coordinates, away from cell edges
+        v = rng.uniform(b + 0.01, d + 1 - 0.01, 16)
+        px += list(gx0 + u / icw); py += list(gy0 + v / ich); poly += [p] * 16
+    poly, px, py = np.array(poly, np.int32), np.array(px), np.array(py)
+    ops = oracle.OraclePolySet(*ps.to_arrays())
+    assert all(ops.locate(int(p), x, y) == 2 for p, x, y in zip(poly, px, py))
+    assert (as_np(ix.relate(poly, px, py)) == 2).all()
+    other = ((poly + 1) % ps.n_polys).astype(np.int32)
+    exp = np.array([ops.locate(int(p), x, y) for p, x, y in zip(other, px, py)], np.uint8)
+    assert np.array_equal(as_np(ix.relate(other, px, py)), exp)
+
+
+def test_relate_unaligned_and_odd_rows(gpu):
+    """The row predicate reads two adjacent rows per lane when the columns are 16-B aligned and row by
+    row otherwise: both layouts, and an odd row count (a last lane with one row), give the same locations."""
+    import torch
+    from geomesa_amd.join import PolygonIndex, synthetic_counties
+    ps = synthetic_counties(NX, NY)
+    poly, px, py = rows(ps, 40_001, seed=31)
+    ix = PolygonIndex(ps)
+    full = as_np(ix.relate(poly, px, py))
+    dx = torch.as_tensor(px, device="cuda")
+    dy = torch.as_tensor(py, device="cuda")
+    shifted = as_np(ix.relate(poly[1:], dx[1:], dy[1:]))   # 8-B offset columns: the row-by-row loads
+    assert np.array_equal(shifted, full[1:])
+    odd = as_np(ix.relate(poly[:12_345], px[:12_345], py[:12_345]))
+    assert np.array_equal(odd, full[:12_345])

@@ -7,8 +7,10 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
 for r in $(seq 1 $rounds); do
   for lib in "$@"; do
     # "legacy" = the product library's round-2 kernel; "legacy:<lib>" = that kernel in variant <lib>
-    unset GM_PIP_JOIN_LEGACY; env_lib=""
+    unset GM_PIP_JOIN_LEGACY GM_PIP_RELATE_SCALAR GM_PIP_NO_CORE; env_lib=""
     case "$lib" in
+      scalar) export GM_PIP_RELATE_SCALAR=1 ;;   # the product library, row-by-row relate loads
+      nocore) export GM_PIP_NO_CORE=1 ;;         # the product library, no core rectangles
       legacy) export GM_PIP_JOIN_LEGACY=1 ;;
       legacy:*) export GM_PIP_JOIN_LEGACY=1; env_lib="GEOMESA_HIP_LIB=$PWD/geomesa_amd/lib/${lib#legacy:}.so" ;;
       *) env_lib="GEOMESA_HIP_LIB=$PWD/geomesa_amd/lib/$lib.so" ;;
@@ -18,4 +20,4 @@ for r in $(seq 1 $rounds); do
     python3 -c "import json; d=json.loads(open('gpurun_out/${tag}_${lib//:/_}_$r.json').read().strip().splitlines()[-1])['pip_join']; print('$lib', $r, round(d['ms_per_step'],3), d['matches'], d.get('row_predicate_ms'))" >> gpurun_out/${tag}_ab.txt
   done
 done
-unset GM_PIP_JOIN_LEGACY
+unset GM_PIP_JOIN_LEGACY GM_PIP_RELATE_SCALAR GM_PIP_NO_CORE
