@@ -46,7 +46,7 @@ def parse():
     p.add_argument("--only", default="", help="comma list: z3,join,extra,table (profiling)")
     p.add_argument("--table-rows", type=int, default=250_000_000,
                    help="rows per GPU of the sorted-table leg (configs[2]: 2B rows over 8 GPUs)")
-    p.add_argument("--join-mode", default="auto", choices=["auto", "direct", "partitioned", "split"])
+    p.add_argument("--join-mode", default="auto", choices=["auto", "direct"])
     p.add_argument("--cells-per-poly", type=int, default=0, help="join grid density (0 = library default)")
     p.add_argument("--join-grid", default="80x40", help="synthetic county grid (experiments)")
     p.add_argument("--no-gather", action="store_true", help="skip the join's result gather to rank 0")
@@ -68,7 +68,9 @@ class Dist:
         backend = os.environ.get("GM_BENCH_BACKEND", "nccl")
         torch.cuda.set_device(self.local)
         self.pg = None
-        if self.world > 1:
+        # a process group whenever torch.distributed.run launched us, even at world 1 (every RCCL branch
+        # then runs with one rank: tests/test_gpu_rccl.py); a plain `python bench.py` has none
+        if self.world > 1 or "TORCHELASTIC_RUN_ID" in os.environ:
             import torch.distributed as dist
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             if backend == "nccl":
@@ -144,8 +146,14 @@ def roofline(bytes_per_launch, ms, traffic=None):
 # ------------------------------------------------------------------------------ CPU baselines
 
 def cpu_threads():
-    """The host's logical CPUs (BASELINE.md:38-43: the CPU baseline runs at 1 thread and at nproc)."""
-    return max(1, os.cpu_count() or 1)
+    """The CPUs this process can actually use: min(affinity set, cgroup CPU quota) -- on the GPU boxes
+    a 16-CPU quota over a 256-CPU machine (BASELINE.md:38-43: the CPU baseline runs at 1 thread and
+    at the usable core count).  The machine's logical count is reported beside it (cpu_info)."""
+    info = cpu_info()
+    n = info["affinity_cpus"] or os.cpu_count() or 1
+    if info["cgroup_cpu_quota"]:
+        n = min(n, max(1, int(info["cgroup_cpu_quota"])))
+    return max(1, n)
 
 
 def cpu_info():
@@ -266,20 +274,42 @@ def cpu_join_baseline(seconds, ps, sample=None):
     return out
 
 
-def cpu_ranges_baseline(kind, q, t, max_ranges, gpu_ms, nq):
+def range_digest(offs, rr):
+    """sha256 over the per-query offsets and every range's (lower, upper, contained)."""
+    import hashlib
+    h = hashlib.sha256(np.ascontiguousarray(offs, np.int64).tobytes())
+    for f in ("lower", "upper", "contained"):
+        h.update(np.ascontiguousarray(rr[f]).tobytes())
+    return h.hexdigest()[:16]
+
+
+def cpu_ranges_baseline(kind, q, t, max_ranges, gpu_ms, nq, gpu_lists=None):
     """The oracle's range decomposition of the same queries on the host's cores (all of them: the
-    nodes-checked total is the work measure of the GPU batch too, SURVEY 8(d) ranges() row)."""
+    nodes-checked total is the work measure of the GPU batch too, SURVEY 8(d) ranges() row).  With the
+    GPU's gathered (offsets, ranges), every query's merged list is compared with the oracle's
+    (lower, upper, contained; XZ2SFC.scala:146-252, XZ3SFC.scala:156-262, ZN.scala:110-242)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     nt = cpu_threads()
     t0 = time.time()
     r, nodes = O.ranges_batch(kind, q, t, max_ranges=max_ranges, nthreads=nt)
     dt = time.time() - t0
-    return {"cpu_baseline": {"value": nq / dt, "unit": "queries/s", "cores": nt, "kind": "port",
-                             "sample": "all %d queries through the C restatement (%d pthreads): %.2f s, %d ranges"
-                                       % (nq, nt, dt, r)},
-            "nodes_checked": nodes, "nodes_checked_per_s": nodes / (gpu_ms * 1e-3),
-            "cpu_ranges": r}
+    out = {"cpu_baseline": {"value": nq / dt, "unit": "queries/s", "cores": nt, "kind": "port",
+                            "sample": "all %d queries through the C restatement (%d pthreads): %.2f s, %d ranges"
+                                      % (nq, nt, dt, r)},
+           "nodes_checked": nodes, "nodes_checked_per_s": nodes / (gpu_ms * 1e-3),
+           "cpu_ranges": r}
+    if gpu_lists is not None:
+        _, _, coffs, crr = O.ranges_batch(kind, q, t, max_ranges=max_ranges, nthreads=nt, lists=True)
+        goffs, grr = gpu_lists
+        grr = grr[:int(goffs[-1])]
+        eq = bool(np.array_equal(coffs, goffs) and
+                  all(np.array_equal(crr[f], grr[f]) for f in ("lower", "upper", "contained")))
+        out["parity"] = {"queries": nq, "ranges": int(coffs[-1]), "ranges_equal": eq,
+                         "oracle_digest": range_digest(coffs, crr), "gpu_digest": range_digest(goffs, grr),
+                         "note": "every query's merged range list (lower, upper, contained) from the GPU batch "
+                                 "against the oracle's, all queries"}
+    return out
 
 
 def pcie_encode(dist, ctx, x, y, t, z_ref, n=64 << 20, chunk=8 << 20, reps=3):
@@ -357,6 +387,7 @@ def ranges_batch(dist, fn, args, n_local, nq, reps=3):
         o, r, _ = R.call_raw(fn, args, n_local, cap, pinned=True)
         g = gather_ranges(dist.pg, o, r[:int(o[-1])])
         res["n"] = int(g[0][-1]) if g is not None else -1
+        res["g"] = g
     step()
     dist.barrier()
     t0 = time.time()
@@ -364,6 +395,9 @@ def ranges_batch(dist, fn, args, n_local, nq, reps=3):
         step()
     dist.barrier()
     dt = dist.max((time.time() - t0) / reps)
+    # the last batch's gathered lists (views of the reused pinned output: copied out, untimed)
+    g = res.pop("g")
+    res["lists"] = (np.array(g[0]), np.array(g[1])) if g is not None else None
     # the same call writing into HBM (the ranges feed a device-side seek such as gm_key_range_scan):
     # no D2H copy of the ranges, no gather; per rank, max over ranks
     import torch
@@ -387,7 +421,7 @@ def ranges_batch(dist, fn, args, n_local, nq, reps=3):
     del dout
     return {"value": nq / dt, "unit": "queries/s", "ms_per_step": dt * 1e3, "ranges": res["n"],
             "device_output": {"ms_per_step": ddt * 1e3, "queries_per_s": nq / ddt, "offsets_equal": same,
-                              "note": "ranges written into HBM (device-side consumer), windows H2D included"}}
+                              "note": "ranges written into HBM (device-side consumer), windows H2D included"}}, res["lists"]
 
 
 def sort_bytes(b, z, n, last):
@@ -460,6 +494,7 @@ def gather_pairs(dist, ptids, plids, k):
 
 
 def bench_table(a, dist, ctx, b, z):
+    import ctypes
     """configs[2]: a Z3 table range-sharded over the GPUs (2B rows over 8 GPUs = 250M per GPU).
     sort_keys: one gm_sort_keys of the rank's rows into table order.  table_ingest: the partitioned
     table built from the rank's rows (local sort, splitters, all-to-all by key range, slice sort).
@@ -509,6 +544,31 @@ def bench_table(a, dist, ctx, b, z):
         res.update(nm=nm, ns=ns, ncl=ncl, n0=int(g[0].numel()) if g is not None else -1)
     ms_scan = timed(dist, query_step, 10, 2)
     matches, scanned = dist.sum(res["nm"]), dist.sum(res["ns"])
+    # the same query as a full scan of every rank's own unsorted rows: bin in the query's bins AND
+    # Z3Filter.inBounds (ranges() covers the query box and the filter passes epochs outside
+    # [minEpoch, maxEpoch], Z3Filter.scala:45-62, Z3IndexKeySpace.scala:196-238), global ids gathered
+    # to rank 0 and compared as sets with the seek-and-filter result (untimed)
+    ids, nm, _, _ = pt.scan(sr, fb)
+    got = gather_rows(dist.pg, [ids])
+    br = np.asarray(ks.bin_ranges(v), np.int16).reshape(-1)
+    fbuf = (ctypes.c_uint8 * len(fb)).from_buffer_copy(fb)
+    fmask = torch.empty((NT + 63) // 64, dtype=torch.int64, device=zs.device)
+    fn = ctypes.c_int64()
+    _lib.check(lib.gm_z3filter_scan(h, fbuf, len(fb), br.ctypes.data, len(br) // 2, P(bs), P(zs), NT, P(fmask),
+                                    None, 0, ctypes.byref(fn)), "gm_z3filter_scan")
+    fids = torch.empty(max(1, fn.value), dtype=torch.int64, device=zs.device)
+    _lib.check(lib.gm_z3filter_scan(h, fbuf, len(fb), br.ctypes.data, len(br) // 2, P(bs), P(zs), NT, P(fmask),
+                                    P(fids), fids.numel(), ctypes.byref(fn)), "gm_z3filter_scan")
+    full = gather_rows(dist.pg, [fids[:fn.value] + dist.rank * NT])
+    qparity = None
+    if dist.rank == 0:
+        a_ids = np.sort(got[0].cpu().numpy()) if got is not None else np.zeros(0, np.int64)
+        b_ids = np.sort(full[0].cpu().numpy()) if full is not None else np.zeros(0, np.int64)
+        qparity = {"seek_ids": int(len(a_ids)), "full_scan_ids": int(len(b_ids)),
+                   "ids_equal": bool(np.array_equal(a_ids, b_ids)),
+                   "note": "ids of the range seek + Z3Filter over the partitioned table against gm_z3filter_scan "
+                           "(bin ranges + Z3Filter.inBounds) over every rank's unsorted rows"}
+    del fmask, fids, got, full
     del holder, pt
     return {
         "sort_keys": {"value": NT * dist.world / (ms_sort * 1e-3), "unit": "rows/s", "ms_per_step": ms_sort,
@@ -527,6 +587,7 @@ def bench_table(a, dist, ctx, b, z):
         "table_query": {"value": 1.0 / (ms_scan * 1e-3), "unit": "queries/s", "ms_per_step": ms_scan,
                         "table_rows": NT * dist.world, "ranges": nr, "ranges_scanned_rank0": res["ncl"],
                         "rows_scanned": int(scanned), "matches": int(matches), "plan_ms": round(plan_ms, 2),
+                        "parity": qparity,
                         "equivalent_scan_rate": NT * dist.world / (ms_scan * 1e-3),
                         "note": "configs[2] query bbox(-10,35,30,60) during 2020-06-01/06-08T12 over the whole "
                                 "partitioned table: each rank clips the ranges to its key slice, seeks + Z3Filter, "
@@ -587,14 +648,22 @@ def bench_config0(a, dist, ctx, x, y, t, n0=10_000_000):
             cpu_r.append(O.z3_ranges(v.spatialBounds, v.temporalBounds[bn], 64,
                                      max(1, 2000 // len(v.temporalBounds))))
         cpu_rng = time.time() - t0
-        gpu_r = [(lo[1], hi[1]) for (_, lo, hi) in res["r"]]
-        cpu_flat = [(r[0], r[1]) for rr in cpu_r for r in rr]
+        # getRanges drops IndexRange.contained (Z3IndexKeySpace.scala:174-194); compare the sfc's own
+        # IndexRanges for the same per-bin queries, contained included
+        tb = v.temporalBounds
+        gpu_ir = ks.sfc.ranges_batch([(v.spatialBounds, tb[bn]) for bn in sorted(tb)], 64, max(1, 2000 // len(tb)))
+        gpu_r = [(int(r.lower), int(r.upper), bool(r.contained)) for rr in gpu_ir for r in rr]
+        cpu_flat = [(int(r[0]), int(r[1]), bool(r[2])) for rr in cpu_r for r in rr]
+        assert len(gpu_r) == len(res["r"])
         out["cpu_baseline"] = {"index_ms": cpu_idx * 1e3, "index_points_per_s": n0 / cpu_idx, "ranges_ms": cpu_rng * 1e3,
                                "cores": 1, "kind": "port", "host": cpu_info(),
                                "sample": "the same %d points and the same query through the C restatement, 1 thread"
                                          % n0}
         out["parity"] = {"keys_equal": bool(np.array_equal(ob, b0.cpu().numpy()) and np.array_equal(oz, z0.cpu().numpy())),
-                         "ranges_equal": gpu_r == cpu_flat}
+                         "ranges_equal": gpu_r == cpu_flat, "ranges": len(cpu_flat),
+                         "contained": sum(r[2] for r in cpu_flat),
+                         "note": "IndexRange (lower, upper, contained) of every bin's getRanges against the oracle "
+                                 "(zorder/sfcurve/package.scala:22-76, ZN.scala:110-242)"}
     del b0, z0
     return out
 
@@ -810,11 +879,27 @@ def main():
         xo = torch.empty(NX, dtype=torch.int64, device=dev)
         rec("xz2_index", lambda: lib.gm_xz2_index(h, P(x), P(y), P(xmax), P(ymax), NX, 12, 0, P(xo), None, None), 40,
             NX, unit="envelopes/s")
+        xstride = max(1, NX // 1_000_000)
+
+        def xz_parity(name, cols, fn):
+            """every xstride-th envelope of the full-size run keyed by the oracle (XZ2SFC.scala:54-77,
+            XZ3SFC.scala:53-76) against the keys the GPU wrote"""
+            if dist.rank != 0 or a.no_cpu:
+                return
+            sys.path.insert(0, os.path.join(ROOT, "oracle"))
+            import oracle as O
+            env = np.stack([c[:NX:xstride].cpu().numpy() for c in cols], 1)
+            ok, ost = getattr(O, fn)(env)
+            gk = xo[:NX:xstride].cpu().numpy()
+            extra[name]["parity_sample"] = {"envelopes": len(env), "stride": xstride,
+                                            "mismatches": int(((ok != gk) | (ost != 0)).sum())}
+        xz_parity("xz2_index", (x, y, xmax, ymax), "xz2_index_batch")
         zmin = torch.remainder(t[:NX], 604_800_000).to(torch.float64) / 1000.0
         zmax = torch.clamp(zmin + torch.pow(10.0, torch.rand(NX, device=dev, dtype=torch.float64, generator=g) * 4.94),
                            max=604800.0)
         rec("xz3_index", lambda: lib.gm_xz3_index(h, P(x), P(y), P(zmin), P(xmax), P(ymax), P(zmax), NX, 12, 1, 0, P(xo),
                                                  None, None), 56, NX, unit="envelopes/s")
+        xz_parity("xz3_index", (x, y, zmin, xmax, ymax, zmax), "xz3_index_batch")
         del xmax, ymax, xo, zmin, zmax
         # batched ranges (configs[4]): the queries sharded over the ranks (contiguous blocks), every
         # rank decomposes its block, offsets + ranges gathered to rank 0 (shard.gather_ranges)
@@ -834,16 +919,18 @@ def main():
                 "pipelined with their result copies), queries "
                 "sharded over the ranks with offsets + ranges gathered to rank 0; 100k %s query windows "
                 "(0.01-20 deg%s), maxRanges 2000, g = 12")
-        m = ranges_batch(dist, lib.gm_xz2_ranges, (h, qhi - qlo, woff.ctypes.data, wl.ctypes.data, 12, 2000),
-                         qhi - qlo, nq)
+        m, gl = ranges_batch(dist, lib.gm_xz2_ranges, (h, qhi - qlo, woff.ctypes.data, wl.ctypes.data, 12, 2000),
+                             qhi - qlo, nq)
         extra["xz2_ranges_batch"] = dict(m, note=note % ("XZ2", ""))
         if dist.rank == 0 and not a.no_cpu:
-            extra["xz2_ranges_batch"].update(cpu_ranges_baseline("xz2", win, None, 2000, m["ms_per_step"], nq))
-        m = ranges_batch(dist, lib.gm_xz3_ranges, (h, qhi - qlo, woff.ctypes.data, wl3.ctypes.data, 12, 1, 2000),
-                         qhi - qlo, nq)
+            extra["xz2_ranges_batch"].update(cpu_ranges_baseline("xz2", win, None, 2000, m["ms_per_step"], nq, gl))
+        del gl
+        m, gl = ranges_batch(dist, lib.gm_xz3_ranges, (h, qhi - qlo, woff.ctypes.data, wl3.ctypes.data, 12, 1, 2000),
+                             qhi - qlo, nq)
         extra["xz3_ranges_batch"] = dict(m, note=note % ("XZ3", " x 1 min-2 days, week period"))
         if dist.rank == 0 and not a.no_cpu:
-            extra["xz3_ranges_batch"].update(cpu_ranges_baseline("xz3", win3, None, 2000, m["ms_per_step"], nq))
+            extra["xz3_ranges_batch"].update(cpu_ranges_baseline("xz3", win3, None, 2000, m["ms_per_step"], nq, gl))
+        del gl
         # batched Z3 ranges (configs[4]/[0]): 4096 queries with target 2000
         rng = np.random.default_rng(1)
         qs = []
@@ -853,14 +940,15 @@ def main():
             qs.append(([(cx - w, cy - hh, cx + w, cy + hh)], [(t0, t0 + 86400)]))
         qlo, qhi = shard_bounds(len(qs), dist.rank, dist.world)
         fn, args, n3, _ = R.prepare_z3(sfc, qs[qlo:qhi], 64, 2000)
-        m = ranges_batch(dist, fn, args, n3, len(qs))
+        m, gl = ranges_batch(dist, fn, args, n3, len(qs))
         extra["z3_ranges_batch"] = dict(m, note="C-ABI call incl. H2D of queries and D2H of ranges (pinned host "
                                                 "output), sharded over the ranks + gather to rank 0; 4096 Z3 queries "
                                                 "(0.2-20 deg boxes x 1 day), maxRanges 2000 (ScanRangesTarget)")
         if dist.rank == 0 and not a.no_cpu:
             qb = np.array([q[0][0] for q in qs], np.float64)
             qt = np.array([q[1][0] for q in qs], np.int64)
-            extra["z3_ranges_batch"].update(cpu_ranges_baseline("z3", qb, qt, 2000, m["ms_per_step"], len(qs)))
+            extra["z3_ranges_batch"].update(cpu_ranges_baseline("z3", qb, qt, 2000, m["ms_per_step"], len(qs), gl))
+        del gl
     # ---------------------------------------------------------------- configs[0]: 10M-point index + one query's ranges
     if "extra" in only and not a.no_extra:
         extra["config0"] = bench_config0(a, dist, ctx, x, y, t)
@@ -882,7 +970,7 @@ def main():
         t_ix = time.time()
         ix = PolygonIndex(ps, ctx, a.cells_per_poly) if dist.rank == 0 else None
         t_build = time.time() - t_ix
-        if dist.world > 1:
+        if dist.pg is not None:
             from geomesa_amd.shard import broadcast_index
             ix = broadcast_index(dist.pg, ix, 0, ctx)
         torch.cuda.synchronize()

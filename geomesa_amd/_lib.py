@@ -31,11 +31,11 @@ GM_PARAM_INDEX_BUILD = 2
 GM_PARAM_RANGES_CHUNK = 3
 GM_PARAM_SORT_MODE = 4
 GM_PARAM_SORT_LAST = 5
+GM_PARAM_INDEX_COARSE = 6
+GM_PARAM_INDEX_CORE = 7
 
 GM_JOIN_AUTO = 0
 GM_JOIN_DIRECT = 1
-GM_JOIN_PARTITIONED = 2
-GM_JOIN_SPLIT = 3
 GM_SPATIAL_NONE, GM_SPATIAL_INTERSECTS, GM_SPATIAL_CONTAINS = 0, 1, 2
 
 

@@ -5,7 +5,7 @@ import sys
 from concurrent.futures import ThreadPoolExecutor
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-SRC = ["gm_ctx.hip", "gm_curve.hip", "gm_filter.hip", "gm_pip.hip", "gm_ranges.hip", "gm_sort.hip", "gm_arrow.hip", "gm_stats.hip", "gm_legacy.hip"]
+SRC = ["gm_ctx.hip", "gm_curve.hip", "gm_filter.hip", "gm_pip_build.hip", "gm_pip_join.hip", "gm_pip_relate.hip", "gm_pip_query.hip", "gm_ranges.hip", "gm_sort.hip", "gm_arrow.hip", "gm_stats.hip", "gm_legacy.hip"]
 OUT = os.path.join(HERE, "lib", "libgeomesa_hip.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math", "-fPIC",

@@ -20,12 +20,14 @@ struct gm_ctx {
   void* ws[4] = {nullptr, nullptr, nullptr, nullptr};   // reusable device workspaces (see ctx_workspace)
   size_t ws_cap[4] = {0, 0, 0, 0};
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  int64_t join_chunk = 0;          // GM_PARAM_JOIN_CHUNK: rows per join pass (0 = each strategy's default)
+  int64_t join_chunk = 0;          // GM_PARAM_JOIN_CHUNK: rows per join pass (0 = default, 2^31)
   int64_t index_build = 0;         // GM_PARAM_INDEX_BUILD: 0 = device build of the join index, 1 = host build
   int64_t ranges_hint = 0;         // largest batched-ranges output seen (sizes the device batch buffer)
   int64_t ranges_chunk = 0;        // GM_PARAM_RANGES_CHUNK: queries per pipelined chunk (0 = default)
   int64_t sort_last = 0;           // GM_PARAM_SORT_LAST (read-only): the last sort's digit passes | 256 if ranked locally
   int64_t sort_mode = 0;           // GM_PARAM_SORT_MODE: 0 = auto (prefix passes + local ranks), 1 = digit passes only
+  int64_t index_coarse = -1;       // GM_PARAM_INDEX_COARSE: the join's coarse sub-block masks (-1 = automatic)
+  int64_t index_core = 1;          // GM_PARAM_INDEX_CORE: the row predicate's core rectangles (1 = built)
   hipStream_t copy_stream = nullptr;   // result copies overlapping the next chunk's kernels (lazy)
   hipEvent_t ev_ready[2] = {nullptr, nullptr}, ev_copied[2] = {nullptr, nullptr};
 };

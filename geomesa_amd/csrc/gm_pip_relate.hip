@@ -1,0 +1,233 @@
+// gm_pip_relate.hip -- the row-wise spatial predicate (Spark SQL's st_* UDFs when the join rule does
+// not apply): PointLocator's location of point i in polygon poly[i], from the polygon index
+// (gm_pip.hpp).  Reference: SpatialRelationFunctions.scala:29-37, SQLFunctionHelper.scala:27-33.
+#include <algorithm>
+
+#include "gm_pip.hpp"
+
+namespace gm {
+
+// ------------------------------------------------------------------ row-wise predicate (UDF path)
+// st_contains / st_covers / st_intersects / ... evaluated row by row, as Spark SQL runs the UDF when
+// the join rule does not apply (SpatialRelationFunctions.scala:29-37 over nullableUDF,
+// SQLFunctionHelper.scala:27-33): row i pairs polygon poly[i] with point i.  Every DE-9IM predicate
+// of an areal geometry and a point is a function of the point's location in the polygon
+// (PointLocator.locate), so the kernel writes that location (LOC_*) and the host maps it.
+// The lookup is the join's: cell word chain, then only the entry of polygon poly[i] -- INTERIOR
+// decides at once, a blob is walked; no entry means the cell misses the polygon (exterior).
+constexpr uint8_t LOC_NULL = 0xff;
+
+__device__ __forceinline__ int entry_locate(const PipDev& d, uint32_t e, double px, double py) {
+  if ((e >> 30) == CELL_INTERIOR) return LOC_INTERIOR;
+  const uint32_t ref = e & 0x3fffffffu;
+  if (!blob_ref_ok(d, ref)) { pip_fault(d, PIP_FAULT_BLOB); return LOC_EXTERIOR; }
+  if (ref & BLOB_COMPACT) {
+    int poly;
+    return compact_locate((const dv2*)(d.compact + 16 * (uint64_t)(ref & (BLOB_COMPACT - 1))), px, py, poly);
+  }
+  const double* b = d.blob + 2 * (uint64_t)ref;
+  return blob_locate(d, b, *(const int2*)b, px, py);
+}
+
+// Per wave: RILP rows per lane per step.  A row resolves at once when its cell is empty, interior, or
+// a list without polygon poly[i] (list_poly search); a boundary entry of the row's polygon is queued
+// in LDS and the wave walks 64 queued blobs at a time (one per lane), as the join does -- every row
+// writes its location exactly once.
+#ifndef GM_RILP
+#define GM_RILP 2
+#endif
+constexpr int RILP = GM_RILP;
+constexpr int RQCAP = 64 * (RILP + 1);
+// VEC: a lane's RILP = 2 rows are adjacent (one 16-B load per coordinate column, one 8-B id load, one
+// 2-B location store when both resolve at once); the host picks it when the columns are aligned
+template <bool VEC>
+__global__ __launch_bounds__(RTPB) void k_pip_relate(const int32_t* __restrict__ poly, const double* __restrict__ px,
+                                                     const double* __restrict__ py, int64_t n, int32_t n_polys,
+                                                     PipDev d, const int32_t* __restrict__ list_poly,
+                                                     uint8_t* __restrict__ loc) {
+  static_assert(!VEC || RILP == 2, "adjacent rows per lane are written for RILP = 2");
+  constexpr int NW = RTPB / 64;
+  __shared__ double s_x[NW][RQCAP], s_y[NW][RQCAP];
+  __shared__ int64_t s_row[NW][RQCAP];
+  __shared__ uint32_t s_e[NW][RQCAP];
+  __shared__ int32_t s_p[NW][RQCAP];
+  // the coarse EMPTY bitmap at this kernel's budget (d.cm2, 16 KiB), staged in LDS like
+  // k_pip_join_q's: rows in EMPTY coarse blocks skip the coarse gather
+  __shared__ uint32_t s_cm[RELATE_CM_WORDS];
+  // each polygon's core rectangle (d.core): a row inside its own polygon's core is INTERIOR at once
+  __shared__ ushort4 s_core[RELATE_CORE_MAX > 0 ? RELATE_CORE_MAX : 1];
+  const int64_t cm_words = d.cm2_words <= RELATE_CM_WORDS ? d.cm2_words : 0;
+  for (int64_t i = threadIdx.x; i < cm_words; i += RTPB) s_cm[i] = d.cm2[i];
+  const int n_core = d.core && d.n_core == n_polys && d.n_core <= RELATE_CORE_MAX ? d.n_core : 0;
+  for (int i = threadIdx.x; i < n_core; i += RTPB) s_core[i] = d.core[i];
+  __syncthreads();
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  double* qx = s_x[wave]; double* qy = s_y[wave];
+  int64_t* qr = s_row[wave]; uint32_t* qe = s_e[wave]; int32_t* qp = s_p[wave];
+  int qn = 0, qg = 0;   // queued line-entry items (from slot 0 up) and blob items (from RQCAP - 1 down)
+  const int64_t wstep = (int64_t)gridDim.x * NW * (64 * RILP);
+  for (int64_t w0 = ((int64_t)blockIdx.x * NW + wave) * (64 * RILP);; w0 += wstep) {
+    const bool have = w0 < n;   // uniform per wave
+    if (have) {
+      int64_t row[RILP];
+      int p[RILP];
+      double x[RILP], y[RILP];
+      uint32_t w[RILP];
+      int cx[RILP], cy[RILP];
+#pragma unroll
+      for (int u = 0; u < RILP; ++u) {
+        row[u] = VEC ? w0 + RILP * lane + u : w0 + u * 64 + lane;
+        p[u] = -1; x[u] = y[u] = 0.0;
+      }
+      if (VEC && row[1] < n) {
+        const uint64_t pp = __builtin_nontemporal_load((const uint64_t*)(poly + row[0]));
+        const dv2 a = __builtin_nontemporal_load((const dv2*)(px + row[0]));
+        const dv2 b = __builtin_nontemporal_load((const dv2*)(py + row[0]));
+        p[0] = (int)(uint32_t)pp; p[1] = (int)(uint32_t)(pp >> 32); x[0] = a.x; x[1] = a.y; y[0] = b.x; y[1] = b.y;
+      } else {
+#pragma unroll
+        for (int u = 0; u < RILP; ++u)
+          if (row[u] < n) { p[u] = poly[row[u]]; x[u] = px[row[u]]; y[u] = py[row[u]]; }
+      }
+#pragma unroll
+      for (int u = 0; u < RILP; ++u) {
+        w[u] = CELL_EMPTY << 30;
+        if (p[u] >= 0 && p[u] < n_polys && x[u] >= d.gx0 && x[u] <= d.gx1 && y[u] >= d.gy0 && y[u] <= d.gy1) {
+          cx[u] = cell_of(x[u], d.gx0, d.inv_cw, d.gx);
+          cy[u] = cell_of(y[u], d.gy0, d.inv_ch, d.gy);
+          bool empty = false, core = false;
+          if (n_core) {
+            const ushort4 b = s_core[p[u]];
+            core = cx[u] >= b.x && cx[u] <= b.z && cy[u] >= b.y && cy[u] <= b.w;
+          }
+          if (cm_words && !core) {
+            const int b = ((cy[u] >> CF_LOG) >> d.cm2_shift) * d.cm2_w + ((cx[u] >> CF_LOG) >> d.cm2_shift);
+            empty = (s_cm[b >> 5] >> (b & 31)) & 1u;
+          }
+          if (core)
+            w[u] = (CELL_INTERIOR << 30) | (uint32_t)p[u];   // what the coarse word of a core cell says
+          else if (!empty) {
+            const uint32_t craw = d.coarse_sc[(int64_t)(cy[u] >> CF_LOG) * d.gxc + (cx[u] >> CF_LOG)];
+            w[u] = coarse_mask(craw, cx[u], cy[u], d.coarse_fmt);
+          }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < RILP; ++u)
+        if ((w[u] >> 30) == CELL_LIST) w[u] = d.cell_sc[(int64_t)cy[u] * d.gx + cx[u]];   // boundary shortcuts applied
+      uint8_t rv[RILP];
+      bool dir[RILP];
+#pragma unroll
+      for (int u = 0; u < RILP; ++u) {
+        uint8_t r = LOC_EXTERIOR;
+        bool queue = false;
+        uint32_t e = w[u];
+        const uint32_t kind = e >> 30;
+        if (p[u] < 0 || p[u] >= n_polys) {
+          r = LOC_NULL;
+        } else if (kind == CELL_INTERIOR) {
+          r = (int)(e & 0x3fffffffu) == p[u] ? LOC_INTERIOR : LOC_EXTERIOR;
+        } else if (kind == CELL_BOUNDARY) {
+          queue = true;   // the blob's polygon is checked when it is walked
+        } else if (kind == CELL_LIST) {
+          int l0 = 4 * (int)((e & 0x3fffffffu) >> 4), ni = (int)(e & 15u);
+          bool found = false;
+          if ((int64_t)l0 + 4 > d.n_list) { pip_fault(d, PIP_FAULT_LIST); ni = 0; }
+          else if (ni <= 4) {
+            // a short list is one 16-B group (lists start at multiples of 4 slots): its polygon ids
+            // and entries in two independent loads instead of a serial search
+            const int4 lp = *(const int4*)(list_poly + l0);
+            const uint4 le = *(const uint4*)(d.list_ent + l0);
+            const int pv = p[u];
+            found = true;
+            if (ni > 0 && lp.x == pv) e = le.x;
+            else if (ni > 1 && lp.y == pv) e = le.y;
+            else if (ni > 2 && lp.z == pv) e = le.z;
+            else if (ni > 3 && lp.w == pv) e = le.w;
+            else found = false;
+            ni = 0;
+          } else if (ni == LIST_LONG) { ni = (int)d.list_ent[l0]; l0 += 1; }
+          if (ni < 0 || (int64_t)l0 + ni > d.n_list) { pip_fault(d, PIP_FAULT_LIST); ni = 0; }
+          int j = 0;
+          while (j < ni && list_poly[l0 + j] != p[u]) ++j;
+          if (j < ni) { e = d.list_ent[l0 + j]; found = true; }
+          if (found) {
+            if ((e >> 30) == CELL_INTERIOR) r = LOC_INTERIOR;
+            else queue = true;
+          }
+        }
+        rv[u] = r;
+        dir[u] = row[u] < n && !queue;
+        if (!VEC && dir[u]) loc[row[u]] = r;
+        // line-entry items and blob items on separate ends, so an evaluation round runs one kind
+        const bool ln = (e & (BLOB_COMPACT | SC_LINE)) == (BLOB_COMPACT | SC_LINE) && d.line_ent;
+        const bool qv = queue && row[u] < n;
+        const uint64_t ml = __ballot(qv && ln), mb = __ballot(qv && !ln);
+        if (qv) {
+          const int o = ln ? qn + lanes_below(ml) : RQCAP - 1 - qg - lanes_below(mb);
+          qx[o] = x[u]; qy[o] = y[u]; qr[o] = row[u]; qe[o] = e; qp[o] = p[u];
+        }
+        qn += __popcll(ml);
+        qg += __popcll(mb);
+      }
+      if (VEC) {
+        if (dir[0] && dir[1]) *(uint16_t*)(loc + row[0]) = (uint16_t)(rv[0] | (rv[1] << 8));
+        else {
+          if (dir[0]) loc[row[0]] = rv[0];
+          if (dir[1]) loc[row[1]] = rv[1];
+        }
+      }
+    }
+    // walk min(qn, 64) queued blobs when the queue holds a full wave, and drain it at the end
+    // (< 64 queued before a step's <= 64 * RILP rows, so both ends fit RQCAP; the fuller kind goes
+    // first, which leaves < 64 again)
+    while (qn + qg >= 64 || (!have && qn + qg > 0)) {
+      wave_lds_sync();
+      const bool lines = qn >= qg;
+      const int kq = min(lines ? qn : qg, 64);
+      const int slot = lines ? qn - kq + lane : RQCAP - qg + lane;
+      if (lane < kq) {
+        const uint32_t ref = qe[slot] & 0x3fffffffu;
+        const double ex = qx[slot], ey = qy[slot];
+        int pl = -1;
+        const int l = item_locate(d, ref, ex, ey, pl);
+        loc[qr[slot]] = (uint8_t)(pl == qp[slot] ? l : LOC_EXTERIOR);
+      }
+      wave_lds_sync();
+      if (lines) qn -= kq;
+      else qg -= kq;
+    }
+    if (!have) break;
+  }
+}
+
+}  // namespace gm
+
+using namespace gm;
+
+extern "C" {
+
+int gm_pip_relate(gm_ctx* ctx, const gm_pip_index* ix, const int32_t* poly, const double* px, const double* py,
+                  int64_t n, uint8_t* loc) {
+  if (!ctx || !ix || n < 0) return GM_E_INVALID;
+  if (n == 0) return GM_OK;
+  if (!poly || !px || !py || !loc) return GM_E_INVALID;
+  GM_HIP(hipSetDevice(ctx->device));
+  const bool vec = RILP == 2 && ((uintptr_t)px | (uintptr_t)py) % 16 == 0 && (uintptr_t)poly % 8 == 0 &&
+                   (uintptr_t)loc % 2 == 0;
+  auto* kern = vec ? k_pip_relate<RILP == 2> : k_pip_relate<false>;
+  const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(resident_blocks((const void*)kern, ctx->device, RTPB, 1),
+                                                                          (n + RTPB * RILP - 1) / (RTPB * RILP)));
+  PipDev dv = ix->dev;
+  int64_t* fault = ctx->d_scratch + 8;   // reference checks (PIP_FAULT_*), as the join's
+  dv.fault = (uint32_t*)fault;
+  GM_HIP(hipMemsetAsync(fault, 0, 8, ctx->stream));
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(RTPB), 0, ctx->stream, poly, px, py, n, ix->n_polys, dv, ix->list_poly, loc);
+  GM_CHECK_LAUNCH();
+  int64_t bits = 0;
+  const int rc = copy_d2h(ctx, &bits, fault, 8);
+  if (rc) return rc;
+  return bits ? index_fault("gm_pip_relate", (uint32_t)bits) : GM_OK;
+}
+
+}  // extern "C"

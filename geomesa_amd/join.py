@@ -166,8 +166,7 @@ class PolygonIndex:
               "gm_pip_join_census")
         return dict(zip(self.CENSUS, c.tolist()))
 
-    MODES = {"auto": _lib.GM_JOIN_AUTO, "direct": _lib.GM_JOIN_DIRECT, "partitioned": _lib.GM_JOIN_PARTITIONED,
-             "split": _lib.GM_JOIN_SPLIT}
+    MODES = {"auto": _lib.GM_JOIN_AUTO, "direct": _lib.GM_JOIN_DIRECT}
 
     PREDICATES = {"st_contains": _lib.GM_SPATIAL_CONTAINS, "st_within": _lib.GM_SPATIAL_CONTAINS,
                   "st_intersects": _lib.GM_SPATIAL_INTERSECTS, "st_covers": _lib.GM_SPATIAL_INTERSECTS}
@@ -175,9 +174,8 @@ class PolygonIndex:
     def join(self, px, py, id_base=0, cap=None, count_only=False, mode="auto", predicate="st_contains"):
         """Returns (pt_ids, poly_ids) device tensors (or the pair count when count_only).
 
-        mode: "auto", "direct" (one pass over the point columns), "partitioned" (points
-        counting-sorted by grid-row band first) or "split" (lookups, then a work list of boundary
-        evaluations); the pair set is the same for every mode.  predicate: the join condition's UDF,
+        mode: "auto" or "direct" (the staged direct pass over the point columns; the two are one
+        strategy on MI355X).  predicate: the join condition's UDF,
         st_contains(polygon, point) / st_within(point, polygon) or st_intersects / st_covers."""
         m = self.MODES[mode]
         pr = self.PREDICATES[predicate]

@@ -41,10 +41,11 @@ def broadcast_polyset(pg, ps, src=0):
     return PolygonSet(*out)
 
 
-def broadcast_index(pg, index, src=0, ctx=None):
+def broadcast_index(pg, index, src=0, ctx=None, reimport=False):
     """Broadcast a built join index (join.PolygonIndex) from rank `src`: its device arrays go out over
     RCCL (xGMI) and every other rank imports them (gm_pip_index_import) -- no per-rank host rebuild.
-    Other ranks pass index=None.  Over gloo the arrays travel through host memory."""
+    Other ranks pass index=None.  Over gloo the arrays travel through host memory.  reimport=True makes
+    `src` import what it broadcast too (a test hook: at world 1 it runs the receiving side)."""
     import ctypes
     import torch
     from . import _lib
@@ -67,7 +68,7 @@ def broadcast_index(pg, index, src=0, ctx=None):
         t = arrs[k].to(dev) if arrs is not None else torch.empty(size, dtype=torch.uint8, device=dev)
         pg.broadcast(t, src)
         out.append(t.to(cuda))
-    if pg.get_rank() == src:
+    if pg.get_rank() == src and not reimport:
         return index
     return PolygonIndex.from_arrays(lay, out, ctx)
 
@@ -82,7 +83,7 @@ def all_reduce_scalar(pg, v, op="max"):
     return float(t.item())
 
 
-def gather_rows(pg, cols, dst=0):
+def gather_rows(pg, cols, dst=0, loopback=False):
     """Gather variable-length per-rank result columns (1-D tensors of equal length per rank: ids,
     or point ids + polygon ids) to rank `dst`, in rank order.
 
@@ -91,7 +92,8 @@ def gather_rows(pg, cols, dst=0):
     batched: over RCCL a group of sends / receives, so `dst` takes every peer's rows at once over its
     own xGMI link), and copies its own rows in.  No padding and no concatenation copy: rank `dst`
     holds the result and nothing else.  Returns the columns on `dst` and None elsewhere; with pg None,
-    `cols`."""
+    `cols`.  loopback=True moves `dst`'s own rows through the same send / receive group instead of a
+    copy (a test hook: at world 1 it is how the RCCL point-to-point path runs on a one-GPU box)."""
     if pg is None:
         return list(cols)
     import torch
@@ -108,7 +110,13 @@ def gather_rows(pg, cols, dst=0):
     for c in cols:
         if rank == dst:
             o = torch.empty(offs[-1], dtype=c.dtype, device=dev)
-            o[offs[dst]:offs[dst + 1]] = c.to(dev)
+            if loopback and counts[dst] > 0:
+                src = c.to(dev).contiguous()
+                keep.append(src)
+                ops.append(pg.P2POp(pg.isend, src, dst))
+                ops.append(pg.P2POp(pg.irecv, o[offs[dst]:offs[dst + 1]], dst))
+            else:
+                o[offs[dst]:offs[dst + 1]] = c.to(dev)
             for r in range(world):
                 if r != dst and counts[r] > 0:
                     ops.append(pg.P2POp(pg.irecv, o[offs[r]:offs[r + 1]], r))
@@ -250,10 +258,16 @@ def exchange_by_key_range(pg, hi, lo, cols=(), samples=1024):
     of the counts, then one of the rows packed as (hi, lo, cols...) int64 records -- over RCCL a
     grouped send / recv on every xGMI link at once.  Returns (hi, lo, cols, (s_hi, s_lo)) of the
     received rows: `world` sorted runs, one per sender, in rank order (the caller re-sorts)."""
-    import torch
     s_hi, s_lo = sample_splitters(pg, hi, lo, samples)
     if pg is None or pg.get_world_size() == 1:
         return hi, lo, list(cols), (s_hi, s_lo)
+    return _exchange_rows(pg, hi, lo, cols, s_hi, s_lo) + ((s_hi, s_lo),)
+
+
+def _exchange_rows(pg, hi, lo, cols, s_hi, s_lo):
+    """The exchange step of exchange_by_key_range for given splitters (valid at any world size; a
+    world of 1 keeps every row -- the RCCL test at world 1 runs it): (hi, lo, cols) received."""
+    import torch
     world = pg.get_world_size()
     dev = _device_of(pg)
     home = hi.device
@@ -268,8 +282,7 @@ def exchange_by_key_range(pg, hi, lo, cols=(), samples=1024):
     pg.all_to_all_single(out, rec, recv, send)
     del rec
     out = out.to(home)
-    return out[:, 0].contiguous(), out[:, 1].contiguous(), [out[:, 2 + k].contiguous() for k in range(len(cols))], \
-        (s_hi, s_lo)
+    return out[:, 0].contiguous(), out[:, 1].contiguous(), [out[:, 2 + k].contiguous() for k in range(len(cols))]
 
 
 def clip_key_ranges(ranges, kmin, kmax):

@@ -92,21 +92,30 @@ int gm_ctx_sync(gm_ctx* ctx);
 void* gm_ctx_stream(gm_ctx* ctx);
 const char* gm_last_error(void);
 /* per-context tuning parameters (library defaults when unset) */
-#define GM_PARAM_JOIN_CHUNK 1   /* points per pass of the join strategies (0 = defaults: direct 2^31,
-                                   partitioned 2^28, split sized to its 6 GiB workspace); smaller
-                                   values only add passes -- the pair set never changes */
+#define GM_PARAM_JOIN_CHUNK 1   /* points per pass of the join (0 = default 2^31; odd values are rounded
+                                   down to even, at least 2); smaller values only add passes -- the
+                                   pair set never changes */
 #define GM_PARAM_INDEX_BUILD 2  /* where gm_pip_index_create builds the join index: 0 (default) = on the
                                    device (same arrays, byte for byte), 1 = on the host */
 #define GM_PARAM_RANGES_CHUNK 3 /* queries per chunk of a batched ranges call whose output is pinned host
                                    memory: chunk k's result copy runs while chunk k + 1 computes (0 =
                                    default: one batch below 16384 queries, else about nq / 8 per chunk);
                                    the output never changes */
-#define GM_PARAM_SORT_MODE 4    /* gm_sort_keys: 0 (default) = three digit passes over the top 24 varying
-                                   key bits, then every run of equal prefixes ranked in LDS (digit passes
-                                   over every varying byte when a run exceeds 1024 rows); 1 = digit passes
-                                   over every varying byte.  The output never changes */
+#define GM_PARAM_SORT_MODE 4    /* gm_sort_keys: 0 (default) = up to four digit passes over the top
+                                   ~log2(n) + 3 varying key bits, then every run of equal prefixes ranked
+                                   in LDS (digit passes over every varying byte when a run exceeds 256
+                                   rows); 1 = digit passes over every varying byte.  The output never
+                                   changes */
 #define GM_PARAM_SORT_LAST 5    /* read-only (gm_ctx_get_param): how the context's last gm_sort_keys ran:
                                    digit passes, plus 256 when the runs were ranked locally */
+#define GM_PARAM_INDEX_COARSE 6 /* the join's coarse-cell sub-block masks, chosen when a polygon index is
+                                   built or imported on this context: -1 (default) = automatic (with
+                                   fewer than 2^14 polygons 8 sub-blocks with EMPTY and INTERIOR-of-one-
+                                   polygon bits, else 16 EMPTY bits), 0 = EMPTY bits, 1 = EMPTY and
+                                   INTERIOR bits.  Results never change */
+#define GM_PARAM_INDEX_CORE 7   /* 1 (default) = a built or imported polygon index carries the row
+                                   predicate's per-polygon core rectangles, 0 = none.  Results never
+                                   change */
 int gm_ctx_set_param(gm_ctx* ctx, int param, int64_t value);
 int gm_ctx_get_param(gm_ctx* ctx, int param, int64_t* value);
 /* device memory helpers for callers without their own allocator (e.g. a JNI shim) */
@@ -297,20 +306,18 @@ int gm_pip_index_import(gm_ctx* ctx, const gm_pip_index_layout* layout, void* co
    pt_ids / poly_ids (device, cap entries; point ids are id_base + row); order within the output is
    unspecified (the reference returns an unordered RDD).  *n_pairs (host) receives the pair count;
    when it exceeds cap, GM_E_CAPACITY is returned and no pair beyond cap is written.  With
-   pt_ids = poly_ids = NULL the call only counts. */
+   pt_ids = poly_ids = NULL the call only counts.  The call synchronises the context stream: it
+   returns GM_E_INDEX when a device reference check of the index failed (a corrupt or mismatched
+   imported index), and the output is then invalid. */
 int gm_pip_join(gm_ctx* ctx, const gm_pip_index* index, const double* px, const double* py, int64_t n,
                 int64_t id_base, int64_t* pt_ids, int32_t* poly_ids, int64_t cap, int64_t* n_pairs);
 
-/* join strategies for gm_pip_join_ex */
-#define GM_JOIN_AUTO 0        /* the faster strategy on MI355X: DIRECT */
-#define GM_JOIN_DIRECT 1      /* one pass over the point columns (random index reads) */
-#define GM_JOIN_PARTITIONED 2 /* counting-sort the points by grid-row band first (device temp:
-                                 24 B per point, at most 2^28 points per pass), then join band by
-                                 band with the band's index data L2-resident */
-#define GM_JOIN_SPLIT 3       /* two passes: cell lookups + interior pairs + a work list of boundary
-                                 (point, blob) items, then the items' exact evaluation (device temp
-                                 per point: 8 B x the most entries of any cell) */
-/* gm_pip_join with an explicit strategy; the pair set is identical for every mode */
+/* join strategies for gm_pip_join_ex.  Both run the staged direct pass over the point columns; a
+   band-partitioned and a two-pass variant measured slower on MI355X and were
+   removed, and any other value returns GM_E_INVALID */
+#define GM_JOIN_AUTO 0
+#define GM_JOIN_DIRECT 1
+/* gm_pip_join with an explicit strategy */
 int gm_pip_join_ex(gm_ctx* ctx, const gm_pip_index* index, const double* px, const double* py, int64_t n,
                    int64_t id_base, int64_t* pt_ids, int32_t* poly_ids, int64_t cap, int64_t* n_pairs, int mode);
 
@@ -353,6 +360,8 @@ int gm_query_scan(gm_ctx* ctx, const double* x, const double* y, const int64_t* 
 #define GM_LOC_BOUNDARY 1
 #define GM_LOC_INTERIOR 2
 #define GM_LOC_NULL 255
+/* Synchronises the context stream; GM_E_INDEX as gm_pip_join (the locations are then invalid).
+   gm_query_scan reports the same checks of its geometry term. */
 int gm_pip_relate(gm_ctx* ctx, const gm_pip_index* index, const int32_t* poly, const double* px, const double* py,
                   int64_t n, uint8_t* loc);
 
@@ -412,7 +421,7 @@ int gm_xz3_index_key_arrow(gm_ctx* ctx, const gm_geom_column* geom, const gm_tim
 /* A point column as x / y device columns (null slots -> NaN): the adapter for every other entry */
 int gm_arrow_points_to_columns(gm_ctx* ctx, const gm_geom_column* geom, int64_t n, double* x, double* y);
 /* gm_pip_join_pred over an Arrow point column (null points never match): the direct pass reads the
-   tuples in place; the partitioned and split strategies go through gm_arrow_points_to_columns */
+   tuples in place */
 int gm_pip_join_arrow(gm_ctx* ctx, const gm_pip_index* index, const gm_geom_column* points, int64_t n,
                       int64_t id_base, int64_t* pt_ids, int32_t* poly_ids, int64_t cap, int64_t* n_pairs, int mode,
                       int predicate);

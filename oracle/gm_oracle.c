@@ -727,6 +727,23 @@ int gmo_xz3_index(int g, int period, double xmin, double ymin, double zmin, doub
   return GMO_OK;
 }
 
+/* column batches of XZ2SFC.index / XZ3SFC.index (the bench's strided full-size parity samples) */
+void gmo_xz2_index_batch(int g, const double* xmin, const double* ymin, const double* xmax, const double* ymax,
+                         int64_t n, int lenient, int64_t* out, uint8_t* status) {
+  for (int64_t i = 0; i < n; i++) {
+    const int st = gmo_xz2_index(g, xmin[i], ymin[i], xmax[i], ymax[i], lenient, &out[i]);
+    if (status) status[i] = (uint8_t)st;
+  }
+}
+void gmo_xz3_index_batch(int g, int period, const double* xmin, const double* ymin, const double* zmin,
+                         const double* xmax, const double* ymax, const double* zmax, int64_t n, int lenient,
+                         int64_t* out, uint8_t* status) {
+  for (int64_t i = 0; i < n; i++) {
+    const int st = gmo_xz3_index(g, period, xmin[i], ymin[i], zmin[i], xmax[i], ymax[i], zmax[i], lenient, &out[i]);
+    if (status) status[i] = (uint8_t)st;
+  }
+}
+
 typedef struct { double mn[3], mx[3], len; int term; } xel;
 typedef struct { xel* v; int64_t head, tail, cap; } xqueue;
 static void xq_push(xqueue* q, const xel* e) {
@@ -1272,12 +1289,15 @@ int64_t gmo_pip_join_ex(const gmo_polyset* ps, const double* px, const double* p
   return total <= cap ? total : -total;
 }
 
-/* ---- batch timing of the range decompositions (the bench's CPU baseline): nq single-box queries on
-   nthreads pthreads, outputs discarded; totals of merged ranges and nodes checked */
+/* ---- batch of the range decompositions (the bench's CPU baseline and its full-size parity): nq
+   single-box queries on nthreads pthreads; totals of merged ranges and nodes checked, and optionally
+   each query's merged-range count (counts[nq]) and, given offsets[nq] from those counts, the ranges
+   themselves at out + offsets[i] */
 typedef struct {
   int kind, period, g, max_ranges, pad;  /* kind 3 = Z3, 12 = XZ2, 13 = XZ3 */
   const double* q; const int64_t* t;
   int64_t lo, hi, ranges, nodes;
+  int64_t* counts; const int64_t* offsets; gmo_range* out;
 } rbatch_task;
 
 static void* rbatch_worker(void* arg) {
@@ -1285,29 +1305,34 @@ static void* rbatch_worker(void* arg) {
   int64_t cap = 1 << 16;
   gmo_range* out = (gmo_range*)malloc(sizeof(gmo_range) * (size_t)cap);
   g_nodes_checked = 0;
+  int64_t nodes = 0;
   for (int64_t i = k->lo; i < k->hi; i++) {
     int64_t m;
     for (;;) {
+      g_nodes_checked = 0;
       if (k->kind == 3) m = gmo_z3_ranges(k->period, 21, k->q + 4 * i, 1, k->t + 2 * i, 1, 64, k->max_ranges, out, cap);
       else if (k->kind == 12) m = gmo_xz2_ranges(k->g, k->q + 4 * i, 1, k->max_ranges, out, cap);
       else m = gmo_xz3_ranges(k->g, k->period, k->q + 6 * i, 1, k->max_ranges, out, cap);
-      if (m < 0 && m > -(INT64_C(1) << 62)) {   /* capacity: grow and redo */
+      if (m < 0 && m > -(INT64_C(1) << 62)) {   /* capacity: grow and redo this query */
         cap = -m;
         out = (gmo_range*)realloc(out, sizeof(gmo_range) * (size_t)cap);
-        g_nodes_checked = 0;
         continue;
       }
       break;
     }
+    nodes += g_nodes_checked;
     if (m > 0) k->ranges += m;
+    if (k->counts) k->counts[i] = m;
+    if (k->out && k->offsets && m > 0) memcpy(k->out + k->offsets[i], out, sizeof(gmo_range) * (size_t)m);
   }
-  k->nodes = g_nodes_checked;
+  k->nodes = nodes;
   free(out);
   return NULL;
 }
 
 int gmo_ranges_batch(int kind, int period, int g, const double* q, const int64_t* t, int64_t nq, int max_ranges,
-                     int nthreads, int64_t* total_ranges, int64_t* total_nodes) {
+                     int nthreads, int64_t* total_ranges, int64_t* total_nodes, int64_t* counts,
+                     const int64_t* offsets, gmo_range* out) {
   if (nthreads < 1) nthreads = 1;
   rbatch_task* tasks = (rbatch_task*)calloc((size_t)nthreads, sizeof(rbatch_task));
   pthread_t* th = (pthread_t*)calloc((size_t)nthreads, sizeof(pthread_t));
@@ -1315,6 +1340,7 @@ int gmo_ranges_batch(int kind, int period, int g, const double* q, const int64_t
   for (int k = 0; k < nthreads; k++) {
     rbatch_task* x = &tasks[k];
     x->kind = kind; x->period = period; x->g = g; x->max_ranges = max_ranges; x->q = q; x->t = t;
+    x->counts = counts; x->offsets = offsets; x->out = out;
     x->lo = (int64_t)k * chunk; x->hi = x->lo + chunk < nq ? x->lo + chunk : nq;
     if (x->lo > nq) x->lo = nq;
     pthread_create(&th[k], NULL, rbatch_worker, x);

@@ -97,6 +97,11 @@ int64_t gmo_z2_ranges(int precision, const double* xy, int nxy, int range_precis
 int     gmo_xz2_index(int g, double xmin, double ymin, double xmax, double ymax, int lenient, int64_t* out);
 int     gmo_xz3_index(int g, int period, double xmin, double ymin, double zmin, double xmax, double ymax,
                       double zmax, int lenient, int64_t* out);
+void    gmo_xz2_index_batch(int g, const double* xmin, const double* ymin, const double* xmax, const double* ymax,
+                            int64_t n, int lenient, int64_t* out, uint8_t* status);
+void    gmo_xz3_index_batch(int g, int period, const double* xmin, const double* ymin, const double* zmin,
+                            const double* xmax, const double* ymax, const double* zmax, int64_t n, int lenient,
+                            int64_t* out, uint8_t* status);
 int64_t gmo_xz2_ranges(int g, const double* q, int nq, int max_ranges, gmo_range* out, int64_t cap);
 int64_t gmo_xz3_ranges(int g, int period, const double* q, int nq, int max_ranges, gmo_range* out, int64_t cap);
 
@@ -140,7 +145,8 @@ int64_t gmo_pip_join_ex(const gmo_polyset* ps, const double* px, const double* p
 /* range decomposition work counter (per thread, read-and-reset) and the batch timing driver */
 int64_t gmo_nodes_checked(void);
 int     gmo_ranges_batch(int kind, int period, int g, const double* q, const int64_t* t, int64_t nq, int max_ranges,
-                         int nthreads, int64_t* total_ranges, int64_t* total_nodes);
+                         int nthreads, int64_t* total_ranges, int64_t* total_nodes, int64_t* counts,
+                         const int64_t* offsets, gmo_range* out);
 #ifdef __cplusplus
 }
 #endif

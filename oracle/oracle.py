@@ -9,6 +9,9 @@ import subprocess
 
 import numpy as np
 
+# gmo_range {int64 lower, upper; int32 contained, pad}: the layout of the library's gm_range
+RANGE_DTYPE = np.dtype([("lower", "<i8"), ("upper", "<i8"), ("contained", "<i4"), ("reserved", "<i4")])
+
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "build", "libgm_oracle.so")
 
@@ -80,6 +83,8 @@ def lib():
             "gmo_z2_ranges": (i64, [ctypes.c_int, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, i64]),
             "gmo_xz2_index": (ctypes.c_int, [ctypes.c_int, d, d, d, d, ctypes.c_int, vp]),
             "gmo_xz3_index": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, d, d, d, d, d, d, ctypes.c_int, vp]),
+            "gmo_xz2_index_batch": (None, [ctypes.c_int, vp, vp, vp, vp, i64, ctypes.c_int, vp, vp]),
+            "gmo_xz3_index_batch": (None, [ctypes.c_int, ctypes.c_int, vp, vp, vp, vp, vp, vp, i64, ctypes.c_int, vp, vp]),
             "gmo_xz2_ranges": (i64, [ctypes.c_int, vp, ctypes.c_int, ctypes.c_int, vp, i64]),
             "gmo_xz3_ranges": (i64, [ctypes.c_int, ctypes.c_int, vp, ctypes.c_int, ctypes.c_int, vp, i64]),
             "gmo_z3filter_in_bounds": (ctypes.c_int, [vp, ctypes.c_size_t, vp, ctypes.c_int]),
@@ -95,7 +100,7 @@ def lib():
             "gmo_pip_join": (i64, [vp, vp, vp, i64, vp, vp, i64, ctypes.c_int]),
             "gmo_nodes_checked": (i64, []),
             "gmo_ranges_batch": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, vp, i64, ctypes.c_int,
-                                                ctypes.c_int, vp, vp]),
+                                                ctypes.c_int, vp, vp, vp, vp, vp]),
             "gmo_pip_join_ex": (i64, [vp, vp, vp, i64, vp, vp, i64, ctypes.c_int, ctypes.c_int, vp]),
         }
         for name, (res, args) in sig.items():
@@ -212,17 +217,27 @@ def nodes_checked():
     return lib().gmo_nodes_checked()
 
 
-def ranges_batch(kind, q, t=None, max_ranges=2000, nthreads=1, g=12, period=WEEK):
-    """Times-able batch of single-box queries: kind "z3" (q = n x 4 boxes, t = n x 2 offsets), "xz2"
-    (n x 4 windows) or "xz3" (n x 6).  Returns (total merged ranges, total nodes checked)."""
+def ranges_batch(kind, q, t=None, max_ranges=2000, nthreads=1, g=12, period=WEEK, lists=False):
+    """Batch of single-box queries: kind "z3" (q = n x 4 boxes, t = n x 2 offsets), "xz2" (n x 4
+    windows) or "xz3" (n x 6).  Returns (total merged ranges, total nodes checked); with lists=True
+    also (offsets [n + 1], ranges RANGE_DTYPE) -- every query's merged list, from a second pass."""
     qa = np.ascontiguousarray(np.asarray(q, np.float64))
     ta = np.ascontiguousarray(np.asarray(t if t is not None else [0, 0], np.int64))
     k = {"z3": 3, "xz2": 12, "xz3": 13}[kind]
     nq = qa.shape[0]
+    mr = 2147483647 if max_ranges is None else max_ranges
     r, nd = ctypes.c_int64(), ctypes.c_int64()
-    lib().gmo_ranges_batch(k, period, g, _p(qa), _p(ta), nq, 2147483647 if max_ranges is None else max_ranges,
-                           nthreads, ctypes.byref(r), ctypes.byref(nd))
-    return r.value, nd.value
+    counts = np.zeros(max(nq, 1), np.int64)
+    lib().gmo_ranges_batch(k, period, g, _p(qa), _p(ta), nq, mr, nthreads, ctypes.byref(r), ctypes.byref(nd),
+                           _p(counts), None, None)
+    if not lists:
+        return r.value, nd.value
+    offs = np.zeros(nq + 1, np.int64)
+    offs[1:] = np.cumsum(np.maximum(counts[:nq], 0))
+    out = np.zeros(max(int(offs[-1]), 1), RANGE_DTYPE)
+    lib().gmo_ranges_batch(k, period, g, _p(qa), _p(ta), nq, mr, nthreads, None, None, _p(counts), _p(offs),
+                           out.ctypes.data)
+    return r.value, nd.value, offs, out[:int(offs[-1])]
 
 
 def xz2_ranges(queries, max_ranges=None, g=12):
@@ -318,20 +333,22 @@ def z2_invert_batch(z):
 
 
 def xz2_index_batch(env, lenient=False, g=12):
+    """XZ2SFC.index over an (n, 4) array of (xmin, ymin, xmax, ymax); returns (keys, status)."""
     env = np.asarray(env, np.float64).reshape(-1, 4)
-    out = np.empty(len(env), np.int64); st = np.empty(len(env), np.uint8)
-    for i, (a, b, c, d) in enumerate(env):
-        s, z = xz2_index(a, b, c, d, lenient, g)
-        out[i] = z; st[i] = s
+    cols = [np.ascontiguousarray(env[:, k]) for k in range(4)]
+    n = len(env)
+    out = np.empty(n, np.int64); st = np.empty(n, np.uint8)
+    lib().gmo_xz2_index_batch(g, *[_p(c) for c in cols], n, int(lenient), _p(out), _p(st))
     return out, st
 
 
 def xz3_index_batch(env, lenient=False, g=12, period=WEEK):
+    """XZ3SFC.index over an (n, 6) array of (xmin, ymin, zmin, xmax, ymax, zmax); returns (keys, status)."""
     env = np.asarray(env, np.float64).reshape(-1, 6)
-    out = np.empty(len(env), np.int64); st = np.empty(len(env), np.uint8)
-    for i, e in enumerate(env):
-        s, z = xz3_index(*e, lenient=lenient, g=g, period=period)
-        out[i] = z; st[i] = s
+    cols = [np.ascontiguousarray(env[:, k]) for k in range(6)]
+    n = len(env)
+    out = np.empty(n, np.int64); st = np.empty(n, np.uint8)
+    lib().gmo_xz3_index_batch(g, period, *[_p(c) for c in cols], n, int(lenient), _p(out), _p(st))
     return out, st
 
 

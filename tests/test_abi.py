@@ -50,14 +50,33 @@ def test_load_without_gpu_fails_loudly():
 
 
 def test_product_build_refuses_timing_hooks():
-    """The GM_JX_* stage-ablation hooks (wrong results by design) cannot reach the shipped library:
-    build.py refuses them for its output path (no compile runs), and the product build defines
-    GM_PRODUCT_BUILD, under which gm_pip.hip #errors on any of them."""
+    """GM_JX_* stage-ablation hooks (wrong results by design) never reach the shipped library: build.py
+    refuses them for its output path (no compile runs), and no product source carries one."""
     import pytest
     from geomesa_amd import build as B
     with pytest.raises(ValueError):
         B.build(defines=("GM_JX_NOBLOB",), verbose=False)
-    src = open(os.path.join(ROOT, "geomesa_amd", "csrc", "gm_pip.hip")).read()
-    hooks = set(re.findall(r"GM_JX_[A-Z0-9]+", src))
-    guard = src[src.index("#if defined(GM_PRODUCT_BUILD)"):src.index("#error")]
-    assert hooks and all(h in guard for h in hooks), hooks
+    for src in B.sources():
+        assert "GM_JX_" not in open(src).read(), src
+
+
+def test_no_environment_selected_kernel_paths():
+    """Which kernel answers a product call is never chosen by the process environment: the library
+    reads only diagnostics (GM_PIP_DEBUG) and the host build's thread count; every knob that changes
+    a kernel path is a gm_ctx_set_param parameter."""
+    csrc = os.path.join(ROOT, "geomesa_amd", "csrc")
+    names = set()
+    for f in os.listdir(csrc):
+        if f.endswith((".hip", ".hpp")):
+            names |= set(re.findall(r'getenv\(\s*"([A-Z0-9_]+)"', open(os.path.join(csrc, f)).read()))
+            assert "getenv(v)" not in open(os.path.join(csrc, f)).read() or f == "gm_pip_build.hip", f
+    assert names <= {"GM_PIP_DEBUG"}, names
+
+
+def test_header_constants_match_binding():
+    """Every GM_PARAM_* / GM_JOIN_* / GM_SPATIAL_* value of the header is the binding's."""
+    src = open(_lib.HEADER).read()
+    defs = dict((k, int(v)) for k, v in re.findall(r"#define\s+(GM_(?:PARAM|JOIN|SPATIAL)_[A-Z0-9_]+)\s+(-?\d+)", src))
+    assert len(defs) >= 12
+    for k, v in defs.items():
+        assert getattr(_lib, k) == v, k

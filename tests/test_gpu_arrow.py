@@ -209,7 +209,7 @@ def polyset_to_arrow(ps, f32=False):
     return pa.array(vals, pa.list_(pa.list_(pa.list_(PT4 if f32 else PT))))
 
 
-@pytest.mark.parametrize("mode", ["auto", "split", "partitioned"])
+@pytest.mark.parametrize("mode", ["auto", "direct"])
 def test_join_arrow_matches_columns(gpu, oracle, mode):
     from geomesa_amd import arrow
     from geomesa_amd.join import PolygonIndex, synthetic_counties, synthetic_points

@@ -24,10 +24,9 @@ def test_index_export_import_same_pairs(gpu, oracle):
     del arrs
     assert ix2.stats() == ix.stats()
     px, py = synthetic_points(300_000, seed=3)
-    for mode in ("direct", "split", "partitioned"):
-        a = _sorted_pairs(*ix.join(px, py, mode=mode))
-        b = _sorted_pairs(*ix2.join(px, py, mode=mode))
-        assert np.array_equal(a, b), mode
+    a = _sorted_pairs(*ix.join(px, py))
+    b = _sorted_pairs(*ix2.join(px, py))
+    assert np.array_equal(a, b)
     poly = np.arange(len(px)) % ps.n_polys
     assert bool((ix.relate(poly, px, py) == ix2.relate(poly, px, py)).all())
 

@@ -81,5 +81,4 @@ def test_device_build_join_equals_oracle(gpu, oracle):
     opt, opl = oracle.OraclePolySet(*ps.to_arrays()).join(px, py, nthreads=16)
     exp = np.stack([opt, opl.astype(np.int64)], 1)
     exp = exp[np.lexsort((exp[:, 1], exp[:, 0]))]
-    for mode in ("direct", "partitioned", "split"):
-        assert np.array_equal(_sorted_pairs(*ix.join(px, py, mode=mode)), exp), mode
+    assert np.array_equal(_sorted_pairs(*ix.join(px, py)), exp)

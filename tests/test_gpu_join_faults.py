@@ -36,7 +36,7 @@ def _edge_points(ps, offset, rng, n=None):
     return px, py
 
 
-def _check(ix, oracle, ps, px, py, modes=("direct", "split", "partitioned")):
+def _check(ix, oracle, ps, px, py, modes=("auto",)):
     op = oracle.OraclePolySet(*ps.to_arrays())
     opt, opl = op.join(px, py, nthreads=8)
     exp = np.stack([opt, opl.astype(np.int64)], 1)
@@ -116,8 +116,8 @@ def test_arrow_nulls_at_tile_ends(gpu, oracle, f32):
 
 def test_corrupt_reference_reports_instead_of_faulting(gpu):
     """What the faulting trees did -- follow a blob reference that points outside the index -- now
-    ends in GM_E_INDEX (device-side reference check), in every join strategy, and the context and a
-    healthy index keep working afterwards."""
+    ends in GM_E_INDEX (device-side reference check) in the join, the row predicate and the fused
+    query scan, and the context and a healthy index keep working afterwards."""
     import torch
     from geomesa_amd import _lib
     from geomesa_amd.join import PolygonIndex, synthetic_counties, synthetic_points
@@ -136,10 +136,15 @@ def test_corrupt_reference_reports_instead_of_faulting(gpu):
     cw[cells] = torch.tensor(bad_word - (1 << 32) if bad_word >= 1 << 31 else bad_word, dtype=torch.int32,
                              device=cw.device)
     bad = PolygonIndex.from_arrays(lay, arrs, polyset=ps)
-    for mode in ("direct", "split", "partitioned"):
+    from geomesa_amd.filters import query_scan
+    calls = {"join": lambda: bad.join(px, py),
+             "join count": lambda: bad.join(px, py, count_only=True),
+             "relate": lambda: bad.relate(np.zeros(len(px), np.int32), px, py),
+             "query": lambda: query_scan(px, py, geoms=bad, op="intersects")}
+    for name, call in calls.items():
         with pytest.raises(_lib.GeomesaHipError) as ei:
-            bad.join(px, py, mode=mode)
-        assert "reference check" in str(ei.value), mode
+            call()
+        assert "reference check" in str(ei.value), name
     # the healthy index on the same context is unaffected
     pt, pl = good.join(px, py)
     pt2, pl2 = PolygonIndex.from_arrays(*good.export_arrays(), polyset=ps).join(px, py)

@@ -40,12 +40,22 @@ def rows(ps, n, seed):
     return poly, px, py
 
 
-@pytest.mark.parametrize("cells", [0, 64])
-def test_relate_rows_match_oracle(gpu, oracle, cells):
+@pytest.mark.parametrize("cells,core", [(0, 1), (64, 1), (0, 0)])
+def test_relate_rows_match_oracle(gpu, oracle, cells, core):
+    """core 0: the index is built without the per-polygon core rectangles (GM_PARAM_INDEX_CORE), so
+    every row takes the coarse / fine lookup chain."""
+    from geomesa_amd import _lib
     from geomesa_amd.join import PolygonIndex, synthetic_counties
     ps = synthetic_counties(NX, NY)
     poly, px, py = rows(ps, 60_000, seed=3 + cells)
-    loc = as_np(PolygonIndex(ps, cells_per_poly=cells).relate(poly, px, py))
+    ctx = _lib.context()
+    try:
+        ctx.set_param(_lib.GM_PARAM_INDEX_CORE, core)
+        ix = PolygonIndex(ps, cells_per_poly=cells)
+    finally:
+        ctx.set_param(_lib.GM_PARAM_INDEX_CORE, 1)
+    assert (ix.core_rects() is not None and len(ix.core_rects()) > 0) == bool(core)
+    loc = as_np(ix.relate(poly, px, py))
     ops = oracle.OraclePolySet(*ps.to_arrays())
     exp = np.array([255 if p < 0 else ops.locate(int(p), x, y) for p, x, y in zip(poly, px, py)], np.uint8)
     assert np.array_equal(loc, exp), np.flatnonzero(loc != exp)[:10]
@@ -91,11 +101,11 @@ def test_relate_box_kats(gpu):
     assert as_np(null).tolist() == [False] * 6 + [True]
 
 
-@pytest.mark.parametrize("mode", ["auto", "split", "partitioned"])
+@pytest.mark.parametrize("mode", ["auto", "direct"])
 def test_st_covers_box_kats(gpu, mode):
     """SpatialRelationFunctionsTest.scala:113-139: st_covers(POLYGON((0 0,0 10,10 10,10 0,0 0)), p) is true
     for POINT(5 5), POINT(0 5) (edge) and POINT(0 0) (corner), false for POINT(-5 0) -- as the join
-    condition (every strategy) and row by row."""
+    condition and row by row."""
     from geomesa_amd.join import PolygonIndex, PolygonSet
     ps = PolygonSet.from_polygons([[[[(0, 0), (0, 10), (10, 10), (10, 0), (0, 0)]]]])
     ix = PolygonIndex(ps)
@@ -130,7 +140,7 @@ def oracle_pairs(oracle, ps, px, py, pred):
     return out
 
 
-@pytest.mark.parametrize("mode", ["auto", "split", "partitioned"])
+@pytest.mark.parametrize("mode", ["auto", "direct"])
 @pytest.mark.parametrize("pred", ["st_intersects", "st_contains"])
 def test_join_predicates_with_boundary_points(gpu, oracle, mode, pred):
     """The join condition's UDF (GeoMesaJoinRelation.scala:67-79): st_intersects keeps the points on

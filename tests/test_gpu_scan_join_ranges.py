@@ -217,13 +217,12 @@ def test_pip_join_synthetic_counties(gpu, oracle, grid, cells_per_poly):
     import oracle as O
     opt, opl = O.OraclePolySet(*ps.to_arrays()).join(px, py, nthreads=8)
     exp = np.stack([opt, opl.astype(np.int64)], 1)
-    for mode in ("direct", "partitioned", "split"):
-        pt, pl = ix.join(px, py, mode=mode)
-        assert np.array_equal(_sorted_pairs(pt, pl), exp), mode
-        assert ix.join(px, py, count_only=True, mode=mode) == len(exp)
-        # capacity path
-        pt2, pl2 = ix.join(px, py, cap=10, mode=mode)
-        assert len(pt2) == len(exp)
+    pt, pl = ix.join(px, py)
+    assert np.array_equal(_sorted_pairs(pt, pl), exp)
+    assert ix.join(px, py, count_only=True) == len(exp)
+    # capacity path
+    pt2, pl2 = ix.join(px, py, cap=10)
+    assert len(pt2) == len(exp)
 
 
 def _sorted_pairs(pt, pl):
@@ -231,8 +230,8 @@ def _sorted_pairs(pt, pl):
     return got[np.lexsort((got[:, 1], got[:, 0]))]
 
 
-def test_pip_join_partitioned_edges(gpu, oracle):
-    """Row-band partition: NaN / off-grid points are dropped, id_base offsets ids, empty input."""
+def test_pip_join_edges(gpu, oracle):
+    """NaN / infinite / off-grid points never match, id_base offsets ids, empty and one-point input."""
     from geomesa_amd.join import PolygonIndex, synthetic_counties, synthetic_points
     ps = synthetic_counties(20, 10)
     ix = PolygonIndex(ps)
@@ -243,15 +242,34 @@ def test_pip_join_partitioned_edges(gpu, oracle):
     import oracle as O
     opt, opl = O.OraclePolySet(*ps.to_arrays()).join(px, py, nthreads=8)
     exp = np.stack([opt + 1000, opl.astype(np.int64)], 1)
-    for mode in ("direct", "partitioned", "split"):
-        pt, pl = ix.join(px, py, id_base=1000, mode=mode)
-        assert np.array_equal(_sorted_pairs(pt, pl), exp), mode
-        assert ix.join(px[:0], py[:0], mode=mode)[0].numel() == 0
-        assert ix.join(px[:1], py[:1], count_only=True, mode=mode) == int((opt == 0).sum())
+    pt, pl = ix.join(px, py, id_base=1000)
+    assert np.array_equal(_sorted_pairs(pt, pl), exp)
+    assert ix.join(px[:0], py[:0])[0].numel() == 0
+    assert ix.join(px[:1], py[:1], count_only=True) == int((opt == 0).sum())
+
+
+def test_pip_join_unknown_mode_rejected(gpu):
+    """Only GM_JOIN_AUTO / GM_JOIN_DIRECT exist (the band-partitioned and two-pass strategies were
+    removed); any other mode is GM_E_INVALID through the C ABI, for columns and Arrow input alike."""
+    import ctypes
+    import torch
+    from geomesa_amd import _lib
+    from geomesa_amd.join import PolygonIndex, synthetic_counties
+    ix = PolygonIndex(synthetic_counties(4, 2))
+    x = torch.full((16,), -100.0, dtype=torch.float64, device="cuda")
+    npairs = ctypes.c_int64(-1)
+    for mode in (2, 3, -1):
+        rc = ix.ctx.lib.gm_pip_join_ex(ix.ctx.handle, ix._h, ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(x.data_ptr()),
+                                       16, 0, None, None, 0, ctypes.byref(npairs), mode)
+        assert rc == _lib.GM_E_INVALID, mode
+    for mode in (_lib.GM_JOIN_AUTO, _lib.GM_JOIN_DIRECT):
+        rc = ix.ctx.lib.gm_pip_join_ex(ix.ctx.handle, ix._h, ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(x.data_ptr()),
+                                       16, 0, None, None, 0, ctypes.byref(npairs), mode)
+        assert rc == _lib.GM_OK and npairs.value == 0
 
 
 def test_pip_join_auto_large(gpu, oracle):
-    """5M points x 3,200 polygons: auto (= direct at every size) and split equal the oracle."""
+    """5M points x 3,200 polygons: auto and direct (the same staged pass) equal the oracle."""
     from geomesa_amd.join import PolygonIndex, synthetic_counties, synthetic_points
     ps = synthetic_counties(80, 40)
     ix = PolygonIndex(ps)
@@ -262,9 +280,8 @@ def test_pip_join_auto_large(gpu, oracle):
     pt, pl = ix.join(px, py)
     assert np.array_equal(_sorted_pairs(pt, pl), exp)
     assert ix.join(px, py, count_only=True, mode="direct") == len(exp)
-    pt, pl = ix.join(px, py, mode="split")
+    pt, pl = ix.join(px, py, mode="direct", predicate="st_within")
     assert np.array_equal(_sorted_pairs(pt, pl), exp)
-    assert ix.join(px, py, count_only=True, mode="split") == len(exp)
 
 
 # ---------------------------------------------------------------- batched ranges

@@ -50,9 +50,8 @@ def test_join_at_shortcut_thresholds(gpu, oracle, grid, cells, predicate):
     exp = np.stack([opt, opl.astype(np.int64)], 1)
     exp = exp[np.lexsort((exp[:, 1], exp[:, 0]))]
     ix = PolygonIndex(ps, cells_per_poly=cells)
-    for mode in ("direct", "partitioned", "split"):
-        pt, pl = ix.join(px, py, mode=mode, predicate=predicate)
-        assert np.array_equal(_sorted_pairs(pt, pl), exp), (mode, len(exp))
+    pt, pl = ix.join(px, py, predicate=predicate)
+    assert np.array_equal(_sorted_pairs(pt, pl), exp), len(exp)
 
 
 def test_relate_at_shortcut_thresholds(gpu, oracle):
@@ -75,13 +74,14 @@ def test_relate_at_shortcut_thresholds(gpu, oracle):
     assert (exp == 1).sum() > 0 and (exp == 2).sum() > 0 and (exp == 0).sum() > 0
 
 
-@pytest.mark.parametrize("fmt", ["0", "1"])
-def test_join_coarse_mask_formats(gpu, oracle, fmt, monkeypatch):
-    """Both layouts of the join's coarse sub-block masks (gm_pip.hip coarse_mask): EMPTY bits of 16
+@pytest.mark.parametrize("fmt", [0, 1])
+def test_join_coarse_mask_formats(gpu, oracle, fmt):
+    """Both layouts of the join's coarse sub-block masks (gm_pip.hpp coarse_mask): EMPTY bits of 16
     sub-blocks (any polygon count) and EMPTY / INTERIOR(main) bits of 8 (fewer than 2^14 polygons),
-    forced through GM_PIP_COARSE_FMT at index build, against the oracle on random and boundary points."""
+    forced through GM_PARAM_INDEX_COARSE at index build, against the oracle on random and boundary
+    points, for the join and the row predicate."""
+    from geomesa_amd import _lib
     from geomesa_amd.join import PolygonIndex, synthetic_counties, synthetic_points
-    monkeypatch.setenv("GM_PIP_COARSE_FMT", fmt)
     ps = synthetic_counties(20, 10)
     px, py = synthetic_points(300_000, seed=9)
     tx, ty = threshold_points(ps, stride=5)
@@ -89,10 +89,21 @@ def test_join_coarse_mask_formats(gpu, oracle, fmt, monkeypatch):
     opt, opl = oracle.OraclePolySet(*ps.to_arrays()).join(px, py, nthreads=16)
     exp = np.stack([opt, opl.astype(np.int64)], 1)
     exp = exp[np.lexsort((exp[:, 1], exp[:, 0]))]
-    ix = PolygonIndex(ps)
-    for mode in ("direct", "partitioned"):
-        pt, pl = ix.join(px, py, mode=mode)
-        assert np.array_equal(_sorted_pairs(pt, pl), exp), (fmt, mode)
+    ctx = _lib.context()
+    try:
+        ctx.set_param(_lib.GM_PARAM_INDEX_COARSE, fmt)
+        ix = PolygonIndex(ps)
+    finally:
+        ctx.set_param(_lib.GM_PARAM_INDEX_COARSE, -1)
+    pt, pl = ix.join(px, py)
+    assert np.array_equal(_sorted_pairs(pt, pl), exp), fmt
+    # the row predicate over the same index: each point against the polygon the oracle pairs it with
+    # (INTERIOR) and against polygon 0 (mostly EXTERIOR)
+    ops = oracle.OraclePolySet(*ps.to_arrays())
+    rows = np.concatenate([exp[:2000, 1], np.zeros(2000, np.int64)]).astype(np.int32)
+    rx = np.concatenate([px[exp[:2000, 0]], px[:2000]]); ry = np.concatenate([py[exp[:2000, 0]], py[:2000]])
+    loc = as_np(ix.relate(rows, rx, ry))
+    assert np.array_equal(loc, np.array([ops.locate(int(p), x, y) for p, x, y in zip(rows, rx, ry)], np.uint8))
 
 
 def test_join_census_accounts_for_every_point(gpu):

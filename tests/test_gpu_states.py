@@ -1,8 +1,8 @@
 """The join on real polygons: the reference's US-state shapefile fixture (52 records, 132 rings,
 13,832 vertices; geomesa-convert-shp/src/test/resources/us_state/cb_2017_us_state_20m.shp, read by
-tests/shapefile.py), against the oracle in every join strategy and for both join predicates
-(SpatialRelationFunctions.scala:29 st_contains, :34 st_intersects), plus join passes forced across
-chunk boundaries (GM_PARAM_JOIN_CHUNK) in every strategy."""
+tests/shapefile.py), against the oracle for both join predicates (SpatialRelationFunctions.scala:29
+st_contains, :34 st_intersects), plus join passes forced across chunk boundaries (GM_PARAM_JOIN_CHUNK,
+even and odd chunk sizes)."""
 import numpy as np
 import pytest
 
@@ -11,7 +11,6 @@ from test_gpu_scan_join_ranges import _sorted_pairs, as_np
 
 pytestmark = pytest.mark.gpu
 
-MODES = ("direct", "partitioned", "split")
 
 
 @pytest.fixture(scope="module")
@@ -46,9 +45,8 @@ def test_states_join_parity(gpu, oracle, states, predicate):
     exp = np.stack([opt, opl.astype(np.int64)], 1)
     exp = exp[np.lexsort((exp[:, 1], exp[:, 0]))]
     ix = PolygonIndex(ps)
-    for mode in MODES:
-        pt, pl = ix.join(px, py, mode=mode, predicate=predicate)
-        assert np.array_equal(_sorted_pairs(pt, pl), exp), (mode, predicate)
+    pt, pl = ix.join(px, py, predicate=predicate)
+    assert np.array_equal(_sorted_pairs(pt, pl), exp), predicate
     # a vertex point lies on its own state's boundary: never contained by it; on shared borders it
     # intersects two states
     n0 = len(px) - (3 * ps.n_vertices - 1)   # first vertex point (after n random points)
@@ -77,11 +75,12 @@ def test_states_city_kats_gpu(gpu, states):
     assert got == {k: k for k in names}
 
 
-@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("chunk", [400_000, 399_999, 131_071])
 @pytest.mark.parametrize("fixture", ["states", "counties"])
-def test_join_across_chunks(gpu, oracle, states, mode, fixture):
+def test_join_across_chunks(gpu, oracle, states, chunk, fixture):
     """GM_PARAM_JOIN_CHUNK forces >= 3 passes: per-pass id offsets, pair counters carried across
-    passes, split-mode segments reused pass after pass, and the capacity path."""
+    passes, and the capacity path.  Odd chunk sizes are rounded down to even, so every chunk of the
+    16-B aligned columns keeps the 16-B pair loads aligned."""
     from geomesa_amd import _lib
     from geomesa_amd.join import PolygonIndex, synthetic_counties, synthetic_points
     if fixture == "states":
@@ -96,15 +95,17 @@ def test_join_across_chunks(gpu, oracle, states, mode, fixture):
     exp = exp[np.lexsort((exp[:, 1], exp[:, 0]))]
     ix = PolygonIndex(ps)
     ctx = ix.ctx
-    chunk = 400_000
     assert (n + chunk - 1) // chunk >= 3
     try:
         ctx.set_param(_lib.GM_PARAM_JOIN_CHUNK, chunk)
         assert ctx.get_param(_lib.GM_PARAM_JOIN_CHUNK) == chunk
-        pt, pl = ix.join(px, py, id_base=77, mode=mode)
+        pt, pl = ix.join(px, py, id_base=77)
         assert np.array_equal(_sorted_pairs(pt, pl), exp)
-        assert ix.join(px, py, id_base=77, mode=mode, count_only=True) == len(exp)
-        pt2, _ = ix.join(px, py, id_base=77, mode=mode, cap=100)   # GM_E_CAPACITY, then the retry
+        assert ix.join(px, py, id_base=77, count_only=True) == len(exp)
+        pt2, _ = ix.join(px, py, id_base=77, cap=100)   # GM_E_CAPACITY, then the retry
         assert len(pt2) == len(exp)
+        # an unaligned column view (scalar loads) across the same chunks
+        pt3, pl3 = ix.join(px[1:], py[1:], id_base=78)
+        assert np.array_equal(_sorted_pairs(pt3, pl3), exp[exp[:, 0] >= 78])
     finally:
         ctx.set_param(_lib.GM_PARAM_JOIN_CHUNK, 0)

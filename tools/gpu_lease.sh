@@ -1,0 +1,98 @@
+#!/bin/bash
+# One GPU lease, parameterised: runs the named steps in order, each under its own time limit, and
+# stops at the first failure (set -e).  Output goes to gpurun_out/<TAG>_*.
+#
+#   bash tools/gpu_lease.sh TAG STEP [STEP ...]
+#
+# steps:
+#   tests[:K]        pytest -m gpu (only tests matching -k K when given)
+#   smoke            __graft_entry__.smoke()
+#   bench            the default bench line (stdout json + detail)
+#   prof             rocprofv3 --kernel-trace --stats of the bench, then the FETCH_SIZE / WRITE_SIZE /
+#                    FP64 passes (one counter group per run) -> make_traffic.py input
+#   pmc:LEG          the counter groups below over one leg (join | table | ranges | hist | z3)
+#   ab:LEG:LIBS      alternating runs of one leg over variant libraries (geomesa_amd/lib/<lib>.so,
+#                    comma-separated; "prod" = the product library), 3 rounds
+#   probe:NAME       python tools/NAME.py (ranges_probe, hist_probe, sort_probe, query_probe, ...)
+set -e
+tag=$1; shift
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out
+out=gpurun_out/$tag
+
+leg_args() {   # the bench arguments of one leg
+  case $1 in
+    join) echo "--only join --no-cpu --no-gather --steps 1 --warmup 0 --join-steps 3" ;;
+    table) echo "--only table --no-cpu --steps 2 --warmup 1" ;;
+    z3) echo "--only z3 --no-cpu --steps 10 --warmup 2" ;;
+    extra) echo "--only extra --no-cpu --steps 6 --warmup 1" ;;
+    *) echo "--no-cpu" ;;
+  esac
+}
+
+for step in "$@"; do
+  name=${step%%:*}; arg=${step#*:}; [ "$arg" = "$step" ] && arg=""
+  echo "[$(date +%T)] $step" >> ${out}_steps.log
+  case $name in
+    tests)
+      k=${arg:+-k $arg}
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v $k --timeout 300 --timeout-method thread \
+        > ${out}_tests.log 2>&1 ;;
+    smoke)
+      timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > ${out}_smoke.log 2>&1 ;;
+    bench)
+      timeout -k 10 600 python -u bench.py > ${out}_bench.json 2> ${out}_bench.err
+      cp gpurun_out/bench_detail_n1.json ${out}_bench_detail.json ;;
+    prof)
+      timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d ${out}_prof -o run -- \
+        python3 bench.py --steps 10 --join-steps 3 --no-cpu > ${out}_prof_bench.json 2> ${out}_prof.err
+      i=0
+      for g in FETCH_SIZE WRITE_SIZE; do
+        timeout -s KILL 200 rocprofv3 --kernel-trace --output-format csv --pmc $g -d ${out}_pmc/p$i -o run -- \
+          python3 bench.py --only z3,extra,table --no-cpu --steps 2 --warmup 1 > ${out}_pmc$i.log 2>&1
+        i=$((i+1))
+      done
+      for g in FETCH_SIZE WRITE_SIZE SQ_INSTS_VALU_FLOPS_FP64; do
+        timeout -s KILL 200 rocprofv3 --kernel-trace --output-format csv --pmc $g -d ${out}_pmc/p$i -o run -- \
+          python3 bench.py --only join --no-cpu --steps 1 --warmup 0 --join-steps 1 > ${out}_pmc$i.log 2>&1
+        i=$((i+1))
+      done ;;
+    pmc)
+      groups=(
+        "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE"
+        "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS"
+        "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_SCA SQ_INST_LEVEL_VMEM"
+        "TA_TA_BUSY_sum TA_FLAT_READ_WAVEFRONTS_sum TD_TD_BUSY_sum TD_TC_STALL_sum"
+        "TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCP_TCC_READ_REQ_LATENCY_sum TCP_PENDING_STALL_CYCLES_sum"
+        "TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum"
+        "FETCH_SIZE"
+        "WRITE_SIZE"
+      )
+      if [ -n "$PMC_GROUPS" ]; then IFS=";" read -ra groups <<< "$PMC_GROUPS"; fi
+      cmd="python3 bench.py $(leg_args $arg)"
+      [ "$arg" = ranges ] && cmd="python3 tools/ranges_probe.py 100000"
+      [ "$arg" = hist ] && cmd="python3 tools/hist_probe.py"
+      mkdir -p ${out}_pmc_$arg
+      i=0
+      for g in "${groups[@]}"; do
+        timeout -s KILL 150 rocprofv3 --kernel-trace --output-format csv --pmc $g -d ${out}_pmc_$arg/p$i -o run -- \
+          $cmd > ${out}_pmc_$arg/p$i.log 2>&1 || { echo "pass $i ($g) failed: $?" >> ${out}_pmc_$arg/failed.txt; exit 1; }
+        i=$((i+1))
+      done ;;
+    ab)
+      leg=${arg%%:*}; libs=${arg#*:}
+      for r in 1 2 3; do
+        for lib in ${libs//,/ }; do
+          if [ "$lib" = prod ]; then unset GEOMESA_HIP_LIB; else export GEOMESA_HIP_LIB=$PWD/geomesa_amd/lib/$lib.so; fi
+          timeout -k 10 300 python -u bench.py $(leg_args $leg) > ${out}_ab_${lib}_$r.json 2> ${out}_ab_${lib}_$r.err
+          cp gpurun_out/bench_detail_n1.json ${out}_ab_${lib}_$r.detail.json
+        done
+      done
+      unset GEOMESA_HIP_LIB
+      python3 tools/show_ab.py ${out}_ab > ${out}_ab.txt ;;
+    probe)
+      timeout -k 10 400 python -u tools/$arg.py > ${out}_$arg.txt 2>&1 ;;
+    *)
+      echo "unknown step $step" >&2; exit 2 ;;
+  esac
+done
