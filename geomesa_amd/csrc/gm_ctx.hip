@@ -196,6 +196,23 @@ __global__ __launch_bounds__(256) void k_gen_points(uint64_t seed, int64_t n, in
 
 }  // namespace gm
 
+namespace gm {
+int take_fault(gm_ctx* c, const char* what) {
+  int64_t bits = 0;
+  GM_HIP(hipMemcpyAsync(c->h_pinned + 63, c->d_scratch + SCRATCH_FAULT, 8, hipMemcpyDeviceToHost, c->stream));
+  GM_HIP(hipStreamSynchronize(c->stream));
+  bits = c->h_pinned[63];
+  if (!bits) return GM_OK;
+  GM_HIP(hipMemsetAsync(c->d_scratch + SCRATCH_FAULT, 0, 8, c->stream));
+  char msg[200];
+  snprintf(msg, sizeof msg, "%s: device reference check failed (PIP_FAULT bits 0x%x): corrupt index or internal "
+           "queue invariant", what, (unsigned)bits);
+  set_error(msg);
+  return GM_E_INDEX;
+}
+}  // namespace gm
+
+
 extern "C" {
 
 int gm_abi_version(void) { return GM_ABI_VERSION; }
@@ -223,6 +240,7 @@ static int ctx_create(int device, void* stream, bool own, gm_ctx** out) {
   }
   hipError_t e = hipMalloc(&c->d_err, 4 * sizeof(int64_t));
   if (e == hipSuccess) e = hipMalloc(&c->d_scratch, 64 * sizeof(int64_t));
+  if (e == hipSuccess) e = hipMemset(c->d_scratch, 0, 64 * sizeof(int64_t));
   if (e == hipSuccess) e = hipHostMalloc(&c->h_pinned, 64 * sizeof(int64_t), hipHostMallocDefault);
   if (e == hipSuccess) e = hipEventCreate(&c->ev0);
   if (e == hipSuccess) e = hipEventCreate(&c->ev1);
@@ -269,7 +287,7 @@ int gm_ctx_destroy(gm_ctx* c) {
 int gm_ctx_sync(gm_ctx* c) {
   if (!c) return GM_E_INVALID;
   GM_HIP(hipStreamSynchronize(c->stream));
-  return GM_OK;
+  return gm::take_fault(c, "gm_ctx_sync");
 }
 
 void* gm_ctx_stream(gm_ctx* c) { return c ? (void*)c->stream : nullptr; }

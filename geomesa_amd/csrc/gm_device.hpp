@@ -350,4 +350,15 @@ __device__ __forceinline__ int jts_orientation(double p1x, double p1y, double p2
   return jts_orientation_dd(p1x, p1y, p2x, p2y, qx, qy);
 }
 
+// wave compaction helpers: the number of set bits of a ballot below this lane, and a wave-scope
+// ordering point for LDS written by other lanes of the same wave
+__device__ __forceinline__ int lanes_below(uint64_t m) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
 }  // namespace gm

@@ -69,6 +69,12 @@ bool host_pinned(const void* p);
 bool device_memory(const void* p);   // device (hipMalloc) memory, as opposed to host memory
 int ctx_copy_stream(gm_ctx* ctx);   // creates copy_stream and its events on first use
 
+// The context's sticky reference-fault word (d_scratch[SCRATCH_FAULT]): the polygon-index kernels OR
+// PIP_FAULT_* bits into it, stream-ordered; take_fault (a synchronising call: a join that returns its
+// pair count, a query scan, gm_ctx_sync) reads and clears it and returns GM_E_INDEX when set.
+constexpr int SCRATCH_FAULT = 63;
+int take_fault(gm_ctx* ctx, const char* what);
+
 // reset the error summary before a call that reports one
 int begin_summary(gm_ctx* ctx, gm_batch_status* summary);
 // read the summary back (synchronises the stream); maps to GM_OK / per-element semantics

@@ -62,6 +62,7 @@ struct PipDev {
   const uint32_t* coarse_sc;     // the join's coarse words over cell_sc; LIST words carry sub-block masks
   int32_t coarse_fmt;            // COARSE_EMPTY_MASK / COARSE_MAIN (see coarse_mask)
   const uint4* line_ent;         // line shortcuts, two uint4 each (see "Boundary shortcuts")
+  const uint2* cell_sc8;         // the join's 8-B fine words: cell_sc, with one-line LINE words inline (sc8_*)
   double gx0, gy0, gx1, gy1, inv_cw, inv_ch;
   int32_t gx, gy, gxc;
   int32_t op;                    // join predicate: JOIN_CONTAINS (interior) or JOIN_INTERSECTS (not exterior)
@@ -329,6 +330,35 @@ __device__ __forceinline__ int line_locate(const uint4 e0, const uint4 e1, doubl
   return ((fl >> (2 * r + 1)) & 1u) ? LOC_INTERIOR : LOC_EXTERIOR;
 }
 
+// The join's 8-B fine words (cell_sc8, derived from cell_sc and line_ent by make_shortcut).  A
+// beyond-L2 gather costs the same for 4 or 16 B per lane (tools/gather_probe.hip: 56-59 G/s either
+// way), so a LINE cell whose entry holds ONE line carries that line in its fine word and its points
+// decide with one gather instead of two (fine word, then the 32-B entry):
+//   tag (bits 63-62) 0: the low half is the cell_sc word (high half 0);
+//   tag 1: bits 61-48 polygon (< 2^14), 47-44 region flags as in the entry (2r located, 2r + 1
+//          interior; r = 0 where f > 0), 43-30 A, 29-16 B (int14), 15-0 C (int16):
+//          f(u, v) = A u + B v - C in units of 2^-12 cell, the entry's line requantized (A / 4 ...).
+// The entry's line is within SC_DEV / 4 = 1 unit of the exact line over the cell and the
+// requantization adds <= 1.52, so a point with |f| > SC8_T is on the exact line's side sign(f) and
+// takes that region's location; a nearer point takes the original word's blob (cell_word), as the
+// entry's near-line points do.
+constexpr double SC8_T = 4.0;
+__device__ __forceinline__ bool sc8_inline(uint2 w) { return (w.y >> 30) == 1u; }
+__device__ __forceinline__ int sc8_poly(uint2 w) { return (int)((w.y >> 16) & 0x3fffu); }
+// LOC_INTERIOR / LOC_EXTERIOR from an inline line, or -1 (near the line, or an unlocated region)
+__device__ __forceinline__ int sc8_locate(uint2 w, double x, double y, const PipDev& d, int cx, int cy) {
+  const uint64_t v = ((uint64_t)w.y << 32) | w.x;
+  const double A = (double)((int64_t)(v << 20) >> 50), B = (double)((int64_t)(v << 34) >> 50);
+  const double C = (double)((int64_t)(v << 48) >> 48);
+  const double u = __dsub_rn(__dmul_rn(__dsub_rn(x, d.gx0), d.inv_cw), (double)cx);
+  const double t = __dsub_rn(__dmul_rn(__dsub_rn(y, d.gy0), d.inv_ch), (double)cy);
+  const double f = __dsub_rn(__dadd_rn(__dmul_rn(A, u), __dmul_rn(B, t)), C);
+  if (!(f > SC8_T || f < -SC8_T)) return -1;
+  const uint32_t fl = (uint32_t)(v >> 44) & 15u, r = f > SC8_T ? 0u : 1u;
+  if (!((fl >> (2 * r)) & 1u)) return -1;
+  return ((fl >> (2 * r + 1)) & 1u) ? LOC_INTERIOR : LOC_EXTERIOR;
+}
+
 // The join's coarse table (coarse_sc, 4 B per coarse cell like coarse_word, so it stays L2-resident)
 // is built over cell_sc: EMPTY / INTERIOR(p) when all its fine cells carry that word, else LIST with
 // bit s of the payload set when all fine cells of sub-block s (4 x 4 sub-blocks of 2 x 2 fine
@@ -377,15 +407,6 @@ __device__ __forceinline__ int item_locate(const PipDev& d, uint32_t ref, double
   poly = h.x;
   return blob_locate(d, b, h, x, y);
 }
-__device__ __forceinline__ int lanes_below(uint64_t m) {
-  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-}
-
-__device__ __forceinline__ void wave_lds_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-}
-
 // ------------------------------------------------------------------ kernel LDS budgets
 // The staged join (gm_pip_join.hip): one 1024-thread block per CU, per wave a fine queue and an item
 // queue; what the queues leave of the 160 KiB holds the coarse EMPTY bitmap, whose block size the
@@ -394,15 +415,11 @@ __device__ __forceinline__ void wave_lds_sync() {
 #define GM_JQ_TPB 1024
 #endif
 constexpr int QTPB = GM_JQ_TPB;
-#ifndef GM_JQ_FBATCH
-#define GM_JQ_FBATCH 64
-#endif
-constexpr int FBATCH = GM_JQ_FBATCH;   // fine words per round (64: 1 per lane, 128: 2 per lane)
+constexpr int FBATCH = 64;              // fine words per round: one per lane, kept in registers
 constexpr int FCAP = FBATCH + 128;     // fine queue (< FBATCH + one step's 128)
 constexpr int ICAP = 128;              // item queue (two ends)
-// per wave: the fine queue (x, y, row; plus each point's fine word when a round resolves two halves)
-// and the item queue (x, y, row, reference)
-constexpr int JQ_WAVE_LDS = FCAP * (FBATCH > 64 ? 24 : 20) + ICAP * 24;
+// per wave: the fine queue (x, y, row) and the item queue (x, y, row, reference)
+constexpr int JQ_WAVE_LDS = FCAP * 20 + ICAP * 24;
 constexpr int CM_WORDS_MAX = (163840 - (QTPB / 64) * JQ_WAVE_LDS - 256) / 4;   // 13,248 words at 1024 threads
 
 // The row predicate (gm_pip_relate.hip): its own, coarser bitmap (16 KiB) and a core rectangle per
@@ -416,16 +433,6 @@ constexpr int RELATE_CM_WORDS = 4032;
 #define GM_RELATE_CORE_MAX 4096
 #endif
 constexpr int RELATE_CORE_MAX = GM_RELATE_CORE_MAX;
-
-// a reference check of a join-family kernel failed on the device (PIP_FAULT_* bits): nothing of the
-// call's output is trusted
-inline int index_fault(const char* what, uint32_t bits) {
-  char msg[160];
-  snprintf(msg, sizeof msg, "%s: device reference check failed (PIP_FAULT bits 0x%x): corrupt index or internal "
-           "queue invariant", what, bits);
-  set_error(msg);
-  return GM_E_INDEX;
-}
 
 }  // namespace gm
 

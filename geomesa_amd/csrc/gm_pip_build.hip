@@ -887,6 +887,45 @@ __global__ __launch_bounds__(256) void k_build_shortcut(PipDev d, int64_t ncell,
   }
 }
 
+// cell_sc8 (gm_pip.hpp, "8-B fine words"): cell_sc zero-extended, and a LINE word whose entry holds one
+// line of a polygon below 2^14 replaced by that line requantized to 2^-12 cell (A / 4, B / 4, C / 4),
+// when the requantization keeps the deviation from the exact line (entry deviation SC_DEV / 4 plus
+// the rounding, over the enlarged cell) a unit below SC8_T
+__global__ __launch_bounds__(256) void k_build_sc8(const uint32_t* __restrict__ cell_sc, const uint4* __restrict__ line_ent,
+                                                   int64_t n_line, int64_t ncell, uint2* __restrict__ out) {
+  for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < ncell; c += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t w = cell_sc[c];
+    uint2 o = make_uint2(w, 0u);
+#ifdef GM_SC8_NOINLINE   // tuning build: every fine word without its inline line (A/B of the inline lines)
+    if (false &&
+#else
+    if (
+#endif
+        line_ent && (w >> 30) == CELL_BOUNDARY && (w & (BLOB_COMPACT | SC_LINE)) == (BLOB_COMPACT | SC_LINE) &&
+        (uint64_t)(w & (SC_LINE - 1)) < (uint64_t)n_line) {
+      const uint64_t li = w & (SC_LINE - 1);
+      const uint4 e0 = line_ent[2 * li], e1 = line_ent[2 * li + 1];
+      if ((e1.y >> 24) == 1u && e0.y < (1u << 14)) {
+        const double A = (double)(int16_t)(e0.z & 0xffffu) / 4.0, B = (double)(int16_t)(e0.z >> 16) / 4.0;
+        const double C = (double)((int32_t)(e0.w << 8) >> 8) / 4.0;
+        const double a = rint(A), b = rint(B), cc = rint(C);
+        double dev = 0.0;
+        for (int q = 0; q < 4; ++q) {
+          const double uc = (q & 1) ? 1.01 : -0.01, vc = (q & 2) ? 1.01 : -0.01;
+          dev = fmax(dev, fabs((a - A) * uc + (b - B) * vc - (cc - C)));
+        }
+        if (dev + SC_DEV / 4.0 <= SC8_T - 1.0 && fabs(a) <= 8191.0 && fabs(b) <= 8191.0 && fabs(cc) <= 32767.0) {
+          const uint64_t v = (1ull << 62) | ((uint64_t)e0.y << 48) | ((uint64_t)((e0.w >> 24) & 15u) << 44) |
+                             (((uint64_t)(int64_t)a & 0x3fffu) << 30) | (((uint64_t)(int64_t)b & 0x3fffu) << 16) |
+                             ((uint64_t)(int64_t)cc & 0xffffu);
+          o = make_uint2((uint32_t)v, (uint32_t)(v >> 32));
+        }
+      }
+    }
+    out[c] = o;
+  }
+}
+
 __global__ void k_build_max(const int32_t* __restrict__ v, int64_t n, int* __restrict__ out) {
   int m = 0;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
@@ -959,6 +998,13 @@ int make_shortcut(gm_pip_index* ix) {
   GM_HIP(hipMalloc(&p, (size_t)std::max<int64_t>(ncell, 1) * 4));
   ix->allocs.push_back(p);
   ix->dev.cell_sc = (const uint32_t*)p;
+  {   // the join's 8-B fine words (k_build_sc8, after the line entries)
+    void* p8 = nullptr;
+    GM_HIP(hipMalloc(&p8, (size_t)std::max<int64_t>(ncell, 1) * 8));
+    ix->allocs.push_back(p8);
+    ix->dev.cell_sc8 = (const uint2*)p8;
+    if (ncell == 0) GM_HIP(hipMemsetD32Async((hipDeviceptr_t)p8, CELL_EMPTY << 30, 2, s));
+  }
   ix->dev.line_ent = nullptr;
   ix->n_lines = 0;
   ix->dev.fault = nullptr;   // set per call (the call's scratch word)
@@ -1010,6 +1056,8 @@ int make_shortcut(gm_pip_index* ix) {
                        (const int64_t*)sl, (uint4*)e);
   }
   if (!rc) {
+    hipLaunchKernelGGL(k_build_sc8, dim3(g), dim3(256), 0, s, (const uint32_t*)p, ix->dev.line_ent, ix->dev.n_line, ncell,
+                       (uint2*)ix->dev.cell_sc8);
     const int gxc = ix->dev.gxc, gyc = (ix->dev.gy + (1 << CF_LOG) - 1) >> CF_LOG;
     hipLaunchKernelGGL(k_build_coarse_sc, dim3((unsigned)std::min<int64_t>(65536, ((int64_t)gxc * gyc + 255) / 256)), dim3(256),
                        0, s, (const uint32_t*)p, ix->dev.gx, ix->dev.gy, gxc, gyc, ix->dev.coarse_fmt,

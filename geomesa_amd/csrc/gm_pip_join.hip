@@ -205,7 +205,7 @@ __global__ __launch_bounds__(QTPB) void k_pip_join_q(const double* __restrict__ 
                                                      int64_t desc_base, ArrowPts ap) {
   constexpr int NW = QTPB / 64;
   __shared__ double s_fx[NW][FCAP], s_fy[NW][FCAP];
-  __shared__ uint32_t s_fid[NW][FCAP], s_fw[NW][FBATCH > 64 ? FCAP : 1];   // one half per round: its words stay in registers
+  __shared__ uint32_t s_fid[NW][FCAP];
   __shared__ double s_ix[NW][ICAP], s_iy[NW][ICAP];
   __shared__ uint32_t s_iid[NW][ICAP], s_iref[NW][ICAP];
   __shared__ uint32_t s_cm[CM_WORDS_MAX];
@@ -278,18 +278,18 @@ __global__ __launch_bounds__(QTPB) void k_pip_join_q(const double* __restrict__ 
   load_pair(step, X0, X1, Y0, Y1);
   load_pair(step + wstride, NX0, NX1, NY0, NY1);
 
-  // pending fine words: a fine round leaves its window [pb, pb + pc) of the fine queue in place and
-  // stores each point's word beside it (s_fw); the window is resolved in two halves of 64 and only
-  // then released.  The list walk of a half reads its point back from the window.
-  int pb = 0, pc = 0, hn = 0, hd = 0;   // wave-uniform: window base and size, next half, halves
+  // pending fine words: a fine round leaves its window [pb, pb + pc) of the fine queue in place, each
+  // lane holding its point's 8-B word in registers (pend_w); the window is resolved in one step and
+  // only then released.  The list walk reads its point back from the window.
+  int pb = 0, pc = 0;
+  bool pend = false;                 // wave-uniform: a window awaits resolution
   bool list_on = false;              // wave-uniform: some lane walks a list
   int l_slot = 0, l_lo = 0, l_n = 0, l_j = 0;
-  uint32_t* fw = s_fw[wv];
-  uint32_t pend_w = CELL_EMPTY << 30;   // FBATCH == 64: the pending window's word of this lane
+  uint2 pend_w = make_uint2(CELL_EMPTY << 30, 0u);
 
   for (;;) {
     // every other stage idle: the item stage drains what is left (a line round may hand blobs over)
-    const bool idle = !list_on && hn == hd && fn == 0 && step >= nstep;
+    const bool idle = !list_on && !pend && fn == 0 && step >= nstep;
     if (qn + qg >= 64 || (idle && qn + qg > 0)) {   // ---- items: one round of the fuller kind
       wave_lds_sync();
       const bool lines = qn >= qg;
@@ -343,15 +343,24 @@ __global__ __launch_bounds__(QTPB) void k_pip_join_q(const double* __restrict__ 
       list_on = __ballot(l_j < l_n) != 0;
       continue;
     }
-    if (hn < hd) {   // ---- resolve one half of the pending window
-      const int slot = pb + hn * 64 + lane;
-      const bool act = slot < pb + pc;
-      ++hn;
-      uint32_t w = CELL_EMPTY << 30, id = 0;
+    if (pend) {   // ---- resolve the pending window
+      const int slot = pb + lane;
+      const bool act = lane < pc;
+      pend = false;
+      uint2 w8 = make_uint2(CELL_EMPTY << 30, 0u);
+      uint32_t id = 0;
       double x = 0.0, y = 0.0;
-      if (act) { w = FBATCH > 64 ? fw[slot] : pend_w; x = fx[slot]; y = fy[slot]; id = fid[slot]; }
+      if (act) { w8 = pend_w; x = fx[slot]; y = fy[slot]; id = fid[slot]; }
+      uint32_t w = w8.x;
+      bool ihit = false;   // an inline line decided the point
+      if (sc8_inline(w8)) {
+        const int cx = cell_of(x, d.gx0, d.inv_cw, d.gx), cy = cell_of(y, d.gy0, d.inv_ch, d.gy);
+        const int loc = sc8_locate(w8, x, y, d, cx, cy);
+        if (loc >= 0) { ihit = join_hit(d.op, loc); w = CELL_EMPTY << 30; }
+        else w = d.cell_word[(int64_t)cy * d.gx + cx];   // near the line: the original word's blob decides
+      }
       const uint32_t kind = w >> 30, ref = w & 0x3fffffffu;
-      pair_push(kind == CELL_INTERIOR, id, (int)ref);
+      pair_push(kind == CELL_INTERIOR || ihit, id, ihit ? sc8_poly(w8) : (int)ref);
       const bool item = kind == CELL_BOUNDARY;
       item_push(item, item && lines_on && (ref & (BLOB_COMPACT | SC_LINE)) == (BLOB_COMPACT | SC_LINE), x, y, id, ref);
       l_j = 0;
@@ -365,30 +374,20 @@ __global__ __launch_bounds__(QTPB) void k_pip_join_q(const double* __restrict__ 
         if (l_n < 0 || (int64_t)l_lo + l_n > d.n_list) { pip_fault(d, PIP_FAULT_LIST); l_n = 0; }
       }
       list_on = __ballot(l_j < l_n) != 0;
-      if (hn == hd) fn = pb;  // the window is released once its last half is resolved (list walks
-                              // of that half run next, before anything can push to the queue)
+      fn = pb;   // the window is released (its list walks run next, before anything can push to the queue)
       continue;
     }
     const bool streaming = step < nstep;
-    if (fn >= FBATCH || (!streaming && fn > 0)) {   // ---- fine round: the newest min(fn, 128) points
+    if (fn >= FBATCH || (!streaming && fn > 0)) {   // ---- fine round: the newest min(fn, 64) points
       wave_lds_sync();
       const int cnt = min(fn, FBATCH);
-      const int a = fn - cnt + lane, b = a + 64;
-      const bool act_a = lane < cnt, act_b = FBATCH > 64 && lane + 64 < cnt;
-      uint32_t wa = CELL_EMPTY << 30, wb = CELL_EMPTY << 30;
-      if (act_a) wa = d.cell_sc[(int64_t)cell_of(fy[a], d.gy0, d.inv_ch, d.gy) * d.gx + cell_of(fx[a], d.gx0, d.inv_cw, d.gx)];
-      if (act_b) wb = d.cell_sc[(int64_t)cell_of(fy[b], d.gy0, d.inv_ch, d.gy) * d.gx + cell_of(fx[b], d.gx0, d.inv_cw, d.gx)];
-      if (FBATCH > 64) {
-        if (act_a) fw[a] = wa;
-        if (act_b) fw[b] = wb;
-      } else {
-        pend_w = wa;
-      }
-      wave_lds_sync();
+      const int a = fn - cnt + lane;
+      pend_w = make_uint2(CELL_EMPTY << 30, 0u);
+      if (lane < cnt)
+        pend_w = d.cell_sc8[(int64_t)cell_of(fy[a], d.gy0, d.inv_ch, d.gy) * d.gx + cell_of(fx[a], d.gx0, d.inv_cw, d.gx)];
       pb = fn - cnt;
       pc = cnt;
-      hn = 0;
-      hd = cnt > 64 ? 2 : 1;
+      pend = true;
       continue;
     }
     if (streaming) {   // ---- stream step: 2 points per lane, their coarse words together
@@ -442,7 +441,7 @@ __global__ __launch_bounds__(QTPB) void k_pip_join_q(const double* __restrict__ 
 enum : int {
   JC_POINTS = 0, JC_OUTSIDE, JC_COARSE_EMPTY, JC_COARSE_INTERIOR, JC_COARSE_RAW_MIXED, JC_FINE, JC_FINE_EMPTY,
   JC_FINE_INTERIOR, JC_FINE_LINE, JC_FINE_COMPACT, JC_FINE_GENERIC, JC_FINE_LIST, JC_LIST_ENTRIES,
-  JC_LIST_BLOBS, JC_LINE_RESOLVED, JC_LINE_FALLBACK, JC_N
+  JC_LIST_BLOBS, JC_LINE_RESOLVED, JC_LINE_FALLBACK, JC_FINE_INLINE, JC_INLINE_FALLBACK, JC_N
 };
 
 __global__ __launch_bounds__(256) void k_pip_census(const double* __restrict__ px, const double* __restrict__ py, int64_t n,
@@ -464,7 +463,13 @@ __global__ __launch_bounds__(256) void k_pip_census(const double* __restrict__ p
     if ((w >> 30) == CELL_EMPTY) { c[JC_COARSE_EMPTY]++; continue; }
     if ((w >> 30) == CELL_INTERIOR) { c[JC_COARSE_INTERIOR]++; continue; }
     c[JC_FINE]++;
-    w = d.cell_sc[(int64_t)cy * d.gx + cx];
+    const uint2 w8 = d.cell_sc8[(int64_t)cy * d.gx + cx];
+    if (sc8_inline(w8)) {   // one inline line (counted apart from the line entries)
+      c[JC_FINE_INLINE]++;
+      if (sc8_locate(w8, x, y, d, cx, cy) < 0) c[JC_INLINE_FALLBACK]++;
+      continue;
+    }
+    w = w8.x;
     const uint32_t kind = w >> 30, ref = w & 0x3fffffffu;
     if (kind == CELL_EMPTY) { c[JC_FINE_EMPTY]++; continue; }
     if (kind == CELL_INTERIOR) { c[JC_FINE_INTERIOR]++; continue; }
@@ -568,14 +573,16 @@ static int join_staged(gm_ctx* ctx, const double* px, const double* py, ArrowPts
   return GM_OK;
 }
 
-// the pair count and the device reference checks of a finished join (synchronises the stream)
+// the pair count and the device reference checks of a finished join (synchronises the stream); without
+// n_pairs the call stays stream-ordered and a fault waits in the context's sticky word
 static int join_result(gm_ctx* ctx, const char* what, unsigned long long* counter, bool write, int64_t cap,
                        int64_t* n_pairs) {
-  GM_HIP(hipMemcpyAsync(ctx->h_pinned, counter, 16, hipMemcpyDeviceToHost, ctx->stream));
-  GM_HIP(hipStreamSynchronize(ctx->stream));
-  if (ctx->h_pinned[1]) return index_fault(what, (uint32_t)ctx->h_pinned[1]);
+  if (!n_pairs) return GM_OK;
+  GM_HIP(hipMemcpyAsync(ctx->h_pinned, counter, 8, hipMemcpyDeviceToHost, ctx->stream));
+  const int rc = take_fault(ctx, what);   // synchronises
+  if (rc) return rc;
   const int64_t total = ctx->h_pinned[0];
-  if (n_pairs) *n_pairs = total;
+  *n_pairs = total;
   return (write && total > cap) ? GM_E_CAPACITY : GM_OK;
 }
 
@@ -614,8 +621,8 @@ int gm_pip_join_pred(gm_ctx* ctx, const gm_pip_index* ix, const double* px, cons
   PipDev dv = ix->dev;
   dv.op = predicate == GM_SPATIAL_INTERSECTS ? JOIN_INTERSECTS : JOIN_CONTAINS;
   unsigned long long* counter = (unsigned long long*)ctx->d_scratch;
-  dv.fault = (uint32_t*)(counter + 1);   // reference-check bits (PIP_FAULT_*), read back with the pair count
-  GM_HIP(hipMemsetAsync(counter, 0, 16, ctx->stream));
+  dv.fault = (uint32_t*)(ctx->d_scratch + SCRATCH_FAULT);   // sticky reference-check bits (PIP_FAULT_*)
+  GM_HIP(hipMemsetAsync(counter, 0, 8, ctx->stream));
   if (n > 0) {
     // chunks start at even rows, so 16-B aligned columns stay aligned in every chunk
     const int rc = aligned16(px) && aligned16(py)
@@ -639,8 +646,8 @@ int gm_pip_join_arrow(gm_ctx* ctx, const gm_pip_index* ix, const gm_geom_column*
   PipDev dv = ix->dev;
   dv.op = predicate == GM_SPATIAL_INTERSECTS ? JOIN_INTERSECTS : JOIN_CONTAINS;
   unsigned long long* counter = (unsigned long long*)ctx->d_scratch;
-  dv.fault = (uint32_t*)(counter + 1);
-  GM_HIP(hipMemsetAsync(counter, 0, 16, ctx->stream));
+  dv.fault = (uint32_t*)(ctx->d_scratch + SCRATCH_FAULT);
+  GM_HIP(hipMemsetAsync(counter, 0, 8, ctx->stream));
   if (n > 0) {   // the tuples are read in place (16 B per Float8 tuple, 8 B per Float4 tuple)
     const int rc = ap.f32 ? join_staged<2, false>(ctx, nullptr, nullptr, ap, 8, n, id_base, dv, pt_ids, poly_ids, cap, counter)
                           : join_staged<1, false>(ctx, nullptr, nullptr, ap, 16, n, id_base, dv, pt_ids, poly_ids, cap, counter);
@@ -654,7 +661,7 @@ int gm_pip_join_census(gm_ctx* ctx, const gm_pip_index* ix, const double* px, co
   if (!ctx || !ix || n < 0 || !counters || (n > 0 && (!px || !py))) return GM_E_INVALID;
   GM_HIP(hipSetDevice(ctx->device));
   unsigned long long* d = (unsigned long long*)ctx->d_scratch;
-  static_assert(JC_N <= 16, "census counters exceed the context scratch");
+  static_assert(JC_N < SCRATCH_FAULT, "census counters reach the context's fault word");
   GM_HIP(hipMemsetAsync(d, 0, JC_N * 8, ctx->stream));
   if (n > 0) {
     hipLaunchKernelGGL(k_pip_census, dim3((unsigned)std::min<int64_t>(8192, (n + 255) / 256)), dim3(256), 0, ctx->stream,

@@ -189,11 +189,7 @@ int gm_query_scan(gm_ctx* ctx, const double* x, const double* y, const int64_t* 
   const double nobb[4] = {0.0, 0.0, 0.0, 0.0};
   const double* bb = bbox ? bbox : nobb;
   PipDev d = spatial_op != GM_SPATIAL_NONE ? geoms->dev : PipDev{};
-  int64_t* fault = ctx->d_scratch + 8;   // reference checks of the geometry term (PIP_FAULT_*)
-  if (spatial_op != GM_SPATIAL_NONE) {
-    d.fault = (uint32_t*)fault;
-    GM_HIP(hipMemsetAsync(fault, 0, 8, ctx->stream));
-  }
+  if (spatial_op != GM_SPATIAL_NONE) d.fault = (uint32_t*)(ctx->d_scratch + SCRATCH_FAULT);   // sticky reference checks
   const unsigned grid = (unsigned)((n + FROWS - 1) / FROWS);
   const bool vec = aligned16(x) && aligned16(y) && (!has_during || aligned16(t_ms));
   if (vec) {
@@ -207,12 +203,7 @@ int gm_query_scan(gm_ctx* ctx, const double* x, const double* y, const int64_t* 
   rc = finish_scan(ctx, n, b, ids, ids_cap, n_match);
   free_scan(ctx, mask, b);
   if (rc) return rc;
-  if (spatial_op != GM_SPATIAL_NONE) {
-    int64_t bits = 0;
-    rc = copy_d2h(ctx, &bits, fault, 8);
-    if (rc) return rc;
-    if (bits) return index_fault("gm_query_scan", (uint32_t)bits);
-  }
+  if (spatial_op != GM_SPATIAL_NONE && (rc = take_fault(ctx, "gm_query_scan"))) return rc;
   if (n_match && ids && *n_match > ids_cap) return GM_E_CAPACITY;
   return GM_OK;
 }

@@ -530,24 +530,6 @@ namespace gm {
 
 // ------------------------------------------------------------------ XZ ranges kernel
 
-struct XZRangesArgs {
-  const int32_t* win_off;   // [nq + 1]
-  const double* win;        // 2*D doubles per window, user space (mins then maxs)
-  int64_t q0;
-  int g;
-  double zhi;               // XZ3 z upper bound (maxOffset(period))
-  int range_stop;
-  int64_t fcap, rcap;
-  uint64_t* fa;             // frontier ping / pong, 2 x fcap per query
-  int64_t* rlo;
-  int64_t* rhi;
-  uint8_t* rc;
-  int64_t* gkey;
-  int32_t* gidx;
-  gm_range* out;            // merged ranges scratch, bo.ocap per block
-  BatchOut bo;
-};
-
 // element (ix, iy[, iz]) at level L packed 30 (XZ2) / 20 (XZ3) bits per coordinate
 template <int D>
 __device__ __forceinline__ uint32_t xcoord(uint64_t e, int d) {
@@ -592,32 +574,110 @@ __device__ __forceinline__ int64_t xspan(int L, int g) {
   return (((int64_t)1 << (sh * (g - L + 1))) - 1) / ((1 << D) - 1);
 }
 
+// ------------------------------------------------------------------ XZ ranges: one wave per query
+// XZ2SFC.ranges / XZ3SFC.ranges (XZ2SFC.scala:130-252, XZ3SFC.scala:139-262) for a batch of queries,
+// one 64-lane wave each, with no block barrier anywhere (a 512-thread workgroup per query was bound by
+// its barriers: most queries emit only 38-388 ranges).
+//
+//  1. walk: the FIFO queue of the reference is processed level by level.  Level L's elements are the
+//     2^D children (XElement.children order) of the overlapping elements of level L - 1 (its
+//     "parents", in queue order; level 1 = the children of the unit element).  Each is classified
+//     disjoint (0) / contained (1) / overlapping (2, its children queued) in chunks of 64 lanes, and the
+//     budget -- element i is processed only while ranges.size < rangeStop (XZ2SFC.scala:205), i.e.
+//     nR + (non-disjoint elements before i) < rangeStop -- is a ballot + mbcnt prefix.  From the first
+//     unprocessed element on, every element of the level is bottomed out as its full interval (3,
+//     :219-227), and so are the queued children of the level's overlapping elements: each of those
+//     parents' children chain (a child's full-interval upper is its next sibling's lower) into exactly
+//     the parent's own full interval, merged with its point interval [cs, cs] -- so such a parent is
+//     recorded as kind 3 itself.  Reaching level g (`while (level < g ...)`) bottoms out the same way.
+//  2. order: the emitted ranges are tree nodes whose sequence codes are in DFS preorder (a parent's
+//     point interval, then its children's subtrees in child order), so the sorted position of every
+//     range follows from subtree counts: an up-sweep over the levels gives each parent T = 1 (its own
+//     point interval; 0 for the unit element) + the ranges of its children's subtrees, a down-sweep
+//     gives each element its position.  No comparison sort.
+//  3. merge: adjacent ranges merge when lower <= previous upper + 1 (Java long wrap), contained = AND
+//     (XZ2SFC.scala:231-249), with ballots over 64 sorted ranges at a time, written straight into the
+//     batch buffer.
+// Per query (global workspace, XzWs): parents of all levels (packed coordinates), T / B per parent,
+// per element kind << 30 | the global parent id of an overlapping element, the pre-merge ranges, and
+// the normalized windows.
+constexpr int XW_TPB = 256;   // 4 waves (= 4 queries) per workgroup
+constexpr int XW_MAXL = 32;   // levels (g <= 29)
+
+struct XzWs {   // byte offsets of one query's arrays within its stride
+  int64_t pcap, ecap, rcap;
+  int64_t o_par, o_tb, o_pi, o_ek, o_lo, o_hi, o_rc, o_win, stride;
+};
+
+__host__ __device__ inline XzWs xz_ws(int D, int64_t pcap, int64_t rcap) {
+  XzWs w{};
+  auto al = [](int64_t v) { return (v + 15) & ~(int64_t)15; };
+  w.pcap = pcap; w.ecap = pcap << D; w.rcap = rcap;
+  w.o_par = 0;
+  w.o_tb = w.o_par + al(pcap * 8);
+  w.o_pi = w.o_tb + al(pcap * 4);
+  w.o_ek = w.o_pi + al(pcap * 4);
+  w.o_lo = w.o_ek + al(w.ecap * 4);
+  w.o_hi = w.o_lo + al(rcap * 8);
+  w.o_rc = w.o_hi + al(rcap * 8);
+  w.o_win = w.o_rc + al(rcap);
+  w.stride = w.o_win + al((int64_t)2 * D * MAXB * 8);
+  return w;
+}
+
+struct XZWaveArgs {
+  const int32_t* win_off;   // [nq + 1]
+  const double* win;        // 2*D doubles per window, user space (mins then maxs)
+  int64_t q0, m;            // first query of this launch, queries in it
+  int g;
+  double zhi;               // XZ3 z upper bound (maxOffset(period))
+  int range_stop;
+  XzWs ws;
+  char* base;               // m query strides
+  BatchOut bo;
+};
+
+__device__ __forceinline__ void wave_mem_sync() {   // this wave's global stores visible to its own lanes
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+}
+
 template <int D>
-__global__ GM_XZ_BOUNDS void k_xzranges(XZRangesArgs a) {
-  __shared__ double s_w[2 * D * MAXB];
-  __shared__ int64_t s_tmp[RNW];
-  __shared__ int s_err, s_stop;
-  __shared__ int64_t s_key[LDS_SORT];
-  __shared__ int16_t s_idx[LDS_SORT];
-
-  const int64_t qc = blockIdx.x;
+__global__ __launch_bounds__(XW_TPB) void k_xzranges_w(XZWaveArgs a) {
+  constexpr int NK = 1 << D;
+  __shared__ int32_t s_lb[XW_TPB / 64][XW_MAXL + 1], s_le[XW_TPB / 64][XW_MAXL + 1], s_lnp[XW_TPB / 64][XW_MAXL + 1];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t qc = (int64_t)blockIdx.x * (XW_TPB / 64) + wv;
+  if (qc >= a.m) return;   // whole wave
   const int64_t q = batch_query(a.bo, a.q0, qc);
-  uint64_t* F = a.fa + qc * 2 * a.fcap;
-  uint64_t* G = F + a.fcap;
-  int64_t* rlo = a.rlo + qc * a.rcap;
-  int64_t* rhi = a.rhi + qc * a.rcap;
-  uint8_t* rc = a.rc + qc * a.rcap;
+  const XzWs W = a.ws;
+  char* qb = a.base + qc * W.stride;
+  uint64_t* par = (uint64_t*)(qb + W.o_par);
+  uint32_t* tb = (uint32_t*)(qb + W.o_tb);
+  uint32_t* pix = (uint32_t*)(qb + W.o_pi);
+  uint32_t* ek = (uint32_t*)(qb + W.o_ek);
+  int64_t* rlo = (int64_t*)(qb + W.o_lo);
+  int64_t* rhi = (int64_t*)(qb + W.o_hi);
+  uint8_t* rcb = (uint8_t*)(qb + W.o_rc);
+  double* wn = (double*)(qb + W.o_win);
+  int32_t* lb = s_lb[wv];
+  int32_t* le = s_le[wv];
+  int32_t* lnp = s_lnp[wv];
   const int g = a.g;
+  auto finish = [&](int64_t base, int64_t m, int st) {
+    if (lane == 0) {
+      a.bo.start[q] = base;
+      a.bo.count[q] = st == QS_OK ? (int32_t)m : 0;
+      a.bo.status[q] = st;
+    }
+  };
 
+  // windows, normalized non-lenient (XZ2SFC.scala:132-135 / XZ3SFC.scala:142-145 -> normalize)
   const int w0 = a.win_off[q], nw = a.win_off[q + 1] - w0;
-  if (threadIdx.x == 0) s_err = nw > MAXB ? QS_TOO_MANY_BOUNDS : QS_OK;
-  __syncthreads();
-  if (s_err || nw <= 0) {
-    batch_finish(a.bo, q, 0, s_err, nullptr);
-    return;
-  }
-  // normalize windows, non-lenient (XZ2SFC.scala:132-135 / XZ3SFC.scala:142-145 -> normalize)
-  for (int j = threadIdx.x; j < nw; j += RTPB) {
+  if (nw > MAXB) { finish(0, 0, QS_TOO_MANY_BOUNDS); return; }
+  if (nw <= 0) { finish(0, 0, QS_OK); return; }
+  int werr = QS_OK;
+  for (int j = lane; j < nw; j += 64) {
     const double* w = a.win + 2 * D * (int64_t)(w0 + j);
     const double lo[3] = {-180.0, -90.0, 0.0}, hi[3] = {180.0, 90.0, a.zhi};
     bool ordered = true, inb = true;
@@ -625,155 +685,198 @@ __global__ GM_XZ_BOUNDS void k_xzranges(XZRangesArgs a) {
       ordered = ordered && (w[d] <= w[D + d]);
       inb = inb && (w[d] >= lo[d]) && (w[D + d] <= hi[d]);
     }
-    if (!ordered) atomicMax(&s_err, QS_UNORDERED);
-    else if (!inb) atomicMax(&s_err, QS_OUT_OF_BOUNDS);
+    if (!ordered) werr = max(werr, (int)QS_UNORDERED);
+    else if (!inb) werr = max(werr, (int)QS_OUT_OF_BOUNDS);
     for (int d = 0; d < D; ++d) {
       const double size = __dsub_rn(hi[d], lo[d]);
-      s_w[2 * D * j + d] = __ddiv_rn(__dsub_rn(w[d], lo[d]), size);
-      s_w[2 * D * j + D + d] = __ddiv_rn(__dsub_rn(w[D + d], lo[d]), size);
+      wn[2 * D * j + d] = __ddiv_rn(__dsub_rn(w[d], lo[d]), size);
+      wn[2 * D * j + D + d] = __ddiv_rn(__dsub_rn(w[D + d], lo[d]), size);
     }
   }
-  __syncthreads();
-  if (s_err) {
-    batch_finish(a.bo, q, 0, s_err, nullptr);
-    return;
+  for (int o = 32; o > 0; o >>= 1) werr = max(werr, __shfl_xor(werr, o, 64));
+  if (werr) { finish(0, 0, werr); return; }
+  wave_mem_sync();
+  // one window (the common case) stays in registers
+  double W1[2 * D];
+  if (nw == 1)
+    for (int k = 0; k < 2 * D; ++k) W1[k] = wn[k];
+  auto classify = [&](uint64_t e, double len) -> int {   // 0 disjoint, 1 contained, 2 overlapping
+    double mn[D], ext[D];
+    for (int d = 0; d < D; ++d) {
+      const double ci = (double)xcoord<D>(e, d);
+      mn[d] = __dmul_rn(ci, len);                    // xmin
+      ext[d] = __dmul_rn(__dadd_rn(ci, 2.0), len);   // xext = xmax + length
+    }
+    if (nw == 1) {
+      bool c = true, o = true;
+      for (int d = 0; d < D; ++d) {
+        c = c && (W1[d] <= mn[d]) && (W1[D + d] >= ext[d]);   // XElement.isContained (XZ2SFC.scala:400-401)
+        o = o && (W1[D + d] >= mn[d]) && (W1[d] <= ext[d]);   // XElement.overlaps (XZ2SFC.scala:403-404)
+      }
+      return c ? 1 : (o ? 2 : 0);
+    }
+    bool ovl = false;
+    for (int w = 0; w < nw; ++w) {
+      const double* Wp = wn + 2 * D * w;
+      bool c = true, o = true;
+      for (int d = 0; d < D; ++d) {
+        const double lo = Wp[d], hi = Wp[D + d];
+        c = c && (lo <= mn[d]) && (hi >= ext[d]);
+        o = o && (hi >= mn[d]) && (lo <= ext[d]);
+      }
+      if (c) return 1;
+      ovl = ovl || o;
+    }
+    return ovl ? 2 : 0;
+  };
+
+  // ---- 1. walk
+  if (lane == 0) { par[0] = 0; lb[1] = 0; le[1] = 0; lnp[1] = 1; }
+  wave_mem_sync();
+  int64_t nP = 1, eb = 0, nR = 0;
+  int L = 1, Lmax = 1, err = QS_OK;
+  const int64_t rs = a.range_stop;
+  for (;; ++L) {
+    const int64_t np = lnp[L], K = np << D, pb = lb[L];
+    const bool last = L >= g;   // never processed (level < g fails): bottomed out as full intervals
+    const double len = ldexp(1.0, -L);
+    int64_t cA = 0, c2 = 0, stop_at = last ? 0 : -1;
+    for (int64_t c = 0; c < K; c += 64) {
+      const int64_t i = c + lane;
+      const bool act = i < K;
+      int kind = 0;
+      if (act && stop_at < 0) kind = classify(xchild<D>(par[pb + (i >> D)], (int)(i & (NK - 1))), len);
+      if (stop_at < 0) {
+        const uint64_t nd = __ballot(act && kind != 0);
+        const int64_t excl = cA + lanes_below(nd);
+        const uint64_t over = __ballot(act && nR + excl >= rs);
+        if (over) {
+          const int sl = __builtin_ctzll(over);
+          stop_at = c + sl;
+          cA += __popcll(nd & ((1ull << sl) - 1));
+        } else {
+          cA += __popcll(nd);
+        }
+      }
+      if (stop_at >= 0 && i >= stop_at) kind = 3;
+      uint32_t fp = 0;
+      if (stop_at < 0) {
+        const uint64_t m2 = __ballot(act && kind == 2);
+        fp = (uint32_t)(nP + c2 + lanes_below(m2));
+        if (act && kind == 2 && (int64_t)fp < W.pcap) {
+          par[fp] = xchild<D>(par[pb + (i >> D)], (int)(i & (NK - 1)));
+          pix[fp] = (uint32_t)(eb + i);   // the parent's own element, for the collapse below
+        }
+        c2 += __popcll(m2);
+      }
+      if (act) ek[eb + i] = ((uint32_t)kind << 30) | fp;
+    }
+    wave_mem_sync();
+    nR += cA;
+    Lmax = L;
+    if (stop_at >= 0 || (c2 > 0 && L + 1 >= g)) {
+      // the queued children are bottomed out: the level's overlapping elements become full intervals
+      for (int64_t c = 0; c < K; c += 64) {
+        const int64_t i = c + lane;
+        if (i < K && (ek[eb + i] >> 30) == 2u) ek[eb + i] = 3u << 30;
+      }
+      // a sibling group wholly past the stop (all its elements bottomed out) chains into exactly its
+      // parent's full interval: the parent becomes a kind-3 leaf and the group is dropped, so the
+      // pre-merge list holds at most rangeStop + 2^D - 1 ranges
+      if (stop_at >= 0 && L >= 2) {
+        const int64_t keep = (stop_at + NK - 1) >> D;
+        for (int64_t j = keep + lane; j < np; j += 64) ek[pix[pb + j]] = 3u << 30;
+        if (lane == 0) lnp[L] = (int32_t)keep;
+      }
+      wave_mem_sync();
+      break;
+    }
+    if (c2 == 0) break;
+    if (nP + c2 > W.pcap || eb + K + (c2 << D) > W.ecap || L + 1 > XW_MAXL - 1) { err = QS_CAPACITY; break; }
+    if (lane == 0) { lb[L + 1] = (int32_t)nP; le[L + 1] = (int32_t)(eb + K); lnp[L + 1] = (int32_t)c2; }
+    wave_mem_sync();
+    nP += c2;
+    eb += K;
+  }
+  if (err) { finish(0, 0, err); return; }
+
+  // ---- 2. order: subtree range counts (up), positions (down)
+  auto S_of = [&](uint32_t x) -> uint32_t { return (x >> 30) == 2u ? tb[x & 0x3fffffffu] : (uint32_t)((x >> 30) != 0u); };
+  for (int l = Lmax; l >= 1; --l) {
+    const int64_t np = lnp[l], pb = lb[l], e0 = le[l];
+    for (int64_t j = lane; j < np; j += 64) {
+      uint32_t t = l == 1 ? 0u : 1u;
+      for (int k = 0; k < NK; ++k) t += S_of(ek[e0 + j * NK + k]);
+      tb[pb + j] = t;
+    }
+    wave_mem_sync();
+  }
+  const int64_t npre = tb[0];
+  if (npre > W.rcap) { finish(0, 0, QS_CAPACITY); return; }
+  if (lane == 0) tb[0] = 0;   // B of the unit element: its children start at 0
+  wave_mem_sync();
+  for (int l = 1; l <= Lmax; ++l) {
+    const int64_t np = lnp[l], pb = lb[l], e0 = le[l];
+    for (int64_t j = lane; j < np; j += 64) {
+      uint32_t pos = tb[pb + j];
+      const uint64_t pe = par[pb + j];
+      for (int k = 0; k < NK; ++k) {
+        const uint32_t x = ek[e0 + j * NK + k], kind = x >> 30;
+        if (!kind) continue;
+        const int64_t cs = xseq<D>(xchild<D>(pe, k), l, g);
+        rlo[pos] = cs;
+        rhi[pos] = kind == 2u ? cs : cs + xspan<D>(l, g);
+        rcb[pos] = kind == 1u;
+        if (kind == 2u) {
+          const uint32_t t = tb[x & 0x3fffffffu];
+          tb[x & 0x3fffffffu] = pos + 1;
+          pos += t;
+        } else {
+          pos += 1;
+        }
+      }
+    }
+    wave_mem_sync();
   }
 
-  // The frontier holds PARENTS: a level's elements are the 2^D children (XElement.children order) of
-  // each overlapping element of the level above, element i = child (i & (2^D - 1)) of parent i >> D.
-  // Level one is the children of the unit element (LevelOneElements).
-  uint64_t* P = F;   // parents of this level's elements
-  uint64_t* Q = G;   // overlapping elements of this level = parents of the next
-  constexpr int NK = 1 << D;
-  if (threadIdx.x == 0) P[0] = 0;
-  __syncthreads();
-  int64_t np = 1;
-  int level = 1;
-  int64_t nR = 0;
-  int err = QS_OK;
-  const int64_t range_stop = a.range_stop;
-  bool bottom = false;   // bottom out this level's elements from first_rest, and the n_kids parents' children
-  int64_t first_rest = 0, n_kids = 0;
-  while (true) {
-    const int64_t K = np << D;
-    if (level >= g) { bottom = true; first_rest = 0; n_kids = 0; break; }  // while (level < g ...)
-    const double len = ldexp(1.0, -level);
-    int64_t a_carry = 0, co_carry = 0;
-    int64_t stop_at = -1;
-    for (int64_t c = 0; c < K; c += RTPB) {
-      const int64_t i = c + threadIdx.x;
-      int kind = 0;  // 0 disjoint, 1 contained, 2 overlapping
-      uint64_t e = 0;
-      if (i < K) {
-        e = xchild<D>(P[i >> D], (int)(i & (NK - 1)));
-        double mn[3], ext[3];
-        for (int d = 0; d < D; ++d) {
-          const double ci = (double)xcoord<D>(e, d);
-          mn[d] = __dmul_rn(ci, len);                    // xmin
-          ext[d] = __dmul_rn(__dadd_rn(ci, 2.0), len);   // xext = xmax + length
-        }
-        bool cont = false, ovl = false;
-        for (int w = 0; w < nw && !cont; ++w) {   // XElement.isContained (XZ2SFC.scala:400-401)
-          const double* W = &s_w[2 * D * w];
-          bool ok = true;
-          for (int d = 0; d < D; ++d) ok = ok && (W[d] <= mn[d]) && (W[D + d] >= ext[d]);
-          cont = ok;
-        }
-        if (!cont) {
-          for (int w = 0; w < nw && !ovl; ++w) {  // XElement.overlaps (XZ2SFC.scala:403-404)
-            const double* W = &s_w[2 * D * w];
-            bool ok = true;
-            for (int d = 0; d < D; ++d) ok = ok && (W[D + d] >= mn[d]) && (W[d] <= ext[d]);
-            ovl = ok;
-          }
-        }
-        kind = cont ? 1 : (ovl ? 2 : 0);
-      }
-      const int ai = kind != 0, co = kind == 2;
-      int64_t pt;   // one scan of (ranges | overlapping << 32)
-      const int64_t px = block_exscan((int64_t)ai | ((int64_t)co << 32), s_tmp, pt);
-      const int64_t ax = px & 0xffffffff, cox = px >> 32, at = pt & 0xffffffff, cot = pt >> 32;
-      // budget: element i is processed only if nR + A(i-1) < rangeStop (XZ2SFC.scala:205); A(i-1) <= at,
-      // so a chunk that cannot reach the stop skips the search
-      int sl = INT32_MAX;
-      if (nR + a_carry + at >= range_stop) {
-        if (threadIdx.x == 0) s_stop = INT32_MAX;
-        __syncthreads();
-        if (i < K && nR + a_carry + ax >= range_stop) atomicMin(&s_stop, (int)threadIdx.x);
-        __syncthreads();
-        sl = s_stop;
-      }
-      if (i < K && (sl == INT32_MAX || (int)threadIdx.x < sl) && kind) {
-        const int64_t rpos = nR + a_carry + ax;
-        const int64_t fpos = co_carry + cox;
-        if (rpos >= a.rcap || fpos + co > a.fcap) {
-          atomicMax(&s_err, QS_CAPACITY);
-        } else {
-          const int64_t cs = xseq<D>(e, level, g);
-          rlo[rpos] = cs;
-          if (kind == 1) { rhi[rpos] = cs + xspan<D>(level, g); rc[rpos] = 1; }
-          else { rhi[rpos] = cs; rc[rpos] = 0; Q[fpos] = e; }   // children queued as their parent
-        }
-      }
-      if (sl != INT32_MAX) {
-        __shared__ int64_t s_a_upto, s_co_upto;
-        if ((int)threadIdx.x == 0) { s_a_upto = 0; s_co_upto = 0; }
-        __syncthreads();
-        if ((int)threadIdx.x == sl) { s_a_upto = a_carry + ax; s_co_upto = co_carry + cox; }
-        __syncthreads();
-        stop_at = c + sl;   // first unprocessed element
-        a_carry = s_a_upto;
-        co_carry = s_co_upto;
-        break;
-      }
-      a_carry += at;
-      co_carry += cot;
-      __syncthreads();
+  // ---- 3. merge adjacent ranges (XZ2SFC.scala:231-249) into the batch buffer
+  auto starts = [&](int64_t j) -> bool {   // range j opens a merged range
+    return j == 0 || !(rlo[j] <= (int64_t)((uint64_t)rhi[j - 1] + 1u));
+  };
+  int64_t M = 0;
+  for (int64_t c = 0; c < npre; c += 64) M += __popcll(__ballot(c + lane < npre && starts(c + lane)));
+  unsigned long long obase = 0;
+  if (lane == 0 && M > 0) obase = atomicAdd(a.bo.total, (unsigned long long)M);
+  obase = __shfl(obase, 0, 64);
+  int64_t runs = 0;          // merged ranges opened before this chunk
+  bool carry_zero = false;   // the run continuing into this chunk has a range that is not contained
+  for (int64_t c = 0; c < npre; c += 64) {
+    const int64_t j = c + lane;
+    const bool act = j < npre;
+    const bool st = act && starts(j);
+    const bool en = act && (j + 1 == npre || starts(j + 1));
+    const uint64_t S = __ballot(st), Z = __ballot(act && !rcb[j]);
+    const uint64_t le_mask = lane == 63 ? ~0ull : ((1ull << (lane + 1)) - 1);
+    const uint64_t sb = S & le_mask;   // starts at or below this lane
+    bool zr;                           // a not-contained range in this lane's run up to here
+    if (sb) {
+      const int s0 = 63 - __builtin_clzll(sb);
+      zr = (Z & le_mask & ~((1ull << s0) - 1)) != 0;
+    } else {
+      zr = carry_zero || (Z & le_mask) != 0;
     }
-    __syncthreads();
-    if (s_err) { err = s_err; break; }
-    nR += a_carry;
-    if (stop_at >= 0) { bottom = true; first_rest = stop_at; n_kids = co_carry; break; }
-    np = co_carry;
-    if (np == 0) break;
-    level += 1;   // LevelTerminator (XZ2SFC.scala:207-212)
-    uint64_t* tmp = P; P = Q; Q = tmp;
-    __syncthreads();
-  }
-  if (!err && bottom) {
-    // bottom out (XZ2SFC.scala:219-227): the rest of this level, then the queued children at level + 1,
-    // as full intervals.  Siblings' full intervals chain (a child's lower is its previous sibling's
-    // upper), so each parent's run of siblings is emitted as the one range the merge below would make
-    // of them: [first sibling's lower, last sibling's upper], not contained.
-    const int64_t g0 = first_rest >> D;
-    const int64_t rest = np - g0;   // sibling groups with unprocessed elements
-    if (nR + rest + n_kids > a.rcap) err = QS_CAPACITY;
-    else {
-      for (int64_t j = threadIdx.x; j < rest; j += RTPB) {
-        const int64_t grp = g0 + j;
-        const int k0 = grp == g0 ? (int)(first_rest & (NK - 1)) : 0;
-        const uint64_t par = P[grp];
-        rlo[nR + j] = xseq<D>(xchild<D>(par, k0), level, g);
-        rhi[nR + j] = xseq<D>(xchild<D>(par, NK - 1), level, g) + xspan<D>(level, g);
-        rc[nR + j] = 0;
-      }
-      for (int64_t j = threadIdx.x; j < n_kids; j += RTPB) {
-        const uint64_t par = Q[j];
-        rlo[nR + rest + j] = xseq<D>(xchild<D>(par, 0), level + 1, g);
-        rhi[nR + rest + j] = xseq<D>(xchild<D>(par, NK - 1), level + 1, g) + xspan<D>(level + 1, g);
-        rc[nR + rest + j] = 0;
-      }
-      nR += rest + n_kids;
+    const int64_t r = runs + __popcll(sb) - 1;
+    if (st && (int64_t)obase + r < a.bo.dcap) a.bo.dbuf[obase + r].lower = rlo[j];
+    if (en && (int64_t)obase + r < a.bo.dcap) {
+      gm_range* o = &a.bo.dbuf[obase + r];
+      o->upper = rhi[j];
+      o->contained = zr ? 0 : 1;
+      o->reserved = 0;
     }
+    runs += __popcll(S);
+    carry_zero = __shfl(zr, 63, 64);
   }
-  __syncthreads();
-  if (err) {
-    batch_finish(a.bo, q, 0, err, nullptr);
-    return;
-  }
-  gm_range* ws = a.out + qc * a.bo.ocap;
-  const int m = sort_merge(rlo, rhi, rc, (int)nR, a.gkey + qc * a.rcap, a.gidx + qc * a.rcap, ws, s_key, s_idx, s_tmp);
-  batch_finish(a.bo, q, m, QS_OK, ws);
+  finish((int64_t)obase, M, QS_OK);
 }
 
 // gather every query's ranges from the batch buffer into query order (one block per query)
@@ -818,8 +921,8 @@ int to_dev(gm_ctx* ctx, const T* h, size_t n, T** d) {
 constexpr int64_t P1CAP = LDS_SORT;
 
 // finish(total, dbuf, dstart, doff): query-order gather of the batch buffer and the copy out
-template <class LaunchFn, class FinishFn>
-int run_batch(gm_ctx* ctx, int64_t q_base, int64_t nq, int64_t fcap, int64_t rcap, size_t felem, LaunchFn& launch,
+template <class PerQFn, class LaunchFn, class FinishFn>
+int run_batch(gm_ctx* ctx, int64_t q_base, int64_t nq, int64_t fcap, int64_t rcap, PerQFn& per_query, LaunchFn& launch,
               int64_t* out_off, int64_t cap, int64_t* needed, int32_t* query_status, FinishFn finish) {
   hipStream_t s = ctx->stream;
   rcap = next_pow2(std::max<int64_t>(rcap, 16));
@@ -861,48 +964,22 @@ int run_batch(gm_ctx* ctx, int64_t q_base, int64_t nq, int64_t fcap, int64_t rca
       dtotal = (unsigned long long*)p;
     }
     GM_HIP(hipMemsetAsync(dtotal, 0, 8, s));
-    // one pass over a query list with caps (fc, rc); qmap null = queries [q_base, q_base + count)
+    // one pass over a query list with caps (fc, rc); qmap null = queries [q_base, q_base + count).  The
+    // launcher's workspace is per_q(fc, rc) bytes per query, chunked by the memory budget
     auto pass = [&](int64_t count, const int32_t* qmap, int64_t fc, int64_t rc) -> int {
-      const bool lds_sort = rc <= LDS_SORT;
-      const bool alias = (int64_t)felem * 2 * fc >= rc * (int64_t)sizeof(gm_range);   // merged output in F|G
-      const int64_t ocap = alias ? 2 * fc * (int64_t)felem / (int64_t)sizeof(gm_range) : rc;
-      const int64_t per_q = fc * (int64_t)felem * 2 + rc * 17 + (lds_sort ? 0 : rc * 12) +
-                            (alias ? 0 : rc * (int64_t)sizeof(gm_range));
+      const int64_t per_q = std::max<int64_t>(16, per_query(fc, rc));
       int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(count, budget / per_q));
       chunk = std::min<int64_t>(chunk, (int64_t)1 << 20);
       const int64_t m_max = std::min(chunk, count);
-      char* fa;
-      int64_t *rlo, *rhi, *gkey = nullptr;
-      uint8_t* rcb;
-      int32_t* gidx = nullptr;
-      gm_range* ws;
-      {
-        const size_t sizes[7] = {al((size_t)(m_max * fc) * felem * 2),
-                                 al((size_t)(m_max * rc) * 8),
-                                 al((size_t)(m_max * rc) * 8),
-                                 al((size_t)(m_max * rc)),
-                                 lds_sort ? 0 : al((size_t)(m_max * rc) * 8),
-                                 lds_sort ? 0 : al((size_t)(m_max * rc) * 4),
-                                 alias ? 0 : al((size_t)(m_max * rc) * sizeof(gm_range))};
-        size_t tot = 0;
-        for (size_t v : sizes) tot += v;
-        void* base = nullptr;
-        int wrc = ctx_workspace(ctx, WS_RANGES, tot, &base);
-        if (wrc) return wrc;
-        char* b = (char*)base;
-        fa = b; b += sizes[0];
-        rlo = (int64_t*)b; b += sizes[1];
-        rhi = (int64_t*)b; b += sizes[2];
-        rcb = (uint8_t*)b; b += sizes[3];
-        if (!lds_sort) { gkey = (int64_t*)b; b += sizes[4]; gidx = (int32_t*)b; b += sizes[5]; }
-        ws = alias ? (gm_range*)fa : (gm_range*)b;
-      }
+      void* base = nullptr;
+      int wrc = ctx_workspace(ctx, WS_RANGES, (size_t)(m_max * per_q), &base);
+      if (wrc) return wrc;
       for (int64_t q0 = 0; q0 < count; q0 += chunk) {
         const int64_t m = std::min(chunk, count - q0);
         // per-query arrays offset so that the kernels index them by absolute query id
-        const BatchOut bo{qmap ? qmap + q0 : nullptr, ocap, dbuf, dcap, dtotal, dstart - q_base, dcount - q_base,
+        const BatchOut bo{qmap ? qmap + q0 : nullptr, 0, dbuf, dcap, dtotal, dstart - q_base, dcount - q_base,
                           dstatus - q_base};
-        launch(qmap ? 0 : q_base + q0, m, fc, rc, fa, rlo, rhi, rcb, gkey, gidx, ws, bo);
+        launch(qmap ? 0 : q_base + q0, m, fc, rc, (char*)base, bo);
         GM_CHECK_LAUNCH();
       }
       return GM_OK;
@@ -943,13 +1020,13 @@ int run_batch(gm_ctx* ctx, int64_t q_base, int64_t nq, int64_t fcap, int64_t rca
 // Batched ranges.  With pinned host output and enough queries, the queries run in chunks and chunk
 // k's result copy (a second stream) overlaps chunk k + 1's kernels: the copy back of 10^7-10^8
 // ranges costs as much as their computation.  The output is identical either way.
-template <class LaunchFn>
-int run_ranges(gm_ctx* ctx, int64_t nq, int64_t fcap, int64_t rcap, size_t felem, LaunchFn launch, int64_t* out_off,
+template <class PerQFn, class LaunchFn>
+int run_ranges(gm_ctx* ctx, int64_t nq, int64_t fcap, int64_t rcap, PerQFn per_query, LaunchFn launch, int64_t* out_off,
                gm_range* out, int64_t cap, int64_t* needed, int32_t* query_status) {
   hipStream_t s = ctx->stream;
   int64_t qc = ctx->ranges_chunk > 0 ? ctx->ranges_chunk : (nq < 16384 ? nq : std::max<int64_t>(8192, (nq + 7) / 8));
   if (out && device_memory(out)) {   // device output (ranges consumed on the device): gathered in place
-    return run_batch(ctx, 0, nq, fcap, rcap, felem, launch, out_off, cap, needed, query_status,
+    return run_batch(ctx, 0, nq, fcap, rcap, per_query, launch, out_off, cap, needed, query_status,
                      [&](int64_t total, const gm_range* dbuf, const int64_t* dstart, const int64_t* doff, int64_t n) -> int {
                        hipLaunchKernelGGL(k_gather_ranges, dim3((unsigned)std::min<int64_t>(n, 65536)), dim3(RTPB), 0, s,
                                           dbuf, dstart, doff, n, out);
@@ -959,7 +1036,7 @@ int run_ranges(gm_ctx* ctx, int64_t nq, int64_t fcap, int64_t rcap, size_t felem
                      });
   }
   if (qc >= nq || !out || !host_pinned(out)) {   // one batch: gather into scratch, one copy
-    return run_batch(ctx, 0, nq, fcap, rcap, felem, launch, out_off, cap, needed, query_status,
+    return run_batch(ctx, 0, nq, fcap, rcap, per_query, launch, out_off, cap, needed, query_status,
                      [&](int64_t total, const gm_range* dbuf, const int64_t* dstart, const int64_t* doff, int64_t n) -> int {
                        void* dout = nullptr;   // the range scratch is free again
                        int rc = ctx_workspace(ctx, WS_RANGES, (size_t)total * sizeof(gm_range), &dout);
@@ -988,7 +1065,7 @@ int run_ranges(gm_ctx* ctx, int64_t nq, int64_t fcap, int64_t rcap, size_t felem
     const int64_t m = std::min(qc, nq - c0);
     off_c.assign((size_t)m + 1, 0);
     int64_t tot = 0;
-    rc = run_batch(ctx, c0, m, fcap, rcap, felem, launch, off_c.data(), INT64_MAX / 32, &tot,
+    rc = run_batch(ctx, c0, m, fcap, rcap, per_query, launch, off_c.data(), INT64_MAX / 32, &tot,
                    query_status ? query_status + c0 : nullptr,
                    [&](int64_t total, const gm_range* dbuf, const int64_t* dstart, const int64_t* doff, int64_t n) -> int {
                      if (over || base + total > cap) { over = true; return GM_OK; }   // capacity: counting only
@@ -1023,6 +1100,35 @@ int run_ranges(gm_ctx* ctx, int64_t nq, int64_t fcap, int64_t rcap, size_t felem
 }
 
 inline int stop_of(int max_ranges) { return max_ranges <= 0 ? INT32_MAX : max_ranges; }
+
+// The Z kernel's workspace for m queries with caps (fc, rc): frontier ping / pong | rlo | rhi | rc |
+// sort keys and ids (global-memory sort only) | merged scratch (unless it aliases the frontier)
+struct ZLayout {
+  bool lds_sort, alias;
+  int64_t ocap, per_q;
+};
+inline ZLayout z_layout(int64_t fc, int64_t rc) {
+  ZLayout z{};
+  z.lds_sort = rc <= LDS_SORT;
+  z.alias = 16 * fc >= rc * (int64_t)sizeof(gm_range);
+  z.ocap = z.alias ? 16 * fc / (int64_t)sizeof(gm_range) : rc;
+  z.per_q = 16 * fc + 17 * rc + (z.lds_sort ? 0 : 12 * rc) + (z.alias ? 0 : rc * (int64_t)sizeof(gm_range)) + 7 * 16;
+  return z;
+}
+inline void z_place(char* base, int64_t m, int64_t fc, int64_t rc, ZRangesArgs& b) {
+  const ZLayout z = z_layout(fc, rc);
+  auto al = [](int64_t v) { return (v + 15) & ~(int64_t)15; };
+  char* p = base;
+  b.fa = (int64_t*)p; p += al(m * fc * 16);
+  b.rlo = (int64_t*)p; p += al(m * rc * 8);
+  b.rhi = (int64_t*)p; p += al(m * rc * 8);
+  b.rc = (uint8_t*)p; p += al(m * rc);
+  b.gkey = nullptr; b.gidx = nullptr;
+  if (!z.lds_sort) { b.gkey = (int64_t*)p; p += al(m * rc * 8); b.gidx = (int32_t*)p; p += al(m * rc * 4); }
+  b.out = z.alias ? (gm_range*)b.fa : (gm_range*)p;
+  b.bo.ocap = z.ocap;
+  b.fcap = fc; b.rcap = rc;
+}
 
 // workspace sizing: the FIFO never holds more than rangeStop + 2^D items before the budget fires
 inline int64_t z_caps(int max_ranges, int D, int64_t cap_hint) {
@@ -1073,13 +1179,11 @@ int gm_z3_ranges(gm_ctx* ctx, int64_t nq, const int32_t* box_off, const double* 
   a.range_stop = stop_of(max_ranges);
   a.recurse_stop = max_recurse < 0 ? INT32_MAX : max_recurse;   // Z3SFC.MaxRecursion = Int.MaxValue
   const int64_t zc = z_caps(max_ranges, 3, cap);
-  rc = run_ranges(ctx, nq, zc, zc, 8,
-                  [&](int64_t q0, int64_t m, int64_t fcap, int64_t rcap, char* fa, int64_t* rlo, int64_t* rhi,
-                      uint8_t* rcb, int64_t* gkey, int32_t* gidx, gm_range* ws, const BatchOut& bo) {
+  rc = run_ranges(ctx, nq, zc, zc, [](int64_t fc, int64_t rcp) { return z_layout(fc, rcp).per_q; },
+                  [&](int64_t q0, int64_t m, int64_t fc, int64_t rcp, char* base, const BatchOut& bo) {
                     ZRangesArgs b = a;
-                    b.q0 = q0; b.fcap = fcap; b.rcap = rcap;
-                    b.fa = (int64_t*)fa; b.rlo = rlo; b.rhi = rhi; b.rc = rcb;
-                    b.gkey = gkey; b.gidx = gidx; b.out = ws; b.bo = bo;
+                    b.q0 = q0; b.bo = bo;
+                    z_place(base, m, fc, rcp, b);
                     hipLaunchKernelGGL(k_zranges<3>, dim3((unsigned)m), dim3(RTPB), 0, s, b);
                   },
                   out_off, out, cap, needed, query_status);
@@ -1110,13 +1214,11 @@ int gm_z2_ranges(gm_ctx* ctx, int64_t nq, const int32_t* box_off, const double* 
   a.range_stop = stop_of(max_ranges);
   a.recurse_stop = max_recurse < 0 ? 7 : max_recurse;   // ZN.DefaultRecurse (ZN.scala:293)
   const int64_t zc = z_caps(max_ranges, 2, cap);
-  rc = run_ranges(ctx, nq, zc, zc, 8,
-                  [&](int64_t q0, int64_t m, int64_t fcap, int64_t rcap, char* fa, int64_t* rlo, int64_t* rhi,
-                      uint8_t* rcb, int64_t* gkey, int32_t* gidx, gm_range* ws, const BatchOut& bo) {
+  rc = run_ranges(ctx, nq, zc, zc, [](int64_t fc, int64_t rcp) { return z_layout(fc, rcp).per_q; },
+                  [&](int64_t q0, int64_t m, int64_t fc, int64_t rcp, char* base, const BatchOut& bo) {
                     ZRangesArgs b = a;
-                    b.q0 = q0; b.fcap = fcap; b.rcap = rcap;
-                    b.fa = (int64_t*)fa; b.rlo = rlo; b.rhi = rhi; b.rc = rcb;
-                    b.gkey = gkey; b.gidx = gidx; b.out = ws; b.bo = bo;
+                    b.q0 = q0; b.bo = bo;
+                    z_place(base, m, fc, rcp, b);
                     hipLaunchKernelGGL(k_zranges<2>, dim3((unsigned)m), dim3(RTPB), 0, s, b);
                   },
                   out_off, out, cap, needed, query_status);
@@ -1138,28 +1240,27 @@ static int xz_ranges(gm_ctx* ctx, int D, int64_t nq, const int32_t* win_off, con
   fr.p[0] = dwo;
   if (!rc) { rc = to_dev(ctx, windows, (size_t)nw * 2 * D, &dw); fr.p[1] = dw; }
   if (rc) return rc;
-  XZRangesArgs a{};
+  XZWaveArgs a{};
   a.win_off = dwo; a.win = dw; a.g = g; a.zhi = (double)max_offset(period);
   a.range_stop = stop_of(max_ranges);
-  // each processed element adds one range and at most one queued parent (its 2^D children); a level
-  // processes at most rangeStop elements; bottom-out adds one range per parent of either level
+  // the walk processes at most rangeStop non-disjoint elements, each at most one parent of the next
+  // level; the pre-merge list holds those ranges plus the unprocessed rest of one sibling group
   int64_t fcap, rcap;
   if (max_ranges > 0) {
     fcap = (int64_t)max_ranges + 2;
-    rcap = (int64_t)max_ranges + 2 * fcap + 16;
+    rcap = (int64_t)max_ranges + (1 << D) + 16;
   } else {
     fcap = std::max<int64_t>(cap, 1 << 16);
-    rcap = 3 * fcap;
+    rcap = (int64_t)fcap << (D + 1);
   }
-  rc = run_ranges(ctx, nq, fcap, rcap, 8,
-                  [&](int64_t q0, int64_t m, int64_t fc, int64_t rcp, char* fa, int64_t* rlo, int64_t* rhi,
-                      uint8_t* rcb, int64_t* gkey, int32_t* gidx, gm_range* ws, const BatchOut& bo) {
-                    XZRangesArgs b = a;
-                    b.q0 = q0; b.fcap = fc; b.rcap = rcp;
-                    b.fa = (uint64_t*)fa; b.rlo = rlo; b.rhi = rhi; b.rc = rcb;
-                    b.gkey = gkey; b.gidx = gidx; b.out = ws; b.bo = bo;
-                    if (D == 2) hipLaunchKernelGGL(k_xzranges<2>, dim3((unsigned)m), dim3(RTPB), 0, s, b);
-                    else hipLaunchKernelGGL(k_xzranges<3>, dim3((unsigned)m), dim3(RTPB), 0, s, b);
+  rc = run_ranges(ctx, nq, fcap, rcap, [D](int64_t fc, int64_t rcp) { return xz_ws(D, fc, rcp).stride; },
+                  [&](int64_t q0, int64_t m, int64_t fc, int64_t rcp, char* base, const BatchOut& bo) {
+                    XZWaveArgs b = a;
+                    b.q0 = q0; b.m = m; b.bo = bo; b.base = base;
+                    b.ws = xz_ws(D, fc, rcp);
+                    const unsigned grid = (unsigned)((m + XW_TPB / 64 - 1) / (XW_TPB / 64));
+                    if (D == 2) hipLaunchKernelGGL(k_xzranges_w<2>, dim3(grid), dim3(XW_TPB), 0, s, b);
+                    else hipLaunchKernelGGL(k_xzranges_w<3>, dim3(grid), dim3(XW_TPB), 0, s, b);
                   },
                   out_off, out, cap, needed, query_status);
   return rc;
@@ -1188,13 +1289,11 @@ int gm_zranges(gm_ctx* ctx, int dims, int64_t nq, const int32_t* bound_off, cons
   a.range_stop = stop_of(max_ranges);
   a.recurse_stop = max_recurse < 0 ? 7 : max_recurse;   // maxRecurse = Some(ZN.DefaultRecurse) (ZN.scala:113,293)
   const int64_t zc = z_caps(max_ranges, dims, cap);
-  rc = run_ranges(ctx, nq, zc, zc, 8,
-                  [&](int64_t q0, int64_t m, int64_t fcap, int64_t rcap, char* fa, int64_t* rlo, int64_t* rhi,
-                      uint8_t* rcb, int64_t* gkey, int32_t* gidx, gm_range* ws, const BatchOut& bo) {
+  rc = run_ranges(ctx, nq, zc, zc, [](int64_t fc, int64_t rcp) { return z_layout(fc, rcp).per_q; },
+                  [&](int64_t q0, int64_t m, int64_t fc, int64_t rcp, char* base, const BatchOut& bo) {
                     ZRangesArgs b = a;
-                    b.q0 = q0; b.fcap = fcap; b.rcap = rcap;
-                    b.fa = (int64_t*)fa; b.rlo = rlo; b.rhi = rhi; b.rc = rcb;
-                    b.gkey = gkey; b.gidx = gidx; b.out = ws; b.bo = bo;
+                    b.q0 = q0; b.bo = bo;
+                    z_place(base, m, fc, rcp, b);
                     if (dims == 3) hipLaunchKernelGGL(k_zranges<3>, dim3((unsigned)m), dim3(RTPB), 0, s, b);
                     else hipLaunchKernelGGL(k_zranges<2>, dim3((unsigned)m), dim3(RTPB), 0, s, b);
                   },

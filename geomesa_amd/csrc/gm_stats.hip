@@ -35,6 +35,7 @@ struct HistArgs {
   NDim lon, lat, tim;
   int row_lo, row_n;  // LDS pass: the time-bin rows [row_lo, row_lo + row_n) of the window it counts
   int tally;          // this launch reports skipped / outside features (the first pass only)
+  int top_s, top_sh;  // TOP path (length 2^m, m <= 21): s = floor((63 - m) / 3), sh = 63 - m - 3 s
 };
 
 // LongBinning.directIndex (BinnedArray.scala:195-201); (value - min) is a Long, divided by a Double
@@ -88,6 +89,47 @@ __device__ __forceinline__ int hist_slot_tab(double x, double y, int64_t ms, con
   return i < 0 ? -1 : rb * a.length + i;
 }
 
+// TOP path, length = 2^m (m <= 21).  The bin is floor(double(z) / 2^(63 - m)) (directIndex's Long ->
+// Double conversion rounds z to 53 bits), i.e. the top m bits of z unless that rounding carries into
+// them.  z interleaves the masked normalized dims (bit 3k + d = bit k of dim d), so z >> 3s is the
+// interleave of the dims' bits >= s, and the top m bits are that >> sh: a few bits per dim instead of
+// the 63-bit key.  A carry from the rounding (which starts below bit 11 of z) reaches bit 3s only
+// through a run of ones, so when some dim has a zero among its bits [s - 4, s) -- a zero of z in
+// [3s - 12, 3s) -- the top bits are the answer; otherwise (probability 2^-12) the exact full path
+// below decides.
+template <int PERIOD, bool UNOBS>
+__device__ __forceinline__ int hist_slot_top(double x, double y, int64_t ms, const HistArgs& a, const uint32_t* sp,
+                                             int& rb, int& skip, int& out) {
+  int16_t b;
+  int64_t off;
+  if (binned_time<PERIOD>(ms, b, off) != ST_OK) { ++skip; return -1; }
+  double td = (double)off;
+  const bool inb = x >= a.lon.min && x <= a.lon.max && y >= a.lat.min && y <= a.lat.max && td >= a.tim.min &&
+                   td <= a.tim.max;
+  if (!inb) {
+    if (!UNOBS) { ++skip; return -1; }
+    x = x < a.lon.min ? a.lon.min : (x > a.lon.max ? a.lon.max : x);
+    y = y < a.lat.min ? a.lat.min : (y > a.lat.max ? a.lat.max : y);
+    td = td < a.tim.min ? a.tim.min : (td > a.tim.max ? a.tim.max : td);
+  }
+  rb = (int)b - a.bin_lo;
+  if (rb < 0 || rb >= a.n_bins) { ++out; return -1; }
+  const uint32_t xn = (uint32_t)normalize(a.lon, x) & 0x1fffffu, yn = (uint32_t)normalize(a.lat, y) & 0x1fffffu;
+  const uint32_t tn = (uint32_t)normalize(a.tim, td) & 0x1fffffu;
+  const int s = a.top_s;
+  const uint32_t low = 15u << (s - 4);
+  int i;
+  if ((xn & yn & tn & low) != low) {
+    i = (int)((spread3_11(xn >> s) | (spread3_11(yn >> s) << 1) | (spread3_11(tn >> s) << 2)) >> a.top_sh);
+  } else {
+    const int64_t z = (int64_t)(z3_split_tab((int32_t)xn, sp) | (z3_split_tab((int32_t)yn, sp) << 1) |
+                                (z3_split_tab((int32_t)tn, sp) << 2));
+    i = long_bin_index(z, a);
+    if (i < 0) return -1;
+  }
+  return rb * a.length + i;
+}
+
 // NARROW: two biased 16-bit counters per 32-bit LDS word (twice the time-bin rows per pass).  A half
 // starts at NB; the thread whose increment lifts it to NB + NS moves NS to the device counter (the
 // decrement that drops it to NB - NS moves -NS), so a half stays within NB +- NS plus the increments
@@ -109,7 +151,7 @@ __device__ __forceinline__ void narrow_dec(uint32_t* w, int sh, unsigned long lo
   }
 }
 
-template <int PERIOD, bool UNOBS, bool VEC, bool NARROW>
+template <int PERIOD, bool UNOBS, bool VEC, bool NARROW, bool TOP>
 __global__ __launch_bounds__(HTPB) void k_z3_hist_lds(const double* __restrict__ x, const double* __restrict__ y,
                                                       const int64_t* __restrict__ t, HistArgs a,
                                                       uint8_t* __restrict__ present,
@@ -132,7 +174,8 @@ __global__ __launch_bounds__(HTPB) void k_z3_hist_lds(const double* __restrict__
   int skip = 0, out = 0;
   auto one = [&](double xx, double yy, int64_t tt) {
     int rb = 0;
-    int c = hist_slot_tab<PERIOD, UNOBS>(xx, yy, tt, a, sp, rb, skip, out);
+    int c = TOP ? hist_slot_top<PERIOD, UNOBS>(xx, yy, tt, a, sp, rb, skip, out)
+                : hist_slot_tab<PERIOD, UNOBS>(xx, yy, tt, a, sp, rb, skip, out);
     rb -= a.row_lo;
     if (c < 0 || rb < 0 || rb >= a.row_n) return;
     c -= a.row_lo * a.length;
@@ -280,8 +323,13 @@ int launch_hist(gm_ctx* ctx, const double* x, const double* y, const int64_t* t,
         return GM_OK;
       };
       int rc;
-      if (vec) rc = narrow ? go(k_z3_hist_lds<PERIOD, UNOBS, true, true>) : go(k_z3_hist_lds<PERIOD, UNOBS, true, false>);
-      else rc = narrow ? go(k_z3_hist_lds<PERIOD, UNOBS, false, true>) : go(k_z3_hist_lds<PERIOD, UNOBS, false, false>);
+      const bool top = a.top_s > 0;
+      if (vec && top)
+        rc = narrow ? go(k_z3_hist_lds<PERIOD, UNOBS, true, true, true>) : go(k_z3_hist_lds<PERIOD, UNOBS, true, false, true>);
+      else if (vec)
+        rc = narrow ? go(k_z3_hist_lds<PERIOD, UNOBS, true, true, false>) : go(k_z3_hist_lds<PERIOD, UNOBS, true, false, false>);
+      else
+        rc = narrow ? go(k_z3_hist_lds<PERIOD, UNOBS, false, true, false>) : go(k_z3_hist_lds<PERIOD, UNOBS, false, false, false>);
       if (rc) return rc;
     }
   } else {
@@ -333,6 +381,13 @@ int gm_z3_histogram(gm_ctx* ctx, const double* x, const double* y, const int64_t
   {
     int e;
     a.inv_bsize = (std::frexp(a.bsize, &e) == 0.5 && e > -1000) ? std::ldexp(1.0, 1 - e) : 0.0;
+  }
+  a.top_s = a.top_sh = 0;
+  if ((length & (length - 1)) == 0 && length <= (1 << 21)) {   // length 2^m: the TOP path
+    int m = 0;
+    while ((1 << m) < length) ++m;
+    a.top_s = (63 - m) / 3;
+    a.top_sh = 63 - m - 3 * a.top_s;
   }
   unsigned long long* c = (unsigned long long*)counts;
   unsigned long long* tl = (unsigned long long*)tally;

@@ -152,7 +152,7 @@ class PolygonIndex:
 
     CENSUS = ["points", "outside", "coarse_empty", "coarse_interior", "coarse_raw_mixed", "fine", "fine_empty",
               "fine_interior", "fine_line", "fine_compact", "fine_generic", "fine_list", "list_entries",
-              "list_blobs", "line_resolved", "line_fallback"]
+              "list_blobs", "line_resolved", "line_fallback", "fine_inline", "inline_fallback"]
 
     def census(self, px, py):
         """Diagnostic: how the lookup chain resolves these points, stage by stage (gm_pip_join_census)."""
@@ -161,7 +161,7 @@ class PolygonIndex:
         dev = torch.device("cuda", self.ctx.device)
         x = torch.as_tensor(px, dtype=torch.float64, device=dev).contiguous()
         y = torch.as_tensor(py, dtype=torch.float64, device=dev).contiguous()
-        c = np.zeros(16, np.int64)
+        c = np.zeros(len(self.CENSUS), np.int64)
         check(self.ctx.lib.gm_pip_join_census(self.ctx.handle, self._h, ptr(x), ptr(y), x.numel(), c.ctypes.data),
               "gm_pip_join_census")
         return dict(zip(self.CENSUS, c.tolist()))
@@ -217,6 +217,7 @@ class PolygonIndex:
         loc = torch.empty(n, dtype=torch.uint8, device=px.device)
         check(self.ctx.lib.gm_pip_relate(self.ctx.handle, self._h, ptr(pid), ptr(px), ptr(py), n, ptr(loc)),
               "gm_pip_relate")
+        self.ctx.sync()   # the call is stream-ordered: a failed device reference check surfaces here
         return loc
 
     def predicate(self, name, poly_ids, px, py):

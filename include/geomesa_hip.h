@@ -88,6 +88,8 @@ int gm_ctx_create(int device, void* stream, gm_ctx** out);
 /* same, on a new non-blocking stream owned (and destroyed) by the context */
 int gm_ctx_create_owned(int device, gm_ctx** out);
 int gm_ctx_destroy(gm_ctx* ctx);
+/* waits for the context stream; GM_E_INDEX when a stream-ordered polygon-index call since the last
+   check failed its device reference checks (gm_pip_join without n_pairs, gm_pip_relate) */
 int gm_ctx_sync(gm_ctx* ctx);
 void* gm_ctx_stream(gm_ctx* ctx);
 const char* gm_last_error(void);
@@ -271,10 +273,11 @@ int gm_pip_index_stats(const gm_pip_index* index, int64_t* stats);
    rects (4 * *n_core uint16, host memory) may be null. */
 int gm_pip_index_core(gm_ctx* ctx, const gm_pip_index* index, uint16_t* rects, int32_t* n_core);
 /* Diagnostic (no reference counterpart): how the join's lookup chain resolves the device points
-   px / py, stage by stage -- counters[16] = points, outside the grid, coarse EMPTY, coarse INTERIOR,
+   px / py, stage by stage -- counters[18] = points, outside the grid, coarse EMPTY, coarse INTERIOR,
    points in mixed coarse cells before the sub-block masks, fine lookups, fine EMPTY, fine INTERIOR,
    fine line entries, fine compact blobs, fine generic blobs, fine lists, list entries, list entries
-   that are blobs, line entries that decide, line entries that fall back to the blob. */
+   that are blobs, line entries that decide, line entries that fall back to the blob, fine words with
+   an inline line, inline lines that fall back to the blob. */
 int gm_pip_join_census(gm_ctx* ctx, const gm_pip_index* index, const double* px, const double* py, int64_t n,
                        int64_t* counters);
 
@@ -306,9 +309,11 @@ int gm_pip_index_import(gm_ctx* ctx, const gm_pip_index_layout* layout, void* co
    pt_ids / poly_ids (device, cap entries; point ids are id_base + row); order within the output is
    unspecified (the reference returns an unordered RDD).  *n_pairs (host) receives the pair count;
    when it exceeds cap, GM_E_CAPACITY is returned and no pair beyond cap is written.  With
-   pt_ids = poly_ids = NULL the call only counts.  The call synchronises the context stream: it
-   returns GM_E_INDEX when a device reference check of the index failed (a corrupt or mismatched
-   imported index), and the output is then invalid. */
+   pt_ids = poly_ids = NULL the call only counts.  With n_pairs = NULL the call is stream-ordered
+   (asynchronous); with n_pairs it synchronises the context stream.  A device reference check of the
+   index that fails (a corrupt or mismatched imported index) makes the output invalid and is reported
+   as GM_E_INDEX by the next synchronising call on the context (this join with n_pairs, gm_query_scan,
+   gm_ctx_sync). */
 int gm_pip_join(gm_ctx* ctx, const gm_pip_index* index, const double* px, const double* py, int64_t n,
                 int64_t id_base, int64_t* pt_ids, int32_t* poly_ids, int64_t cap, int64_t* n_pairs);
 
@@ -360,8 +365,9 @@ int gm_query_scan(gm_ctx* ctx, const double* x, const double* y, const int64_t* 
 #define GM_LOC_BOUNDARY 1
 #define GM_LOC_INTERIOR 2
 #define GM_LOC_NULL 255
-/* Synchronises the context stream; GM_E_INDEX as gm_pip_join (the locations are then invalid).
-   gm_query_scan reports the same checks of its geometry term. */
+/* Stream-ordered; a failed device reference check is reported as for gm_pip_join (GM_E_INDEX at the
+   next synchronising call: the locations are then invalid).  gm_query_scan checks its geometry term
+   the same way and reports it itself. */
 int gm_pip_relate(gm_ctx* ctx, const gm_pip_index* index, const int32_t* poly, const double* px, const double* py,
                   int64_t n, uint8_t* loc);
 

@@ -145,6 +145,19 @@ def test_corrupt_reference_reports_instead_of_faulting(gpu):
         with pytest.raises(_lib.GeomesaHipError) as ei:
             call()
         assert "reference check" in str(ei.value), name
+    # a stream-ordered join (no pair count asked) reports at the next synchronising call, once
+    import ctypes
+    x = torch.as_tensor(px, device="cuda"); y = torch.as_tensor(py, device="cuda")
+    pt0 = torch.empty(len(px) * 2, dtype=torch.int64, device="cuda")
+    pl0 = torch.empty(len(px) * 2, dtype=torch.int32, device="cuda")
+    rc = bad.ctx.lib.gm_pip_join_ex(bad.ctx.handle, bad._h, ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(y.data_ptr()),
+                                    len(px), 0, ctypes.c_void_p(pt0.data_ptr()), ctypes.c_void_p(pl0.data_ptr()),
+                                    len(px) * 2, None, _lib.GM_JOIN_AUTO)
+    assert rc == _lib.GM_OK
+    with pytest.raises(_lib.GeomesaHipError) as ei:
+        bad.ctx.sync()
+    assert "reference check" in str(ei.value)
+    bad.ctx.sync()   # cleared once reported
     # the healthy index on the same context is unaffected
     pt, pl = good.join(px, py)
     pt2, pl2 = PolygonIndex.from_arrays(*good.export_arrays(), polyset=ps).join(px, py)

@@ -55,6 +55,57 @@ def test_z3_histogram_parity(gpu, oracle, period, length, lo, nb):
     assert np.array_equal(P2, op)
 
 
+def _points_with_normalized(oracle, xn, yn, tn, week_bin=2610):
+    """Points whose normalized (lon, lat, week offset) are exactly (xn, yn, tn) where reachable: cell
+    centres for x / y; for t the second whose normalized offset is tn (skipped when none is)."""
+    xs, ys, ts = [], [], []
+    for a, b, c in zip(xn, yn, tn):
+        x = -180.0 + (a + 0.5) * (360.0 / 2 ** 21)
+        y = -90.0 + (b + 0.5) * (180.0 / 2 ** 21)
+        assert oracle.normalize(-180.0, 180.0, 21, x) == a and oracle.normalize(-90.0, 90.0, 21, y) == b
+        # a normalized week offset advances ~3.5 per second: not every value is reachable, so the
+        # lowest 3 bits of tn (z bits 2, 5, 8: below any carry) are lowered until one is
+        done = False
+        for cj in range(c, max(c - 8, -1), -1):
+            sec = int(cj * 604800 / 2 ** 21)
+            for s_ in range(sec - 2, sec + 4):
+                if 0 <= s_ < 604800 and oracle.normalize(0.0, 604800.0, 21, float(s_)) == cj:
+                    xs.append(x); ys.append(y); ts.append(week_bin * 604800000 + s_ * 1000 + 7)
+                    done = True
+                    break
+            if done:
+                break
+    return np.array(xs), np.array(ys), np.array(ts, np.int64)
+
+
+@pytest.mark.parametrize("length", [512, 1024, 2048, 64])
+def test_z3_histogram_top_bits_rounding(gpu, oracle, length):
+    """Power-of-two lengths bin from the top bits of z (gm_stats.hip TOP path) unless the Long -> Double
+    rounding of directIndex can carry into them: keys whose bits below a bin boundary are all ones
+    (the rounding carries into the next bin), one zero bit at every position below the boundary (no
+    carry), and random keys, against the oracle's exact directIndex."""
+    m = length.bit_length() - 1
+    s_ = (63 - m) // 3
+    rng = np.random.default_rng(length)
+    xn, yn, tn = [], [], []
+    for k in range(1, 1 << (21 - s_)):
+        top = k << s_
+        for dims in range(3):   # all ones below the boundary, in every dim (a carry) ...
+            xn.append(top - 1); yn.append(top - 1); tn.append(top - 1)
+            for zb in range(3, s_):   # ... and with one zero bit in one dim (no carry past it)
+                v = [top - 1] * 3
+                v[dims] &= ~(1 << zb)
+                xn.append(v[0]); yn.append(v[1]); tn.append(v[2])
+    r = rng.integers(0, 2 ** 21, (3, 4000))
+    xn += r[0].tolist(); yn += r[1].tolist(); tn += r[2].tolist()
+    x, y, t = _points_with_normalized(oracle, xn, yn, tn)
+    assert len(x) > 200
+    lo, nb = 2609, 3
+    P, C, tl = run_hist(x, y, t, WEEK, length, lo, nb)
+    op, oc, ot = oracle.z3_histogram(x, y, t, length, lo, nb, period=WEEK)
+    assert np.array_equal(C, oc) and np.array_equal(P, op) and np.array_equal(tl, ot)
+
+
 @pytest.mark.parametrize("length,lo,nb", [(1024, 2600, 53), (64, 2607, 4)])
 def test_z3_histogram_hot_counters(gpu, oracle, length, lo, nb):
     """8M features on 3 positions: tens of thousands of increments per counter per workgroup, past the

@@ -10,6 +10,7 @@
 #   bench            the default bench line (stdout json + detail)
 #   prof             rocprofv3 --kernel-trace --stats of the bench, then the FETCH_SIZE / WRITE_SIZE /
 #                    FP64 passes (one counter group per run) -> make_traffic.py input
+#   kstats:LEG       rocprofv3 --kernel-trace --stats of one leg (summary via tools/kstats.py)
 #   pmc:LEG          the counter groups below over one leg (join | table | ranges | hist | z3)
 #   ab:LEG:LIBS      alternating runs of one leg over variant libraries (geomesa_amd/lib/<lib>.so,
 #                    comma-separated; "prod" = the product library), 3 rounds
@@ -23,6 +24,7 @@ out=gpurun_out/$tag
 leg_args() {   # the bench arguments of one leg
   case $1 in
     join) echo "--only join --no-cpu --no-gather --steps 1 --warmup 0 --join-steps 3" ;;
+    ranges) echo "--only extra --no-cpu --no-gather --steps 2 --warmup 1" ;;
     table) echo "--only table --no-cpu --steps 2 --warmup 1" ;;
     z3) echo "--only z3 --no-cpu --steps 10 --warmup 2" ;;
     extra) echo "--only extra --no-cpu --steps 6 --warmup 1" ;;
@@ -57,6 +59,10 @@ for step in "$@"; do
           python3 bench.py --only join --no-cpu --steps 1 --warmup 0 --join-steps 1 > ${out}_pmc$i.log 2>&1
         i=$((i+1))
       done ;;
+    kstats)
+      timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d ${out}_kstats_$arg -o run -- \
+        python3 bench.py $(leg_args $arg) > ${out}_kstats_$arg.json 2> ${out}_kstats_$arg.err
+      python3 tools/kstats.py ${out}_kstats_$arg > ${out}_kstats_$arg.txt 2>&1 || true ;;
     pmc)
       groups=(
         "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE"
