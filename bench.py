@@ -469,6 +469,37 @@ def sort_bytes(b, z, n, last):
     return total, len(passes), "digit passes"
 
 
+# Chip-wide access rates measured by tools/gather_probe.hip on MI355X (profiles/r2_gather_probe*.log:
+# 2^30 accesses per launch, every CU busy): coalesced 16-B stream, a divergent 4/16-B gather from a
+# table resident in L2 (1-4 MB), one that misses L2 (64 MB Infinity-Cache-resident to 1 GB tables:
+# 56-59 G/s either way), and 8 lanes reading one random 128-B line together.
+PROBE_STREAM_GBS, PROBE_L2_GPS, PROBE_FAR_GPS, PROBE_LINE_GPS = 6313.0, 270.0, 57.0, 14.3
+
+
+def gather_model(census, points, pairs, ms):
+    """The join's gather roofline: its lookups priced at the probe rates, per
+    launch, from the lookup census of the same points.  Terms: the point stream and the pair writes
+    (HBM), the coarse-table gathers (L2-resident table; points in EMPTY coarse blocks are answered by
+    the LDS bitmap), the fine-word, line-entry and inline-fallback gathers (beyond L2: the fine table
+    is ~210 MB), and the blob walks (~1.5 lines each at the shared-line rate).  frac = model / measured:
+    how close the kernel is to what its gathers allow when every term runs back to back on the
+    vector-memory path (the bound the r3 PMC named: TD busy > 90%)."""
+    c = census
+    far = c["fine"] + c["fine_line"] + c["inline_fallback"]
+    blobs = c["fine_compact"] + c["fine_generic"] + c["line_fallback"] + c["inline_fallback"]
+    terms = {"stream_ms": 16.0 * points / (PROBE_STREAM_GBS * 1e9) * 1e3,
+             "pair_writes_ms": 12.0 * pairs / (PROBE_STREAM_GBS * 1e9) * 1e3,
+             "coarse_l2_gathers_ms": c["coarse_gather"] / (PROBE_L2_GPS * 1e9) * 1e3,
+             "beyond_l2_gathers_ms": far / (PROBE_FAR_GPS * 1e9) * 1e3,
+             "blob_lines_ms": 1.5 * blobs / (PROBE_LINE_GPS * 1e9) * 1e3}
+    model = sum(terms.values())
+    return dict({k: round(v, 3) for k, v in terms.items()}, model_ms=round(model, 3), measured_ms=round(ms, 3),
+                frac=round(model / ms, 4), counts={"coarse_gathers": c["coarse_gather"], "beyond_l2_gathers": far,
+                                                   "blob_walks": blobs},
+                rates="probe: stream %.0f GB/s, L2 gather %.0f G/s, beyond-L2 gather %.0f G/s, 128-B lines %.1f G/s"
+                      % (PROBE_STREAM_GBS, PROBE_L2_GPS, PROBE_FAR_GPS, PROBE_LINE_GPS))
+
+
 def gather_pairs(dist, ptids, plids, k):
     """Result gather of the join: per-rank pair counts, then every rank's
     (point id, polygon id) pairs to rank 0 over RCCL (shard.gather_rows), timed max over ranks.
@@ -722,7 +753,9 @@ def compact(out):
              "points_per_s": _r(pj["points_per_s"], 1), "matches": pj["matches"],
              "roofline": {"bound": rf["bound"], "achieved": rf["achieved"], "peak": rf["peak"], "unit": rf["unit"],
                           "frac": rf["frac"], "traffic": rf["traffic"],
-                          "kernel_fp64_frac": _r((rf.get("fp64") or {}).get("kernel_fp64_frac"), 5)}}
+                          "kernel_fp64_frac": _r((rf.get("fp64") or {}).get("kernel_fp64_frac"), 5),
+                          "gather_model_ms": (rf.get("gather_model") or {}).get("model_ms"),
+                          "gather_frac": (rf.get("gather_model") or {}).get("frac")}}
         if "row_predicate" in pj:
             j["row_predicate_ms"] = _r(pj["row_predicate"]["ms_per_step"])
         jc = pj.get("cpu_baseline")
@@ -1016,6 +1049,7 @@ def main():
                           "(BASELINE configs[3]); index built on rank 0, broadcast over RCCL when N > 1"
                           % (J, n_polys)}
         pj["roofline"]["bytes_per_unit"] = "16 B/point + 12 B/pair"
+        pj["roofline"]["gather_model"] = gather_model(census, J, npairs.value, jms)
         # FP64 work: E_c = the edges of every (point, polygon) pair whose envelope test
         # passes, counted by the C restatement over a prefix of the same device point stream, scaled;
         # 7 FP64 ops per candidate edge is the reference walk's orientation arithmetic

@@ -441,7 +441,7 @@ __global__ __launch_bounds__(QTPB) void k_pip_join_q(const double* __restrict__ 
 enum : int {
   JC_POINTS = 0, JC_OUTSIDE, JC_COARSE_EMPTY, JC_COARSE_INTERIOR, JC_COARSE_RAW_MIXED, JC_FINE, JC_FINE_EMPTY,
   JC_FINE_INTERIOR, JC_FINE_LINE, JC_FINE_COMPACT, JC_FINE_GENERIC, JC_FINE_LIST, JC_LIST_ENTRIES,
-  JC_LIST_BLOBS, JC_LINE_RESOLVED, JC_LINE_FALLBACK, JC_FINE_INLINE, JC_INLINE_FALLBACK, JC_N
+  JC_LIST_BLOBS, JC_LINE_RESOLVED, JC_LINE_FALLBACK, JC_FINE_INLINE, JC_INLINE_FALLBACK, JC_COARSE_GATHER, JC_N
 };
 
 __global__ __launch_bounds__(256) void k_pip_census(const double* __restrict__ px, const double* __restrict__ py, int64_t n,
@@ -457,6 +457,13 @@ __global__ __launch_bounds__(256) void k_pip_census(const double* __restrict__ p
     c[JC_POINTS]++;
     if (!(x >= d.gx0 && x <= d.gx1 && y >= d.gy0 && y <= d.gy1)) { c[JC_OUTSIDE]++; continue; }
     const int cx = cell_of(x, d.gx0, d.inv_cw, d.gx), cy = cell_of(y, d.gy0, d.inv_ch, d.gy);
+    // the join's LDS bitmap answers EMPTY coarse blocks without the coarse gather (when it fits)
+    bool bm_empty = false;
+    if (d.cm_words > 0 && d.cm_words <= CM_WORDS_MAX) {
+      const int b = ((cy >> CF_LOG) >> d.cm_shift) * d.cm_w + ((cx >> CF_LOG) >> d.cm_shift);
+      bm_empty = (d.cm[b >> 5] >> (b & 31)) & 1u;
+    }
+    if (!bm_empty) c[JC_COARSE_GATHER]++;
     const uint32_t raw = d.coarse_sc[(int64_t)(cy >> CF_LOG) * d.gxc + (cx >> CF_LOG)];
     if ((raw >> 30) == CELL_LIST) c[JC_COARSE_RAW_MIXED]++;
     uint32_t w = coarse_mask(raw, cx, cy, d.coarse_fmt);

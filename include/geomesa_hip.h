@@ -273,11 +273,12 @@ int gm_pip_index_stats(const gm_pip_index* index, int64_t* stats);
    rects (4 * *n_core uint16, host memory) may be null. */
 int gm_pip_index_core(gm_ctx* ctx, const gm_pip_index* index, uint16_t* rects, int32_t* n_core);
 /* Diagnostic (no reference counterpart): how the join's lookup chain resolves the device points
-   px / py, stage by stage -- counters[18] = points, outside the grid, coarse EMPTY, coarse INTERIOR,
+   px / py, stage by stage -- counters[19] = points, outside the grid, coarse EMPTY, coarse INTERIOR,
    points in mixed coarse cells before the sub-block masks, fine lookups, fine EMPTY, fine INTERIOR,
    fine line entries, fine compact blobs, fine generic blobs, fine lists, list entries, list entries
    that are blobs, line entries that decide, line entries that fall back to the blob, fine words with
-   an inline line, inline lines that fall back to the blob. */
+   an inline line, inline lines that fall back to the blob, coarse-table gathers (points the LDS
+   EMPTY bitmap does not answer). */
 int gm_pip_join_census(gm_ctx* ctx, const gm_pip_index* index, const double* px, const double* py, int64_t n,
                        int64_t* counters);
 
