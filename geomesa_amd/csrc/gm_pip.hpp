@@ -62,6 +62,7 @@ struct PipDev {
   const uint32_t* coarse_sc;     // the join's coarse words over cell_sc; LIST words carry sub-block masks
   int32_t coarse_fmt;            // COARSE_EMPTY_MASK / COARSE_MAIN (see coarse_mask)
   const uint4* line_ent;         // line shortcuts, two uint4 each (see "Boundary shortcuts")
+  const uint2* coarse8;          // GM_COARSE8: 16 sub-blocks of 2 x 2 with a 2-bit code each (coarse_mask8)
   const uint2* cell_sc8;         // the join's 8-B fine words: cell_sc, with one-line LINE words inline (sc8_*)
   double gx0, gy0, gx1, gy1, inv_cw, inv_ch;
   int32_t gx, gy, gxc;
@@ -332,29 +333,65 @@ __device__ __forceinline__ int line_locate(const uint4 e0, const uint4 e1, doubl
 
 // The join's 8-B fine words (cell_sc8, derived from cell_sc and line_ent by make_shortcut).  A
 // beyond-L2 gather costs the same for 4 or 16 B per lane (tools/gather_probe.hip: 56-59 G/s either
-// way), so a LINE cell whose entry holds ONE line carries that line in its fine word and its points
-// decide with one gather instead of two (fine word, then the 32-B entry):
+// way), so a LINE cell carries its lines in its fine word when they fit, and its points decide with
+// one gather instead of two (fine word, then the 32-B entry):
 //   tag (bits 63-62) 0: the low half is the cell_sc word (high half 0);
-//   tag 1: bits 61-48 polygon (< 2^14), 47-44 region flags as in the entry (2r located, 2r + 1
-//          interior; r = 0 where f > 0), 43-30 A, 29-16 B (int14), 15-0 C (int16):
+//   tag 1, one line: bits 61-48 polygon (< 2^14), 47-44 region flags as in the entry (2r located,
+//          2r + 1 interior; r = 0 where f > 0), 43-30 A, 29-16 B (int14), 15-0 C (int16):
 //          f(u, v) = A u + B v - C in units of 2^-12 cell, the entry's line requantized (A / 4 ...).
-// The entry's line is within SC_DEV / 4 = 1 unit of the exact line over the cell and the
-// requantization adds <= 1.52, so a point with |f| > SC8_T is on the exact line's side sign(f) and
-// takes that region's location; a nearer point takes the original word's blob (cell_word), as the
-// entry's near-line points do.
+//          The entry's line is within SC_DEV / 4 = 1 unit of the exact line over the cell and the
+//          requantization adds <= 1.52, so a point with |f| > SC8_T is on the exact line's side
+//          sign(f) and takes that region's location;
+//   tag 2, two lines meeting inside the cell (the two segments of a vertex in the cell): bits 61-48
+//          polygon, 47-40 the entry's flags of regions r = side1 + 2 side2, 39-30 / 29-20 the lines'
+//          intersection V = ((a + 0.5) / 1024, (b + 0.5) / 1024) in cell units, 19-10 / 9-0 each line's
+//          normal direction (A, B) as an angle q 2 pi / 1024.  f_k = cos(q_k) (u - Vu) + sin(q_k) (v - Vv)
+//          is within SC8_T2 of the signed distance (cells) to the exact line k over the cell: the
+//          entry's lines are within 4 / 2^14, V within 0.5 sqrt(2) / 1024, the angle within pi / 1024 at
+//          most sqrt(2) from V, plus float rounding.
+// A nearer point takes the original word's blob (cell_word), as the entry's near-line points do.
 constexpr double SC8_T = 4.0;
-__device__ __forceinline__ bool sc8_inline(uint2 w) { return (w.y >> 30) == 1u; }
+constexpr float SC8_T2 = 7.0e-3f;
+__device__ __forceinline__ bool sc8_inline(uint2 w) { return (w.y >> 30) == 1u || (w.y >> 30) == 2u; }
 __device__ __forceinline__ int sc8_poly(uint2 w) { return (int)((w.y >> 16) & 0x3fffu); }
-// LOC_INTERIOR / LOC_EXTERIOR from an inline line, or -1 (near the line, or an unlocated region)
+// (sin, cos) of the angle q 2 pi / 1024: quadrant q >> 8, then Taylor series in float of the angle within
+// the quadrant (< pi / 2: remainders below 4e-6, far inside SC8_T2's margin)
+__device__ __forceinline__ void sc8_dir(uint32_t q, float& sn, float& cs) {
+  const float a = (float)(q & 255u) * (6.2831853071795865f / 1024.0f), a2 = a * a;
+  const float s0 = a * (1.0f - a2 * (1.0f / 6.0f - a2 * (1.0f / 120.0f - a2 * (1.0f / 5040.0f - a2 * (1.0f / 362880.0f)))));
+  const float c0 = 1.0f - a2 * (0.5f - a2 * (1.0f / 24.0f - a2 * (1.0f / 720.0f - a2 * (1.0f / 40320.0f - a2 * (1.0f / 3628800.0f)))));
+  switch (q >> 8) {
+    case 0: sn = s0; cs = c0; break;
+    case 1: sn = c0; cs = -s0; break;
+    case 2: sn = -s0; cs = -c0; break;
+    default: sn = -c0; cs = s0; break;
+  }
+}
+
+// LOC_INTERIOR / LOC_EXTERIOR from an inline word, or -1 (near a line, or an unlocated region)
 __device__ __forceinline__ int sc8_locate(uint2 w, double x, double y, const PipDev& d, int cx, int cy) {
   const uint64_t v = ((uint64_t)w.y << 32) | w.x;
-  const double A = (double)((int64_t)(v << 20) >> 50), B = (double)((int64_t)(v << 34) >> 50);
-  const double C = (double)((int64_t)(v << 48) >> 48);
   const double u = __dsub_rn(__dmul_rn(__dsub_rn(x, d.gx0), d.inv_cw), (double)cx);
   const double t = __dsub_rn(__dmul_rn(__dsub_rn(y, d.gy0), d.inv_ch), (double)cy);
-  const double f = __dsub_rn(__dadd_rn(__dmul_rn(A, u), __dmul_rn(B, t)), C);
-  if (!(f > SC8_T || f < -SC8_T)) return -1;
-  const uint32_t fl = (uint32_t)(v >> 44) & 15u, r = f > SC8_T ? 0u : 1u;
+  uint32_t fl, r;
+  if ((w.y >> 30) == 1u) {
+    const double A = (double)((int64_t)(v << 20) >> 50), B = (double)((int64_t)(v << 34) >> 50);
+    const double C = (double)((int64_t)(v << 48) >> 48);
+    const double f = __dsub_rn(__dadd_rn(__dmul_rn(A, u), __dmul_rn(B, t)), C);
+    if (!(f > SC8_T || f < -SC8_T)) return -1;
+    fl = (uint32_t)(v >> 44) & 15u;
+    r = f > SC8_T ? 0u : 1u;
+  } else {
+    const float du = (float)(u - ((double)((v >> 30) & 1023u) + 0.5) * (1.0 / 1024.0));
+    const float dv = (float)(t - ((double)((v >> 20) & 1023u) + 0.5) * (1.0 / 1024.0));
+    float s1, c1, s2, c2;
+    sc8_dir((uint32_t)(v >> 10) & 1023u, s1, c1);
+    sc8_dir((uint32_t)v & 1023u, s2, c2);
+    const float f1 = c1 * du + s1 * dv, f2 = c2 * du + s2 * dv;
+    if (!(f1 > SC8_T2 || f1 < -SC8_T2) || !(f2 > SC8_T2 || f2 < -SC8_T2)) return -1;
+    fl = (uint32_t)(v >> 40) & 255u;
+    r = (f1 > 0.0f ? 0u : 1u) + (f2 > 0.0f ? 0u : 2u);
+  }
   if (!((fl >> (2 * r)) & 1u)) return -1;
   return ((fl >> (2 * r + 1)) & 1u) ? LOC_INTERIOR : LOC_EXTERIOR;
 }
@@ -381,6 +418,19 @@ __device__ __forceinline__ uint32_t coarse_mask(uint32_t w, int cx, int cy, int3
   }
   const int sub = (((cy & CM) >> SUB_LOG) << 2) | ((cx & CM) >> SUB_LOG);   // 16 sub-blocks of 2 x 2: EMPTY mask
   return ((w >> sub) & 1u) ? (CELL_EMPTY << 30) : w;
+}
+
+// GM_COARSE8 (timing variant): an 8-B coarse entry per coarse cell, {coarse_sc word, 0} for EMPTY /
+// INTERIOR cells, {LIST | main, 16 x 2-bit codes} for mixed ones: code 1 = the 2 x 2 sub-block is
+// EMPTY, 2 = INTERIOR(main), 0 = a fine lookup
+__device__ __forceinline__ uint32_t coarse_mask8(uint2 w, int cx, int cy) {
+  if ((w.x >> 30) != CELL_LIST) return w.x;
+  constexpr int CM = (1 << CF_LOG) - 1;
+  const int sub = (((cy & CM) >> SUB_LOG) << 2) | ((cx & CM) >> SUB_LOG);
+  const uint32_t code = (w.y >> (2 * sub)) & 3u;
+  if (code == 1u) return CELL_EMPTY << 30;
+  if (code == 2u) return (CELL_INTERIOR << 30) | (w.x & 0x3fffffffu);
+  return CELL_LIST << 30;
 }
 
 // PointLocator's location of a point for one BOUNDARY item (ref = the word's payload): a line

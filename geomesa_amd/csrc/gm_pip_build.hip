@@ -752,6 +752,39 @@ __global__ __launch_bounds__(256) void k_build_coarse_sc(const uint32_t* __restr
   }
 }
 
+#ifdef GM_COARSE8
+// coarse8 (coarse_mask8) over cell_sc and coarse_sc
+__global__ __launch_bounds__(256) void k_build_coarse8(const uint32_t* __restrict__ cell_sc, const uint32_t* __restrict__ coarse_sc,
+                                                       int gx, int gy, int gxc, int gyc, uint2* __restrict__ out) {
+  const int64_t n = (int64_t)gxc * gyc;
+  constexpr int CF = 1 << CF_LOG, SB = 1 << SUB_LOG;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t w = coarse_sc[i];
+    if ((w >> 30) != CELL_LIST) { out[i] = make_uint2(w, 0u); continue; }
+    const int yc = (int)(i / gxc), xc = (int)(i % gxc);
+    uint32_t main = 0x3fffffffu;
+    for (int yy = yc * CF; yy < min(gy, (yc + 1) * CF) && main == 0x3fffffffu; ++yy)
+      for (int xx = xc * CF; xx < min(gx, (xc + 1) * CF); ++xx) {
+        const uint32_t f = cell_sc[(int64_t)yy * gx + xx];
+        if ((f >> 30) == CELL_INTERIOR) { main = f & 0x3fffffffu; break; }
+      }
+    uint32_t codes = 0;
+    for (int sb = 0; sb < 16; ++sb) {
+      const int x0 = xc * CF + (sb & 3) * SB, y0 = yc * CF + (sb >> 2) * SB;
+      bool empty = true, inner = main != 0x3fffffffu;
+      for (int yy = y0; yy < min(gy, y0 + SB); ++yy)
+        for (int xx = x0; xx < min(gx, x0 + SB); ++xx) {
+          const uint32_t f = cell_sc[(int64_t)yy * gx + xx];
+          empty &= (f >> 30) == CELL_EMPTY;
+          inner &= f == ((CELL_INTERIOR << 30) | main);
+        }
+      codes |= (empty ? 1u : inner ? 2u : 0u) << (2 * sb);
+    }
+    out[i] = make_uint2((CELL_LIST << 30) | main, codes);
+  }
+}
+#endif
+
 // the coarse EMPTY bitmap over coarse_sc: one thread per 32-bit word
 __global__ __launch_bounds__(256) void k_build_cmask(const uint32_t* __restrict__ coarse_sc, int gxc, int gyc, int shift,
                                                      int cw, int ch, int64_t nwords, uint32_t* __restrict__ out) {
@@ -887,16 +920,17 @@ __global__ __launch_bounds__(256) void k_build_shortcut(PipDev d, int64_t ncell,
   }
 }
 
-// cell_sc8 (gm_pip.hpp, "8-B fine words"): cell_sc zero-extended, and a LINE word whose entry holds one
-// line of a polygon below 2^14 replaced by that line requantized to 2^-12 cell (A / 4, B / 4, C / 4),
-// when the requantization keeps the deviation from the exact line (entry deviation SC_DEV / 4 plus
-// the rounding, over the enlarged cell) a unit below SC8_T
+// cell_sc8 (gm_pip.hpp, "8-B fine words"): cell_sc zero-extended; a LINE word of a polygon below 2^14
+// replaced by its entry's lines when they fit:
+//  * one line: requantized to 2^-12 cell (A / 4, B / 4, C / 4) when the deviation from the exact line
+//    (entry deviation SC_DEV / 4 plus the rounding, over the enlarged cell) stays a unit below SC8_T;
+//  * two lines meeting inside the cell: their intersection and normal angles at 10 bits (tag 2)
 __global__ __launch_bounds__(256) void k_build_sc8(const uint32_t* __restrict__ cell_sc, const uint4* __restrict__ line_ent,
                                                    int64_t n_line, int64_t ncell, uint2* __restrict__ out) {
   for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < ncell; c += (int64_t)gridDim.x * blockDim.x) {
     const uint32_t w = cell_sc[c];
     uint2 o = make_uint2(w, 0u);
-#ifdef GM_SC8_NOINLINE   // tuning build: every fine word without its inline line (A/B of the inline lines)
+#ifdef GM_SC8_NOINLINE   // tuning build: every fine word without its inline lines (A/B of the inline lines)
     if (false &&
 #else
     if (
@@ -905,7 +939,8 @@ __global__ __launch_bounds__(256) void k_build_sc8(const uint32_t* __restrict__ 
         (uint64_t)(w & (SC_LINE - 1)) < (uint64_t)n_line) {
       const uint64_t li = w & (SC_LINE - 1);
       const uint4 e0 = line_ent[2 * li], e1 = line_ent[2 * li + 1];
-      if ((e1.y >> 24) == 1u && e0.y < (1u << 14)) {
+      const uint32_t nl = e1.y >> 24;
+      if (nl == 1u && e0.y < (1u << 14)) {
         const double A = (double)(int16_t)(e0.z & 0xffffu) / 4.0, B = (double)(int16_t)(e0.z >> 16) / 4.0;
         const double C = (double)((int32_t)(e0.w << 8) >> 8) / 4.0;
         const double a = rint(A), b = rint(B), cc = rint(C);
@@ -921,6 +956,31 @@ __global__ __launch_bounds__(256) void k_build_sc8(const uint32_t* __restrict__ 
           o = make_uint2((uint32_t)v, (uint32_t)(v >> 32));
         }
       }
+#ifndef GM_SC8_NOLINE2   // tuning build: one-line words only (A/B of the two-line words)
+      else if (nl == 2u && e0.y < (1u << 14)) {
+        const double A1 = (double)(int16_t)(e0.z & 0xffffu), B1 = (double)(int16_t)(e0.z >> 16);
+        const double C1 = (double)((int32_t)(e0.w << 8) >> 8);
+        const double A2 = (double)(int16_t)(e1.x & 0xffffu), B2 = (double)(int16_t)(e1.x >> 16);
+        const double C2 = (double)((int32_t)(e1.y << 8) >> 8);
+        const double det = A1 * B2 - A2 * B1;   // exact: |products| < 2^29
+        if (fabs(det) >= 1.0) {
+          const double vu = (C1 * B2 - C2 * B1) / det, vv = (A1 * C2 - A2 * C1) / det;
+          if (vu >= 0.0 && vu < 1.0 && vv >= 0.0 && vv < 1.0) {
+            const double tp = 6.283185307179586;
+            auto ang = [&](double a_, double b_) -> uint32_t {
+              double q = rint(atan2(b_, a_) / tp * 1024.0);
+              if (q < 0) q += 1024.0;
+              return (uint32_t)q & 1023u;
+            };
+            const uint64_t v = (2ull << 62) | ((uint64_t)e0.y << 48) | ((uint64_t)((e0.w >> 24) & 255u) << 40) |
+                               ((uint64_t)((uint32_t)floor(vu * 1024.0) & 1023u) << 30) |
+                               ((uint64_t)((uint32_t)floor(vv * 1024.0) & 1023u) << 20) |
+                               ((uint64_t)ang(A1, B1) << 10) | (uint64_t)ang(A2, B2);
+            o = make_uint2((uint32_t)v, (uint32_t)(v >> 32));
+          }
+        }
+      }
+#endif
     }
     out[c] = o;
   }
@@ -1009,6 +1069,7 @@ int make_shortcut(gm_pip_index* ix) {
   ix->n_lines = 0;
   ix->dev.fault = nullptr;   // set per call (the call's scratch word)
   ix->dev.cm = nullptr;      // the coarse EMPTY bitmaps, built after coarse_sc
+  ix->dev.coarse8 = nullptr;
   ix->dev.cm_words = 0;
   ix->dev.cm2 = nullptr;
   ix->dev.cm2_words = 0;
@@ -1062,6 +1123,16 @@ int make_shortcut(gm_pip_index* ix) {
     hipLaunchKernelGGL(k_build_coarse_sc, dim3((unsigned)std::min<int64_t>(65536, ((int64_t)gxc * gyc + 255) / 256)), dim3(256),
                        0, s, (const uint32_t*)p, ix->dev.gx, ix->dev.gy, gxc, gyc, ix->dev.coarse_fmt,
                        (uint32_t*)ix->dev.coarse_sc);
+#ifdef GM_COARSE8
+    {
+      void* c8 = nullptr;
+      if (hipMalloc(&c8, (size_t)gxc * gyc * 8) != hipSuccess) { cleanup(); return hip_fail(hipErrorOutOfMemory, "gm_pip_index coarse8"); }
+      ix->allocs.push_back(c8);
+      hipLaunchKernelGGL(k_build_coarse8, dim3((unsigned)std::min<int64_t>(65536, ((int64_t)gxc * gyc + 255) / 256)), dim3(256),
+                         0, s, (const uint32_t*)p, ix->dev.coarse_sc, ix->dev.gx, ix->dev.gy, gxc, gyc, (uint2*)c8);
+      ix->dev.coarse8 = (const uint2*)c8;
+    }
+#endif
     // the coarse EMPTY bitmaps: the finest block size whose bitmap fits each kernel's LDS budget
     // (the join's, the row predicate's)
     auto bitmap = [&](int64_t budget_words, const uint32_t** out, int32_t* shift, int32_t* w, int64_t* words) -> int {

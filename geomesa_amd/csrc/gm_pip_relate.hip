@@ -112,9 +112,23 @@ __global__ __launch_bounds__(RTPB) void k_pip_relate(const int32_t* __restrict__
           }
         }
       }
+      // the fine words (8 B, boundary shortcuts applied; a one-line cell decides from its inline line)
+      int pre[RILP];   // a location the inline line decided, else -1
 #pragma unroll
-      for (int u = 0; u < RILP; ++u)
-        if ((w[u] >> 30) == CELL_LIST) w[u] = d.cell_sc[(int64_t)cy[u] * d.gx + cx[u]];   // boundary shortcuts applied
+      for (int u = 0; u < RILP; ++u) {
+        pre[u] = -1;
+        if ((w[u] >> 30) == CELL_LIST) {
+          const int64_t c = (int64_t)cy[u] * d.gx + cx[u];
+          const uint2 w8 = d.cell_sc8[c];
+          w[u] = w8.x;
+          if (sc8_inline(w8)) {
+            w[u] = CELL_EMPTY << 30;
+            if (sc8_poly(w8) != p[u]) pre[u] = LOC_EXTERIOR;   // the cell's one entry is another polygon's
+            else if ((pre[u] = sc8_locate(w8, x[u], y[u], d, cx[u], cy[u])) < 0)
+              w[u] = d.cell_word[c];   // near the line: the original word's blob decides
+          }
+        }
+      }
       uint8_t rv[RILP];
       bool dir[RILP];
 #pragma unroll
@@ -125,6 +139,8 @@ __global__ __launch_bounds__(RTPB) void k_pip_relate(const int32_t* __restrict__
         const uint32_t kind = e >> 30;
         if (p[u] < 0 || p[u] >= n_polys) {
           r = LOC_NULL;
+        } else if (pre[u] >= 0) {
+          r = (uint8_t)pre[u];
         } else if (kind == CELL_INTERIOR) {
           r = (int)(e & 0x3fffffffu) == p[u] ? LOC_INTERIOR : LOC_EXTERIOR;
         } else if (kind == CELL_BOUNDARY) {

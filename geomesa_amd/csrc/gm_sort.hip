@@ -8,14 +8,17 @@
 //   * gm_z3_key_bytes  -- the row-key prefix bytes, staged through LDS so the stores are 16-B wide;
 //   * gm_sort_keys     -- a stable sort of (shard u8, bin u16, z u64) in that byte order.  The key
 //                         K = shard:bin:z is an 88-bit integer; one read finds its varying bits (OR /
-//                         AND).  Three stable digit passes (8-bit digits, per-block segments:
-//                         histogram -> one-block scan -> scatter, wave ballots rank equal digits, LDS
-//                         reorders each 8192-row tile so the global writes are digit runs) order the
-//                         rows by the top 24 varying bits; then k_sort_local ranks every run of
-//                         equal 24-bit prefixes (~15 rows for 250M uniform keys) by full key in LDS
-//                         and writes the rows to their final places.  A run longer than 1024 rows
-//                         (skewed keys) sends the call to digit passes over every varying byte (LSD,
-//                         the same kernels), which is also GM_PARAM_SORT_MODE 1;
+//                         AND), a second counts every pass's digits at once (k_sort_count).  Then
+//                         one-sweep digit passes (8-bit digits, k_sort_pass): 4096-row tiles taken in
+//                         order, ranked in LDS (wave ballots rank equal digits), each tile's digit
+//                         offsets found by a decoupled look-back over the tiles before it (8-B
+//                         {count, tag} granules), and the tile leaves as digit runs of 16-B records
+//                         {z, row, bin | shard << 16}.  The passes order the rows by the top
+//                         ~log2(n) - 4 varying bits; k_sort_local then ranks every run of equal
+//                         prefixes (~16 rows for 250M uniform keys) by full key in LDS and writes the
+//                         user columns.  A run longer than 256 rows (skewed keys) sends the call to
+//                         digit passes over every varying byte (LSD, the same kernels), which is also
+//                         GM_PARAM_SORT_MODE 1.
 // The range scan over a sorted table (gm_key_range_scan) lives with the other row-filter scans in
 // gm_filter.hip.
 #include <string.h>
@@ -27,8 +30,9 @@
 
 namespace gm {
 
-constexpr int STPB = 256;               // sort / scan threads per block
+constexpr int STPB = 256;               // key-byte threads per block
 constexpr int NPASS = 11;               // digit positions: z bytes 0..7, bin bytes 0..1, shard
+constexpr int MAXTAG = 16;              // pass tags per call: prefix passes + a fallback's digit passes
 
 // 24 bits of K = bs:z (bs = bin | shard << 16) from bit `off` (0 <= off < 88) up; a digit is the low 8
 __device__ __forceinline__ uint32_t key_bits(uint32_t bs, uint64_t z, int off) {
@@ -42,14 +46,46 @@ __device__ __forceinline__ uint32_t key_bits(uint32_t bs, uint64_t z, int off) {
 }
 __device__ __forceinline__ uint32_t key_digit(uint32_t bs, uint64_t z, int off) { return key_bits(bs, z, off) & 255u; }
 
+// a row in flight between passes: {z lo, z hi, input row, bin | shard << 16}
+__device__ __forceinline__ uint64_t rec_z(uint4 r) { return (uint64_t)r.x | ((uint64_t)r.y << 32); }
+__device__ __forceinline__ uint4 make_rec(uint64_t z, uint32_t row, uint32_t bs) {
+  return make_uint4((uint32_t)z, (uint32_t)(z >> 32), row, bs);
+}
+
 __device__ __forceinline__ uint64_t lanemask_lt() {
   const int lane = threadIdx.x & 63;
   return lane ? (~0ull >> (64 - lane)) : 0ull;
 }
 
+// The caller's columns, read two rows per lane (16-B z, 4-B bin, 2-B shard loads) when `vec` (aligned
+// columns) and both rows exist, else row by row.  bs = bin | shard << 16.
+struct KeyCols {
+  const uint8_t* sh;
+  const uint16_t* bin;
+  const uint64_t* z;
+};
+template <bool SH>
+__device__ __forceinline__ void load_pair(const KeyCols& c, int64_t i, int64_t n, bool vec, uint64_t& z0, uint64_t& z1,
+                                          uint32_t& bs0, uint32_t& bs1) {
+  if (vec && i + 1 < n) {
+    const ulonglong2 zz = *(const ulonglong2*)(c.z + i);
+    const uint32_t bb = *(const uint32_t*)(c.bin + i);
+    z0 = zz.x; z1 = zz.y;
+    bs0 = bb & 0xffffu; bs1 = bb >> 16;
+    if (SH) {
+      const uint32_t ss = *(const uint16_t*)(c.sh + i);
+      bs0 |= (ss & 0xffu) << 16; bs1 |= (ss >> 8) << 16;
+    }
+  } else {
+    z0 = z1 = 0; bs0 = bs1 = 0;
+    if (i < n) { z0 = c.z[i]; bs0 = (uint32_t)c.bin[i] | (SH ? (uint32_t)c.sh[i] << 16 : 0u); }
+    if (i + 1 < n) { z1 = c.z[i + 1]; bs1 = (uint32_t)c.bin[i + 1] | (SH ? (uint32_t)c.sh[i + 1] << 16 : 0u); }
+  }
+}
+
 // which digit passes carry information: the OR and the AND of every key column (a digit on which
 // OR == AND is the same for every key, so its pass would be the identity and is skipped).
-// acc[0] = OR z, acc[1] = OR (bin | shard << 16), acc[2] = AND z, acc[3] = AND (bin | shard << 16).
+// acc[0] = OR z, acc[1] = OR bs, acc[2] = AND z, acc[3] = AND bs.  Four pairs per lane in flight.
 __device__ __forceinline__ uint64_t wave_or(uint64_t v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v |= __shfl_xor(v, o, 64);
@@ -60,28 +96,22 @@ __device__ __forceinline__ uint64_t wave_and(uint64_t v) {
   for (int o = 32; o > 0; o >>= 1) v &= __shfl_xor(v, o, 64);
   return v;
 }
-__global__ __launch_bounds__(STPB) void k_key_or_and(const uint8_t* __restrict__ sh, const uint16_t* __restrict__ bin,
-                                                     const uint64_t* __restrict__ z, int64_t n,
-                                                     unsigned long long* __restrict__ acc, int vec) {
+constexpr int CT = 1024;   // or/and and count threads per block
+constexpr int CU4 = 4;     // pairs per lane per step
+template <bool SH>
+__global__ __launch_bounds__(CT) void k_key_or_and(KeyCols c, int64_t n, unsigned long long* __restrict__ acc, int vec) {
   uint64_t zo = 0, za = ~0ull, bo = 0, ba = ~0ull;
-  const int64_t np = n >> 1;   // pairs: 16-B z loads
-  for (int64_t p = (int64_t)blockIdx.x * STPB + threadIdx.x; p < np; p += (int64_t)gridDim.x * STPB) {
-    uint64_t z0, z1, b0, b1;
-    if (vec) {
-      const ulonglong2 zz = *(const ulonglong2*)(z + 2 * p);
-      const ushort2 bb = *(const ushort2*)(bin + 2 * p);
-      z0 = zz.x; z1 = zz.y; b0 = bb.x; b1 = bb.y;
-      if (sh) { const uchar2 ss = *(const uchar2*)(sh + 2 * p); b0 |= (uint64_t)ss.x << 16; b1 |= (uint64_t)ss.y << 16; }
-    } else {
-      z0 = z[2 * p]; z1 = z[2 * p + 1]; b0 = bin[2 * p]; b1 = bin[2 * p + 1];
-      if (sh) { b0 |= (uint64_t)sh[2 * p] << 16; b1 |= (uint64_t)sh[2 * p + 1] << 16; }
-    }
-    zo |= z0 | z1; za &= z0 & z1;
-    bo |= b0 | b1; ba &= b0 & b1;
-  }
-  if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
-    const uint64_t b0 = (uint64_t)bin[n - 1] | (sh ? (uint64_t)sh[n - 1] << 16 : 0);
-    zo |= z[n - 1]; za &= z[n - 1]; bo |= b0; ba &= b0;
+  const int64_t step = (int64_t)gridDim.x * CT * 2 * CU4;
+  for (int64_t i0 = ((int64_t)blockIdx.x * CT * CU4 + threadIdx.x) * 2; i0 < n; i0 += step) {
+    uint64_t z[CU4][2];
+    uint32_t b[CU4][2];
+#pragma unroll
+    for (int u = 0; u < CU4; ++u) load_pair<SH>(c, i0 + (int64_t)u * CT * 2, n, vec, z[u][0], z[u][1], b[u][0], b[u][1]);
+#pragma unroll
+    for (int u = 0; u < CU4; ++u)
+#pragma unroll
+      for (int e = 0; e < 2; ++e)
+        if (i0 + (int64_t)u * CT * 2 + e < n) { zo |= z[u][e]; za &= z[u][e]; bo |= b[u][e]; ba &= b[u][e]; }
   }
   zo = wave_or(zo); za = wave_and(za); bo = wave_or(bo); ba = wave_and(ba);
   if ((threadIdx.x & 63) == 0) {
@@ -89,71 +119,52 @@ __global__ __launch_bounds__(STPB) void k_key_or_and(const uint8_t* __restrict__
   }
 }
 
-// per-block segment histogram of one digit (bits [off, off + 8) of K), digit-major:
-// hist[d * gridDim.x + block].  1024 threads, two rows per lane (16-B z loads), only the columns the
-// digit touches are read, per-wave LDS counters summed at the end.
-constexpr int HT = 1024;
-__global__ __launch_bounds__(HT) void k_sort_hist(const uint8_t* __restrict__ sh, const uint16_t* __restrict__ bin,
-                                                  const uint64_t* __restrict__ z, int64_t n, int64_t per_block,
-                                                  int off, uint32_t* __restrict__ hist, int vec) {
-  __shared__ uint32_t h[HT / 64][256];
-  const int wave = threadIdx.x >> 6;
-  for (int i = threadIdx.x; i < (HT / 64) * 256; i += HT) (&h[0][0])[i] = 0;
+// Every pass's digit counts in one read: counts[k * 256 + d] = rows whose digit at offs[k] is d.
+// Four LDS copies of the counters (by wave) cut the atomic collisions.
+struct DigitOffs {
+  int off[NPASS];
+  int np;
+};
+template <bool SH>
+__global__ __launch_bounds__(CT) void k_sort_count(KeyCols c, int64_t n, DigitOffs o, uint32_t* __restrict__ counts, int vec) {
+  __shared__ uint32_t h[4][NPASS * 256];
+  const int copy = (threadIdx.x >> 6) & 3;
+  for (int i = threadIdx.x; i < 4 * o.np * 256; i += CT) h[i / (o.np * 256)][i % (o.np * 256)] = 0u;
   __syncthreads();
-  const int64_t b0 = (int64_t)blockIdx.x * per_block, b1 = min(n, b0 + per_block);
-  const bool nz = off < 64, nb = off + 8 > 64 && off < 80, ns = sh != nullptr && off + 8 > 80;
-  // full stretches: 4 pairs per lane, loads issued together (a digit extraction between loads made
-  // the compiler wait for each pair before the next load)
-  constexpr int HU = 4;
-  int64_t i = b0 + 2 * threadIdx.x;
-  if (vec)
-    for (; i + 2 * HT * (HU - 1) + 1 < b1; i += 2 * HT * HU) {
-      ulonglong2 zz[HU];
-      uint32_t bb[HU], ss[HU];
+  const int64_t step = (int64_t)gridDim.x * CT * 2 * CU4;
+  for (int64_t i0 = ((int64_t)blockIdx.x * CT * CU4 + threadIdx.x) * 2; i0 < n; i0 += step) {
+    uint64_t z[CU4][2];
+    uint32_t b[CU4][2];
 #pragma unroll
-      for (int u = 0; u < HU; ++u) {
-        zz[u] = nz ? *(const ulonglong2*)(z + i + 2 * HT * u) : make_ulonglong2(0ull, 0ull);
-        bb[u] = nb ? *(const uint32_t*)(bin + i + 2 * HT * u) : 0u;
-        ss[u] = ns ? (uint32_t)*(const uint16_t*)(sh + i + 2 * HT * u) : 0u;
-      }
+    for (int u = 0; u < CU4; ++u) load_pair<SH>(c, i0 + (int64_t)u * CT * 2, n, vec, z[u][0], z[u][1], b[u][0], b[u][1]);
 #pragma unroll
-      for (int u = 0; u < HU; ++u) {
-        atomicAdd(&h[wave][key_digit((bb[u] & 0xffffu) | ((ss[u] & 0xffu) << 16), zz[u].x, off)], 1u);
-        atomicAdd(&h[wave][key_digit((bb[u] >> 16) | ((ss[u] >> 8) << 16), zz[u].y, off)], 1u);
-      }
-    }
-  for (; i < b1; i += 2 * HT) {   // b0 is even (tile multiple)
+    for (int u = 0; u < CU4; ++u)
 #pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const int64_t r = i + e;
-      if (r >= b1) continue;
-      const uint32_t bs = (nb ? (uint32_t)bin[r] : 0u) | (ns ? (uint32_t)sh[r] << 16 : 0u);
-      atomicAdd(&h[wave][key_digit(bs, nz ? z[r] : 0ull, off)], 1u);
-    }
+      for (int e = 0; e < 2; ++e)
+        if (i0 + (int64_t)u * CT * 2 + e < n)
+          for (int k = 0; k < o.np; ++k) atomicAdd(&h[copy][k * 256 + key_digit(b[u][e], z[u][e], o.off[k])], 1u);
   }
   __syncthreads();
-  if (threadIdx.x < 256) {
-    uint32_t c = 0;
-#pragma unroll
-    for (int w = 0; w < HT / 64; ++w) c += h[w][threadIdx.x];
-    hist[(int64_t)threadIdx.x * gridDim.x + blockIdx.x] = c;
+  for (int i = threadIdx.x; i < o.np * 256; i += CT) {
+    const uint32_t v = h[0][i] + h[1][i] + h[2][i] + h[3][i];
+    if (v) atomicAdd(&counts[i], v);
   }
 }
 
-// Stable scatter of one digit pass, one 1024-thread workgroup per CU.  Each block walks its segment
-// in 8192-row tiles; wave w owns rows [512 w, 512 w + 512) of a tile and reads them in 4 slots of
-// 128 rows, 2 per lane (16-B z loads).  Within a slot, lanes holding the same digit find each other
-// with 16 ballots (8 digit bits x even / odd row); a per-wave LDS counter per digit turns slot ranks
-// into wave ranks, a scan over the waves into block ranks, so a row's place in the tile is (digit,
-// wave, slot, lane, even/odd) = stable.  The tile is reordered in LDS and leaves as digit runs at
-// the block's cursor for each digit (runs average 32 rows for uniform digits: 256-B z segments).
-#ifndef GM_SORT_BT
-#define GM_SORT_BT 1024
-#endif
-constexpr int BT = GM_SORT_BT;      // scatter threads per block
-constexpr int BW = BT / 64;         // waves
-constexpr int BSLOT = 4;            // slots of 2 rows per lane
-constexpr int BTILE = BT * 2 * BSLOT;   // 8192 rows per tile
+// One-sweep digit pass.  Block b takes tile k (the next in a counter, so every lower tile is already
+// running) of 4096 rows; wave w owns rows [512 w, 512 w + 512) of it and reads them in 4 slots of 128
+// rows, 2 per lane.  Within a slot, lanes holding the same digit find each other with 16 ballots
+// (8 digit bits x even / odd row); a per-wave LDS counter per digit turns slot ranks into wave
+// ranks, a scan over the waves into tile ranks, so a row's place in the tile is (digit, wave, slot,
+// lane, even / odd) = stable.  The tile's digit offsets in the output are the digit's global start
+// plus its rows in every lower tile: each of 256 threads publishes its digit's tile count as soon as
+// the tile is ranked ({count, AGG} granule, one 8-B write-through store), then walks back over the
+// lower tiles' granules, adding counts until it meets an inclusive prefix (PRE), and publishes its
+// own (decoupled look-back).  The tile is reordered in LDS meanwhile and leaves as digit runs
+// (16 rows on average: 256-B record runs).  Granule tags carry the pass (tag) so no pass reads
+// another's; the status array is cleared once per call.
+constexpr int PT = 512, PW = PT / 64, PSLOT = 4, PTILE = PT * 2 * PSLOT;   // 4096 rows per tile
+constexpr uint64_t GR_VAL = (1ull << 48) - 1;
 
 __device__ __forceinline__ uint64_t digit_mask(const uint64_t* bal, uint32_t d) {
   uint64_t m = ~0ull;
@@ -162,169 +173,170 @@ __device__ __forceinline__ uint64_t digit_mask(const uint64_t* bal, uint32_t d) 
   return m;
 }
 
-// SH: a shard column; PIN: a permutation input (else the row index).  The next tile's loads only issue
-// into raw registers (z pair, bin pair, shard pair, permutation pair) and are combined when ranked:
-// a combine (or a column test) between loads made the compiler wait for each slot's loads before
-// issuing the next ones, which serialised the "prefetch" into four round trips per tile.
-template <bool SH, bool PIN>
-__global__ __launch_bounds__(BT) void k_sort_scatter(const uint8_t* __restrict__ sh_in, const uint16_t* __restrict__ bin_in,
-                                                     const uint64_t* __restrict__ z_in,
-                                                     const uint32_t* __restrict__ perm_in, uint8_t* __restrict__ sh_out,
-                                                     uint16_t* __restrict__ bin_out, uint64_t* __restrict__ z_out,
-                                                     uint32_t* __restrict__ perm_out, int64_t* __restrict__ perm64_out,
-                                                     int64_t n, int64_t per_block, int doff,
-                                                     const uint32_t* __restrict__ off, int vec) {
-  __shared__ uint64_t s_z[BTILE];
-  __shared__ uint32_t s_perm[BTILE];
-  __shared__ uint16_t s_bin[BTILE];
-  __shared__ uint8_t s_sh[SH ? BTILE : 1];
-  __shared__ uint16_t s_wcnt[BW][256];      // per wave: rows of each digit so far (then: wave offsets)
-  __shared__ uint32_t s_gcur[256], s_tot[256], s_dstart[256], s_wsum[4];
+struct PassArgs {
+  KeyCols in;             // the caller's columns (first pass) ...
+  const uint4* rec_in;    // ... or the previous pass's records
+  uint8_t* sh_out;        // the caller's outputs (last pass) ...
+  uint16_t* bin_out;
+  uint64_t* z_out;
+  int64_t* perm_out;
+  uint4* rec_out;         // ... or records
+  int64_t n;
+  int off;                // digit bit offset
+  uint32_t tag;           // 1..MAXTAG
+  const uint32_t* counts;           // this pass's 256 digit counts
+  unsigned long long* status;       // ntiles x 256 granules
+  unsigned int* ctr;                // this pass's tile counter
+  int vec;
+};
+
+template <bool IN_REC, bool OUT_USER, bool SH>
+__global__ __launch_bounds__(PT) void k_sort_pass(PassArgs a) {
+  __shared__ uint4 s_rec[PTILE];
+  __shared__ uint16_t s_wcnt[PW][256];   // per wave: rows of each digit so far (then: wave offsets)
+  __shared__ uint32_t s_tot[256], s_dstart[256], s_base[256];
+  __shared__ long long s_gpos[256];
+  __shared__ uint32_t s_wsum[2][4];
+  __shared__ uint32_t s_tile;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  if (t < 256) s_gcur[t] = off[(int64_t)t * gridDim.x + blockIdx.x];
-  const int64_t b0 = (int64_t)blockIdx.x * per_block, b1 = min(n, b0 + per_block);
-  const uint64_t lt = lanemask_lt();
-  // raw loads of this lane's rows of a tile (2 rows per slot)
-  ulonglong2 rz[BSLOT];
-  uint32_t rb[BSLOT];    // bin pair (ushort2 bits)
-  uint32_t rs[BSLOT];    // shard pair (uchar2 bits)
-  uint2 rp[BSLOT];       // permutation pair
-  auto load = [&](int64_t t0) __attribute__((always_inline)) {
-    const bool full = vec && t0 + BTILE <= b1;   // block-uniform: every slot holds two rows
-    if (full) {
+  if (t == 0) s_tile = atomicAdd(a.ctr, 1u);
+  for (int i = t; i < PW * 256 / 2; i += PT) ((uint32_t*)&s_wcnt[0][0])[i] = 0u;
+  __syncthreads();
+  const int64_t tile = s_tile, t0 = tile * PTILE, n = a.n;
+  // this lane's rows
+  uint4 rv[PSLOT][2];
+  const bool vec = a.vec && t0 + PTILE <= n;
 #pragma unroll
-      for (int k = 0; k < BSLOT; ++k) {
-        const int64_t i = t0 + wave * (2 * 64 * BSLOT) + k * 128 + 2 * lane;
-        rz[k] = *(const ulonglong2*)(z_in + i);
-        rb[k] = *(const uint32_t*)(bin_in + i);
-        if (SH) rs[k] = *(const uint16_t*)(sh_in + i);
-        if (PIN) rp[k] = *(const uint2*)(perm_in + i);
-      }
+  for (int k = 0; k < PSLOT; ++k) {
+    const int64_t i = t0 + wave * (2 * 64 * PSLOT) + k * 128 + 2 * lane;
+    if (IN_REC) {
+      rv[k][0] = i < n ? a.rec_in[i] : make_uint4(0u, 0u, 0u, 0u);
+      rv[k][1] = i + 1 < n ? a.rec_in[i + 1] : make_uint4(0u, 0u, 0u, 0u);
     } else {
+      uint64_t z0, z1;
+      uint32_t b0, b1;
+      load_pair<SH>(a.in, i, n, vec, z0, z1, b0, b1);
+      rv[k][0] = make_rec(z0, (uint32_t)i, b0);
+      rv[k][1] = make_rec(z1, (uint32_t)(i + 1), b1);
+    }
+  }
+  const uint64_t lt = lanemask_lt();
+  uint32_t rd[PSLOT][2];   // wave rank | digit << 16; rank 0xffff = no row
 #pragma unroll
-      for (int k = 0; k < BSLOT; ++k) {
-        const int64_t i = t0 + wave * (2 * 64 * BSLOT) + k * 128 + 2 * lane;
-        const bool ok0 = i < b1, ok1 = i + 1 < b1;
-        rz[k].x = ok0 ? z_in[i] : 0; rz[k].y = ok1 ? z_in[i + 1] : 0;
-        rb[k] = (ok0 ? (uint32_t)bin_in[i] : 0u) | ((ok1 ? (uint32_t)bin_in[i + 1] : 0u) << 16);
-        if (SH) rs[k] = (ok0 ? (uint32_t)sh_in[i] : 0u) | ((ok1 ? (uint32_t)sh_in[i + 1] : 0u) << 8);
-        if (PIN) rp[k] = make_uint2(ok0 ? perm_in[i] : 0u, ok1 ? perm_in[i + 1] : 0u);
+  for (int k = 0; k < PSLOT; ++k) {
+    const int64_t i = t0 + wave * (2 * 64 * PSLOT) + k * 128 + 2 * lane;
+    const bool ok0 = i < n, ok1 = i + 1 < n;
+    const uint32_t d0 = key_digit(rv[k][0].w, rec_z(rv[k][0]), a.off);
+    const uint32_t d1 = key_digit(rv[k][1].w, rec_z(rv[k][1]), a.off);
+    uint64_t bal0[8], bal1[8];
+#pragma unroll
+    for (int bit = 0; bit < 8; ++bit) {
+      bal0[bit] = __ballot((d0 >> bit) & 1u);
+      bal1[bit] = __ballot((d1 >> bit) & 1u);
+    }
+    const uint64_t okm0 = __ballot(ok0), okm1 = __ballot(ok1);
+    // masks of lanes whose even / odd row holds my even / odd row's digit
+    const uint64_t m00 = digit_mask(bal0, d0) & okm0, m01 = digit_mask(bal1, d0) & okm1;
+    const uint64_t m10 = digit_mask(bal0, d1) & okm0, m11 = digit_mask(bal1, d1) & okm1;
+    const uint64_t le = lt | (1ull << lane);
+    const int r0 = __popcll(m00 & lt) + __popcll(m01 & lt);
+    const int r1 = __popcll(m10 & le) + __popcll(m11 & lt);
+    // wave counters: read before this slot's increments, then the first row of each digit adds
+    const uint32_t c0 = s_wcnt[wave][d0], c1 = s_wcnt[wave][d1];
+    rd[k][0] = (ok0 ? c0 + r0 : 0xffffu) | (d0 << 16);
+    rd[k][1] = (ok1 ? c1 + r1 : 0xffffu) | (d1 << 16);
+    __builtin_amdgcn_wave_barrier();
+    if (ok0 && r0 == 0) s_wcnt[wave][d0] = (uint16_t)(c0 + __popcll(m00) + __popcll(m01));
+    if (ok1 && r1 == 0) s_wcnt[wave][d1] = (uint16_t)(c1 + __popcll(m10) + __popcll(m11));
+    __builtin_amdgcn_wave_barrier();
+  }
+  __syncthreads();
+  uint32_t tot = 0, xt = 0, xb = 0, cg = 0;
+  if (t < 256) {   // per digit: exclusive offsets over the waves, the tile total; scans over the digits
+#pragma unroll
+    for (int w = 0; w < PW; ++w) {
+      const uint32_t c = s_wcnt[w][t];
+      s_wcnt[w][t] = (uint16_t)tot;
+      tot += c;
+    }
+    s_tot[t] = tot;
+    cg = a.counts[t];
+    xt = tot; xb = cg;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(xt, o, 64), yb = __shfl_up(xb, o, 64);
+      if (lane >= o) { xt += y; xb += yb; }
+    }
+    if (lane == 63) { s_wsum[0][wave] = xt; s_wsum[1][wave] = xb; }
+    // the tile's count for this digit, published before anything else
+    const uint64_t agg = ((uint64_t)(2 * a.tag) << 48) | tot;
+    const uint64_t pre = ((uint64_t)(2 * a.tag + 1) << 48) | tot;
+    __hip_atomic_store(a.status + tile * 256 + t, tile == 0 ? pre : agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (t < 256) {
+    uint32_t pt = 0, pb = 0;
+    for (int w = 0; w < wave; ++w) { pt += s_wsum[0][w]; pb += s_wsum[1][w]; }
+    s_dstart[t] = pt + xt - tot;
+    s_base[t] = pb + xb - cg;
+  }
+  __syncthreads();
+  // the tile reordered by digit in LDS
+#pragma unroll
+  for (int k = 0; k < PSLOT; ++k) {
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const uint32_t r = rd[k][e] & 0xffffu, d = rd[k][e] >> 16;
+      if (r == 0xffffu) continue;
+      s_rec[s_dstart[d] + s_wcnt[wave][d] + r] = rv[k][e];
+    }
+  }
+  if (t < 256) {   // look-back: the digit's rows in every lower tile
+    uint64_t excl = 0;
+    if (tile > 0) {
+      const uint64_t tag_agg = 2 * a.tag, tag_pre = 2 * a.tag + 1;
+      int64_t p = tile - 1;
+      for (;;) {
+        const uint64_t v = __hip_atomic_load(a.status + p * 256 + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t tg = v >> 48;
+        if (tg == tag_pre) { excl += v & GR_VAL; break; }
+        if (tg == tag_agg) { excl += v & GR_VAL; --p; }
+        else __builtin_amdgcn_s_sleep(1);
       }
+      __hip_atomic_store(a.status + tile * 256 + t, ((uint64_t)(2 * a.tag + 1) << 48) | (excl + s_tot[t]),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-  };
-  if (b0 < b1) load(b0);
-  for (int64_t t0 = b0; t0 < b1; t0 += BTILE) {
-    // this tile's rows out of the raw registers
-    uint64_t zv[BSLOT][2];
-    uint32_t pv[BSLOT][2];
-    uint32_t bs[BSLOT][2];   // bin | shard << 16
-#pragma unroll
-    for (int k = 0; k < BSLOT; ++k) {
-      const int64_t i = t0 + wave * (2 * 64 * BSLOT) + k * 128 + 2 * lane;
-      zv[k][0] = rz[k].x; zv[k][1] = rz[k].y;
-      bs[k][0] = (rb[k] & 0xffffu) | (SH ? (rs[k] & 0xffu) << 16 : 0u);
-      bs[k][1] = (rb[k] >> 16) | (SH ? ((rs[k] >> 8) & 0xffu) << 16 : 0u);
-      if (PIN) { pv[k][0] = rp[k].x; pv[k][1] = rp[k].y; }
-      else { pv[k][0] = (uint32_t)i; pv[k][1] = (uint32_t)(i + 1); }
+    s_gpos[t] = (long long)s_base[t] + (long long)excl - (long long)s_dstart[t];
+  }
+  __syncthreads();
+  const int cnt = (int)min((int64_t)PTILE, n - t0);
+  for (int q = t; q < cnt; q += PT) {
+    const uint4 r = s_rec[q];
+    const int64_t g = s_gpos[key_digit(r.w, rec_z(r), a.off)] + q;
+    if (OUT_USER) {
+      a.z_out[g] = rec_z(r);
+      a.bin_out[g] = (uint16_t)r.w;
+      if (SH) a.sh_out[g] = (uint8_t)(r.w >> 16);
+      a.perm_out[g] = (int64_t)r.z;
+    } else {
+      a.rec_out[g] = r;
     }
-    for (int i = t; i < BW * 256 / 2; i += BT) ((uint32_t*)&s_wcnt[0][0])[i] = 0u;
-    __syncthreads();
-    uint32_t rd[BSLOT][2];   // wave rank | digit << 16; rank 0xffff = no row
-#pragma unroll
-    for (int k = 0; k < BSLOT; ++k) {
-      const int64_t i = t0 + wave * (2 * 64 * BSLOT) + k * 128 + 2 * lane;
-      const bool ok0 = i < b1, ok1 = i + 1 < b1;
-      const uint32_t d0 = key_digit(bs[k][0], zv[k][0], doff);
-      const uint32_t d1 = key_digit(bs[k][1], zv[k][1], doff);
-      uint64_t bal0[8], bal1[8];
-#pragma unroll
-      for (int bit = 0; bit < 8; ++bit) {
-        bal0[bit] = __ballot((d0 >> bit) & 1u);
-        bal1[bit] = __ballot((d1 >> bit) & 1u);
-      }
-      const uint64_t okm0 = __ballot(ok0), okm1 = __ballot(ok1);
-      // masks of lanes whose even / odd row holds my even / odd row's digit
-      const uint64_t m00 = digit_mask(bal0, d0) & okm0, m01 = digit_mask(bal1, d0) & okm1;
-      const uint64_t m10 = digit_mask(bal0, d1) & okm0, m11 = digit_mask(bal1, d1) & okm1;
-      const uint64_t le = lt | (1ull << lane);
-      const int r0 = __popcll(m00 & lt) + __popcll(m01 & lt);
-      const int r1 = __popcll(m10 & le) + __popcll(m11 & lt);
-      // wave counters: read before this slot's increments, then the first row of each digit adds
-      const uint32_t c0 = s_wcnt[wave][d0], c1 = s_wcnt[wave][d1];
-      rd[k][0] = (ok0 ? c0 + r0 : 0xffffu) | (d0 << 16);
-      rd[k][1] = (ok1 ? c1 + r1 : 0xffffu) | (d1 << 16);
-      __builtin_amdgcn_wave_barrier();
-      if (ok0 && r0 == 0) s_wcnt[wave][d0] = (uint16_t)(c0 + __popcll(m00) + __popcll(m01));
-      if (ok1 && r1 == 0) s_wcnt[wave][d1] = (uint16_t)(c1 + __popcll(m10) + __popcll(m11));
-      __builtin_amdgcn_wave_barrier();
-    }
-    __syncthreads();
-    uint32_t run = 0, x = 0;
-    if (t < 256) {   // per digit: exclusive offsets over the waves, and the digit's tile total
-#pragma unroll
-      for (int w = 0; w < BW; ++w) {
-        const uint32_t c = s_wcnt[w][t];
-        s_wcnt[w][t] = (uint16_t)run;
-        run += c;
-      }
-      s_tot[t] = run;
-      x = run;   // inclusive scan of the digit totals within the wave (waves 0-3 hold the 256 digits)
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(x, o, 64);
-        if (lane >= o) x += y;
-      }
-      if (lane == 63) s_wsum[wave] = x;
-    }
-    __syncthreads();
-    if (t < 256) {
-      uint32_t pre = 0;
-      for (int w = 0; w < wave; ++w) pre += s_wsum[w];
-      s_dstart[t] = pre + x - run;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < BSLOT; ++k) {
-#pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        const uint32_t r = rd[k][e] & 0xffffu, d = rd[k][e] >> 16;
-        if (r == 0xffffu) continue;
-        const uint32_t pos = s_dstart[d] + s_wcnt[wave][d] + r;
-        s_z[pos] = zv[k][e]; s_bin[pos] = (uint16_t)bs[k][e];
-        if (SH) s_sh[pos] = (uint8_t)(bs[k][e] >> 16);
-        s_perm[pos] = pv[k][e];
-      }
-    }
-    __syncthreads();
-    if (t0 + BTILE < b1) load(t0 + BTILE);   // issued before the write-out: in flight during it
-    const int cnt = (int)min((int64_t)BTILE, b1 - t0);
-    for (int q = t; q < cnt; q += BT) {
-      const uint32_t d = key_digit((uint32_t)s_bin[q] | (SH ? (uint32_t)s_sh[q] << 16 : 0u), s_z[q], doff);
-      const int64_t g = (int64_t)s_gcur[d] + (q - (int)s_dstart[d]);
-      z_out[g] = s_z[q];
-      bin_out[g] = s_bin[q];
-      if (SH) sh_out[g] = s_sh[q];
-      if (perm64_out) perm64_out[g] = s_perm[q];
-      else perm_out[g] = s_perm[q];
-    }
-    __syncthreads();
-    if (t < 256) s_gcur[t] += s_tot[t];
   }
 }
 
 // Final placement after the prefix passes: the digit passes at bit offsets o1 > o2 > ... (each digit
 // ends at a varying bit, and only constant bits lie between them) leave the rows grouped, stably, by
-// P = digit(o1) : digit(o2) : ... -- the key's top varying bits, ~log2(n) + 3 of them, so that runs
-// of equal P are short (Poisson(n / 2^bits) for uniform keys).  Tile k covers the runs of
-// equal P that start in [k LSTEP, (k + 1) LSTEP); its rows are staged in LDS, a block scan marks each
-// row's run (start, and at the start its end), each row counts the rows of its run with a smaller key
-// (ties by position: stable) and goes to run start + rank: O(run length) LDS reads per row.  A run
-// longer than RUN_MAX rows (skewed or repeated keys) sets *flag and the host sorts with digit passes
-// over every varying byte instead.
+// P = digit(o1) : digit(o2) : ... -- the key's top varying bits, ~log2(n) - 4 of them, so that runs
+// of equal P are short (Poisson(n / 2^bits) for uniform keys, 16 rows on average).  Tile k covers the
+// runs of equal P that start in [k LSTEP, (k + 1) LSTEP); its rows are staged in LDS, a block scan
+// marks each row's run (start, and at the start its end), each row counts the rows of its run with a
+// smaller key (ties by position: stable) and goes to run start + rank: O(run length) LDS reads per
+// row.  A run longer than RUN_MAX rows (skewed or repeated keys) sets *flag and the host sorts with
+// digit passes over every varying byte instead.
 constexpr int LT = 512, LCAP = 4096, LPT = LCAP / LT, RUN_MAX = 256, LSTEP = LCAP - RUN_MAX;
 
 // the prefix digits (offsets o.x > o.y > ...; an offset < 0: no digit)
-__device__ __forceinline__ uint32_t prefix3(uint32_t bs, uint64_t z, int4 o) {
+__device__ __forceinline__ uint32_t prefix4(uint32_t bs, uint64_t z, int4 o) {
   uint32_t p = 0;
   p = (p << 8) | (o.x >= 0 ? key_digit(bs, z, o.x) : 0u);
   p = (p << 8) | (o.y >= 0 ? key_digit(bs, z, o.y) : 0u);
@@ -334,28 +346,27 @@ __device__ __forceinline__ uint32_t prefix3(uint32_t bs, uint64_t z, int4 o) {
 }
 
 template <bool SH>
-__global__ __launch_bounds__(LT) void k_sort_local(const uint8_t* __restrict__ sh_in, const uint16_t* __restrict__ bin_in,
-                                                   const uint64_t* __restrict__ z_in, const uint32_t* __restrict__ perm_in,
-                                                   uint8_t* __restrict__ sh_out, uint16_t* __restrict__ bin_out,
-                                                   uint64_t* __restrict__ z_out, int64_t* __restrict__ perm_out,
-                                                   int64_t n, int4 po, uint32_t* __restrict__ flag) {
+__global__ __launch_bounds__(LT) void k_sort_local(const uint4* __restrict__ rec_in, uint8_t* __restrict__ sh_out,
+                                                   uint16_t* __restrict__ bin_out, uint64_t* __restrict__ z_out,
+                                                   int64_t* __restrict__ perm_out, int64_t n, int4 po,
+                                                   uint32_t* __restrict__ flag) {
   __shared__ uint64_t s_z[LCAP];
   __shared__ uint32_t s_bs[LCAP];
   __shared__ uint32_t s_run[LCAP];   // prefix; then run start (low 16) | at a run start, its end << 16
   __shared__ int64_t s_ab[2];
   __shared__ uint32_t s_wmax[LT / 64];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  auto gbs = [&](int64_t r) -> uint32_t { return (uint32_t)bin_in[r] | (SH ? (uint32_t)sh_in[r] << 16 : 0u); };
+  auto pre_of = [&](int64_t r) -> uint32_t { const uint4 v = rec_in[r]; return prefix4(v.w, rec_z(v), po); };
   const int64_t ntile = (n + LSTEP - 1) / LSTEP;
   for (int64_t tk = blockIdx.x; tk < ntile; tk += gridDim.x) {   // block-uniform
     if (wave < 2) {   // waves 0 / 1: the first run start at or after p (none within RUN_MAX rows: flag)
       int64_t p = min(n, (tk + wave) * LSTEP);
       if (p > 0 && p < n) {
-        const uint32_t pp = prefix3(gbs(p - 1), z_in[p - 1], po);
+        const uint32_t pp = pre_of(p - 1);
         int64_t found = -1;
         for (int c = 0; c <= RUN_MAX / 64 && found < 0; ++c) {   // wave-uniform
           const int64_t r = p + c * 64 + lane;
-          const bool diff = r >= n || prefix3(gbs(r), z_in[r], po) != pp;
+          const bool diff = r >= n || pre_of(r) != pp;
           const uint64_t bal = __ballot(diff);
           if (bal) found = p + c * 64 + __builtin_ctzll(bal);
         }
@@ -370,9 +381,9 @@ __global__ __launch_bounds__(LT) void k_sort_local(const uint8_t* __restrict__ s
     if (a < 0 || b < 0) continue;   // flagged: the host redoes the sort
     const int m = (int)(b - a);     // <= LSTEP + RUN_MAX = LCAP
     for (int i = t; i < m; i += LT) {
-      const uint64_t zz = z_in[a + i];
-      const uint32_t bb = gbs(a + i);
-      s_z[i] = zz; s_bs[i] = bb; s_run[i] = prefix3(bb, zz, po);
+      const uint4 v = rec_in[a + i];
+      const uint64_t zz = rec_z(v);
+      s_z[i] = zz; s_bs[i] = v.w; s_run[i] = prefix4(v.w, zz, po);
     }
     __syncthreads();
     // run starts: a block max-scan of (row starts a run ? row : 0) over rows [LPT t, LPT t + LPT)
@@ -429,14 +440,14 @@ __global__ __launch_bounds__(LT) void k_sort_local(const uint8_t* __restrict__ s
       z_out[dst] = zi;
       bin_out[dst] = (uint16_t)bi;
       if (SH) sh_out[dst] = (uint8_t)(bi >> 16);
-      perm_out[dst] = perm_in ? (int64_t)perm_in[a + i] : a + i;
+      perm_out[dst] = (int64_t)((const uint32_t*)(rec_in + a + i))[2];
     }
     __syncthreads();
   }
 }
 
-__global__ __launch_bounds__(STPB) void k_widen_perm(const uint32_t* __restrict__ p32, int64_t n, int64_t* __restrict__ p64) {
-  for (int64_t i = (int64_t)blockIdx.x * STPB + threadIdx.x; i < n; i += (int64_t)gridDim.x * STPB) p64[i] = p32 ? p32[i] : i;
+__global__ __launch_bounds__(STPB) void k_widen_perm(int64_t n, int64_t* __restrict__ p64) {
+  for (int64_t i = (int64_t)blockIdx.x * STPB + threadIdx.x; i < n; i += (int64_t)gridDim.x * STPB) p64[i] = i;
 }
 
 // ------------------------------------------------------------------ row-key bytes
@@ -497,17 +508,17 @@ int gm_sort_keys(gm_ctx* ctx, const uint8_t* shard, const int16_t* bin, const in
     return GM_E_INVALID;
   hipStream_t s = ctx->stream;
   const uint8_t* sh = shard;
-  // 16-B z / 4-B bin / 2-B shard pair loads need aligned caller columns (the workspaces are)
-  const bool user_vec = ((uintptr_t)z % 16) == 0 && ((uintptr_t)bin % 4) == 0 && (!sh || ((uintptr_t)sh % 2) == 0);
-  const bool out_vec = ((uintptr_t)z_out % 16) == 0 && ((uintptr_t)bin_out % 4) == 0 &&
-                       (!sh || ((uintptr_t)shard_out % 2) == 0);
+  const KeyCols in{sh, (const uint16_t*)bin, (const uint64_t*)z};
+  // 16-B z / 4-B bin / 2-B shard pair loads need aligned caller columns
+  const int user_vec = ((uintptr_t)z % 16) == 0 && ((uintptr_t)bin % 4) == 0 && (!sh || ((uintptr_t)sh % 2) == 0);
+  const int cgrid = (int)std::max<int64_t>(1, std::min<int64_t>(1024, (n + 2 * CT * CU4 - 1) / (2 * CT * CU4)));
   // which key bits vary (k_key_or_and): acc = OR z, OR bs, AND z, AND bs (bs = bin | shard << 16)
   unsigned long long* acc = (unsigned long long*)ctx->d_scratch;
   GM_HIP(hipMemsetAsync(acc, 0, 16, s));
   GM_HIP(hipMemsetAsync(acc + 2, 0xff, 16, s));
   GM_HIP(hipMemsetAsync(acc + 4, 0, 8, s));   // k_sort_local's flag
-  hipLaunchKernelGGL(k_key_or_and, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(2048, (n / 2 + STPB - 1) / STPB))),
-                     dim3(STPB), 0, s, sh, (const uint16_t*)bin, (const uint64_t*)z, n, acc, (int)user_vec);
+  if (sh) hipLaunchKernelGGL(k_key_or_and<true>, dim3(cgrid), dim3(CT), 0, s, in, n, acc, user_vec);
+  else hipLaunchKernelGGL(k_key_or_and<false>, dim3(cgrid), dim3(CT), 0, s, in, n, acc, user_vec);
   GM_CHECK_LAUNCH();
   unsigned long long hacc[4];
   GM_HIP(hipMemcpyAsync(hacc, acc, sizeof(hacc), hipMemcpyDeviceToHost, s));
@@ -524,20 +535,20 @@ int gm_sort_keys(gm_ctx* ctx, const uint8_t* shard, const int16_t* bin, const in
     if (sh) GM_HIP(hipMemcpyAsync(shard_out, sh, (size_t)n, hipMemcpyDeviceToDevice, s));
     GM_HIP(hipMemcpyAsync(bin_out, bin, (size_t)n * 2, hipMemcpyDeviceToDevice, s));
     GM_HIP(hipMemcpyAsync(z_out, z, (size_t)n * 8, hipMemcpyDeviceToDevice, s));
-    hipLaunchKernelGGL(k_widen_perm, dim3((unsigned)std::min<int64_t>(4096, (n + STPB - 1) / STPB)), dim3(STPB), 0, s,
-                       nullptr, n, perm_out);
+    hipLaunchKernelGGL(k_widen_perm, dim3((unsigned)std::min<int64_t>(4096, (n + STPB - 1) / STPB)), dim3(STPB), 0, s, n,
+                       perm_out);
     GM_CHECK_LAUNCH();
     ctx->sort_last = 0;
     return GM_OK;
   }
   // prefix passes: digits each ending at the highest varying bit below the previous one (only constant
-  // bits are skipped), ceil((log2 n + 3) / 8) of them (at most 4), when that is fewer than the
-  // varying bytes
+  // bits are skipped), ceil((log2 n - 4) / 8) of them (1..4: runs of ~16 equal prefixes for uniform
+  // keys), when that is fewer than the varying bytes
   const uint64_t vz = hacc[0] ^ hacc[2], vb = (hacc[1] ^ hacc[3]) & 0xffffffull;
   auto varying = [&](int bit) -> bool { return bit < 64 ? ((vz >> bit) & 1u) : ((vb >> (bit - 64)) & 1u); };
   int lg = 0;
   while (((int64_t)1 << lg) < n) ++lg;
-  const int npre = std::min(4, (lg + 3 + 7) / 8);
+  const int npre = std::max(1, std::min(4, (lg - 4 + 7) / 8));
   int pofs[4] = {-1, -1, -1, -1};
   int nfound = 0;
   {
@@ -551,81 +562,74 @@ int gm_sort_keys(gm_ctx* ctx, const uint8_t* shard, const int16_t* bin, const in
     }
   }
   const bool prefix_mode = ctx->sort_mode == 0 && (int)lsd.size() > npre && nfound == npre;
-  // one resident wave of blocks: the scatter's LDS (~139 KiB) allows one 1024-thread block per CU
-  const int resident = resident_blocks((const void*)k_sort_scatter<false, true>, ctx->device, BT, 1);
-  const int nblk = (int)std::max<int64_t>(1, std::min<int64_t>(resident, (n + BTILE - 1) / BTILE));
-  const int64_t per = ((n + nblk - 1) / nblk + BTILE - 1) / BTILE * BTILE;
-  const int grid = (int)((n + per - 1) / per);
-  // ping-pong: the user outputs and one temp set
-  uint8_t* tsh = nullptr;
-  uint16_t* tbin = nullptr;
-  uint64_t* tz = nullptr;
-  uint32_t *p0 = nullptr, *p1 = nullptr, *hist = nullptr;
-  int64_t* hpart = nullptr;
-  {  // context-owned workspace: z | perm 0 | perm 1 | bin | hist | shard, 16-B aligned pieces
+  const int64_t ntiles = (n + PTILE - 1) / PTILE;
+  uint4 *rec[2] = {nullptr, nullptr};
+  unsigned long long* status = nullptr;
+  uint32_t* counts = nullptr;
+  unsigned int* ctr = nullptr;
+  {  // context-owned workspace: records x 2 | granules | counts | tile counters, 16-B aligned pieces
     auto al = [](size_t v) { return (v + 15) & ~(size_t)15; };
-    const size_t a_z = al((size_t)n * 8), a_p = al((size_t)n * 4), a_b = al((size_t)n * 2),
-                 a_h = al((size_t)256 * grid * 4), a_s = sh ? al((size_t)n) : 0,
-                 a_pt = al((size_t)scan_partials_len((int64_t)256 * grid) * 8);
+    const size_t a_r = al((size_t)n * 16), a_st = al((size_t)ntiles * 256 * 8), a_c = al((size_t)MAXTAG * 256 * 4),
+                 a_t = al((size_t)MAXTAG * 4);
     void* base = nullptr;
-    int wrc = ctx_workspace(ctx, WS_SORT, a_z + 2 * a_p + a_b + a_h + a_pt + a_s, &base);
+    int wrc = ctx_workspace(ctx, WS_SORT, 2 * a_r + a_st + a_c + a_t, &base);
     if (wrc) return wrc;
     char* q = (char*)base;
-    tz = (uint64_t*)q; q += a_z;
-    p0 = (uint32_t*)q; q += a_p;
-    p1 = (uint32_t*)q; q += a_p;
-    tbin = (uint16_t*)q; q += a_b;
-    hist = (uint32_t*)q; q += a_h;
-    hpart = (int64_t*)q; q += a_pt;
-    if (sh) tsh = (uint8_t*)q;
+    rec[0] = (uint4*)q; q += a_r;
+    rec[1] = (uint4*)q; q += a_r;
+    status = (unsigned long long*)q; q += a_st;
+    counts = (uint32_t*)q; q += a_c;
+    ctr = (unsigned int*)q;
+    GM_HIP(hipMemsetAsync(status, 0, a_st + a_c + a_t, s));   // granules (tag 0 = none), counts, counters
   }
-  // digit passes at bit offsets `offs` (LSD order) from the caller's columns; the last pass lands in
-  // the user outputs when `to_user_last`, else in the workspace (read by k_sort_local); `perm64`:
-  // the last pass writes the 64-bit permutation
-  const uint8_t *rsh = nullptr;
-  const uint16_t* rbin = nullptr;
-  const uint64_t* rz = nullptr;
-  const uint32_t* rperm = nullptr;
-  auto passes = [&](const std::vector<int>& offs, bool to_user_last) -> int {
+  // digit passes at bit offsets `offs` (LSD order) from the caller's columns, tags tag0 + 1...; the
+  // last pass lands in the user outputs when `to_user_last`, else in records (*last_rec)
+  const uint4* last_rec = nullptr;
+  auto passes = [&](const std::vector<int>& offs, bool to_user_last, int tag0) -> int {
     const int np = (int)offs.size();
-    const uint8_t* ish = sh;
-    const uint16_t* ibin = (const uint16_t*)bin;
-    const uint64_t* iz = (const uint64_t*)z;
-    const uint32_t* iperm = nullptr;
+    DigitOffs o{};
+    o.np = np;
+    for (int k = 0; k < np; ++k) o.off[k] = offs[k];
+    uint32_t* cnt = counts + (size_t)tag0 * 256;
+    if (sh) hipLaunchKernelGGL(k_sort_count<true>, dim3(cgrid), dim3(CT), 0, s, in, n, o, cnt, user_vec);
+    else hipLaunchKernelGGL(k_sort_count<false>, dim3(cgrid), dim3(CT), 0, s, in, n, o, cnt, user_vec);
+    if (hipGetLastError() != hipSuccess) return hip_fail(hipErrorLaunchFailure, "k_sort_count");
     for (int k = 0; k < np; ++k) {
-      const bool to_user = ((np - 1 - k) % 2 == 0) == to_user_last;
-      uint8_t* osh = sh ? (to_user ? shard_out : tsh) : nullptr;
-      uint16_t* obin = to_user ? (uint16_t*)bin_out : tbin;
-      uint64_t* oz = to_user ? (uint64_t*)z_out : tz;
-      uint32_t* operm = (k % 2) ? p1 : p0;
-      // pass 0 reads the caller's columns, a later pass reads the caller's outputs or the workspace
-      const int vec = k == 0 ? (int)user_vec : (ibin == (const uint16_t*)bin_out ? (int)out_vec : 1);
-      hipLaunchKernelGGL(k_sort_hist, dim3(grid), dim3(HT), 0, s, ish, ibin, iz, n, per, offs[k], hist, vec);
-      launch_excl_scan(s, hist, (int64_t)256 * grid, hist, hpart, (int64_t*)nullptr);
-      const bool last64 = to_user_last && k == np - 1;   // the last pass writes the 64-bit permutation itself
-      auto scatter = sh ? (iperm ? k_sort_scatter<true, true> : k_sort_scatter<true, false>)
-                        : (iperm ? k_sort_scatter<false, true> : k_sort_scatter<false, false>);
-      hipLaunchKernelGGL(scatter, dim3(grid), dim3(BT), 0, s, ish, ibin, iz, iperm, osh, obin, oz,
-                         last64 ? nullptr : operm, last64 ? perm_out : nullptr, n, per, offs[k], hist, vec);
-      if (hipGetLastError() != hipSuccess) return hip_fail(hipErrorLaunchFailure, "k_sort_scatter");
-      ish = osh; ibin = obin; iz = oz; iperm = operm;
+      PassArgs a{};
+      a.in = in;
+      a.rec_in = k > 0 ? rec[(k - 1) & 1] : nullptr;
+      a.sh_out = shard_out; a.bin_out = (uint16_t*)bin_out; a.z_out = (uint64_t*)z_out; a.perm_out = perm_out;
+      a.rec_out = rec[k & 1];
+      a.n = n; a.off = offs[k]; a.tag = (uint32_t)(tag0 + k + 1);
+      a.counts = cnt + (size_t)k * 256;
+      a.status = status;
+      a.ctr = ctr + tag0 + k;
+      a.vec = user_vec;
+      const bool first = k == 0, user = to_user_last && k == np - 1;
+      void (*kern)(PassArgs) =
+          sh ? (first ? (user ? k_sort_pass<false, true, true> : k_sort_pass<false, false, true>)
+                      : (user ? k_sort_pass<true, true, true> : k_sort_pass<true, false, true>))
+             : (first ? (user ? k_sort_pass<false, true, false> : k_sort_pass<false, false, false>)
+                      : (user ? k_sort_pass<true, true, false> : k_sort_pass<true, false, false>));
+      hipLaunchKernelGGL(kern, dim3((unsigned)ntiles), dim3(PT), 0, s, a);
+      if (hipGetLastError() != hipSuccess) return hip_fail(hipErrorLaunchFailure, "k_sort_pass");
+      last_rec = rec[k & 1];
     }
-    rsh = ish; rbin = ibin; rz = iz; rperm = iperm;
     return GM_OK;
   };
   if (prefix_mode) {
     std::vector<int> offs(pofs, pofs + npre);
     std::reverse(offs.begin(), offs.end());   // LSD order: lowest digit first
-    int rc = passes(offs, false);
+    int rc = passes(offs, false, 0);
     if (rc) return rc;
     const int4 po = make_int4(pofs[0], pofs[1], pofs[2], pofs[3]);
     const int lgrid = resident_blocks((const void*)k_sort_local<false>, ctx->device, LT, 2);
     if (sh)
-      hipLaunchKernelGGL(k_sort_local<true>, dim3(lgrid), dim3(LT), 0, s, rsh, rbin, rz, rperm, shard_out,
-                         (uint16_t*)bin_out, (uint64_t*)z_out, perm_out, n, po, (uint32_t*)(acc + 4));
+      hipLaunchKernelGGL(k_sort_local<true>, dim3(lgrid), dim3(LT), 0, s, last_rec, shard_out, (uint16_t*)bin_out,
+                         (uint64_t*)z_out, perm_out, n, po, (uint32_t*)(acc + 4));
     else
-      hipLaunchKernelGGL(k_sort_local<false>, dim3(lgrid), dim3(LT), 0, s, rsh, rbin, rz, rperm, nullptr,
-                         (uint16_t*)bin_out, (uint64_t*)z_out, perm_out, n, po, (uint32_t*)(acc + 4));
+      hipLaunchKernelGGL(k_sort_local<false>, dim3(lgrid), dim3(LT), 0, s, last_rec, nullptr, (uint16_t*)bin_out,
+                         (uint64_t*)z_out, perm_out, n, po, (uint32_t*)(acc + 4));
     GM_CHECK_LAUNCH();
     uint32_t flag = 0;
     GM_HIP(hipMemcpyAsync(&flag, acc + 4, 4, hipMemcpyDeviceToHost, s));
@@ -637,7 +641,7 @@ int gm_sort_keys(gm_ctx* ctx, const uint8_t* shard, const int16_t* bin, const in
     // a run of equal prefixes longer than RUN_MAX: digit passes over every varying byte
   }
   ctx->sort_last = (int64_t)lsd.size() + (prefix_mode ? npre : 0);   // (a failed prefix attempt included)
-  return passes(lsd, true);
+  return passes(lsd, true, prefix_mode ? npre : 0);
 }
 
 }  // extern "C"

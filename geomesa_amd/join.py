@@ -152,7 +152,8 @@ class PolygonIndex:
 
     CENSUS = ["points", "outside", "coarse_empty", "coarse_interior", "coarse_raw_mixed", "fine", "fine_empty",
               "fine_interior", "fine_line", "fine_compact", "fine_generic", "fine_list", "list_entries",
-              "list_blobs", "line_resolved", "line_fallback", "fine_inline", "inline_fallback", "coarse_gather"]
+              "list_blobs", "line_resolved", "line_fallback", "fine_inline", "inline_fallback", "coarse_gather",
+              "fine_inline2"]
 
     def census(self, px, py):
         """Diagnostic: how the lookup chain resolves these points, stage by stage (gm_pip_join_census)."""

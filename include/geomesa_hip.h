@@ -103,8 +103,8 @@ const char* gm_last_error(void);
                                    memory: chunk k's result copy runs while chunk k + 1 computes (0 =
                                    default: one batch below 16384 queries, else about nq / 8 per chunk);
                                    the output never changes */
-#define GM_PARAM_SORT_MODE 4    /* gm_sort_keys: 0 (default) = up to four digit passes over the top
-                                   ~log2(n) + 3 varying key bits, then every run of equal prefixes ranked
+#define GM_PARAM_SORT_MODE 4    /* gm_sort_keys: 0 (default) = one to four digit passes over the top
+                                   ~log2(n) - 4 varying key bits, then every run of equal prefixes ranked
                                    in LDS (digit passes over every varying byte when a run exceeds 256
                                    rows); 1 = digit passes over every varying byte.  The output never
                                    changes */
@@ -273,12 +273,12 @@ int gm_pip_index_stats(const gm_pip_index* index, int64_t* stats);
    rects (4 * *n_core uint16, host memory) may be null. */
 int gm_pip_index_core(gm_ctx* ctx, const gm_pip_index* index, uint16_t* rects, int32_t* n_core);
 /* Diagnostic (no reference counterpart): how the join's lookup chain resolves the device points
-   px / py, stage by stage -- counters[19] = points, outside the grid, coarse EMPTY, coarse INTERIOR,
+   px / py, stage by stage -- counters[20] = points, outside the grid, coarse EMPTY, coarse INTERIOR,
    points in mixed coarse cells before the sub-block masks, fine lookups, fine EMPTY, fine INTERIOR,
    fine line entries, fine compact blobs, fine generic blobs, fine lists, list entries, list entries
    that are blobs, line entries that decide, line entries that fall back to the blob, fine words with
-   an inline line, inline lines that fall back to the blob, coarse-table gathers (points the LDS
-   EMPTY bitmap does not answer). */
+   inline lines, inline words that fall back to the blob, coarse-table gathers (points the LDS
+   EMPTY bitmap does not answer), fine words with two inline lines. */
 int gm_pip_join_census(gm_ctx* ctx, const gm_pip_index* index, const double* px, const double* py, int64_t n,
                        int64_t* counters);
 
@@ -449,7 +449,7 @@ int gm_z3_key_bytes(gm_ctx* ctx, const uint8_t* shard, const int16_t* bin, const
 /* Sorts key columns into the table's row order -- the byte order of the row keys above: shard,
    then bin as an unsigned big-endian short, then z as an unsigned big-endian long (what Accumulo /
    HBase keep sorted).  Stable; perm_out[i] = the input row of table row i.  shard / shard_out may
-   be NULL together (unsharded table).  n < 2^32.  Device temporaries: about 23 B per row. */
+   be NULL together (unsharded table).  n < 2^32.  Device temporaries: about 32.5 B per row. */
 int gm_sort_keys(gm_ctx* ctx, const uint8_t* shard, const int16_t* bin, const int64_t* z, int64_t n,
                  uint8_t* shard_out, int16_t* bin_out, int64_t* z_out, int64_t* perm_out);
 

@@ -117,6 +117,7 @@ def test_join_census_accounts_for_every_point(gpu):
     assert c["points"] == c["outside"] + c["coarse_empty"] + c["coarse_interior"] + c["fine"]
     assert c["fine"] == (c["fine_empty"] + c["fine_interior"] + c["fine_line"] + c["fine_compact"] + c["fine_generic"]
                          + c["fine_list"] + c["fine_inline"])
-    assert c["fine_inline"] > 0 and c["inline_fallback"] < c["fine_inline"]
+    assert c["fine_inline"] > c["fine_inline2"] > 0 and c["inline_fallback"] < c["fine_inline"]
+    assert c["coarse_gather"] <= c["points"] - c["outside"]
     assert c["fine_line"] == c["line_resolved"] + c["line_fallback"]
     assert c["outside"] >= 3 and c["fine"] > 0 and c["coarse_interior"] > 0

@@ -33,8 +33,8 @@ def expected_order(bins, z, shard=None):
 @pytest.mark.parametrize("sharded", [False, True])
 @pytest.mark.parametrize("mode", [0, 1])
 def test_sort_keys_parity(gpu, n, kind, sharded, mode):
-    """mode 0: prefix passes + local ranks (digit passes when a run of equal 24-bit prefixes exceeds
-    256 rows: "dups"); mode 1: digit passes over every varying byte (GM_PARAM_SORT_MODE)."""
+    """mode 0: prefix passes + local ranks (digit passes when a run of equal prefixes exceeds 256
+    rows: "dups"); mode 1: digit passes over every varying byte (GM_PARAM_SORT_MODE)."""
     import torch
     from geomesa_amd import _lib
     rng = np.random.default_rng(n + sharded)
@@ -80,7 +80,7 @@ def test_sort_keys_parity(gpu, n, kind, sharded, mode):
     if mode == 1:
         assert last < 256
     elif kind in ("rand", "keys", "narrow", "runs") and n > 100_000:
-        assert last >= 256 + 3, last          # prefix passes + local ranks
+        assert last > 256, last               # prefix passes + local ranks
     elif kind == "dups":
         assert last < 256 and last > 3, last  # runs > 256 rows: digit passes
 

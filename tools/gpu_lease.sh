@@ -14,7 +14,8 @@
 #   pmc:LEG          the counter groups below over one leg (join | table | ranges | hist | z3)
 #   ab:LEG:LIBS      alternating runs of one leg over variant libraries (geomesa_amd/lib/<lib>.so,
 #                    comma-separated; "prod" = the product library), 3 rounds
-#   probe:NAME       python tools/NAME.py (ranges_probe, hist_probe, sort_probe, query_probe, ...)
+#   probe:NAME       python tools/NAME.py $PROBE_ARGS (ranges_probe, hist_probe, sort_probe, query_probe, ...)
+#   abprobe:NAME:LIBS  the probe over variant libraries (as ab), 3 rounds, into one text file
 set -e
 tag=$1; shift
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
@@ -97,7 +98,17 @@ for step in "$@"; do
       unset GEOMESA_HIP_LIB
       python3 tools/show_ab.py ${out}_ab > ${out}_ab.txt ;;
     probe)
-      timeout -k 10 400 python -u tools/$arg.py > ${out}_$arg.txt 2>&1 ;;
+      timeout -k 10 400 python -u tools/$arg.py $PROBE_ARGS > ${out}_$arg.txt 2>&1 ;;
+    abprobe)
+      pname=${arg%%:*}; libs=${arg#*:}
+      for r in 1 2 3; do
+        for lib in ${libs//,/ }; do
+          if [ "$lib" = prod ]; then unset GEOMESA_HIP_LIB; else export GEOMESA_HIP_LIB=$PWD/geomesa_amd/lib/$lib.so; fi
+          echo "== $lib round $r" >> ${out}_abprobe_$pname.txt
+          timeout -k 10 300 python -u tools/$pname.py $PROBE_ARGS >> ${out}_abprobe_$pname.txt 2>&1
+        done
+      done
+      unset GEOMESA_HIP_LIB ;;
     *)
       echo "unknown step $step" >&2; exit 2 ;;
   esac
