@@ -283,7 +283,7 @@ def range_digest(offs, rr):
     return h.hexdigest()[:16]
 
 
-def cpu_ranges_baseline(kind, q, t, max_ranges, gpu_ms, nq, gpu_lists=None):
+def cpu_ranges_baseline(kind, q, t, max_ranges, gpu_ms, nq, gpu_lists=None, dev_ms=None):
     """The oracle's range decomposition of the same queries on the host's cores (all of them: the
     nodes-checked total is the work measure of the GPU batch too, SURVEY 8(d) ranges() row).  With the
     GPU's gathered (offsets, ranges), every query's merged list is compared with the oracle's
@@ -299,6 +299,8 @@ def cpu_ranges_baseline(kind, q, t, max_ranges, gpu_ms, nq, gpu_lists=None):
                                       % (nq, nt, dt, r)},
            "nodes_checked": nodes, "nodes_checked_per_s": nodes / (gpu_ms * 1e-3),
            "cpu_ranges": r}
+    if dev_ms:   # the same work measure over the device-output time (ranges left in HBM)
+        out["nodes_checked_per_s_device_output"] = nodes / (dev_ms * 1e-3)
     if gpu_lists is not None:
         _, _, coffs, crr = O.ranges_batch(kind, q, t, max_ranges=max_ranges, nthreads=nt, lists=True)
         goffs, grr = gpu_lists
@@ -956,13 +958,13 @@ def main():
                              qhi - qlo, nq)
         extra["xz2_ranges_batch"] = dict(m, note=note % ("XZ2", ""))
         if dist.rank == 0 and not a.no_cpu:
-            extra["xz2_ranges_batch"].update(cpu_ranges_baseline("xz2", win, None, 2000, m["ms_per_step"], nq, gl))
+            extra["xz2_ranges_batch"].update(cpu_ranges_baseline("xz2", win, None, 2000, m["ms_per_step"], nq, gl, m.get("device_output", {}).get("ms_per_step")))
         del gl
         m, gl = ranges_batch(dist, lib.gm_xz3_ranges, (h, qhi - qlo, woff.ctypes.data, wl3.ctypes.data, 12, 1, 2000),
                              qhi - qlo, nq)
         extra["xz3_ranges_batch"] = dict(m, note=note % ("XZ3", " x 1 min-2 days, week period"))
         if dist.rank == 0 and not a.no_cpu:
-            extra["xz3_ranges_batch"].update(cpu_ranges_baseline("xz3", win3, None, 2000, m["ms_per_step"], nq, gl))
+            extra["xz3_ranges_batch"].update(cpu_ranges_baseline("xz3", win3, None, 2000, m["ms_per_step"], nq, gl, m.get("device_output", {}).get("ms_per_step")))
         del gl
         # batched Z3 ranges (configs[4]/[0]): 4096 queries with target 2000
         rng = np.random.default_rng(1)
@@ -980,7 +982,7 @@ def main():
         if dist.rank == 0 and not a.no_cpu:
             qb = np.array([q[0][0] for q in qs], np.float64)
             qt = np.array([q[1][0] for q in qs], np.int64)
-            extra["z3_ranges_batch"].update(cpu_ranges_baseline("z3", qb, qt, 2000, m["ms_per_step"], len(qs), gl))
+            extra["z3_ranges_batch"].update(cpu_ranges_baseline("z3", qb, qt, 2000, m["ms_per_step"], len(qs), gl, m.get("device_output", {}).get("ms_per_step")))
         del gl
     # ---------------------------------------------------------------- configs[0]: 10M-point index + one query's ranges
     if "extra" in only and not a.no_extra:

@@ -9,16 +9,16 @@
 //   * gm_sort_keys     -- a stable sort of (shard u8, bin u16, z u64) in that byte order.  The key
 //                         K = shard:bin:z is an 88-bit integer; one read finds its varying bits (OR /
 //                         AND), a second counts every pass's digits at once (k_sort_count).  Then
-//                         one-sweep digit passes (8-bit digits, k_sort_pass): 4096-row tiles taken in
-//                         order, ranked in LDS (wave ballots rank equal digits), each tile's digit
-//                         offsets found by a decoupled look-back over the tiles before it (8-B
+//                         one-sweep digit passes (digits of <= 9 bits, k_sort_pass): 4096-row tiles
+//                         taken in order, ranked in LDS (wave ballots rank equal digits), each tile's
+//                         digit offsets found by a decoupled look-back over the tiles before it (8-B
 //                         {count, tag} granules), and the tile leaves as digit runs of 16-B records
 //                         {z, row, bin | shard << 16}.  The passes order the rows by the top
-//                         ~log2(n) - 4 varying bits; k_sort_local then ranks every run of equal
-//                         prefixes (~16 rows for 250M uniform keys) by full key in LDS and writes the
-//                         user columns.  A run longer than 256 rows (skewed keys) sends the call to
-//                         digit passes over every varying byte (LSD, the same kernels), which is also
-//                         GM_PARAM_SORT_MODE 1.
+//                         ~log2(n) - 1 varying bits (three 9-bit digits at 250M rows); k_sort_local
+//                         then ranks every run of equal prefixes (a few rows) by full key in LDS and
+//                         writes the user columns.  A run longer than 256 rows (skewed keys) sends the
+//                         call to 8-bit digit passes over every varying byte (LSD, the same kernels),
+//                         which is also GM_PARAM_SORT_MODE 1.
 // The range scan over a sorted table (gm_key_range_scan) lives with the other row-filter scans in
 // gm_filter.hip.
 #include <string.h>
@@ -119,17 +119,28 @@ __global__ __launch_bounds__(CT) void k_key_or_and(KeyCols c, int64_t n, unsigne
   }
 }
 
-// Every pass's digit counts in one read: counts[k * 256 + d] = rows whose digit at offs[k] is d.
-// Four LDS copies of the counters (by wave) cut the atomic collisions.
+// Every pass's digit counts in one read: counts[base_k + d] = rows whose digit k (bits [off_k, off_k +
+// w_k) of K) is d, base_k = k * 512.  Four LDS copies of the counters (by wave) cut the atomic
+// collisions.
+constexpr int WMAX = 9;                 // widest digit: 512 buckets
+constexpr int NB_MAX = 1 << WMAX;
 struct DigitOffs {
   int off[NPASS];
+  int w[NPASS];
   int np;
 };
+__device__ __forceinline__ uint32_t key_digit_w(uint32_t bs, uint64_t z, int off, int w) {
+  return key_bits(bs, z, off) & ((1u << w) - 1u);
+}
+constexpr int CNT_LDS = 2816;           // 11 byte digits x 256, or 4 prefix digits x 512 (<= 2048)
 template <bool SH>
 __global__ __launch_bounds__(CT) void k_sort_count(KeyCols c, int64_t n, DigitOffs o, uint32_t* __restrict__ counts, int vec) {
-  __shared__ uint32_t h[4][NPASS * 256];
+  __shared__ uint32_t h[4][CNT_LDS];
   const int copy = (threadIdx.x >> 6) & 3;
-  for (int i = threadIdx.x; i < 4 * o.np * 256; i += CT) h[i / (o.np * 256)][i % (o.np * 256)] = 0u;
+  int base[NPASS];
+  int tot = 0;
+  for (int k = 0; k < o.np; ++k) { base[k] = tot; tot += 1 << o.w[k]; }
+  for (int i = threadIdx.x; i < 4 * CNT_LDS; i += CT) (&h[0][0])[i] = 0u;
   __syncthreads();
   const int64_t step = (int64_t)gridDim.x * CT * 2 * CU4;
   for (int64_t i0 = ((int64_t)blockIdx.x * CT * CU4 + threadIdx.x) * 2; i0 < n; i0 += step) {
@@ -142,36 +153,32 @@ __global__ __launch_bounds__(CT) void k_sort_count(KeyCols c, int64_t n, DigitOf
 #pragma unroll
       for (int e = 0; e < 2; ++e)
         if (i0 + (int64_t)u * CT * 2 + e < n)
-          for (int k = 0; k < o.np; ++k) atomicAdd(&h[copy][k * 256 + key_digit(b[u][e], z[u][e], o.off[k])], 1u);
+          for (int k = 0; k < o.np; ++k) atomicAdd(&h[copy][base[k] + key_digit_w(b[u][e], z[u][e], o.off[k], o.w[k])], 1u);
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < o.np * 256; i += CT) {
-    const uint32_t v = h[0][i] + h[1][i] + h[2][i] + h[3][i];
-    if (v) atomicAdd(&counts[i], v);
-  }
+  for (int k = 0; k < o.np; ++k)
+    for (int d = threadIdx.x; d < (1 << o.w[k]); d += CT) {
+      const int i = base[k] + d;
+      const uint32_t v = h[0][i] + h[1][i] + h[2][i] + h[3][i];
+      if (v) atomicAdd(&counts[k * NB_MAX + d], v);
+    }
 }
 
-// One-sweep digit pass.  Block b takes tile k (the next in a counter, so every lower tile is already
-// running) of 4096 rows; wave w owns rows [512 w, 512 w + 512) of it and reads them in 4 slots of 128
-// rows, 2 per lane.  Within a slot, lanes holding the same digit find each other with 16 ballots
-// (8 digit bits x even / odd row); a per-wave LDS counter per digit turns slot ranks into wave
-// ranks, a scan over the waves into tile ranks, so a row's place in the tile is (digit, wave, slot,
-// lane, even / odd) = stable.  The tile's digit offsets in the output are the digit's global start
-// plus its rows in every lower tile: each of 256 threads publishes its digit's tile count as soon as
-// the tile is ranked ({count, AGG} granule, one 8-B write-through store), then walks back over the
-// lower tiles' granules, adding counts until it meets an inclusive prefix (PRE), and publishes its
-// own (decoupled look-back).  The tile is reordered in LDS meanwhile and leaves as digit runs
-// (16 rows on average: 256-B record runs).  Granule tags carry the pass (tag) so no pass reads
-// another's; the status array is cleared once per call.
+// One-sweep digit pass over a digit of w <= 9 bits.  Block b takes tile k (the next in a counter, so
+// every lower tile is already running) of 4096 rows; wave w owns rows [512 w, 512 w + 512) of it and
+// reads them in 4 slots of 128 rows, 2 per lane.  Within a slot, lanes holding the same digit find each
+// other with 2 w ballots (w digit bits x even / odd row); a per-wave LDS counter per digit turns slot
+// ranks into wave ranks, a scan over the waves into tile ranks, so a row's place in the tile is
+// (digit, wave, slot, lane, even / odd) = stable.  The tile's digit offsets in the output are the
+// digit's global start plus its rows in every lower tile: thread d publishes digit d's tile count as
+// soon as the tile is ranked ({count, AGG} granule, one 8-B write-through store), then walks back over
+// the lower tiles' granules, adding counts until it meets an inclusive prefix (PRE), and publishes its
+// own (decoupled look-back).  The tile is reordered in LDS meanwhile and leaves as digit runs of 16-B
+// records.  Granule tags carry the pass (tag) so no pass reads another's; the status array is cleared
+// once per call.  LDS 78 KB: two blocks (16 waves) per CU.
 constexpr int PT = 512, PW = PT / 64, PSLOT = 4, PTILE = PT * 2 * PSLOT;   // 4096 rows per tile
+static_assert(PT >= NB_MAX, "one thread per digit");
 constexpr uint64_t GR_VAL = (1ull << 48) - 1;
-
-__device__ __forceinline__ uint64_t digit_mask(const uint64_t* bal, uint32_t d) {
-  uint64_t m = ~0ull;
-#pragma unroll
-  for (int bit = 0; bit < 8; ++bit) m &= ((d >> bit) & 1u) ? bal[bit] : ~bal[bit];
-  return m;
-}
 
 struct PassArgs {
   KeyCols in;             // the caller's columns (first pass) ...
@@ -182,10 +189,10 @@ struct PassArgs {
   int64_t* perm_out;
   uint4* rec_out;         // ... or records
   int64_t n;
-  int off;                // digit bit offset
+  int off, w;             // digit: bits [off, off + w) of K
   uint32_t tag;           // 1..MAXTAG
-  const uint32_t* counts;           // this pass's 256 digit counts
-  unsigned long long* status;       // ntiles x 256 granules
+  const uint32_t* counts;           // this pass's 2^w digit counts
+  unsigned long long* status;       // ntiles x 2^w granules
   unsigned int* ctr;                // this pass's tile counter
   int vec;
 };
@@ -193,14 +200,15 @@ struct PassArgs {
 template <bool IN_REC, bool OUT_USER, bool SH>
 __global__ __launch_bounds__(PT) void k_sort_pass(PassArgs a) {
   __shared__ uint4 s_rec[PTILE];
-  __shared__ uint16_t s_wcnt[PW][256];   // per wave: rows of each digit so far (then: wave offsets)
-  __shared__ uint32_t s_tot[256], s_dstart[256], s_base[256];
-  __shared__ long long s_gpos[256];
-  __shared__ uint32_t s_wsum[2][4];
+  __shared__ uint16_t s_wcnt[PW][NB_MAX];   // per wave: rows of each digit so far (then: wave offsets)
+  __shared__ uint32_t s_dstart[NB_MAX];     // the digit's first slot in the tile
+  __shared__ uint32_t s_gpos[NB_MAX];       // output row of tile slot q = s_gpos[d] + q (mod 2^32)
+  __shared__ uint32_t s_wsum[2][PW];
   __shared__ uint32_t s_tile;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int w = a.w, nb = 1 << w;
   if (t == 0) s_tile = atomicAdd(a.ctr, 1u);
-  for (int i = t; i < PW * 256 / 2; i += PT) ((uint32_t*)&s_wcnt[0][0])[i] = 0u;
+  for (int i = t; i < PW * NB_MAX / 2; i += PT) ((uint32_t*)&s_wcnt[0][0])[i] = 0u;
   __syncthreads();
   const int64_t tile = s_tile, t0 = tile * PTILE, n = a.n;
   // this lane's rows
@@ -226,18 +234,21 @@ __global__ __launch_bounds__(PT) void k_sort_pass(PassArgs a) {
   for (int k = 0; k < PSLOT; ++k) {
     const int64_t i = t0 + wave * (2 * 64 * PSLOT) + k * 128 + 2 * lane;
     const bool ok0 = i < n, ok1 = i + 1 < n;
-    const uint32_t d0 = key_digit(rv[k][0].w, rec_z(rv[k][0]), a.off);
-    const uint32_t d1 = key_digit(rv[k][1].w, rec_z(rv[k][1]), a.off);
-    uint64_t bal0[8], bal1[8];
-#pragma unroll
-    for (int bit = 0; bit < 8; ++bit) {
-      bal0[bit] = __ballot((d0 >> bit) & 1u);
-      bal1[bit] = __ballot((d1 >> bit) & 1u);
-    }
-    const uint64_t okm0 = __ballot(ok0), okm1 = __ballot(ok1);
+    const uint32_t d0 = key_digit_w(rv[k][0].w, rec_z(rv[k][0]), a.off, w);
+    const uint32_t d1 = key_digit_w(rv[k][1].w, rec_z(rv[k][1]), a.off, w);
     // masks of lanes whose even / odd row holds my even / odd row's digit
-    const uint64_t m00 = digit_mask(bal0, d0) & okm0, m01 = digit_mask(bal1, d0) & okm1;
-    const uint64_t m10 = digit_mask(bal0, d1) & okm0, m11 = digit_mask(bal1, d1) & okm1;
+    uint64_t m00 = __ballot(ok0), m01 = __ballot(ok1);
+    uint64_t m10 = m00, m11 = m01;
+#pragma unroll
+    for (int bit = 0; bit < WMAX; ++bit) {
+      if (bit < w) {   // wave-uniform
+        const uint64_t b0 = __ballot((d0 >> bit) & 1u), b1 = __ballot((d1 >> bit) & 1u);
+        m00 &= ((d0 >> bit) & 1u) ? b0 : ~b0;
+        m01 &= ((d0 >> bit) & 1u) ? b1 : ~b1;
+        m10 &= ((d1 >> bit) & 1u) ? b0 : ~b0;
+        m11 &= ((d1 >> bit) & 1u) ? b1 : ~b1;
+      }
+    }
     const uint64_t le = lt | (1ull << lane);
     const int r0 = __popcll(m00 & lt) + __popcll(m01 & lt);
     const int r1 = __popcll(m10 & le) + __popcll(m11 & lt);
@@ -251,34 +262,36 @@ __global__ __launch_bounds__(PT) void k_sort_pass(PassArgs a) {
     __builtin_amdgcn_wave_barrier();
   }
   __syncthreads();
+  // thread t owns digit t (t < nb): wave offsets, the tile total, scans of totals and global counts
   uint32_t tot = 0, xt = 0, xb = 0, cg = 0;
-  if (t < 256) {   // per digit: exclusive offsets over the waves, the tile total; scans over the digits
+  const bool own = t < nb;
+  if (own) {
 #pragma unroll
-    for (int w = 0; w < PW; ++w) {
-      const uint32_t c = s_wcnt[w][t];
-      s_wcnt[w][t] = (uint16_t)tot;
+    for (int v = 0; v < PW; ++v) {
+      const uint32_t c = s_wcnt[v][t];
+      s_wcnt[v][t] = (uint16_t)tot;
       tot += c;
     }
-    s_tot[t] = tot;
-    cg = a.counts[t];
-    xt = tot; xb = cg;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t y = __shfl_up(xt, o, 64), yb = __shfl_up(xb, o, 64);
-      if (lane >= o) { xt += y; xb += yb; }
-    }
-    if (lane == 63) { s_wsum[0][wave] = xt; s_wsum[1][wave] = xb; }
     // the tile's count for this digit, published before anything else
-    const uint64_t agg = ((uint64_t)(2 * a.tag) << 48) | tot;
-    const uint64_t pre = ((uint64_t)(2 * a.tag + 1) << 48) | tot;
-    __hip_atomic_store(a.status + tile * 256 + t, tile == 0 ? pre : agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t g0 = ((uint64_t)(2 * a.tag + (tile == 0 ? 1 : 0)) << 48) | tot;
+    __hip_atomic_store(a.status + tile * nb + t, g0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    cg = a.counts[t];
   }
+  xt = tot; xb = cg;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(xt, o, 64), yb = __shfl_up(xb, o, 64);
+    if (lane >= o) { xt += y; xb += yb; }
+  }
+  if (lane == 63) { s_wsum[0][wave] = xt; s_wsum[1][wave] = xb; }
   __syncthreads();
-  if (t < 256) {
+  uint32_t dstart = 0, gbase = 0;
+  if (own) {
     uint32_t pt = 0, pb = 0;
-    for (int w = 0; w < wave; ++w) { pt += s_wsum[0][w]; pb += s_wsum[1][w]; }
-    s_dstart[t] = pt + xt - tot;
-    s_base[t] = pb + xb - cg;
+    for (int v = 0; v < wave; ++v) { pt += s_wsum[0][v]; pb += s_wsum[1][v]; }
+    dstart = pt + xt - tot;
+    gbase = pb + xb - cg;
+    s_dstart[t] = dstart;
   }
   __syncthreads();
   // the tile reordered by digit in LDS
@@ -291,28 +304,28 @@ __global__ __launch_bounds__(PT) void k_sort_pass(PassArgs a) {
       s_rec[s_dstart[d] + s_wcnt[wave][d] + r] = rv[k][e];
     }
   }
-  if (t < 256) {   // look-back: the digit's rows in every lower tile
+  if (own) {   // look-back: the digit's rows in every lower tile
     uint64_t excl = 0;
     if (tile > 0) {
       const uint64_t tag_agg = 2 * a.tag, tag_pre = 2 * a.tag + 1;
       int64_t p = tile - 1;
       for (;;) {
-        const uint64_t v = __hip_atomic_load(a.status + p * 256 + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t v = __hip_atomic_load(a.status + p * nb + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const uint64_t tg = v >> 48;
         if (tg == tag_pre) { excl += v & GR_VAL; break; }
         if (tg == tag_agg) { excl += v & GR_VAL; --p; }
         else __builtin_amdgcn_s_sleep(1);
       }
-      __hip_atomic_store(a.status + tile * 256 + t, ((uint64_t)(2 * a.tag + 1) << 48) | (excl + s_tot[t]),
+      __hip_atomic_store(a.status + tile * nb + t, ((uint64_t)(2 * a.tag + 1) << 48) | (excl + tot),
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    s_gpos[t] = (long long)s_base[t] + (long long)excl - (long long)s_dstart[t];
+    s_gpos[t] = gbase + (uint32_t)excl - dstart;   // mod 2^32: every output row is < n <= 2^32 - 1
   }
   __syncthreads();
   const int cnt = (int)min((int64_t)PTILE, n - t0);
   for (int q = t; q < cnt; q += PT) {
     const uint4 r = s_rec[q];
-    const int64_t g = s_gpos[key_digit(r.w, rec_z(r), a.off)] + q;
+    const int64_t g = (int64_t)(uint32_t)(s_gpos[key_digit_w(r.w, rec_z(r), a.off, w)] + (uint32_t)q);
     if (OUT_USER) {
       a.z_out[g] = rec_z(r);
       a.bin_out[g] = (uint16_t)r.w;
@@ -326,8 +339,8 @@ __global__ __launch_bounds__(PT) void k_sort_pass(PassArgs a) {
 
 // Final placement after the prefix passes: the digit passes at bit offsets o1 > o2 > ... (each digit
 // ends at a varying bit, and only constant bits lie between them) leave the rows grouped, stably, by
-// P = digit(o1) : digit(o2) : ... -- the key's top varying bits, ~log2(n) - 4 of them, so that runs
-// of equal P are short (Poisson(n / 2^bits) for uniform keys, 16 rows on average).  Tile k covers the
+// P = digit(o1) : digit(o2) : ... -- the key's top varying bits, ~log2(n) - 1 of them, so that runs
+// of equal P are short (Poisson(n / 2^bits) for uniform keys, 2 rows on average).  Tile k covers the
 // runs of equal P that start in [k LSTEP, (k + 1) LSTEP); its rows are staged in LDS, a block scan
 // marks each row's run (start, and at the start its end), each row counts the rows of its run with a
 // smaller key (ties by position: stable) and goes to run start + rank: O(run length) LDS reads per
@@ -335,34 +348,35 @@ __global__ __launch_bounds__(PT) void k_sort_pass(PassArgs a) {
 // digit passes over every varying byte instead.
 constexpr int LT = 512, LCAP = 4096, LPT = LCAP / LT, RUN_MAX = 256, LSTEP = LCAP - RUN_MAX;
 
-// the prefix digits (offsets o.x > o.y > ...; an offset < 0: no digit)
-__device__ __forceinline__ uint32_t prefix4(uint32_t bs, uint64_t z, int4 o) {
-  uint32_t p = 0;
-  p = (p << 8) | (o.x >= 0 ? key_digit(bs, z, o.x) : 0u);
-  p = (p << 8) | (o.y >= 0 ? key_digit(bs, z, o.y) : 0u);
-  p = (p << 8) | (o.z >= 0 ? key_digit(bs, z, o.z) : 0u);
-  p = (p << 8) | (o.w >= 0 ? key_digit(bs, z, o.w) : 0u);
+// the prefix digits of width w (offsets o.x > o.y > ...; an offset < 0: no digit)
+__device__ __forceinline__ uint64_t prefix4(uint32_t bs, uint64_t z, int4 o, int w) {
+  uint64_t p = 0;
+  p = (p << w) | (o.x >= 0 ? key_digit_w(bs, z, o.x, w) : 0u);
+  p = (p << w) | (o.y >= 0 ? key_digit_w(bs, z, o.y, w) : 0u);
+  p = (p << w) | (o.z >= 0 ? key_digit_w(bs, z, o.z, w) : 0u);
+  p = (p << w) | (o.w >= 0 ? key_digit_w(bs, z, o.w, w) : 0u);
   return p;
 }
 
 template <bool SH>
 __global__ __launch_bounds__(LT) void k_sort_local(const uint4* __restrict__ rec_in, uint8_t* __restrict__ sh_out,
                                                    uint16_t* __restrict__ bin_out, uint64_t* __restrict__ z_out,
-                                                   int64_t* __restrict__ perm_out, int64_t n, int4 po,
+                                                   int64_t* __restrict__ perm_out, int64_t n, int4 po, int pw,
                                                    uint32_t* __restrict__ flag) {
   __shared__ uint64_t s_z[LCAP];
   __shared__ uint32_t s_bs[LCAP];
-  __shared__ uint32_t s_run[LCAP];   // prefix; then run start (low 16) | at a run start, its end << 16
+  __shared__ uint32_t s_run[LCAP];   // run start (low 16) | at a run start, its end << 16
+  __shared__ uint8_t s_new[LCAP];    // the row starts a new prefix
   __shared__ int64_t s_ab[2];
   __shared__ uint32_t s_wmax[LT / 64];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  auto pre_of = [&](int64_t r) -> uint32_t { const uint4 v = rec_in[r]; return prefix4(v.w, rec_z(v), po); };
+  auto pre_of = [&](int64_t r) -> uint64_t { const uint4 v = rec_in[r]; return prefix4(v.w, rec_z(v), po, pw); };
   const int64_t ntile = (n + LSTEP - 1) / LSTEP;
   for (int64_t tk = blockIdx.x; tk < ntile; tk += gridDim.x) {   // block-uniform
     if (wave < 2) {   // waves 0 / 1: the first run start at or after p (none within RUN_MAX rows: flag)
       int64_t p = min(n, (tk + wave) * LSTEP);
       if (p > 0 && p < n) {
-        const uint32_t pp = pre_of(p - 1);
+        const uint64_t pp = pre_of(p - 1);
         int64_t found = -1;
         for (int c = 0; c <= RUN_MAX / 64 && found < 0; ++c) {   // wave-uniform
           const int64_t r = p + c * 64 + lane;
@@ -383,8 +397,11 @@ __global__ __launch_bounds__(LT) void k_sort_local(const uint4* __restrict__ rec
     for (int i = t; i < m; i += LT) {
       const uint4 v = rec_in[a + i];
       const uint64_t zz = rec_z(v);
-      s_z[i] = zz; s_bs[i] = v.w; s_run[i] = prefix4(v.w, zz, po);
+      s_z[i] = zz; s_bs[i] = v.w;
     }
+    __syncthreads();
+    for (int i = t; i < m; i += LT)
+      s_new[i] = i == 0 || prefix4(s_bs[i], s_z[i], po, pw) != prefix4(s_bs[i - 1], s_z[i - 1], po, pw);
     __syncthreads();
     // run starts: a block max-scan of (row starts a run ? row : 0) over rows [LPT t, LPT t + LPT)
     uint32_t st[LPT];
@@ -392,7 +409,7 @@ __global__ __launch_bounds__(LT) void k_sort_local(const uint4* __restrict__ rec
 #pragma unroll
     for (int k = 0; k < LPT; ++k) {
       const int i = LPT * t + k;
-      if (i < m && (i == 0 || s_run[i] != s_run[i - 1])) run = (uint32_t)i;
+      if (i < m && s_new[i]) run = (uint32_t)i;
       st[k] = run;
     }
     uint32_t x = run;
@@ -409,7 +426,6 @@ __global__ __launch_bounds__(LT) void k_sort_local(const uint4* __restrict__ rec
     if (lane > 0) carry = max(carry, prev);
 #pragma unroll
     for (int k = 0; k < LPT; ++k) st[k] = max(st[k], carry);
-    __syncthreads();   // every prefix read before s_run is overwritten
 #pragma unroll
     for (int k = 0; k < LPT; ++k)
       if (LPT * t + k < m) s_run[LPT * t + k] = st[k];
@@ -541,14 +557,16 @@ int gm_sort_keys(gm_ctx* ctx, const uint8_t* shard, const int16_t* bin, const in
     ctx->sort_last = 0;
     return GM_OK;
   }
-  // prefix passes: digits each ending at the highest varying bit below the previous one (only constant
-  // bits are skipped), ceil((log2 n - 4) / 8) of them (1..4: runs of ~16 equal prefixes for uniform
-  // keys), when that is fewer than the varying bytes
+  // prefix passes: npre digits of pw <= 9 bits, each ending at the highest varying bit below the
+  // previous one (only constant bits are skipped), over the top ~log2(n) - 1 varying bits (runs of
+  // ~2 equal prefixes for uniform keys), when that is fewer passes than the varying bytes
   const uint64_t vz = hacc[0] ^ hacc[2], vb = (hacc[1] ^ hacc[3]) & 0xffffffull;
   auto varying = [&](int bit) -> bool { return bit < 64 ? ((vz >> bit) & 1u) : ((vb >> (bit - 64)) & 1u); };
   int lg = 0;
   while (((int64_t)1 << lg) < n) ++lg;
-  const int npre = std::max(1, std::min(4, (lg - 4 + 7) / 8));
+  const int pbits = std::max(1, lg - 1);
+  const int npre = std::min(4, (pbits + WMAX - 1) / WMAX);
+  const int pw = std::min(WMAX, (pbits + npre - 1) / npre);
   int pofs[4] = {-1, -1, -1, -1};
   int nfound = 0;
   {
@@ -556,7 +574,7 @@ int gm_sort_keys(gm_ctx* ctx, const uint8_t* shard, const int16_t* bin, const in
     for (int k = 0; k < npre; ++k) {
       while (bit >= 0 && !varying(bit)) --bit;
       if (bit < 0) break;
-      pofs[k] = std::max(0, bit - 7);
+      pofs[k] = std::max(0, bit - (pw - 1));
       bit = pofs[k] - 1;
       ++nfound;
     }
@@ -569,7 +587,7 @@ int gm_sort_keys(gm_ctx* ctx, const uint8_t* shard, const int16_t* bin, const in
   unsigned int* ctr = nullptr;
   {  // context-owned workspace: records x 2 | granules | counts | tile counters, 16-B aligned pieces
     auto al = [](size_t v) { return (v + 15) & ~(size_t)15; };
-    const size_t a_r = al((size_t)n * 16), a_st = al((size_t)ntiles * 256 * 8), a_c = al((size_t)MAXTAG * 256 * 4),
+    const size_t a_r = al((size_t)n * 16), a_st = al((size_t)ntiles * NB_MAX * 8), a_c = al((size_t)MAXTAG * NB_MAX * 4),
                  a_t = al((size_t)MAXTAG * 4);
     void* base = nullptr;
     int wrc = ctx_workspace(ctx, WS_SORT, 2 * a_r + a_st + a_c + a_t, &base);
@@ -585,12 +603,12 @@ int gm_sort_keys(gm_ctx* ctx, const uint8_t* shard, const int16_t* bin, const in
   // digit passes at bit offsets `offs` (LSD order) from the caller's columns, tags tag0 + 1...; the
   // last pass lands in the user outputs when `to_user_last`, else in records (*last_rec)
   const uint4* last_rec = nullptr;
-  auto passes = [&](const std::vector<int>& offs, bool to_user_last, int tag0) -> int {
+  auto passes = [&](const std::vector<int>& offs, int w, bool to_user_last, int tag0) -> int {
     const int np = (int)offs.size();
     DigitOffs o{};
     o.np = np;
-    for (int k = 0; k < np; ++k) o.off[k] = offs[k];
-    uint32_t* cnt = counts + (size_t)tag0 * 256;
+    for (int k = 0; k < np; ++k) { o.off[k] = offs[k]; o.w[k] = w; }
+    uint32_t* cnt = counts + (size_t)tag0 * NB_MAX;
     if (sh) hipLaunchKernelGGL(k_sort_count<true>, dim3(cgrid), dim3(CT), 0, s, in, n, o, cnt, user_vec);
     else hipLaunchKernelGGL(k_sort_count<false>, dim3(cgrid), dim3(CT), 0, s, in, n, o, cnt, user_vec);
     if (hipGetLastError() != hipSuccess) return hip_fail(hipErrorLaunchFailure, "k_sort_count");
@@ -600,8 +618,8 @@ int gm_sort_keys(gm_ctx* ctx, const uint8_t* shard, const int16_t* bin, const in
       a.rec_in = k > 0 ? rec[(k - 1) & 1] : nullptr;
       a.sh_out = shard_out; a.bin_out = (uint16_t*)bin_out; a.z_out = (uint64_t*)z_out; a.perm_out = perm_out;
       a.rec_out = rec[k & 1];
-      a.n = n; a.off = offs[k]; a.tag = (uint32_t)(tag0 + k + 1);
-      a.counts = cnt + (size_t)k * 256;
+      a.n = n; a.off = offs[k]; a.w = w; a.tag = (uint32_t)(tag0 + k + 1);
+      a.counts = cnt + (size_t)k * NB_MAX;
       a.status = status;
       a.ctr = ctr + tag0 + k;
       a.vec = user_vec;
@@ -620,16 +638,16 @@ int gm_sort_keys(gm_ctx* ctx, const uint8_t* shard, const int16_t* bin, const in
   if (prefix_mode) {
     std::vector<int> offs(pofs, pofs + npre);
     std::reverse(offs.begin(), offs.end());   // LSD order: lowest digit first
-    int rc = passes(offs, false, 0);
+    int rc = passes(offs, pw, false, 0);
     if (rc) return rc;
     const int4 po = make_int4(pofs[0], pofs[1], pofs[2], pofs[3]);
     const int lgrid = resident_blocks((const void*)k_sort_local<false>, ctx->device, LT, 2);
     if (sh)
       hipLaunchKernelGGL(k_sort_local<true>, dim3(lgrid), dim3(LT), 0, s, last_rec, shard_out, (uint16_t*)bin_out,
-                         (uint64_t*)z_out, perm_out, n, po, (uint32_t*)(acc + 4));
+                         (uint64_t*)z_out, perm_out, n, po, pw, (uint32_t*)(acc + 4));
     else
       hipLaunchKernelGGL(k_sort_local<false>, dim3(lgrid), dim3(LT), 0, s, last_rec, nullptr, (uint16_t*)bin_out,
-                         (uint64_t*)z_out, perm_out, n, po, (uint32_t*)(acc + 4));
+                         (uint64_t*)z_out, perm_out, n, po, pw, (uint32_t*)(acc + 4));
     GM_CHECK_LAUNCH();
     uint32_t flag = 0;
     GM_HIP(hipMemcpyAsync(&flag, acc + 4, 4, hipMemcpyDeviceToHost, s));
@@ -641,7 +659,7 @@ int gm_sort_keys(gm_ctx* ctx, const uint8_t* shard, const int16_t* bin, const in
     // a run of equal prefixes longer than RUN_MAX: digit passes over every varying byte
   }
   ctx->sort_last = (int64_t)lsd.size() + (prefix_mode ? npre : 0);   // (a failed prefix attempt included)
-  return passes(lsd, true, prefix_mode ? npre : 0);
+  return passes(lsd, 8, true, prefix_mode ? npre : 0);
 }
 
 }  // extern "C"

@@ -104,7 +104,7 @@ const char* gm_last_error(void);
                                    default: one batch below 16384 queries, else about nq / 8 per chunk);
                                    the output never changes */
 #define GM_PARAM_SORT_MODE 4    /* gm_sort_keys: 0 (default) = one to four digit passes over the top
-                                   ~log2(n) - 4 varying key bits, then every run of equal prefixes ranked
+                                   ~log2(n) - 1 varying key bits, then every run of equal prefixes ranked
                                    in LDS (digit passes over every varying byte when a run exceeds 256
                                    rows); 1 = digit passes over every varying byte.  The output never
                                    changes */

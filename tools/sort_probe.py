@@ -1,5 +1,5 @@
-"""Times gm_sort_keys on the bench's table leg (250M rows of Z3 keys of uniform points over 8
-weeks, optionally with a 4-way shard byte) and checks the result on the GPU: keys in table order,
+"""Times gm_sort_keys on the bench's table leg (250M rows of Z3 keys of uniform points over 2020,
+53 week bins, optionally with a 4-way shard byte) and checks the result on the GPU: keys in table order,
 perm a permutation that maps the output back to the input.  For A/B runs of library builds
 (GEOMESA_HIP_LIB) in one GPU call.
 
@@ -22,7 +22,7 @@ def main(n=250_000_000, sharded=False):
     g = torch.Generator(device=dev).manual_seed(7)
     x = torch.rand(n, device=dev, generator=g, dtype=torch.float64) * 360 - 180
     y = torch.rand(n, device=dev, generator=g, dtype=torch.float64) * 180 - 90
-    t = (torch.rand(n, device=dev, generator=g, dtype=torch.float64) * 8 * 604800000).to(torch.int64) + 1590969600000
+    t = (torch.rand(n, device=dev, generator=g, dtype=torch.float64) * 31622400000).to(torch.int64) + 1577836800000
     b, z = Z3SFC("week").index_keys(x, y, t)
     del x, y, t
     sh = (torch.arange(n, device=dev) % 4).to(torch.uint8) if sharded else None
