@@ -427,48 +427,23 @@ def ranges_batch(dist, fn, args, n_local, nq, reps=3):
 
 
 def sort_bytes(b, z, n, last):
-    """Algorithmic bytes of gm_sort_keys over n rows, for the path the library reports
+    """Algorithmic bytes of gm_sort_keys over n unsharded rows, for the path the library reports
     (GM_PARAM_SORT_LAST: digit passes, + 256 when the runs of equal prefixes were ranked locally):
-    the OR/AND read of the key columns that finds the varying bits (10 B/row); per digit pass a
-    histogram read of the columns its 8 bits touch (8 B z and/or 2 B bin) and a scatter that reads and
-    writes z, bin and the 4-B permutation (none read on the first pass); then either the local ranking
-    (reads z, bin, the 4-B permutation; writes z, bin, an 8-B permutation: 32 B/row) or, for the plain
-    digit passes, the last pass writing the permutation as 8 B.  Returns (bytes, passes, path)."""
-    import torch
+    the OR/AND read of the key columns that finds the varying bits and the read that counts every
+    pass's digits (10 B/row each); the first pass reads the columns (10 B) and writes 16-B records
+    {z, row, bin}, every later pass reads and writes records (32 B); then the local ranking reads the
+    records and writes z, bin and the 8-B permutation (16 + 18 B), or the last digit pass writes those
+    itself (18 B instead of 16).  Returns (bytes, passes, path)."""
     local = last >= 256
     npass = last - 256 if local else last
-    total = 10.0 * n
-    if local:   # npass digit passes over the top varying bits of K = bin:z (the library's greedy choice:
-        # each digit ends at the highest varying bit below the previous one)
-        bb = b.to(torch.int64) & 0xFFFF
-
-        def varies(bit):
-            col, sh = (z, bit) if bit < 64 else (bb, bit - 64)
-            v = (col >> sh) & 1
-            return int(v.min()) != int(v.max())
-        offs, bit = [], 79
-        for _ in range(npass):
-            while bit >= 0 and not varies(bit):
-                bit -= 1
-            offs.append(max(0, bit - 7))
-            bit = offs[-1] - 1
-        for k, off in enumerate(reversed(offs)):
-            h = (8 if off < 64 else 0) + (2 if off + 8 > 64 else 0)
-            total += (h + 28.0 - (4.0 if k == 0 else 0.0)) * n
-        total += 32.0 * n
-        return total, npass, "prefix passes + local ranks"
-    passes = []
-    for p in range(8):
-        d = (z >> (8 * p)) & 255
-        if int(d.min()) != int(d.max()):
-            passes.append(8)
-    bb = b.to(torch.int32) & 0xFFFF
-    for p in range(2):
-        d = (bb >> (8 * p)) & 255
-        if int(d.min()) != int(d.max()):
-            passes.append(2)
-    total += sum(h + 28.0 for h in passes) * n - (4.0 * n if passes else 0) + (4.0 * n if passes else 0)
-    return total, len(passes), "digit passes"
+    total = 20.0 * n
+    if npass:
+        total += (10.0 + 16.0 + 32.0 * (npass - 1)) * n
+    if local:
+        total += 34.0 * n
+        return total, npass, "one-sweep prefix passes + local ranks"
+    total += 2.0 * n if npass else 0.0
+    return total, npass, "one-sweep digit passes"
 
 
 # Chip-wide access rates measured by tools/gather_probe.hip on MI355X (profiles/r2_gather_probe*.log:
@@ -608,15 +583,16 @@ def bench_table(a, dist, ctx, b, z):
                       "rows_per_gpu": NT, "digit_passes": npass, "path": spath,
                       "roofline": dict(roofline(sbytes, ms_sort), bytes_per_unit=round(sbytes / NT, 2),
                                        kernel="gm_sort_keys (all launches of one sort)"),
-                      "note": "stable sort of (bin, z) into table byte order (ingest side): digit passes over the top "
-                              "~log2(n) + 3 varying key bits, then every run of equal prefixes ranked by full key in LDS "
-                              "(digit passes over every varying byte when a run exceeds 256 rows); bytes = 10 B/row "
-                              "OR/AND read + per pass (digit column read + 28 B/row scatter, no permutation read on the "
-                              "first) + 32 B/row local ranking (see sort_bytes)"},
+                      "note": "stable sort of (bin, z) into table byte order (ingest side): one-sweep digit passes "
+                              "(look-back, 16-B records) over the top ~log2(n) - 1 varying key bits, then every run of "
+                              "equal prefixes ranked by full key in LDS (8-bit digit passes over every varying byte when "
+                              "a run exceeds 256 rows); bytes: see sort_bytes"},
         "table_ingest": {"value": NT * dist.world / (ms_ingest * 1e-3), "unit": "rows/s", "ms_per_step": ms_ingest,
                          "rows_per_gpu": NT, "slice_rows": slice_rows,
                          "note": "key-range partitioned table: local sort, splitter sampling (1024 keys per rank), "
-                                 "all-to-all of the rows by key range (24 B/row), sort of the received slice"},
+                                 "all-to-all of the rows by key range (24 B/row), sort of the received slice; the "
+                                 "slice keeps its ids in arrival order beside the sort's permutation (a query maps "
+                                 "only its matches); at world 1 the local sort is the table"},
         "table_query": {"value": 1.0 / (ms_scan * 1e-3), "unit": "queries/s", "ms_per_step": ms_scan,
                         "table_rows": NT * dist.world, "ranges": nr, "ranges_scanned_rank0": res["ncl"],
                         "rows_scanned": int(scanned), "matches": int(matches), "plan_ms": round(plan_ms, 2),

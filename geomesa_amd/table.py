@@ -133,7 +133,10 @@ class PartitionedZ3Table:
     the key's first byte).  A query's scan ranges (getRangeBytes, Z3IndexKeySpace.scala:196-238) are
     clipped to the slice's first and last key (the per-tablet range binning of a batch scanner) and
     each rank scans only those; the ids that come back are global row ids, so the union over ranks
-    equals the scan of one unpartitioned table.  pg None = a single unpartitioned slice."""
+    equals the scan of one unpartitioned table.  The slice keeps the ids in the order its rows arrived
+    (src_ids) beside the table's permutation, so a scan maps only its matches to ids (the seek
+    already resolves table rows through the permutation) instead of the ingest permuting every id.
+    pg None = a single unpartitioned slice."""
 
     def __init__(self, pg, bins, z, ids, shard=None, shards=None, period="week", samples=1024):
         import torch
@@ -145,7 +148,7 @@ class PartitionedZ3Table:
             self.table, self.splitters = local, (np.zeros(0, np.int64), np.zeros(0, np.int64))
             if sharded and shards:
                 self.table.shards = int(shards)
-            self.gid = torch.as_tensor(ids).to(local.z.device, torch.int64)[local.perm]
+            self.src_ids = torch.as_tensor(ids).to(local.z.device, torch.int64)
             self.n = local.n
             self._bounds()
             return
@@ -159,7 +162,7 @@ class PartitionedZ3Table:
         if sharded:
             self.table.shards = int(shards) if shards else (
                 int(S.all_reduce_scalar(pg, float(self.table.shards or 0), "max")))
-        self.gid = gid[self.table.perm]   # global row id of each table row
+        self.src_ids = gid   # global row id of each received row (the table's perm maps table rows to them)
         self.n = self.table.n
         self._bounds()
 
@@ -190,8 +193,8 @@ class PartitionedZ3Table:
         """(global row ids of this slice's matches, n_match, n_scanned, n_ranges scanned)."""
         arr, _ = key_ranges(scan_ranges, self.table.shards)
         arr = self.clip(arr)
-        ids, nm, ns = self.table.scan_key_ranges(arr, z3filter, map_rows=False)
-        return self.gid[ids], nm, ns, len(arr)
+        rows, nm, ns = self.table.scan_key_ranges(arr, z3filter, map_rows=True)   # input rows of the slice
+        return self.src_ids[rows], nm, ns, len(arr)
 
     def query(self, bboxes=None, intervals=None, target=2000):
         """bbox + during query (Z3Filter on the rows of the clipped ranges) on this rank's slice."""
