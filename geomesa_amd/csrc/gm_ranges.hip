@@ -1,9 +1,9 @@
 // gm_ranges.hip -- batched range decomposition: ZN.zranges (Z2/Z3) and XZ2/XZ3 ranges on gfx950.
 //
-// One 256-thread workgroup per query.  The Scala code walks a FIFO queue one node at a time
-// (ZN.scala:193-218, XZ2SFC.scala:205-227) and its maxRanges budget truncates at an exact FIFO
-// position.  Here a whole tree level is processed in parallel and the FIFO semantics are
-// reconstructed with block-wide prefix sums:
+// Z curves: one 256-thread workgroup per query (k_zranges).  XZ curves: one 64-lane wave per query
+// (k_xzranges_w, below).  The Scala code walks a FIFO queue one node at a time (ZN.scala:193-218,
+// XZ2SFC.scala:205-227) and its maxRanges budget truncates at an exact FIFO position.  Here a whole
+// tree level is processed in parallel and the FIFO semantics are reconstructed with prefix sums:
 //
 //   Z curves   after node i of a level the queue holds (K-i-1) level nodes + the queued children,
 //              so the budget fires at the first i with
@@ -15,9 +15,10 @@
 //                 nR + A(i-1) >= rangeStop        (A = inclusive count of non-disjoint elements);
 //              bottom-out emits full intervals at the current and the next level (:219-227).
 //
-// Emitted ranges are tree nodes that never nest, so after the walk they are disjoint; an LDS
-// bitonic sort on `lower` (global memory above 4096 ranges) followed by a parallel adjacency merge
-// reproduces the sort + merge of ZN.scala:221-241 / XZ2SFC.scala:231-249 exactly.
+// Z: emitted ranges are tree nodes that never nest, so after the walk they are disjoint; a merge of
+// the walk's sorted runs by rank (or an LDS bitonic sort) followed by a parallel adjacency merge
+// reproduces the sort + merge of ZN.scala:221-241 exactly.  XZ: the sorted order follows from subtree
+// counts (no comparison sort) and the merge is a ballot per 64 ranges (XZ2SFC.scala:231-249).
 //
 // Frontier and range lists live in per-query global workspaces (HBM is plentiful); the zbounds /
 // normalized query windows sit in LDS.
