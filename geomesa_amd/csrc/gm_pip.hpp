@@ -94,6 +94,13 @@ enum : uint32_t { PIP_FAULT_LINE = 1, PIP_FAULT_COMPACT = 2, PIP_FAULT_BLOB = 4,
 __device__ __forceinline__ void pip_fault(const PipDev& d, uint32_t code) {
   if (d.fault) atomicOr(d.fault, code);
 }
+// a reference / queue check; GM_NO_REF_CHECKS (timing variant only) compiles every check out to price
+// them
+#ifdef GM_NO_REF_CHECKS
+#define GM_REF_BAD(c) (false)
+#else
+#define GM_REF_BAD(c) (c)
+#endif
 
 
 #ifndef GM_CF_LOG
@@ -439,7 +446,7 @@ __device__ __forceinline__ int item_locate(const PipDev& d, uint32_t ref, double
   int loc = -1;
   if ((ref & BLOB_COMPACT) && d.line_ent && (ref & SC_LINE)) {
     const uint64_t li = ref & (SC_LINE - 1);
-    if (li >= (uint64_t)d.n_line) { pip_fault(d, PIP_FAULT_LINE); poly = -1; return LOC_EXTERIOR; }
+    if (GM_REF_BAD(li >= (uint64_t)d.n_line)) { pip_fault(d, PIP_FAULT_LINE); poly = -1; return LOC_EXTERIOR; }
     const uint4 e0 = d.line_ent[2 * li], e1 = d.line_ent[2 * li + 1];
     poly = (int)e0.y;
     loc = line_locate(e0, e1, x, y, d);
@@ -448,10 +455,10 @@ __device__ __forceinline__ int item_locate(const PipDev& d, uint32_t ref, double
   if (loc >= 0) return loc;
   if (ref & BLOB_COMPACT) {
     const uint64_t ci = ref & (BLOB_COMPACT - 1);
-    if (ci >= (uint64_t)d.n_compact_lines) { pip_fault(d, PIP_FAULT_COMPACT); poly = -1; return LOC_EXTERIOR; }
+    if (GM_REF_BAD(ci >= (uint64_t)d.n_compact_lines)) { pip_fault(d, PIP_FAULT_COMPACT); poly = -1; return LOC_EXTERIOR; }
     return compact_locate((const dv2*)(d.compact + 16 * ci), x, y, poly);
   }
-  if ((uint64_t)ref >= (uint64_t)d.n_blob16) { pip_fault(d, PIP_FAULT_BLOB); poly = -1; return LOC_EXTERIOR; }
+  if (GM_REF_BAD((uint64_t)ref >= (uint64_t)d.n_blob16)) { pip_fault(d, PIP_FAULT_BLOB); poly = -1; return LOC_EXTERIOR; }
   const double* b = d.blob + 2 * (uint64_t)ref;
   const int2 h = *(const int2*)b;
   poly = h.x;

@@ -242,7 +242,7 @@ __global__ __launch_bounds__(QTPB) void k_pip_join_q(const double* __restrict__ 
   auto item_push = [&](bool valid, bool is_line, double x, double y, uint32_t id, uint32_t ref) __attribute__((always_inline)) {
     const uint64_t ml = __ballot(valid && is_line), mb = __ballot(valid && !is_line);
     if (!(ml | mb)) return;
-    if (qn + qg + 64 > ICAP) { if (lane == 0) pip_fault(d, PIP_FAULT_QUEUE); return; }   // cannot happen: < 64 here
+    if (GM_REF_BAD(qn + qg + 64 > ICAP)) { if (lane == 0) pip_fault(d, PIP_FAULT_QUEUE); return; }   // cannot happen: < 64 here
     if (valid) {
       const int o = is_line ? qn + lanes_below(ml) : ICAP - 1 - qg - lanes_below(mb);
       qx[o] = x; qy[o] = y; qid[o] = id; qref[o] = ref;
@@ -308,7 +308,7 @@ __global__ __launch_bounds__(QTPB) void k_pip_join_q(const double* __restrict__ 
         uint32_t blob = 0;
         if (act) {
           const uint64_t li = ref & (SC_LINE - 1);
-          if (li >= (uint64_t)d.n_line) { pip_fault(d, PIP_FAULT_LINE); loc = LOC_EXTERIOR; }
+          if (GM_REF_BAD(li >= (uint64_t)d.n_line)) { pip_fault(d, PIP_FAULT_LINE); loc = LOC_EXTERIOR; }
           else {
             const uint4 e0 = d.line_ent[2 * li], e1 = d.line_ent[2 * li + 1];
             poly = (int)e0.y;
@@ -369,9 +369,9 @@ __global__ __launch_bounds__(QTPB) void k_pip_join_q(const double* __restrict__ 
         l_slot = slot;
         l_lo = 4 * (int)(ref >> 4);
         l_n = (int)(w & 15u);
-        if ((int64_t)l_lo + 4 > d.n_list) { pip_fault(d, PIP_FAULT_LIST); l_n = 0; }
+        if (GM_REF_BAD((int64_t)l_lo + 4 > d.n_list)) { pip_fault(d, PIP_FAULT_LIST); l_n = 0; }
         else if (l_n == LIST_LONG) { l_n = (int)d.list_ent[l_lo]; l_lo += 1; }
-        if (l_n < 0 || (int64_t)l_lo + l_n > d.n_list) { pip_fault(d, PIP_FAULT_LIST); l_n = 0; }
+        if (GM_REF_BAD(l_n < 0 || (int64_t)l_lo + l_n > d.n_list)) { pip_fault(d, PIP_FAULT_LIST); l_n = 0; }
       }
       list_on = __ballot(l_j < l_n) != 0;
       fn = pb;   // the window is released (its list walks run next, before anything can push to the queue)
@@ -424,7 +424,7 @@ __global__ __launch_bounds__(QTPB) void k_pip_join_q(const double* __restrict__ 
       pair_push((c1 >> 30) == CELL_INTERIOR, id1, (int)(c1 & 0x3fffffffu));
       const bool f0 = (c0 >> 30) == CELL_LIST, f1 = (c1 >> 30) == CELL_LIST;
       const uint64_t m0 = __ballot(f0), m1 = __ballot(f1);
-      if (fn + 128 > FCAP) { if (lane == 0 && (m0 | m1)) pip_fault(d, PIP_FAULT_QUEUE); }   // cannot happen: fn < 128
+      if (GM_REF_BAD(fn + 128 > FCAP)) { if (lane == 0 && (m0 | m1)) pip_fault(d, PIP_FAULT_QUEUE); }   // cannot happen: fn < 128
       else {
         if (f0) { const int o = fn + lanes_below(m0); fx[o] = X0; fy[o] = Y0; fid[o] = id0; }
         fn += __popcll(m0);

@@ -25,7 +25,7 @@ template <int OP>
 __device__ __forceinline__ bool entry_pred(const PipDev& d, uint32_t e, double px, double py) {
   if ((e >> 30) == CELL_INTERIOR) return true;   // every point of the cell is interior
   const uint32_t ref = e & 0x3fffffffu;
-  if (!blob_ref_ok(d, ref)) { pip_fault(d, PIP_FAULT_BLOB); return false; }
+  if (GM_REF_BAD(!blob_ref_ok(d, ref))) { pip_fault(d, PIP_FAULT_BLOB); return false; }
   int loc;
   if (ref & BLOB_COMPACT) {
     int poly;
@@ -129,9 +129,9 @@ __global__ __launch_bounds__(FTPB, GM_QUERY_WAVES) void k_query_mask(const doubl
       bool hit;
       if ((w >> 30) == CELL_LIST) {
         int l0 = 4 * (int)((w & 0x3fffffffu) >> 4), ni = (int)(w & 15u);
-        if ((int64_t)l0 + 4 > d.n_list) { pip_fault(d, PIP_FAULT_LIST); ni = 0; }
+        if (GM_REF_BAD((int64_t)l0 + 4 > d.n_list)) { pip_fault(d, PIP_FAULT_LIST); ni = 0; }
         else if (ni == LIST_LONG) { ni = (int)d.list_ent[l0]; l0 += 1; }
-        if (ni < 0 || (int64_t)l0 + ni > d.n_list) { pip_fault(d, PIP_FAULT_LIST); ni = 0; }
+        if (GM_REF_BAD(ni < 0 || (int64_t)l0 + ni > d.n_list)) { pip_fault(d, PIP_FAULT_LIST); ni = 0; }
         hit = false;
         for (int j = 0; j < ni && !hit; ++j) hit = entry_pred<OP>(d, d.list_ent[l0 + j], px, py);
       } else {

@@ -20,7 +20,7 @@ constexpr uint8_t LOC_NULL = 0xff;
 __device__ __forceinline__ int entry_locate(const PipDev& d, uint32_t e, double px, double py) {
   if ((e >> 30) == CELL_INTERIOR) return LOC_INTERIOR;
   const uint32_t ref = e & 0x3fffffffu;
-  if (!blob_ref_ok(d, ref)) { pip_fault(d, PIP_FAULT_BLOB); return LOC_EXTERIOR; }
+  if (GM_REF_BAD(!blob_ref_ok(d, ref))) { pip_fault(d, PIP_FAULT_BLOB); return LOC_EXTERIOR; }
   if (ref & BLOB_COMPACT) {
     int poly;
     return compact_locate((const dv2*)(d.compact + 16 * (uint64_t)(ref & (BLOB_COMPACT - 1))), px, py, poly);
@@ -148,7 +148,7 @@ __global__ __launch_bounds__(RTPB) void k_pip_relate(const int32_t* __restrict__
         } else if (kind == CELL_LIST) {
           int l0 = 4 * (int)((e & 0x3fffffffu) >> 4), ni = (int)(e & 15u);
           bool found = false;
-          if ((int64_t)l0 + 4 > d.n_list) { pip_fault(d, PIP_FAULT_LIST); ni = 0; }
+          if (GM_REF_BAD((int64_t)l0 + 4 > d.n_list)) { pip_fault(d, PIP_FAULT_LIST); ni = 0; }
           else if (ni <= 4) {
             // a short list is one 16-B group (lists start at multiples of 4 slots): its polygon ids
             // and entries in two independent loads instead of a serial search
@@ -163,7 +163,7 @@ __global__ __launch_bounds__(RTPB) void k_pip_relate(const int32_t* __restrict__
             else found = false;
             ni = 0;
           } else if (ni == LIST_LONG) { ni = (int)d.list_ent[l0]; l0 += 1; }
-          if (ni < 0 || (int64_t)l0 + ni > d.n_list) { pip_fault(d, PIP_FAULT_LIST); ni = 0; }
+          if (GM_REF_BAD(ni < 0 || (int64_t)l0 + ni > d.n_list)) { pip_fault(d, PIP_FAULT_LIST); ni = 0; }
           int j = 0;
           while (j < ni && list_poly[l0 + j] != p[u]) ++j;
           if (j < ni) { e = d.list_ent[l0 + j]; found = true; }
