@@ -137,9 +137,6 @@ template <bool SH>
 __global__ __launch_bounds__(CT) void k_sort_count(KeyCols c, int64_t n, DigitOffs o, uint32_t* __restrict__ counts, int vec) {
   __shared__ uint32_t h[4][CNT_LDS];
   const int copy = (threadIdx.x >> 6) & 3;
-  int base[NPASS];
-  int tot = 0;
-  for (int k = 0; k < o.np; ++k) { base[k] = tot; tot += 1 << o.w[k]; }
   for (int i = threadIdx.x; i < 4 * CNT_LDS; i += CT) (&h[0][0])[i] = 0u;
   __syncthreads();
   const int64_t step = (int64_t)gridDim.x * CT * 2 * CU4;
@@ -153,12 +150,13 @@ __global__ __launch_bounds__(CT) void k_sort_count(KeyCols c, int64_t n, DigitOf
 #pragma unroll
       for (int e = 0; e < 2; ++e)
         if (i0 + (int64_t)u * CT * 2 + e < n)
-          for (int k = 0; k < o.np; ++k) atomicAdd(&h[copy][base[k] + key_digit_w(b[u][e], z[u][e], o.off[k], o.w[k])], 1u);
+          for (int k = 0, bk = 0; k < o.np; bk += 1 << o.w[k], ++k)
+            atomicAdd(&h[copy][bk + key_digit_w(b[u][e], z[u][e], o.off[k], o.w[k])], 1u);
   }
   __syncthreads();
-  for (int k = 0; k < o.np; ++k)
+  for (int k = 0, bk = 0; k < o.np; bk += 1 << o.w[k], ++k)
     for (int d = threadIdx.x; d < (1 << o.w[k]); d += CT) {
-      const int i = base[k] + d;
+      const int i = bk + d;
       const uint32_t v = h[0][i] + h[1][i] + h[2][i] + h[3][i];
       if (v) atomicAdd(&counts[k * NB_MAX + d], v);
     }
