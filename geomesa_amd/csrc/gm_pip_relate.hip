@@ -114,19 +114,21 @@ __global__ __launch_bounds__(RTPB) void k_pip_relate(const int32_t* __restrict__
       }
       // the fine words (8 B, boundary shortcuts applied; a one-line cell decides from its inline line)
       int pre[RILP];   // a location the inline line decided, else -1
+      uint2 w8[RILP];   // every row's load issued before any is inspected
 #pragma unroll
       for (int u = 0; u < RILP; ++u) {
         pre[u] = -1;
-        if ((w[u] >> 30) == CELL_LIST) {
-          const int64_t c = (int64_t)cy[u] * d.gx + cx[u];
-          const uint2 w8 = d.cell_sc8[c];
-          w[u] = w8.x;
-          if (sc8_inline(w8)) {
-            w[u] = CELL_EMPTY << 30;
-            if (sc8_poly(w8) != p[u]) pre[u] = LOC_EXTERIOR;   // the cell's one entry is another polygon's
-            else if ((pre[u] = sc8_locate(w8, x[u], y[u], d, cx[u], cy[u])) < 0)
-              w[u] = d.cell_word[c];   // near the line: the original word's blob decides
-          }
+        w8[u] = make_uint2(w[u], 0u);
+        if ((w[u] >> 30) == CELL_LIST) w8[u] = d.cell_sc8[(int64_t)cy[u] * d.gx + cx[u]];
+      }
+#pragma unroll
+      for (int u = 0; u < RILP; ++u) {
+        w[u] = w8[u].x;
+        if (sc8_inline(w8[u])) {
+          w[u] = CELL_EMPTY << 30;
+          if (sc8_poly(w8[u]) != p[u]) pre[u] = LOC_EXTERIOR;   // the cell's one entry is another polygon's
+          else if ((pre[u] = sc8_locate(w8[u], x[u], y[u], d, cx[u], cy[u])) < 0)
+            w[u] = d.cell_word[(int64_t)cy[u] * d.gx + cx[u]];   // near the line: the original word's blob decides
         }
       }
       uint8_t rv[RILP];

@@ -17,7 +17,6 @@
 // 64-bit device counters (scattered per-lane device atomics run ~22 G/s on MI355X, so they only win
 // over many passes).
 #include <cmath>
-#include <type_traits>
 
 #include "gm_keys.hpp"
 
@@ -137,6 +136,21 @@ __device__ __forceinline__ int hist_slot_top(double x, double y, int64_t ms, con
 // in flight and never carries into its neighbour.  The final flush adds half - NB.
 constexpr uint32_t NB = 0x8000u, NS = 0x4000u;
 
+__device__ __forceinline__ void narrow_inc(uint32_t* w, int sh, unsigned long long* g) {
+  const uint32_t old = atomicAdd(w, 1u << sh);
+  if (((old >> sh) & 0xFFFFu) == NB + NS - 1) {
+    atomicSub(w, NS << sh);
+    atomicAdd(g, (unsigned long long)NS);
+  }
+}
+__device__ __forceinline__ void narrow_dec(uint32_t* w, int sh, unsigned long long* g) {
+  const uint32_t old = atomicSub(w, 1u << sh);
+  if (((old >> sh) & 0xFFFFu) == NB - NS + 1) {
+    atomicAdd(w, NS << sh);
+    atomicAdd(g, (unsigned long long)(-(long long)NS));
+  }
+}
+
 template <int PERIOD, bool UNOBS, bool VEC, bool NARROW, bool TOP>
 __global__ __launch_bounds__(HTPB) void k_z3_hist_lds(const double* __restrict__ x, const double* __restrict__ y,
                                                       const int64_t* __restrict__ t, HistArgs a,
@@ -158,53 +172,25 @@ __global__ __launch_bounds__(HTPB) void k_z3_hist_lds(const double* __restrict__
   if (threadIdx.x == 0) { s_skip = 0; s_out = 0; }
   __syncthreads();
   int skip = 0, out = 0;
-  // the LDS counter of one feature in this pass's rows, or -1
-  auto slot = [&](double xx, double yy, int64_t tt) -> int {
+  auto one = [&](double xx, double yy, int64_t tt) {
     int rb = 0;
     int c = TOP ? hist_slot_top<PERIOD, UNOBS>(xx, yy, tt, a, sp, rb, skip, out)
                 : hist_slot_tab<PERIOD, UNOBS>(xx, yy, tt, a, sp, rb, skip, out);
     rb -= a.row_lo;
-    if (c < 0 || rb < 0 || rb >= a.row_n) return -1;
+    if (c < 0 || rb < 0 || rb >= a.row_n) return;
     c -= a.row_lo * a.length;
-    if (UNOBS && !pres[rb]) return -1;    // binMap.get(timeBin).foreach(_.add(z, -1))
-    return c;
-  };
-  // K features' increments (decrements) issued together, then the 16-bit halves' carry checks: a
-  // check right after each returning atomic would wait for it before the next one issues
-  auto add = [&](const int* c, auto k_const) __attribute__((always_inline)) {
-    constexpr int K = decltype(k_const)::value;
-    if (!NARROW) {
-#pragma unroll
-      for (int k = 0; k < K; ++k)
-        if (c[k] >= 0) atomicAdd(&cnt[c[k]], UNOBS ? -1 : 1);
-      return;
-    }
-    uint32_t old[K];
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const int sh = (c[k] & 1) * 16;
-      if (c[k] >= 0) old[k] = UNOBS ? atomicSub((uint32_t*)&cnt[c[k] >> 1], 1u << sh) : atomicAdd((uint32_t*)&cnt[c[k] >> 1], 1u << sh);
-    }
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      if (c[k] < 0) continue;
-      const int sh = (c[k] & 1) * 16;
-      const uint32_t h = (old[k] >> sh) & 0xFFFFu;
-      if (!UNOBS && h == NB + NS - 1) {   // this increment lifted the half to NB + NS: move NS out
-        atomicSub((uint32_t*)&cnt[c[k] >> 1], NS << sh);
-        atomicAdd(&counts[c[k]], (unsigned long long)NS);
+    if (UNOBS) {
+      if (pres[rb]) {                        // binMap.get(timeBin).foreach(_.add(z, -1))
+        if (NARROW) narrow_dec((uint32_t*)&cnt[c >> 1], (c & 1) * 16, &counts[c]);
+        else atomicAdd(&cnt[c], -1);
       }
-      if (UNOBS && h == NB - NS + 1) {
-        atomicAdd((uint32_t*)&cnt[c[k] >> 1], NS << sh);
-        atomicAdd(&counts[c[k]], (unsigned long long)(-(long long)NS));
-      }
+    } else {
+      if (NARROW) narrow_inc((uint32_t*)&cnt[c >> 1], (c & 1) * 16, &counts[c]);
+      else atomicAdd(&cnt[c], 1);
       // binMap.getOrElseUpdate(timeBin, newBins): a row is present iff one of its features was
       // counted; int32 counters only grow here, so the flush derives it from the row (no per-point
       // LDS read); biased 16-bit halves move to the device counters and cannot tell, so they mark it
-      if (!UNOBS) {
-        const int rb = c[k] / a.length;
-        if (!pres[rb]) pres[rb] = 1;
-      }
+      if (NARROW && !pres[rb]) pres[rb] = 1;
     }
   };
   const int64_t stride = (int64_t)gridDim.x * HTPB;
@@ -235,26 +221,16 @@ __global__ __launch_bounds__(HTPB) void k_z3_hist_lds(const double* __restrict__
         const int64_t q = pn + u * stride;
         if (q < np) { xb[u] = ld_stream(&x2[q]); yb[u] = ld_stream(&y2[q]); tb[u] = ld_stream(&t2[q]); }
       }
-      int c[2 * HU];
 #pragma unroll
       for (int u = 0; u < HU; ++u) {
-        const bool ok = p + u * stride < np;
-        c[2 * u] = ok ? slot(xa[u].x, ya[u].x, ta[u].x) : -1;
-        c[2 * u + 1] = ok ? slot(xa[u].y, ya[u].y, ta[u].y) : -1;
+        if (p + u * stride < np) { one(xa[u].x, ya[u].x, ta[u].x); one(xa[u].y, ya[u].y, ta[u].y); }
         xa[u] = xb[u]; ya[u] = yb[u]; ta[u] = tb[u];
       }
-      add(c, std::integral_constant<int, 2 * HU>());
       p = pn;
     }
-    if ((a.n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
-      const int c1 = slot(x[a.n - 1], y[a.n - 1], t[a.n - 1]);
-      add(&c1, std::integral_constant<int, 1>());
-    }
+    if ((a.n & 1) && blockIdx.x == 0 && threadIdx.x == 0) one(x[a.n - 1], y[a.n - 1], t[a.n - 1]);
   } else {
-    for (int64_t i = (int64_t)blockIdx.x * HTPB + threadIdx.x; i < a.n; i += stride) {
-      const int c1 = slot(x[i], y[i], t[i]);
-      add(&c1, std::integral_constant<int, 1>());
-    }
+    for (int64_t i = (int64_t)blockIdx.x * HTPB + threadIdx.x; i < a.n; i += stride) one(x[i], y[i], t[i]);
   }
   if (skip) atomicAdd(&s_skip, skip);
   if (out) atomicAdd(&s_out, out);

@@ -16,6 +16,7 @@
 #                    comma-separated; "prod" = the product library), 3 rounds
 #   probe:NAME       python tools/NAME.py $PROBE_ARGS (ranges_probe, hist_probe, sort_probe, query_probe, ...)
 #   abprobe:NAME:LIBS  the probe over variant libraries (as ab), 3 rounds, into one text file
+#   kprobe:NAME:LIB  rocprofv3 --kernel-trace --stats of one probe run with one library (prod = shipped)
 set -e
 tag=$1; shift
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
@@ -38,8 +39,8 @@ for step in "$@"; do
   echo "[$(date +%T)] $step" >> ${out}_steps.log
   case $name in
     tests)
-      k=${arg:+-k $arg}
-      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v $k --timeout 300 --timeout-method thread \
+      if [ -n "$arg" ]; then kk=(-k "$arg"); else kk=(); fi
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v "${kk[@]}" --timeout 300 --timeout-method thread \
         > ${out}_tests.log 2>&1 ;;
     smoke)
       timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > ${out}_smoke.log 2>&1 ;;
@@ -109,6 +110,13 @@ for step in "$@"; do
         done
       done
       unset GEOMESA_HIP_LIB ;;
+    kprobe)
+      pname=${arg%%:*}; lib=${arg#*:}
+      if [ "$lib" = prod ]; then unset GEOMESA_HIP_LIB; else export GEOMESA_HIP_LIB=$PWD/geomesa_amd/lib/$lib.so; fi
+      timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d ${out}_kprobe_${pname}_$lib -o run -- \
+        python3 tools/$pname.py $PROBE_ARGS > ${out}_kprobe_${pname}_$lib.txt 2>&1
+      unset GEOMESA_HIP_LIB
+      python3 tools/kstats.py ${out}_kprobe_${pname}_$lib >> ${out}_kprobe_${pname}_$lib.txt 2>&1 || true ;;
     *)
       echo "unknown step $step" >&2; exit 2 ;;
   esac
