@@ -112,25 +112,9 @@ __global__ __launch_bounds__(RTPB) void k_pip_relate(const int32_t* __restrict__
           }
         }
       }
-      // the fine words (8 B, boundary shortcuts applied; a one-line cell decides from its inline line)
-      int pre[RILP];   // a location the inline line decided, else -1
-      uint2 w8[RILP];   // every row's load issued before any is inspected
 #pragma unroll
-      for (int u = 0; u < RILP; ++u) {
-        pre[u] = -1;
-        w8[u] = make_uint2(w[u], 0u);
-        if ((w[u] >> 30) == CELL_LIST) w8[u] = d.cell_sc8[(int64_t)cy[u] * d.gx + cx[u]];
-      }
-#pragma unroll
-      for (int u = 0; u < RILP; ++u) {
-        w[u] = w8[u].x;
-        if (sc8_inline(w8[u])) {
-          w[u] = CELL_EMPTY << 30;
-          if (sc8_poly(w8[u]) != p[u]) pre[u] = LOC_EXTERIOR;   // the cell's one entry is another polygon's
-          else if ((pre[u] = sc8_locate(w8[u], x[u], y[u], d, cx[u], cy[u])) < 0)
-            w[u] = d.cell_word[(int64_t)cy[u] * d.gx + cx[u]];   // near the line: the original word's blob decides
-        }
-      }
+      for (int u = 0; u < RILP; ++u)
+        if ((w[u] >> 30) == CELL_LIST) w[u] = d.cell_sc[(int64_t)cy[u] * d.gx + cx[u]];   // boundary shortcuts applied
       uint8_t rv[RILP];
       bool dir[RILP];
 #pragma unroll
@@ -141,8 +125,6 @@ __global__ __launch_bounds__(RTPB) void k_pip_relate(const int32_t* __restrict__
         const uint32_t kind = e >> 30;
         if (p[u] < 0 || p[u] >= n_polys) {
           r = LOC_NULL;
-        } else if (pre[u] >= 0) {
-          r = (uint8_t)pre[u];
         } else if (kind == CELL_INTERIOR) {
           r = (int)(e & 0x3fffffffu) == p[u] ? LOC_INTERIOR : LOC_EXTERIOR;
         } else if (kind == CELL_BOUNDARY) {

@@ -96,23 +96,38 @@ __device__ __forceinline__ uint64_t wave_and(uint64_t v) {
   for (int o = 32; o > 0; o >>= 1) v &= __shfl_xor(v, o, 64);
   return v;
 }
-constexpr int CT = 1024;   // or/and and count threads per block
-constexpr int CU4 = 4;     // pairs per lane per step
-template <bool SH>
-__global__ __launch_bounds__(CT) void k_key_or_and(KeyCols c, int64_t n, unsigned long long* __restrict__ acc, int vec) {
-  uint64_t zo = 0, za = ~0ull, bo = 0, ba = ~0ull;
-  const int64_t step = (int64_t)gridDim.x * CT * 2 * CU4;
-  for (int64_t i0 = ((int64_t)blockIdx.x * CT * CU4 + threadIdx.x) * 2; i0 < n; i0 += step) {
-    uint64_t z[CU4][2];
-    uint32_t b[CU4][2];
-#pragma unroll
-    for (int u = 0; u < CU4; ++u) load_pair<SH>(c, i0 + (int64_t)u * CT * 2, n, vec, z[u][0], z[u][1], b[u][0], b[u][1]);
-#pragma unroll
-    for (int u = 0; u < CU4; ++u)
-#pragma unroll
-      for (int e = 0; e < 2; ++e)
-        if (i0 + (int64_t)u * CT * 2 + e < n) { zo |= z[u][e]; za &= z[u][e]; bo |= b[u][e]; ba &= b[u][e]; }
+// f(z, bs) over every row of the caller's columns, pairs of rows per lane (16-B z, 4-B bin, 2-B shard
+// loads when `vec`), two pairs in flight; thread `tid` of `nthreads`
+template <bool SH, class F>
+__device__ __forceinline__ void for_rows(const KeyCols& c, int64_t n, int vec, int64_t tid, int64_t nthreads, F f) {
+  const int64_t np = n >> 1;
+  auto pair = [&](int64_t p, uint64_t& z0, uint64_t& z1, uint32_t& b0, uint32_t& b1) __attribute__((always_inline)) {
+    load_pair<SH>(c, 2 * p, n, vec, z0, z1, b0, b1);
+  };
+  int64_t p = tid;
+  for (; p + nthreads < np; p += 2 * nthreads) {
+    uint64_t z0, z1, z2, z3;
+    uint32_t b0, b1, b2, b3;
+    pair(p, z0, z1, b0, b1);
+    pair(p + nthreads, z2, z3, b2, b3);
+    f(z0, b0); f(z1, b1); f(z2, b2); f(z3, b3);
   }
+  for (; p < np; p += nthreads) {
+    uint64_t z0, z1;
+    uint32_t b0, b1;
+    pair(p, z0, z1, b0, b1);
+    f(z0, b0); f(z1, b1);
+  }
+  if ((n & 1) && tid == 0) f(c.z[n - 1], (uint32_t)c.bin[n - 1] | (SH ? (uint32_t)c.sh[n - 1] << 16 : 0u));
+}
+
+constexpr int OT = 256;    // or/and threads per block
+template <bool SH>
+__global__ __launch_bounds__(OT) void k_key_or_and(KeyCols c, int64_t n, unsigned long long* __restrict__ acc, int vec) {
+  uint64_t zo = 0, za = ~0ull, bo = 0, ba = ~0ull;
+  for_rows<SH>(c, n, vec, (int64_t)blockIdx.x * OT + threadIdx.x, (int64_t)gridDim.x * OT, [&](uint64_t z, uint32_t b) {
+    zo |= z; za &= z; bo |= b; ba &= b;
+  });
   zo = wave_or(zo); za = wave_and(za); bo = wave_or(bo); ba = wave_and(ba);
   if ((threadIdx.x & 63) == 0) {
     atomicOr(&acc[0], zo); atomicOr(&acc[1], bo); atomicAnd(&acc[2], za); atomicAnd(&acc[3], ba);
@@ -133,26 +148,17 @@ __device__ __forceinline__ uint32_t key_digit_w(uint32_t bs, uint64_t z, int off
   return key_bits(bs, z, off) & ((1u << w) - 1u);
 }
 constexpr int CNT_LDS = 2816;           // 11 byte digits x 256, or 4 prefix digits x 512 (<= 2048)
+constexpr int CT = 1024;   // count threads per block
 template <bool SH>
 __global__ __launch_bounds__(CT) void k_sort_count(KeyCols c, int64_t n, DigitOffs o, uint32_t* __restrict__ counts, int vec) {
   __shared__ uint32_t h[4][CNT_LDS];
   const int copy = (threadIdx.x >> 6) & 3;
   for (int i = threadIdx.x; i < 4 * CNT_LDS; i += CT) (&h[0][0])[i] = 0u;
   __syncthreads();
-  const int64_t step = (int64_t)gridDim.x * CT * 2 * CU4;
-  for (int64_t i0 = ((int64_t)blockIdx.x * CT * CU4 + threadIdx.x) * 2; i0 < n; i0 += step) {
-    uint64_t z[CU4][2];
-    uint32_t b[CU4][2];
-#pragma unroll
-    for (int u = 0; u < CU4; ++u) load_pair<SH>(c, i0 + (int64_t)u * CT * 2, n, vec, z[u][0], z[u][1], b[u][0], b[u][1]);
-#pragma unroll
-    for (int u = 0; u < CU4; ++u)
-#pragma unroll
-      for (int e = 0; e < 2; ++e)
-        if (i0 + (int64_t)u * CT * 2 + e < n)
-          for (int k = 0, bk = 0; k < o.np; bk += 1 << o.w[k], ++k)
-            atomicAdd(&h[copy][bk + key_digit_w(b[u][e], z[u][e], o.off[k], o.w[k])], 1u);
-  }
+  for_rows<SH>(c, n, vec, (int64_t)blockIdx.x * CT + threadIdx.x, (int64_t)gridDim.x * CT, [&](uint64_t z, uint32_t b) {
+    for (int k = 0, bk = 0; k < o.np; bk += 1 << o.w[k], ++k)
+      atomicAdd(&h[copy][bk + key_digit_w(b, z, o.off[k], o.w[k])], 1u);
+  });
   __syncthreads();
   for (int k = 0, bk = 0; k < o.np; bk += 1 << o.w[k], ++k)
     for (int d = threadIdx.x; d < (1 << o.w[k]); d += CT) {
@@ -346,9 +352,10 @@ __global__ __launch_bounds__(PT) void k_sort_pass(PassArgs a) {
 // digit passes over every varying byte instead.
 constexpr int LT = 512, LCAP = 4096, LPT = LCAP / LT, RUN_MAX = 256, LSTEP = LCAP - RUN_MAX;
 
-// the prefix digits of width w (offsets o.x > o.y > ...; an offset < 0: no digit)
-__device__ __forceinline__ uint64_t prefix4(uint32_t bs, uint64_t z, int4 o, int w) {
-  uint64_t p = 0;
+// the prefix digits of width w (offsets o.x > o.y > ...; an offset < 0: no digit): at most 32 bits
+// (npre * pw <= 32 for n < 2^32, see gm_sort_keys)
+__device__ __forceinline__ uint32_t prefix4(uint32_t bs, uint64_t z, int4 o, int w) {
+  uint32_t p = 0;
   p = (p << w) | (o.x >= 0 ? key_digit_w(bs, z, o.x, w) : 0u);
   p = (p << w) | (o.y >= 0 ? key_digit_w(bs, z, o.y, w) : 0u);
   p = (p << w) | (o.z >= 0 ? key_digit_w(bs, z, o.z, w) : 0u);
@@ -363,18 +370,17 @@ __global__ __launch_bounds__(LT) void k_sort_local(const uint4* __restrict__ rec
                                                    uint32_t* __restrict__ flag) {
   __shared__ uint64_t s_z[LCAP];
   __shared__ uint32_t s_bs[LCAP];
-  __shared__ uint32_t s_run[LCAP];   // run start (low 16) | at a run start, its end << 16
-  __shared__ uint8_t s_new[LCAP];    // the row starts a new prefix
+  __shared__ uint32_t s_run[LCAP];   // prefix; then run start (low 16) | at a run start, its end << 16
   __shared__ int64_t s_ab[2];
   __shared__ uint32_t s_wmax[LT / 64];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  auto pre_of = [&](int64_t r) -> uint64_t { const uint4 v = rec_in[r]; return prefix4(v.w, rec_z(v), po, pw); };
+  auto pre_of = [&](int64_t r) -> uint32_t { const uint4 v = rec_in[r]; return prefix4(v.w, rec_z(v), po, pw); };
   const int64_t ntile = (n + LSTEP - 1) / LSTEP;
   for (int64_t tk = blockIdx.x; tk < ntile; tk += gridDim.x) {   // block-uniform
     if (wave < 2) {   // waves 0 / 1: the first run start at or after p (none within RUN_MAX rows: flag)
       int64_t p = min(n, (tk + wave) * LSTEP);
       if (p > 0 && p < n) {
-        const uint64_t pp = pre_of(p - 1);
+        const uint32_t pp = pre_of(p - 1);
         int64_t found = -1;
         for (int c = 0; c <= RUN_MAX / 64 && found < 0; ++c) {   // wave-uniform
           const int64_t r = p + c * 64 + lane;
@@ -395,11 +401,8 @@ __global__ __launch_bounds__(LT) void k_sort_local(const uint4* __restrict__ rec
     for (int i = t; i < m; i += LT) {
       const uint4 v = rec_in[a + i];
       const uint64_t zz = rec_z(v);
-      s_z[i] = zz; s_bs[i] = v.w;
+      s_z[i] = zz; s_bs[i] = v.w; s_run[i] = prefix4(v.w, zz, po, pw);
     }
-    __syncthreads();
-    for (int i = t; i < m; i += LT)
-      s_new[i] = i == 0 || prefix4(s_bs[i], s_z[i], po, pw) != prefix4(s_bs[i - 1], s_z[i - 1], po, pw);
     __syncthreads();
     // run starts: a block max-scan of (row starts a run ? row : 0) over rows [LPT t, LPT t + LPT)
     uint32_t st[LPT];
@@ -407,7 +410,7 @@ __global__ __launch_bounds__(LT) void k_sort_local(const uint4* __restrict__ rec
 #pragma unroll
     for (int k = 0; k < LPT; ++k) {
       const int i = LPT * t + k;
-      if (i < m && s_new[i]) run = (uint32_t)i;
+      if (i < m && (i == 0 || s_run[i] != s_run[i - 1])) run = (uint32_t)i;
       st[k] = run;
     }
     uint32_t x = run;
@@ -424,6 +427,7 @@ __global__ __launch_bounds__(LT) void k_sort_local(const uint4* __restrict__ rec
     if (lane > 0) carry = max(carry, prev);
 #pragma unroll
     for (int k = 0; k < LPT; ++k) st[k] = max(st[k], carry);
+    __syncthreads();   // every prefix read before s_run is overwritten
 #pragma unroll
     for (int k = 0; k < LPT; ++k)
       if (LPT * t + k < m) s_run[LPT * t + k] = st[k];
@@ -525,14 +529,15 @@ int gm_sort_keys(gm_ctx* ctx, const uint8_t* shard, const int16_t* bin, const in
   const KeyCols in{sh, (const uint16_t*)bin, (const uint64_t*)z};
   // 16-B z / 4-B bin / 2-B shard pair loads need aligned caller columns
   const int user_vec = ((uintptr_t)z % 16) == 0 && ((uintptr_t)bin % 4) == 0 && (!sh || ((uintptr_t)sh % 2) == 0);
-  const int cgrid = (int)std::max<int64_t>(1, std::min<int64_t>(1024, (n + 2 * CT * CU4 - 1) / (2 * CT * CU4)));
+  const int ogrid = (int)std::max<int64_t>(1, std::min<int64_t>(2048, (n / 2 + OT - 1) / OT));
+  const int cgrid = (int)std::max<int64_t>(1, std::min<int64_t>(768, (n / 2 + CT - 1) / CT));
   // which key bits vary (k_key_or_and): acc = OR z, OR bs, AND z, AND bs (bs = bin | shard << 16)
   unsigned long long* acc = (unsigned long long*)ctx->d_scratch;
   GM_HIP(hipMemsetAsync(acc, 0, 16, s));
   GM_HIP(hipMemsetAsync(acc + 2, 0xff, 16, s));
   GM_HIP(hipMemsetAsync(acc + 4, 0, 8, s));   // k_sort_local's flag
-  if (sh) hipLaunchKernelGGL(k_key_or_and<true>, dim3(cgrid), dim3(CT), 0, s, in, n, acc, user_vec);
-  else hipLaunchKernelGGL(k_key_or_and<false>, dim3(cgrid), dim3(CT), 0, s, in, n, acc, user_vec);
+  if (sh) hipLaunchKernelGGL(k_key_or_and<true>, dim3(ogrid), dim3(OT), 0, s, in, n, acc, user_vec);
+  else hipLaunchKernelGGL(k_key_or_and<false>, dim3(ogrid), dim3(OT), 0, s, in, n, acc, user_vec);
   GM_CHECK_LAUNCH();
   unsigned long long hacc[4];
   GM_HIP(hipMemcpyAsync(hacc, acc, sizeof(hacc), hipMemcpyDeviceToHost, s));
