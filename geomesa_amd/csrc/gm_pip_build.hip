@@ -1593,7 +1593,7 @@ int gm_pip_index_create_ex(gm_ctx* ctx, const gm_polyset* ps, int cells_per_poly
 
   // ---- grid: ~cells_per_poly cells per polygon over the set's envelope
   const double W = any ? G[2] - G[0] : 0.0, H = any ? G[3] - G[1] : 0.0;
-  const int64_t cells_per_poly = cells_per_poly_in > 0 ? cells_per_poly_in : 8192;
+  const int64_t cells_per_poly = cells_per_poly_in > 0 ? cells_per_poly_in : 16384;
   int64_t target = std::min<int64_t>(std::max<int64_t>((int64_t)P * cells_per_poly, 64), (int64_t)1 << GM_MAX_CELLS_LOG);
   int gx = 1, gy = 1;
   const bool degenerate = !(W > 0 && H > 0);

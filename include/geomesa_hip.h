@@ -260,7 +260,7 @@ typedef struct gm_pip_index gm_pip_index;
    plus per-ring y-slab edge buckets). */
 int gm_pip_index_create(gm_ctx* ctx, const gm_polyset* polys, gm_pip_index** out);
 /* same with an explicit grid density: ~cells_per_poly grid cells per polygon over the set's
-   envelope (0 = default 8192, at most 2^26 cells; a coarse 8x8-cell table in front of it stays
+   envelope (0 = default 16384, at most 2^26 cells; a coarse 8x8-cell table in front of it stays
    L2-resident) */
 int gm_pip_index_create_ex(gm_ctx* ctx, const gm_polyset* polys, int cells_per_poly, gm_pip_index** out);
 int gm_pip_index_destroy(gm_pip_index* index);
