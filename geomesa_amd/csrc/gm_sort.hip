@@ -96,36 +96,46 @@ __device__ __forceinline__ uint64_t wave_and(uint64_t v) {
   for (int o = 32; o > 0; o >>= 1) v &= __shfl_xor(v, o, 64);
   return v;
 }
-// f(z, bs) over every row of the caller's columns, pairs of rows per lane (16-B z, 4-B bin, 2-B shard
-// loads when `vec`), two pairs in flight; thread `tid` of `nthreads`
-template <bool SH, class F>
-__device__ __forceinline__ void for_rows(const KeyCols& c, int64_t n, int vec, int64_t tid, int64_t nthreads, F f) {
-  const int64_t np = n >> 1;
-  auto pair = [&](int64_t p, uint64_t& z0, uint64_t& z1, uint32_t& b0, uint32_t& b1) __attribute__((always_inline)) {
-    load_pair<SH>(c, 2 * p, n, vec, z0, z1, b0, b1);
-  };
-  int64_t p = tid;
-  for (; p + nthreads < np; p += 2 * nthreads) {
-    uint64_t z0, z1, z2, z3;
-    uint32_t b0, b1, b2, b3;
-    pair(p, z0, z1, b0, b1);
-    pair(p + nthreads, z2, z3, b2, b3);
-    f(z0, b0); f(z1, b1); f(z2, b2); f(z3, b3);
+// f(z, bs) over every row of the caller's columns, one wave per 512-row chunk.  With 16-B aligned
+// columns (`wide`) every load is one contiguous 1 KiB per wave instruction: z as 16-B pairs (rows
+// 128 u + 2 lane, + 1), bin as 8 rows per lane and the shard byte as 16 per lane, staged through the
+// wave's LDS slice so each lane meets the bins of its z rows (narrow per-lane loads stream at about
+// half the 16-B rate on gfx950); other chunks go row by row.
+constexpr int RCH = 512;   // rows per wave chunk
+template <bool SH, int NWAVE, class F>
+__device__ __forceinline__ void for_rows(const KeyCols& c, int64_t n, int wide, F f) {
+  __shared__ __attribute__((aligned(16))) uint16_t s_b[NWAVE][RCH];
+  __shared__ __attribute__((aligned(16))) uint8_t s_s[NWAVE][SH ? RCH : 16];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t nchunk = (n + RCH - 1) / RCH, stride = (int64_t)gridDim.x * NWAVE;
+  for (int64_t ch = (int64_t)blockIdx.x * NWAVE + wave; ch < nchunk; ch += stride) {   // wave-uniform
+    const int64_t r0 = ch * RCH;
+    if (wide && r0 + RCH <= n) {
+      ulonglong2 zz[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) zz[u] = *(const ulonglong2*)(c.z + r0 + 128 * u + 2 * lane);
+      *(uint4*)&s_b[wave][8 * lane] = *(const uint4*)(c.bin + r0 + 8 * lane);
+      if (SH && lane < RCH / 16) *(uint4*)&s_s[wave][16 * lane] = *(const uint4*)(c.sh + r0 + 16 * lane);
+      wave_lds_sync();
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int j = 128 * u + 2 * lane;
+        f(zz[u].x, (uint32_t)s_b[wave][j] | (SH ? (uint32_t)s_s[wave][j] << 16 : 0u));
+        f(zz[u].y, (uint32_t)s_b[wave][j + 1] | (SH ? (uint32_t)s_s[wave][j + 1] << 16 : 0u));
+      }
+      wave_lds_sync();   // the slice is free for the next chunk
+    } else {
+      for (int64_t r = r0 + lane; r < min(n, r0 + RCH); r += 64)
+        f(c.z[r], (uint32_t)c.bin[r] | (SH ? (uint32_t)c.sh[r] << 16 : 0u));
+    }
   }
-  for (; p < np; p += nthreads) {
-    uint64_t z0, z1;
-    uint32_t b0, b1;
-    pair(p, z0, z1, b0, b1);
-    f(z0, b0); f(z1, b1);
-  }
-  if ((n & 1) && tid == 0) f(c.z[n - 1], (uint32_t)c.bin[n - 1] | (SH ? (uint32_t)c.sh[n - 1] << 16 : 0u));
 }
 
 constexpr int OT = 256;    // or/and threads per block
 template <bool SH>
-__global__ __launch_bounds__(OT) void k_key_or_and(KeyCols c, int64_t n, unsigned long long* __restrict__ acc, int vec) {
+__global__ __launch_bounds__(OT) void k_key_or_and(KeyCols c, int64_t n, unsigned long long* __restrict__ acc, int wide) {
   uint64_t zo = 0, za = ~0ull, bo = 0, ba = ~0ull;
-  for_rows<SH>(c, n, vec, (int64_t)blockIdx.x * OT + threadIdx.x, (int64_t)gridDim.x * OT, [&](uint64_t z, uint32_t b) {
+  for_rows<SH, OT / 64>(c, n, wide, [&](uint64_t z, uint32_t b) {
     zo |= z; za &= z; bo |= b; ba &= b;
   });
   zo = wave_or(zo); za = wave_and(za); bo = wave_or(bo); ba = wave_and(ba);
@@ -150,12 +160,12 @@ __device__ __forceinline__ uint32_t key_digit_w(uint32_t bs, uint64_t z, int off
 constexpr int CNT_LDS = 2816;           // 11 byte digits x 256, or 4 prefix digits x 512 (<= 2048)
 constexpr int CT = 1024;   // count threads per block
 template <bool SH>
-__global__ __launch_bounds__(CT) void k_sort_count(KeyCols c, int64_t n, DigitOffs o, uint32_t* __restrict__ counts, int vec) {
+__global__ __launch_bounds__(CT) void k_sort_count(KeyCols c, int64_t n, DigitOffs o, uint32_t* __restrict__ counts, int wide) {
   __shared__ uint32_t h[4][CNT_LDS];
   const int copy = (threadIdx.x >> 6) & 3;
   for (int i = threadIdx.x; i < 4 * CNT_LDS; i += CT) (&h[0][0])[i] = 0u;
   __syncthreads();
-  for_rows<SH>(c, n, vec, (int64_t)blockIdx.x * CT + threadIdx.x, (int64_t)gridDim.x * CT, [&](uint64_t z, uint32_t b) {
+  for_rows<SH, CT / 64>(c, n, wide, [&](uint64_t z, uint32_t b) {
     for (int k = 0, bk = 0; k < o.np; bk += 1 << o.w[k], ++k)
       atomicAdd(&h[copy][bk + key_digit_w(b, z, o.off[k], o.w[k])], 1u);
   });
@@ -180,7 +190,10 @@ __global__ __launch_bounds__(CT) void k_sort_count(KeyCols c, int64_t n, DigitOf
 // own (decoupled look-back).  The tile is reordered in LDS meanwhile and leaves as digit runs of 16-B
 // records.  Granule tags carry the pass (tag) so no pass reads another's; the status array is cleared
 // once per call.  LDS 78 KB: two blocks (16 waves) per CU.
-constexpr int PT = 512, PW = PT / 64, PSLOT = 4, PTILE = PT * 2 * PSLOT;   // 4096 rows per tile
+#ifndef GM_SORT_PSLOT
+#define GM_SORT_PSLOT 4
+#endif
+constexpr int PT = 512, PW = PT / 64, PSLOT = GM_SORT_PSLOT, PTILE = PT * 2 * PSLOT;   // 4096 rows per tile
 static_assert(PT >= NB_MAX, "one thread per digit");
 constexpr uint64_t GR_VAL = (1ull << 48) - 1;
 
@@ -350,7 +363,10 @@ __global__ __launch_bounds__(PT) void k_sort_pass(PassArgs a) {
 // smaller key (ties by position: stable) and goes to run start + rank: O(run length) LDS reads per
 // row.  A run longer than RUN_MAX rows (skewed or repeated keys) sets *flag and the host sorts with
 // digit passes over every varying byte instead.
-constexpr int LT = 512, LCAP = 4096, LPT = LCAP / LT, RUN_MAX = 256, LSTEP = LCAP - RUN_MAX;
+#ifndef GM_SORT_LCAP
+#define GM_SORT_LCAP 4096
+#endif
+constexpr int LT = 512, LCAP = GM_SORT_LCAP, LPT = LCAP / LT, RUN_MAX = 256, LSTEP = LCAP - RUN_MAX;
 
 // the prefix digits of width w (offsets o.x > o.y > ...; an offset < 0: no digit): at most 32 bits
 // (npre * pw <= 32 for n < 2^32, see gm_sort_keys)
@@ -398,10 +414,23 @@ __global__ __launch_bounds__(LT) void k_sort_local(const uint4* __restrict__ rec
     __syncthreads();
     if (a < 0 || b < 0) continue;   // flagged: the host redoes the sort
     const int m = (int)(b - a);     // <= LSTEP + RUN_MAX = LCAP
-    for (int i = t; i < m; i += LT) {
-      const uint4 v = rec_in[a + i];
-      const uint64_t zz = rec_z(v);
-      s_z[i] = zz; s_bs[i] = v.w; s_run[i] = prefix4(v.w, zz, po, pw);
+    // the tile's rows: all LPT loads of a thread issued together; a row's input index stays in a
+    // register for the write-out (thread t handles rows t + k LT in both phases)
+    uint4 v[LPT];
+#pragma unroll
+    for (int k = 0; k < LPT; ++k) {
+      const int i = t + k * LT;
+      if (i < m) v[k] = rec_in[a + i];
+    }
+    uint32_t row[LPT];
+#pragma unroll
+    for (int k = 0; k < LPT; ++k) {
+      const int i = t + k * LT;
+      row[k] = v[k].z;
+      if (i < m) {
+        const uint64_t zz = rec_z(v[k]);
+        s_z[i] = zz; s_bs[i] = v[k].w; s_run[i] = prefix4(v[k].w, zz, po, pw);
+      }
     }
     __syncthreads();
     // run starts: a block max-scan of (row starts a run ? row : 0) over rows [LPT t, LPT t + LPT)
@@ -443,7 +472,10 @@ __global__ __launch_bounds__(LT) void k_sort_local(const uint4* __restrict__ rec
       if (i == m - 1) s_run[st[k]] = st[k] | ((uint32_t)m << 16);
     }
     __syncthreads();
-    for (int i = t; i < m; i += LT) {
+#pragma unroll
+    for (int k = 0; k < LPT; ++k) {
+      const int i = t + k * LT;
+      if (i >= m) continue;
       const int s0 = (int)(s_run[i] & 0xffffu), e0 = (int)(s_run[s0] >> 16);
       if (e0 - s0 > RUN_MAX) { *flag = 1u; continue; }
       const uint64_t zi = s_z[i];
@@ -458,7 +490,7 @@ __global__ __launch_bounds__(LT) void k_sort_local(const uint4* __restrict__ rec
       z_out[dst] = zi;
       bin_out[dst] = (uint16_t)bi;
       if (SH) sh_out[dst] = (uint8_t)(bi >> 16);
-      perm_out[dst] = (int64_t)((const uint32_t*)(rec_in + a + i))[2];
+      perm_out[dst] = (int64_t)row[k];
     }
     __syncthreads();
   }
@@ -529,15 +561,18 @@ int gm_sort_keys(gm_ctx* ctx, const uint8_t* shard, const int16_t* bin, const in
   const KeyCols in{sh, (const uint16_t*)bin, (const uint64_t*)z};
   // 16-B z / 4-B bin / 2-B shard pair loads need aligned caller columns
   const int user_vec = ((uintptr_t)z % 16) == 0 && ((uintptr_t)bin % 4) == 0 && (!sh || ((uintptr_t)sh % 2) == 0);
-  const int ogrid = (int)std::max<int64_t>(1, std::min<int64_t>(2048, (n / 2 + OT - 1) / OT));
-  const int cgrid = (int)std::max<int64_t>(1, std::min<int64_t>(768, (n / 2 + CT - 1) / CT));
+  // 16-B loads of every column in the OR/AND and count reads
+  const int user_wide = ((uintptr_t)z % 16) == 0 && ((uintptr_t)bin % 16) == 0 && (!sh || ((uintptr_t)sh % 16) == 0);
+  const int64_t nchunk = (n + RCH - 1) / RCH;
+  const int ogrid = (int)std::max<int64_t>(1, std::min<int64_t>(2048, (nchunk + OT / 64 - 1) / (OT / 64)));
+  const int cgrid = (int)std::max<int64_t>(1, std::min<int64_t>(512, (nchunk + CT / 64 - 1) / (CT / 64)));
   // which key bits vary (k_key_or_and): acc = OR z, OR bs, AND z, AND bs (bs = bin | shard << 16)
   unsigned long long* acc = (unsigned long long*)ctx->d_scratch;
   GM_HIP(hipMemsetAsync(acc, 0, 16, s));
   GM_HIP(hipMemsetAsync(acc + 2, 0xff, 16, s));
   GM_HIP(hipMemsetAsync(acc + 4, 0, 8, s));   // k_sort_local's flag
-  if (sh) hipLaunchKernelGGL(k_key_or_and<true>, dim3(ogrid), dim3(OT), 0, s, in, n, acc, user_vec);
-  else hipLaunchKernelGGL(k_key_or_and<false>, dim3(ogrid), dim3(OT), 0, s, in, n, acc, user_vec);
+  if (sh) hipLaunchKernelGGL(k_key_or_and<true>, dim3(ogrid), dim3(OT), 0, s, in, n, acc, user_wide);
+  else hipLaunchKernelGGL(k_key_or_and<false>, dim3(ogrid), dim3(OT), 0, s, in, n, acc, user_wide);
   GM_CHECK_LAUNCH();
   unsigned long long hacc[4];
   GM_HIP(hipMemcpyAsync(hacc, acc, sizeof(hacc), hipMemcpyDeviceToHost, s));
@@ -612,8 +647,8 @@ int gm_sort_keys(gm_ctx* ctx, const uint8_t* shard, const int16_t* bin, const in
     o.np = np;
     for (int k = 0; k < np; ++k) { o.off[k] = offs[k]; o.w[k] = w; }
     uint32_t* cnt = counts + (size_t)tag0 * NB_MAX;
-    if (sh) hipLaunchKernelGGL(k_sort_count<true>, dim3(cgrid), dim3(CT), 0, s, in, n, o, cnt, user_vec);
-    else hipLaunchKernelGGL(k_sort_count<false>, dim3(cgrid), dim3(CT), 0, s, in, n, o, cnt, user_vec);
+    if (sh) hipLaunchKernelGGL(k_sort_count<true>, dim3(cgrid), dim3(CT), 0, s, in, n, o, cnt, user_wide);
+    else hipLaunchKernelGGL(k_sort_count<false>, dim3(cgrid), dim3(CT), 0, s, in, n, o, cnt, user_wide);
     if (hipGetLastError() != hipSuccess) return hip_fail(hipErrorLaunchFailure, "k_sort_count");
     for (int k = 0; k < np; ++k) {
       PassArgs a{};
