@@ -193,7 +193,10 @@ __global__ __launch_bounds__(CT) void k_sort_count(KeyCols c, int64_t n, DigitOf
 #ifndef GM_SORT_PSLOT
 #define GM_SORT_PSLOT 4
 #endif
-constexpr int PT = 512, PW = PT / 64, PSLOT = GM_SORT_PSLOT, PTILE = PT * 2 * PSLOT;   // 4096 rows per tile
+#ifndef GM_SORT_PT
+#define GM_SORT_PT 512
+#endif
+constexpr int PT = GM_SORT_PT, PW = PT / 64, PSLOT = GM_SORT_PSLOT, PTILE = PT * 2 * PSLOT;   // 4096 rows per tile
 static_assert(PT >= NB_MAX, "one thread per digit");
 constexpr uint64_t GR_VAL = (1ull << 48) - 1;
 
@@ -366,7 +369,10 @@ __global__ __launch_bounds__(PT) void k_sort_pass(PassArgs a) {
 #ifndef GM_SORT_LCAP
 #define GM_SORT_LCAP 4096
 #endif
-constexpr int LT = 512, LCAP = GM_SORT_LCAP, LPT = LCAP / LT, RUN_MAX = 256, LSTEP = LCAP - RUN_MAX;
+#ifndef GM_SORT_LT
+#define GM_SORT_LT 512
+#endif
+constexpr int LT = GM_SORT_LT, LCAP = GM_SORT_LCAP, LPT = LCAP / LT, RUN_MAX = 256, LSTEP = LCAP - RUN_MAX;
 
 // the prefix digits of width w (offsets o.x > o.y > ...; an offset < 0: no digit): at most 32 bits
 // (npre * pw <= 32 for n < 2^32, see gm_sort_keys)
