@@ -26,13 +26,14 @@ STREAMING = {
     "xz2_index": ("k_xz2_index_v", "xz", 40.0),
     "z3_histogram": ("k_z3_hist_lds<", "points", 24.0),
     "pip_relate": ("k_pip_relate", "points", 21.0),
-    "sort_scatter": ("k_sort_scatter", "rows", 28.0),
-    "sort_local": ("k_sort_local", "rows", 32.0),
+    "sort_or_and": ("k_key_or_and<", "rows", 10.0),
+    "sort_count": ("k_sort_count<", "rows", 10.0),
+    "sort_pass_first": ("k_sort_pass<false, false", "rows", 26.0),
+    "sort_pass": ("k_sort_pass<true, false", "rows", 32.0),
+    "sort_local": ("k_sort_local<", "rows", 34.0),
 }
-# join step kernels and the points per dispatch: direct = one pass per 2^31 points, partitioned =
-# hist + scan + scatter + join per 2^28-point chunk
-JOIN_MODES = {"direct": (["k_pip_join_q<true", "k_pair_plan", "k_pair_move"], 1 << 31),
-              "partitioned": (["k_band_hist", "k_band_scan", "k_band_scatter", "k_pip_join<true, true, false"], 1 << 28)}
+# join step kernels and the points per dispatch: one direct pass per 2^31 points
+JOIN_MODES = {"direct": (["k_pip_join_q<true", "k_pair_plan", "k_pair_move"], 1 << 31)}
 
 
 def per_dispatch(root):
