@@ -73,14 +73,14 @@ struct PipDev {
   uint32_t* fault;
   int64_t n_line, n_compact_lines, n_blob16, n_list;
   // coarse EMPTY bitmap (make_shortcut; staged in LDS by the direct join): bit (by * cm_w + bx) set when
-  // every coarse cell of block (bx, by) = coarse cells [bx << cm_shift, (bx + 1) << cm_shift) x (same
-  // in y) is EMPTY; cm_words = 0: no bitmap
+  // every coarse cell of block (bx, by) = coarse cells [bx << cm_shift, (bx + 1) << cm_shift) x
+  // [by << cm_shift_y, (by + 1) << cm_shift_y) is EMPTY; cm_words = 0: no bitmap
   const uint32_t* cm;
-  int32_t cm_shift, cm_w;
+  int32_t cm_shift, cm_shift_y, cm_w;
   int64_t cm_words;
   // the same bitmap at the row predicate's smaller LDS budget (RELATE_CM_WORDS)
   const uint32_t* cm2;
-  int32_t cm2_shift, cm2_w;
+  int32_t cm2_shift, cm2_shift_y, cm2_w;
   int64_t cm2_words;
   // per polygon p, a rectangle of fine cells (x0, y0, x1, y1 inclusive; x0 > x1 = none) whose words
   // are all INTERIOR(p) (make_shortcut, k_core_*): the row predicate answers a row of polygon p inside

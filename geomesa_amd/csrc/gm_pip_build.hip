@@ -786,8 +786,8 @@ __global__ __launch_bounds__(256) void k_build_coarse8(const uint32_t* __restric
 #endif
 
 // the coarse EMPTY bitmap over coarse_sc: one thread per 32-bit word
-__global__ __launch_bounds__(256) void k_build_cmask(const uint32_t* __restrict__ coarse_sc, int gxc, int gyc, int shift,
-                                                     int cw, int ch, int64_t nwords, uint32_t* __restrict__ out) {
+__global__ __launch_bounds__(256) void k_build_cmask(const uint32_t* __restrict__ coarse_sc, int gxc, int gyc, int shx,
+                                                     int shy, int cw, int ch, int64_t nwords, uint32_t* __restrict__ out) {
   for (int64_t wi = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; wi < nwords; wi += (int64_t)gridDim.x * blockDim.x) {
     uint32_t w = 0;
     for (int k = 0; k < 32; ++k) {
@@ -795,8 +795,8 @@ __global__ __launch_bounds__(256) void k_build_cmask(const uint32_t* __restrict_
       if (b >= (int64_t)cw * ch) break;
       const int by = (int)(b / cw), bx = (int)(b % cw);
       bool empty = true;
-      for (int y = by << shift; empty && y < min(gyc, (by + 1) << shift); ++y)
-        for (int x = bx << shift; x < min(gxc, (bx + 1) << shift); ++x)
+      for (int y = by << shy; empty && y < min(gyc, (by + 1) << shy); ++y)
+        for (int x = bx << shx; x < min(gxc, (bx + 1) << shx); ++x)
           if ((coarse_sc[(int64_t)y * gxc + x] >> 30) != CELL_EMPTY) { empty = false; break; }
       if (empty) w |= 1u << k;
     }
@@ -1135,21 +1135,27 @@ int make_shortcut(gm_pip_index* ix) {
 #endif
     // the coarse EMPTY bitmaps: the finest block size whose bitmap fits each kernel's LDS budget
     // (the join's, the row predicate's)
-    auto bitmap = [&](int64_t budget_words, const uint32_t** out, int32_t* shift, int32_t* w, int64_t* words) -> int {
-      int sh = 0;
-      while ((int64_t)((gxc + (1 << sh) - 1) >> sh) * ((gyc + (1 << sh) - 1) >> sh) > budget_words * 32) ++sh;
-      const int cw = (gxc + (1 << sh) - 1) >> sh, ch = (gyc + (1 << sh) - 1) >> sh;
+    auto bitmap = [&](int64_t budget_words, const uint32_t** out, int32_t* shift, int32_t* shift_y, int32_t* w,
+                      int64_t* words) -> int {
+      // blocks of 2^shx x 2^shy coarse cells, shx = shy or shy + 1: the finest that fits the budget
+      int shx = 0, shy = 0;
+      while ((int64_t)((gxc + (1 << shx) - 1) >> shx) * ((gyc + (1 << shy) - 1) >> shy) > budget_words * 32) {
+        if (shx == shy) ++shx;
+        else ++shy;
+      }
+      const int cw = (gxc + (1 << shx) - 1) >> shx, ch = (gyc + (1 << shy) - 1) >> shy;
       const int64_t nw = ((int64_t)cw * ch + 31) / 32;
       void* cm = nullptr;
       if (hipMalloc(&cm, (size_t)nw * 4) != hipSuccess) return hip_fail(hipErrorOutOfMemory, "gm_pip_index bitmap");
       ix->allocs.push_back(cm);
       hipLaunchKernelGGL(k_build_cmask, dim3((unsigned)std::min<int64_t>(4096, (nw + 255) / 256)), dim3(256), 0, s,
-                         (const uint32_t*)ix->dev.coarse_sc, gxc, gyc, sh, cw, ch, nw, (uint32_t*)cm);
-      *out = (const uint32_t*)cm; *shift = sh; *w = cw; *words = nw;
+                         (const uint32_t*)ix->dev.coarse_sc, gxc, gyc, shx, shy, cw, ch, nw, (uint32_t*)cm);
+      *out = (const uint32_t*)cm; *shift = shx; *shift_y = shy; *w = cw; *words = nw;
       return GM_OK;
     };
-    rc = bitmap(CM_WORDS_MAX, &ix->dev.cm, &ix->dev.cm_shift, &ix->dev.cm_w, &ix->dev.cm_words);
-    if (!rc) rc = bitmap(RELATE_CM_WORDS, &ix->dev.cm2, &ix->dev.cm2_shift, &ix->dev.cm2_w, &ix->dev.cm2_words);
+    rc = bitmap(CM_WORDS_MAX, &ix->dev.cm, &ix->dev.cm_shift, &ix->dev.cm_shift_y, &ix->dev.cm_w, &ix->dev.cm_words);
+    if (!rc)
+      rc = bitmap(RELATE_CM_WORDS, &ix->dev.cm2, &ix->dev.cm2_shift, &ix->dev.cm2_shift_y, &ix->dev.cm2_w, &ix->dev.cm2_words);
     // the row predicate's core rectangles (fine-cell coordinates in 16 bits; polygon count within its LDS table)
     if (!rc && ix->n_polys > 0 && ix->n_polys <= RELATE_CORE_MAX && ix->dev.gx < 65535 && ix->dev.gy < 65535 &&
         ix->ctx->index_core) {

@@ -398,8 +398,8 @@ __global__ __launch_bounds__(QTPB) void k_pip_join_q(const double* __restrict__ 
       if (g0) { cx0 = cell_of(X0, d.gx0, d.inv_cw, d.gx); cy0 = cell_of(Y0, d.gy0, d.inv_ch, d.gy); }
       if (g1) { cx1 = cell_of(X1, d.gx0, d.inv_cw, d.gx); cy1 = cell_of(Y1, d.gy0, d.inv_ch, d.gy); }
       if (cm_words) {   // EMPTY coarse blocks from the LDS bitmap: no gather
-        const int b0 = ((cy0 >> CF_LOG) >> d.cm_shift) * d.cm_w + ((cx0 >> CF_LOG) >> d.cm_shift);
-        const int b1 = ((cy1 >> CF_LOG) >> d.cm_shift) * d.cm_w + ((cx1 >> CF_LOG) >> d.cm_shift);
+        const int b0 = ((cy0 >> CF_LOG) >> d.cm_shift_y) * d.cm_w + ((cx0 >> CF_LOG) >> d.cm_shift);
+        const int b1 = ((cy1 >> CF_LOG) >> d.cm_shift_y) * d.cm_w + ((cx1 >> CF_LOG) >> d.cm_shift);
         const bool e0 = (s_cm[b0 >> 5] >> (b0 & 31)) & 1u, e1 = (s_cm[b1 >> 5] >> (b1 & 31)) & 1u;
         g0 = g0 && !e0;
         g1 = g1 && !e1;
@@ -471,7 +471,7 @@ __global__ __launch_bounds__(256) void k_pip_census(const double* __restrict__ p
     // the join's LDS bitmap answers EMPTY coarse blocks without the coarse gather (when it fits)
     bool bm_empty = false;
     if (d.cm_words > 0 && d.cm_words <= CM_WORDS_MAX) {
-      const int b = ((cy >> CF_LOG) >> d.cm_shift) * d.cm_w + ((cx >> CF_LOG) >> d.cm_shift);
+      const int b = ((cy >> CF_LOG) >> d.cm_shift_y) * d.cm_w + ((cx >> CF_LOG) >> d.cm_shift);
       bm_empty = (d.cm[b >> 5] >> (b & 31)) & 1u;
     }
     if (!bm_empty) c[JC_COARSE_GATHER]++;

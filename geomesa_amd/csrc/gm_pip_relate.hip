@@ -101,7 +101,7 @@ __global__ __launch_bounds__(RTPB) void k_pip_relate(const int32_t* __restrict__
             core = cx[u] >= b.x && cx[u] <= b.z && cy[u] >= b.y && cy[u] <= b.w;
           }
           if (cm_words && !core) {
-            const int b = ((cy[u] >> CF_LOG) >> d.cm2_shift) * d.cm2_w + ((cx[u] >> CF_LOG) >> d.cm2_shift);
+            const int b = ((cy[u] >> CF_LOG) >> d.cm2_shift_y) * d.cm2_w + ((cx[u] >> CF_LOG) >> d.cm2_shift);
             empty = (s_cm[b >> 5] >> (b & 31)) & 1u;
           }
           if (core)
