@@ -12,6 +12,9 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fn
          "-Wall", "-Wno-unused-function"]
 
 
+VARIANT_ONLY = ("GM_JX_", "GM_NO_REF_CHECKS", "GM_SC8_NOINLINE", "GM_SC8_NOLINE2")
+
+
 def sources():
     return [os.path.join(HERE, "csrc", s) for s in SRC if os.path.exists(os.path.join(HERE, "csrc", s))]
 
@@ -30,9 +33,11 @@ def build(force=False, verbose=True, out=OUT, defines=()):
     GM_JILP=8) to another path for side-by-side measurement."""
     if out == OUT and not defines and not force and not needs_build():
         return OUT
-    if out == OUT and any(d.startswith("GM_JX_") for d in defines):
-        # GM_JX_* are wrong-result timing hooks (stage ablations): never in the shipped library
-        raise ValueError("GM_JX_* timing hooks cannot be built into %s; pass --out=<other path>" % OUT)
+    if out == OUT and any(d.startswith(VARIANT_ONLY) for d in defines):
+        # timing variants (stage ablations, checks compiled out, measured-and-dropped layouts): never
+        # in the shipped library
+        raise ValueError("timing-variant defines %s cannot be built into %s; pass --out=<other path>"
+                         % ([d for d in defines if d.startswith(VARIANT_ONLY)], OUT))
     if out == OUT:
         defines = tuple(defines) + ("GM_PRODUCT_BUILD",)
     os.makedirs(os.path.dirname(out), exist_ok=True)

@@ -62,7 +62,6 @@ struct PipDev {
   const uint32_t* coarse_sc;     // the join's coarse words over cell_sc; LIST words carry sub-block masks
   int32_t coarse_fmt;            // COARSE_EMPTY_MASK / COARSE_MAIN (see coarse_mask)
   const uint4* line_ent;         // line shortcuts, two uint4 each (see "Boundary shortcuts")
-  const uint2* coarse8;          // GM_COARSE8: 16 sub-blocks of 2 x 2 with a 2-bit code each (coarse_mask8)
   const uint2* cell_sc8;         // the join's 8-B fine words: cell_sc, with one-line LINE words inline (sc8_*)
   double gx0, gy0, gx1, gy1, inv_cw, inv_ch;
   int32_t gx, gy, gxc;
@@ -425,19 +424,6 @@ __device__ __forceinline__ uint32_t coarse_mask(uint32_t w, int cx, int cy, int3
   }
   const int sub = (((cy & CM) >> SUB_LOG) << 2) | ((cx & CM) >> SUB_LOG);   // 16 sub-blocks of 2 x 2: EMPTY mask
   return ((w >> sub) & 1u) ? (CELL_EMPTY << 30) : w;
-}
-
-// GM_COARSE8 (timing variant): an 8-B coarse entry per coarse cell, {coarse_sc word, 0} for EMPTY /
-// INTERIOR cells, {LIST | main, 16 x 2-bit codes} for mixed ones: code 1 = the 2 x 2 sub-block is
-// EMPTY, 2 = INTERIOR(main), 0 = a fine lookup
-__device__ __forceinline__ uint32_t coarse_mask8(uint2 w, int cx, int cy) {
-  if ((w.x >> 30) != CELL_LIST) return w.x;
-  constexpr int CM = (1 << CF_LOG) - 1;
-  const int sub = (((cy & CM) >> SUB_LOG) << 2) | ((cx & CM) >> SUB_LOG);
-  const uint32_t code = (w.y >> (2 * sub)) & 3u;
-  if (code == 1u) return CELL_EMPTY << 30;
-  if (code == 2u) return (CELL_INTERIOR << 30) | (w.x & 0x3fffffffu);
-  return CELL_LIST << 30;
 }
 
 // PointLocator's location of a point for one BOUNDARY item (ref = the word's payload): a line

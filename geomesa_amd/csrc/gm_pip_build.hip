@@ -752,39 +752,6 @@ __global__ __launch_bounds__(256) void k_build_coarse_sc(const uint32_t* __restr
   }
 }
 
-#ifdef GM_COARSE8
-// coarse8 (coarse_mask8) over cell_sc and coarse_sc
-__global__ __launch_bounds__(256) void k_build_coarse8(const uint32_t* __restrict__ cell_sc, const uint32_t* __restrict__ coarse_sc,
-                                                       int gx, int gy, int gxc, int gyc, uint2* __restrict__ out) {
-  const int64_t n = (int64_t)gxc * gyc;
-  constexpr int CF = 1 << CF_LOG, SB = 1 << SUB_LOG;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const uint32_t w = coarse_sc[i];
-    if ((w >> 30) != CELL_LIST) { out[i] = make_uint2(w, 0u); continue; }
-    const int yc = (int)(i / gxc), xc = (int)(i % gxc);
-    uint32_t main = 0x3fffffffu;
-    for (int yy = yc * CF; yy < min(gy, (yc + 1) * CF) && main == 0x3fffffffu; ++yy)
-      for (int xx = xc * CF; xx < min(gx, (xc + 1) * CF); ++xx) {
-        const uint32_t f = cell_sc[(int64_t)yy * gx + xx];
-        if ((f >> 30) == CELL_INTERIOR) { main = f & 0x3fffffffu; break; }
-      }
-    uint32_t codes = 0;
-    for (int sb = 0; sb < 16; ++sb) {
-      const int x0 = xc * CF + (sb & 3) * SB, y0 = yc * CF + (sb >> 2) * SB;
-      bool empty = true, inner = main != 0x3fffffffu;
-      for (int yy = y0; yy < min(gy, y0 + SB); ++yy)
-        for (int xx = x0; xx < min(gx, x0 + SB); ++xx) {
-          const uint32_t f = cell_sc[(int64_t)yy * gx + xx];
-          empty &= (f >> 30) == CELL_EMPTY;
-          inner &= f == ((CELL_INTERIOR << 30) | main);
-        }
-      codes |= (empty ? 1u : inner ? 2u : 0u) << (2 * sb);
-    }
-    out[i] = make_uint2((CELL_LIST << 30) | main, codes);
-  }
-}
-#endif
-
 // the coarse EMPTY bitmap over coarse_sc: one thread per 32-bit word
 __global__ __launch_bounds__(256) void k_build_cmask(const uint32_t* __restrict__ coarse_sc, int gxc, int gyc, int shx,
                                                      int shy, int cw, int ch, int64_t nwords, uint32_t* __restrict__ out) {
@@ -1069,7 +1036,6 @@ int make_shortcut(gm_pip_index* ix) {
   ix->n_lines = 0;
   ix->dev.fault = nullptr;   // set per call (the call's scratch word)
   ix->dev.cm = nullptr;      // the coarse EMPTY bitmaps, built after coarse_sc
-  ix->dev.coarse8 = nullptr;
   ix->dev.cm_words = 0;
   ix->dev.cm2 = nullptr;
   ix->dev.cm2_words = 0;
@@ -1123,16 +1089,6 @@ int make_shortcut(gm_pip_index* ix) {
     hipLaunchKernelGGL(k_build_coarse_sc, dim3((unsigned)std::min<int64_t>(65536, ((int64_t)gxc * gyc + 255) / 256)), dim3(256),
                        0, s, (const uint32_t*)p, ix->dev.gx, ix->dev.gy, gxc, gyc, ix->dev.coarse_fmt,
                        (uint32_t*)ix->dev.coarse_sc);
-#ifdef GM_COARSE8
-    {
-      void* c8 = nullptr;
-      if (hipMalloc(&c8, (size_t)gxc * gyc * 8) != hipSuccess) { cleanup(); return hip_fail(hipErrorOutOfMemory, "gm_pip_index coarse8"); }
-      ix->allocs.push_back(c8);
-      hipLaunchKernelGGL(k_build_coarse8, dim3((unsigned)std::min<int64_t>(65536, ((int64_t)gxc * gyc + 255) / 256)), dim3(256),
-                         0, s, (const uint32_t*)p, ix->dev.coarse_sc, ix->dev.gx, ix->dev.gy, gxc, gyc, (uint2*)c8);
-      ix->dev.coarse8 = (const uint2*)c8;
-    }
-#endif
     // the coarse EMPTY bitmaps: the finest block size whose bitmap fits each kernel's LDS budget
     // (the join's, the row predicate's)
     auto bitmap = [&](int64_t budget_words, const uint32_t** out, int32_t* shift, int32_t* shift_y, int32_t* w,

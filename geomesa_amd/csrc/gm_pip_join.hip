@@ -404,21 +404,10 @@ __global__ __launch_bounds__(QTPB) void k_pip_join_q(const double* __restrict__ 
         g0 = g0 && !e0;
         g1 = g1 && !e1;
       }
-#ifdef GM_COARSE8
-      if (d.coarse8) {
-        uint2 e0 = make_uint2(CELL_EMPTY << 30, 0u), e1 = e0;
-        if (g0) e0 = d.coarse8[(int64_t)(cy0 >> CF_LOG) * d.gxc + (cx0 >> CF_LOG)];
-        if (g1) e1 = d.coarse8[(int64_t)(cy1 >> CF_LOG) * d.gxc + (cx1 >> CF_LOG)];
-        c0 = coarse_mask8(e0, cx0, cy0);
-        c1 = coarse_mask8(e1, cx1, cy1);
-      } else
-#endif
-      {
-        if (g0) c0 = d.coarse_sc[(int64_t)(cy0 >> CF_LOG) * d.gxc + (cx0 >> CF_LOG)];
-        if (g1) c1 = d.coarse_sc[(int64_t)(cy1 >> CF_LOG) * d.gxc + (cx1 >> CF_LOG)];
-        c0 = coarse_mask(c0, cx0, cy0, d.coarse_fmt);
-        c1 = coarse_mask(c1, cx1, cy1, d.coarse_fmt);
-      }
+      if (g0) c0 = d.coarse_sc[(int64_t)(cy0 >> CF_LOG) * d.gxc + (cx0 >> CF_LOG)];
+      if (g1) c1 = d.coarse_sc[(int64_t)(cy1 >> CF_LOG) * d.gxc + (cx1 >> CF_LOG)];
+      c0 = coarse_mask(c0, cx0, cy0, d.coarse_fmt);
+      c1 = coarse_mask(c1, cx1, cy1, d.coarse_fmt);
       const uint32_t id0 = (uint32_t)(2 * (step * 64 + lane)), id1 = id0 + 1;
       pair_push((c0 >> 30) == CELL_INTERIOR, id0, (int)(c0 & 0x3fffffffu));
       pair_push((c1 >> 30) == CELL_INTERIOR, id1, (int)(c1 & 0x3fffffffu));
@@ -478,9 +467,6 @@ __global__ __launch_bounds__(256) void k_pip_census(const double* __restrict__ p
     const uint32_t raw = d.coarse_sc[(int64_t)(cy >> CF_LOG) * d.gxc + (cx >> CF_LOG)];
     if ((raw >> 30) == CELL_LIST) c[JC_COARSE_RAW_MIXED]++;
     uint32_t w = coarse_mask(raw, cx, cy, d.coarse_fmt);
-#ifdef GM_COARSE8
-    if (d.coarse8) w = coarse_mask8(d.coarse8[(int64_t)(cy >> CF_LOG) * d.gxc + (cx >> CF_LOG)], cx, cy);
-#endif
     if ((w >> 30) == CELL_EMPTY) { c[JC_COARSE_EMPTY]++; continue; }
     if ((w >> 30) == CELL_INTERIOR) { c[JC_COARSE_INTERIOR]++; continue; }
     c[JC_FINE]++;

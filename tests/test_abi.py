@@ -50,12 +50,14 @@ def test_load_without_gpu_fails_loudly():
 
 
 def test_product_build_refuses_timing_hooks():
-    """GM_JX_* stage-ablation hooks (wrong results by design) never reach the shipped library: build.py
-    refuses them for its output path (no compile runs), and no product source carries one."""
+    """Timing-variant defines (stage ablations, the reference checks compiled out, the inline-word
+    ablations) never reach the shipped library: build.py refuses them for its output path before any
+    compile runs, and no product source carries a GM_JX_ hook."""
     import pytest
     from geomesa_amd import build as B
-    with pytest.raises(ValueError):
-        B.build(defines=("GM_JX_NOBLOB",), verbose=False)
+    for d in ("GM_JX_NOBLOB", "GM_NO_REF_CHECKS", "GM_SC8_NOINLINE", "GM_SC8_NOLINE2"):
+        with pytest.raises(ValueError):
+            B.build(defines=(d,), verbose=False)
     for src in B.sources():
         assert "GM_JX_" not in open(src).read(), src
 
