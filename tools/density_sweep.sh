@@ -1,4 +1,7 @@
-for c in 24576 32768; do
-  timeout -k 10 300 python -u bench.py --only join --no-cpu --no-gather --steps 1 --warmup 0 --join-steps 3 --cells-per-poly $c > gpurun_out/r4h_dens_$c.json 2> gpurun_out/r4h_dens_$c.err || exit 1
-  cp gpurun_out/bench_detail_n1.json gpurun_out/r4h_dens_$c.detail.json
+# join grid density sweep on one box (bench join leg), each density twice, alternating
+i=0
+for c in 16384 20480 16384 20480; do
+  i=$((i+1))
+  timeout -k 10 300 python -u bench.py --only join --no-cpu --no-gather --steps 1 --warmup 0 --join-steps 3 --cells-per-poly $c > gpurun_out/${DTAG:-dens}_${c}_$i.json 2> gpurun_out/${DTAG:-dens}_${c}_$i.err || exit 1
+  cp gpurun_out/bench_detail_n1.json gpurun_out/${DTAG:-dens}_${c}_$i.detail.json
 done
