@@ -85,6 +85,56 @@ def test_sort_keys_parity(gpu, n, kind, sharded, mode):
         assert last < 256 and last > 3, last  # runs > 256 rows: digit passes
 
 
+def _check_table_order_on_device(bins, z, ob, oz, op, sh=None, osh=None):
+    """Device-side checks of a large sort: output = input[perm], perm a permutation, keys
+    nondecreasing in (shard, bin unsigned, z unsigned) order, and stable (equal keys keep input
+    order)."""
+    import torch
+    n = z.numel()
+    assert torch.equal(ob, bins[op]) and torch.equal(oz, z[op])
+    if sh is not None:
+        assert torch.equal(osh, sh[op])
+    seen = torch.zeros(n, dtype=torch.bool, device=z.device)
+    seen[op] = True
+    assert bool(seen.all())
+    hi = (ob.to(torch.int64) & 0xFFFF) | ((osh.to(torch.int64) << 16) if osh is not None else 0)
+    lo = oz ^ (-(1 << 63))   # unsigned order as signed
+    dh, dl = hi[1:] - hi[:-1], lo[1:] - lo[:-1]
+    le = (dh > 0) | ((dh == 0) & (lo[1:] >= lo[:-1]))
+    assert bool(le.all())
+    tie = (dh == 0) & (dl == 0)
+    assert bool((op[1:][tie] > op[:-1][tie]).all())
+
+
+@pytest.mark.parametrize("kind", ["week_keys", "dups"])
+def test_sort_keys_prefix_path_at_bench_size(gpu, kind):
+    """The bench's sort path (2^27 < n: three 9-bit prefix digits + local ranks) on 140M rows: Z3 keys
+    of uniform points over 2020 (53 weekly bins, runs of equal prefixes of a few rows), and the same
+    keys with every key repeated 4 times (ties: stability); checked on the device."""
+    import torch
+    from geomesa_amd import _lib
+    from geomesa_amd.curve import Z3SFC
+    n = 140_000_000
+    g = torch.Generator(device="cuda").manual_seed(3)
+    m = n // 4 if kind == "dups" else n
+    x = torch.rand(m, device="cuda", generator=g, dtype=torch.float64) * 360 - 180
+    y = torch.rand(m, device="cuda", generator=g, dtype=torch.float64) * 180 - 90
+    t = (torch.rand(m, device="cuda", generator=g, dtype=torch.float64) * 31622400000).to(torch.int64) + T2020
+    b, z = Z3SFC("week").index_keys(x, y, t)
+    del x, y, t
+    if kind == "dups":
+        idx = torch.randperm(n, device="cuda", generator=g) % m
+        b, z = b[idx].contiguous(), z[idx].contiguous()
+        del idx
+    ob, oz = torch.empty_like(b), torch.empty_like(z)
+    op = torch.empty(n, dtype=torch.int64, device="cuda")
+    ctx = _lib.context()
+    _lib.check(ctx.lib.gm_sort_keys(ctx.handle, None, _lib.ptr(b), _lib.ptr(z), n, None, _lib.ptr(ob), _lib.ptr(oz),
+                                    _lib.ptr(op)), "sort")
+    assert ctx.get_param(_lib.GM_PARAM_SORT_LAST) == 256 + 3   # three prefix passes + local ranks
+    _check_table_order_on_device(b, z, ob, oz, op)
+
+
 @pytest.mark.parametrize("in_off,out_off", [(1, 0), (0, 1), (1, 3)])
 def test_sort_keys_unaligned_columns(gpu, in_off, out_off):
     """Caller columns off the 16-B grid (slices): the pair-load paths must not be taken for them."""
