@@ -465,13 +465,16 @@ constexpr int ICAP = 128;              // item queue (two ends)
 constexpr int JQ_WAVE_LDS = FCAP * 20 + ICAP * 24;
 constexpr int CM_WORDS_MAX = (163840 - (QTPB / 64) * JQ_WAVE_LDS - 256) / 4;   // 13,248 words at 1024 threads
 
-// The row predicate (gm_pip_relate.hip): its own, coarser bitmap (16 KiB) and a core rectangle per
-// polygon (8 B each) in LDS.
+// The row predicate (gm_pip_relate.hip): its own, coarser bitmap (32 KiB: what its queues and the core
+// rectangles leave of the LDS, 163,584 B per block) and a core rectangle per polygon (8 B each).
 #ifndef GM_RELATE_TPB
 #define GM_RELATE_TPB 1024
 #endif
 constexpr int RTPB = GM_RELATE_TPB;
-constexpr int RELATE_CM_WORDS = 4032;
+#ifndef GM_RELATE_CM_WORDS
+#define GM_RELATE_CM_WORDS 8128
+#endif
+constexpr int RELATE_CM_WORDS = GM_RELATE_CM_WORDS;
 #ifndef GM_RELATE_CORE_MAX
 #define GM_RELATE_CORE_MAX 4096
 #endif
