@@ -192,13 +192,14 @@ __global__ __launch_bounds__(256) void k_pair_move(PairOut o, const PairPlan* __
 // before any push of <= 64 (and a line round hands over at most the items it took), F < 128 before
 // a stream step pushes <= 128.  Both are checked (PIP_FAULT_QUEUE).  Pairs are staged per wave and
 // flushed with one atomic per flush.
-// One 1024-thread block per CU (16 waves, 9 KiB of queues each) leaves 16 KiB of LDS for the coarse
-// EMPTY bitmap (one bit per 2 x 2 coarse cells on the bench's index; 768 threads left 52 KiB for one
-// bit per coarse cell, but 16 waves hide more: 11.45 -> 10.88 ms): a point whose coarse block is
-// EMPTY costs no gather at all.  The join is bound by the
-// vector-memory path (TD busy 97%, the L1 stalled on its outstanding misses 83% of the kernel, r3
-// PMC), and the coarse lookups were 70% of its L1 misses; 55% of the bench's points sit in EMPTY
-// coarse cells.
+// One 1024-thread block per CU (16 waves, 6.75 KiB of queues each: the pending fine words live in
+// registers) leaves 51.75 KiB of LDS for the coarse EMPTY bitmap (CM_WORDS_MAX: one bit per coarse
+// cell up to 424k coarse cells, else per 2 x 1, 2 x 2, ... block; 2 x 1 on the bench's default grid):
+// a point whose coarse block is EMPTY costs no gather at all.  The join is bound by the memory
+// pipeline (TD busy 94%, the L1 stalled on its outstanding misses 83% of the kernel, r4 PMC): every
+// access holds one of the CU's outstanding-miss slots for its latency, so the cost is the count of
+// gathers by kind (the gather model); 42% of the bench's points stop at the
+// bitmap.
 template <bool WRITE, int SRC, bool VEC>
 __global__ __launch_bounds__(QTPB) void k_pip_join_q(const double* __restrict__ px, const double* __restrict__ py,
                                                      int64_t n, int64_t id_base, PipDev d, PairOut po,

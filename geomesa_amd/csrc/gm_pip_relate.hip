@@ -51,7 +51,7 @@ __global__ __launch_bounds__(RTPB) void k_pip_relate(const int32_t* __restrict__
   __shared__ int64_t s_row[NW][RQCAP];
   __shared__ uint32_t s_e[NW][RQCAP];
   __shared__ int32_t s_p[NW][RQCAP];
-  // the coarse EMPTY bitmap at this kernel's budget (d.cm2, 16 KiB), staged in LDS like
+  // the coarse EMPTY bitmap at this kernel's budget (d.cm2, 31.75 KiB), staged in LDS like
   // k_pip_join_q's: rows in EMPTY coarse blocks skip the coarse gather
   __shared__ uint32_t s_cm[RELATE_CM_WORDS];
   // each polygon's core rectangle (d.core): a row inside its own polygon's core is INTERIOR at once
