@@ -30,11 +30,9 @@ struct PairOut {
 };
 
 __device__ __forceinline__ void pair_store(const PairOut& o, int64_t pos, int64_t id, int32_t poly) {
-#ifdef GM_JX_NTPAIR
+  // non-temporal: the pair lines are written once and not read back by the join, so they should not
+  // take L2 from the coarse and fine words (9.89-9.93 -> 9.83-9.85 ms, profiles/r4/join_nt_ab.txt)
   if (pos < o.cap) { __builtin_nontemporal_store(id, &o.pt[pos]); __builtin_nontemporal_store(poly, &o.pl[pos]); }
-#else
-  if (pos < o.cap) { o.pt[pos] = id; o.pl[pos] = poly; }
-#endif
   else if (pos - o.cap < o.ocap) { o.opt[pos - o.cap] = id; o.opl[pos - o.cap] = poly; }
 }
 
@@ -315,14 +313,7 @@ __global__ __launch_bounds__(QTPB) void k_pip_join_q(const double* __restrict__ 
           const uint64_t li = ref & (SC_LINE - 1);
           if (GM_REF_BAD(li >= (uint64_t)d.n_line)) { pip_fault(d, PIP_FAULT_LINE); loc = LOC_EXTERIOR; }
           else {
-#ifdef GM_JX_NTFINE
-            typedef unsigned int uv4 __attribute__((ext_vector_type(4)));
-            const uv4 a0 = __builtin_nontemporal_load((const uv4*)&d.line_ent[2 * li]);
-            const uv4 a1 = __builtin_nontemporal_load((const uv4*)&d.line_ent[2 * li + 1]);
-            const uint4 e0 = make_uint4(a0.x, a0.y, a0.z, a0.w), e1 = make_uint4(a1.x, a1.y, a1.z, a1.w);
-#else
             const uint4 e0 = d.line_ent[2 * li], e1 = d.line_ent[2 * li + 1];
-#endif
             poly = (int)e0.y;
             loc = line_locate(e0, e1, x, y, d);
             blob = e0.x & 0x3fffffffu;
@@ -395,16 +386,8 @@ __global__ __launch_bounds__(QTPB) void k_pip_join_q(const double* __restrict__ 
       const int cnt = min(fn, FBATCH);
       const int a = fn - cnt + lane;
       pend_w = make_uint2(CELL_EMPTY << 30, 0u);
-      if (lane < cnt) {
-        const int64_t ci = (int64_t)cell_of(fy[a], d.gy0, d.inv_ch, d.gy) * d.gx + cell_of(fx[a], d.gx0, d.inv_cw, d.gx);
-#ifdef GM_JX_NTFINE
-        typedef unsigned int uv2 __attribute__((ext_vector_type(2)));
-        const uv2 v = __builtin_nontemporal_load((const uv2*)&d.cell_sc8[ci]);
-        pend_w = make_uint2(v.x, v.y);
-#else
-        pend_w = d.cell_sc8[ci];
-#endif
-      }
+      if (lane < cnt)
+        pend_w = d.cell_sc8[(int64_t)cell_of(fy[a], d.gy0, d.inv_ch, d.gy) * d.gx + cell_of(fx[a], d.gx0, d.inv_cw, d.gx)];
       pb = fn - cnt;
       pc = cnt;
       pend = true;

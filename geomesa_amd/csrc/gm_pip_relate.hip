@@ -114,13 +114,7 @@ __global__ __launch_bounds__(RTPB) void k_pip_relate(const int32_t* __restrict__
       }
 #pragma unroll
       for (int u = 0; u < RILP; ++u)
-        if ((w[u] >> 30) == CELL_LIST) {   // boundary shortcuts applied
-#ifdef GM_JX_RNTFINE
-          w[u] = __builtin_nontemporal_load(&d.cell_sc[(int64_t)cy[u] * d.gx + cx[u]]);
-#else
-          w[u] = d.cell_sc[(int64_t)cy[u] * d.gx + cx[u]];
-#endif
-        }
+        if ((w[u] >> 30) == CELL_LIST) w[u] = d.cell_sc[(int64_t)cy[u] * d.gx + cx[u]];   // boundary shortcuts applied
       uint8_t rv[RILP];
       bool dir[RILP];
 #pragma unroll
@@ -177,11 +171,7 @@ __global__ __launch_bounds__(RTPB) void k_pip_relate(const int32_t* __restrict__
         qg += __popcll(mb);
       }
       if (VEC) {
-#ifdef GM_JX_RNTLOC
-        if (dir[0] && dir[1]) __builtin_nontemporal_store((uint16_t)(rv[0] | (rv[1] << 8)), (uint16_t*)(loc + row[0]));
-#else
         if (dir[0] && dir[1]) *(uint16_t*)(loc + row[0]) = (uint16_t)(rv[0] | (rv[1] << 8));
-#endif
         else {
           if (dir[0]) loc[row[0]] = rv[0];
           if (dir[1]) loc[row[1]] = rv[1];

@@ -14,9 +14,10 @@
 //                         digit offsets found by a decoupled look-back over the tiles before it (8-B
 //                         {count, tag} granules), and the tile leaves as digit runs of 16-B records
 //                         {z, row, bin | shard << 16}.  The passes order the rows by the top
-//                         ~log2(n) - 1 varying bits (three 9-bit digits at 250M rows); k_sort_local
-//                         then ranks every run of equal prefixes (a few rows) by full key in LDS and
-//                         writes the user columns.  A run longer than 256 rows (skewed keys) sends the
+//                         ~log2(n) - 1 varying bits (three 9-bit digits at 250M rows); k_local_bounds
+//                         cuts the result into ~4096-row tiles at run starts and k_sort_local ranks
+//                         every run of equal prefixes (a few rows) by full key in LDS and writes the
+//                         user columns.  A run longer than 256 rows (skewed keys) sends the
 //                         call to 8-bit digit passes over every varying byte (LSD, the same kernels),
 //                         which is also GM_PARAM_SORT_MODE 1.
 // The range scan over a sorted table (gm_key_range_scan) lives with the other row-filter scans in
@@ -131,13 +132,22 @@ __device__ __forceinline__ void for_rows(const KeyCols& c, int64_t n, int wide, 
   }
 }
 
-constexpr int OT = 256;    // or/and threads per block
+// The OR / AND of a strided sample of the keys (65,536 rows, the last row included): the host plans the
+// digits from it and k_sort_count counts them in the same read that takes the exact OR / AND; a plan
+// that the exact bits change is counted again (GM_PARAM_SORT_LAST reports the path either way)
+constexpr int SAMPLE = 65536;
 template <bool SH>
-__global__ __launch_bounds__(OT) void k_key_or_and(KeyCols c, int64_t n, unsigned long long* __restrict__ acc, int wide) {
+__global__ __launch_bounds__(256) void k_key_or_and_sample(KeyCols c, int64_t n, unsigned long long* __restrict__ acc) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t step = n > SAMPLE ? n / SAMPLE : 1;
   uint64_t zo = 0, za = ~0ull, bo = 0, ba = ~0ull;
-  for_rows<SH, OT / 64>(c, n, wide, [&](uint64_t z, uint32_t b) {
+  auto take = [&](int64_t r) {
+    const uint64_t z = c.z[r];
+    const uint32_t b = (uint32_t)c.bin[r] | (SH ? (uint32_t)c.sh[r] << 16 : 0u);
     zo |= z; za &= z; bo |= b; ba &= b;
-  });
+  };
+  if (i < SAMPLE && i * step < n) take(i * step);
+  if (i == 0) take(n - 1);
   zo = wave_or(zo); za = wave_and(za); bo = wave_or(bo); ba = wave_and(ba);
   if ((threadIdx.x & 63) == 0) {
     atomicOr(&acc[0], zo); atomicOr(&acc[1], bo); atomicAnd(&acc[2], za); atomicAnd(&acc[3], ba);
@@ -146,7 +156,8 @@ __global__ __launch_bounds__(OT) void k_key_or_and(KeyCols c, int64_t n, unsigne
 
 // Every pass's digit counts in one read: counts[base_k + d] = rows whose digit k (bits [off_k, off_k +
 // w_k) of K) is d, base_k = k * 512.  Four LDS copies of the counters (by wave) cut the atomic
-// collisions.
+// collisions.  ORAND: the same read also takes the exact OR / AND of the key columns into
+// acc[0..3] = OR z, OR bs, AND z, AND bs (bs = bin | shard << 16).
 constexpr int WMAX = 9;                 // widest digit: 512 buckets
 constexpr int NB_MAX = 1 << WMAX;
 struct DigitOffs {
@@ -159,16 +170,25 @@ __device__ __forceinline__ uint32_t key_digit_w(uint32_t bs, uint64_t z, int off
 }
 constexpr int CNT_LDS = 2816;           // 11 byte digits x 256, or 4 prefix digits x 512 (<= 2048)
 constexpr int CT = 1024;   // count threads per block
-template <bool SH>
-__global__ __launch_bounds__(CT) void k_sort_count(KeyCols c, int64_t n, DigitOffs o, uint32_t* __restrict__ counts, int wide) {
+template <bool SH, bool ORAND>
+__global__ __launch_bounds__(CT) void k_sort_count(KeyCols c, int64_t n, DigitOffs o, uint32_t* __restrict__ counts, int wide,
+                                                   unsigned long long* __restrict__ acc) {
   __shared__ uint32_t h[4][CNT_LDS];
   const int copy = (threadIdx.x >> 6) & 3;
   for (int i = threadIdx.x; i < 4 * CNT_LDS; i += CT) (&h[0][0])[i] = 0u;
   __syncthreads();
+  uint64_t zo = 0, za = ~0ull, bo = 0, ba = ~0ull;
   for_rows<SH, CT / 64>(c, n, wide, [&](uint64_t z, uint32_t b) {
+    if (ORAND) { zo |= z; za &= z; bo |= b; ba &= b; }
     for (int k = 0, bk = 0; k < o.np; bk += 1 << o.w[k], ++k)
       atomicAdd(&h[copy][bk + key_digit_w(b, z, o.off[k], o.w[k])], 1u);
   });
+  if (ORAND) {
+    zo = wave_or(zo); za = wave_and(za); bo = wave_or(bo); ba = wave_and(ba);
+    if ((threadIdx.x & 63) == 0) {
+      atomicOr(&acc[0], zo); atomicOr(&acc[1], bo); atomicAnd(&acc[2], za); atomicAnd(&acc[3], ba);
+    }
+  }
   __syncthreads();
   for (int k = 0, bk = 0; k < o.np; bk += 1 << o.w[k], ++k)
     for (int d = threadIdx.x; d < (1 << o.w[k]); d += CT) {
@@ -385,39 +405,49 @@ __device__ __forceinline__ uint32_t prefix4(uint32_t bs, uint64_t z, int4 o, int
   return p;
 }
 
+// the local tiles' bounds: bounds[k] = the first run start at or after k LSTEP (0 and n at the ends;
+// -1 and the flag when no run starts within RUN_MAX rows), one wave per bound, so that k_sort_local
+// reads its next tile's bounds while it ranks the current one
+__global__ __launch_bounds__(256) void k_local_bounds(const uint4* __restrict__ rec_in, int64_t n, int4 po, int pw,
+                                                      int64_t* __restrict__ bounds, uint32_t* __restrict__ flag) {
+  const int lane = threadIdx.x & 63;
+  const int64_t k = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t ntile = (n + LSTEP - 1) / LSTEP;
+  if (k > ntile) return;   // wave-uniform
+  int64_t p = min(n, k * LSTEP);
+  if (p > 0 && p < n) {
+    const uint4 v0 = rec_in[p - 1];
+    const uint32_t pp = prefix4(v0.w, rec_z(v0), po, pw);
+    int64_t found = -1;
+    for (int c = 0; c <= RUN_MAX / 64 && found < 0; ++c) {   // wave-uniform
+      const int64_t r = p + c * 64 + lane;
+      bool diff = r >= n;
+      if (!diff) { const uint4 v = rec_in[r]; diff = prefix4(v.w, rec_z(v), po, pw) != pp; }
+      const uint64_t bal = __ballot(diff);
+      if (bal) found = p + c * 64 + __builtin_ctzll(bal);
+    }
+    p = (found < 0 || found - p > RUN_MAX) ? -1 : found;
+    if (p < 0 && lane == 0) *flag = 1u;
+  }
+  if (lane == 0) bounds[k] = p;
+}
+
 template <bool SH>
 __global__ __launch_bounds__(LT) void k_sort_local(const uint4* __restrict__ rec_in, uint8_t* __restrict__ sh_out,
                                                    uint16_t* __restrict__ bin_out, uint64_t* __restrict__ z_out,
                                                    int64_t* __restrict__ perm_out, int64_t n, int4 po, int pw,
-                                                   uint32_t* __restrict__ flag) {
+                                                   uint32_t* __restrict__ flag, const int64_t* __restrict__ bounds) {
   __shared__ uint64_t s_z[LCAP];
   __shared__ uint32_t s_bs[LCAP];
   __shared__ uint32_t s_run[LCAP];   // prefix; then run start (low 16) | at a run start, its end << 16
-  __shared__ int64_t s_ab[2];
   __shared__ uint32_t s_wmax[LT / 64];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  auto pre_of = [&](int64_t r) -> uint32_t { const uint4 v = rec_in[r]; return prefix4(v.w, rec_z(v), po, pw); };
   const int64_t ntile = (n + LSTEP - 1) / LSTEP;
+  int64_t an = -1, bn = -1;   // the next tile's bounds (uniform: scalar loads, one tile ahead)
+  if ((int64_t)blockIdx.x < ntile) { an = bounds[blockIdx.x]; bn = bounds[blockIdx.x + 1]; }
   for (int64_t tk = blockIdx.x; tk < ntile; tk += gridDim.x) {   // block-uniform
-    if (wave < 2) {   // waves 0 / 1: the first run start at or after p (none within RUN_MAX rows: flag)
-      int64_t p = min(n, (tk + wave) * LSTEP);
-      if (p > 0 && p < n) {
-        const uint32_t pp = pre_of(p - 1);
-        int64_t found = -1;
-        for (int c = 0; c <= RUN_MAX / 64 && found < 0; ++c) {   // wave-uniform
-          const int64_t r = p + c * 64 + lane;
-          const bool diff = r >= n || pre_of(r) != pp;
-          const uint64_t bal = __ballot(diff);
-          if (bal) found = p + c * 64 + __builtin_ctzll(bal);
-        }
-        p = (found < 0 || found - p > RUN_MAX) ? -1 : found;
-        if (p < 0 && lane == 0) *flag = 1u;
-      }
-      if (lane == 0) s_ab[wave] = p;
-    }
-    __syncthreads();
-    const int64_t a = s_ab[0], b = s_ab[1];
-    __syncthreads();
+    const int64_t a = an, b = bn;
+    if (tk + gridDim.x < ntile) { an = bounds[tk + gridDim.x]; bn = bounds[tk + gridDim.x + 1]; }
     if (a < 0 || b < 0) continue;   // flagged: the host redoes the sort
     const int m = (int)(b - a);     // <= LSTEP + RUN_MAX = LCAP
     // the tile's rows: all LPT loads of a thread issued together; a row's input index stays in a
@@ -539,6 +569,63 @@ __global__ __launch_bounds__(STPB) void k_key_bytes(const uint8_t* __restrict__ 
   }
 }
 
+// The digits of one sort, from the OR / AND of the keys: `lsd` = every byte on which some keys differ
+// (LSD order); prefix mode = npre digits of pw <= 9 bits, each ending at the highest varying bit below
+// the previous one (only constant bits are skipped), over the top ~log2(n) - 1 varying bits (runs of
+// ~2 equal prefixes for uniform keys), when that is fewer passes than the varying bytes
+struct SortPlan {
+  std::vector<int> lsd;
+  int npre = 0, pw = 0, pofs[4] = {-1, -1, -1, -1};
+  bool prefix = false;
+  std::vector<int> first_offs() const {   // the first digit passes, LSD order
+    if (!prefix) return lsd;
+    std::vector<int> o(pofs, pofs + npre);
+    std::reverse(o.begin(), o.end());
+    return o;
+  }
+  DigitOffs first_digits() const {
+    DigitOffs o{};
+    const std::vector<int> f = first_offs();
+    o.np = (int)f.size();
+    for (int k = 0; k < o.np; ++k) { o.off[k] = f[k]; o.w[k] = prefix ? pw : 8; }
+    return o;
+  }
+};
+inline bool operator==(const DigitOffs& a, const DigitOffs& b) {
+  if (a.np != b.np) return false;
+  for (int k = 0; k < a.np; ++k)
+    if (a.off[k] != b.off[k] || a.w[k] != b.w[k]) return false;
+  return true;
+}
+static SortPlan plan_sort(const unsigned long long h[4], bool sh, int64_t n, int sort_mode) {
+  SortPlan p;
+  for (int b = 0; b < NPASS; ++b) {
+    if (b == 10 && !sh) continue;
+    const uint64_t o = b < 8 ? h[0] >> (8 * b) : h[1] >> (8 * (b - 8));
+    const uint64_t a = b < 8 ? h[2] >> (8 * b) : h[3] >> (8 * (b - 8));
+    if (((o ^ a) & 255u) != 0) p.lsd.push_back(8 * b);
+  }
+  if (p.lsd.empty()) return p;
+  const uint64_t vz = h[0] ^ h[2], vb = (h[1] ^ h[3]) & 0xffffffull;
+  auto varying = [&](int bit) -> bool { return bit < 64 ? ((vz >> bit) & 1u) : ((vb >> (bit - 64)) & 1u); };
+  int lg = 0;
+  while (((int64_t)1 << lg) < n) ++lg;
+  const int pbits = std::max(1, lg - 1);
+  p.npre = std::min(4, (pbits + WMAX - 1) / WMAX);
+  p.pw = std::min(WMAX, (pbits + p.npre - 1) / p.npre);
+  int nfound = 0;
+  int bit = 87;
+  for (int k = 0; k < p.npre; ++k) {
+    while (bit >= 0 && !varying(bit)) --bit;
+    if (bit < 0) break;
+    p.pofs[k] = std::max(0, bit - (p.pw - 1));
+    bit = p.pofs[k] - 1;
+    ++nfound;
+  }
+  p.prefix = sort_mode == 0 && (int)p.lsd.size() > p.npre && nfound == p.npre;
+  return p;
+}
+
 }  // namespace gm
 
 using namespace gm;
@@ -570,27 +657,58 @@ int gm_sort_keys(gm_ctx* ctx, const uint8_t* shard, const int16_t* bin, const in
   // 16-B loads of every column in the OR/AND and count reads
   const int user_wide = ((uintptr_t)z % 16) == 0 && ((uintptr_t)bin % 16) == 0 && (!sh || ((uintptr_t)sh % 16) == 0);
   const int64_t nchunk = (n + RCH - 1) / RCH;
-  const int ogrid = (int)std::max<int64_t>(1, std::min<int64_t>(2048, (nchunk + OT / 64 - 1) / (OT / 64)));
   const int cgrid = (int)std::max<int64_t>(1, std::min<int64_t>(512, (nchunk + CT / 64 - 1) / (CT / 64)));
-  // which key bits vary (k_key_or_and): acc = OR z, OR bs, AND z, AND bs (bs = bin | shard << 16)
+  const int64_t ntiles = (n + PTILE - 1) / PTILE;
+  uint4 *rec[2] = {nullptr, nullptr};
+  unsigned long long* status = nullptr;
+  uint32_t* counts = nullptr;
+  unsigned int* ctr = nullptr;
+  int64_t* lbounds = nullptr;
+  size_t counts_bytes = 0;
+  {  // context-owned workspace: records x 2 | granules | counts | tile counters | local bounds, 16-B aligned
+    auto al = [](size_t v) { return (v + 15) & ~(size_t)15; };
+    const size_t a_r = al((size_t)n * 16), a_st = al((size_t)ntiles * NB_MAX * 8), a_c = al((size_t)MAXTAG * NB_MAX * 4),
+                 a_t = al((size_t)MAXTAG * 4), a_b = al((size_t)((n + LSTEP - 1) / LSTEP + 1) * 8);
+    void* base = nullptr;
+    int wrc = ctx_workspace(ctx, WS_SORT, 2 * a_r + a_st + a_c + a_t + a_b, &base);
+    if (wrc) return wrc;
+    char* q = (char*)base;
+    rec[0] = (uint4*)q; q += a_r;
+    rec[1] = (uint4*)q; q += a_r;
+    status = (unsigned long long*)q; q += a_st;
+    counts = (uint32_t*)q; q += a_c;
+    ctr = (unsigned int*)q; q += a_t;
+    lbounds = (int64_t*)q;
+    counts_bytes = a_c;
+    GM_HIP(hipMemsetAsync(status, 0, a_st + a_c + a_t, s));   // granules (tag 0 = none), counts, counters
+  }
+  // which key bits vary: acc[0..3] = OR z, OR bs, AND z, AND bs of every key (k_sort_count), acc[8..11]
+  // the same over a sample (k_key_or_and_sample), acc[4] k_sort_local's flag
   unsigned long long* acc = (unsigned long long*)ctx->d_scratch;
   GM_HIP(hipMemsetAsync(acc, 0, 16, s));
   GM_HIP(hipMemsetAsync(acc + 2, 0xff, 16, s));
-  GM_HIP(hipMemsetAsync(acc + 4, 0, 8, s));   // k_sort_local's flag
-  if (sh) hipLaunchKernelGGL(k_key_or_and<true>, dim3(ogrid), dim3(OT), 0, s, in, n, acc, user_wide);
-  else hipLaunchKernelGGL(k_key_or_and<false>, dim3(ogrid), dim3(OT), 0, s, in, n, acc, user_wide);
+  GM_HIP(hipMemsetAsync(acc + 4, 0, 8, s));
+  GM_HIP(hipMemsetAsync(acc + 8, 0, 16, s));
+  GM_HIP(hipMemsetAsync(acc + 10, 0xff, 16, s));
+  if (sh) hipLaunchKernelGGL(k_key_or_and_sample<true>, dim3(SAMPLE / 256), dim3(256), 0, s, in, n, acc + 8);
+  else hipLaunchKernelGGL(k_key_or_and_sample<false>, dim3(SAMPLE / 256), dim3(256), 0, s, in, n, acc + 8);
   GM_CHECK_LAUNCH();
+  unsigned long long hs[4];
+  GM_HIP(hipMemcpyAsync(hs, acc + 8, sizeof(hs), hipMemcpyDeviceToHost, s));
+  GM_HIP(hipStreamSynchronize(s));
+  const SortPlan guess = plan_sort(hs, sh != nullptr, n, ctx->sort_mode);
+  // the guessed plan's first digit set counted in the read that takes the exact OR / AND
+  {
+    const DigitOffs o = guess.first_digits();
+    if (sh) hipLaunchKernelGGL((k_sort_count<true, true>), dim3(cgrid), dim3(CT), 0, s, in, n, o, counts, user_wide, acc);
+    else hipLaunchKernelGGL((k_sort_count<false, true>), dim3(cgrid), dim3(CT), 0, s, in, n, o, counts, user_wide, acc);
+    GM_CHECK_LAUNCH();
+  }
   unsigned long long hacc[4];
   GM_HIP(hipMemcpyAsync(hacc, acc, sizeof(hacc), hipMemcpyDeviceToHost, s));
   GM_HIP(hipStreamSynchronize(s));
-  // LSD digit offsets: every byte on which some keys differ
-  std::vector<int> lsd;
-  for (int p = 0; p < NPASS; ++p) {
-    if (p == 10 && !sh) continue;
-    const uint64_t o = p < 8 ? hacc[0] >> (8 * p) : hacc[1] >> (8 * (p - 8));
-    const uint64_t a = p < 8 ? hacc[2] >> (8 * p) : hacc[3] >> (8 * (p - 8));
-    if (((o ^ a) & 255u) != 0) lsd.push_back(8 * p);
-  }
+  const SortPlan plan = plan_sort(hacc, sh != nullptr, n, ctx->sort_mode);
+  const std::vector<int>& lsd = plan.lsd;
   if (lsd.empty()) {  // every key equal: table order = input order
     if (sh) GM_HIP(hipMemcpyAsync(shard_out, sh, (size_t)n, hipMemcpyDeviceToDevice, s));
     GM_HIP(hipMemcpyAsync(bin_out, bin, (size_t)n * 2, hipMemcpyDeviceToDevice, s));
@@ -601,49 +719,12 @@ int gm_sort_keys(gm_ctx* ctx, const uint8_t* shard, const int16_t* bin, const in
     ctx->sort_last = 0;
     return GM_OK;
   }
-  // prefix passes: npre digits of pw <= 9 bits, each ending at the highest varying bit below the
-  // previous one (only constant bits are skipped), over the top ~log2(n) - 1 varying bits (runs of
-  // ~2 equal prefixes for uniform keys), when that is fewer passes than the varying bytes
-  const uint64_t vz = hacc[0] ^ hacc[2], vb = (hacc[1] ^ hacc[3]) & 0xffffffull;
-  auto varying = [&](int bit) -> bool { return bit < 64 ? ((vz >> bit) & 1u) : ((vb >> (bit - 64)) & 1u); };
-  int lg = 0;
-  while (((int64_t)1 << lg) < n) ++lg;
-  const int pbits = std::max(1, lg - 1);
-  const int npre = std::min(4, (pbits + WMAX - 1) / WMAX);
-  const int pw = std::min(WMAX, (pbits + npre - 1) / npre);
-  int pofs[4] = {-1, -1, -1, -1};
-  int nfound = 0;
-  {
-    int bit = 87;
-    for (int k = 0; k < npre; ++k) {
-      while (bit >= 0 && !varying(bit)) --bit;
-      if (bit < 0) break;
-      pofs[k] = std::max(0, bit - (pw - 1));
-      bit = pofs[k] - 1;
-      ++nfound;
-    }
-  }
-  const bool prefix_mode = ctx->sort_mode == 0 && (int)lsd.size() > npre && nfound == npre;
-  const int64_t ntiles = (n + PTILE - 1) / PTILE;
-  uint4 *rec[2] = {nullptr, nullptr};
-  unsigned long long* status = nullptr;
-  uint32_t* counts = nullptr;
-  unsigned int* ctr = nullptr;
-  {  // context-owned workspace: records x 2 | granules | counts | tile counters, 16-B aligned pieces
-    auto al = [](size_t v) { return (v + 15) & ~(size_t)15; };
-    const size_t a_r = al((size_t)n * 16), a_st = al((size_t)ntiles * NB_MAX * 8), a_c = al((size_t)MAXTAG * NB_MAX * 4),
-                 a_t = al((size_t)MAXTAG * 4);
-    void* base = nullptr;
-    int wrc = ctx_workspace(ctx, WS_SORT, 2 * a_r + a_st + a_c + a_t, &base);
-    if (wrc) return wrc;
-    char* q = (char*)base;
-    rec[0] = (uint4*)q; q += a_r;
-    rec[1] = (uint4*)q; q += a_r;
-    status = (unsigned long long*)q; q += a_st;
-    counts = (uint32_t*)q; q += a_c;
-    ctr = (unsigned int*)q;
-    GM_HIP(hipMemsetAsync(status, 0, a_st + a_c + a_t, s));   // granules (tag 0 = none), counts, counters
-  }
+  // the sample's plan holds when the exact bits give the same first digits; else count again
+  bool counted = guess.first_digits() == plan.first_digits();
+  if (!counted) GM_HIP(hipMemsetAsync(counts, 0, counts_bytes, s));
+  const bool prefix_mode = plan.prefix;
+  const int npre = plan.npre, pw = plan.pw;
+  const int* pofs = plan.pofs;
   // digit passes at bit offsets `offs` (LSD order) from the caller's columns, tags tag0 + 1...; the
   // last pass lands in the user outputs when `to_user_last`, else in records (*last_rec)
   const uint4* last_rec = nullptr;
@@ -653,9 +734,12 @@ int gm_sort_keys(gm_ctx* ctx, const uint8_t* shard, const int16_t* bin, const in
     o.np = np;
     for (int k = 0; k < np; ++k) { o.off[k] = offs[k]; o.w[k] = w; }
     uint32_t* cnt = counts + (size_t)tag0 * NB_MAX;
-    if (sh) hipLaunchKernelGGL(k_sort_count<true>, dim3(cgrid), dim3(CT), 0, s, in, n, o, cnt, user_wide);
-    else hipLaunchKernelGGL(k_sort_count<false>, dim3(cgrid), dim3(CT), 0, s, in, n, o, cnt, user_wide);
-    if (hipGetLastError() != hipSuccess) return hip_fail(hipErrorLaunchFailure, "k_sort_count");
+    if (!counted) {
+      if (sh) hipLaunchKernelGGL((k_sort_count<true, false>), dim3(cgrid), dim3(CT), 0, s, in, n, o, cnt, user_wide, nullptr);
+      else hipLaunchKernelGGL((k_sort_count<false, false>), dim3(cgrid), dim3(CT), 0, s, in, n, o, cnt, user_wide, nullptr);
+      if (hipGetLastError() != hipSuccess) return hip_fail(hipErrorLaunchFailure, "k_sort_count");
+    }
+    counted = false;   // a later call (the fallback) counts its own digits
     for (int k = 0; k < np; ++k) {
       PassArgs a{};
       a.in = in;
@@ -680,18 +764,19 @@ int gm_sort_keys(gm_ctx* ctx, const uint8_t* shard, const int16_t* bin, const in
     return GM_OK;
   };
   if (prefix_mode) {
-    std::vector<int> offs(pofs, pofs + npre);
-    std::reverse(offs.begin(), offs.end());   // LSD order: lowest digit first
-    int rc = passes(offs, pw, false, 0);
+    int rc = passes(plan.first_offs(), pw, false, 0);
     if (rc) return rc;
     const int4 po = make_int4(pofs[0], pofs[1], pofs[2], pofs[3]);
     const int lgrid = resident_blocks((const void*)k_sort_local<false>, ctx->device, LT, 2);
+    const int64_t nbound = (n + LSTEP - 1) / LSTEP + 1;
+    hipLaunchKernelGGL(k_local_bounds, dim3((unsigned)((nbound + 3) / 4)), dim3(256), 0, s, last_rec, n, po, pw, lbounds,
+                       (uint32_t*)(acc + 4));
     if (sh)
       hipLaunchKernelGGL(k_sort_local<true>, dim3(lgrid), dim3(LT), 0, s, last_rec, shard_out, (uint16_t*)bin_out,
-                         (uint64_t*)z_out, perm_out, n, po, pw, (uint32_t*)(acc + 4));
+                         (uint64_t*)z_out, perm_out, n, po, pw, (uint32_t*)(acc + 4), lbounds);
     else
       hipLaunchKernelGGL(k_sort_local<false>, dim3(lgrid), dim3(LT), 0, s, last_rec, nullptr, (uint16_t*)bin_out,
-                         (uint64_t*)z_out, perm_out, n, po, pw, (uint32_t*)(acc + 4));
+                         (uint64_t*)z_out, perm_out, n, po, pw, (uint32_t*)(acc + 4), lbounds);
     GM_CHECK_LAUNCH();
     uint32_t flag = 0;
     GM_HIP(hipMemcpyAsync(&flag, acc + 4, 4, hipMemcpyDeviceToHost, s));

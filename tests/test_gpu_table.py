@@ -135,6 +135,41 @@ def test_sort_keys_prefix_path_at_bench_size(gpu, kind):
     _check_table_order_on_device(b, z, ob, oz, op)
 
 
+@pytest.mark.parametrize("where", ["bin", "shard", "z"])
+@pytest.mark.parametrize("mode", [0, 1])
+def test_sort_keys_sample_misses_a_varying_bit(gpu, where, mode):
+    """The digits are planned from the OR / AND of a strided sample (every (n // 65536)-th row and
+    the last) and counted in the read that takes the exact OR / AND; here the highest varying bit
+    changes in one row the sample skips, so the exact plan differs and the digits are counted again."""
+    import torch
+    from geomesa_amd import _lib
+    n, odd = 1_000_003, 500_001
+    assert odd % (n // 65536) != 0
+    rng = np.random.default_rng(11)
+    bins = np.full(n, 2610, np.int16)
+    z = rng.integers(0, 2**40, n, dtype=np.int64)
+    shard = np.full(n, 2, np.uint8)
+    if where == "bin":
+        bins[odd] = 2700
+    elif where == "shard":
+        shard[odd] = 3
+    else:
+        z[odd] |= 1 << 62
+    ctx = _lib.context()
+    ctx.set_param(_lib.GM_PARAM_SORT_MODE, mode)
+    db, dz, ds = torch.from_numpy(bins).cuda(), torch.from_numpy(z).cuda(), torch.from_numpy(shard).cuda()
+    ob, oz, os_ = torch.empty_like(db), torch.empty_like(dz), torch.empty_like(ds)
+    op = torch.empty(n, dtype=torch.int64, device="cuda")
+    _lib.check(ctx.lib.gm_sort_keys(ctx.handle, _lib.ptr(ds), _lib.ptr(db), _lib.ptr(dz), n, _lib.ptr(os_),
+                                    _lib.ptr(ob), _lib.ptr(oz), _lib.ptr(op)), "sort")
+    ctx.set_param(_lib.GM_PARAM_SORT_MODE, 0)
+    order = expected_order(bins, z, shard)
+    assert np.array_equal(as_np(op), order)
+    assert np.array_equal(as_np(ob), bins[order]) and np.array_equal(as_np(oz), z[order])
+    assert np.array_equal(as_np(os_), shard[order])
+    assert as_np(op)[-1] == odd   # the one key with the highest varying bit set sorts last
+
+
 @pytest.mark.parametrize("in_off,out_off", [(1, 0), (0, 1), (1, 3)])
 def test_sort_keys_unaligned_columns(gpu, in_off, out_off):
     """Caller columns off the 16-B grid (slices): the pair-load paths must not be taken for them."""
