@@ -15,7 +15,7 @@
 //                         {count, tag} granules), and the tile leaves as digit runs of 16-B records
 //                         {z, row, bin | shard << 16}.  The passes order the rows by the top
 //                         ~log2(n) - 1 varying bits (three 9-bit digits at 250M rows); k_local_bounds
-//                         cuts the result into ~4096-row tiles at run starts and k_sort_local ranks
+//                         cuts the result into ~2048-row tiles at run starts and k_sort_local ranks
 //                         every run of equal prefixes (a few rows) by full key in LDS and writes the
 //                         user columns.  A run longer than 256 rows (skewed keys) sends the
 //                         call to 8-bit digit passes over every varying byte (LSD, the same kernels),
@@ -387,7 +387,7 @@ __global__ __launch_bounds__(PT) void k_sort_pass(PassArgs a) {
 // row.  A run longer than RUN_MAX rows (skewed or repeated keys) sets *flag and the host sorts with
 // digit passes over every varying byte instead.
 #ifndef GM_SORT_LCAP
-#define GM_SORT_LCAP 4096
+#define GM_SORT_LCAP 2048
 #endif
 #ifndef GM_SORT_LT
 #define GM_SORT_LT 512
