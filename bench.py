@@ -429,14 +429,15 @@ def ranges_batch(dist, fn, args, n_local, nq, reps=3):
 def sort_bytes(b, z, n, last):
     """Algorithmic bytes of gm_sort_keys over n unsharded rows, for the path the library reports
     (GM_PARAM_SORT_LAST: digit passes, + 256 when the runs of equal prefixes were ranked locally):
-    the OR/AND read of the key columns that finds the varying bits and the read that counts every
-    pass's digits (10 B/row each); the first pass reads the columns (10 B) and writes 16-B records
+    the read that counts every pass's digits and takes the exact varying bits (10 B/row; the digits are
+    planned from a 65,536-row sample, and a plan the exact bits change costs a second count read, which
+    the bench's keys never need); the first pass reads the columns (10 B) and writes 16-B records
     {z, row, bin}, every later pass reads and writes records (32 B); then the local ranking reads the
     records and writes z, bin and the 8-B permutation (16 + 18 B), or the last digit pass writes those
     itself (18 B instead of 16).  Returns (bytes, passes, path)."""
     local = last >= 256
     npass = last - 256 if local else last
-    total = 20.0 * n
+    total = 10.0 * n
     if npass:
         total += (10.0 + 16.0 + 32.0 * (npass - 1)) * n
     if local:

@@ -148,9 +148,19 @@ __global__ __launch_bounds__(256) void k_key_or_and_sample(KeyCols c, int64_t n,
   };
   if (i < SAMPLE && i * step < n) take(i * step);
   if (i == 0) take(n - 1);
+  __shared__ uint64_t s_oa[4][4];
   zo = wave_or(zo); za = wave_and(za); bo = wave_or(bo); ba = wave_and(ba);
   if ((threadIdx.x & 63) == 0) {
-    atomicOr(&acc[0], zo); atomicOr(&acc[1], bo); atomicAnd(&acc[2], za); atomicAnd(&acc[3], ba);
+    uint64_t* e = s_oa[threadIdx.x >> 6];
+    e[0] = zo; e[1] = bo; e[2] = za; e[3] = ba;
+  }
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    const int j = threadIdx.x;
+    uint64_t v = s_oa[0][j];
+    for (int w = 1; w < 4; ++w) v = j < 2 ? (v | s_oa[w][j]) : (v & s_oa[w][j]);
+    if (j < 2) atomicOr(&acc[j], (unsigned long long)v);
+    else atomicAnd(&acc[j], (unsigned long long)v);
   }
 }
 
@@ -183,13 +193,22 @@ __global__ __launch_bounds__(CT) void k_sort_count(KeyCols c, int64_t n, DigitOf
     for (int k = 0, bk = 0; k < o.np; bk += 1 << o.w[k], ++k)
       atomicAdd(&h[copy][bk + key_digit_w(b, z, o.off[k], o.w[k])], 1u);
   });
-  if (ORAND) {
+  __shared__ uint64_t s_oa[ORAND ? CT / 64 : 1][4];
+  if (ORAND) {   // per wave, then one device atomic per value per block (not per wave: same 4 addresses)
     zo = wave_or(zo); za = wave_and(za); bo = wave_or(bo); ba = wave_and(ba);
     if ((threadIdx.x & 63) == 0) {
-      atomicOr(&acc[0], zo); atomicOr(&acc[1], bo); atomicAnd(&acc[2], za); atomicAnd(&acc[3], ba);
+      uint64_t* e = s_oa[threadIdx.x >> 6];
+      e[0] = zo; e[1] = bo; e[2] = za; e[3] = ba;
     }
   }
   __syncthreads();
+  if (ORAND && threadIdx.x < 4) {
+    const int j = threadIdx.x;
+    uint64_t v = s_oa[0][j];
+    for (int w = 1; w < CT / 64; ++w) v = j < 2 ? (v | s_oa[w][j]) : (v & s_oa[w][j]);
+    if (j < 2) atomicOr(&acc[j], (unsigned long long)v);
+    else atomicAnd(&acc[j], (unsigned long long)v);
+  }
   for (int k = 0, bk = 0; k < o.np; bk += 1 << o.w[k], ++k)
     for (int d = threadIdx.x; d < (1 << o.w[k]); d += CT) {
       const int i = bk + d;
