@@ -26,7 +26,6 @@ STREAMING = {
     "xz2_index": ("k_xz2_index_v", "xz", 40.0),
     "z3_histogram": ("k_z3_hist_lds<", "points", 24.0),
     "pip_relate": ("k_pip_relate", "points", 21.0),
-    "sort_or_and": ("k_key_or_and<", "rows", 10.0),
     "sort_count": ("k_sort_count<", "rows", 10.0),
     "sort_pass_first": ("k_sort_pass<false, false", "rows", 26.0),
     "sort_pass": ("k_sort_pass<true, false", "rows", 32.0),
