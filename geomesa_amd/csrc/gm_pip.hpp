@@ -59,7 +59,6 @@ struct PipDev {
   const uint32_t* list_ent;      // entries in cell-word form (kind INTERIOR or BOUNDARY)
   const double* blob;            // boundary blobs, 16-byte aligned
   const uint32_t* cell_sc;       // per cell: the cell word with the boundary shortcuts applied (k_build_shortcut)
-  const uint32_t* cell_scb;      // GM_JX_SCBLK (tuning build): cell_sc stored by coarse cell (sc8_at order)
   const uint32_t* coarse_sc;     // the join's coarse words over cell_sc; LIST words carry sub-block masks
   int32_t coarse_fmt;            // COARSE_EMPTY_MASK / COARSE_MAIN (see coarse_mask)
   const uint4* line_ent;         // line shortcuts, two uint4 each (see "Boundary shortcuts")
@@ -413,21 +412,6 @@ __device__ __forceinline__ int sc8_locate(uint2 w, double x, double y, const Pip
 constexpr int SUB_LOG = CF_LOG - 2;
 static_assert(CF_LOG >= 2, "sub-block masks need at least 4 x 4 fine cells per coarse cell");
 enum : int32_t { COARSE_EMPTY_MASK = 0, COARSE_MAIN = 1 };
-
-// the join's 8-B fine word of cell (cx, cy): with GM_JX_SC8BLK (tuning build) the words are stored by
-// coarse cell, each coarse cell's 8 x 8 words contiguous (512 B: four 128-B lines), else row-major
-__device__ __forceinline__ int64_t blk_at(int cx, int cy, const PipDev& d) {
-  constexpr int CM = (1 << CF_LOG) - 1;
-  return ((int64_t)((cy >> CF_LOG) * d.gxc + (cx >> CF_LOG)) << (2 * CF_LOG)) + ((cy & CM) << CF_LOG) + (cx & CM);
-}
-__device__ __forceinline__ int64_t sc8_at(int cx, int cy, const PipDev& d) {
-#ifdef GM_JX_SC8BLK
-  constexpr int CM = (1 << CF_LOG) - 1;
-  return ((int64_t)((cy >> CF_LOG) * d.gxc + (cx >> CF_LOG)) << (2 * CF_LOG)) + ((cy & CM) << CF_LOG) + (cx & CM);
-#else
-  return (int64_t)cy * d.gx + cx;
-#endif
-}
 
 __device__ __forceinline__ uint32_t coarse_mask(uint32_t w, int cx, int cy, int32_t fmt) {
   if ((w >> 30) != CELL_LIST) return w;

@@ -887,22 +887,13 @@ __global__ __launch_bounds__(256) void k_build_shortcut(PipDev d, int64_t ncell,
   }
 }
 
-#ifdef GM_JX_SCBLK
-__global__ __launch_bounds__(256) void k_build_scb(const uint32_t* __restrict__ cell_sc, int64_t ncell, PipDev d,
-                                                   uint32_t* __restrict__ out) {
-  for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < ncell; c += (int64_t)gridDim.x * blockDim.x)
-    out[blk_at((int)(c % d.gx), (int)(c / d.gx), d)] = cell_sc[c];
-}
-#endif
-
 // cell_sc8 (gm_pip.hpp, "8-B fine words"): cell_sc zero-extended; a LINE word of a polygon below 2^14
 // replaced by its entry's lines when they fit:
 //  * one line: requantized to 2^-12 cell (A / 4, B / 4, C / 4) when the deviation from the exact line
 //    (entry deviation SC_DEV / 4 plus the rounding, over the enlarged cell) stays a unit below SC8_T;
 //  * two lines meeting inside the cell: their intersection and normal angles at 10 bits (tag 2)
 __global__ __launch_bounds__(256) void k_build_sc8(const uint32_t* __restrict__ cell_sc, const uint4* __restrict__ line_ent,
-                                                   int64_t n_line, int64_t ncell, uint2* __restrict__ out, int gx,
-                                                   int gxc) {
+                                                   int64_t n_line, int64_t ncell, uint2* __restrict__ out) {
   for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < ncell; c += (int64_t)gridDim.x * blockDim.x) {
     const uint32_t w = cell_sc[c];
     uint2 o = make_uint2(w, 0u);
@@ -958,16 +949,7 @@ __global__ __launch_bounds__(256) void k_build_sc8(const uint32_t* __restrict__ 
       }
 #endif
     }
-#ifdef GM_JX_SC8BLK
-    {
-      constexpr int CM = (1 << CF_LOG) - 1;
-      const int cx = (int)(c % gx), cy = (int)(c / gx);
-      out[((int64_t)((cy >> CF_LOG) * gxc + (cx >> CF_LOG)) << (2 * CF_LOG)) + ((cy & CM) << CF_LOG) + (cx & CM)] = o;
-    }
-#else
-    (void)gx; (void)gxc;
     out[c] = o;
-#endif
   }
 }
 
@@ -1045,12 +1027,7 @@ int make_shortcut(gm_pip_index* ix) {
   ix->dev.cell_sc = (const uint32_t*)p;
   {   // the join's 8-B fine words (k_build_sc8, after the line entries)
     void* p8 = nullptr;
-#ifdef GM_JX_SC8BLK   // by coarse cell: gxc x gyc blocks of 8 x 8 words
-    const int64_t n8 = std::max<int64_t>(ncell, (int64_t)ix->dev.gxc * ((ix->dev.gy + (1 << CF_LOG) - 1) >> CF_LOG) << (2 * CF_LOG));
-#else
-    const int64_t n8 = ncell;
-#endif
-    GM_HIP(hipMalloc(&p8, (size_t)std::max<int64_t>(n8, 1) * 8));
+    GM_HIP(hipMalloc(&p8, (size_t)std::max<int64_t>(ncell, 1) * 8));
     ix->allocs.push_back(p8);
     ix->dev.cell_sc8 = (const uint2*)p8;
     if (ncell == 0) GM_HIP(hipMemsetD32Async((hipDeviceptr_t)p8, CELL_EMPTY << 30, 2, s));
@@ -1107,17 +1084,7 @@ int make_shortcut(gm_pip_index* ix) {
   }
   if (!rc) {
     hipLaunchKernelGGL(k_build_sc8, dim3(g), dim3(256), 0, s, (const uint32_t*)p, ix->dev.line_ent, ix->dev.n_line, ncell,
-                       (uint2*)ix->dev.cell_sc8, ix->dev.gx, ix->dev.gxc);
-#ifdef GM_JX_SCBLK
-    {
-      void* pb = nullptr;
-      const int64_t nb = std::max<int64_t>(ncell, (int64_t)ix->dev.gxc * ((ix->dev.gy + (1 << CF_LOG) - 1) >> CF_LOG) << (2 * CF_LOG));
-      GM_HIP(hipMalloc(&pb, (size_t)std::max<int64_t>(nb, 1) * 4));
-      ix->allocs.push_back(pb);
-      hipLaunchKernelGGL(k_build_scb, dim3(g), dim3(256), 0, s, (const uint32_t*)p, ncell, ix->dev, (uint32_t*)pb);
-      ix->dev.cell_scb = (const uint32_t*)pb;
-    }
-#endif
+                       (uint2*)ix->dev.cell_sc8);
     const int gxc = ix->dev.gxc, gyc = (ix->dev.gy + (1 << CF_LOG) - 1) >> CF_LOG;
     hipLaunchKernelGGL(k_build_coarse_sc, dim3((unsigned)std::min<int64_t>(65536, ((int64_t)gxc * gyc + 255) / 256)), dim3(256),
                        0, s, (const uint32_t*)p, ix->dev.gx, ix->dev.gy, gxc, gyc, ix->dev.coarse_fmt,

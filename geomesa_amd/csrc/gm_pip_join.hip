@@ -387,7 +387,7 @@ __global__ __launch_bounds__(QTPB) void k_pip_join_q(const double* __restrict__ 
       const int a = fn - cnt + lane;
       pend_w = make_uint2(CELL_EMPTY << 30, 0u);
       if (lane < cnt)
-        pend_w = d.cell_sc8[sc8_at(cell_of(fx[a], d.gx0, d.inv_cw, d.gx), cell_of(fy[a], d.gy0, d.inv_ch, d.gy), d)];
+        pend_w = d.cell_sc8[(int64_t)cell_of(fy[a], d.gy0, d.inv_ch, d.gy) * d.gx + cell_of(fx[a], d.gx0, d.inv_cw, d.gx)];
       pb = fn - cnt;
       pc = cnt;
       pend = true;
@@ -473,7 +473,7 @@ __global__ __launch_bounds__(256) void k_pip_census(const double* __restrict__ p
     if ((w >> 30) == CELL_EMPTY) { c[JC_COARSE_EMPTY]++; continue; }
     if ((w >> 30) == CELL_INTERIOR) { c[JC_COARSE_INTERIOR]++; continue; }
     c[JC_FINE]++;
-    const uint2 w8 = d.cell_sc8[sc8_at(cx, cy, d)];
+    const uint2 w8 = d.cell_sc8[(int64_t)cy * d.gx + cx];
     if (sc8_inline(w8)) {   // one inline line (counted apart from the line entries)
       c[JC_FINE_INLINE]++;
       if ((w8.y >> 30) == 2u) c[JC_FINE_INLINE2]++;

@@ -114,11 +114,7 @@ __global__ __launch_bounds__(RTPB) void k_pip_relate(const int32_t* __restrict__
       }
 #pragma unroll
       for (int u = 0; u < RILP; ++u)
-#ifdef GM_JX_SCBLK
-        if ((w[u] >> 30) == CELL_LIST) w[u] = d.cell_scb[blk_at(cx[u], cy[u], d)];   // boundary shortcuts applied
-#else
         if ((w[u] >> 30) == CELL_LIST) w[u] = d.cell_sc[(int64_t)cy[u] * d.gx + cx[u]];   // boundary shortcuts applied
-#endif
       uint8_t rv[RILP];
       bool dir[RILP];
 #pragma unroll
