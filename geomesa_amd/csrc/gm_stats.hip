@@ -12,8 +12,7 @@
 // nonzero counters with one 64-bit device atomic each at the end, so HBM traffic is the 24 B/point
 // read plus grid x counters x 8 B; the grid is one resident wave of workgroups (1-2 per CU).  A
 // histogram larger than one LDS block of int32 counters keeps biased 16-bit counters instead (two
-// per word, NARROW below: 1024 x 54 week bins fit one pass; PER, a tuning build, drains plain halves
-// periodically instead of returning atomics), and beyond that takes up to
+// per word, NARROW below: 1024 x 54 week bins fit one pass), and beyond that takes up to
 // HIST_MAX_PASSES passes over the points, one per row block; beyond that it adds straight into the
 // 64-bit device counters (scattered per-lane device atomics run ~22 G/s on MI355X, so they only win
 // over many passes).
@@ -26,9 +25,6 @@ namespace gm {
 constexpr int HTPB = 1024;
 constexpr int HIST_LDS_MAX = 32768;  // int32 counters per workgroup (128 KB of the 160 KB LDS)
 constexpr int HIST_MAX_PASSES = 4;
-#ifndef GM_HIST_HU_PER
-#define GM_HIST_HU_PER 2   // pairs per lane in flight in the PER loop (PER_CHK * HU * 2 * HTPB <= 0x4000)
-#endif
 
 struct HistArgs {
   int64_t n;
@@ -155,14 +151,7 @@ __device__ __forceinline__ void narrow_dec(uint32_t* w, int sh, unsigned long lo
   }
 }
 
-// PER (observe, 16-B aligned columns): 16-bit halves from 0 with plain increments (no returning
-// atomic); every PER_CHK loop trips (<= 16384 points per workgroup) the workgroup moves every half at
-// or above 0x8000 to the device counters, so a half stays below 0x8000 + 0x4000 and never carries.
-// Would replace NARROW for observe (1024 x 54 week bins in one pass); GM_HIST_PER tuning build.
-constexpr int PER_CHK = 4;
-static_assert(PER_CHK * GM_HIST_HU_PER * 2 * HTPB <= 0x4000, "a half must not carry between drains");
-
-template <int PERIOD, bool UNOBS, bool VEC, bool NARROW, bool TOP, bool PER = false>
+template <int PERIOD, bool UNOBS, bool VEC, bool NARROW, bool TOP>
 __global__ __launch_bounds__(HTPB) void k_z3_hist_lds(const double* __restrict__ x, const double* __restrict__ y,
                                                       const int64_t* __restrict__ t, HistArgs a,
                                                       uint8_t* __restrict__ present,
@@ -170,14 +159,14 @@ __global__ __launch_bounds__(HTPB) void k_z3_hist_lds(const double* __restrict__
                                                       unsigned long long* __restrict__ tally) {
   extern __shared__ int lds[];
   const int total = a.row_n * a.length;
-  const int cwords = (NARROW || PER) ? (total + 1) / 2 : total;
+  const int cwords = NARROW ? (total + 1) / 2 : total;
   int* cnt = lds;                          // [row_n * length] (NARROW: 16-bit halves)
   int* pres = lds + cwords;                // [row_n]: bin present (observe sets, unobserve reads)
   uint32_t* sp = (uint32_t*)(pres + a.row_n);  // [2048]: spread3_11 table
   __shared__ int s_skip, s_out;
   counts += (int64_t)a.row_lo * a.length;
   present += a.row_lo;
-  for (int i = threadIdx.x; i < cwords; i += HTPB) cnt[i] = (NARROW && !PER) ? (int)(NB | (NB << 16)) : 0;
+  for (int i = threadIdx.x; i < cwords; i += HTPB) cnt[i] = NARROW ? (int)(NB | (NB << 16)) : 0;
   for (int i = threadIdx.x; i < a.row_n; i += HTPB) pres[i] = UNOBS ? (int)present[i] : 0;
   fill_spread_table(sp, threadIdx.x, HTPB);
   if (threadIdx.x == 0) { s_skip = 0; s_out = 0; }
@@ -196,59 +185,16 @@ __global__ __launch_bounds__(HTPB) void k_z3_hist_lds(const double* __restrict__
         else atomicAdd(&cnt[c], -1);
       }
     } else {
-      if (PER) atomicAdd((uint32_t*)&cnt[c >> 1], 1u << ((c & 1) * 16));
-      else if (NARROW) narrow_inc((uint32_t*)&cnt[c >> 1], (c & 1) * 16, &counts[c]);
+      if (NARROW) narrow_inc((uint32_t*)&cnt[c >> 1], (c & 1) * 16, &counts[c]);
       else atomicAdd(&cnt[c], 1);
       // binMap.getOrElseUpdate(timeBin, newBins): a row is present iff one of its features was
       // counted; int32 counters only grow here, so the flush derives it from the row (no per-point
       // LDS read); biased 16-bit halves move to the device counters and cannot tell, so they mark it
-      if ((NARROW || PER) && !pres[rb]) pres[rb] = 1;
+      if (NARROW && !pres[rb]) pres[rb] = 1;
     }
   };
   const int64_t stride = (int64_t)gridDim.x * HTPB;
-  if (VEC && PER) {
-    // the workgroup's trips are counted from its first pair, so the drains below are block-uniform
-    const dv2* x2 = (const dv2*)x;
-    const dv2* y2 = (const dv2*)y;
-    const lv2* t2 = (const lv2*)t;
-    const int64_t np = a.n >> 1, b0 = (int64_t)blockIdx.x * HTPB;
-    constexpr int HU = GM_HIST_HU_PER;
-    dv2 xa[HU], ya[HU];
-    lv2 ta[HU];
-    const int64_t p0 = b0 + threadIdx.x;
-#pragma unroll
-    for (int u = 0; u < HU; ++u) {
-      const int64_t q = p0 + u * stride;
-      if (q < np) { xa[u] = ld_stream(&x2[q]); ya[u] = ld_stream(&y2[q]); ta[u] = ld_stream(&t2[q]); }
-    }
-    for (int it = 0; b0 + (int64_t)it * HU * stride < np; ++it) {   // block-uniform
-      const int64_t p = p0 + (int64_t)it * HU * stride, pn = p + HU * stride;
-      dv2 xb[HU], yb[HU];
-      lv2 tb[HU];
-#pragma unroll
-      for (int u = 0; u < HU; ++u) {
-        const int64_t q = pn + u * stride;
-        if (q < np) { xb[u] = ld_stream(&x2[q]); yb[u] = ld_stream(&y2[q]); tb[u] = ld_stream(&t2[q]); }
-      }
-#pragma unroll
-      for (int u = 0; u < HU; ++u) {
-        if (p + u * stride < np) { one(xa[u].x, ya[u].x, ta[u].x); one(xa[u].y, ya[u].y, ta[u].y); }
-        xa[u] = xb[u]; ya[u] = yb[u]; ta[u] = tb[u];
-      }
-      if ((it % PER_CHK) == PER_CHK - 1) {   // drain: <= PER_CHK * HU * 2 * HTPB = 16384 increments since the last
-        __syncthreads();
-        for (int i = threadIdx.x; i < cwords; i += HTPB) {
-          const uint32_t v = (uint32_t)cnt[i];
-          uint32_t sub = 0;
-          if ((v & 0xFFFFu) >= 0x8000u) { sub |= 0x8000u; atomicAdd(&counts[2 * i], 0x8000ull); }
-          if ((v >> 16) >= 0x8000u) { sub |= 0x8000u << 16; atomicAdd(&counts[2 * i + 1], 0x8000ull); }
-          if (sub) cnt[i] = (int)(v - sub);
-        }
-        __syncthreads();
-      }
-    }
-    if ((a.n & 1) && blockIdx.x == 0 && threadIdx.x == 0) one(x[a.n - 1], y[a.n - 1], t[a.n - 1]);
-  } else if (VEC) {
+  if (VEC) {
     const dv2* x2 = (const dv2*)x;
     const dv2* y2 = (const dv2*)y;
     const lv2* t2 = (const lv2*)t;
@@ -290,11 +236,10 @@ __global__ __launch_bounds__(HTPB) void k_z3_hist_lds(const double* __restrict__
   if (out) atomicAdd(&s_out, out);
   __syncthreads();
   for (int i = threadIdx.x; i < total; i += HTPB) {
-    const int v = (NARROW || PER) ? (int)((((uint32_t)cnt[i >> 1]) >> ((i & 1) * 16)) & 0xFFFFu) - (PER ? 0 : (int)NB)
-                                  : cnt[i];
+    const int v = NARROW ? (int)((((uint32_t)cnt[i >> 1]) >> ((i & 1) * 16)) & 0xFFFFu) - (int)NB : cnt[i];
     if (v) atomicAdd(&counts[i], (unsigned long long)(long long)v);
   }
-  if (!UNOBS && !NARROW && !PER) {   // a row with a nonzero counter was seen by this workgroup
+  if (!UNOBS && !NARROW) {   // a row with a nonzero counter was seen by this workgroup
     for (int i = threadIdx.x; i < total; i += HTPB)
       if (cnt[i] && !pres[i / a.length]) pres[i / a.length] = 1;
     __syncthreads();
@@ -353,24 +298,17 @@ int launch_hist(gm_ctx* ctx, const double* x, const double* y, const int64_t* t,
 #else
   const bool narrow = rows32 < a.n_bins;
 #endif
-  const bool vec = aligned16(x) && aligned16(y) && aligned16(t);
-  // observe over aligned columns: 16-bit halves with periodic drains (PER) instead of the returning
-  // atomics of NARROW when int32 counters do not fit
-#ifdef GM_HIST_PER   // tuning build until measured: PER for observe whenever NARROW would run
-  const bool per = !UNOBS && vec && narrow;
-#else
-  const bool per = false;
-#endif
-  const int rows = (narrow || per) ? (int)((2 * (int64_t)HIST_LDS_MAX - 2) / (a.length + 2)) : rows32;
+  const int rows = narrow ? (int)((2 * (int64_t)HIST_LDS_MAX - 2) / (a.length + 2)) : rows32;
   const int passes = rows > 0 ? (a.n_bins + rows - 1) / rows : 1 << 30;
   if (passes <= HIST_MAX_PASSES) {
+    const bool vec = aligned16(x) && aligned16(y) && aligned16(t);
     int cus = 256;
     GM_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
     for (int k = 0; k < passes; ++k) {
       a.row_lo = k * rows;
       a.row_n = std::min(rows, a.n_bins - a.row_lo);
       a.tally = k == 0;
-      const int64_t cwords = (narrow || per) ? ((int64_t)a.row_n * a.length + 1) / 2 : (int64_t)a.row_n * a.length;
+      const int64_t cwords = narrow ? ((int64_t)a.row_n * a.length + 1) / 2 : (int64_t)a.row_n * a.length;
       const size_t lds = (size_t)(cwords + a.row_n + 2048) * sizeof(int);
       const int per_cu = lds <= 72 * 1024 ? 2 : 1;  // 2 x 1024 threads is the CU's wave limit
       // per workgroup <= 2^31 increments so the int32 LDS counters cannot wrap
@@ -386,16 +324,6 @@ int launch_hist(gm_ctx* ctx, const double* x, const double* y, const int64_t* t,
       };
       int rc;
       const bool top = a.top_s > 0;
-#ifdef GM_HIST_PER
-      if constexpr (!UNOBS) {
-        if (per) {
-          rc = top ? go(k_z3_hist_lds<PERIOD, false, true, false, true, true>)
-                   : go(k_z3_hist_lds<PERIOD, false, true, false, false, true>);
-          if (rc) return rc;
-          continue;
-        }
-      }
-#endif
       if (vec && top)
         rc = narrow ? go(k_z3_hist_lds<PERIOD, UNOBS, true, true, true>) : go(k_z3_hist_lds<PERIOD, UNOBS, true, false, true>);
       else if (vec)
