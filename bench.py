@@ -478,6 +478,30 @@ def gather_model(census, points, pairs, ms):
                       % (PROBE_STREAM_GBS, PROBE_L2_GPS, PROBE_FAR_GPS, PROBE_LINE_GPS))
 
 
+def scan_parity(dist, a, mask, n, check, stride_rows=2_000_000, max_matches=200_000):
+    """Oracle sample of a full-size filter scan (rank 0, untimed): the mask bit (bit r & 63 of word
+    r >> 6) of every stride-th row against the oracle's answer for those rows, plus the first
+    `max_matches` rows the GPU marked as matches (a strided sample sees few of the rare matches).
+    `check(rows)` maps a device int64 row tensor to the oracle's numpy bool answer."""
+    if dist.rank != 0 or a.no_cpu:
+        return None
+    import torch
+    stride = max(1, n // stride_rows)
+    rows = torch.arange(0, n, stride, device=mask.device, dtype=torch.int64)
+    got = (((mask[rows >> 6] >> (rows & 63)) & 1) != 0).cpu().numpy()
+    exp = np.asarray(check(rows), bool)
+    bit = torch.arange(64, device=mask.device, dtype=torch.int64)
+    nzw = torch.nonzero(mask[:(n + 63) // 64]).flatten()[:max_matches]
+    mb = ((mask[nzw].view(-1, 1) >> bit) & 1) != 0
+    mrows = (nzw.view(-1, 1) * 64 + bit)[mb]
+    mrows = mrows[mrows < n][:max_matches]
+    mexp = np.asarray(check(mrows), bool) if mrows.numel() else np.zeros(0, bool)
+    return {"rows": int(len(got)), "stride": stride, "sample_matches": int(exp.sum()),
+            "gpu_matches_checked": int(len(mexp)), "false_positives": int((~mexp).sum()),
+            "mismatches": int((got != exp).sum()) + int((~mexp).sum()),
+            "note": "oracle (C restatement) on every stride-th row and on the first GPU matches of the full-size run"}
+
+
 def gather_pairs(dist, ptids, plids, k):
     """Result gather of the join: per-rank pair counts, then every rank's
     (point id, polygon id) pairs to rank 0 over RCCL (shard.gather_rows), timed max over ranks.
@@ -503,12 +527,12 @@ def gather_pairs(dist, ptids, plids, k):
 
 
 def bench_table(a, dist, ctx, b, z):
-    import ctypes
     """configs[2]: a Z3 table range-sharded over the GPUs (2B rows over 8 GPUs = 250M per GPU).
     sort_keys: one gm_sort_keys of the rank's rows into table order.  table_ingest: the partitioned
     table built from the rank's rows (local sort, splitters, all-to-all by key range, slice sort).
     table_query: the configs[2] bbox + during query over the whole table -- ranges clipped to each
     slice, gm_key_range_scan (seek + Z3Filter), global ids gathered to rank 0."""
+    import ctypes
     import torch
     from geomesa_amd import _lib
     from geomesa_amd import filters as F
@@ -556,28 +580,47 @@ def bench_table(a, dist, ctx, b, z):
     # the same query as a full scan of every rank's own unsorted rows: bin in the query's bins AND
     # Z3Filter.inBounds (ranges() covers the query box and the filter passes epochs outside
     # [minEpoch, maxEpoch], Z3Filter.scala:45-62, Z3IndexKeySpace.scala:196-238), global ids gathered
-    # to rank 0 and compared as sets with the seek-and-filter result (untimed)
+    # to rank 0 and compared as sets with the seek-and-filter result (untimed).  The full scan is the
+    # oracle's (the C restatement, every row of the rank, chunked over the host threads); with --no-cpu
+    # it is the library's own gm_z3filter_scan instead
     ids, nm, _, _ = pt.scan(sr, fb)
     got = gather_rows(dist.pg, [ids])
     br = np.asarray(ks.bin_ranges(v), np.int16).reshape(-1)
-    fbuf = (ctypes.c_uint8 * len(fb)).from_buffer_copy(fb)
-    fmask = torch.empty((NT + 63) // 64, dtype=torch.int64, device=zs.device)
-    fn = ctypes.c_int64()
-    _lib.check(lib.gm_z3filter_scan(h, fbuf, len(fb), br.ctypes.data, len(br) // 2, P(bs), P(zs), NT, P(fmask),
-                                    None, 0, ctypes.byref(fn)), "gm_z3filter_scan")
-    fids = torch.empty(max(1, fn.value), dtype=torch.int64, device=zs.device)
-    _lib.check(lib.gm_z3filter_scan(h, fbuf, len(fb), br.ctypes.data, len(br) // 2, P(bs), P(zs), NT, P(fmask),
-                                    P(fids), fids.numel(), ctypes.byref(fn)), "gm_z3filter_scan")
-    full = gather_rows(dist.pg, [fids[:fn.value] + dist.rank * NT])
+    if not a.no_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle as O
+        from concurrent.futures import ThreadPoolExecutor
+        hb, hz = bs.cpu().numpy(), zs.cpu().numpy()
+        nt = cpu_threads()
+        step = (NT + nt - 1) // nt
+        with ThreadPoolExecutor(nt) as ex:   # ctypes drops the GIL inside the C call
+            parts = list(ex.map(lambda k: np.nonzero(O.z3filter_scan(fb, br, hb[k:k + step], hz[k:k + step]))[0] + k,
+                                range(0, NT, step)))
+        fids = torch.as_tensor(np.concatenate(parts).astype(np.int64), device=zs.device)
+        del hb, hz, parts
+        how = "the oracle's z3filter_scan (C restatement) over every rank's unsorted rows"
+    else:
+        fbuf = (ctypes.c_uint8 * len(fb)).from_buffer_copy(fb)
+        fmask = torch.empty((NT + 63) // 64, dtype=torch.int64, device=zs.device)
+        fn = ctypes.c_int64()
+        _lib.check(lib.gm_z3filter_scan(h, fbuf, len(fb), br.ctypes.data, len(br) // 2, P(bs), P(zs), NT, P(fmask),
+                                        None, 0, ctypes.byref(fn)), "gm_z3filter_scan")
+        fids = torch.empty(max(1, fn.value), dtype=torch.int64, device=zs.device)
+        _lib.check(lib.gm_z3filter_scan(h, fbuf, len(fb), br.ctypes.data, len(br) // 2, P(bs), P(zs), NT, P(fmask),
+                                        P(fids), fids.numel(), ctypes.byref(fn)), "gm_z3filter_scan")
+        fids = fids[:fn.value]
+        del fmask
+        how = "gm_z3filter_scan (bin ranges + Z3Filter.inBounds) over every rank's unsorted rows"
+    full = gather_rows(dist.pg, [fids + dist.rank * NT])
     qparity = None
     if dist.rank == 0:
         a_ids = np.sort(got[0].cpu().numpy()) if got is not None else np.zeros(0, np.int64)
         b_ids = np.sort(full[0].cpu().numpy()) if full is not None else np.zeros(0, np.int64)
         qparity = {"seek_ids": int(len(a_ids)), "full_scan_ids": int(len(b_ids)),
                    "ids_equal": bool(np.array_equal(a_ids, b_ids)),
-                   "note": "ids of the range seek + Z3Filter over the partitioned table against gm_z3filter_scan "
-                           "(bin ranges + Z3Filter.inBounds) over every rank's unsorted rows"}
-    del fmask, fids, got, full
+                   "mismatches": int(len(np.setxor1d(a_ids, b_ids))),
+                   "note": "ids of the range seek + Z3Filter over the partitioned table against " + how}
+    del fids, got, full
     del holder, pt
     return {
         "sort_keys": {"value": NT * dist.world / (ms_sort * 1e-3), "unit": "rows/s", "ms_per_step": ms_sort,
@@ -665,12 +708,16 @@ def bench_config0(a, dist, ctx, x, y, t, n0=10_000_000):
         gpu_r = [(int(r.lower), int(r.upper), bool(r.contained)) for rr in gpu_ir for r in rr]
         cpu_flat = [(int(r[0]), int(r[1]), bool(r[2])) for rr in cpu_r for r in rr]
         assert len(gpu_r) == len(res["r"])
+        # the timed path's own output (getRanges: (bin, lower) / (bin, upper) pairs) against the oracle too
+        cpu_bins = [(bn, int(r[0]), int(r[1])) for bn, rr in zip(sorted(tb), cpu_r) for r in rr]
+        timed_r = [(int(lo[0]), int(lo[1]), int(hi[1])) for kind, lo, hi in res["r"] if kind == "bounded"]
         out["cpu_baseline"] = {"index_ms": cpu_idx * 1e3, "index_points_per_s": n0 / cpu_idx, "ranges_ms": cpu_rng * 1e3,
                                "cores": 1, "kind": "port", "host": cpu_info(),
                                "sample": "the same %d points and the same query through the C restatement, 1 thread"
                                          % n0}
         out["parity"] = {"keys_equal": bool(np.array_equal(ob, b0.cpu().numpy()) and np.array_equal(oz, z0.cpu().numpy())),
-                         "ranges_equal": gpu_r == cpu_flat, "ranges": len(cpu_flat),
+                         "ranges_equal": gpu_r == cpu_flat, "timed_ranges_equal": timed_r == cpu_bins,
+                         "ranges": len(cpu_flat),
                          "contained": sum(r[2] for r in cpu_flat),
                          "note": "IndexRange (lower, upper, contained) of every bin's getRanges against the oracle "
                                  "(zorder/sfcurve/package.scala:22-76, ZN.scala:110-242)"}
@@ -814,12 +861,30 @@ def main():
         # columns): pinned host -> device copies of 24 B/point, the kernel, 10 B/point back; one
         # 64M-point batch in 8M-point chunks, copies of chunk k+1 overlapping the kernel of chunk k
         extra["z3_index_key_host_buffers"] = pcie_encode(dist, ctx, x, y, t, z)
+        def elem_parity(name, outs, check):
+            """every stride-th element of a full-size encode / decode leg against the oracle (rank 0, untimed)"""
+            if dist.rank != 0 or a.no_cpu:
+                return
+            stride = max(1, N // 2_000_000)
+            r = torch.arange(0, N, stride, device=dev, dtype=torch.int64)
+            exp = check(r)
+            bad = np.zeros(len(r), bool)
+            for o, e in zip(outs, exp):
+                g = o[r].cpu().numpy()
+                bad |= (g.view(np.int64) != np.asarray(e).view(np.int64)) if g.dtype == np.float64 else (g != e)
+            extra[name]["parity_sample"] = {"elements": int(len(r)), "stride": stride, "mismatches": int(bad.sum()),
+                                            "note": "oracle on every stride-th element (FP64 compared bit for bit)"}
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle as O   # the checker of the parity samples (untimed, rank 0)
         xi = torch.empty_like(x); yi = torch.empty_like(y); ti = torch.empty_like(t)
         rec("z3_invert", lambda: lib.gm_z3_invert(h, P(z), N, 1, 21, P(xi), P(yi), P(ti)), 32, N)
+        elem_parity("z3_invert", (xi, yi, ti), lambda r: O.z3_invert_batch(z[r].cpu().numpy()))
         del xi, yi, ti
         z2 = torch.empty_like(z)
         rec("z2_index", lambda: lib.gm_z2_index(h, P(x), P(y), N, 31, 0, P(z2), None, None), 24, N)
+        elem_parity("z2_index", (z2,), lambda r: O.z2_index_batch(x[r].cpu().numpy(), y[r].cpu().numpy())[:1])
         rec("z2_invert", lambda: lib.gm_z2_invert(h, P(z2), N, 31, P(x), P(y)), 24, N)
+        elem_parity("z2_invert", (x, y), lambda r: O.z2_invert_batch(z2[r].cpu().numpy()))
         del z2
         # the same encode from a geomesa-arrow-jts PointVector ([y, x] Float8 tuples) + date vector, read in place
         from geomesa_amd.arrow import GeomColumnC, TimeColumnC
@@ -852,6 +917,11 @@ def main():
         mask = torch.empty((N + 63) // 64, dtype=torch.int64, device=dev)
         rec("z3filter_scan", lambda: lib.gm_z3filter_scan(h, fbuf, len(fb), br.ctypes.data, len(br) // 2, P(b), P(z),
                                                          N, P(mask), None, 0, None), 10.125, N, unit="rows/s")
+        if dist.rank == 0 and not a.no_cpu:
+            sys.path.insert(0, os.path.join(ROOT, "oracle"))
+            import oracle as O
+        extra["z3filter_scan"]["parity_sample"] = scan_parity(
+            dist, a, mask, N, lambda r: O.z3filter_scan(fb, br, b[r].cpu().numpy(), z[r].cpu().numpy()))
         # strict columnar filter (SURVEY 8(d) "Filter scan, strict columnar", 24 B/point): GeoTools BBOX
         # (GeometryProcessing.scala:129) AND FastDuring (FastTemporalOperator.scala:123-126) on x / y / t
         bbq = (ctypes.c_double * 4)(-10.0, 35.0, 30.0, 60.0)
@@ -862,6 +932,9 @@ def main():
                                       ctypes.byref(nm)), "strict")
         extra["strict_scan"]["matches"] = nm.value
         extra["strict_scan"]["query"] = "bbox(-10,35,30,60) AND dtg DURING 2020-06-01T00:00Z/2020-06-08T12:00Z"
+        extra["strict_scan"]["parity_sample"] = scan_parity(
+            dist, a, mask, N, lambda r: O.strict_scan(x[r].cpu().numpy(), y[r].cpu().numpy(), t[r].cpu().numpy(),
+                                                      (-10.0, 35.0, 30.0, 60.0), (1590969600000, 1591617600000)))
         # fused full filter (north star: bbox + time window + point-in-polygon in one pass) over the
         # resident x/y/t columns: a 1,024-vertex query polygon with a hole around Europe, as
         # (a) INTERSECTS + BBOX + DURING (the Z3 query of the filter scan above) and (b) INTERSECTS alone
@@ -871,8 +944,15 @@ def main():
         qmask = torch.empty((N + 63) // 64, dtype=torch.int64, device=dev)
         rec("query_scan", lambda: lib.gm_query_scan(h, P(x), P(y), P(t), N, bbq, 1, 1590969600000, 1591617600000, qix._h,
                                                    1, P(qmask), None, 0, None), 24.125, N, unit="rows/s")
+        qoracle = O.OraclePolySet(*qpoly.to_arrays()) if dist.rank == 0 and not a.no_cpu else None
+        extra["query_scan"]["parity_sample"] = scan_parity(
+            dist, a, qmask, N, lambda r: O.query_scan(x[r].cpu().numpy(), y[r].cpu().numpy(), t[r].cpu().numpy(),
+                                                      (-10.0, 35.0, 30.0, 60.0), (1590969600000, 1591617600000),
+                                                      polys=qoracle, op=1))
         rec("query_scan_polygon", lambda: lib.gm_query_scan(h, P(x), P(y), None, N, None, 0, 0, 0, qix._h, 1, P(qmask),
                                                            None, 0, None), 16.125, N, unit="rows/s")
+        extra["query_scan_polygon"]["parity_sample"] = scan_parity(
+            dist, a, qmask, N, lambda r: O.query_scan(x[r].cpu().numpy(), y[r].cpu().numpy(), polys=qoracle, op=1))
         nm = ctypes.c_int64()
         _lib.check(lib.gm_query_scan(h, P(x), P(y), None, N, None, 0, 0, 0, qix._h, 1, P(qmask), None, 0,
                                      ctypes.byref(nm)), "query")

@@ -12,7 +12,7 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fn
          "-Wall", "-Wno-unused-function"]
 
 
-VARIANT_ONLY = ("GM_JX_", "GM_NO_REF_CHECKS", "GM_SC8_NOINLINE", "GM_SC8_NOLINE2")
+VARIANT_ONLY = ("GM_JX_", "GM_NO_REF_CHECKS")
 
 
 def sources():

@@ -202,11 +202,18 @@ int take_fault(gm_ctx* c, const char* what) {
   GM_HIP(hipMemcpyAsync(c->h_pinned + 63, c->d_scratch + SCRATCH_FAULT, 8, hipMemcpyDeviceToHost, c->stream));
   GM_HIP(hipStreamSynchronize(c->stream));
   bits = c->h_pinned[63];
+  const uint32_t calls = c->fault_calls;
+  c->fault_calls = 0;
   if (!bits) return GM_OK;
   GM_HIP(hipMemsetAsync(c->d_scratch + SCRATCH_FAULT, 0, 8, c->stream));
-  char msg[200];
+  std::string src;
+  const char* names[4] = {"gm_pip_join", "gm_pip_join_arrow", "gm_pip_relate", "gm_query_scan"};
+  for (int k = 0; k < 4; ++k)
+    if (calls & (1u << k)) src += std::string(src.empty() ? "" : ", ") + names[k];
+  char msg[400];
   snprintf(msg, sizeof msg, "%s: device reference check failed (PIP_FAULT bits 0x%x): corrupt index or internal "
-           "queue invariant", what, (unsigned)bits);
+           "queue invariant; raised by a kernel of one of the calls on this context since the last check "
+           "(stream-ordered calls report here): %s", what, (unsigned)bits, src.empty() ? "unknown" : src.c_str());
   set_error(msg);
   return GM_E_INDEX;
 }

@@ -21,13 +21,10 @@ __global__ __launch_bounds__(TPB) void k_z3_index_key(const dv2* __restrict__ x,
                                                       short2* __restrict__ bin, lv2* __restrict__ z,
                                                       uchar2* __restrict__ status, NDim lon, NDim lat, NDim tim,
                                                       int64_t* __restrict__ err) {
-#ifdef GM_KEY_TABLE
-  __shared__ uint32_t sp[2048];
-#endif
-#ifndef GM_BIN_REG   // bins leave as one 16-B store per lane (the block's 2048 bins staged in LDS):
-                     // 3.5% faster than a 4-B store per pair (A/B on one box, tools/key_ab2.sh)
+  // bins leave as one 16-B store per lane (the block's 2048 bins staged in LDS): 3.5% faster than a
+  // 4-B store per pair (A/B on one box, round 2)
   __shared__ uint32_t s_bin[TPB * UNROLL];
-#endif
+  static_assert(UNROLL == 4, "staged bins: 4 pairs per lane");
   const int64_t npairs = n >> 1;
   const int64_t base = (int64_t)blockIdx.x * (TPB * UNROLL) + threadIdx.x;
   dv2 xv[UNROLL], yv[UNROLL];
@@ -41,38 +38,22 @@ __global__ __launch_bounds__(TPB) void k_z3_index_key(const dv2* __restrict__ x,
       tv[u] = ld_stream(&t[p]);
     }
   }
-#ifdef GM_KEY_TABLE
-  fill_spread_table(sp, threadIdx.x, TPB);  // while the loads are in flight
-  __syncthreads();
-#endif
 #pragma unroll
   for (int u = 0; u < UNROLL; ++u) {
     const int64_t p = base + (int64_t)u * TPB;
     if (p < npairs) {
       int16_t b0, b1;
       int64_t z0, z1;
-#ifndef GM_KEY_TABLE  // default: magic-number spreads in registers (A/B with the LDS table: within noise, tools/key_ab.sh)
       uint8_t s0 = z3_key_one<PERIOD, LENIENT>(xv[u].x, yv[u].x, tv[u].x, lon, lat, tim, b0, z0);
       uint8_t s1 = z3_key_one<PERIOD, LENIENT>(xv[u].y, yv[u].y, tv[u].y, lon, lat, tim, b1, z1);
-#else
-      uint8_t s0 = z3_key_one_tab<PERIOD, LENIENT>(xv[u].x, yv[u].x, tv[u].x, lon, lat, tim, sp, b0, z0);
-      uint8_t s1 = z3_key_one_tab<PERIOD, LENIENT>(xv[u].y, yv[u].y, tv[u].y, lon, lat, tim, sp, b1, z1);
-#endif
       st_stream(lv2{z0, z1}, &z[p]);
-#if !defined(GM_BIN_REG)
       s_bin[u * TPB + threadIdx.x] = bin_pair(b0, b1);
-#else
-      bin[p] = make_short2(b0, b1);
-#endif
       if (STATUS) status[p] = make_uchar2(s0, s1);
       if (s0) report_error(err, 2 * p, s0);
       if (s1) report_error(err, 2 * p + 1, s1);
     }
   }
-#ifndef GM_BIN_REG
-  static_assert(UNROLL == 4, "staged bins: 4 pairs per lane");
   store_staged_bins<TPB>(s_bin, bin, npairs);
-#endif
   if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
     const int64_t i = n - 1;
     int16_t b;

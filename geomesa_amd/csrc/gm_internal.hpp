@@ -28,6 +28,8 @@ struct gm_ctx {
   int64_t sort_mode = 0;           // GM_PARAM_SORT_MODE: 0 = auto (prefix passes + local ranks), 1 = digit passes only
   int64_t index_coarse = -1;       // GM_PARAM_INDEX_COARSE: the join's coarse sub-block masks (-1 = automatic)
   int64_t index_core = 1;          // GM_PARAM_INDEX_CORE: the row predicate's core rectangles (1 = built)
+  uint32_t fault_calls = 0;        // FC_* bits: the entry points that enqueued reference-checked kernels
+                                   // since the fault word was last read (take_fault names them)
   hipStream_t copy_stream = nullptr;   // result copies overlapping the next chunk's kernels (lazy)
   hipEvent_t ev_ready[2] = {nullptr, nullptr}, ev_copied[2] = {nullptr, nullptr};
 };
@@ -72,7 +74,12 @@ int ctx_copy_stream(gm_ctx* ctx);   // creates copy_stream and its events on fir
 // The context's sticky reference-fault word (d_scratch[SCRATCH_FAULT]): the polygon-index kernels OR
 // PIP_FAULT_* bits into it, stream-ordered; take_fault (a synchronising call: a join that returns its
 // pair count, a query scan, gm_ctx_sync) reads and clears it and returns GM_E_INDEX when set.
+// A stream-ordered call (gm_pip_relate, a join without n_pairs) leaves its bits for a later
+// synchronising call, so each call that enqueues checked kernels records itself (note_fault_call) and
+// the error text names every such call since the last read, not only the call that read the word.
 constexpr int SCRATCH_FAULT = 63;
+enum : uint32_t { FC_JOIN = 1, FC_JOIN_ARROW = 2, FC_RELATE = 4, FC_QUERY = 8 };
+inline void note_fault_call(gm_ctx* ctx, uint32_t fc) { ctx->fault_calls |= fc; }
 int take_fault(gm_ctx* ctx, const char* what);
 
 // reset the error summary before a call that reports one

@@ -7,24 +7,14 @@
 
 namespace gm {
 
-#ifndef GM_NT
-#define GM_NT 1
-#endif
+// every column kernel streams: non-temporal loads and stores (the data is touched once)
 template <class T>
 __device__ __forceinline__ T ld_stream(const T* p) {
-#if GM_NT
   return __builtin_nontemporal_load(p);
-#else
-  return *p;
-#endif
 }
 template <class T>
 __device__ __forceinline__ void st_stream(T v, T* p) {
-#if GM_NT
   __builtin_nontemporal_store(v, p);
-#else
-  *p = v;
-#endif
 }
 
 // Bins of a key kernel's block leave as one 16-B store per lane: pair j of the block (pairs
@@ -80,7 +70,7 @@ __device__ __forceinline__ uint8_t z3_key_one(double x, double y, int64_t ms, co
 }
 
 // Z3.split through an LDS table of spread3_11 (2048 entries): two lookups per dimension replace the
-// two 8-op magic-number spreads; the Z3 encode kernels are VALU-bound, the LDS pipe is idle
+// two 8-op magic-number spreads (the Z3Histogram kernels, gm_stats.hip)
 __device__ __forceinline__ uint64_t z3_split_tab(int32_t value, const uint32_t* sp) {
   const uint32_t v = (uint32_t)value & 0x1fffffu;
   return ((uint64_t)sp[v >> 11] << 33) | (uint64_t)sp[v & 0x7ffu];
@@ -88,31 +78,6 @@ __device__ __forceinline__ uint64_t z3_split_tab(int32_t value, const uint32_t* 
 __device__ __forceinline__ void fill_spread_table(uint32_t* sp, int tid, int nthreads) {
   for (int i = tid; i < 2048; i += nthreads) sp[i] = spread3_11((uint32_t)i);
 }
-// z3_key_one with the table spread (identical results: same bounds, clamps and normalize)
-template <int PERIOD, bool LENIENT>
-__device__ __forceinline__ uint8_t z3_key_one_tab(double x, double y, int64_t ms, const NDim& lon, const NDim& lat,
-                                                  const NDim& tim, const uint32_t* sp, int16_t& bin, int64_t& z) {
-  int64_t off;
-  uint8_t st = binned_time<PERIOD>(ms, bin, off);
-  if (st == ST_OK) {
-    double td = (double)off;
-    const bool inb = x >= lon.min && x <= lon.max && y >= lat.min && y <= lat.max && td >= tim.min && td <= tim.max;
-    if (!inb && !LENIENT) {
-      st = ST_OUT_OF_BOUNDS;
-    } else {
-      if (!inb) {
-        x = x < lon.min ? lon.min : (x > lon.max ? lon.max : x);
-        y = y < lat.min ? lat.min : (y > lat.max ? lat.max : y);
-        td = td < tim.min ? tim.min : (td > tim.max ? tim.max : td);
-      }
-      z = (int64_t)(z3_split_tab(normalize(lon, x), sp) | (z3_split_tab(normalize(lat, y), sp) << 1) |
-                    (z3_split_tab(normalize(tim, td), sp) << 2));
-    }
-  }
-  if (st != ST_OK) { bin = 0; z = 0; }
-  return st;
-}
-
 template <bool LENIENT>
 __device__ __forceinline__ uint8_t z2_index_one(double x, double y, const NDim& lon, const NDim& lat,
                                                 int64_t& z) {

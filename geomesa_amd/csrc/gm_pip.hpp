@@ -94,7 +94,11 @@ __device__ __forceinline__ void pip_fault(const PipDev& d, uint32_t code) {
   if (d.fault) atomicOr(d.fault, code);
 }
 // a reference / queue check; GM_NO_REF_CHECKS (timing variant only) compiles every check out to price
-// them
+// them.  The shipped library (GM_PRODUCT_BUILD, geomesa_amd/build.py) refuses it at compile time too, so
+// no build path can ship without the device reference checks.
+#if defined(GM_PRODUCT_BUILD) && defined(GM_NO_REF_CHECKS)
+#error "GM_NO_REF_CHECKS is a timing variant: it cannot be built into the shipped library"
+#endif
 #ifdef GM_NO_REF_CHECKS
 #define GM_REF_BAD(c) (false)
 #else

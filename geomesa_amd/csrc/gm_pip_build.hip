@@ -897,12 +897,7 @@ __global__ __launch_bounds__(256) void k_build_sc8(const uint32_t* __restrict__ 
   for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < ncell; c += (int64_t)gridDim.x * blockDim.x) {
     const uint32_t w = cell_sc[c];
     uint2 o = make_uint2(w, 0u);
-#ifdef GM_SC8_NOINLINE   // tuning build: every fine word without its inline lines (A/B of the inline lines)
-    if (false &&
-#else
-    if (
-#endif
-        line_ent && (w >> 30) == CELL_BOUNDARY && (w & (BLOB_COMPACT | SC_LINE)) == (BLOB_COMPACT | SC_LINE) &&
+    if (line_ent && (w >> 30) == CELL_BOUNDARY && (w & (BLOB_COMPACT | SC_LINE)) == (BLOB_COMPACT | SC_LINE) &&
         (uint64_t)(w & (SC_LINE - 1)) < (uint64_t)n_line) {
       const uint64_t li = w & (SC_LINE - 1);
       const uint4 e0 = line_ent[2 * li], e1 = line_ent[2 * li + 1];
@@ -923,7 +918,6 @@ __global__ __launch_bounds__(256) void k_build_sc8(const uint32_t* __restrict__ 
           o = make_uint2((uint32_t)v, (uint32_t)(v >> 32));
         }
       }
-#ifndef GM_SC8_NOLINE2   // tuning build: one-line words only (A/B of the two-line words)
       else if (nl == 2u && e0.y < (1u << 14)) {
         const double A1 = (double)(int16_t)(e0.z & 0xffffu), B1 = (double)(int16_t)(e0.z >> 16);
         const double C1 = (double)((int32_t)(e0.w << 8) >> 8);
@@ -947,7 +941,6 @@ __global__ __launch_bounds__(256) void k_build_sc8(const uint32_t* __restrict__ 
           }
         }
       }
-#endif
     }
     out[c] = o;
   }

@@ -633,6 +633,7 @@ int gm_pip_join_pred(gm_ctx* ctx, const gm_pip_index* ix, const double* px, cons
   dv.op = predicate == GM_SPATIAL_INTERSECTS ? JOIN_INTERSECTS : JOIN_CONTAINS;
   unsigned long long* counter = (unsigned long long*)ctx->d_scratch;
   dv.fault = (uint32_t*)(ctx->d_scratch + SCRATCH_FAULT);   // sticky reference-check bits (PIP_FAULT_*)
+  note_fault_call(ctx, FC_JOIN);
   GM_HIP(hipMemsetAsync(counter, 0, 8, ctx->stream));
   if (n > 0) {
     // chunks start at even rows, so 16-B aligned columns stay aligned in every chunk
@@ -658,6 +659,7 @@ int gm_pip_join_arrow(gm_ctx* ctx, const gm_pip_index* ix, const gm_geom_column*
   dv.op = predicate == GM_SPATIAL_INTERSECTS ? JOIN_INTERSECTS : JOIN_CONTAINS;
   unsigned long long* counter = (unsigned long long*)ctx->d_scratch;
   dv.fault = (uint32_t*)(ctx->d_scratch + SCRATCH_FAULT);
+  note_fault_call(ctx, FC_JOIN_ARROW);
   GM_HIP(hipMemsetAsync(counter, 0, 8, ctx->stream));
   if (n > 0) {   // the tuples are read in place (16 B per Float8 tuple, 8 B per Float4 tuple)
     const int rc = ap.f32 ? join_staged<2, false>(ctx, nullptr, nullptr, ap, 8, n, id_base, dv, pt_ids, poly_ids, cap, counter)

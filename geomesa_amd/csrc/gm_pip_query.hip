@@ -189,7 +189,10 @@ int gm_query_scan(gm_ctx* ctx, const double* x, const double* y, const int64_t* 
   const double nobb[4] = {0.0, 0.0, 0.0, 0.0};
   const double* bb = bbox ? bbox : nobb;
   PipDev d = spatial_op != GM_SPATIAL_NONE ? geoms->dev : PipDev{};
-  if (spatial_op != GM_SPATIAL_NONE) d.fault = (uint32_t*)(ctx->d_scratch + SCRATCH_FAULT);   // sticky reference checks
+  if (spatial_op != GM_SPATIAL_NONE) {   // sticky reference checks
+    d.fault = (uint32_t*)(ctx->d_scratch + SCRATCH_FAULT);
+    note_fault_call(ctx, FC_QUERY);
+  }
   const unsigned grid = (unsigned)((n + FROWS - 1) / FROWS);
   const bool vec = aligned16(x) && aligned16(y) && (!has_during || aligned16(t_ms));
   if (vec) {

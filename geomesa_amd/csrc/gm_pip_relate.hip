@@ -220,6 +220,7 @@ int gm_pip_relate(gm_ctx* ctx, const gm_pip_index* ix, const int32_t* poly, cons
                                                                           (n + RTPB * RILP - 1) / (RTPB * RILP)));
   PipDev dv = ix->dev;
   dv.fault = (uint32_t*)(ctx->d_scratch + SCRATCH_FAULT);   // sticky reference checks, as the join's
+  note_fault_call(ctx, FC_RELATE);
   hipLaunchKernelGGL(kern, dim3(grid), dim3(RTPB), 0, ctx->stream, poly, px, py, n, ix->n_polys, dv, ix->list_poly, loc);
   GM_CHECK_LAUNCH();
   return GM_OK;

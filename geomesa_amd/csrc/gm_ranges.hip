@@ -42,11 +42,7 @@ constexpr int MAXB = 256;       // zbounds / windows per query
 #define GM_LDS_SORT 4096
 #endif
 constexpr int LDS_SORT = GM_LDS_SORT;  // ranges sorted in LDS; larger lists sort in global memory
-#ifdef GM_RANGES_MINW   // tuning: minimum waves per SIMD for the XZ walk (caps its VGPRs)
-#define GM_XZ_BOUNDS __launch_bounds__(RTPB, GM_RANGES_MINW)
-#else
 #define GM_XZ_BOUNDS __launch_bounds__(RTPB)
-#endif
 
 enum : int32_t { QS_OK = 0, QS_OUT_OF_BOUNDS = 1, QS_UNORDERED = 3, QS_CAPACITY = 4, QS_TOO_MANY_BOUNDS = 5 };
 
@@ -1251,9 +1247,15 @@ static int xz_ranges(gm_ctx* ctx, int D, int64_t nq, const int32_t* win_off, con
     fcap = (int64_t)max_ranges + 2;
     rcap = (int64_t)max_ranges + (1 << D) + 16;
   } else {
-    fcap = std::max<int64_t>(cap, 1 << 16);
+    // unbounded (maxRanges <= 0): the frontier is not bounded by a budget, so the worst-case caps are
+    // capped instead (~320 B per frontier slot per query for XZ3) -- a query past them reports
+    // QS_CAPACITY in its status -- and kept inside the kernel's packed fields: parent ids in 30 bits of
+    // an element word, element / range counts in int32
+    fcap = std::min<int64_t>(std::max<int64_t>(cap, 1 << 16), (int64_t)1 << 24);
     rcap = (int64_t)fcap << (D + 1);
   }
+  if (fcap >= ((int64_t)1 << 30) || (fcap << D) >= ((int64_t)1 << 31) || rcap >= ((int64_t)1 << 31))
+    return hip_fail(hipErrorInvalidValue, "xz ranges: workspace caps past the kernel's packed fields");
   rc = run_ranges(ctx, nq, fcap, rcap, [D](int64_t fc, int64_t rcp) { return xz_ws(D, fc, rcp).stride; },
                   [&](int64_t q0, int64_t m, int64_t fc, int64_t rcp, char* base, const BatchOut& bo) {
                     XZWaveArgs b = a;

@@ -413,14 +413,15 @@ __global__ __launch_bounds__(PT) void k_sort_pass(PassArgs a) {
 #endif
 constexpr int LT = GM_SORT_LT, LCAP = GM_SORT_LCAP, LPT = LCAP / LT, RUN_MAX = 256, LSTEP = LCAP - RUN_MAX;
 
-// the prefix digits of width w (offsets o.x > o.y > ...; an offset < 0: no digit): at most 32 bits
-// (npre * pw <= 32 for n < 2^32, see gm_sort_keys)
+// the prefix digits of width w (offsets o.x > o.y > ...; an offset < 0: no digit, and every later
+// offset is < 0 too): npre * w <= 32 bits (gm_sort_keys), so the digits that exist are shifted in and
+// the absent ones are not -- a shift per absent digit would push the first digit's top bits out of the
+// word and merge distinct prefixes into one run
 __device__ __forceinline__ uint32_t prefix4(uint32_t bs, uint64_t z, int4 o, int w) {
-  uint32_t p = 0;
-  p = (p << w) | (o.x >= 0 ? key_digit_w(bs, z, o.x, w) : 0u);
-  p = (p << w) | (o.y >= 0 ? key_digit_w(bs, z, o.y, w) : 0u);
-  p = (p << w) | (o.z >= 0 ? key_digit_w(bs, z, o.z, w) : 0u);
-  p = (p << w) | (o.w >= 0 ? key_digit_w(bs, z, o.w, w) : 0u);
+  uint32_t p = o.x >= 0 ? key_digit_w(bs, z, o.x, w) : 0u;
+  if (o.y >= 0) p = (p << w) | key_digit_w(bs, z, o.y, w);
+  if (o.z >= 0) p = (p << w) | key_digit_w(bs, z, o.z, w);
+  if (o.w >= 0) p = (p << w) | key_digit_w(bs, z, o.w, w);
   return p;
 }
 

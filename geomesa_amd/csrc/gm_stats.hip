@@ -293,11 +293,7 @@ int launch_hist(gm_ctx* ctx, const double* x, const double* y, const int64_t* t,
   // passes lose to the device-atomic kernel (measured: 2 LDS passes ~12 ms vs 45 ms atomics per 1B)
   // 32-bit LDS counters when every time-bin row fits one pass, else 16-bit halves (NARROW)
   const int rows32 = (HIST_LDS_MAX) / (a.length + 1);
-#ifdef GM_HIST_FORCE_NARROW   // timing experiment: 16-bit counters (half the LDS) even when 32-bit fit
-  const bool narrow = true;
-#else
   const bool narrow = rows32 < a.n_bins;
-#endif
   const int rows = narrow ? (int)((2 * (int64_t)HIST_LDS_MAX - 2) / (a.length + 2)) : rows32;
   const int passes = rows > 0 ? (a.n_bins + rows - 1) / rows : 1 << 30;
   if (passes <= HIST_MAX_PASSES) {

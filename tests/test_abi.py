@@ -55,7 +55,7 @@ def test_product_build_refuses_timing_hooks():
     compile runs, and no product source carries a GM_JX_ hook."""
     import pytest
     from geomesa_amd import build as B
-    for d in ("GM_JX_NOBLOB", "GM_NO_REF_CHECKS", "GM_SC8_NOINLINE", "GM_SC8_NOLINE2"):
+    for d in ("GM_JX_NOBLOB", "GM_NO_REF_CHECKS"):
         with pytest.raises(ValueError):
             B.build(defines=(d,), verbose=False)
     for src in B.sources():

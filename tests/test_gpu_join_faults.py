@@ -157,7 +157,17 @@ def test_corrupt_reference_reports_instead_of_faulting(gpu):
     with pytest.raises(_lib.GeomesaHipError) as ei:
         bad.ctx.sync()
     assert "reference check" in str(ei.value)
+    assert "gm_pip_join" in str(ei.value) and "gm_pip_relate" not in str(ei.value)   # names the call that raised it
     bad.ctx.sync()   # cleared once reported
+    # a stream-ordered row predicate on the bad index, read by a later synchronising join on the
+    # healthy one: the text names the row predicate as a possible source
+    rid = torch.zeros(len(px), dtype=torch.int32, device="cuda")
+    loc = torch.empty(len(px), dtype=torch.uint8, device="cuda")
+    assert bad.ctx.lib.gm_pip_relate(bad.ctx.handle, bad._h, ctypes.c_void_p(rid.data_ptr()), ctypes.c_void_p(x.data_ptr()),
+                                     ctypes.c_void_p(y.data_ptr()), len(px), ctypes.c_void_p(loc.data_ptr())) == _lib.GM_OK
+    with pytest.raises(_lib.GeomesaHipError) as ei:
+        bad.ctx.sync()
+    assert "gm_pip_relate" in str(ei.value)
     # the healthy index on the same context is unaffected
     pt, pl = good.join(px, py)
     pt2, pl2 = PolygonIndex.from_arrays(*good.export_arrays(), polyset=ps).join(px, py)

@@ -135,6 +135,30 @@ def test_sort_keys_prefix_path_at_bench_size(gpu, kind):
     _check_table_order_on_device(b, z, ob, oz, op)
 
 
+def test_sort_keys_prefix_keeps_first_digit_top_bits(gpu):
+    """n in (2^25, 2^28]: three 9-bit prefix digits.  The only varying bits of the first digit are its
+    top four (z bits 59-62); the other two digits see 16 varying bits (z bits 16-31), so a prefix that
+    dropped the first digit's top bits would merge 16 runs into one of ~512 rows, past RUN_MAX, and send
+    the sort down the every-byte fallback.  The prefix keeps them: the local-rank path runs."""
+    import torch
+    from geomesa_amd import _lib
+    n = (1 << 25) + 4096
+    g = torch.Generator(device="cuda").manual_seed(5)
+    top = torch.randint(0, 16, (n,), device="cuda", generator=g, dtype=torch.int64) << 59
+    mid = torch.randint(0, 1 << 16, (n,), device="cuda", generator=g, dtype=torch.int64) << 16
+    low = torch.randint(0, 2, (n,), device="cuda", generator=g, dtype=torch.int64)
+    z = top | mid | low
+    b = torch.full((n,), 2610, dtype=torch.int16, device="cuda")
+    del top, mid, low
+    ob, oz = torch.empty_like(b), torch.empty_like(z)
+    op = torch.empty(n, dtype=torch.int64, device="cuda")
+    ctx = _lib.context()
+    _lib.check(ctx.lib.gm_sort_keys(ctx.handle, None, _lib.ptr(b), _lib.ptr(z), n, None, _lib.ptr(ob), _lib.ptr(oz),
+                                    _lib.ptr(op)), "sort")
+    assert ctx.get_param(_lib.GM_PARAM_SORT_LAST) == 256 + 3
+    _check_table_order_on_device(b, z, ob, oz, op)
+
+
 @pytest.mark.parametrize("where", ["bin", "shard", "z"])
 @pytest.mark.parametrize("mode", [0, 1])
 def test_sort_keys_sample_misses_a_varying_bit(gpu, where, mode):
