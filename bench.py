@@ -93,6 +93,25 @@ class Dist:
         return all_reduce_scalar(self.pg, v, "sum")
 
 
+def box_copy_gbs(dist, src):
+    """HBM rate (read + write bytes / time) of a 4 GB device-to-device copy (torch copy_, the best of
+    5) on this rank's GPU, the slowest rank's: the box's own streaming ceiling."""
+    import torch
+    n = min(src.numel() * src.element_size(), 4 << 30)
+    a = src.view(torch.uint8)[:n]
+    b = torch.empty(n, dtype=torch.uint8, device=src.device)
+    best = None
+    for _ in range(5):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        b.copy_(a)
+        e.record()
+        torch.cuda.synchronize()
+        best = s.elapsed_time(e) if best is None else min(best, s.elapsed_time(e))
+    del b
+    return all_reduce_scalar(dist.pg, 2.0 * n / (best * 1e-3) / 1e9, "min")
+
+
 def timed(dist, fn, steps, warmup):
     """Barrier + sync on both sides; HIP events on the stream the kernels run on; max over ranks."""
     import torch
@@ -502,15 +521,25 @@ def scan_parity(dist, a, mask, n, check, stride_rows=2_000_000, max_matches=200_
             "note": "oracle (C restatement) on every stride-th row and on the first GPU matches of the full-size run"}
 
 
-def gather_pairs(dist, ptids, plids, k):
-    """Result gather of the join: per-rank pair counts, then every rank's
-    (point id, polygon id) pairs to rank 0 over RCCL (shard.gather_rows), timed max over ranks.
-    Reported, never part of the join's ms_per_step.  A failure is reported, not raised, so the
-    scaling line survives it."""
+def gather_pairs(dist, ptids, plids, k, id_base, n_polys):
+    """Result gather of the join, reported beside the sharded result the step leaves
+    (the reference's join leaves its pairs in the RDD's partitions, GeoMesaJoinRelation.scala:41-91;
+    ms_per_step is that placement).  Two wire formats to rank 0 over RCCL point-to-point: the full
+    12-B pairs (shard.gather_rows) and the compact 6-B form (4-B shard-local row + 2-B polygon,
+    shard.gather_pairs_compact, expanded on rank 0).  Each: measured ms (max over ranks), bytes on the
+    wire, and the model estimate (largest peer's bytes over one ~153 GB/s xGMI link, or rank 0's HBM
+    writes).  Never part of ms_per_step.  A failure is reported, not raised, so the scaling line
+    survives it."""
     import torch
-    from geomesa_amd.shard import gather_rows
+    from geomesa_amd.shard import gather_estimate_ms, gather_pairs_compact, gather_rows
+    full_b = [12 * int(v) for v in all_gather_ints(dist, k)]
+    comp_b = [(6 if n_polys <= 65536 else 12) * v // 12 for v in full_b]
+    out = {"placement": "ms_per_step leaves the pairs sharded on their ranks (the reference's RDD partitions)",
+           "est_ms_full": round(gather_estimate_ms(full_b), 3), "est_ms_compact": round(gather_estimate_ms(comp_b), 3),
+           "bytes_full": sum(full_b[1:]), "bytes_compact": sum(comp_b[1:])}
     if dist.pg is None:   # one rank: the pairs already sit on rank 0, nothing moves
-        return {"noop": True, "ms": 0.0, "bytes": 0, "pairs_on_rank0": int(k)}
+        out.update(noop=True, ms=0.0, bytes=0, pairs_on_rank0=int(k))
+        return out
     try:
         dist.barrier()
         t0 = time.time()
@@ -520,10 +549,22 @@ def gather_pairs(dist, ptids, plids, k):
         n = int(g[0].numel()) if g is not None else 0
         del g
         torch.cuda.empty_cache()
-        return {"ms": ms, "pairs_on_rank0": n if dist.rank == 0 else None, "bytes": 12 * n,
-                "how": "all_gather of counts, then batched point-to-point receives of exact sizes into rank 0's output slices (RCCL send/recv over xGMI)"}
+        dist.barrier()
+        t0 = time.time()
+        gc, _ = gather_pairs_compact(dist.pg, ptids[:k], plids[:k], id_base, n_polys)
+        torch.cuda.synchronize()
+        msc = dist.max((time.time() - t0) * 1e3)
+        nc = int(gc[0].numel()) if gc is not None else 0
+        del gc
+        torch.cuda.empty_cache()
+        out.update(ms=ms, pairs_on_rank0=n if dist.rank == 0 else None, bytes=sum(full_b[1:]),
+                   ms_compact=msc, pairs_on_rank0_compact=nc if dist.rank == 0 else None,
+                   how="all_gather of counts, then batched point-to-point receives of exact sizes into rank 0's "
+                       "output slices (RCCL send/recv over xGMI); compact: 6 B per pair on the wire, expanded on rank 0")
+        return out
     except Exception as e:  # noqa: BLE001 -- reported in the JSON line
-        return {"error": repr(e)[:200]}
+        out["error"] = repr(e)[:200]
+        return out
 
 
 def bench_table(a, dist, ctx, b, z):
@@ -626,7 +667,11 @@ def bench_table(a, dist, ctx, b, z):
         "sort_keys": {"value": NT * dist.world / (ms_sort * 1e-3), "unit": "rows/s", "ms_per_step": ms_sort,
                       "rows_per_gpu": NT, "digit_passes": npass, "path": spath,
                       "roofline": dict(roofline(sbytes, ms_sort), bytes_per_unit=round(sbytes / NT, 2),
-                                       kernel="gm_sort_keys (all launches of one sort)"),
+                                       kernel="gm_sort_keys (all launches of one sort)",
+                                       # against the compulsory bytes alone: the key columns read once
+                                       # (bin 2 + z 8) and the sorted columns + 8-B permutation written once
+                                       frac_compulsory=round(28.0 * NT / (ms_sort * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                                       compulsory_bytes_per_unit=28),
                       "note": "stable sort of (bin, z) into table byte order (ingest side): one-sweep digit passes "
                               "(look-back, 16-B records) over the top ~log2(n) - 1 varying key bits, then every run of "
                               "equal prefixes ranked by full key in LDS (8-bit digit passes over every varying byte when "
@@ -764,7 +809,7 @@ def compact(out):
     c = {k: out[k] for k in keep if k in out}
     if "roofline" in out:
         c["roofline"] = {k: _r(out["roofline"].get(k)) for k in ("bound", "achieved", "peak", "unit", "frac", "traffic",
-                                                                 "kernel")}
+                                                                 "kernel", "box_copy_gbs", "frac_of_box_copy")}
     cb = out.get("cpu_baseline")
     if cb:
         c["cpu_baseline"] = {"value": _r(cb["value"], 1), "unit": cb["unit"], "cores": cb["cores"], "kind": cb["kind"],
@@ -843,6 +888,13 @@ def main():
         out["roofline"] = roofline(34.0 * N, ms, load_pmc("z3_index_key", N))
         out["roofline"]["bytes_per_unit"] = 34
         out["roofline"]["kernel"] = "k_z3_index_key<WEEK,false,false,4>"
+        # this box's own streaming ceiling beside the spec peak: the HBM rate of a device-to-device copy
+        # of the same 34 GB shape (HBM rates differ between boxes by up to ~15%), so the fraction can be
+        # compared across captures
+        cp = box_copy_gbs(dist, z)
+        out["roofline"]["box_copy_gbs"] = round(cp, 1)
+        out["roofline"]["frac_of_box_copy"] = round(out["roofline"]["achieved"] / cp, 4)
+        out["roofline"]["box_copy_note"] = "4 GB device-to-device copy, best of 5, read + write bytes / time"
     out["config"] = {"workload": "configs[1]: Z3IndexKeySpace.toIndexKey batch (BinnedTime + Z3SFC(week).index), "
                                  "%d resident points per GPU" % N,
                      "points_per_gpu": N, "period": "week", "parallelism": "point shards, no collective"}
@@ -1166,7 +1218,7 @@ def main():
         del px, py
         torch.cuda.empty_cache()
         if not a.no_gather:
-            pj["gather"] = gather_pairs(dist, ptids, plids, int(npairs.value))
+            pj["gather"] = gather_pairs(dist, ptids, plids, int(npairs.value), jlo, n_polys)
         if dist.rank == 0 and not a.no_cpu:
             pj["cpu_baseline"] = cpu_join_baseline(a.cpu_seconds, ps, join_sample)
         out["pip_join"] = pj

@@ -32,7 +32,7 @@ GM_PARAM_RANGES_CHUNK = 3
 GM_PARAM_SORT_MODE = 4
 GM_PARAM_SORT_LAST = 5
 GM_PARAM_INDEX_COARSE = 6
-GM_PARAM_INDEX_CORE = 7
+GM_PARAM_HIST_GRID = 8
 
 GM_JOIN_AUTO = 0
 GM_JOIN_DIRECT = 1
@@ -130,7 +130,6 @@ SIGNATURES = {
     "gm_pip_index_create_ex": (cint, [vp, vp, cint, vp]),
     "gm_pip_index_destroy": (cint, [vp]),
     "gm_pip_index_stats": (cint, [vp, vp]),
-    "gm_pip_index_core": (cint, [vp, vp, vp, vp]),
     "gm_pip_join_census": (cint, [vp, vp, vp, vp, i64, vp]),
     "gm_pip_index_export": (cint, [vp, vp]),
     "gm_pip_index_copy_array": (cint, [vp, vp, cint, vp]),

@@ -322,9 +322,9 @@ int gm_ctx_set_param(gm_ctx* c, int param, int64_t value) {
       if (value < -1 || value > 1) return GM_E_INVALID;
       c->index_coarse = value;
       return GM_OK;
-    case GM_PARAM_INDEX_CORE:
-      if (value != 0 && value != 1) return GM_E_INVALID;
-      c->index_core = value;
+    case GM_PARAM_HIST_GRID:
+      if (value < 0 || value > (1 << 20)) return GM_E_INVALID;
+      c->hist_grid = value;
       return GM_OK;
     default:
       gm::set_error("gm_ctx_set_param: unknown parameter");
@@ -341,7 +341,7 @@ int gm_ctx_get_param(gm_ctx* c, int param, int64_t* value) {
     case GM_PARAM_SORT_MODE: *value = c->sort_mode; return GM_OK;
     case GM_PARAM_SORT_LAST: *value = c->sort_last; return GM_OK;
     case GM_PARAM_INDEX_COARSE: *value = c->index_coarse; return GM_OK;
-    case GM_PARAM_INDEX_CORE: *value = c->index_core; return GM_OK;
+    case GM_PARAM_HIST_GRID: *value = c->hist_grid; return GM_OK;
     default: return GM_E_INVALID;
   }
 }

@@ -77,15 +77,6 @@ struct PipDev {
   const uint32_t* cm;
   int32_t cm_shift, cm_shift_y, cm_w;
   int64_t cm_words;
-  // the same bitmap at the row predicate's smaller LDS budget (RELATE_CM_WORDS)
-  const uint32_t* cm2;
-  int32_t cm2_shift, cm2_shift_y, cm2_w;
-  int64_t cm2_words;
-  // per polygon p, a rectangle of fine cells (x0, y0, x1, y1 inclusive; x0 > x1 = none) whose words
-  // are all INTERIOR(p) (make_shortcut, k_core_*): the row predicate answers a row of polygon p inside
-  // it from LDS, without the coarse and fine gathers.  n_core = 0: no table
-  const ushort4* core;
-  int32_t n_core;
 };
 
 enum : uint32_t { PIP_FAULT_LINE = 1, PIP_FAULT_COMPACT = 2, PIP_FAULT_BLOB = 4, PIP_FAULT_LIST = 8, PIP_FAULT_QUEUE = 16 };
@@ -282,6 +273,36 @@ __device__ __forceinline__ int compact_locate(const dv2* __restrict__ c, double 
   return (cr & 1) ? LOC_INTERIOR : LOC_EXTERIOR;
 }
 
+// compact_locate with one 16-B load at a time (a rolled loop over the record's 2 x 8 pairs of words):
+// the same arithmetic in the same order per segment and the same breakpoint count, for kernels whose
+// walk must not hold the two lines' 64 VGPRs (the fused query scan's block-level walk).  Segment j
+// occupies the word pairs cseg_word(j) / 2 and cseg_word(j) / 2 + 1; every other pair is two
+// breakpoint slots (a segment slot past E included).
+__device__ inline int compact_locate_lean(const dv2* __restrict__ c, double px, double py, int& poly) {
+  const dv2 h = c[0];
+  const int64_t meta = __double_as_longlong(h.x);
+  poly = (int)meta;
+  const int E = (int)((meta >> 32) & 0xff), lines = (int)((meta >> 40) & 0xff);
+  int k = 0, cr = 0;
+  bool on = false;
+  const int np = lines > 1 ? 16 : 8;
+  for (int i = 1; i < np; ++i) {
+    // segment j starting at pair i: i = 1, 3, 5 (line 0), 8, 10, 12, 14 (line 1)
+    const int j = (i < 7 && (i & 1)) ? (i - 1) / 2 : ((i >= 8 && !(i & 1)) ? 3 + (i - 8) / 2 : -1);
+    if (j >= 0 && j < E) {
+      const dv2 a = c[i], b = c[i + 1];
+      if (!on) on = count_segment(a.x, a.y, b.x, b.y, px, py, cr);
+      ++i;   // the segment's second pair
+    } else {
+      const dv2 q = c[i];
+      k += (q.x <= py) + (q.y <= py);
+    }
+  }
+  if (on) return LOC_BOUNDARY;
+  cr += (int)(((uint64_t)__double_as_longlong(h.y) >> k) & 1ull);
+  return (cr & 1) ? LOC_INTERIOR : LOC_EXTERIOR;
+}
+
 __device__ __forceinline__ bool compact_contains(const dv2* __restrict__ c, double px, double py, int& poly) {
   return compact_locate(c, px, py, poly) == LOC_INTERIOR;
 }
@@ -430,8 +451,39 @@ __device__ __forceinline__ uint32_t coarse_mask(uint32_t w, int cx, int cy, int3
   return ((w >> sub) & 1u) ? (CELL_EMPTY << 30) : w;
 }
 
+// a point's position inside its cell (cx, cy) in cell units, as the shortcut tests take it; a kernel
+// may keep it in float (|error| <= 2^-25 cell, so |delta f| <= (|A| + |B|) 2^-25 <= 2^-10 units of the
+// lines' 2^-14 cell: far inside the SC_T - SC_DEV = 2 units the line decision keeps in hand)
+__device__ __forceinline__ double cell_u(double x, const PipDev& d, int cx) {
+  return __dsub_rn(__dmul_rn(__dsub_rn(x, d.gx0), d.inv_cw), (double)cx);
+}
+__device__ __forceinline__ double cell_v(double y, const PipDev& d, int cy) {
+  return __dsub_rn(__dmul_rn(__dsub_rn(y, d.gy0), d.inv_ch), (double)cy);
+}
+// line_locate from the in-cell position (u, v)
+__device__ __forceinline__ int line_locate_uv(const uint4 e0, const uint4 e1, double u, double v) {
+  auto f = [&](uint32_t ab, uint32_t c) -> double {
+    const double A = (double)(int16_t)(ab & 0xffffu), B = (double)(int16_t)(ab >> 16);
+    const double C = (double)((int32_t)(c << 8) >> 8);
+    return __dsub_rn(__dadd_rn(__dmul_rn(A, u), __dmul_rn(B, v)), C);
+  };
+  const double g1 = f(e0.z, e0.w);
+  if (!(g1 > SC_T || g1 < -SC_T)) return -1;
+  uint32_t r = g1 > SC_T ? 0u : 1u;
+  if ((e1.y >> 24) > 1) {
+    const double g2 = f(e1.x, e1.y);
+    if (!(g2 > SC_T || g2 < -SC_T)) return -1;
+    r |= g2 > SC_T ? 0u : 2u;
+  }
+  const uint32_t fl = e0.w >> 24;
+  if (!((fl >> (2 * r)) & 1u)) return -1;
+  return ((fl >> (2 * r + 1)) & 1u) ? LOC_INTERIOR : LOC_EXTERIOR;
+}
+
 // PointLocator's location of a point for one BOUNDARY item (ref = the word's payload): a line
-// shortcut (near the line: the entry's own blob), a compact blob or a generic blob
+// shortcut (near the line: the entry's own blob), a compact blob or a generic blob.  LEAN: the compact
+// blob one 16-B load at a time (compact_locate_lean)
+template <bool LEAN = false>
 __device__ __forceinline__ int item_locate(const PipDev& d, uint32_t ref, double x, double y, int& poly) {
   int loc = -1;
   if ((ref & BLOB_COMPACT) && d.line_ent && (ref & SC_LINE)) {
@@ -446,7 +498,8 @@ __device__ __forceinline__ int item_locate(const PipDev& d, uint32_t ref, double
   if (ref & BLOB_COMPACT) {
     const uint64_t ci = ref & (BLOB_COMPACT - 1);
     if (GM_REF_BAD(ci >= (uint64_t)d.n_compact_lines)) { pip_fault(d, PIP_FAULT_COMPACT); poly = -1; return LOC_EXTERIOR; }
-    return compact_locate((const dv2*)(d.compact + 16 * ci), x, y, poly);
+    return LEAN ? compact_locate_lean((const dv2*)(d.compact + 16 * ci), x, y, poly)
+                : compact_locate((const dv2*)(d.compact + 16 * ci), x, y, poly);
   }
   if (GM_REF_BAD((uint64_t)ref >= (uint64_t)d.n_blob16)) { pip_fault(d, PIP_FAULT_BLOB); poly = -1; return LOC_EXTERIOR; }
   const double* b = d.blob + 2 * (uint64_t)ref;
@@ -469,20 +522,15 @@ constexpr int ICAP = 128;              // item queue (two ends)
 constexpr int JQ_WAVE_LDS = FCAP * 20 + ICAP * 24;
 constexpr int CM_WORDS_MAX = (163840 - (QTPB / 64) * JQ_WAVE_LDS - 256) / 4;   // 13,248 words at 1024 threads
 
-// The row predicate (gm_pip_relate.hip): its own, coarser bitmap (32 KiB: what its queues and the core
-// rectangles leave of the LDS, 163,584 B per block) and a core rectangle per polygon (8 B each).
+// The row predicate (gm_pip_relate.hip): one 1024-thread block per CU, per wave a fine queue and an
+// item queue of 20-B entries (a row's fine cell or reference, its in-cell position in float, row and
+// polygon), beside the join's coarse EMPTY bitmap (cm, CM_WORDS_MAX words).
+constexpr int RFCAP = FBATCH + 128, RICAP = 128;
+static_assert((GM_JQ_TPB / 64) * 20 * (RFCAP + RICAP) + 4 * CM_WORDS_MAX + 256 <= 163840, "row predicate LDS");
 #ifndef GM_RELATE_TPB
 #define GM_RELATE_TPB 1024
 #endif
 constexpr int RTPB = GM_RELATE_TPB;
-#ifndef GM_RELATE_CM_WORDS
-#define GM_RELATE_CM_WORDS 8128
-#endif
-constexpr int RELATE_CM_WORDS = GM_RELATE_CM_WORDS;
-#ifndef GM_RELATE_CORE_MAX
-#define GM_RELATE_CORE_MAX 4096
-#endif
-constexpr int RELATE_CORE_MAX = GM_RELATE_CORE_MAX;
 
 }  // namespace gm
 

@@ -771,98 +771,6 @@ __global__ __launch_bounds__(256) void k_build_cmask(const uint32_t* __restrict_
   }
 }
 
-// The row predicate's core rectangles (PipDev::core): for every polygon, a large rectangle of fine
-// cells whose words are all INTERIOR(p).  Any such rectangle is exact (a row in it gets the answer its
-// cell word gives).  The search runs on the coarse grid -- the largest rectangle of INTERIOR(p) coarse
-// cells with its top-left corner on any cell, extents capped at CORE_CAP coarse cells so the build
-// stays linear in the coarse grid -- and k_core_write widens it over the fine cells.
-constexpr int CORE_CAP = 256;
-
-// run[i] = how many coarse cells from i rightwards (<= CORE_CAP) carry i's INTERIOR word; 0 otherwise
-__global__ __launch_bounds__(256) void k_core_run(const uint32_t* __restrict__ coarse_sc, int gxc, int64_t n,
-                                                  int32_t n_polys, int32_t* __restrict__ run) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const uint32_t w = coarse_sc[i];
-    int r = 0;
-    if ((w >> 30) == CELL_INTERIOR && (int64_t)(w & 0x3fffffffu) < n_polys) {
-      const int xc = (int)(i % gxc);
-      r = 1;
-      while (r < CORE_CAP && xc + r < gxc && coarse_sc[i + r] == w) ++r;
-    }
-    run[i] = r;
-  }
-}
-
-// the largest rectangle with its top-left corner on coarse cell i (first maximum scanning down)
-__device__ __forceinline__ int core_rect(const uint32_t* coarse_sc, const int32_t* run, int gxc, int gyc, int64_t i,
-                                         int& bw, int& bh) {
-  const uint32_t w = coarse_sc[i];
-  const int yc = (int)(i / gxc);
-  int best = 0, wmin = run[i];
-  bw = bh = 0;
-  for (int h = 1; h <= CORE_CAP && yc + h - 1 < gyc && wmin > 0; ++h) {
-    const int64_t j = i + (int64_t)(h - 1) * gxc;
-    wmin = coarse_sc[j] == w ? min(wmin, (int)run[j]) : 0;
-    if (wmin * h > best) { best = wmin * h; bw = wmin; bh = h; }
-  }
-  return best;
-}
-
-// best[p] = max over p's cells of (area << 40 | cell): deterministic (ties go to the larger cell index)
-__global__ __launch_bounds__(256) void k_core_best(const uint32_t* __restrict__ coarse_sc, const int32_t* __restrict__ run,
-                                                   int gxc, int gyc, unsigned long long* __restrict__ best) {
-  const int64_t n = (int64_t)gxc * gyc;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    if (run[i] == 0) continue;
-    int bw, bh;
-    const int a = core_rect(coarse_sc, run, gxc, gyc, i, bw, bh);
-    if (a > 0) atomicMax(&best[coarse_sc[i] & 0x3fffffffu], ((unsigned long long)a << 40) | (unsigned long long)i);
-  }
-}
-
-// core[p] in fine cells: the coarse rectangle widened cell by cell (at most one coarse cell per side)
-// while the new column / row of fine cells still carries INTERIOR(p) -- the fine cells of the mixed
-// coarse ring around it that are interior too
-__global__ __launch_bounds__(256) void k_core_write(const uint32_t* __restrict__ coarse_sc, const uint32_t* __restrict__ cell_sc,
-                                                    const int32_t* __restrict__ run, int gx, int gy, int gxc, int gyc,
-                                                    const unsigned long long* __restrict__ best, int32_t n_polys,
-                                                    ushort4* __restrict__ core) {
-  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < n_polys; p += gridDim.x * blockDim.x) {
-    const unsigned long long v = best[p];
-    ushort4 r = make_ushort4(1, 1, 0, 0);   // none
-    if (v) {
-      const int64_t i = (int64_t)(v & ((1ull << 40) - 1));
-      int bw, bh;
-      core_rect(coarse_sc, run, gxc, gyc, i, bw, bh);
-      const int xc = (int)(i % gxc), yc = (int)(i / gxc);
-      const uint32_t w = coarse_sc[i];
-      int X0 = xc << CF_LOG, Y0 = yc << CF_LOG;
-      int X1 = min(gx, (xc + bw) << CF_LOG) - 1, Y1 = min(gy, (yc + bh) << CF_LOG) - 1;
-      auto col_ok = [&](int X) {
-        if (X < 0 || X >= gx) return false;
-        for (int Y = Y0; Y <= Y1; ++Y)
-          if (cell_sc[(int64_t)Y * gx + X] != w) return false;
-        return true;
-      };
-      auto row_ok = [&](int Y) {
-        if (Y < 0 || Y >= gy) return false;
-        for (int X = X0; X <= X1; ++X)
-          if (cell_sc[(int64_t)Y * gx + X] != w) return false;
-        return true;
-      };
-      for (int k = 0; k < (1 << CF_LOG); ++k) {
-        bool grew = false;
-        if (col_ok(X0 - 1)) { --X0; grew = true; }
-        if (col_ok(X1 + 1)) { ++X1; grew = true; }
-        if (row_ok(Y0 - 1)) { --Y0; grew = true; }
-        if (row_ok(Y1 + 1)) { ++Y1; grew = true; }
-        if (!grew) break;
-      }
-      r = make_ushort4((unsigned short)X0, (unsigned short)Y0, (unsigned short)X1, (unsigned short)Y1);
-    }
-    core[p] = r;
-  }
-}
 
 // pass 0 (ent == nullptr): cell_sc = resolved words, is_line[c] = 1 for line cells;
 // pass 1: the line entries at their scanned slots, and the LINE words
@@ -1030,10 +938,6 @@ int make_shortcut(gm_pip_index* ix) {
   ix->dev.fault = nullptr;   // set per call (the call's scratch word)
   ix->dev.cm = nullptr;      // the coarse EMPTY bitmaps, built after coarse_sc
   ix->dev.cm_words = 0;
-  ix->dev.cm2 = nullptr;
-  ix->dev.cm2_words = 0;
-  ix->dev.core = nullptr;    // the row predicate's core rectangles, built after the bitmaps
-  ix->dev.n_core = 0;
   ix->dev.n_line = 0;
   ix->dev.n_compact_lines = ix->arr_bytes[5] / 128;
   ix->dev.n_blob16 = ix->arr_bytes[7] / 16;
@@ -1103,34 +1007,6 @@ int make_shortcut(gm_pip_index* ix) {
       return GM_OK;
     };
     rc = bitmap(CM_WORDS_MAX, &ix->dev.cm, &ix->dev.cm_shift, &ix->dev.cm_shift_y, &ix->dev.cm_w, &ix->dev.cm_words);
-    if (!rc)
-      rc = bitmap(RELATE_CM_WORDS, &ix->dev.cm2, &ix->dev.cm2_shift, &ix->dev.cm2_shift_y, &ix->dev.cm2_w, &ix->dev.cm2_words);
-    // the row predicate's core rectangles (fine-cell coordinates in 16 bits; polygon count within its LDS table)
-    if (!rc && ix->n_polys > 0 && ix->n_polys <= RELATE_CORE_MAX && ix->dev.gx < 65535 && ix->dev.gy < 65535 &&
-        ix->ctx->index_core) {
-      const int64_t nc = (int64_t)gxc * gyc;
-      void *run = nullptr, *best = nullptr, *core = nullptr;
-      if (hipMalloc(&run, (size_t)nc * 4) != hipSuccess || hipMalloc(&best, (size_t)ix->n_polys * 8) != hipSuccess ||
-          hipMalloc(&core, (size_t)ix->n_polys * 8) != hipSuccess) {
-        (void)hipFree(run); (void)hipFree(best); (void)hipFree(core);
-        cleanup();
-        return hip_fail(hipErrorOutOfMemory, "gm_pip_index core");
-      }
-      ix->allocs.push_back(core);
-      const unsigned gc = (unsigned)std::min<int64_t>(65536, (nc + 255) / 256);
-      hipLaunchKernelGGL(k_core_run, dim3(gc), dim3(256), 0, s, ix->dev.coarse_sc, gxc, nc, ix->n_polys, (int32_t*)run);
-      GM_HIP(hipMemsetAsync(best, 0, (size_t)ix->n_polys * 8, s));
-      hipLaunchKernelGGL(k_core_best, dim3(gc), dim3(256), 0, s, ix->dev.coarse_sc, (const int32_t*)run, gxc, gyc,
-                         (unsigned long long*)best);
-      hipLaunchKernelGGL(k_core_write, dim3((unsigned)((ix->n_polys + 255) / 256)), dim3(256), 0, s, ix->dev.coarse_sc,
-                         ix->dev.cell_sc, (const int32_t*)run, ix->dev.gx, ix->dev.gy, gxc, gyc,
-                         (const unsigned long long*)best, ix->n_polys, (ushort4*)core);
-      const bool ok = hipStreamSynchronize(s) == hipSuccess;
-      (void)hipFree(run); (void)hipFree(best);
-      if (!ok) { cleanup(); return hip_fail(hipErrorLaunchFailure, "k_core_*"); }
-      ix->dev.core = (const ushort4*)core;
-      ix->dev.n_core = ix->n_polys;
-    }
     if (rc) { cleanup(); return rc; }
   }
   if (!rc && hipStreamSynchronize(s) != hipSuccess) rc = hip_fail(hipErrorLaunchFailure, "k_build_shortcut");
@@ -1968,12 +1844,5 @@ int gm_pip_index_stats(const gm_pip_index* ix, int64_t* stats) {
   return GM_OK;
 }
 
-int gm_pip_index_core(gm_ctx* ctx, const gm_pip_index* ix, uint16_t* rects, int32_t* n_core) {
-  if (!ctx || !ix || !n_core) return GM_E_INVALID;
-  *n_core = ix->dev.core ? ix->dev.n_core : 0;
-  if (!rects || *n_core == 0) return GM_OK;
-  GM_HIP(hipSetDevice(ctx->device));
-  return copy_d2h(ctx, rects, ix->dev.core, (size_t)*n_core * 8);
-}
 
 }  // extern "C"

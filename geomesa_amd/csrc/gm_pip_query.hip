@@ -20,6 +20,7 @@ namespace gm {
 // rate of the strict scan (24 B per row) plus a few L2 hits per candidate row.  Rows are laid out
 // as in the other mask kernels (pair_scan: 16-B loads, ballot-interleaved mask words).
 enum : int { SP_NONE = 0, SP_INTERSECTS = 1, SP_CONTAINS = 2 };
+static_assert(CF_LOG == 3, "k_query_mask packs a fine cell's 3 + 3 bit place in its coarse cell");
 
 template <int OP>
 __device__ __forceinline__ bool entry_pred(const PipDev& d, uint32_t e, double px, double py) {
@@ -29,7 +30,7 @@ __device__ __forceinline__ bool entry_pred(const PipDev& d, uint32_t e, double p
   int loc;
   if (ref & BLOB_COMPACT) {
     int poly;
-    loc = compact_locate((const dv2*)(d.compact + 16 * (uint64_t)(ref & (BLOB_COMPACT - 1))), px, py, poly);
+    loc = compact_locate_lean((const dv2*)(d.compact + 16 * (uint64_t)(ref & (BLOB_COMPACT - 1))), px, py, poly);
   } else {
     const double* b = d.blob + 2 * (uint64_t)ref;
     loc = blob_locate(d, b, *(const int2*)b, px, py);
@@ -37,34 +38,51 @@ __device__ __forceinline__ bool entry_pred(const PipDev& d, uint32_t e, double p
   return OP == SP_INTERSECTS ? loc != LOC_EXTERIOR : loc == LOC_INTERIOR;
 }
 
-// Phases per lane, over the lane's 2 * FPAIRS rows:
+// Phases per lane, over the lane's 2 NP rows:
 //  1. the streaming terms (16-B loads, registers only); rows inside the index envelope keep their
 //     coarse and fine cell numbers;
-//  2. the coarse words of all surviving rows, then the fine words of those in LIST coarse cells --
-//     independent loads issued together, so the chain costs two L2 round trips per lane, not two
-//     per row;
-//  3. the rows still undecided (boundary cells, multi-polygon lists) walk their blobs one per loop
-//     trip, re-reading the row's coordinates (keeping the staged columns live through the walk
-//     costs 32 VGPRs).
-#ifndef GM_QUERY_WAVES
-#define GM_QUERY_WAVES 1
+//  2. the coarse words of all surviving rows (the join's coarse table, coarse_sc: EMPTY / INTERIOR
+//     coarse cells and the sub-block masks of mixed ones decide most rows), then the fine words of the
+//     rest (cell_sc: the cell words with the boundary shortcuts applied) -- independent loads issued
+//     together, so the chain costs two L2 round trips per lane, not two per row;
+//  3. the rows still undecided walk one per loop trip, re-reading the row's coordinates (keeping the
+//     staged columns live through the walk costs 32 VGPRs): a boundary cell crossed by one or two
+//     segments decides from its 32-B line entry (item_locate), only a row near a line or in a cell the
+//     shortcuts left walks its blob; a multi-polygon list tests its entries.
+// Block shape: FROWS = 4096 rows per block (the shared mask / count / compaction layout) as TPB threads
+// x 2 NP rows.  Without a geometry term 256 x 16 rows (the strict scan's shape).  With one, TPB x 2 NP
+// = GM_QUERY_TPB x ...: the lookup chain's per-row state (coarse and fine cells, words) shrinks with NP,
+// so the kernel holds fewer VGPRs and more waves hide the chain's L2 round trips behind other waves'
+// streams.
+#ifndef GM_QUERY_TPB
+#define GM_QUERY_TPB 512
 #endif
+#ifndef GM_QUERY_COARSE_LDS
+#define GM_QUERY_COARSE_LDS 4096
+#endif
+constexpr int QCOARSE_LDS = GM_QUERY_COARSE_LDS;   // coarse words staged in LDS (16 KB)
+template <int OP>
+struct QueryShape {
+  static constexpr int TPB = OP == SP_NONE ? FTPB : GM_QUERY_TPB;
+  static constexpr int NP = FROWS / (2 * TPB);
+};
 template <bool VEC, bool DURING, int OP>
-__global__ __launch_bounds__(FTPB, GM_QUERY_WAVES) void k_query_mask(const double* __restrict__ x, const double* __restrict__ y,
+__global__ __launch_bounds__(QueryShape<OP>::TPB) void k_query_mask(const double* __restrict__ x, const double* __restrict__ y,
                                                      const int64_t* __restrict__ t, int64_t n, int has_bbox,
                                                      double bx0, double by0, double bx1, double by1, int64_t lo,
                                                      int64_t hi, PipDev d, uint64_t* __restrict__ mask,
                                                      int32_t* __restrict__ block_counts) {
-  constexpr int R = 2 * FPAIRS;
+  constexpr int TPB = QueryShape<OP>::TPB, NP = QueryShape<OP>::NP;
+  constexpr int R = 2 * NP;
   const int64_t npairs = n >> 1, nwords = (n + 63) >> 6;
   const int wave = threadIdx.x >> 6;
-  const int64_t pbase = (int64_t)blockIdx.x * (FTPB * FPAIRS);
-  dv2 xv[FPAIRS], yv[FPAIRS];
-  lv2 tv[FPAIRS];
+  const int64_t pbase = (int64_t)blockIdx.x * (TPB * NP);
+  dv2 xv[NP], yv[NP];
+  lv2 tv[NP];
   uint32_t live = 0;   // bit 2u + j: row j of pair step u exists
 #pragma unroll
-  for (int u = 0; u < FPAIRS; ++u) {
-    const int64_t p = pbase + (int64_t)u * FTPB + threadIdx.x;
+  for (int u = 0; u < NP; ++u) {
+    const int64_t p = pbase + (int64_t)u * TPB + threadIdx.x;
     xv[u] = yv[u] = dv2{0.0, 0.0};
     tv[u] = lv2{0, 0};
     if (p < npairs) {
@@ -85,6 +103,15 @@ __global__ __launch_bounds__(FTPB, GM_QUERY_WAVES) void k_query_mask(const doubl
       if (DURING) tv[u].x = t[2 * p];
     }
   }
+  // a query-sized index's whole coarse table (<= QCOARSE_LDS words: a polygon's 65,536-cell index has
+  // 1,024) staged in LDS while the rows load: its lookups cost an LDS read instead of an L2 round trip
+  __shared__ uint32_t s_coarse[OP == SP_NONE ? 1 : QCOARSE_LDS];
+  const int64_t ncoarse = (int64_t)d.gxc * ((d.gy + (1 << CF_LOG) - 1) >> CF_LOG);
+  const bool coarse_lds = OP != SP_NONE && ncoarse <= QCOARSE_LDS;
+  if (coarse_lds) {
+    for (int i = threadIdx.x; i < ncoarse; i += TPB) s_coarse[i] = d.coarse_sc[i];
+    __syncthreads();
+  }
   uint32_t pass = 0;
   int fc[R], cc[R];   // fine / coarse cell of each row (geometry term only)
   auto cheap = [&](double px, double py, int64_t tt, int k) {
@@ -94,12 +121,14 @@ __global__ __launch_bounds__(FTPB, GM_QUERY_WAVES) void k_query_mask(const doubl
       ok = ok && px >= d.gx0 && px <= d.gx1 && py >= d.gy0 && py <= d.gy1;
       const int cx = cell_of(px, d.gx0, d.inv_cw, d.gx), cy = cell_of(py, d.gy0, d.inv_ch, d.gy);
       fc[k] = cy * d.gx + cx;
-      cc[k] = (cy >> CF_LOG) * d.gxc + (cx >> CF_LOG);
+      // the coarse cell (< 2^20 of them: the grid has at most 2^26 cells) and, in the top 6 bits, the
+      // fine cell's place in it (what coarse_mask reads)
+      cc[k] = ((cy >> CF_LOG) * d.gxc + (cx >> CF_LOG)) | (((cy & 7) << 3 | (cx & 7)) << 26);
     }
     return ok;
   };
 #pragma unroll
-  for (int u = 0; u < FPAIRS; ++u) {
+  for (int u = 0; u < NP; ++u) {
     pass |= (uint32_t)cheap(xv[u].x, yv[u].x, tv[u].x, 2 * u) << (2 * u);
     pass |= (uint32_t)cheap(xv[u].y, yv[u].y, tv[u].y, 2 * u + 1) << (2 * u + 1);
   }
@@ -107,10 +136,16 @@ __global__ __launch_bounds__(FTPB, GM_QUERY_WAVES) void k_query_mask(const doubl
   if (OP != SP_NONE && pass) {
     uint32_t cw[R];
 #pragma unroll
-    for (int k = 0; k < R; ++k) cw[k] = ((pass >> k) & 1u) ? d.coarse_word[cc[k]] : (CELL_EMPTY << 30);
+    for (int k = 0; k < R; ++k)
+      cw[k] = ((pass >> k) & 1u) ? (coarse_lds ? s_coarse[cc[k] & 0x3ffffff] : d.coarse_sc[cc[k] & 0x3ffffff]) : (CELL_EMPTY << 30);
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      const uint32_t sb = (uint32_t)cc[k] >> 26;
+      cw[k] = coarse_mask(cw[k], (int)(sb & 7u), (int)(sb >> 3), d.coarse_fmt);
+    }
 #pragma unroll
     for (int k = 0; k < R; ++k)
-      if ((cw[k] >> 30) == CELL_LIST) cw[k] = d.cell_word[fc[k]];
+      if ((cw[k] >> 30) == CELL_LIST) cw[k] = d.cell_sc[fc[k]];
     uint32_t slow = 0;
 #pragma unroll
     for (int k = 0; k < R; ++k) {
@@ -124,7 +159,7 @@ __global__ __launch_bounds__(FTPB, GM_QUERY_WAVES) void k_query_mask(const doubl
 #pragma unroll
       for (int j = 1; j < R; ++j)
         if (k == j) w = cw[j];
-      const int64_t row = 2 * (pbase + (int64_t)(k >> 1) * FTPB + threadIdx.x) + (k & 1);
+      const int64_t row = 2 * (pbase + (int64_t)(k >> 1) * TPB + threadIdx.x) + (k & 1);
       const double px = x[row], py = y[row];
       bool hit;
       if ((w >> 30) == CELL_LIST) {
@@ -134,20 +169,22 @@ __global__ __launch_bounds__(FTPB, GM_QUERY_WAVES) void k_query_mask(const doubl
         if (GM_REF_BAD(ni < 0 || (int64_t)l0 + ni > d.n_list)) { pip_fault(d, PIP_FAULT_LIST); ni = 0; }
         hit = false;
         for (int j = 0; j < ni && !hit; ++j) hit = entry_pred<OP>(d, d.list_ent[l0 + j], px, py);
-      } else {
-        hit = entry_pred<OP>(d, w, px, py);
+      } else {   // a boundary cell: its line entry (LINE words), else its blob
+        int poly;
+        const int loc = item_locate<true>(d, w & 0x3fffffffu, px, py, poly);
+        hit = OP == SP_INTERSECTS ? loc != LOC_EXTERIOR : loc == LOC_INTERIOR;
       }
       if (!hit) pass &= ~(1u << k);
     }
   }
   int cnt = 0;
 #pragma unroll
-  for (int u = 0; u < FPAIRS; ++u) {
+  for (int u = 0; u < NP; ++u) {
     const uint64_t be = __ballot((pass >> (2 * u)) & 1u), bo = __ballot((pass >> (2 * u + 1)) & 1u);
     cnt += __popcll(be) + __popcll(bo);
-    put_pair_words(be, bo, mask, ((pbase + (int64_t)u * FTPB + wave * 64) * 2) >> 6, nwords);
+    put_pair_words(be, bo, mask, ((pbase + (int64_t)u * TPB + wave * 64) * 2) >> 6, nwords);
   }
-  block_count_waves(cnt, block_counts);
+  block_count_waves<TPB>(cnt, block_counts);
 }
 template <bool VEC, bool DURING>
 void launch_query(hipStream_t s, unsigned grid, int op, const double* x, const double* y, const int64_t* t, int64_t n,
@@ -155,15 +192,15 @@ void launch_query(hipStream_t s, unsigned grid, int op, const double* x, const d
                   int32_t* counts) {
   switch (op) {
     case SP_INTERSECTS:
-      hipLaunchKernelGGL((k_query_mask<VEC, DURING, SP_INTERSECTS>), dim3(grid), dim3(FTPB), 0, s, x, y, t, n, has_bbox,
+      hipLaunchKernelGGL((k_query_mask<VEC, DURING, SP_INTERSECTS>), dim3(grid), dim3(QueryShape<SP_INTERSECTS>::TPB), 0, s, x, y, t, n, has_bbox,
                          bb[0], bb[1], bb[2], bb[3], lo, hi, d, mask, counts);
       break;
     case SP_CONTAINS:
-      hipLaunchKernelGGL((k_query_mask<VEC, DURING, SP_CONTAINS>), dim3(grid), dim3(FTPB), 0, s, x, y, t, n, has_bbox,
+      hipLaunchKernelGGL((k_query_mask<VEC, DURING, SP_CONTAINS>), dim3(grid), dim3(QueryShape<SP_CONTAINS>::TPB), 0, s, x, y, t, n, has_bbox,
                          bb[0], bb[1], bb[2], bb[3], lo, hi, d, mask, counts);
       break;
     default:
-      hipLaunchKernelGGL((k_query_mask<VEC, DURING, SP_NONE>), dim3(grid), dim3(FTPB), 0, s, x, y, t, n, has_bbox,
+      hipLaunchKernelGGL((k_query_mask<VEC, DURING, SP_NONE>), dim3(grid), dim3(QueryShape<SP_NONE>::TPB), 0, s, x, y, t, n, has_bbox,
                          bb[0], bb[1], bb[2], bb[3], lo, hi, d, mask, counts);
   }
 }

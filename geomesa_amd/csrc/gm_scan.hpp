@@ -41,14 +41,15 @@ __device__ __forceinline__ void put_pair_words(uint64_t even, uint64_t odd, uint
   }
 }
 
+template <int TPB = FTPB>
 __device__ __forceinline__ void block_count_waves(int wave_cnt, int32_t* block_counts) {
-  __shared__ int s_wc[FTPB / 64];
+  __shared__ int s_wc[TPB / 64];
   if ((threadIdx.x & 63) == 0) s_wc[threadIdx.x >> 6] = wave_cnt;
   __syncthreads();
   if (threadIdx.x == 0) {
     int s = 0;
 #pragma unroll
-    for (int i = 0; i < FTPB / 64; ++i) s += s_wc[i];
+    for (int i = 0; i < TPB / 64; ++i) s += s_wc[i];
     block_counts[blockIdx.x] = s;
   }
 }

@@ -11,8 +11,8 @@
 // time-bin rows of the [n_bins][length] counters in LDS (<= 32768 int32 = 128 KB) and flushes the
 // nonzero counters with one 64-bit device atomic each at the end, so HBM traffic is the 24 B/point
 // read plus grid x counters x 8 B; the grid is one resident wave of workgroups (1-2 per CU).  A
-// histogram larger than one LDS block of int32 counters keeps biased 16-bit counters instead (two
-// per word, NARROW below: 1024 x 54 week bins fit one pass), and beyond that takes up to
+// histogram larger than one LDS block of int32 counters keeps three 21-bit counters per 64-bit word
+// instead (WIDE below: 1024 x 54 week bins fit one pass), and beyond that takes up to
 // HIST_MAX_PASSES passes over the points, one per row block; beyond that it adds straight into the
 // 64-bit device counters (scattered per-lane device atomics run ~22 G/s on MI355X, so they only win
 // over many passes).
@@ -24,6 +24,9 @@ namespace gm {
 
 constexpr int HTPB = 1024;
 constexpr int HIST_LDS_MAX = 32768;  // int32 counters per workgroup (128 KB of the 160 KB LDS)
+// LDS for the WIDE counters, the row flags and what rounding leaves: 160 KB less the 8 KB spread table
+// and the kernel's two scalars
+constexpr int HIST_WIDE_BYTES = 163840 - 8192 - 64;
 constexpr int HIST_MAX_PASSES = 4;
 
 struct HistArgs {
@@ -130,43 +133,40 @@ __device__ __forceinline__ int hist_slot_top(double x, double y, int64_t ms, con
   return rb * a.length + i;
 }
 
-// NARROW: two biased 16-bit counters per 32-bit LDS word (twice the time-bin rows per pass).  A half
-// starts at NB; the thread whose increment lifts it to NB + NS moves NS to the device counter (the
-// decrement that drops it to NB - NS moves -NS), so a half stays within NB +- NS plus the increments
-// in flight and never carries into its neighbour.  The final flush adds half - NB.
-constexpr uint32_t NB = 0x8000u, NS = 0x4000u;
-
-__device__ __forceinline__ void narrow_inc(uint32_t* w, int sh, unsigned long long* g) {
-  const uint32_t old = atomicAdd(w, 1u << sh);
-  if (((old >> sh) & 0xFFFFu) == NB + NS - 1) {
-    atomicSub(w, NS << sh);
-    atomicAdd(g, (unsigned long long)NS);
-  }
-}
-__device__ __forceinline__ void narrow_dec(uint32_t* w, int sh, unsigned long long* g) {
-  const uint32_t old = atomicSub(w, 1u << sh);
-  if (((old >> sh) & 0xFFFFu) == NB - NS + 1) {
-    atomicAdd(w, NS << sh);
-    atomicAdd(g, (unsigned long long)(-(long long)NS));
-  }
+// WIDE: three 21-bit counters per 64-bit LDS word (55,296 counters -- 1024 x 54 week bins -- in one
+// 144 KB pass, where int32 counters need 216 KB).  Increments are plain non-returning 64-bit LDS adds
+// (ds_add_u64) of 1 << (21 k); a field cannot carry into its neighbour because the workgroup drains
+// every field to the device counters (and resets it) before any field can have moved by 2^21 - 1
+// (observe, fields from 0) or 2^20 - 1 (unobserve, fields biased at 2^20): the drain comes after a
+// fixed number of block iterations, each of which counts at most HTPB * HU * 2 points.  So the hot loop
+// carries no returning atomic and no per-point check (the former 16-bit halves took a returning LDS
+// atomic per increment: 4.71-4.75 vs 4.36 ms per 1B points for int32 counters).
+constexpr int WBITS = 21;
+constexpr uint64_t WMASK = (1ull << WBITS) - 1;
+__device__ __forceinline__ uint64_t wide_bias(bool unobs) { return unobs ? (1ull << 20) : 0ull; }
+__device__ __forceinline__ uint64_t wide_fill(bool unobs) {
+  const uint64_t b = wide_bias(unobs);
+  return b | (b << WBITS) | (b << (2 * WBITS));
 }
 
-template <int PERIOD, bool UNOBS, bool VEC, bool NARROW, bool TOP>
+template <int PERIOD, bool UNOBS, bool VEC, bool WIDE, bool TOP>
 __global__ __launch_bounds__(HTPB) void k_z3_hist_lds(const double* __restrict__ x, const double* __restrict__ y,
                                                       const int64_t* __restrict__ t, HistArgs a,
                                                       uint8_t* __restrict__ present,
                                                       unsigned long long* __restrict__ counts,
                                                       unsigned long long* __restrict__ tally) {
-  extern __shared__ int lds[];
+  extern __shared__ uint64_t lds64[];
   const int total = a.row_n * a.length;
-  const int cwords = NARROW ? (total + 1) / 2 : total;
-  int* cnt = lds;                          // [row_n * length] (NARROW: 16-bit halves)
-  int* pres = lds + cwords;                // [row_n]: bin present (observe sets, unobserve reads)
+  const int cw64 = WIDE ? (total + 2) / 3 : (total + 1) / 2;   // 64-bit words of counters
+  int* cnt = (int*)lds64;                  // int32 counters [row_n * length] (!WIDE)
+  uint64_t* wcnt = lds64;                  // 3 x 21-bit counters per word (WIDE)
+  int* pres = (int*)(lds64 + cw64);        // [row_n]: bin present (observe sets, unobserve reads)
   uint32_t* sp = (uint32_t*)(pres + a.row_n);  // [2048]: spread3_11 table
   __shared__ int s_skip, s_out;
   counts += (int64_t)a.row_lo * a.length;
   present += a.row_lo;
-  for (int i = threadIdx.x; i < cwords; i += HTPB) cnt[i] = NARROW ? (int)(NB | (NB << 16)) : 0;
+  if (WIDE) for (int i = threadIdx.x; i < cw64; i += HTPB) wcnt[i] = wide_fill(UNOBS);
+  else for (int i = threadIdx.x; i < total; i += HTPB) cnt[i] = 0;
   for (int i = threadIdx.x; i < a.row_n; i += HTPB) pres[i] = UNOBS ? (int)present[i] : 0;
   fill_spread_table(sp, threadIdx.x, HTPB);
   if (threadIdx.x == 0) { s_skip = 0; s_out = 0; }
@@ -181,39 +181,61 @@ __global__ __launch_bounds__(HTPB) void k_z3_hist_lds(const double* __restrict__
     c -= a.row_lo * a.length;
     if (UNOBS) {
       if (pres[rb]) {                        // binMap.get(timeBin).foreach(_.add(z, -1))
-        if (NARROW) narrow_dec((uint32_t*)&cnt[c >> 1], (c & 1) * 16, &counts[c]);
+        if (WIDE) { const int q = c / 3; atomicSub((unsigned long long*)&wcnt[q], 1ull << (WBITS * (c - 3 * q))); }
         else atomicAdd(&cnt[c], -1);
       }
     } else {
-      if (NARROW) narrow_inc((uint32_t*)&cnt[c >> 1], (c & 1) * 16, &counts[c]);
-      else atomicAdd(&cnt[c], 1);
       // binMap.getOrElseUpdate(timeBin, newBins): a row is present iff one of its features was
-      // counted; int32 counters only grow here, so the flush derives it from the row (no per-point
-      // LDS read); biased 16-bit halves move to the device counters and cannot tell, so they mark it
-      if (NARROW && !pres[rb]) pres[rb] = 1;
+      // counted; the drains and the flush derive it from the counters (no per-point LDS read)
+      if (WIDE) { const int q = c / 3; atomicAdd((unsigned long long*)&wcnt[q], 1ull << (WBITS * (c - 3 * q))); }
+      else atomicAdd(&cnt[c], 1);
     }
   };
+  // every field's change since the last drain to the device counters (and, observing, the rows it
+  // shows present); reset = the fields back to their bias.  All threads, two barriers.
+  auto drain = [&](bool reset) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < cw64; i += HTPB) {
+      const uint64_t w = wcnt[i];
+      if (w == wide_fill(UNOBS)) continue;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const int c = 3 * i + k;
+        const int64_t v = (int64_t)((w >> (WBITS * k)) & WMASK) - (int64_t)wide_bias(UNOBS);
+        if (c < total && v) {
+          atomicAdd(&counts[c], (unsigned long long)v);
+          if (!UNOBS && !pres[c / a.length]) pres[c / a.length] = 1;
+        }
+      }
+      if (reset) wcnt[i] = wide_fill(UNOBS);
+    }
+    __syncthreads();
+  };
+  // block iterations between drains: each counts at most HTPB * (VEC ? 2 * HU : 1) points, so no field
+  // moves by more than the field's room (2^21 - 1 up from 0, 2^20 - 1 down from 2^20) in between
+  const int64_t room = UNOBS ? (1 << 20) - 1 : (1 << 21) - 1;
   const int64_t stride = (int64_t)gridDim.x * HTPB;
+  int since = 0;
   if (VEC) {
     const dv2* x2 = (const dv2*)x;
     const dv2* y2 = (const dv2*)y;
     const lv2* t2 = (const lv2*)t;
     const int64_t np = a.n >> 1;
     // software-pipelined: the next HU pairs per lane are in flight while the current ones are binned
-#ifndef GM_HIST_HU
-#define GM_HIST_HU 2
-#endif
-    constexpr int HU = GM_HIST_HU;
+    constexpr int HU = 2;
+    const int drain_every = (int)(room / (HTPB * 2 * HU)) - 1;   // -1: the odd last row of block 0
     dv2 xa[HU], ya[HU];
     lv2 ta[HU];
-    int64_t p = (int64_t)blockIdx.x * HTPB + threadIdx.x;
+    const int64_t p0 = (int64_t)blockIdx.x * HTPB;
 #pragma unroll
     for (int u = 0; u < HU; ++u) {
-      const int64_t q = p + u * stride;
+      const int64_t q = p0 + threadIdx.x + u * stride;
       if (q < np) { xa[u] = ld_stream(&x2[q]); ya[u] = ld_stream(&y2[q]); ta[u] = ld_stream(&t2[q]); }
     }
-    while (p < np) {
-      const int64_t pn = p + HU * stride;
+    // the loop bound is the block's first pair, so every thread of the block runs the same iterations
+    // (the drains' barriers)
+    for (int64_t pb = p0; pb < np; pb += HU * stride) {
+      const int64_t p = pb + threadIdx.x, pn = p + HU * stride;
       dv2 xb[HU], yb[HU];
       lv2 tb[HU];
 #pragma unroll
@@ -226,23 +248,30 @@ __global__ __launch_bounds__(HTPB) void k_z3_hist_lds(const double* __restrict__
         if (p + u * stride < np) { one(xa[u].x, ya[u].x, ta[u].x); one(xa[u].y, ya[u].y, ta[u].y); }
         xa[u] = xb[u]; ya[u] = yb[u]; ta[u] = tb[u];
       }
-      p = pn;
+      if (WIDE && ++since == drain_every) { drain(true); since = 0; }
     }
     if ((a.n & 1) && blockIdx.x == 0 && threadIdx.x == 0) one(x[a.n - 1], y[a.n - 1], t[a.n - 1]);
   } else {
-    for (int64_t i = (int64_t)blockIdx.x * HTPB + threadIdx.x; i < a.n; i += stride) one(x[i], y[i], t[i]);
+    const int drain_every = (int)(room / HTPB);
+    for (int64_t ib = (int64_t)blockIdx.x * HTPB; ib < a.n; ib += stride) {
+      const int64_t i = ib + threadIdx.x;
+      if (i < a.n) one(x[i], y[i], t[i]);
+      if (WIDE && ++since == drain_every) { drain(true); since = 0; }
+    }
   }
   if (skip) atomicAdd(&s_skip, skip);
   if (out) atomicAdd(&s_out, out);
-  __syncthreads();
-  for (int i = threadIdx.x; i < total; i += HTPB) {
-    const int v = NARROW ? (int)((((uint32_t)cnt[i >> 1]) >> ((i & 1) * 16)) & 0xFFFFu) - (int)NB : cnt[i];
-    if (v) atomicAdd(&counts[i], (unsigned long long)(long long)v);
-  }
-  if (!UNOBS && !NARROW) {   // a row with a nonzero counter was seen by this workgroup
-    for (int i = threadIdx.x; i < total; i += HTPB)
-      if (cnt[i] && !pres[i / a.length]) pres[i / a.length] = 1;
+  if (WIDE) {
+    drain(false);
+  } else {
     __syncthreads();
+    for (int i = threadIdx.x; i < total; i += HTPB)
+      if (cnt[i]) atomicAdd(&counts[i], (unsigned long long)(long long)cnt[i]);
+    if (!UNOBS) {   // a row with a nonzero counter was seen by this workgroup
+      for (int i = threadIdx.x; i < total; i += HTPB)
+        if (cnt[i] && !pres[i / a.length]) pres[i / a.length] = 1;
+      __syncthreads();
+    }
   }
   if (!UNOBS) {
     for (int i = threadIdx.x; i < a.row_n; i += HTPB)
@@ -291,10 +320,16 @@ int launch_hist(gm_ctx* ctx, const double* x, const double* y, const int64_t* t,
   hipStream_t s = ctx->stream;
   // time-bin rows per LDS pass; every pass re-reads the 24 B/point, so more than HIST_MAX_PASSES
   // passes lose to the device-atomic kernel (measured: 2 LDS passes ~12 ms vs 45 ms atomics per 1B)
-  // 32-bit LDS counters when every time-bin row fits one pass, else 16-bit halves (NARROW)
+  // 32-bit LDS counters when every time-bin row fits one pass, else three 21-bit counters per 64-bit
+  // word (WIDE): rows of `length` counters in (HIST_WIDE_BYTES / 8) words
   const int rows32 = (HIST_LDS_MAX) / (a.length + 1);
   const bool narrow = rows32 < a.n_bins;
-  const int rows = narrow ? (int)((2 * (int64_t)HIST_LDS_MAX - 2) / (a.length + 2)) : rows32;
+  int rows = rows32;
+  if (narrow) {
+    auto bytes = [&](int64_t r) { return (r * a.length + 2) / 3 * 8 + r * 4; };
+    rows = (int)std::min<int64_t>(a.n_bins, HIST_WIDE_BYTES / (a.length * 8 / 3 + 4) + 1);
+    while (rows > 0 && bytes(rows) > HIST_WIDE_BYTES) --rows;
+  }
   const int passes = rows > 0 ? (a.n_bins + rows - 1) / rows : 1 << 30;
   if (passes <= HIST_MAX_PASSES) {
     const bool vec = aligned16(x) && aligned16(y) && aligned16(t);
@@ -304,14 +339,16 @@ int launch_hist(gm_ctx* ctx, const double* x, const double* y, const int64_t* t,
       a.row_lo = k * rows;
       a.row_n = std::min(rows, a.n_bins - a.row_lo);
       a.tally = k == 0;
-      const int64_t cwords = narrow ? ((int64_t)a.row_n * a.length + 1) / 2 : (int64_t)a.row_n * a.length;
-      const size_t lds = (size_t)(cwords + a.row_n + 2048) * sizeof(int);
+      const int64_t tot = (int64_t)a.row_n * a.length;
+      const int64_t cw64 = narrow ? (tot + 2) / 3 : (tot + 1) / 2;
+      const size_t lds = (size_t)cw64 * 8 + (size_t)(a.row_n + 2048) * sizeof(int);
       const int per_cu = lds <= 72 * 1024 ? 2 : 1;  // 2 x 1024 threads is the CU's wave limit
       // per workgroup <= 2^31 increments so the int32 LDS counters cannot wrap
       const int64_t need = (a.n + (int64_t)2147483647 - 1) / (int64_t)2147483647;
       const int64_t want = (a.n + HTPB - 1) / HTPB;
       int64_t grid = std::min<int64_t>((int64_t)cus * per_cu, std::max<int64_t>(want, 1));
       grid = std::max(grid, need);
+      if (ctx->hist_grid > 0) grid = std::max<int64_t>(ctx->hist_grid, need);   // GM_PARAM_HIST_GRID (drain tests)
       auto go = [&](auto kern) -> int {
         GM_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(HTPB), lds, s, x, y, t, a, present, counts, tally);

@@ -138,18 +138,6 @@ class PolygonIndex:
         check(self.ctx.lib.gm_pip_index_stats(self._h, st.ctypes.data), "gm_pip_index_stats")
         return dict(zip(["cells", "entries", "boundary", "records", "slow", "blob_bytes", "compact"], st.tolist()))
 
-    def core_rects(self):
-        """Diagnostic: the row predicate's core rectangles (gm_pip_index_core) as an (n, 4) uint16 array of
-        inclusive grid-cell boxes x0, y0, x1, y1 (x0 > x1: none); empty when no table was built."""
-        import numpy as np
-        n = ctypes.c_int32()
-        check(self.ctx.lib.gm_pip_index_core(self.ctx.handle, self._h, None, ctypes.byref(n)), "gm_pip_index_core")
-        r = np.zeros((n.value, 4), np.uint16)
-        if n.value:
-            check(self.ctx.lib.gm_pip_index_core(self.ctx.handle, self._h, r.ctypes.data, ctypes.byref(n)),
-                  "gm_pip_index_core")
-        return r
-
     CENSUS = ["points", "outside", "coarse_empty", "coarse_interior", "coarse_raw_mixed", "fine", "fine_empty",
               "fine_interior", "fine_line", "fine_compact", "fine_generic", "fine_list", "list_entries",
               "list_blobs", "line_resolved", "line_fallback", "fine_inline", "inline_fallback", "coarse_gather",

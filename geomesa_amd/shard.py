@@ -74,12 +74,12 @@ def broadcast_index(pg, index, src=0, ctx=None, reimport=False):
 
 
 def all_reduce_scalar(pg, v, op="max"):
-    """max / sum of one float over all ranks (identity without a process group)."""
+    """max / min / sum of one float over all ranks (identity without a process group)."""
     if pg is None:
         return float(v)
     import torch
     t = torch.tensor([float(v)], dtype=torch.float64, device=_device_of(pg))
-    pg.all_reduce(t, op={"max": pg.ReduceOp.MAX, "sum": pg.ReduceOp.SUM}[op])
+    pg.all_reduce(t, op={"max": pg.ReduceOp.MAX, "min": pg.ReduceOp.MIN, "sum": pg.ReduceOp.SUM}[op])
     return float(t.item())
 
 
@@ -129,6 +129,72 @@ def gather_rows(pg, cols, dst=0, loopback=False):
         for req in pg.batch_isend_irecv(ops):
             req.wait()
     return out if rank == dst else None
+
+
+# xGMI on MI355X: 7 point-to-point links per GPU, ~153 GB/s each (MI355X_MICROARCH.md); rank dst takes
+# every peer's rows at once, each over its own link, so a gather costs its largest peer's bytes / link
+XGMI_LINK_GBS = 153.0
+
+
+def gather_pairs_compact(pg, pt_ids, pl_ids, id_base, n_polys, dst=0, loopback=False):
+    """The join's result gather (GeoMesaJoinRelation.scala:41-91 leaves the pairs in the RDD's
+    partitions; here they come to rank `dst`) in a compact wire format: each rank's pairs travel as a
+    4-B shard-local row (point id - the rank's id_base) and a 2-B polygon id -- 6 B per pair instead of
+    12 -- and rank `dst` expands them to (int64 point id, int32 polygon id) in rank order, exactly the
+    pairs gather_rows would deliver.  The full 12-B format is used when some rank's rows do not fit 32
+    bits or there are more than 65,536 polygons.  Returns ((pt, pl), wire_bytes_per_rank) on `dst` and
+    (None, wire_bytes_per_rank) elsewhere; with pg None, ((pt_ids, pl_ids), [12 * n])."""
+    import torch
+    n = int(pt_ids.numel())
+    if pg is None:
+        return (pt_ids, pl_ids), [12 * n]
+    dev = _device_of(pg)
+    world, rank = pg.get_world_size(), pg.get_rank()
+    span = int((pt_ids.max() - id_base).item()) + 1 if n else 0
+    lo_ok = n == 0 or int(pt_ids.min().item()) >= id_base
+    mine = torch.tensor([n, int(id_base), int(span <= (1 << 32) and lo_ok)], dtype=torch.int64, device=dev)
+    allv = [torch.zeros_like(mine) for _ in range(world)]
+    pg.all_gather(allv, mine)
+    counts = [int(v[0].item()) for v in allv]
+    bases = [int(v[1].item()) for v in allv]
+    compact = n_polys <= (1 << 16) and all(int(v[2].item()) for v in allv)
+    if not compact:
+        g = gather_rows(pg, [pt_ids, pl_ids], dst, loopback)
+        return (tuple(g) if g is not None else None), [12 * c for c in counts]
+    # one byte buffer per rank -- [4-B rows | 2-B polygons | pad to 8 B] -- so a peer's pairs are one
+    # point-to-point message (RCCL moves no int16 tensors) and every segment stays 8-B aligned on dst
+    rows = (pt_ids - id_base).to(torch.int64)
+    rows = torch.where(rows >= (1 << 31), rows - (1 << 32), rows).to(torch.int32)    # the u32 bit pattern
+    polys = torch.where(pl_ids >= (1 << 15), pl_ids - (1 << 16), pl_ids).to(torch.int16)   # the u16 bit pattern
+    seg = lambda c: (6 * c + 7) // 8 * 8   # noqa: E731
+    buf = torch.zeros(seg(n), dtype=torch.uint8, device=pt_ids.device)
+    buf[:4 * n] = rows.view(torch.uint8)
+    buf[4 * n:6 * n] = polys.view(torch.uint8)
+    g = gather_rows(pg, [buf], dst, loopback)
+    if rank != dst:
+        return None, [6 * c for c in counts]
+    out, o = g[0], 0
+    rs, ps = [], []
+    for c in counts:
+        part = out[o:o + seg(c)]
+        rs.append(part[:4 * c].view(torch.int32))
+        ps.append(part[4 * c:6 * c].view(torch.int16))
+        o += seg(c)
+    r, p = torch.cat(rs), torch.cat(ps)
+    base = torch.repeat_interleave(torch.tensor(bases, dtype=torch.int64, device=dev),
+                                   torch.tensor(counts, dtype=torch.int64, device=dev))
+    pt = (r.to(torch.int64) & 0xFFFFFFFF) + base
+    pl = p.to(torch.int32) & 0xFFFF
+    return (pt, pl), [6 * c for c in counts]
+
+
+def gather_estimate_ms(wire_bytes, dst=0, hbm_gbs=5000.0):
+    """The gather's model time: the largest peer's bytes over one xGMI link (the peers send at once,
+    each on its own link), against rank dst's HBM writing every received byte; the larger of the two."""
+    peers = [b for r, b in enumerate(wire_bytes) if r != dst]
+    link = max(peers) / (XGMI_LINK_GBS * 1e9) * 1e3 if peers else 0.0
+    hbm = sum(peers) / (hbm_gbs * 1e9) * 1e3
+    return max(link, hbm)
 
 
 def merge_histograms(pg, counts, present, bin_lo, length=None):

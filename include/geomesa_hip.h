@@ -115,9 +115,9 @@ const char* gm_last_error(void);
                                    fewer than 2^14 polygons 8 sub-blocks with EMPTY and INTERIOR-of-one-
                                    polygon bits, else 16 EMPTY bits), 0 = EMPTY bits, 1 = EMPTY and
                                    INTERIOR bits.  Results never change */
-#define GM_PARAM_INDEX_CORE 7   /* 1 (default) = a built or imported polygon index carries the row
-                                   predicate's per-polygon core rectangles, 0 = none.  Results never
-                                   change */
+#define GM_PARAM_HIST_GRID 8    /* gm_z3_histogram: workgroups of the LDS-counter kernel (0 = default: one
+                                   resident wave of workgroups); fewer workgroups each count more features
+                                   and drain their packed counters more often.  Results never change */
 int gm_ctx_set_param(gm_ctx* ctx, int param, int64_t value);
 int gm_ctx_get_param(gm_ctx* ctx, int param, int64_t* value);
 /* device memory helpers for callers without their own allocator (e.g. a JNI shim) */
@@ -267,11 +267,6 @@ int gm_pip_index_destroy(gm_pip_index* index);
 /* index statistics: stats[0..6] = cells, (cell, polygon) entries, boundary entries, ring records,
    ring records that fall back to the slab walk, boundary blob bytes, compact (one-line) blobs */
 int gm_pip_index_stats(const gm_pip_index* index, int64_t* stats);
-/* Diagnostic (no reference counterpart): the row predicate's per-polygon core rectangles, grid
-   cells (x0, y0, x1, y1) inclusive whose cell words are all INTERIOR(p); x0 > x1 = none.  *n_core =
-   polygons with a table (0: none built, e.g. more polygons than gm_pip_relate's LDS table holds);
-   rects (4 * *n_core uint16, host memory) may be null. */
-int gm_pip_index_core(gm_ctx* ctx, const gm_pip_index* index, uint16_t* rects, int32_t* n_core);
 /* Diagnostic (no reference counterpart): how the join's lookup chain resolves the device points
    px / py, stage by stage -- counters[20] = points, outside the grid, coarse EMPTY, coarse INTERIOR,
    points in mixed coarse cells before the sub-block masks, fine lookups, fine EMPTY, fine INTERIOR,

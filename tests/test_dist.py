@@ -405,3 +405,55 @@ def test_gather_rows_exact_sizes(sizes, dst):
     assert ids.tolist() == [1000 * r + i for r in range(world) for i in range(sizes[r])]
     assert pl.tolist() == [r for r in range(world) for _ in range(sizes[r])]
     assert ids.dtype == np.int64 and pl.dtype == np.int32
+
+
+def _gcompact_worker(rank, world, port, sizes, n_polys, q):
+    sys.path.insert(0, ROOT)
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from geomesa_amd.shard import gather_pairs_compact
+        k = sizes[rank]
+        base = (3 << 32) + rank * ((1 << 32) + 17)      # each rank's first global row
+        g = torch.Generator().manual_seed(rank)
+        rows = torch.randint(0, 1 << 32, (k,), generator=g, dtype=torch.int64)
+        if k:
+            rows[0] = (1 << 32) - 1                      # the top of the u32 range (sign bit set on the wire)
+        pl = torch.randint(0, n_polys, (k,), generator=g, dtype=torch.int64).to(torch.int32)
+        if k:
+            pl[-1] = n_polys - 1
+        got, wire = gather_pairs_compact(dist, rows + base, pl, base, n_polys, dst=0)
+        q.put((rank, (rows + base).numpy(), pl.numpy(), None if got is None else (got[0].numpy(), got[1].numpy()), wire))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("sizes,n_polys", [((5, 0, 3000), 65536), ((0, 4, 2), 3200), ((100, 7, 0), 70000)])
+def test_gather_pairs_compact_round_trip(sizes, n_polys):
+    """The join's compact result gather (4-B shard-local rows + 2-B polygon ids on the wire, expanded on
+    rank 0) delivers exactly the (int64 point id, int32 polygon id) pairs of the full gather, in rank
+    order; past 65,536 polygons it falls back to the 12-B format."""
+    world = len(sizes)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gcompact_worker, args=(r, world, port, sizes, n_polys, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = {}
+    for _ in range(world):
+        r, ids, pl, g, wire = q.get(timeout=240)
+        got[r] = (ids, pl, g, wire)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    pt, pp = got[0][2]
+    assert pt.dtype == np.int64 and pp.dtype == np.int32
+    assert np.array_equal(pt, np.concatenate([got[r][0] for r in range(world)]))
+    assert np.array_equal(pp, np.concatenate([got[r][1] for r in range(world)]))
+    per = 6 if n_polys <= 65536 else 12
+    assert got[0][3] == [per * s for s in sizes]
+    assert all(got[r][2] is None for r in range(1, world))

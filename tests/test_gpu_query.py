@@ -46,7 +46,7 @@ def _points(n, seed, ps):
     return x, y, t
 
 
-@pytest.mark.parametrize("cells", [0, 1, 16, 65536])
+@pytest.mark.parametrize("cells", [0, 1, 16, 65536, 1 << 20])   # 1 << 20: a coarse table too large for LDS
 @pytest.mark.parametrize("op,oop", [("intersects", 1), ("contains", 2)])
 def test_query_scan_parity(gpu, oracle, cells, op, oop):
     from geomesa_amd import filters as F
@@ -112,3 +112,36 @@ def test_query_scan_empty(gpu):
     ps = PolygonSet.from_wkt([BOX])
     m, ids, nm = F.query_scan(np.zeros(0), np.zeros(0), geoms=ps, want_ids=True)
     assert nm == 0 and m.numel() == 0
+
+
+@pytest.mark.parametrize("cells", [4096, 65536])
+def test_query_scan_lobed_polygon_near_edges(gpu, oracle, cells):
+    """The bench's query geometry (1,024-vertex lobed ring with a 64-vertex hole) over points in its
+    envelope plus every vertex, every edge midpoint and points a hair off each vertex: the scan's lookup
+    chain (coarse sub-block masks, fine words with boundary shortcuts, line entries, compact and generic
+    blobs walked by the block) against the oracle's PointLocator, both predicates."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    from geomesa_amd import filters as F
+    from geomesa_amd.join import PolygonIndex
+    ps = bench.query_polygon()
+    ix = PolygonIndex(ps, cells_per_poly=cells)
+    ops = oracle.OraclePolySet(*ps.to_arrays())
+    rng = np.random.default_rng(cells)
+    x = [rng.uniform(-15, 35, 400_000)]
+    y = [rng.uniform(30, 64, 400_000)]
+    vx, vy = ps.vx, ps.vy
+    x += [vx, (vx[1:] + vx[:-1]) / 2]
+    y += [vy, (vy[1:] + vy[:-1]) / 2]
+    for eps in (1e-12, 1e-9, 1e-6, 1e-3):
+        for sx, sy in ((1, 0), (0, 1), (-1, -1), (1, -1)):
+            x.append(vx + sx * eps)
+            y.append(vy + sy * eps)
+    x, y = np.concatenate(x), np.concatenate(y)
+    for op, oop in (("intersects", 1), ("contains", 2)):
+        exp = oracle.query_scan(x, y, polys=ops, op=oop)
+        m, ids, nm = F.query_scan(x, y, geoms=ix, op=op, want_ids=True)
+        assert np.array_equal(as_np(m), exp), op
+        assert nm == int(exp.sum()) and np.array_equal(as_np(ids), np.nonzero(exp)[0])

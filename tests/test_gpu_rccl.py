@@ -59,6 +59,11 @@ def _rccl_worker(port, q):
         res["gather_device"] = str(g[0].device)
         g0 = S.gather_rows(dist, [pt[:0]], loopback=True)   # an empty rank: no point-to-point op
         res["gather_empty"] = int(g0[0].numel())
+        # the compact wire format (4-B rows + 2-B polygons through the same P2P group), expanded on rank 0
+        (ct, cl), wire = S.gather_pairs_compact(dist, pt, pl, 5, ix.polyset.n_polys, loopback=True)
+        res["compact_equal"] = bool(torch.equal(ct, pt) and torch.equal(cl, pl) and ct.dtype == torch.int64 and
+                                    cl.dtype == torch.int32)
+        res["compact_wire"] = wire == [6 * int(pt.numel())]
         # the key-range exchange step: all_to_all_single of the counts and of the packed records
         hi = torch.arange(1000, dtype=torch.int64, device="cuda") // 7
         lo = torch.arange(1000, dtype=torch.int64, device="cuda") * 3
@@ -103,6 +108,7 @@ def test_shard_plumbing_over_rccl_world1(gpu):
     assert res["backend"] == "nccl"
     assert res["reimported"] and res["broadcast_pairs_equal"] and res["pairs"] > 0
     assert res["gather_equal"] and res["gather_device"].startswith("cuda") and res["gather_empty"] == 0
+    assert res["compact_equal"] and res["compact_wire"]
     assert res["exchange_equal"] and res["exchange_world1"]
     assert res["max"] == 3.5 and res["sum"] == 2.0 and res["hist_ok"]
     assert res["ranges_equal"]
@@ -124,5 +130,6 @@ def test_bench_under_torchrun_world1(gpu):
     detail = json.loads([ln for ln in r.stderr.splitlines() if ln.startswith("BENCH_DETAIL ")][-1][13:])
     pj = detail["pip_join"]
     assert pj["gather"].get("pairs_on_rank0") == pj["matches"], pj["gather"]
+    assert pj["gather"].get("pairs_on_rank0_compact") == pj["matches"], pj["gather"]
     tq = detail["extra"]["table_query"]
     assert tq["parity"]["ids_equal"], tq["parity"]

@@ -109,7 +109,7 @@ def test_z3_histogram_top_bits_rounding(gpu, oracle, length):
 @pytest.mark.parametrize("length,lo,nb", [(1024, 2600, 53), (64, 2607, 4)])
 def test_z3_histogram_hot_counters(gpu, oracle, length, lo, nb):
     """8M features on 3 positions: tens of thousands of increments per counter per workgroup, past the
-    16-bit counters' spill threshold (length 1024 x 53 runs the NARROW path) and the int32 path."""
+    int32 path and the packed 21-bit counters (length 1024 x 53 runs the WIDE path)."""
     rng = np.random.default_rng(9)
     n = 8_000_000
     k = rng.integers(0, 3, n)
@@ -125,6 +125,54 @@ def test_z3_histogram_hot_counters(gpu, oracle, length, lo, nb):
     oracle.z3_histogram(x[:h], y[:h], t[:h], length, lo, nb, unobserve=True, period=WEEK, present=op, counts=oc,
                         tally=ot)
     assert np.array_equal(C2, oc) and np.array_equal(P2, op)
+
+
+@pytest.mark.parametrize("grid,length,nb,aligned", [(1, 1024, 53, True), (3, 1024, 53, True), (1, 2048, 54, True),
+                                                     (1, 1024, 53, False)])
+def test_z3_histogram_wide_counter_drains(gpu, oracle, grid, length, nb, aligned):
+    """The packed 21-bit LDS counters (WIDE: histograms past int32 LDS) drain to the device counters on a
+    fixed schedule so no field carries into its neighbour: with one or three workgroups
+    (GM_PARAM_HIST_GRID) every workgroup counts millions of features into three hot counters -- past
+    2^21 per field -- and drains many times; observe, then unobserve (fields biased at 2^20, drained
+    twice as often) of 6M of them, bit-exact against the oracle.  length 2048 x 54 takes two LDS passes;
+    an unaligned column takes the scalar loop."""
+    import torch
+    from geomesa_amd import _lib
+    rng = np.random.default_rng(12)
+    n = 8_000_001
+    k = rng.integers(0, 3, n)
+    x = np.array([10.0, -75.5, 139.7])[k]
+    y = np.array([47.0, 40.1, 35.6])[k]
+    t = np.array([T2020 + 5 * 86400000, T2020 + 5 * 86400000 + 1, T2020 + 9 * 86400000])[k]
+    if not aligned:   # an odd element in front: the columns' data start 8 B off the 16-B grid
+        x, y, t = (np.concatenate([v[:1], v]) for v in (x, y, t))
+    ctx = _lib.context()
+    ctx.set_param(_lib.GM_PARAM_HIST_GRID, grid)
+    try:
+        lo = 2600
+        sl = slice(1, None) if not aligned else slice(None)
+
+        def run(xs, ys, ts, unobs=False, P0=None, C0=None):
+            X, Y, T = (_dev(v, torch) for v in (xs, ys, ts))
+            if not aligned:
+                X, Y, T = X[1:], Y[1:], T[1:]
+            P = _dev(P0 if P0 is not None else np.zeros(nb, np.uint8), torch)
+            C = _dev(C0 if C0 is not None else np.zeros((nb, length), np.int64), torch)
+            tl = torch.zeros(2, dtype=torch.int64, device="cuda")
+            _lib.check(ctx.lib.gm_z3_histogram(ctx.handle, _lib.ptr(X), _lib.ptr(Y), _lib.ptr(T), X.numel(), WEEK, length,
+                                               int(unobs), lo, nb, _lib.ptr(P), _lib.ptr(C), _lib.ptr(tl)), "hist")
+            return P.cpu().numpy(), C.cpu().numpy(), tl.cpu().numpy()
+        P, C, tl = run(x, y, t)
+        op, oc, ot = oracle.z3_histogram(x[sl], y[sl], t[sl], length, lo, nb, period=WEEK)
+        assert np.array_equal(C, oc) and np.array_equal(P, op) and np.array_equal(tl, ot)
+        assert C.max() > (1 << 21)          # a field's worth, several times over, through one workgroup's drains
+        h = 6_000_000 + (0 if aligned else 1)
+        P2, C2, _ = run(x[:h], y[:h], t[:h], True, P, C)
+        oracle.z3_histogram(x[sl][:6_000_000], y[sl][:6_000_000], t[sl][:6_000_000], length, lo, nb, unobserve=True,
+                            period=WEEK, present=op, counts=oc, tally=ot)
+        assert np.array_equal(C2, oc) and np.array_equal(P2, op)
+    finally:
+        ctx.set_param(_lib.GM_PARAM_HIST_GRID, 0)
 
 
 def test_z3_histogram_unaligned_and_small(gpu, oracle):

@@ -11,7 +11,7 @@
 #   prof             rocprofv3 --kernel-trace --stats of the bench, then the FETCH_SIZE / WRITE_SIZE /
 #                    FP64 passes (one counter group per run) -> make_traffic.py input
 #   kstats:LEG       rocprofv3 --kernel-trace --stats of one leg (summary via tools/kstats.py)
-#   pmc:LEG          the counter groups below over one leg (join | table | ranges | hist | sort | z3)
+#   pmc:LEG          the counter groups below over one leg (join | table | ranges | hist | sort | z3 | xz | query)
 #   ab:LEG:LIBS      alternating runs of one leg over variant libraries (geomesa_amd/lib/<lib>.so,
 #                    comma-separated; "prod" = the product library), 3 rounds
 #   probe:NAME       python tools/NAME.py $PROBE_ARGS (ranges_probe, hist_probe, sort_probe, query_probe, ...)
@@ -81,6 +81,8 @@ for step in "$@"; do
       [ "$arg" = ranges ] && cmd="python3 tools/ranges_probe.py 100000"
       [ "$arg" = hist ] && cmd="python3 tools/hist_probe.py"
       [ "$arg" = sort ] && cmd="python3 tools/sort_probe.py"
+      [ "$arg" = xz ] && cmd="python3 tools/xz_probe.py"
+      [ "$arg" = query ] && cmd="python3 tools/query_probe.py"
       mkdir -p ${out}_pmc_$arg
       i=0
       for g in "${groups[@]}"; do
