@@ -328,43 +328,6 @@ __global__ __launch_bounds__(TPB) void k_xz2_index_v(const dv2* __restrict__ xmi
   }
 }
 
-// XZ2 index as a resident grid, software-pipelined: each lane's next pair is in flight while the
-// current one is keyed (the per-element divisions make the keying long enough to starve a one-shot
-// block of loads in flight)
-template <bool LENIENT, bool STATUS>
-__global__ __launch_bounds__(TPB) void k_xz2_index_p(const dv2* __restrict__ xmin, const dv2* __restrict__ ymin,
-                                                     const dv2* __restrict__ xmax, const dv2* __restrict__ ymax,
-                                                     int64_t n, int g, lv2* __restrict__ out,
-                                                     uchar2* __restrict__ status, int64_t* __restrict__ err) {
-  const int64_t np = n >> 1, stride = (int64_t)gridDim.x * TPB;
-  int64_t p = (int64_t)blockIdx.x * TPB + threadIdx.x;
-  dv2 a = {0.0, 0.0}, b = a, c = a, d = a;
-  if (p < np) { a = ld_stream(&xmin[p]); b = ld_stream(&ymin[p]); c = ld_stream(&xmax[p]); d = ld_stream(&ymax[p]); }
-  while (p < np) {
-    const int64_t q = p + stride;
-    dv2 a2 = {0.0, 0.0}, b2 = a2, c2 = a2, d2 = a2;
-    if (q < np) { a2 = ld_stream(&xmin[q]); b2 = ld_stream(&ymin[q]); c2 = ld_stream(&xmax[q]); d2 = ld_stream(&ymax[q]); }
-    int64_t o0, o1;
-    const uint8_t s0 = xz2_one<LENIENT>(g, a.x, b.x, c.x, d.x, o0);
-    const uint8_t s1 = xz2_one<LENIENT>(g, a.y, b.y, c.y, d.y, o1);
-    st_stream(lv2{o0, o1}, &out[p]);
-    if (STATUS) status[p] = make_uchar2(s0, s1);
-    if (s0) report_error(err, 2 * p, s0);
-    if (s1) report_error(err, 2 * p + 1, s1);
-    a = a2; b = b2; c = c2; d = d2;
-    p = q;
-  }
-  if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
-    const int64_t i = n - 1;
-    int64_t o;
-    const uint8_t s = xz2_one<LENIENT>(g, ((const double*)xmin)[i], ((const double*)ymin)[i],
-                                       ((const double*)xmax)[i], ((const double*)ymax)[i], o);
-    ((int64_t*)out)[i] = o;
-    if (STATUS) ((uint8_t*)status)[i] = s;
-    if (s) report_error(err, i, s);
-  }
-}
-
 template <bool LENIENT, bool STATUS, int UNROLL>
 __global__ __launch_bounds__(TPB) void k_xz3_index_v(const dv2* __restrict__ xmin, const dv2* __restrict__ ymin,
                                                      const dv2* __restrict__ zmin, const dv2* __restrict__ xmax,
@@ -617,14 +580,8 @@ int gm_xz2_index(gm_ctx* ctx, const double* xmin, const double* ymin, const doub
       if (status) hipLaunchKernelGGL((k_xz2_index_v<true, true, UNROLL_XZ>), dim3(vg), dim3(TPB), 0, s, a, b, c, d, n, g, o, st, ctx->d_err);
       else hipLaunchKernelGGL((k_xz2_index_v<true, false, UNROLL_XZ>), dim3(vg), dim3(TPB), 0, s, a, b, c, d, n, g, o, st, ctx->d_err);
     } else {
-#ifdef GM_TMP_XZ_PIPE
-      const unsigned pg = (unsigned)std::min<int64_t>(vg, resident_blocks((const void*)k_xz2_index_p<false, false>, ctx->device, TPB, 1) * GM_TMP_XZ_PIPE);
-      if (status) hipLaunchKernelGGL((k_xz2_index_p<false, true>), dim3(pg), dim3(TPB), 0, s, a, b, c, d, n, g, o, st, ctx->d_err);
-      else hipLaunchKernelGGL((k_xz2_index_p<false, false>), dim3(pg), dim3(TPB), 0, s, a, b, c, d, n, g, o, st, ctx->d_err);
-#else
       if (status) hipLaunchKernelGGL((k_xz2_index_v<false, true, UNROLL_XZ>), dim3(vg), dim3(TPB), 0, s, a, b, c, d, n, g, o, st, ctx->d_err);
       else hipLaunchKernelGGL((k_xz2_index_v<false, false, UNROLL_XZ>), dim3(vg), dim3(TPB), 0, s, a, b, c, d, n, g, o, st, ctx->d_err);
-#endif
     }
   } else if (lenient) {
     if (status) hipLaunchKernelGGL((k_xz2_index<true, true>), dim3(grid), dim3(TPB), 0, s, xmin, ymin, xmax, ymax, n, g, out, status, ctx->d_err);

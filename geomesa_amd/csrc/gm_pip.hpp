@@ -451,35 +451,6 @@ __device__ __forceinline__ uint32_t coarse_mask(uint32_t w, int cx, int cy, int3
   return ((w >> sub) & 1u) ? (CELL_EMPTY << 30) : w;
 }
 
-// a point's position inside its cell (cx, cy) in cell units, as the shortcut tests take it; a kernel
-// may keep it in float (|error| <= 2^-25 cell, so |delta f| <= (|A| + |B|) 2^-25 <= 2^-10 units of the
-// lines' 2^-14 cell: far inside the SC_T - SC_DEV = 2 units the line decision keeps in hand)
-__device__ __forceinline__ double cell_u(double x, const PipDev& d, int cx) {
-  return __dsub_rn(__dmul_rn(__dsub_rn(x, d.gx0), d.inv_cw), (double)cx);
-}
-__device__ __forceinline__ double cell_v(double y, const PipDev& d, int cy) {
-  return __dsub_rn(__dmul_rn(__dsub_rn(y, d.gy0), d.inv_ch), (double)cy);
-}
-// line_locate from the in-cell position (u, v)
-__device__ __forceinline__ int line_locate_uv(const uint4 e0, const uint4 e1, double u, double v) {
-  auto f = [&](uint32_t ab, uint32_t c) -> double {
-    const double A = (double)(int16_t)(ab & 0xffffu), B = (double)(int16_t)(ab >> 16);
-    const double C = (double)((int32_t)(c << 8) >> 8);
-    return __dsub_rn(__dadd_rn(__dmul_rn(A, u), __dmul_rn(B, v)), C);
-  };
-  const double g1 = f(e0.z, e0.w);
-  if (!(g1 > SC_T || g1 < -SC_T)) return -1;
-  uint32_t r = g1 > SC_T ? 0u : 1u;
-  if ((e1.y >> 24) > 1) {
-    const double g2 = f(e1.x, e1.y);
-    if (!(g2 > SC_T || g2 < -SC_T)) return -1;
-    r |= g2 > SC_T ? 0u : 2u;
-  }
-  const uint32_t fl = e0.w >> 24;
-  if (!((fl >> (2 * r)) & 1u)) return -1;
-  return ((fl >> (2 * r + 1)) & 1u) ? LOC_INTERIOR : LOC_EXTERIOR;
-}
-
 // PointLocator's location of a point for one BOUNDARY item (ref = the word's payload): a line
 // shortcut (near the line: the entry's own blob), a compact blob or a generic blob.  LEAN: the compact
 // blob one 16-B load at a time (compact_locate_lean)
@@ -522,11 +493,8 @@ constexpr int ICAP = 128;              // item queue (two ends)
 constexpr int JQ_WAVE_LDS = FCAP * 20 + ICAP * 24;
 constexpr int CM_WORDS_MAX = (163840 - (QTPB / 64) * JQ_WAVE_LDS - 256) / 4;   // 13,248 words at 1024 threads
 
-// The row predicate (gm_pip_relate.hip): one 1024-thread block per CU, per wave a fine queue and an
-// item queue of 20-B entries (a row's fine cell or reference, its in-cell position in float, row and
-// polygon), beside the join's coarse EMPTY bitmap (cm, CM_WORDS_MAX words).
-constexpr int RFCAP = FBATCH + 128, RICAP = 128;
-static_assert((GM_JQ_TPB / 64) * 20 * (RFCAP + RICAP) + 4 * CM_WORDS_MAX + 256 <= 163840, "row predicate LDS");
+// The row predicate (gm_pip_relate.hip): one 1024-thread block per CU whose item queues leave room
+// for the join's coarse EMPTY bitmap (cm, CM_WORDS_MAX words).
 #ifndef GM_RELATE_TPB
 #define GM_RELATE_TPB 1024
 #endif

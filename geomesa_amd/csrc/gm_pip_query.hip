@@ -50,17 +50,12 @@ __device__ __forceinline__ bool entry_pred(const PipDev& d, uint32_t e, double p
 //     segments decides from its 32-B line entry (item_locate), only a row near a line or in a cell the
 //     shortcuts left walks its blob; a multi-polygon list tests its entries.
 // Block shape: FROWS = 4096 rows per block (the shared mask / count / compaction layout) as TPB threads
-// x 2 NP rows.  Without a geometry term 256 x 16 rows (the strict scan's shape).  With one, TPB x 2 NP
-// = GM_QUERY_TPB x ...: the lookup chain's per-row state (coarse and fine cells, words) shrinks with NP,
-// so the kernel holds fewer VGPRs and more waves hide the chain's L2 round trips behind other waves'
-// streams.
+// x 2 NP rows; 256 x 16 rows by default.  Fewer rows per lane with a geometry term hold fewer VGPRs
+// (512 threads: 85 instead of 110) but the wave then waits for its few lookups every 8 rows instead of
+// every 16: measured slower (GM_QUERY_TPB, profiles/r5/query_block_shape_ab.txt).
 #ifndef GM_QUERY_TPB
-#define GM_QUERY_TPB 512
+#define GM_QUERY_TPB 256   // 256 / 512 / 1024: 2.76 / 4.04 / 5.11 ms per 1B rows (profiles/r5/query_block_shape_ab.txt)
 #endif
-#ifndef GM_QUERY_COARSE_LDS
-#define GM_QUERY_COARSE_LDS 4096
-#endif
-constexpr int QCOARSE_LDS = GM_QUERY_COARSE_LDS;   // coarse words staged in LDS (16 KB)
 template <int OP>
 struct QueryShape {
   static constexpr int TPB = OP == SP_NONE ? FTPB : GM_QUERY_TPB;
@@ -103,15 +98,6 @@ __global__ __launch_bounds__(QueryShape<OP>::TPB) void k_query_mask(const double
       if (DURING) tv[u].x = t[2 * p];
     }
   }
-  // a query-sized index's whole coarse table (<= QCOARSE_LDS words: a polygon's 65,536-cell index has
-  // 1,024) staged in LDS while the rows load: its lookups cost an LDS read instead of an L2 round trip
-  __shared__ uint32_t s_coarse[OP == SP_NONE ? 1 : QCOARSE_LDS];
-  const int64_t ncoarse = (int64_t)d.gxc * ((d.gy + (1 << CF_LOG) - 1) >> CF_LOG);
-  const bool coarse_lds = OP != SP_NONE && ncoarse <= QCOARSE_LDS;
-  if (coarse_lds) {
-    for (int i = threadIdx.x; i < ncoarse; i += TPB) s_coarse[i] = d.coarse_sc[i];
-    __syncthreads();
-  }
   uint32_t pass = 0;
   int fc[R], cc[R];   // fine / coarse cell of each row (geometry term only)
   auto cheap = [&](double px, double py, int64_t tt, int k) {
@@ -136,8 +122,7 @@ __global__ __launch_bounds__(QueryShape<OP>::TPB) void k_query_mask(const double
   if (OP != SP_NONE && pass) {
     uint32_t cw[R];
 #pragma unroll
-    for (int k = 0; k < R; ++k)
-      cw[k] = ((pass >> k) & 1u) ? (coarse_lds ? s_coarse[cc[k] & 0x3ffffff] : d.coarse_sc[cc[k] & 0x3ffffff]) : (CELL_EMPTY << 30);
+    for (int k = 0; k < R; ++k) cw[k] = ((pass >> k) & 1u) ? d.coarse_sc[cc[k] & 0x3ffffff] : (CELL_EMPTY << 30);
 #pragma unroll
     for (int k = 0; k < R; ++k) {
       const uint32_t sb = (uint32_t)cc[k] >> 26;

@@ -193,229 +193,6 @@ __global__ __launch_bounds__(RTPB) void k_pip_relate(const int32_t* __restrict__
   }
 }
 
-// ------------------------------------------------------------------ staged row predicate
-// The row-wise predicate as the join's staged pass (k_pip_join_q): per wave, a stream step of 128 rows
-// (2 per lane: the polygon ids, x and y as 8- / 16-B loads) answers every row its coarse word decides
-// (EMPTY bitmap in LDS, then the L2-resident coarse table: EMPTY, INTERIOR(q) -> q == p, sub-block
-// masks) and queues the rest in the fine queue (fine cell, in-cell position in float, row, polygon); a
-// fine round takes 64 of them -- one full-wave gather of their 4-B fine words (cell_sc) instead of the
-// handful of lanes a step has -- and resolves them the next loop trip: INTERIOR / EMPTY, a list searched
-// for the row's polygon, or an item (a line entry, decided from the float position, or a blob, walked
-// with the row's exact point read again).  Stages run by priority from one loop (items, pending fine
-// words, fine rounds, the stream) so every queue stays bounded: the item queue holds < 64 before a push of
-// <= 64 (a line round hands back at most what it took), the fine queue < 64 before a stream step's <= 128.
-// Rows are chunk-relative (32-bit); every row's location is written exactly once.
-template <bool VEC>
-__global__ __launch_bounds__(RTPB) void k_pip_relate_q(const int32_t* __restrict__ poly, const double* __restrict__ px,
-                                                       const double* __restrict__ py, int64_t n, int32_t n_polys,
-                                                       PipDev d, const int32_t* __restrict__ list_poly,
-                                                       uint8_t* __restrict__ loc) {
-  constexpr int NW = RTPB / 64;
-  __shared__ uint32_t s_fc[NW][RFCAP], s_frow[NW][RFCAP];
-  __shared__ int32_t s_fp[NW][RFCAP];
-  __shared__ float s_fu[NW][RFCAP], s_fv[NW][RFCAP];
-  __shared__ uint32_t s_iref[NW][RICAP], s_irow[NW][RICAP];
-  __shared__ int32_t s_ip[NW][RICAP];
-  __shared__ float s_iu[NW][RICAP], s_iv[NW][RICAP];
-  __shared__ uint32_t s_cm[CM_WORDS_MAX];
-  const int64_t cm_words = d.cm_words <= CM_WORDS_MAX ? d.cm_words : 0;
-  for (int64_t i = threadIdx.x; i < cm_words; i += RTPB) s_cm[i] = d.cm[i];
-  __syncthreads();
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  uint32_t* fc = s_fc[wv]; uint32_t* frow = s_frow[wv]; int32_t* fp = s_fp[wv]; float* fu = s_fu[wv]; float* fv = s_fv[wv];
-  uint32_t* iref = s_iref[wv]; uint32_t* irow = s_irow[wv]; int32_t* ip = s_ip[wv]; float* iu = s_iu[wv]; float* iv = s_iv[wv];
-  int fn = 0, qn = 0, qg = 0;   // wave-uniform fills: fine queue, line items (from 0 up), blob items (from RICAP - 1 down)
-  const bool lines_on = d.line_ent != nullptr;
-
-  auto item_push = [&](bool valid, bool is_line, float u, float v, uint32_t row, int32_t p, uint32_t ref) __attribute__((always_inline)) {
-    const uint64_t ml = __ballot(valid && is_line), mb = __ballot(valid && !is_line);
-    if (!(ml | mb)) return;
-    if (GM_REF_BAD(qn + qg + 64 > RICAP)) { if (lane == 0) pip_fault(d, PIP_FAULT_QUEUE); return; }   // cannot happen: < 64 here
-    if (valid) {
-      const int o = is_line ? qn + lanes_below(ml) : RICAP - 1 - qg - lanes_below(mb);
-      iu[o] = u; iv[o] = v; irow[o] = row; ip[o] = p; iref[o] = ref;
-    }
-    qn += __popcll(ml);
-    qg += __popcll(mb);
-  };
-
-  // stream: step k covers rows [128 k, 128 k + 128) of the chunk, 2 per lane
-  const int64_t nstep = (n + 127) >> 7;
-  const int64_t wstride = (int64_t)gridDim.x * NW;
-  int64_t step = (int64_t)blockIdx.x * NW + wv;
-  int pb = 0, pc = 0;          // the pending fine window [pb, pb + pc) of the fine queue
-  bool pend = false;
-  uint32_t pend_w = CELL_EMPTY << 30;
-
-  for (;;) {
-    const bool idle = !pend && fn == 0 && step >= nstep;
-    if (qn + qg >= 64 || (idle && qn + qg > 0)) {   // ---- items: one round of the fuller kind
-      wave_lds_sync();
-      const bool lines = qn >= qg;
-      const int kq = min(lines ? qn : qg, 64);
-      const int slot = lines ? qn - kq + lane : RICAP - qg + lane;
-      const bool act = lane < kq;
-      float u = 0.0f, v = 0.0f;
-      uint32_t row = 0, ref = 0;
-      int32_t p = -1;
-      if (act) { u = iu[slot]; v = iv[slot]; row = irow[slot]; p = ip[slot]; ref = iref[slot]; }
-      wave_lds_sync();
-      if (lines) qn -= kq;
-      else qg -= kq;
-      if (lines) {
-        int l = -1;
-        uint32_t blob = 0;
-        int pl = -1;
-        if (act) {
-          const uint64_t li = ref & (SC_LINE - 1);
-          if (GM_REF_BAD(li >= (uint64_t)d.n_line)) { pip_fault(d, PIP_FAULT_LINE); l = LOC_EXTERIOR; }
-          else {
-            const uint4 e0 = d.line_ent[2 * li], e1 = d.line_ent[2 * li + 1];
-            pl = (int)e0.y;
-            l = line_locate_uv(e0, e1, (double)u, (double)v);
-            blob = e0.x & 0x3fffffffu;
-          }
-          if (l >= 0) loc[row] = (uint8_t)(pl == p ? l : LOC_EXTERIOR);
-        }
-        // near a line: the entry's own blob, as a blob item (fits: at most kq were taken)
-        const bool fb = act && l < 0;
-        const uint64_t mb = __ballot(fb);
-        if (fb) {
-          const int o = RICAP - 1 - qg - lanes_below(mb);
-          irow[o] = row; ip[o] = p; iref[o] = blob;
-        }
-        qg += __popcll(mb);
-      } else if (act) {
-        const double x = px[row], y = py[row];   // the row's exact point, read again
-        int pl = -1;
-        const int l = item_locate<true>(d, ref, x, y, pl);
-        loc[row] = (uint8_t)(pl == p ? l : LOC_EXTERIOR);
-      }
-      continue;
-    }
-    if (pend) {   // ---- resolve the pending fine window
-      const int slot = pb + lane;
-      const bool act = lane < pc;
-      pend = false;
-      uint32_t e = act ? pend_w : (CELL_EMPTY << 30);
-      uint32_t row = 0;
-      int32_t p = -1;
-      float u = 0.0f, v = 0.0f;
-      if (act) { row = frow[slot]; p = fp[slot]; u = fu[slot]; v = fv[slot]; }
-      fn = pb;   // the window is released
-      uint32_t kind = e >> 30;
-      int out = -1;   // a location decided here
-      if (kind == CELL_INTERIOR) out = (int)(e & 0x3fffffffu) == p ? LOC_INTERIOR : LOC_EXTERIOR;
-      else if (kind == CELL_EMPTY) out = LOC_EXTERIOR;
-      else if (kind == CELL_LIST) {   // the row's polygon in the cell's list
-        int l0 = 4 * (int)((e & 0x3fffffffu) >> 4), ni = (int)(e & 15u);
-        bool found = false;
-        if (GM_REF_BAD((int64_t)l0 + 4 > d.n_list)) { pip_fault(d, PIP_FAULT_LIST); ni = 0; }
-        else if (ni <= 4) {   // one 16-B group: its polygon ids and entries in two independent loads
-          const int4 lp = *(const int4*)(list_poly + l0);
-          const uint4 le = *(const uint4*)(d.list_ent + l0);
-          found = true;
-          if (ni > 0 && lp.x == p) e = le.x;
-          else if (ni > 1 && lp.y == p) e = le.y;
-          else if (ni > 2 && lp.z == p) e = le.z;
-          else if (ni > 3 && lp.w == p) e = le.w;
-          else found = false;
-          ni = 0;
-        } else if (ni == LIST_LONG) { ni = (int)d.list_ent[l0]; l0 += 1; }
-        if (GM_REF_BAD(ni < 0 || (int64_t)l0 + ni > d.n_list)) { pip_fault(d, PIP_FAULT_LIST); ni = 0; }
-        int j = 0;
-        while (j < ni && list_poly[l0 + j] != p) ++j;
-        if (j < ni) { e = d.list_ent[l0 + j]; found = true; }
-        if (!found) out = LOC_EXTERIOR;
-        else if ((e >> 30) == CELL_INTERIOR) out = LOC_INTERIOR;
-        else kind = CELL_BOUNDARY;   // the entry's blob (its polygon is p)
-      }
-      if (act && out >= 0) loc[row] = (uint8_t)out;
-      const bool item = act && out < 0 && kind == CELL_BOUNDARY;
-      const uint32_t ref = e & 0x3fffffffu;
-      item_push(item, item && lines_on && (ref & (BLOB_COMPACT | SC_LINE)) == (BLOB_COMPACT | SC_LINE), u, v, row, p, ref);
-      continue;
-    }
-    const bool streaming = step < nstep;
-    if (fn >= FBATCH || (!streaming && fn > 0)) {   // ---- fine round: the newest min(fn, 64) rows
-      wave_lds_sync();
-      const int cnt = min(fn, FBATCH);
-      const int a = fn - cnt + lane;
-      pend_w = CELL_EMPTY << 30;
-      if (lane < cnt) pend_w = d.cell_sc[fc[a]];
-      pb = fn - cnt;
-      pc = cnt;
-      pend = true;
-      continue;
-    }
-    if (streaming) {   // ---- stream step: 2 rows per lane
-      const int64_t r0 = 2 * (step * 64 + lane);
-      int32_t p[2] = {-1, -1};
-      double x[2] = {0.0, 0.0}, y[2] = {0.0, 0.0};
-      if (VEC && r0 + 1 < n) {
-        const uint64_t pp = __builtin_nontemporal_load((const uint64_t*)(poly + r0));
-        const dv2 a = __builtin_nontemporal_load((const dv2*)(px + r0));
-        const dv2 b = __builtin_nontemporal_load((const dv2*)(py + r0));
-        p[0] = (int32_t)(uint32_t)pp; p[1] = (int32_t)(uint32_t)(pp >> 32); x[0] = a.x; x[1] = a.y; y[0] = b.x; y[1] = b.y;
-      } else {
-#pragma unroll
-        for (int u = 0; u < 2; ++u)
-          if (r0 + u < n) { p[u] = poly[r0 + u]; x[u] = px[r0 + u]; y[u] = py[r0 + u]; }
-      }
-      int out[2];
-      uint32_t w[2];
-      int cx[2] = {0, 0}, cy[2] = {0, 0};
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        w[u] = CELL_EMPTY << 30;
-        const bool valid = r0 + u < n && p[u] >= 0 && p[u] < n_polys;
-        out[u] = r0 + u < n ? (valid ? LOC_EXTERIOR : (int)LOC_NULL) : -2;   // -2: no row
-        if (valid && x[u] >= d.gx0 && x[u] <= d.gx1 && y[u] >= d.gy0 && y[u] <= d.gy1) {   // NaN fails
-          cx[u] = cell_of(x[u], d.gx0, d.inv_cw, d.gx);
-          cy[u] = cell_of(y[u], d.gy0, d.inv_ch, d.gy);
-          bool empty = false;
-          if (cm_words) {
-            const int b = ((cy[u] >> CF_LOG) >> d.cm_shift_y) * d.cm_w + ((cx[u] >> CF_LOG) >> d.cm_shift);
-            empty = (s_cm[b >> 5] >> (b & 31)) & 1u;
-          }
-          if (!empty) w[u] = d.coarse_sc[(int64_t)(cy[u] >> CF_LOG) * d.gxc + (cx[u] >> CF_LOG)];
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        w[u] = coarse_mask(w[u], cx[u], cy[u], d.coarse_fmt);
-        if ((w[u] >> 30) == CELL_INTERIOR) out[u] = (int)(w[u] & 0x3fffffffu) == p[u] ? LOC_INTERIOR : LOC_EXTERIOR;
-        else if ((w[u] >> 30) == CELL_LIST) out[u] = -1;   // the fine queue decides
-      }
-      if (VEC && out[0] >= 0 && out[1] >= 0) *(uint16_t*)(loc + r0) = (uint16_t)(out[0] | (out[1] << 8));
-      else {
-#pragma unroll
-        for (int u = 0; u < 2; ++u)
-          if (out[u] >= 0) loc[r0 + u] = (uint8_t)out[u];
-      }
-      // rows of mixed coarse cells: the fine queue (< 64 queued here, so 128 more fit)
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const bool q = out[u] == -1;
-        const uint64_t m = __ballot(q);
-        if (GM_REF_BAD(fn + 64 > RFCAP)) { if (lane == 0 && m) pip_fault(d, PIP_FAULT_QUEUE); continue; }   // cannot happen
-        if (q) {
-          const int o = fn + lanes_below(m);
-          fc[o] = (uint32_t)cy[u] * (uint32_t)d.gx + (uint32_t)cx[u];
-          fu[o] = (float)cell_u(x[u], d, cx[u]);
-          fv[o] = (float)cell_v(y[u], d, cy[u]);
-          frow[o] = (uint32_t)(r0 + u);
-          fp[o] = p[u];
-        }
-        fn += __popcll(m);
-      }
-      step += wstride;
-      continue;
-    }
-    break;   // every stage idle and the item queue drained
-  }
-}
-
 }  // namespace gm
 
 using namespace gm;
@@ -431,7 +208,6 @@ int gm_pip_relate(gm_ctx* ctx, const gm_pip_index* ix, const int32_t* poly, cons
   PipDev dv = ix->dev;
   dv.fault = (uint32_t*)(ctx->d_scratch + SCRATCH_FAULT);   // sticky reference checks, as the join's
   note_fault_call(ctx, FC_RELATE);
-#ifdef GM_TMP_RELATE_OLD
   const bool vec = RILP == 2 && ((uintptr_t)px | (uintptr_t)py) % 16 == 0 && (uintptr_t)poly % 8 == 0 &&
                    (uintptr_t)loc % 2 == 0;
   auto* kern = vec ? k_pip_relate<RILP == 2> : k_pip_relate<false>;
@@ -439,23 +215,6 @@ int gm_pip_relate(gm_ctx* ctx, const gm_pip_index* ix, const int32_t* poly, cons
                                                                           (n + RTPB * RILP - 1) / (RTPB * RILP)));
   hipLaunchKernelGGL(kern, dim3(grid), dim3(RTPB), 0, ctx->stream, poly, px, py, n, ix->n_polys, dv, ix->list_poly, loc);
   GM_CHECK_LAUNCH();
-#else
-  // chunks of 2^31 rows (32-bit rows in the queues); chunks start at even rows so aligned columns stay
-  // aligned
-  const int64_t CHUNK = (int64_t)1 << 31;
-  for (int64_t c0 = 0; c0 < n; c0 += CHUNK) {
-    const int64_t m = std::min(CHUNK, n - c0);
-    const bool vec = ((uintptr_t)(px + c0) | (uintptr_t)(py + c0)) % 16 == 0 && (uintptr_t)(poly + c0) % 8 == 0 &&
-                     (uintptr_t)(loc + c0) % 2 == 0;
-    auto* kern = vec ? k_pip_relate_q<true> : k_pip_relate_q<false>;
-    const int64_t steps = (m + 127) / 128;
-    const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(resident_blocks((const void*)kern, ctx->device, RTPB, 1),
-                                                                            (steps + RTPB / 64 - 1) / (RTPB / 64)));
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(RTPB), 0, ctx->stream, poly + c0, px + c0, py + c0, m, ix->n_polys, dv,
-                       ix->list_poly, loc + c0);
-    GM_CHECK_LAUNCH();
-  }
-#endif
   return GM_OK;
 }
 

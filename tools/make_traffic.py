@@ -24,6 +24,8 @@ STREAMING = {
     "z2_invert": ("k_z2_invert<", "points", 24.0),
     "z3filter_scan": ("k_z3filter_mask_v", "points", 10.125),
     "xz2_index": ("k_xz2_index_v", "xz", 40.0),
+    "xz3_index": ("k_xz3_index_v", "xz", 56.0),
+    "query_scan_polygon": ("k_query_mask<true, false, 1>", "points", 16.125),
     "z3_histogram": ("k_z3_hist_lds<", "points", 24.0),
     "pip_relate": ("k_pip_relate", "points", 21.0),
     "sort_count": ("k_sort_count<", "rows", 10.0),
