@@ -44,6 +44,12 @@ for step in "$@"; do
         > ${out}_tests.log 2>&1 ;;
     smoke)
       timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > ${out}_smoke.log 2>&1 ;;
+    n2)   # the N > 1 paths with two ranks on the box's one GPU and gloo collectives (reduced sizes)
+      GM_BENCH_DEVICE=0 GM_BENCH_BACKEND=gloo timeout -k 10 900 python -m torch.distributed.run --nnodes=1 \
+        --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 2 --steps 3 --warmup 1 \
+        --join-steps 2 --points 250000000 --join-points 250000000 --table-rows 100000000 \
+        > ${out}_n2.json 2> ${out}_n2.err
+      cp gpurun_out/bench_detail_n2.json ${out}_n2_detail.json ;;
     bench)
       timeout -k 10 600 python -u bench.py > ${out}_bench.json 2> ${out}_bench.err
       cp gpurun_out/bench_detail_n1.json ${out}_bench_detail.json ;;
