@@ -196,3 +196,28 @@ def test_relate_unaligned_and_odd_rows(gpu):
     assert np.array_equal(shifted, full[1:])
     odd = as_np(ix.relate(poly[:12_345], px[:12_345], py[:12_345]))
     assert np.array_equal(odd, full[:12_345])
+
+
+@pytest.mark.parametrize("cells", [0, 64, 16384])
+def test_relate_and_join_lattice_exact(gpu, cells):
+    """The kernels against exact rational arithmetic (tests/test_oracle_exact.py): lattice polygons
+    with holes and MultiPolygon parts sharing an edge / a vertex, every lattice point on multiples of
+    1/8 -- thousands exactly on edges and vertices.  Row predicate: the location per row; join: the
+    st_contains pairs."""
+    from geomesa_amd.join import PolygonIndex, PolygonSet
+    from test_oracle_exact import LATTICE, _locate_exact, lattice_polys
+    polys = lattice_polys()
+    ps = PolygonSet.from_polygons(polys)
+    gx, gy = np.meshgrid(LATTICE, LATTICE)
+    px, py = gx.ravel().copy(), gy.ravel().copy()
+    exp = np.array([[_locate_exact(parts, float(x), float(y)) for x, y in zip(px, py)] for parts in polys], np.uint8)
+    ix = PolygonIndex(ps, cells_per_poly=cells)
+    n = len(px)
+    poly = np.repeat(np.arange(len(polys), dtype=np.int32), n)
+    loc = as_np(ix.relate(poly, np.tile(px, len(polys)), np.tile(py, len(polys))))
+    assert np.array_equal(loc, exp.ravel()), np.flatnonzero(loc != exp.ravel())[:10]
+    pt, pl = ix.join(px, py)
+    got = set(zip(as_np(pt).tolist(), as_np(pl).tolist()))
+    want = {(i, p) for p in range(len(polys)) for i in np.flatnonzero(exp[p] == 2).tolist()}
+    assert got == want
+    assert (exp == 1).sum() > 300
