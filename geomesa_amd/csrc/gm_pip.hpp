@@ -77,6 +77,10 @@ struct PipDev {
   const uint32_t* cm;
   int32_t cm_shift, cm_shift_y, cm_w;
   int64_t cm_words;
+  // the same bitmap at the row predicate's resolution (RM_WORDS_MAX: what its 32-bit-row queues leave)
+  const uint32_t* rm;
+  int32_t rm_shift, rm_shift_y, rm_w;
+  int64_t rm_words;
 };
 
 enum : uint32_t { PIP_FAULT_LINE = 1, PIP_FAULT_COMPACT = 2, PIP_FAULT_BLOB = 4, PIP_FAULT_LIST = 8, PIP_FAULT_QUEUE = 16 };
@@ -494,11 +498,15 @@ constexpr int JQ_WAVE_LDS = FCAP * 20 + ICAP * 24;
 constexpr int CM_WORDS_MAX = (163840 - (QTPB / 64) * JQ_WAVE_LDS - 256) / 4;   // 13,248 words at 1024 threads
 
 // The row predicate (gm_pip_relate.hip): one 1024-thread block per CU whose item queues leave room
-// for the join's coarse EMPTY bitmap (cm, CM_WORDS_MAX words).
+// for a coarse EMPTY bitmap in LDS: the join's (cm, CM_WORDS_MAX words) beside 64-bit-row queues of
+// 192 items, or its own finer one (rm, RM_WORDS_MAX words) beside 32-bit-row queues of 128 items
+// (x, y, row, reference, polygon: 28 B) when the rows fit 32 bits.
 #ifndef GM_RELATE_TPB
 #define GM_RELATE_TPB 1024
 #endif
 constexpr int RTPB = GM_RELATE_TPB;
+constexpr int RQCAP32 = 128;
+constexpr int RM_WORDS_MAX = (163840 - (RTPB / 64) * RQCAP32 * 28 - 256) / 4;   // 26,560 words at 1024 threads
 
 }  // namespace gm
 

@@ -938,6 +938,8 @@ int make_shortcut(gm_pip_index* ix) {
   ix->dev.fault = nullptr;   // set per call (the call's scratch word)
   ix->dev.cm = nullptr;      // the coarse EMPTY bitmaps, built after coarse_sc
   ix->dev.cm_words = 0;
+  ix->dev.rm = nullptr;
+  ix->dev.rm_words = 0;
   ix->dev.n_line = 0;
   ix->dev.n_compact_lines = ix->arr_bytes[5] / 128;
   ix->dev.n_blob16 = ix->arr_bytes[7] / 16;
@@ -1007,6 +1009,7 @@ int make_shortcut(gm_pip_index* ix) {
       return GM_OK;
     };
     rc = bitmap(CM_WORDS_MAX, &ix->dev.cm, &ix->dev.cm_shift, &ix->dev.cm_shift_y, &ix->dev.cm_w, &ix->dev.cm_words);
+    if (!rc) rc = bitmap(RM_WORDS_MAX, &ix->dev.rm, &ix->dev.rm_shift, &ix->dev.rm_shift_y, &ix->dev.rm_w, &ix->dev.rm_words);
     if (rc) { cleanup(); return rc; }
   }
   if (!rc && hipStreamSynchronize(s) != hipSuccess) rc = hip_fail(hipErrorLaunchFailure, "k_build_shortcut");
@@ -1458,8 +1461,8 @@ int gm_pip_index_create_ex(gm_ctx* ctx, const gm_polyset* ps, int cells_per_poly
       ix->dev.gx0 = G[0]; ix->dev.gy0 = G[1]; ix->dev.gx1 = G[2]; ix->dev.gy1 = G[3];
       ix->dev.inv_cw = inv_cw; ix->dev.inv_ch = inv_ch;
       ix->dev.gx = gx; ix->dev.gy = gy;
-      rc = make_list_poly(ix);
-      if (!rc) rc = make_shortcut(ix);
+      rc = make_shortcut(ix);   // first: it sets the reference bounds entry_poly checks
+      if (!rc) rc = make_list_poly(ix);
       if (rc) { gm_pip_index_destroy(ix); return rc; }
       if (getenv("GM_PIP_DEBUG")) {
         GM_HIP(hipStreamSynchronize(ctx->stream));
@@ -1746,8 +1749,8 @@ int gm_pip_index_create_ex(gm_ctx* ctx, const gm_polyset* ps, int cells_per_poly
   ix->dev.gx0 = G[0]; ix->dev.gy0 = G[1]; ix->dev.gx1 = G[2]; ix->dev.gy1 = G[3];
   ix->dev.inv_cw = inv_cw; ix->dev.inv_ch = inv_ch;
   ix->dev.gx = gx; ix->dev.gy = gy; ix->dev.gxc = gxc;
-  rc = make_list_poly(ix);
-  if (!rc) rc = make_shortcut(ix);
+  rc = make_shortcut(ix);   // first: it sets the reference bounds entry_poly checks
+  if (!rc) rc = make_list_poly(ix);
   if (rc) { gm_pip_index_destroy(ix); return rc; }
   if (getenv("GM_PIP_DEBUG")) {
     GM_HIP(hipStreamSynchronize(ctx->stream));
@@ -1824,8 +1827,8 @@ int gm_pip_index_import(gm_ctx* ctx, const gm_pip_index_layout* lay, void* const
   ix->n_cells = lay->stats[0]; ix->n_entries = lay->stats[1]; ix->n_boundary = lay->stats[2];
   ix->n_records = lay->stats[3]; ix->n_slow = lay->stats[4]; ix->blob_bytes = lay->stats[5];
   ix->n_compact = lay->stats[6]; ix->max_bnd_per_cell = lay->stats[7]; ix->max_ent_per_cell = lay->stats[8];
-  int rc = make_list_poly(ix);
-  if (!rc) rc = make_shortcut(ix);
+  int rc = make_shortcut(ix);   // first: it sets the reference bounds entry_poly checks
+  if (!rc) rc = make_list_poly(ix);
   if (!rc && hipStreamSynchronize(ctx->stream) != hipSuccess) rc = hip_fail(hipErrorLaunchFailure, "gm_pip_index_import");
   if (rc) { gm_pip_index_destroy(ix); return rc; }
   *out = ix;

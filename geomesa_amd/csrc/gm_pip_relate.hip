@@ -2,6 +2,7 @@
 // not apply): PointLocator's location of point i in polygon poly[i], from the polygon index
 // (gm_pip.hpp).  Reference: SpatialRelationFunctions.scala:29-37, SQLFunctionHelper.scala:27-33.
 #include <algorithm>
+#include <type_traits>
 
 #include "gm_pip.hpp"
 
@@ -39,30 +40,61 @@ __device__ __forceinline__ int entry_locate(const PipDev& d, uint32_t e, double 
 constexpr int RILP = GM_RILP;
 constexpr int RQCAP = 64 * (RILP + 1);
 // VEC: a lane's RILP = 2 rows are adjacent (one 16-B load per coordinate column, one 8-B id load, one
-// 2-B location store when both resolve at once); the host picks it when the columns are aligned
-template <bool VEC>
+// 2-B location store when both resolve at once); the host picks it when the columns are aligned.
+// R32 (rows < 2^32): queue rows as 32-bit values and walk the queue after each of the RILP rows, so
+// a queue holds < 128 items (RQCAP32) instead of < 192 and the LDS they free holds the finer coarse
+// EMPTY bitmap rm instead of the join's cm
+template <bool VEC, bool R32>
 __global__ __launch_bounds__(RTPB) void k_pip_relate(const int32_t* __restrict__ poly, const double* __restrict__ px,
                                                      const double* __restrict__ py, int64_t n, int32_t n_polys,
                                                      PipDev d, const int32_t* __restrict__ list_poly,
                                                      uint8_t* __restrict__ loc) {
   static_assert(!VEC || RILP == 2, "adjacent rows per lane are written for RILP = 2");
   constexpr int NW = RTPB / 64;
-  __shared__ double s_x[NW][RQCAP], s_y[NW][RQCAP];
-  __shared__ int64_t s_row[NW][RQCAP];
-  __shared__ uint32_t s_e[NW][RQCAP];
-  __shared__ int32_t s_p[NW][RQCAP];
-  // the join's coarse EMPTY bitmap (d.cm, 52 KiB: what the queues leave), staged in LDS like
-  // k_pip_join_q's: rows in EMPTY coarse blocks skip the coarse gather.  (Round 4's per-polygon core
-  // rectangles in LDS beside a bitmap of half the resolution answered rows deep inside their polygon;
-  // the finer bitmap answers more: 10.31-10.37 vs 10.47-10.51 ms, profiles/r5/relate_bitmap_vs_core_ab.txt)
-  __shared__ uint32_t s_cm[CM_WORDS_MAX];
-  const int64_t cm_words = d.cm_words <= CM_WORDS_MAX ? d.cm_words : 0;
-  for (int64_t i = threadIdx.x; i < cm_words; i += RTPB) s_cm[i] = d.cm[i];
+  constexpr int CAP = R32 ? RQCAP32 : RQCAP;
+  constexpr int BM_MAX = R32 ? RM_WORDS_MAX : CM_WORDS_MAX;
+  using RowT = typename std::conditional<R32, uint32_t, int64_t>::type;
+  __shared__ double s_x[NW][CAP], s_y[NW][CAP];
+  __shared__ RowT s_row[NW][CAP];
+  __shared__ uint32_t s_e[NW][CAP];
+  __shared__ int32_t s_p[NW][CAP];
+  // a coarse EMPTY bitmap staged in LDS like k_pip_join_q's: rows in EMPTY coarse blocks skip the
+  // coarse gather -- the join's cm (2 x 1 coarse cells per bit at the bench density) or, R32, the
+  // finer rm the smaller queues leave room for.  (Round 4's per-polygon core rectangles in LDS beside
+  // a bitmap of half the join's resolution answered fewer rows: profiles/r5/relate_bitmap_vs_core_ab.txt)
+  __shared__ uint32_t s_cm[BM_MAX];
+  const uint32_t* bm = R32 ? d.rm : d.cm;
+  const int64_t bm_n = R32 ? d.rm_words : d.cm_words;
+  const int bm_sx = R32 ? d.rm_shift : d.cm_shift, bm_sy = R32 ? d.rm_shift_y : d.cm_shift_y;
+  const int bm_w = R32 ? d.rm_w : d.cm_w;
+  const int64_t cm_words = bm_n <= BM_MAX ? bm_n : 0;
+  for (int64_t i = threadIdx.x; i < cm_words; i += RTPB) s_cm[i] = bm[i];
   __syncthreads();
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   double* qx = s_x[wave]; double* qy = s_y[wave];
-  int64_t* qr = s_row[wave]; uint32_t* qe = s_e[wave]; int32_t* qp = s_p[wave];
-  int qn = 0, qg = 0;   // queued line-entry items (from slot 0 up) and blob items (from RQCAP - 1 down)
+  RowT* qr = s_row[wave]; uint32_t* qe = s_e[wave]; int32_t* qp = s_p[wave];
+  int qn = 0, qg = 0;   // queued line-entry items (from slot 0 up) and blob items (from CAP - 1 down)
+  // walk min(qn, 64) queued items of one kind while the queue holds a full wave, and drain it at the
+  // end (< 64 queued before a step's (R32: a row's) <= 64 * RILP (64) new items, so both ends fit CAP;
+  // the fuller kind goes first, which leaves < 64 again)
+  auto walk = [&](bool drain) {
+    while (qn + qg >= 64 || (drain && qn + qg > 0)) {
+      wave_lds_sync();
+      const bool lines = qn >= qg;
+      const int kq = min(lines ? qn : qg, 64);
+      const int slot = lines ? qn - kq + lane : CAP - qg + lane;
+      if (lane < kq) {
+        const uint32_t ref = qe[slot] & 0x3fffffffu;
+        const double ex = qx[slot], ey = qy[slot];
+        int pl = -1;
+        const int l = item_locate(d, ref, ex, ey, pl);
+        loc[(int64_t)qr[slot]] = (uint8_t)(pl == qp[slot] ? l : LOC_EXTERIOR);
+      }
+      wave_lds_sync();
+      if (lines) qn -= kq;
+      else qg -= kq;
+    }
+  };
   const int64_t wstep = (int64_t)gridDim.x * NW * (64 * RILP);
   for (int64_t w0 = ((int64_t)blockIdx.x * NW + wave) * (64 * RILP);; w0 += wstep) {
     const bool have = w0 < n;   // uniform per wave
@@ -95,7 +127,7 @@ __global__ __launch_bounds__(RTPB) void k_pip_relate(const int32_t* __restrict__
           cy[u] = cell_of(y[u], d.gy0, d.inv_ch, d.gy);
           bool empty = false;
           if (cm_words) {
-            const int b = ((cy[u] >> CF_LOG) >> d.cm_shift_y) * d.cm_w + ((cx[u] >> CF_LOG) >> d.cm_shift);
+            const int b = ((cy[u] >> CF_LOG) >> bm_sy) * bm_w + ((cx[u] >> CF_LOG) >> bm_sx);
             empty = (s_cm[b >> 5] >> (b & 31)) & 1u;
           }
           if (!empty) {
@@ -156,11 +188,12 @@ __global__ __launch_bounds__(RTPB) void k_pip_relate(const int32_t* __restrict__
         const bool qv = queue && row[u] < n;
         const uint64_t ml = __ballot(qv && ln), mb = __ballot(qv && !ln);
         if (qv) {
-          const int o = ln ? qn + lanes_below(ml) : RQCAP - 1 - qg - lanes_below(mb);
-          qx[o] = x[u]; qy[o] = y[u]; qr[o] = row[u]; qe[o] = e; qp[o] = p[u];
+          const int o = ln ? qn + lanes_below(ml) : CAP - 1 - qg - lanes_below(mb);
+          qx[o] = x[u]; qy[o] = y[u]; qr[o] = (RowT)row[u]; qe[o] = e; qp[o] = p[u];
         }
         qn += __popcll(ml);
         qg += __popcll(mb);
+        if (R32) walk(false);
       }
       if (VEC) {
         if (dir[0] && dir[1]) *(uint16_t*)(loc + row[0]) = (uint16_t)(rv[0] | (rv[1] << 8));
@@ -170,25 +203,7 @@ __global__ __launch_bounds__(RTPB) void k_pip_relate(const int32_t* __restrict__
         }
       }
     }
-    // walk min(qn, 64) queued blobs when the queue holds a full wave, and drain it at the end
-    // (< 64 queued before a step's <= 64 * RILP rows, so both ends fit RQCAP; the fuller kind goes
-    // first, which leaves < 64 again)
-    while (qn + qg >= 64 || (!have && qn + qg > 0)) {
-      wave_lds_sync();
-      const bool lines = qn >= qg;
-      const int kq = min(lines ? qn : qg, 64);
-      const int slot = lines ? qn - kq + lane : RQCAP - qg + lane;
-      if (lane < kq) {
-        const uint32_t ref = qe[slot] & 0x3fffffffu;
-        const double ex = qx[slot], ey = qy[slot];
-        int pl = -1;
-        const int l = item_locate(d, ref, ex, ey, pl);
-        loc[qr[slot]] = (uint8_t)(pl == qp[slot] ? l : LOC_EXTERIOR);
-      }
-      wave_lds_sync();
-      if (lines) qn -= kq;
-      else qg -= kq;
-    }
+    walk(!have);
     if (!have) break;
   }
 }
@@ -210,7 +225,10 @@ int gm_pip_relate(gm_ctx* ctx, const gm_pip_index* ix, const int32_t* poly, cons
   note_fault_call(ctx, FC_RELATE);
   const bool vec = RILP == 2 && ((uintptr_t)px | (uintptr_t)py) % 16 == 0 && (uintptr_t)poly % 8 == 0 &&
                    (uintptr_t)loc % 2 == 0;
-  auto* kern = vec ? k_pip_relate<RILP == 2> : k_pip_relate<false>;
+  // 32-bit queue rows and the finer bitmap when the rows fit and the index built it
+  const bool r32 = n <= (int64_t)UINT32_MAX && dv.rm_words > 0 && dv.rm_words <= RM_WORDS_MAX;
+  auto* kern = vec ? (r32 ? k_pip_relate<RILP == 2, true> : k_pip_relate<RILP == 2, false>)
+                   : (r32 ? k_pip_relate<false, true> : k_pip_relate<false, false>);
   const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(resident_blocks((const void*)kern, ctx->device, RTPB, 1),
                                                                           (n + RTPB * RILP - 1) / (RTPB * RILP)));
   hipLaunchKernelGGL(kern, dim3(grid), dim3(RTPB), 0, ctx->stream, poly, px, py, n, ix->n_polys, dv, ix->list_poly, loc);

@@ -198,8 +198,8 @@ def test_relate_unaligned_and_odd_rows(gpu):
     assert np.array_equal(odd, full[:12_345])
 
 
-@pytest.mark.parametrize("cells", [0, 64, 16384])
-def test_relate_and_join_lattice_exact(gpu, cells):
+@pytest.mark.parametrize("cells,host", [(0, False), (64, False), (16384, False), (0, True)])
+def test_relate_and_join_lattice_exact(gpu, cells, host):
     """The kernels against exact rational arithmetic (tests/test_oracle_exact.py): lattice polygons
     with holes and MultiPolygon parts sharing an edge / a vertex, every lattice point on multiples of
     1/8 -- thousands exactly on edges and vertices.  Row predicate: the location per row; join: the
@@ -211,7 +211,13 @@ def test_relate_and_join_lattice_exact(gpu, cells):
     gx, gy = np.meshgrid(LATTICE, LATTICE)
     px, py = gx.ravel().copy(), gy.ravel().copy()
     exp = np.array([[_locate_exact(parts, float(x), float(y)) for x, y in zip(px, py)] for parts in polys], np.uint8)
-    ix = PolygonIndex(ps, cells_per_poly=cells)
+    from geomesa_amd import _lib
+    ctx = _lib.context()
+    try:   # the device build (default) and the host build (GM_PARAM_INDEX_BUILD = 1)
+        ctx.set_param(_lib.GM_PARAM_INDEX_BUILD, 1 if host else 0)
+        ix = PolygonIndex(ps, ctx, cells)
+    finally:
+        ctx.set_param(_lib.GM_PARAM_INDEX_BUILD, 0)
     n = len(px)
     poly = np.repeat(np.arange(len(polys), dtype=np.int32), n)
     loc = as_np(ix.relate(poly, np.tile(px, len(polys)), np.tile(py, len(polys))))
@@ -220,4 +226,37 @@ def test_relate_and_join_lattice_exact(gpu, cells):
     got = set(zip(as_np(pt).tolist(), as_np(pl).tolist()))
     want = {(i, p) for p in range(len(polys)) for i in np.flatnonzero(exp[p] == 2).tolist()}
     assert got == want
+    pt, pl = ix.join(px, py, predicate="st_intersects")
+    got = set(zip(as_np(pt).tolist(), as_np(pl).tolist()))
+    want = {(i, p) for p in range(len(polys)) for i in np.flatnonzero(exp[p] != 0).tolist()}
+    assert got == want
     assert (exp == 1).sum() > 300
+
+
+def test_relate_us_states_shared_borders(gpu, oracle):
+    """Real polygons whose neighbours share borders (the reference's us_state shapefile fixture): cells
+    on a border list two or more polygons with BOUNDARY entries, the case the list search
+    (list_poly) decides.  Rows: random points with the state of a neighbouring point, plus every
+    vertex with its own state and with a random other state."""
+    from geomesa_amd.join import PolygonIndex
+    from shapefile import us_states
+    ps, _ = us_states()
+    rng = np.random.default_rng(29)
+    n = 200_000
+    px = rng.uniform(-125.0, -66.0, n); py = rng.uniform(24.0, 50.0, n)
+    ops = oracle.OraclePolySet(*ps.to_arrays())
+    pt, pl = ops.join(px, py, nthreads=8, predicate="st_intersects")
+    poly = rng.integers(0, ps.n_polys, n).astype(np.int32)
+    poly[pt] = pl                                      # the point's own state where it has one
+    shift = np.roll(np.arange(n), 1)
+    poly[::3] = poly[shift[::3]]                       # a neighbouring point's state (often a border pair)
+    ppo, pro, rvo, vx, vy = ps.to_arrays()
+    vi = rng.choice(len(vx), 10_000, replace=False)
+    vpoly = np.searchsorted(np.asarray(ppo)[1:], np.searchsorted(np.asarray(pro)[1:], np.searchsorted(np.asarray(rvo)[1:], vi, side="right"), side="right"), side="right").astype(np.int32)
+    vpoly[1::2] = rng.integers(0, ps.n_polys, len(vpoly[1::2]))
+    poly = np.concatenate([poly, vpoly]); px = np.concatenate([px, vx[vi]]); py = np.concatenate([py, vy[vi]])
+    for cells in (0, 4096):
+        loc = as_np(PolygonIndex(ps, cells_per_poly=cells).relate(poly, px, py))
+        exp = np.array([ops.locate(int(p), x, y) for p, x, y in zip(poly, px, py)], np.uint8)
+        assert np.array_equal(loc, exp), (cells, np.flatnonzero(loc != exp)[:10])
+        assert (exp == 1).sum() > 4_000 and (exp == 2).sum() > 50_000
