@@ -140,13 +140,11 @@ __device__ __forceinline__ int hist_slot_top(double x, double y, int64_t ms, con
 // (observe, fields from 0) or 2^20 - 1 (unobserve, fields biased at 2^20): the drain comes after a
 // fixed number of block iterations, each of which counts at most HTPB * HU * 2 points.  So the hot loop
 // carries no returning atomic and no per-point check (the former 16-bit halves took a returning LDS
-// atomic per increment: 4.71-4.75 vs 4.36 ms per 1B points for int32 counters).
-#ifndef GM_HIST_SPLIT32
-#define GM_HIST_SPLIT32 0
-#endif
-#ifndef GM_HIST_WIDE_ALL
-#define GM_HIST_WIDE_ALL 0
-#endif
+// atomic per increment: 4.71-4.75 vs 4.36 ms per 1B points for int32 counters).  What the 1024 x 54
+// histogram still pays over 512 x 54 int32 counters (4.72-4.76 vs 4.24-4.32 ms) is half the 64-bit
+// adds (WIDE at 512: 4.47-4.51) and half the larger table; 32-bit adds for the two fields that lie
+// inside one dword (fields 0 and 2) cost more (4.86-4.90: the lanes split over two LDS instructions),
+// profiles/r5/hist_atomic_width_ab.txt.
 constexpr int WBITS = 21;
 constexpr uint64_t WMASK = (1ull << WBITS) - 1;
 __device__ __forceinline__ uint64_t wide_bias(bool unobs) { return unobs ? (1ull << 20) : 0ull; }
@@ -158,16 +156,6 @@ __device__ __forceinline__ uint64_t wide_fill(bool unobs) {
 template <bool SUB>
 __device__ __forceinline__ void wide_add(uint64_t* wcnt, int c) {
   const int q = c / 3, k = c - 3 * q;
-#if GM_HIST_SPLIT32
-  // fields 0 and 2 lie inside one 32-bit half (bits 0-20 / 42-62): a 32-bit add cannot carry out of
-  // it between drains, so only field 1 (bits 21-41) needs the 64-bit add
-  if (k != 1) {
-    unsigned* h = (unsigned*)&wcnt[q] + (k >> 1);
-    const unsigned v = k ? 1u << (2 * WBITS - 32) : 1u;
-    if (SUB) atomicSub(h, v); else atomicAdd(h, v);
-    return;
-  }
-#endif
   if (SUB) atomicSub((unsigned long long*)&wcnt[q], 1ull << (WBITS * k));
   else atomicAdd((unsigned long long*)&wcnt[q], 1ull << (WBITS * k));
 }
@@ -346,7 +334,7 @@ int launch_hist(gm_ctx* ctx, const double* x, const double* y, const int64_t* t,
   // 32-bit LDS counters when every time-bin row fits one pass, else three 21-bit counters per 64-bit
   // word (WIDE): rows of `length` counters in (HIST_WIDE_BYTES / 8) words
   const int rows32 = (HIST_LDS_MAX) / (a.length + 1);
-  const bool narrow = rows32 < a.n_bins || GM_HIST_WIDE_ALL;
+  const bool narrow = rows32 < a.n_bins;
   int rows = rows32;
   if (narrow) {
     auto bytes = [&](int64_t r) { return (r * a.length + 2) / 3 * 8 + r * 4; };

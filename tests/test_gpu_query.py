@@ -147,21 +147,19 @@ def test_query_scan_lobed_polygon_near_edges(gpu, oracle, cells):
         assert nm == int(exp.sum()) and np.array_equal(as_np(ids), np.nonzero(exp)[0])
 
 
+@pytest.mark.parametrize("which", ["lattice", "stacked"])
 @pytest.mark.parametrize("cells", [0, 16, 65536])
-def test_query_scan_lattice_exact(gpu, oracle, cells):
+def test_query_scan_lattice_exact(gpu, oracle, cells, which):
     """The fused filter's polygon term against exact rational arithmetic (tests/test_oracle_exact.py):
     overlapping lattice polygons with holes and MultiPolygon parts sharing an edge / a vertex, every
     point of a 1/8 lattice (thousands exactly on edges).  The polygon term is the OR of the set's
     polygons: contains = INTERIOR of some polygon, intersects = not EXTERIOR of some polygon."""
     from geomesa_amd import filters as F
     from geomesa_amd.join import PolygonIndex, PolygonSet
-    from test_oracle_exact import LATTICE, _locate_exact, lattice_polys
-    polys = lattice_polys()
+    from test_oracle_exact import exact_lattice
+    polys, x, y, loc = exact_lattice(which)
     ps = PolygonSet.from_polygons(polys)
-    gx, gy = np.meshgrid(LATTICE, LATTICE)
-    x, y = gx.ravel().copy(), gy.ravel().copy()
     t = np.arange(len(x), dtype=np.int64)
-    loc = np.array([[_locate_exact(parts, float(a), float(b)) for a, b in zip(x, y)] for parts in polys])
     ix = PolygonIndex(ps, cells_per_poly=cells)
     ops = oracle.OraclePolySet(*ps.to_arrays())
     for op, oop, exp in (("contains", 2, (loc == 2).any(0)), ("intersects", 1, (loc != 0).any(0))):

@@ -198,19 +198,17 @@ def test_relate_unaligned_and_odd_rows(gpu):
     assert np.array_equal(odd, full[:12_345])
 
 
+@pytest.mark.parametrize("which", ["lattice", "stacked"])
 @pytest.mark.parametrize("cells,host", [(0, False), (64, False), (16384, False), (0, True)])
-def test_relate_and_join_lattice_exact(gpu, cells, host):
+def test_relate_and_join_lattice_exact(gpu, cells, host, which):
     """The kernels against exact rational arithmetic (tests/test_oracle_exact.py): lattice polygons
     with holes and MultiPolygon parts sharing an edge / a vertex, every lattice point on multiples of
     1/8 -- thousands exactly on edges and vertices.  Row predicate: the location per row; join: the
     st_contains pairs."""
     from geomesa_amd.join import PolygonIndex, PolygonSet
-    from test_oracle_exact import LATTICE, _locate_exact, lattice_polys
-    polys = lattice_polys()
+    from test_oracle_exact import exact_lattice
+    polys, px, py, exp = exact_lattice(which)
     ps = PolygonSet.from_polygons(polys)
-    gx, gy = np.meshgrid(LATTICE, LATTICE)
-    px, py = gx.ravel().copy(), gy.ravel().copy()
-    exp = np.array([[_locate_exact(parts, float(x), float(y)) for x, y in zip(px, py)] for parts in polys], np.uint8)
     from geomesa_amd import _lib
     ctx = _lib.context()
     try:   # the device build (default) and the host build (GM_PARAM_INDEX_BUILD = 1)

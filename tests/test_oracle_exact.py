@@ -11,9 +11,11 @@ polygons whose lattice points fall exactly on their edges.  Where the double-dou
 (every case here), JTS, the oracle and exact arithmetic must agree, so these cases pin the
 boundary / near-collinear behaviour that the reference's own box KATs leave open.
 """
+import functools
 from fractions import Fraction as F
 
 import numpy as np
+import pytest
 
 from geomesa_amd.join import PolygonSet
 
@@ -107,13 +109,42 @@ def lattice_polys():
     ]
 
 
+def stacked_polys():
+    """24 polygons stacked over one region (nested squares, diamonds with slanted edges, squares with
+    a hole, two-part MultiPolygons): cells in the middle list 15 or more polygons, the long-list
+    encoding (LIST_LONG, a count slot before the entries)."""
+    polys = []
+    for k in range(8):
+        a = 0.25 * k
+        polys.append([[_closed([(a, a), (6 - a, a), (6 - a, 6 - a), (a, 6 - a)])]])                 # nested squares
+        c = 3.0
+        r = 3.0 - 0.25 * k
+        polys.append([[_closed([(c - r, c), (c, c - r), (c + r, c), (c, c + r)])]])                 # diamonds
+        h = 0.5 + 0.125 * k
+        polys.append([[_closed([(1, 1), (5, 1), (5, 5), (1, 5)]), _closed([(3 - h, 3 - h), (3 + h, 3 - h), (3, 3 + h)])],
+                      [_closed([(5.5, 0.25 * k), (6.5, 0.25 * k), (6.5, 0.25 * k + 1), (5.5, 0.25 * k + 1)])]])
+    return polys
+
+
 LATTICE = np.arange(-1, 7.01, 0.125)   # lattice points on multiples of 1/8
 
 
-def test_locate_lattice_polygons_exact(oracle):
-    """lattice_polys() against every lattice point: many lie exactly on edges, vertices and shared
-    edges."""
-    polys = lattice_polys()
+@functools.lru_cache(maxsize=None)
+def exact_lattice(which):
+    """(polygons, x, y, exact location [polygon, point]) of every LATTICE point, computed once per set
+    (the GPU tests reuse it across grid densities)."""
+    polys = lattice_polys() if which == "lattice" else stacked_polys()
+    gx, gy = np.meshgrid(LATTICE, LATTICE)
+    x, y = gx.ravel().copy(), gy.ravel().copy()
+    loc = np.array([[_locate_exact(parts, float(a), float(b)) for a, b in zip(x, y)] for parts in polys], np.uint8)
+    return polys, x, y, loc
+
+
+@pytest.mark.parametrize("which", ["lattice", "stacked"])
+def test_locate_lattice_polygons_exact(oracle, which):
+    """lattice_polys() / stacked_polys() against every lattice point: many lie exactly on edges,
+    vertices and shared edges."""
+    polys = lattice_polys() if which == "lattice" else stacked_polys()
     ps = PolygonSet.from_polygons(polys)
     ops = oracle.OraclePolySet(*ps.to_arrays())
     g = LATTICE
