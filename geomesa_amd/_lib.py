@@ -33,6 +33,7 @@ GM_PARAM_SORT_MODE = 4
 GM_PARAM_SORT_LAST = 5
 GM_PARAM_INDEX_COARSE = 6
 GM_PARAM_HIST_GRID = 8
+GM_PARAM_RELATE_ROWS64 = 9
 
 GM_JOIN_AUTO = 0
 GM_JOIN_DIRECT = 1

@@ -28,6 +28,7 @@ struct gm_ctx {
   int64_t sort_mode = 0;           // GM_PARAM_SORT_MODE: 0 = auto (prefix passes + local ranks), 1 = digit passes only
   int64_t index_coarse = -1;       // GM_PARAM_INDEX_COARSE: the join's coarse sub-block masks (-1 = automatic)
   int64_t hist_grid = 0;           // GM_PARAM_HIST_GRID: Z3Histogram LDS-kernel workgroups (0 = default)
+  int64_t relate_rows64 = 0;       // GM_PARAM_RELATE_ROWS64: the row predicate's 64-bit-row kernel always
   uint32_t fault_calls = 0;        // FC_* bits: the entry points that enqueued reference-checked kernels
                                    // since the fault word was last read (take_fault names them)
   hipStream_t copy_stream = nullptr;   // result copies overlapping the next chunk's kernels (lazy)

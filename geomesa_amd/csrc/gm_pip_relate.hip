@@ -226,7 +226,7 @@ int gm_pip_relate(gm_ctx* ctx, const gm_pip_index* ix, const int32_t* poly, cons
   const bool vec = RILP == 2 && ((uintptr_t)px | (uintptr_t)py) % 16 == 0 && (uintptr_t)poly % 8 == 0 &&
                    (uintptr_t)loc % 2 == 0;
   // 32-bit queue rows and the finer bitmap when the rows fit and the index built it
-  const bool r32 = n <= (int64_t)UINT32_MAX && dv.rm_words > 0 && dv.rm_words <= RM_WORDS_MAX;
+  const bool r32 = !ctx->relate_rows64 && n <= (int64_t)UINT32_MAX && dv.rm_words > 0 && dv.rm_words <= RM_WORDS_MAX;
   auto* kern = vec ? (r32 ? k_pip_relate<RILP == 2, true> : k_pip_relate<RILP == 2, false>)
                    : (r32 ? k_pip_relate<false, true> : k_pip_relate<false, false>);
   const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(resident_blocks((const void*)kern, ctx->device, RTPB, 1),

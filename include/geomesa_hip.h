@@ -118,6 +118,10 @@ const char* gm_last_error(void);
 #define GM_PARAM_HIST_GRID 8    /* gm_z3_histogram: workgroups of the LDS-counter kernel (0 = default: one
                                    resident wave of workgroups); fewer workgroups each count more features
                                    and drain their packed counters more often.  Results never change */
+#define GM_PARAM_RELATE_ROWS64 9 /* gm_pip_relate: 1 = always the kernel with 64-bit queue rows and the
+                                   join's coarse bitmap (the one calls of 2^32 rows or more take);
+                                   0 (default) = 32-bit queue rows and the finer bitmap below 2^32 rows.
+                                   Results never change */
 int gm_ctx_set_param(gm_ctx* ctx, int param, int64_t value);
 int gm_ctx_get_param(gm_ctx* ctx, int param, int64_t* value);
 /* device memory helpers for callers without their own allocator (e.g. a JNI shim) */

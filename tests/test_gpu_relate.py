@@ -1,7 +1,10 @@
 """GPU parity for the row-wise predicate path (Spark SQL st_* UDFs without the join rule):
 gm_pip_relate's per-row location against the oracle's PointLocator restatement (oracle gmo_locate),
-including points exactly on vertices and edges, holes, multipolygon parts and null rows.
-JTS semantics beyond the reference's box KATs are parity unpinned."""
+including points exactly on vertices and edges, holes, multipolygon parts and null rows; and the
+kernels against exact rational arithmetic on lattice polygons (tests/test_oracle_exact.py), which pins
+the boundary cases the reference's box KATs leave open."""
+import contextlib
+
 import numpy as np
 import pytest
 
@@ -40,13 +43,28 @@ def rows(ps, n, seed):
     return poly, px, py
 
 
+@contextlib.contextmanager
+def rows64(on):
+    """GM_PARAM_RELATE_ROWS64: the kernel with 64-bit queue rows and the join's bitmap (the path of
+    calls with 2^32 rows or more) instead of the default 32-bit rows and the finer bitmap."""
+    from geomesa_amd import _lib
+    ctx = _lib.context()
+    ctx.set_param(_lib.GM_PARAM_RELATE_ROWS64, 1 if on else 0)
+    try:
+        yield
+    finally:
+        ctx.set_param(_lib.GM_PARAM_RELATE_ROWS64, 0)
+
+
+@pytest.mark.parametrize("wide", [False, True])
 @pytest.mark.parametrize("cells", [0, 64, 16384])
-def test_relate_rows_match_oracle(gpu, oracle, cells):
+def test_relate_rows_match_oracle(gpu, oracle, cells, wide):
     from geomesa_amd.join import PolygonIndex, synthetic_counties
     ps = synthetic_counties(NX, NY)
     poly, px, py = rows(ps, 60_000, seed=3 + cells)
     ix = PolygonIndex(ps, cells_per_poly=cells)
-    loc = as_np(ix.relate(poly, px, py))
+    with rows64(wide):
+        loc = as_np(ix.relate(poly, px, py))
     ops = oracle.OraclePolySet(*ps.to_arrays())
     exp = np.array([255 if p < 0 else ops.locate(int(p), x, y) for p, x, y in zip(poly, px, py)], np.uint8)
     assert np.array_equal(loc, exp), np.flatnonzero(loc != exp)[:10]
@@ -218,8 +236,10 @@ def test_relate_and_join_lattice_exact(gpu, cells, host, which):
         ctx.set_param(_lib.GM_PARAM_INDEX_BUILD, 0)
     n = len(px)
     poly = np.repeat(np.arange(len(polys), dtype=np.int32), n)
-    loc = as_np(ix.relate(poly, np.tile(px, len(polys)), np.tile(py, len(polys))))
-    assert np.array_equal(loc, exp.ravel()), np.flatnonzero(loc != exp.ravel())[:10]
+    for wide in (False, True):
+        with rows64(wide):
+            loc = as_np(ix.relate(poly, np.tile(px, len(polys)), np.tile(py, len(polys))))
+        assert np.array_equal(loc, exp.ravel()), (wide, np.flatnonzero(loc != exp.ravel())[:10])
     pt, pl = ix.join(px, py)
     got = set(zip(as_np(pt).tolist(), as_np(pl).tolist()))
     want = {(i, p) for p in range(len(polys)) for i in np.flatnonzero(exp[p] == 2).tolist()}
@@ -253,8 +273,9 @@ def test_relate_us_states_shared_borders(gpu, oracle):
     vpoly = np.searchsorted(np.asarray(ppo)[1:], np.searchsorted(np.asarray(pro)[1:], np.searchsorted(np.asarray(rvo)[1:], vi, side="right"), side="right"), side="right").astype(np.int32)
     vpoly[1::2] = rng.integers(0, ps.n_polys, len(vpoly[1::2]))
     poly = np.concatenate([poly, vpoly]); px = np.concatenate([px, vx[vi]]); py = np.concatenate([py, vy[vi]])
-    for cells in (0, 4096):
-        loc = as_np(PolygonIndex(ps, cells_per_poly=cells).relate(poly, px, py))
+    for cells, wide in ((0, False), (4096, False), (4096, True)):
+        with rows64(wide):
+            loc = as_np(PolygonIndex(ps, cells_per_poly=cells).relate(poly, px, py))
         exp = np.array([ops.locate(int(p), x, y) for p, x, y in zip(poly, px, py)], np.uint8)
         assert np.array_equal(loc, exp), (cells, np.flatnonzero(loc != exp)[:10])
         assert (exp == 1).sum() > 4_000 and (exp == 2).sum() > 50_000
