@@ -915,7 +915,10 @@ def main():
                            "roofline": roofline(bytes_per_unit * n_units, m, load_pmc(name, n_units))}
         # the same encode when the caller hands HOST buffers (the JVM boundary without device
         # columns): pinned host -> device copies of 24 B/point, the kernel, 10 B/point back; one
-        # 64M-point batch in 8M-point chunks, copies of chunk k+1 overlapping the kernel of chunk k
+        # 64M-point batch in 8M-point chunks, chunk k+1's H2D and chunk k-1's D2H overlapping chunk
+        # k's kernel; checked against the resident-column keys (computed here when the z3 leg is off)
+        if "z3" not in only:
+            z3_step()
         extra["z3_index_key_host_buffers"] = pcie_encode(dist, ctx, x, y, t, z)
         def elem_parity(name, outs, check):
             """every stride-th element of a full-size encode / decode leg against the oracle (rank 0, untimed)"""
