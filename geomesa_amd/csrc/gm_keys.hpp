@@ -7,7 +7,12 @@
 
 namespace gm {
 
-// every column kernel streams: non-temporal loads and stores (the data is touched once)
+// every column kernel streams: non-temporal loads and stores (the data is touched once).
+// A kernel's batch of loads is issued unconditionally, past-the-end lanes reading the last valid
+// element (index clamped, result unused): loads under a per-lane branch cannot be counted by the
+// compiler, which then waits for every outstanding load (s_waitcnt vmcnt(0)) before the first
+// element's arithmetic instead of only for that element's loads, so arithmetic and the tail of the
+// batch's loads no longer overlap.
 template <class T>
 __device__ __forceinline__ T ld_stream(const T* p) {
   return __builtin_nontemporal_load(p);

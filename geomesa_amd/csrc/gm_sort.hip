@@ -272,19 +272,46 @@ __global__ __launch_bounds__(PT) void k_sort_pass(PassArgs a) {
   const int64_t tile = s_tile, t0 = tile * PTILE, n = a.n;
   // this lane's rows
   uint4 rv[PSLOT][2];
-  const bool vec = a.vec && t0 + PTILE <= n;
+  const bool full = t0 + PTILE <= n;   // every tile but the last (uniform)
+  const bool vec = a.vec && full;
+  if (IN_REC && full) {
+    // a full tile's loads are unconditional, so the compiler counts them: all 2 * PSLOT are in flight
+    // before the first wait.  (Under the per-row `i < n` selects each load sat in its own branch and
+    // was waited for before the next one was issued: one load in flight per lane.)
 #pragma unroll
-  for (int k = 0; k < PSLOT; ++k) {
-    const int64_t i = t0 + wave * (2 * 64 * PSLOT) + k * 128 + 2 * lane;
-    if (IN_REC) {
-      rv[k][0] = i < n ? a.rec_in[i] : make_uint4(0u, 0u, 0u, 0u);
-      rv[k][1] = i + 1 < n ? a.rec_in[i + 1] : make_uint4(0u, 0u, 0u, 0u);
-    } else {
-      uint64_t z0, z1;
-      uint32_t b0, b1;
-      load_pair<SH>(a.in, i, n, vec, z0, z1, b0, b1);
-      rv[k][0] = make_rec(z0, (uint32_t)i, b0);
-      rv[k][1] = make_rec(z1, (uint32_t)(i + 1), b1);
+    for (int k = 0; k < PSLOT; ++k) {
+      const int64_t i = t0 + wave * (2 * 64 * PSLOT) + k * 128 + 2 * lane;
+      rv[k][0] = a.rec_in[i];
+      rv[k][1] = a.rec_in[i + 1];
+    }
+  } else if (!IN_REC && vec) {   // the same for the first pass's column loads
+#pragma unroll
+    for (int k = 0; k < PSLOT; ++k) {
+      const int64_t i = t0 + wave * (2 * 64 * PSLOT) + k * 128 + 2 * lane;
+      const ulonglong2 zz = *(const ulonglong2*)(a.in.z + i);
+      uint32_t bb = *(const uint32_t*)(a.in.bin + i);
+      uint32_t b0 = bb & 0xffffu, b1 = bb >> 16;
+      if (SH) {
+        const uint32_t ss = *(const uint16_t*)(a.in.sh + i);
+        b0 |= (ss & 0xffu) << 16; b1 |= (ss >> 8) << 16;
+      }
+      rv[k][0] = make_rec(zz.x, (uint32_t)i, b0);
+      rv[k][1] = make_rec(zz.y, (uint32_t)(i + 1), b1);
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < PSLOT; ++k) {
+      const int64_t i = t0 + wave * (2 * 64 * PSLOT) + k * 128 + 2 * lane;
+      if (IN_REC) {
+        rv[k][0] = i < n ? a.rec_in[i] : make_uint4(0u, 0u, 0u, 0u);
+        rv[k][1] = i + 1 < n ? a.rec_in[i + 1] : make_uint4(0u, 0u, 0u, 0u);
+      } else {
+        uint64_t z0, z1;
+        uint32_t b0, b1;
+        load_pair<SH>(a.in, i, n, vec, z0, z1, b0, b1);
+        rv[k][0] = make_rec(z0, (uint32_t)i, b0);
+        rv[k][1] = make_rec(z1, (uint32_t)(i + 1), b1);
+      }
     }
   }
   const uint64_t lt = lanemask_lt();

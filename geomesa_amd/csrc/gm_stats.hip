@@ -238,10 +238,13 @@ __global__ __launch_bounds__(HTPB) void k_z3_hist_lds(const double* __restrict__
     dv2 xa[HU], ya[HU];
     lv2 ta[HU];
     const int64_t p0 = (int64_t)blockIdx.x * HTPB;
+    if (p0 < np) {   // uniform per block; below it every clamped index is a valid pair
 #pragma unroll
-    for (int u = 0; u < HU; ++u) {
-      const int64_t q = p0 + threadIdx.x + u * stride;
-      if (q < np) { xa[u] = ld_stream(&x2[q]); ya[u] = ld_stream(&y2[q]); ta[u] = ld_stream(&t2[q]); }
+      for (int u = 0; u < HU; ++u) {
+        const int64_t q = p0 + threadIdx.x + u * stride;
+        const int64_t qc = q < np ? q : np - 1;   // unconditional loads (see below)
+        xa[u] = ld_stream(&x2[qc]); ya[u] = ld_stream(&y2[qc]); ta[u] = ld_stream(&t2[qc]);
+      }
     }
     // the loop bound is the block's first pair, so every thread of the block runs the same iterations
     // (the drains' barriers)
@@ -252,7 +255,11 @@ __global__ __launch_bounds__(HTPB) void k_z3_hist_lds(const double* __restrict__
 #pragma unroll
       for (int u = 0; u < HU; ++u) {
         const int64_t q = pn + u * stride;
-        if (q < np) { xb[u] = ld_stream(&x2[q]); yb[u] = ld_stream(&y2[q]); tb[u] = ld_stream(&t2[q]); }
+        // unconditional (clamped) loads: with the loads under a branch the compiler cannot count them and
+        // waits for all outstanding loads (vmcnt(0)) before binning the current pairs, which serialises
+        // this iteration's prefetch with its arithmetic
+        const int64_t qc = q < np ? q : np - 1;
+        xb[u] = ld_stream(&x2[qc]); yb[u] = ld_stream(&y2[qc]); tb[u] = ld_stream(&t2[qc]);
       }
 #pragma unroll
       for (int u = 0; u < HU; ++u) {
