@@ -8,11 +8,15 @@
 namespace gm {
 
 // every column kernel streams: non-temporal loads and stores (the data is touched once).
-// A kernel's batch of loads is issued unconditionally, past-the-end lanes reading the last valid
-// element (index clamped, result unused): loads under a per-lane branch cannot be counted by the
-// compiler, which then waits for every outstanding load (s_waitcnt vmcnt(0)) before the first
-// element's arithmetic instead of only for that element's loads, so arithmetic and the tail of the
-// batch's loads no longer overlap.
+// Loads under a per-lane branch (`if (p < n) v = load(p)`) cannot be counted by the compiler: it
+// waits for every outstanding load (s_waitcnt vmcnt(0)) at the branch's end, and a select around a
+// load (`v = p < n ? load(p) : 0`) is waited for before the next load is even issued.  Where a
+// batch of loads must be in flight together (the sort passes, the histogram's prefetch) it is issued
+// unconditionally, past-the-end lanes reading the last valid element (index clamped, result unused).
+// The per-pair kernels keep their conditional batches (all of a lane's loads are issued before the
+// one wait anyway): the unconditional form, which lets each pair's arithmetic start on its own loads,
+// measured 1-3% slower for the Z3 key and no faster for XZ and the fused filter
+// (profiles/r5/unconditional_loads_ab.txt, unconditional_loads_xz_query_ab.txt).
 template <class T>
 __device__ __forceinline__ T ld_stream(const T* p) {
   return __builtin_nontemporal_load(p);

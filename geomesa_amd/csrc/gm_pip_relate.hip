@@ -119,9 +119,14 @@ __global__ __launch_bounds__(RTPB) void k_pip_relate(const int32_t* __restrict__
         for (int u = 0; u < RILP; ++u)
           if (row[u] < n) { p[u] = poly[row[u]]; x[u] = px[row[u]]; y[u] = py[row[u]]; }
       }
+      // the rows' coarse gathers are issued together and only then resolved: with the gather and its
+      // coarse_mask in one per-row branch the first row's gather was waited for before the second row's
+      // was issued
+      bool gat[RILP];
 #pragma unroll
       for (int u = 0; u < RILP; ++u) {
-        w[u] = CELL_EMPTY << 30;
+        gat[u] = false;
+        cx[u] = cy[u] = 0;
         if (p[u] >= 0 && p[u] < n_polys && x[u] >= d.gx0 && x[u] <= d.gx1 && y[u] >= d.gy0 && y[u] <= d.gy1) {
           cx[u] = cell_of(x[u], d.gx0, d.inv_cw, d.gx);
           cy[u] = cell_of(y[u], d.gy0, d.inv_ch, d.gy);
@@ -130,12 +135,17 @@ __global__ __launch_bounds__(RTPB) void k_pip_relate(const int32_t* __restrict__
             const int b = ((cy[u] >> CF_LOG) >> bm_sy) * bm_w + ((cx[u] >> CF_LOG) >> bm_sx);
             empty = (s_cm[b >> 5] >> (b & 31)) & 1u;
           }
-          if (!empty) {
-            const uint32_t craw = d.coarse_sc[(int64_t)(cy[u] >> CF_LOG) * d.gxc + (cx[u] >> CF_LOG)];
-            w[u] = coarse_mask(craw, cx[u], cy[u], d.coarse_fmt);
-          }
+          gat[u] = !empty;
         }
       }
+      uint32_t craw[RILP];
+#pragma unroll
+      for (int u = 0; u < RILP; ++u) {
+        craw[u] = CELL_EMPTY << 30;
+        if (gat[u]) craw[u] = d.coarse_sc[(int64_t)(cy[u] >> CF_LOG) * d.gxc + (cx[u] >> CF_LOG)];
+      }
+#pragma unroll
+      for (int u = 0; u < RILP; ++u) w[u] = coarse_mask(craw[u], cx[u], cy[u], d.coarse_fmt);
 #pragma unroll
       for (int u = 0; u < RILP; ++u)
         if ((w[u] >> 30) == CELL_LIST) w[u] = d.cell_sc[(int64_t)cy[u] * d.gx + cx[u]];   // boundary shortcuts applied
