@@ -9,7 +9,7 @@
 //   * gm_sort_keys     -- a stable sort of (shard u8, bin u16, z u64) in that byte order.  The key
 //                         K = shard:bin:z is an 88-bit integer; one read finds its varying bits (OR /
 //                         AND), a second counts every pass's digits at once (k_sort_count).  Then
-//                         one-sweep digit passes (digits of <= 9 bits, k_sort_pass): 4096-row tiles
+//                         one-sweep digit passes (digits of <= 9 bits, k_sort_pass): 8192-row tiles
 //                         taken in order, ranked in LDS (wave ballots rank equal digits), each tile's
 //                         digit offsets found by a decoupled look-back over the tiles before it (8-B
 //                         {count, tag} granules), and the tile leaves as digit runs of 16-B records
@@ -228,14 +228,17 @@ __global__ __launch_bounds__(CT) void k_sort_count(KeyCols c, int64_t n, DigitOf
 // the lower tiles' granules, adding counts until it meets an inclusive prefix (PRE), and publishes its
 // own (decoupled look-back).  The tile is reordered in LDS meanwhile and leaves as digit runs of 16-B
 // records.  Granule tags carry the pass (tag) so no pass reads another's; the status array is cleared
-// once per call.  LDS 78 KB: two blocks (16 waves) per CU.
+// once per call.  1024-thread blocks over 8192-row tiles (LDS ~148 KB: one block, 16 waves, per CU):
+// 10.84-10.86 -> 10.48-10.51 ms per 250M-row sort against 512 threads / 4096 rows at two blocks per CU
+// once the tile's loads were all in flight together (profiles/r5/sort_tile_shape_ab.txt; 768 threads
+// 11.97-11.99, 1024 x 2048 rows 13.75-13.77, 1024 x 6144 11.63-11.67, 512 x 8192 11.30-11.35).
 #ifndef GM_SORT_PSLOT
 #define GM_SORT_PSLOT 4
 #endif
 #ifndef GM_SORT_PT
-#define GM_SORT_PT 512
+#define GM_SORT_PT 1024
 #endif
-constexpr int PT = GM_SORT_PT, PW = PT / 64, PSLOT = GM_SORT_PSLOT, PTILE = PT * 2 * PSLOT;   // 4096 rows per tile
+constexpr int PT = GM_SORT_PT, PW = PT / 64, PSLOT = GM_SORT_PSLOT, PTILE = PT * 2 * PSLOT;   // 8192 rows per tile
 static_assert(PT >= NB_MAX, "one thread per digit");
 constexpr uint64_t GR_VAL = (1ull << 48) - 1;
 
