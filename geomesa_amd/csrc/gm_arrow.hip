@@ -107,13 +107,24 @@ __global__ __launch_bounds__(ATPB) void k_z3_key_arrow_v(ArrowPts g, ArrowTime t
   const int64_t base = (int64_t)blockIdx.x * (ATPB * UNROLL) + threadIdx.x;
   dv2 a[UNROLL], b[UNROLL];
   lv2 tv[UNROLL];
+  if (((int64_t)blockIdx.x + 1) * (ATPB * UNROLL) <= npairs) {
+    // a full block: every load unconditional, so all 2-3 x UNROLL are in flight before the first wait
+    // (the guarded form below is waited for pair by pair: see ld_stream, gm_keys.hpp)
 #pragma unroll
-  for (int u = 0; u < UNROLL; ++u) {
-    const int64_t p = base + (int64_t)u * ATPB;
-    tv[u] = lv2{0, 0};
-    if (p < npairs) {
+    for (int u = 0; u < UNROLL; ++u) {
+      const int64_t p = base + (int64_t)u * ATPB;
       arrow_tuple_pair<F32>(g.c, p, a[u], b[u]);
-      if (TIME) tv[u] = __builtin_nontemporal_load(&((const lv2*)tc.ms)[p]);
+      tv[u] = TIME ? __builtin_nontemporal_load(&((const lv2*)tc.ms)[p]) : lv2{0, 0};
+    }
+  } else {
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      const int64_t p = base + (int64_t)u * ATPB;
+      tv[u] = lv2{0, 0};
+      if (p < npairs) {
+        arrow_tuple_pair<F32>(g.c, p, a[u], b[u]);
+        if (TIME) tv[u] = __builtin_nontemporal_load(&((const lv2*)tc.ms)[p]);
+      }
     }
   }
 #pragma unroll
