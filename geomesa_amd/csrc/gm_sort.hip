@@ -218,7 +218,7 @@ __global__ __launch_bounds__(CT) void k_sort_count(KeyCols c, int64_t n, DigitOf
 }
 
 // One-sweep digit pass over a digit of w <= 9 bits.  Block b takes tile k (the next in a counter, so
-// every lower tile is already running) of 4096 rows; wave w owns rows [512 w, 512 w + 512) of it and
+// every lower tile is already running) of 8192 rows; wave w owns rows [512 w, 512 w + 512) of it and
 // reads them in 4 slots of 128 rows, 2 per lane.  Within a slot, lanes holding the same digit find each
 // other with 2 w ballots (w digit bits x even / odd row); a per-wave LDS counter per digit turns slot
 // ranks into wave ranks, a scan over the waves into tile ranks, so a row's place in the tile is
