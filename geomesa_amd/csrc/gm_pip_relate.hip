@@ -146,9 +146,29 @@ __global__ __launch_bounds__(RTPB) void k_pip_relate(const int32_t* __restrict__
       }
 #pragma unroll
       for (int u = 0; u < RILP; ++u) w[u] = coarse_mask(craw[u], cx[u], cy[u], d.coarse_fmt);
+      // the join's 8-B fine words: a cell crossed by one or two boundary lines carries them inline, so
+      // the row decides in registers instead of gathering the 4-B word and then its line entry
+      // (10.04-10.16 -> 9.52-9.53 ms per 1B rows, profiles/r5/relate_inline_lines_ab.txt; round 4's
+      // attempt, which decided both rows' lines in one pass over more registers, lost)
+      uint32_t hi[RILP];
 #pragma unroll
-      for (int u = 0; u < RILP; ++u)
-        if ((w[u] >> 30) == CELL_LIST) w[u] = d.cell_sc[(int64_t)cy[u] * d.gx + cx[u]];   // boundary shortcuts applied
+      for (int u = 0; u < RILP; ++u) {
+        hi[u] = 0u;
+        if ((w[u] >> 30) == CELL_LIST) {
+          const uint2 w8 = d.cell_sc8[(int64_t)cy[u] * d.gx + cx[u]];
+          w[u] = w8.x; hi[u] = w8.y;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < RILP; ++u) {
+        if (sc8_inline(make_uint2(w[u], hi[u]))) {
+          const uint2 w8 = make_uint2(w[u], hi[u]);
+          const int l = sc8_locate(w8, x[u], y[u], d, cx[u], cy[u]);
+          if (l == LOC_INTERIOR) w[u] = (CELL_INTERIOR << 30) | (uint32_t)sc8_poly(w8);   // compared with p below
+          else if (l == LOC_EXTERIOR) w[u] = CELL_EMPTY << 30;
+          else w[u] = d.cell_sc[(int64_t)cy[u] * d.gx + cx[u]];   // near a line: the entry, then the blob
+        }
+      }
       uint8_t rv[RILP];
       bool dir[RILP];
 #pragma unroll
