@@ -13,7 +13,7 @@
 //                         taken in order, ranked in LDS (wave ballots rank equal digits), each tile's
 //                         digit offsets found by a decoupled look-back over the tiles before it (8-B
 //                         {count, tag} granules), and the tile leaves as digit runs of 16-B records
-//                         {z, row, bin | shard << 16}.  The passes order the rows by the top
+//                         {z, row, bs} (bs = bin | shard << sq, squeeze_bs).  The passes order the rows by the top
 //                         ~log2(n) - 1 varying bits (three 9-bit digits at 250M rows); k_local_bounds
 //                         cuts the result into ~2048-row tiles at run starts and k_sort_local ranks
 //                         every run of equal prefixes (a few rows) by full key in LDS and writes the
@@ -47,12 +47,22 @@ __device__ __forceinline__ uint32_t key_bits(uint32_t bs, uint64_t z, int off) {
 }
 __device__ __forceinline__ uint32_t key_digit(uint32_t bs, uint64_t z, int off) { return key_bits(bs, z, off) & 255u; }
 
-// a row in flight between passes: {z lo, z hi, input row, bin | shard << 16}
+// a row in flight between passes: {z lo, z hi, input row, bs} (bs = bin | shard << sq, squeeze_bs)
 __device__ __forceinline__ uint64_t rec_z(uint4 r) { return (uint64_t)r.x | ((uint64_t)r.y << 32); }
 __device__ __forceinline__ uint4 make_rec(uint64_t z, uint32_t row, uint32_t bs) {
   return make_uint4((uint32_t)z, (uint32_t)(z >> 32), row, bs);
 }
 
+// With a shard byte, the sort's key packs it right above bin's highest varying bit: bs = bin low bits |
+// shard << sq (sq = that bit + 1, 16 without a shard).  The bits of bin above it are the same in every
+// key (binhi), so this order is the (shard, bin) order, and the key's varying bits are contiguous: the
+// prefix digits cover shard and bin together instead of a 9-bit digit spanning bin's constant top bits
+// (with 4 shards and weekly bins that digit held 2 varying bits of 9, the runs of equal prefixes grew to
+// ~128 rows and the sort took 31.5 ms per 250M rows instead of ~10.5).
+__device__ __forceinline__ uint32_t squeeze_bs(uint32_t b, int sq) { return (b & ((1u << sq) - 1u)) | ((b >> 16) << sq); }
+__device__ __forceinline__ uint16_t bs_bin(uint32_t w, int sq, uint32_t binhi) {
+  return (uint16_t)((w & ((1u << sq) - 1u)) | binhi);
+}
 __device__ __forceinline__ uint64_t lanemask_lt() {
   const int lane = threadIdx.x & 63;
   return lane ? (~0ull >> (64 - lane)) : 0ull;
@@ -182,16 +192,17 @@ constexpr int CNT_LDS = 2816;           // 11 byte digits x 256, or 4 prefix dig
 constexpr int CT = 1024;   // count threads per block
 template <bool SH, bool ORAND>
 __global__ __launch_bounds__(CT) void k_sort_count(KeyCols c, int64_t n, DigitOffs o, uint32_t* __restrict__ counts, int wide,
-                                                   unsigned long long* __restrict__ acc) {
+                                                   unsigned long long* __restrict__ acc, int sq) {
   __shared__ uint32_t h[4][CNT_LDS];
   const int copy = (threadIdx.x >> 6) & 3;
   for (int i = threadIdx.x; i < 4 * CNT_LDS; i += CT) (&h[0][0])[i] = 0u;
   __syncthreads();
   uint64_t zo = 0, za = ~0ull, bo = 0, ba = ~0ull;
   for_rows<SH, CT / 64>(c, n, wide, [&](uint64_t z, uint32_t b) {
-    if (ORAND) { zo |= z; za &= z; bo |= b; ba &= b; }
+    if (ORAND) { zo |= z; za &= z; bo |= b; ba &= b; }   // of the caller's bs (bin | shard << 16)
+    const uint32_t bk_s = SH ? squeeze_bs(b, sq) : b;
     for (int k = 0, bk = 0; k < o.np; bk += 1 << o.w[k], ++k)
-      atomicAdd(&h[copy][bk + key_digit_w(b, z, o.off[k], o.w[k])], 1u);
+      atomicAdd(&h[copy][bk + key_digit_w(bk_s, z, o.off[k], o.w[k])], 1u);
   });
   __shared__ uint64_t s_oa[ORAND ? CT / 64 : 1][4];
   if (ORAND) {   // per wave, then one device atomic per value per block (not per wave: same 4 addresses)
@@ -257,6 +268,8 @@ struct PassArgs {
   unsigned long long* status;       // ntiles x 2^w granules
   unsigned int* ctr;                // this pass's tile counter
   int vec;
+  int sq;                 // the shard's place in the records' bs (squeeze_bs) ...
+  uint32_t binhi;         // ... and bin's constant bits above it
 };
 
 template <bool IN_REC, bool OUT_USER, bool SH>
@@ -296,7 +309,7 @@ __global__ __launch_bounds__(PT) void k_sort_pass(PassArgs a) {
       uint32_t b0 = bb & 0xffffu, b1 = bb >> 16;
       if (SH) {
         const uint32_t ss = *(const uint16_t*)(a.in.sh + i);
-        b0 |= (ss & 0xffu) << 16; b1 |= (ss >> 8) << 16;
+        b0 = squeeze_bs(b0 | (ss & 0xffu) << 16, a.sq); b1 = squeeze_bs(b1 | (ss >> 8) << 16, a.sq);
       }
       rv[k][0] = make_rec(zz.x, (uint32_t)i, b0);
       rv[k][1] = make_rec(zz.y, (uint32_t)(i + 1), b1);
@@ -312,6 +325,7 @@ __global__ __launch_bounds__(PT) void k_sort_pass(PassArgs a) {
         uint64_t z0, z1;
         uint32_t b0, b1;
         load_pair<SH>(a.in, i, n, vec, z0, z1, b0, b1);
+        if (SH) { b0 = squeeze_bs(b0, a.sq); b1 = squeeze_bs(b1, a.sq); }
         rv[k][0] = make_rec(z0, (uint32_t)i, b0);
         rv[k][1] = make_rec(z1, (uint32_t)(i + 1), b1);
       }
@@ -417,8 +431,8 @@ __global__ __launch_bounds__(PT) void k_sort_pass(PassArgs a) {
     const int64_t g = (int64_t)(uint32_t)(s_gpos[key_digit_w(r.w, rec_z(r), a.off, w)] + (uint32_t)q);
     if (OUT_USER) {
       a.z_out[g] = rec_z(r);
-      a.bin_out[g] = (uint16_t)r.w;
-      if (SH) a.sh_out[g] = (uint8_t)(r.w >> 16);
+      a.bin_out[g] = SH ? bs_bin(r.w, a.sq, a.binhi) : (uint16_t)r.w;
+      if (SH) a.sh_out[g] = (uint8_t)(r.w >> a.sq);
       a.perm_out[g] = (int64_t)r.z;
     } else {
       a.rec_out[g] = r;
@@ -482,11 +496,18 @@ __global__ __launch_bounds__(256) void k_local_bounds(const uint4* __restrict__ 
   if (lane == 0) bounds[k] = p;
 }
 
+// waves per SIMD: 8 = four resident 512-thread blocks per CU (64 VGPRs, no spills; the tiles' LDS is
+// 32 KB each): 10.42-10.44 -> 10.22-10.25 ms per sort over the compiler's 75 VGPRs / three blocks;
+// loading the next tile while ranking the current one instead: 11.61-11.66 ms
+// (profiles/r5/sort_local_occupancy_ab.txt)
+#ifndef GM_SORT_LOCAL_WPE
+#define GM_SORT_LOCAL_WPE 8
+#endif
 template <bool SH>
-__global__ __launch_bounds__(LT) void k_sort_local(const uint4* __restrict__ rec_in, uint8_t* __restrict__ sh_out,
-                                                   uint16_t* __restrict__ bin_out, uint64_t* __restrict__ z_out,
-                                                   int64_t* __restrict__ perm_out, int64_t n, int4 po, int pw,
-                                                   uint32_t* __restrict__ flag, const int64_t* __restrict__ bounds) {
+__global__ __launch_bounds__(LT) __attribute__((amdgpu_waves_per_eu(GM_SORT_LOCAL_WPE))) void k_sort_local(
+    const uint4* __restrict__ rec_in, uint8_t* __restrict__ sh_out, uint16_t* __restrict__ bin_out,
+    uint64_t* __restrict__ z_out, int64_t* __restrict__ perm_out, int64_t n, int4 po, int pw,
+    uint32_t* __restrict__ flag, const int64_t* __restrict__ bounds, int sq, uint32_t binhi) {
   __shared__ uint64_t s_z[LCAP];
   __shared__ uint32_t s_bs[LCAP];
   __shared__ uint32_t s_run[LCAP];   // prefix; then run start (low 16) | at a run start, its end << 16
@@ -574,8 +595,8 @@ __global__ __launch_bounds__(LT) void k_sort_local(const uint4* __restrict__ rec
       }
       const int64_t dst = a + s0 + r;
       z_out[dst] = zi;
-      bin_out[dst] = (uint16_t)bi;
-      if (SH) sh_out[dst] = (uint8_t)(bi >> 16);
+      bin_out[dst] = SH ? bs_bin(bi, sq, binhi) : (uint16_t)bi;
+      if (SH) sh_out[dst] = (uint8_t)(bi >> sq);
       perm_out[dst] = (int64_t)row[k];
     }
     __syncthreads();
@@ -627,6 +648,8 @@ struct SortPlan {
   std::vector<int> lsd;
   int npre = 0, pw = 0, pofs[4] = {-1, -1, -1, -1};
   bool prefix = false;
+  int sq = 16;            // the shard's bit in bs (squeeze_bs), and bin's constant bits above it
+  uint32_t binhi = 0;
   std::vector<int> first_offs() const {   // the first digit passes, LSD order
     if (!prefix) return lsd;
     std::vector<int> o(pofs, pofs + npre);
@@ -647,8 +670,19 @@ inline bool operator==(const DigitOffs& a, const DigitOffs& b) {
     if (a.off[k] != b.off[k] || a.w[k] != b.w[k]) return false;
   return true;
 }
-static SortPlan plan_sort(const unsigned long long h[4], bool sh, int64_t n, int sort_mode) {
+static SortPlan plan_sort(const unsigned long long h_raw[4], bool sh, int64_t n, int sort_mode) {
   SortPlan p;
+  unsigned long long h[4] = {h_raw[0], h_raw[1], h_raw[2], h_raw[3]};
+  if (sh) {   // the digits are planned over the squeezed key (squeeze_bs)
+    const uint32_t vbin = (uint32_t)((h_raw[1] ^ h_raw[3]) & 0xffffu);
+    p.sq = vbin ? 32 - __builtin_clz(vbin) : 0;
+    p.binhi = (uint32_t)h_raw[3] & 0xffffu & ~((1u << p.sq) - 1u);
+    auto sqz = [&](unsigned long long b) {
+      return (unsigned long long)(((uint32_t)b & ((1u << p.sq) - 1u)) | (((uint32_t)b >> 16) << p.sq));
+    };
+    h[1] = sqz(h_raw[1]);
+    h[3] = sqz(h_raw[3]);
+  }
   for (int b = 0; b < NPASS; ++b) {
     if (b == 10 && !sh) continue;
     const uint64_t o = b < 8 ? h[0] >> (8 * b) : h[1] >> (8 * (b - 8));
@@ -750,8 +784,8 @@ int gm_sort_keys(gm_ctx* ctx, const uint8_t* shard, const int16_t* bin, const in
   // the guessed plan's first digit set counted in the read that takes the exact OR / AND
   {
     const DigitOffs o = guess.first_digits();
-    if (sh) hipLaunchKernelGGL((k_sort_count<true, true>), dim3(cgrid), dim3(CT), 0, s, in, n, o, counts, user_wide, acc);
-    else hipLaunchKernelGGL((k_sort_count<false, true>), dim3(cgrid), dim3(CT), 0, s, in, n, o, counts, user_wide, acc);
+    if (sh) hipLaunchKernelGGL((k_sort_count<true, true>), dim3(cgrid), dim3(CT), 0, s, in, n, o, counts, user_wide, acc, guess.sq);
+    else hipLaunchKernelGGL((k_sort_count<false, true>), dim3(cgrid), dim3(CT), 0, s, in, n, o, counts, user_wide, acc, 16);
     GM_CHECK_LAUNCH();
   }
   unsigned long long hacc[4];
@@ -770,7 +804,7 @@ int gm_sort_keys(gm_ctx* ctx, const uint8_t* shard, const int16_t* bin, const in
     return GM_OK;
   }
   // the sample's plan holds when the exact bits give the same first digits; else count again
-  bool counted = guess.first_digits() == plan.first_digits();
+  bool counted = guess.first_digits() == plan.first_digits() && guess.sq == plan.sq;
   if (!counted) GM_HIP(hipMemsetAsync(counts, 0, counts_bytes, s));
   const bool prefix_mode = plan.prefix;
   const int npre = plan.npre, pw = plan.pw;
@@ -785,8 +819,8 @@ int gm_sort_keys(gm_ctx* ctx, const uint8_t* shard, const int16_t* bin, const in
     for (int k = 0; k < np; ++k) { o.off[k] = offs[k]; o.w[k] = w; }
     uint32_t* cnt = counts + (size_t)tag0 * NB_MAX;
     if (!counted) {
-      if (sh) hipLaunchKernelGGL((k_sort_count<true, false>), dim3(cgrid), dim3(CT), 0, s, in, n, o, cnt, user_wide, nullptr);
-      else hipLaunchKernelGGL((k_sort_count<false, false>), dim3(cgrid), dim3(CT), 0, s, in, n, o, cnt, user_wide, nullptr);
+      if (sh) hipLaunchKernelGGL((k_sort_count<true, false>), dim3(cgrid), dim3(CT), 0, s, in, n, o, cnt, user_wide, nullptr, plan.sq);
+      else hipLaunchKernelGGL((k_sort_count<false, false>), dim3(cgrid), dim3(CT), 0, s, in, n, o, cnt, user_wide, nullptr, 16);
       if (hipGetLastError() != hipSuccess) return hip_fail(hipErrorLaunchFailure, "k_sort_count");
     }
     counted = false;   // a later call (the fallback) counts its own digits
@@ -801,6 +835,7 @@ int gm_sort_keys(gm_ctx* ctx, const uint8_t* shard, const int16_t* bin, const in
       a.status = status;
       a.ctr = ctr + tag0 + k;
       a.vec = user_vec;
+      a.sq = plan.sq; a.binhi = plan.binhi;
       const bool first = k == 0, user = to_user_last && k == np - 1;
       void (*kern)(PassArgs) =
           sh ? (first ? (user ? k_sort_pass<false, true, true> : k_sort_pass<false, false, true>)
@@ -823,10 +858,10 @@ int gm_sort_keys(gm_ctx* ctx, const uint8_t* shard, const int16_t* bin, const in
                        (uint32_t*)(acc + 4));
     if (sh)
       hipLaunchKernelGGL(k_sort_local<true>, dim3(lgrid), dim3(LT), 0, s, last_rec, shard_out, (uint16_t*)bin_out,
-                         (uint64_t*)z_out, perm_out, n, po, pw, (uint32_t*)(acc + 4), lbounds);
+                         (uint64_t*)z_out, perm_out, n, po, pw, (uint32_t*)(acc + 4), lbounds, plan.sq, plan.binhi);
     else
       hipLaunchKernelGGL(k_sort_local<false>, dim3(lgrid), dim3(LT), 0, s, last_rec, nullptr, (uint16_t*)bin_out,
-                         (uint64_t*)z_out, perm_out, n, po, pw, (uint32_t*)(acc + 4), lbounds);
+                         (uint64_t*)z_out, perm_out, n, po, pw, (uint32_t*)(acc + 4), lbounds, plan.sq, plan.binhi);
     GM_CHECK_LAUNCH();
     uint32_t flag = 0;
     GM_HIP(hipMemcpyAsync(&flag, acc + 4, 4, hipMemcpyDeviceToHost, s));

@@ -34,7 +34,7 @@ def expected_order(bins, z, shard=None):
 @pytest.mark.parametrize("mode", [0, 1])
 def test_sort_keys_parity(gpu, n, kind, sharded, mode):
     """mode 0: prefix passes + local ranks (digit passes when a run of equal prefixes exceeds 256
-    rows: "dups"); mode 1: digit passes over every varying byte (GM_PARAM_SORT_MODE)."""
+    rows: unsharded "dups"); mode 1: digit passes over every varying byte (GM_PARAM_SORT_MODE)."""
     import torch
     from geomesa_amd import _lib
     rng = np.random.default_rng(n + sharded)
@@ -81,8 +81,10 @@ def test_sort_keys_parity(gpu, n, kind, sharded, mode):
         assert last < 256
     elif kind in ("rand", "keys", "narrow", "runs") and n > 100_000:
         assert last > 256, last               # prefix passes + local ranks
-    elif kind == "dups":
+    elif kind == "dups" and not sharded:
         assert last < 256 and last > 3, last  # runs > 256 rows: digit passes
+    elif kind == "dups":
+        assert last > 256, last               # 4 shards split each 300-row run into ~75: ranked locally
 
 
 def _check_table_order_on_device(bins, z, ob, oz, op, sh=None, osh=None):
@@ -106,11 +108,14 @@ def _check_table_order_on_device(bins, z, ob, oz, op, sh=None, osh=None):
     assert bool((op[1:][tie] > op[:-1][tie]).all())
 
 
-@pytest.mark.parametrize("kind", ["week_keys", "dups"])
+@pytest.mark.parametrize("kind", ["week_keys", "dups", "sharded"])
 def test_sort_keys_prefix_path_at_bench_size(gpu, kind):
     """The bench's sort path (2^27 < n: three 9-bit prefix digits + local ranks) on 140M rows: Z3 keys
-    of uniform points over 2020 (53 weekly bins, runs of equal prefixes of a few rows), and the same
-    keys with every key repeated 4 times (ties: stability); checked on the device."""
+    of uniform points over 2020 (53 weekly bins, runs of equal prefixes of a few rows), the same
+    keys with every key repeated 4 times (ties: stability), and the keys with GeoMesa's default 4
+    shards (geomesa.z.splits, Conversions.scala:312): the shard sits right above bin's varying bits in
+    the sort key, so the prefix digits still cover ~log2(n) varying bits and the local ranks run
+    (a digit spanning bin's constant top bits sent this case to 3x the time); checked on the device."""
     import torch
     from geomesa_amd import _lib
     from geomesa_amd.curve import Z3SFC
@@ -126,13 +131,17 @@ def test_sort_keys_prefix_path_at_bench_size(gpu, kind):
         idx = torch.randperm(n, device="cuda", generator=g) % m
         b, z = b[idx].contiguous(), z[idx].contiguous()
         del idx
+    sh = osh = None
+    if kind == "sharded":
+        sh = torch.randint(0, 4, (n,), device="cuda", generator=g, dtype=torch.uint8)
+        osh = torch.empty_like(sh)
     ob, oz = torch.empty_like(b), torch.empty_like(z)
     op = torch.empty(n, dtype=torch.int64, device="cuda")
     ctx = _lib.context()
-    _lib.check(ctx.lib.gm_sort_keys(ctx.handle, None, _lib.ptr(b), _lib.ptr(z), n, None, _lib.ptr(ob), _lib.ptr(oz),
-                                    _lib.ptr(op)), "sort")
+    _lib.check(ctx.lib.gm_sort_keys(ctx.handle, _lib.ptr(sh), _lib.ptr(b), _lib.ptr(z), n, _lib.ptr(osh), _lib.ptr(ob),
+                                    _lib.ptr(oz), _lib.ptr(op)), "sort")
     assert ctx.get_param(_lib.GM_PARAM_SORT_LAST) == 256 + 3   # three prefix passes + local ranks
-    _check_table_order_on_device(b, z, ob, oz, op)
+    _check_table_order_on_device(b, z, ob, oz, op, sh, osh)
 
 
 def test_sort_keys_prefix_keeps_first_digit_top_bits(gpu):
