@@ -537,7 +537,11 @@ def gather_pairs(dist, ptids, plids, k, id_base, n_polys):
     import torch
     from geomesa_amd.shard import gather_estimate_ms, gather_pairs_compact, gather_rows
     full_b = [12 * int(v) for v in all_gather_ints(dist, k)]
-    comp_b = [(6 if n_polys <= 65536 else 12) * v // 12 for v in full_b]
+    # the compact format's bytes as gather_pairs_compact decides them: 6 B per pair only while every rank's
+    # rows span < 2^32 and there are at most 65,536 polygons (else it sends the full 12-B pairs)
+    span = int((ptids[:k].max() - id_base).item()) + 1 if k else 0
+    fits = all(v == 1 for v in all_gather_ints(dist, int(span <= (1 << 32))))
+    comp_b = [(6 if (n_polys <= 65536 and fits) else 12) * v // 12 for v in full_b]
     out = {"placement": "ms_per_step leaves the pairs sharded on their ranks (the reference's RDD partitions)",
            "est_ms_full": round(gather_estimate_ms(full_b), 3), "est_ms_compact": round(gather_estimate_ms(comp_b), 3),
            "bytes_full": sum(full_b[1:]), "bytes_compact": sum(comp_b[1:])}
@@ -555,7 +559,8 @@ def gather_pairs(dist, ptids, plids, k, id_base, n_polys):
         torch.cuda.empty_cache()
         dist.barrier()
         t0 = time.time()
-        gc, _ = gather_pairs_compact(dist.pg, ptids[:k], plids[:k], id_base, n_polys)
+        gc, wire = gather_pairs_compact(dist.pg, ptids[:k], plids[:k], id_base, n_polys)
+        out.update(bytes_compact=sum(wire[1:]), est_ms_compact=round(gather_estimate_ms(wire), 3))   # as sent
         torch.cuda.synchronize()
         msc = dist.max((time.time() - t0) * 1e3)
         nc = int(gc[0].numel()) if gc is not None else 0
@@ -598,15 +603,15 @@ def bench_table(a, dist, ctx, b, z):
     # splitters and exchange rows by key range (one all-to-all over RCCL), each sorts its slice
     from geomesa_amd.table import PartitionedZ3Table
     ks = Z3IndexKeySpace()
-    gids = torch.arange(NT, dtype=torch.int64, device=zs.device) + dist.rank * NT
     holder = {}
 
     def ingest_step():
         holder.pop("t", None)
-        holder["t"] = PartitionedZ3Table(dist.pg, bs, zs, gids)
+        # ids = the rank's first global row: rows travel as 4-B rows and map back through the senders' bases
+        holder["t"] = PartitionedZ3Table(dist.pg, bs, zs, dist.rank * NT)
     ms_ingest = timed(dist, ingest_step, 1, 1)
     pt = holder["t"]
-    del gids
+    phases = {k: (round(dist.max(v), 3) if isinstance(v, float) else v) for k, v in pt.timing.items()}
     slice_rows = [int(v) for v in (all_gather_ints(dist, pt.n))]
     v = ks.get_index_values([(-10, 35, 30, 60)], [during(1590969600000, 1591617600000)])
     t0 = time.time()
@@ -681,11 +686,13 @@ def bench_table(a, dist, ctx, b, z):
                               "equal prefixes ranked by full key in LDS (8-bit digit passes over every varying byte when "
                               "a run exceeds 256 rows); bytes: see sort_bytes"},
         "table_ingest": {"value": NT * dist.world / (ms_ingest * 1e-3), "unit": "rows/s", "ms_per_step": ms_ingest,
-                         "rows_per_gpu": NT, "slice_rows": slice_rows,
-                         "note": "key-range partitioned table: local sort, splitter sampling (1024 keys per rank), "
-                                 "all-to-all of the rows by key range (24 B/row), sort of the received slice; the "
-                                 "slice keeps its ids in arrival order beside the sort's permutation (a query maps "
-                                 "only its matches); at world 1 the local sort is the table"},
+                         "rows_per_gpu": NT, "slice_rows": slice_rows, "phases_max_over_ranks": phases,
+                         "note": "key-range partitioned table from every rank's unsorted keys: key sample (1024 per "
+                                 "rank, gm_key_sample) + splitters (one all_gather), one partition pass "
+                                 "(gm_key_partition: count, scan, stable scatter into destination runs), one "
+                                 "all-to-all per column (z 8 + bin 2 + 4-B source row = 14 B/row), one sort of the "
+                                 "received slice (gm_sort_keys); the slice keeps each row's source beside the sort's "
+                                 "permutation (a query maps only its matches); at world 1 the sort is the table"},
         "table_query": {"value": 1.0 / (ms_scan * 1e-3), "unit": "queries/s", "ms_per_step": ms_scan,
                         "table_rows": NT * dist.world, "ranges": nr, "ranges_scanned_rank0": res["ncl"],
                         "rows_scanned": int(scanned), "matches": int(matches), "plan_ms": round(plan_ms, 2),

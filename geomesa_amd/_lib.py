@@ -32,6 +32,7 @@ GM_PARAM_RANGES_CHUNK = 3
 GM_PARAM_SORT_MODE = 4
 GM_PARAM_SORT_LAST = 5
 GM_PARAM_INDEX_COARSE = 6
+GM_PARAM_INDEX_CORE_RETIRED = 7
 GM_PARAM_HIST_GRID = 8
 GM_PARAM_RELATE_ROWS64 = 9
 
@@ -61,6 +62,17 @@ class Range(ctypes.Structure):
 class KeyRange(ctypes.Structure):
     _fields_ = [("z_lo", ctypes.c_int64), ("z_hi", ctypes.c_int64), ("bin_lo", ctypes.c_int16),
                 ("bin_hi", ctypes.c_int16), ("shard", ctypes.c_uint8), ("reserved", ctypes.c_uint8 * 3)]
+
+
+class ScanFilter(ctypes.Structure):
+    """gm_scan_filter: the row filter (Z3Filter or Z2Filter bytes) and the full filter (envelopes x boxes,
+    dtg during) of gm_table_scan."""
+    _fields_ = [("z3filter", ctypes.c_void_p), ("z3filter_len", ctypes.c_size_t),
+                ("z2filter", ctypes.c_void_p), ("z2filter_len", ctypes.c_size_t),
+                ("xmin", ctypes.c_void_p), ("ymin", ctypes.c_void_p), ("xmax", ctypes.c_void_p),
+                ("ymax", ctypes.c_void_p), ("boxes", ctypes.c_void_p), ("n_boxes", ctypes.c_int32),
+                ("during", ctypes.c_int32), ("t_ms", ctypes.c_void_p), ("t_lo", ctypes.c_int64),
+                ("t_hi", ctypes.c_int64)]
 
 
 # numpy view of gm_key_range rows (24 B, the KeyRange layout)
@@ -116,6 +128,7 @@ SIGNATURES = {
     "gm_binned_time": (cint, [vp, vp, i64, cint, vp, vp, vp, vp]),
     "gm_xz2_index": (cint, [vp, vp, vp, vp, vp, i64, cint, cint, vp, vp, vp]),
     "gm_xz3_index": (cint, [vp, vp, vp, vp, vp, vp, vp, i64, cint, cint, cint, vp, vp, vp]),
+    "gm_xz3_index_key": (cint, [vp, vp, vp, vp, vp, vp, i64, cint, cint, cint, vp, vp, vp, vp]),
     "gm_z3_ranges": (cint, [vp, i64, vp, vp, vp, vp, cint, cint, cint, cint, cint, vp, vp, i64, vp, vp]),
     "gm_z2_ranges": (cint, [vp, i64, vp, vp, cint, cint, cint, cint, vp, vp, i64, vp, vp]),
     "gm_zranges": (cint, [vp, cint, i64, vp, vp, cint, cint, cint, vp, vp, i64, vp, vp]),
@@ -141,6 +154,10 @@ SIGNATURES = {
     "gm_z3_key_bytes": (cint, [vp, vp, vp, vp, i64, vp]),
     "gm_sort_keys": (cint, [vp, vp, vp, vp, i64, vp, vp, vp, vp]),
     "gm_key_range_scan": (cint, [vp, vp, vp, vp, i64, vp, i64, vp, sz, vp, vp, i64, vp, vp]),
+    "gm_table_scan": (cint, [vp, vp, vp, vp, i64, vp, i64, vp, vp, vp, i64, vp, vp]),
+    "gm_z2_key_bytes": (cint, [vp, vp, vp, i64, vp]),
+    "gm_key_sample": (cint, [vp, vp, vp, vp, i64, i32, vp, vp]),
+    "gm_key_partition": (cint, [vp, vp, vp, vp, i64, vp, vp, i32, vp, i64, vp, vp, vp, vp, vp, vp]),
     "gm_z3_index_key_arrow": (cint, [vp, vp, vp, i64, cint, cint, vp, vp, vp, vp]),
     "gm_z2_index_key_arrow": (cint, [vp, vp, i64, cint, vp, vp, vp]),
     "gm_xz2_index_key_arrow": (cint, [vp, vp, i64, cint, cint, vp, vp, vp]),

@@ -330,6 +330,8 @@ int gm_ctx_set_param(gm_ctx* c, int param, int64_t value) {
       if (value != 0 && value != 1) return GM_E_INVALID;
       c->relate_rows64 = value;
       return GM_OK;
+    case GM_PARAM_INDEX_CORE_RETIRED:   // retired in round 5: accepted, ignored (one release)
+      return GM_OK;
     default:
       gm::set_error("gm_ctx_set_param: unknown parameter");
       return GM_E_INVALID;
@@ -346,6 +348,7 @@ int gm_ctx_get_param(gm_ctx* c, int param, int64_t* value) {
     case GM_PARAM_SORT_LAST: *value = c->sort_last; return GM_OK;
     case GM_PARAM_INDEX_COARSE: *value = c->index_coarse; return GM_OK;
     case GM_PARAM_HIST_GRID: *value = c->hist_grid; return GM_OK;
+    case GM_PARAM_INDEX_CORE_RETIRED: *value = 0; return GM_OK;
     case GM_PARAM_RELATE_ROWS64: *value = c->relate_rows64; return GM_OK;
     default: return GM_E_INVALID;
   }

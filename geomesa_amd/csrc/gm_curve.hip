@@ -286,6 +286,31 @@ __global__ __launch_bounds__(TPB) void k_xz3_index(const double* __restrict__ xm
   }
 }
 
+// XZ3IndexKeySpace.toIndexKey (idx/index/z3/XZ3IndexKeySpace.scala:60-95) over envelope + dtg columns:
+// BinnedTime(dtg) (null dtg column -> 0) outside the lenient try, then XZ3SFC.index of the envelope at
+// the period offset.  A failed row gets bin 0 and key 0 and its status.
+template <int PERIOD, bool LENIENT, bool STATUS>
+__global__ __launch_bounds__(TPB) void k_xz3_index_key(const double* __restrict__ xmin, const double* __restrict__ ymin,
+                                                       const double* __restrict__ xmax, const double* __restrict__ ymax,
+                                                       const int64_t* __restrict__ t_ms, int64_t n, int g, double zhi,
+                                                       int16_t* __restrict__ bin, int64_t* __restrict__ out,
+                                                       uint8_t* __restrict__ status, int64_t* __restrict__ err) {
+  for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < n; i += (int64_t)gridDim.x * TPB) {
+    int64_t o = 0, off = 0;
+    int16_t b = 0;
+    uint8_t s = binned_time<PERIOD>(t_ms ? t_ms[i] : 0, b, off);
+    if (s == ST_OK) {
+      const double t = (double)off;
+      s = xz3_one<LENIENT>(g, zhi, xmin[i], ymin[i], t, xmax[i], ymax[i], t, o);
+    }
+    if (s != ST_OK) { o = 0; b = 0; }
+    out[i] = o;
+    bin[i] = b;
+    if (STATUS) status[i] = s;
+    if (s) report_error(err, i, s);
+  }
+}
+
 // 16-B form: 2 envelopes per lane per column (one dwordx4 each), UNROLL pairs in flight per lane,
 // the same coalesced layout as the Z3 key kernel; the odd last envelope goes to lane 0 of block 0.
 template <bool LENIENT, bool STATUS, int UNROLL>
@@ -626,6 +651,35 @@ int gm_xz3_index(gm_ctx* ctx, const double* xmin, const double* ymin, const doub
     if (status) hipLaunchKernelGGL((k_xz3_index<false, true>), dim3(grid), dim3(TPB), 0, s, xmin, ymin, zmin, xmax, ymax, zmax, n, g, zhi, out, status, ctx->d_err);
     else hipLaunchKernelGGL((k_xz3_index<false, false>), dim3(grid), dim3(TPB), 0, s, xmin, ymin, zmin, xmax, ymax, zmax, n, g, zhi, out, status, ctx->d_err);
   }
+  GM_CHECK_LAUNCH();
+  return end_summary(ctx, summary);
+}
+
+int gm_xz3_index_key(gm_ctx* ctx, const double* xmin, const double* ymin, const double* xmax, const double* ymax,
+                     const int64_t* t_ms, int64_t n, int g, int period, int lenient, int16_t* bin, int64_t* xz,
+                     uint8_t* status, gm_batch_status* summary) {
+  if (!ctx || n < 0 || g < 1 || g > 20 || !valid_period(period)) return GM_E_INVALID;
+  if (n == 0) { if (summary) *summary = gm_batch_status{0, -1, 0, 0}; return GM_OK; }
+  if (!xmin || !ymin || !xmax || !ymax || !bin || !xz) return GM_E_INVALID;
+  int rc = begin_summary(ctx, summary);
+  if (rc) return rc;
+  const unsigned grid = stride_grid(n);
+  const double zhi = (double)max_offset(period);
+  hipStream_t s = ctx->stream;
+#define GM_XZ3K(P)                                                                                                   \
+  do {                                                                                                               \
+    auto k = lenient ? (status ? k_xz3_index_key<P, true, true> : k_xz3_index_key<P, true, false>)                  \
+                     : (status ? k_xz3_index_key<P, false, true> : k_xz3_index_key<P, false, false>);               \
+    hipLaunchKernelGGL(k, dim3(grid), dim3(TPB), 0, s, xmin, ymin, xmax, ymax, t_ms, n, g, zhi, bin, xz, status,     \
+                       ctx->d_err);                                                                                  \
+  } while (0)
+  switch (period) {
+    case GM_DAY: GM_XZ3K(GM_DAY); break;
+    case GM_WEEK: GM_XZ3K(GM_WEEK); break;
+    case GM_MONTH: GM_XZ3K(GM_MONTH); break;
+    default: GM_XZ3K(GM_YEAR); break;
+  }
+#undef GM_XZ3K
   GM_CHECK_LAUNCH();
   return end_summary(ctx, summary);
 }

@@ -410,8 +410,9 @@ __device__ __forceinline__ bool key_lt(uint32_t ka, uint64_t za, uint32_t kb, ui
   return ka < kb || (ka == kb && za < zb);
 }
 
+// bin = null: a key space without a time bin (Z2 / XZ2: [shard][z BE64]), every row's bin reads as 0
 __device__ __forceinline__ uint32_t row_kb(const uint8_t* sh, const uint16_t* bin, int64_t i) {
-  return ((uint32_t)(sh ? sh[i] : 0) << 16) | bin[i];
+  return ((uint32_t)(sh ? sh[i] : 0) << 16) | (bin ? bin[i] : 0u);
 }
 
 // row interval of each range: [first row >= lo, first row > hi)
@@ -470,12 +471,32 @@ __device__ __forceinline__ int64_t cand_row(const int64_t* __restrict__ coff, co
 }
 
 
-// candidate-space mask: candidate c = the c-th row inside the (disjoint, sorted) intervals
-template <bool FILTER>
+// candidate-space mask: candidate c = the c-th row inside the (disjoint, sorted) intervals.  RF: the row
+// filter the tablet server runs on the key (RowFilterIterator.scala:52-66): none, Z3Filter.inBounds on
+// (bin, z) (Z3Filter.scala:26-62) or Z2Filter.inBounds on z (Z2Filter.scala:20-35).  ENV / DUR: the full
+// filter on the feature (the XZ key spaces' useFullFilter = true, XZ2IndexKeySpace.scala:122-125,
+// XZ3IndexKeySpace.scala:247-250) over the caller's input-order columns, reached through perm: JTS
+// Envelope.intersects with any query box (inclusive), and FastDuring (exclusive, ms) on the dtg.
+enum : int { RF_NONE = 0, RF_Z3 = 1, RF_Z2 = 2 };
+struct FullFilter {
+  const double *xmin, *ymin, *xmax, *ymax;   // feature envelopes (input order)
+  const int64_t* t;                           // feature dtg (input order)
+  const double* boxes;                        // nbox x (xmin, ymin, xmax, ymax), device
+  int nbox;
+  int64_t t_lo, t_hi;
+  const int64_t* perm;                        // table row -> input row (null: the identity)
+};
+// JTS Envelope.intersects(Envelope): false for a null envelope (maxx < minx) on either side
+__device__ __forceinline__ bool env_intersects(double ax0, double ay0, double ax1, double ay1, const double* q) {
+  if (ax1 < ax0 || q[2] < q[0]) return false;
+  return !(q[0] > ax1 || q[2] < ax0 || q[1] > ay1 || q[3] < ay0);
+}
+template <int RF, bool ENV, bool DUR>
 __global__ __launch_bounds__(FTPB) void k_range_mask(const uint16_t* __restrict__ bin, const uint64_t* __restrict__ z,
                                                      const int64_t* __restrict__ coff, const int64_t* __restrict__ start,
-                                                     int64_t nr, int64_t total, const int32_t* __restrict__ fdesc,
-                                                     uint64_t* __restrict__ mask, int32_t* __restrict__ block_counts) {
+                                                     int64_t nr, int64_t total, const int32_t* __restrict__ fdesc, int nxy,
+                                                     FullFilter ff, uint64_t* __restrict__ mask,
+                                                     int32_t* __restrict__ block_counts) {
   const int64_t base = (int64_t)blockIdx.x * FROWS;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   int local = 0;
@@ -484,9 +505,32 @@ __global__ __launch_bounds__(FTPB) void k_range_mask(const uint16_t* __restrict_
     bool ok = false;
     if (c < total) {
       ok = true;
-      if (FILTER) {
+      if (RF != RF_NONE || ENV || DUR) {
         const int64_t row = cand_row(coff, start, nr, c);
-        ok = z3_in_bounds(fdesc, (int16_t)bin[row], (int64_t)z[row]);
+        if (RF == RF_Z3) ok = z3_in_bounds(fdesc, (int16_t)bin[row], (int64_t)z[row]);
+        if (RF == RF_Z2) {
+          const int64_t zz = (int64_t)z[row];
+          const int32_t x = z2_combine(zz), y = z2_combine(zz >> 1);
+          bool in = false;
+          for (int k = 0; k < nxy && !in; ++k) {
+            const int32_t* q = fdesc + 4 * k;
+            in = x >= q[0] && x <= q[2] && y >= q[1] && y <= q[3];
+          }
+          ok = in;
+        }
+        if ((ENV || DUR) && ok) {
+          const int64_t r = ff.perm ? ff.perm[row] : row;
+          if (DUR) {
+            const int64_t t = ff.t[r];
+            ok = t > ff.t_lo && t < ff.t_hi;
+          }
+          if (ENV && ok) {
+            const double x0 = ff.xmin[r], y0 = ff.ymin[r], x1 = ff.xmax[r], y1 = ff.ymax[r];
+            bool in = false;
+            for (int k = 0; k < ff.nbox && !in; ++k) in = env_intersects(x0, y0, x1, y1, ff.boxes + 4 * k);
+            ok = in;
+          }
+        }
       }
     }
     const uint64_t w = __ballot(ok);
@@ -836,11 +880,37 @@ int gm_strict_scan(gm_ctx* ctx, const double* x, const double* y, const int64_t*
   return GM_OK;
 }
 
-int gm_key_range_scan(gm_ctx* ctx, const uint8_t* shard, const int16_t* bin, const int64_t* z, int64_t n,
-                      const gm_key_range* ranges, int64_t n_ranges, const uint8_t* filter_bytes, size_t filter_len,
-                      const int64_t* perm, int64_t* ids, int64_t ids_cap, int64_t* n_match, int64_t* n_scanned) {
+int gm_table_scan(gm_ctx* ctx, const uint8_t* shard, const int16_t* bin, const int64_t* z, int64_t n,
+                  const gm_key_range* ranges, int64_t n_ranges, const gm_scan_filter* f, const int64_t* perm,
+                  int64_t* ids, int64_t ids_cap, int64_t* n_match, int64_t* n_scanned) {
   if (!ctx || n < 0 || n_ranges < 0 || (n_ranges > 0 && !ranges) || ids_cap < 0) return GM_E_INVALID;
-  if (n > 0 && (!bin || !z)) return GM_E_INVALID;
+  if (n > 0 && !z) return GM_E_INVALID;
+  gm_scan_filter none{};
+  if (!f) f = &none;
+  if (f->z3filter && f->z2filter) return set_error("gm_table_scan: a Z3Filter and a Z2Filter together"), GM_E_INVALID;
+  if (f->z3filter && !bin) return set_error("gm_table_scan: a Z3Filter needs the bin column"), GM_E_INVALID;
+  const bool env = f->n_boxes > 0, dur = f->during != 0;
+  if (f->n_boxes < 0 || (env && (!f->boxes || !f->xmin || !f->ymin || !f->xmax || !f->ymax)) || (dur && !f->t_ms))
+    return GM_E_INVALID;
+  // the row filter's descriptor: Z3Filter.deserializeFromBytes or Z2Filter's boxes
+  std::vector<int32_t> desc;
+  int rf = RF_NONE, nxy = 0;
+  if (f->z3filter) {
+    if (!build_z3_desc(f->z3filter, f->z3filter_len, desc)) {
+      set_error("gm_table_scan: malformed Z3Filter bytes");
+      return GM_E_INVALID;
+    }
+    rf = RF_Z3;
+  } else if (f->z2filter) {
+    if (f->z2filter_len < 4) return GM_E_INVALID;
+    nxy = be32(f->z2filter);
+    if (nxy < 0 || 4 + (size_t)nxy * 16 > f->z2filter_len) {
+      set_error("gm_table_scan: malformed Z2Filter bytes");
+      return GM_E_INVALID;
+    }
+    for (int i = 0; i < 4 * nxy; ++i) desc.push_back(be32(f->z2filter + 4 + 4 * i));
+    rf = RF_Z2;
+  }
   // the BatchScanner's view of the ranges: sorted, overlapping / adjacent ones merged
   std::vector<HostRange> rs;
   rs.reserve((size_t)n_ranges);
@@ -892,25 +962,31 @@ int gm_key_range_scan(gm_ctx* ctx, const uint8_t* shard, const int16_t* bin, con
   int rc = GM_OK;
   int64_t nm = 0;
   if (total > 0) {
-    std::vector<int32_t> desc;
-    if (filter_bytes && !build_z3_desc(filter_bytes, filter_len, desc)) {
-      set_error("gm_key_range_scan: malformed Z3Filter bytes");
-      rc = GM_E_INVALID;
-    }
+    // device descriptor: [query boxes f64 x 4 nbox][row-filter words]
+    const size_t box_words = env ? (size_t)f->n_boxes * 8 : 0;
+    std::vector<int32_t> buf(box_words + desc.size());
+    if (env) memcpy(buf.data(), f->boxes, (size_t)f->n_boxes * 32);
+    if (!desc.empty()) memcpy(buf.data() + box_words, desc.data(), desc.size() * 4);
     ScanBufs b;
-    if (!rc) rc = alloc_scan(ctx, total, nullptr, desc.size(), b);
+    rc = alloc_scan(ctx, total, nullptr, buf.size() + 4, b);
     if (!rc) {
-      if (!desc.empty()) {
-        GM_HIP(hipMemcpyAsync(b.desc, desc.data(), desc.size() * 4, hipMemcpyHostToDevice, s));
+      if (!buf.empty()) {
+        GM_HIP(hipMemcpyAsync(b.desc, buf.data(), buf.size() * 4, hipMemcpyHostToDevice, s));
         GM_HIP(hipStreamSynchronize(s));
       }
+      FullFilter ff{f->xmin, f->ymin, f->xmax, f->ymax, f->t_ms, env ? (const double*)b.desc : nullptr, f->n_boxes,
+                    f->t_lo, f->t_hi, perm};
+      const int32_t* d_desc = b.desc + box_words;
       const int64_t nblocks = (total + FROWS - 1) / FROWS;
-      if (filter_bytes)
-        hipLaunchKernelGGL(k_range_mask<true>, dim3((unsigned)nblocks), dim3(FTPB), 0, s, (const uint16_t*)bin,
-                           (const uint64_t*)z, coff, start, nr, total, b.desc, b.mask, b.counts);
-      else
-        hipLaunchKernelGGL(k_range_mask<false>, dim3((unsigned)nblocks), dim3(FTPB), 0, s, (const uint16_t*)bin,
-                           (const uint64_t*)z, coff, start, nr, total, b.desc, b.mask, b.counts);
+      void (*kern)(const uint16_t*, const uint64_t*, const int64_t*, const int64_t*, int64_t, int64_t, const int32_t*,
+                   int, FullFilter, uint64_t*, int32_t*) = nullptr;
+#define GM_RANGE_MASK(R)                                                                   \
+  (env ? (dur ? k_range_mask<R, true, true> : k_range_mask<R, true, false>)               \
+       : (dur ? k_range_mask<R, false, true> : k_range_mask<R, false, false>))
+      kern = rf == RF_Z3 ? GM_RANGE_MASK(RF_Z3) : rf == RF_Z2 ? GM_RANGE_MASK(RF_Z2) : GM_RANGE_MASK(RF_NONE);
+#undef GM_RANGE_MASK
+      hipLaunchKernelGGL(kern, dim3((unsigned)nblocks), dim3(FTPB), 0, s, (const uint16_t*)bin, (const uint64_t*)z, coff,
+                         start, nr, total, d_desc, nxy, ff, b.mask, b.counts);
       if (hipGetLastError() != hipSuccess) rc = hip_fail(hipErrorLaunchFailure, "k_range_mask");
       if (!rc) rc = finish_scan(ctx, total, b, ids, ids_cap, &nm);
       if (!rc && ids && nm > 0) {
@@ -929,6 +1005,17 @@ int gm_key_range_scan(gm_ctx* ctx, const uint8_t* shard, const int16_t* bin, con
   if (n_match) *n_match = nm;
   if (ids && nm > ids_cap) return GM_E_CAPACITY;
   return GM_OK;
+}
+
+int gm_key_range_scan(gm_ctx* ctx, const uint8_t* shard, const int16_t* bin, const int64_t* z, int64_t n,
+                      const gm_key_range* ranges, int64_t n_ranges, const uint8_t* filter_bytes, size_t filter_len,
+                      const int64_t* perm, int64_t* ids, int64_t ids_cap, int64_t* n_match, int64_t* n_scanned) {
+  if (!ctx) return GM_E_INVALID;
+  if (n > 0 && !bin) return GM_E_INVALID;
+  gm_scan_filter f{};
+  f.z3filter = filter_bytes;
+  f.z3filter_len = filter_len;
+  return gm_table_scan(ctx, shard, bin, z, n, ranges, n_ranges, &f, perm, ids, ids_cap, n_match, n_scanned);
 }
 
 }  // extern "C"

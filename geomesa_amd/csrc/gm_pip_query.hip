@@ -99,7 +99,10 @@ __global__ __launch_bounds__(QueryShape<OP>::TPB) void k_query_mask(const double
     }
   }
   uint32_t pass = 0;
-  int fc[R], cc[R];   // fine / coarse cell of each row (geometry term only)
+  int fc[R];          // fine cell of each row (geometry term only)
+  uint32_t cc[R];     // its coarse cell (low 26 bits) and the fine cell's place in it (top 6 bits)
+  static_assert(CF_LOG == 3, "cc packs the fine cell's 3 + 3 bits of position in its coarse cell into bits 26-31");
+  constexpr int CF_MASK = (1 << CF_LOG) - 1;
   auto cheap = [&](double px, double py, int64_t tt, int k) {
     bool ok = !has_bbox || (px >= bx0 && px <= bx1 && py >= by0 && py <= by1);
     if (DURING) ok = ok && tt > lo && tt < hi;
@@ -109,7 +112,8 @@ __global__ __launch_bounds__(QueryShape<OP>::TPB) void k_query_mask(const double
       fc[k] = cy * d.gx + cx;
       // the coarse cell (< 2^20 of them: the grid has at most 2^26 cells) and, in the top 6 bits, the
       // fine cell's place in it (what coarse_mask reads)
-      cc[k] = ((cy >> CF_LOG) * d.gxc + (cx >> CF_LOG)) | (((cy & 7) << 3 | (cx & 7)) << 26);
+      cc[k] = (uint32_t)((cy >> CF_LOG) * d.gxc + (cx >> CF_LOG)) |
+              ((uint32_t)((cy & CF_MASK) << CF_LOG | (cx & CF_MASK)) << 26);
     }
     return ok;
   };
@@ -125,7 +129,7 @@ __global__ __launch_bounds__(QueryShape<OP>::TPB) void k_query_mask(const double
     for (int k = 0; k < R; ++k) cw[k] = ((pass >> k) & 1u) ? d.coarse_sc[cc[k] & 0x3ffffff] : (CELL_EMPTY << 30);
 #pragma unroll
     for (int k = 0; k < R; ++k) {
-      const uint32_t sb = (uint32_t)cc[k] >> 26;
+      const uint32_t sb = cc[k] >> 26;
       cw[k] = coarse_mask(cw[k], (int)(sb & 7u), (int)(sb >> 3), d.coarse_fmt);
     }
 #pragma unroll

@@ -1244,8 +1244,10 @@ static int xz_ranges(gm_ctx* ctx, int D, int64_t nq, const int32_t* win_off, con
   // level; the pre-merge list holds those ranges plus the unprocessed rest of one sibling group
   int64_t fcap, rcap;
   if (max_ranges > 0) {
-    fcap = (int64_t)max_ranges + 2;
-    rcap = (int64_t)max_ranges + (1 << D) + 16;
+    // a budget past the unbounded caps (a caller passing a huge maxRanges to mean "unlimited") gets
+    // the unbounded caps, so a query past them reports QS_CAPACITY like an unbounded one
+    fcap = std::min<int64_t>((int64_t)max_ranges + 2, (int64_t)1 << 24);
+    rcap = std::min<int64_t>((int64_t)max_ranges + (1 << D) + 16, fcap << (D + 1));
   } else {
     // unbounded (maxRanges <= 0): the frontier is not bounded by a budget, so the worst-case caps are
     // capped instead (~320 B per frontier slot per query for XZ3) -- a query past them reports

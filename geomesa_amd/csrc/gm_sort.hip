@@ -619,10 +619,12 @@ __global__ __launch_bounds__(STPB) void k_key_bytes(const uint8_t* __restrict__ 
   if (i < n) {
     uint8_t* o = s + threadIdx.x * klen;
     int k = 0;
-    if (klen == 11) o[k++] = sh[i];
-    const uint16_t b = (uint16_t)bin[i];
-    o[k++] = (uint8_t)(b >> 8);
-    o[k++] = (uint8_t)b;
+    if (sh) o[k++] = sh[i];
+    if (bin) {   // no bin: the Z2 / XZ2 layout [shard][z BE64]
+      const uint16_t b = (uint16_t)bin[i];
+      o[k++] = (uint8_t)(b >> 8);
+      o[k++] = (uint8_t)b;
+    }
     const uint64_t zz = (uint64_t)z[i];
 #pragma unroll
     for (int j = 7; j >= 0; --j) o[k++] = (uint8_t)(zz >> (8 * j));
@@ -710,6 +712,199 @@ static SortPlan plan_sort(const unsigned long long h_raw[4], bool sh, int64_t n,
   return p;
 }
 
+// ------------------------------------------------------------------ key-range partition (multi-GPU ingest)
+// A table split into `nd` contiguous key ranges (tablets / regions; one per GPU) by nd - 1 ascending
+// splitter keys: row r goes to destination d = the number of splitters <= its key (a key equal to a
+// splitter opens the upper range).  Keys compare as the row bytes do: (shard << 16 | bin as u16, z as
+// u64), unsigned.  One read counts every tile's rows per destination (k_part_count), a device scan of
+// those counts in destination-major order gives each (destination, tile) its output start, and a
+// second read (k_part_scatter) ranks the tile's rows per destination in LDS (wave ballots, stable:
+// within a destination rows keep their input order) and writes them as contiguous destination runs,
+// so that destination d's rows are one slice of every output column -- what one all-to-all sends.
+constexpr int XT = 256;                  // partition threads per block
+constexpr int XTILE = 2048;              // rows per tile: wave w owns rows [512 w, 512 w + 512)
+constexpr int XSLOT = XTILE / XT;        // 8 rows per lane, one per 64-row slot
+constexpr int XMAX = 256;                // destinations at most (ranks of the partitioned table)
+
+struct SplitLds {
+  uint32_t hi[XMAX];
+  uint64_t lo[XMAX];
+};
+// destination of key (hi, lo): first splitter greater than the key (binary search, ns < XMAX)
+__device__ __forceinline__ int part_dest(const SplitLds& s, int ns, uint32_t hi, uint64_t lo) {
+  int a = 0, b = ns;
+  while (a < b) {
+    const int m = (a + b) >> 1;
+    const bool le = s.hi[m] < hi || (s.hi[m] == hi && s.lo[m] <= lo);
+    if (le) a = m + 1;
+    else b = m;
+  }
+  return a;
+}
+__device__ __forceinline__ void load_splitters(SplitLds& s, const uint64_t* __restrict__ split, int ns) {
+  for (int k = threadIdx.x; k < ns; k += blockDim.x) {
+    s.hi[k] = (uint32_t)split[2 * k];
+    s.lo[k] = split[2 * k + 1];
+  }
+}
+// lanes of this wave whose destination equals mine (among the lanes with `ok`), from nbits ballots
+__device__ __forceinline__ uint64_t match_dest(uint32_t d, bool ok, int nbits) {
+  uint64_t m = __ballot(ok);
+  for (int bit = 0; bit < nbits; ++bit) {   // uniform
+    const uint64_t b = __ballot((d >> bit) & 1u);
+    m &= ((d >> bit) & 1u) ? b : ~b;
+  }
+  return m;
+}
+template <bool SH>
+__device__ __forceinline__ void part_load_tile(const KeyCols& c, int64_t t0, int64_t n, uint64_t (&z)[XSLOT],
+                                               uint32_t (&bs)[XSLOT]) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t r0 = t0 + wave * (64 * XSLOT) + lane;
+  if (t0 + XTILE <= n) {   // uniform: a full tile's loads are unconditional, all in flight together
+#pragma unroll
+    for (int s = 0; s < XSLOT; ++s) {
+      z[s] = c.z[r0 + 64 * s];
+      bs[s] = (uint32_t)c.bin[r0 + 64 * s] | (SH ? (uint32_t)c.sh[r0 + 64 * s] << 16 : 0u);
+    }
+  } else {
+#pragma unroll
+    for (int s = 0; s < XSLOT; ++s) {
+      const int64_t r = r0 + 64 * s;
+      z[s] = r < n ? c.z[r] : 0ull;
+      bs[s] = r < n ? ((uint32_t)c.bin[r] | (SH ? (uint32_t)c.sh[r] << 16 : 0u)) : 0u;
+    }
+  }
+}
+
+// cnt[d * ntiles + tile] = rows of the tile bound for d (destination-major: the exclusive scan of cnt
+// is each (destination, tile)'s first output row); dtot[d] += the same
+template <bool SH>
+__global__ __launch_bounds__(XT) void k_part_count(KeyCols c, int64_t n, const uint64_t* __restrict__ split, int ns,
+                                                   int nbits, uint32_t* __restrict__ cnt, int64_t ntiles,
+                                                   unsigned long long* __restrict__ dtot) {
+  __shared__ SplitLds s_sp;
+  __shared__ uint32_t s_c[XMAX];
+  const int nd = ns + 1, lane = threadIdx.x & 63;
+  load_splitters(s_sp, split, ns);
+  for (int d = threadIdx.x; d < nd; d += XT) s_c[d] = 0u;
+  __syncthreads();
+  const int64_t tile = blockIdx.x, t0 = tile * XTILE;
+  uint64_t z[XSLOT];
+  uint32_t bs[XSLOT];
+  part_load_tile<SH>(c, t0, n, z, bs);
+  const int wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int s = 0; s < XSLOT; ++s) {
+    const bool ok = t0 + wave * (64 * XSLOT) + 64 * s + lane < n;
+    const uint32_t d = ok ? (uint32_t)part_dest(s_sp, ns, bs[s], z[s]) : 0u;
+    const uint64_t m = match_dest(d, ok, nbits);
+    if (ok && (m & lanemask_lt()) == 0) atomicAdd(&s_c[d], (uint32_t)__popcll(m));   // one add per destination
+  }
+  __syncthreads();
+  for (int d = threadIdx.x; d < nd; d += XT) {
+    const uint32_t v = s_c[d];
+    cnt[(int64_t)d * ntiles + tile] = v;
+    if (v) atomicAdd(&dtot[d], (unsigned long long)v);
+  }
+}
+
+// The tile ranked per destination in LDS and written as destination runs.  offs = the exclusive scan
+// of k_part_count's cnt.  Per row: z_out, bin_out, shard_out (SH), and the row's source as ids_out =
+// ids[row] (IDS) or id_base + row, and / or rows_out = row (u32); either output may be null.
+template <bool SH, bool IDS>
+__global__ __launch_bounds__(XT) void k_part_scatter(KeyCols c, int64_t n, const uint64_t* __restrict__ split, int ns,
+                                                     int nbits, const int64_t* __restrict__ offs, int64_t ntiles,
+                                                     const int64_t* __restrict__ ids, int64_t id_base,
+                                                     int64_t* __restrict__ ids_out, uint32_t* __restrict__ rows_out,
+                                                     uint8_t* __restrict__ sh_out, uint16_t* __restrict__ bin_out,
+                                                     uint64_t* __restrict__ z_out) {
+  __shared__ SplitLds s_sp;
+  __shared__ uint4 s_rec[XTILE];                 // {z lo, z hi, bs, tile row | destination << 16}
+  __shared__ uint16_t s_wcnt[XT / 64][XMAX];     // per wave: rows of each destination (then: wave offsets)
+  __shared__ uint32_t s_dstart[XMAX];            // the destination's first slot in the tile
+  __shared__ int64_t s_g[XMAX];                  // output row of tile slot q = s_g[d] + q
+  __shared__ uint32_t s_wsum[XT / 64];
+  const int nd = ns + 1, t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  load_splitters(s_sp, split, ns);
+  for (int i = t; i < (XT / 64) * XMAX; i += XT) (&s_wcnt[0][0])[i] = 0;
+  __syncthreads();
+  const int64_t tile = blockIdx.x, t0 = tile * XTILE;
+  uint64_t z[XSLOT];
+  uint32_t bs[XSLOT];
+  part_load_tile<SH>(c, t0, n, z, bs);
+  uint32_t rd[XSLOT];   // wave rank | destination << 16; rank 0xffff = no row
+  const uint64_t lt = lanemask_lt();
+#pragma unroll
+  for (int s = 0; s < XSLOT; ++s) {
+    const bool ok = t0 + wave * (64 * XSLOT) + 64 * s + lane < n;
+    const uint32_t d = ok ? (uint32_t)part_dest(s_sp, ns, bs[s], z[s]) : 0u;
+    const uint64_t m = match_dest(d, ok, nbits);
+    const int r = __popcll(m & lt);
+    const uint32_t c0 = s_wcnt[wave][d];
+    rd[s] = (ok ? c0 + r : 0xffffu) | (d << 16);
+    __builtin_amdgcn_wave_barrier();
+    if (ok && r == 0) s_wcnt[wave][d] = (uint16_t)(c0 + __popcll(m));
+    __builtin_amdgcn_wave_barrier();
+  }
+  __syncthreads();
+  // thread d: its wave offsets and tile total, then a block scan of the totals over destinations
+  uint32_t tot = 0;
+  if (t < nd) {
+#pragma unroll
+    for (int v = 0; v < XT / 64; ++v) {
+      const uint32_t cv = s_wcnt[v][t];
+      s_wcnt[v][t] = (uint16_t)tot;
+      tot += cv;
+    }
+  }
+  uint32_t x = tot;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) s_wsum[wave] = x;
+  __syncthreads();
+  if (t < nd) {
+    uint32_t p = 0;
+    for (int v = 0; v < wave; ++v) p += s_wsum[v];
+    const uint32_t ds = p + x - tot;
+    s_dstart[t] = ds;
+    s_g[t] = offs[(int64_t)t * ntiles + tile] - (int64_t)ds;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int s = 0; s < XSLOT; ++s) {
+    const uint32_t r = rd[s] & 0xffffu, d = rd[s] >> 16;
+    if (r == 0xffffu) continue;
+    const uint32_t row = (uint32_t)(wave * (64 * XSLOT) + 64 * s + lane);
+    s_rec[s_dstart[d] + s_wcnt[wave][d] + r] = make_uint4((uint32_t)z[s], (uint32_t)(z[s] >> 32), bs[s], row | (d << 16));
+  }
+  __syncthreads();
+  const int cntt = (int)min((int64_t)XTILE, n - t0);
+  for (int q = t; q < cntt; q += XT) {
+    const uint4 v = s_rec[q];
+    const int64_t g = s_g[v.w >> 16] + q;
+    const int64_t row = t0 + (v.w & 0xffffu);
+    z_out[g] = (uint64_t)v.x | ((uint64_t)v.y << 32);
+    bin_out[g] = (uint16_t)v.z;
+    if (SH) sh_out[g] = (uint8_t)(v.z >> 16);
+    if (ids_out) ids_out[g] = IDS ? ids[row] : id_base + row;
+    if (rows_out) rows_out[g] = (uint32_t)row;
+  }
+}
+
+// n_samples keys at rows floor((2i + 1) n / (2 n_samples)): out[2i] = shard << 16 | bin (u16), out[2i + 1] = z
+template <bool SH>
+__global__ __launch_bounds__(256) void k_key_sample(KeyCols c, int64_t n, int ns, uint64_t* __restrict__ out) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= ns) return;
+  const int64_t r = (int64_t)((uint64_t)(2 * i + 1) * (uint64_t)n / (2 * (uint64_t)ns));   // < 2^49: ns <= 2^16, n < 2^32
+  out[2 * i] = (uint64_t)c.bin[r] | (SH ? (uint64_t)c.sh[r] << 16 : 0ull);
+  out[2 * i + 1] = c.z[r];
+}
+
 }  // namespace gm
 
 using namespace gm;
@@ -727,13 +922,34 @@ int gm_z3_key_bytes(gm_ctx* ctx, const uint8_t* shard, const int16_t* bin, const
   return GM_OK;
 }
 
+int gm_z2_key_bytes(gm_ctx* ctx, const uint8_t* shard, const int64_t* z, int64_t n, uint8_t* out) {
+  if (!ctx || n < 0) return GM_E_INVALID;
+  if (n == 0) return GM_OK;
+  if (!z || !out) return GM_E_INVALID;
+  hipLaunchKernelGGL(k_key_bytes, dim3((unsigned)((n + STPB - 1) / STPB)), dim3(STPB), 0, ctx->stream, shard, nullptr, z,
+                     n, shard ? 9 : 8, out);
+  GM_CHECK_LAUNCH();
+  return GM_OK;
+}
+
 int gm_sort_keys(gm_ctx* ctx, const uint8_t* shard, const int16_t* bin, const int64_t* z, int64_t n,
                  uint8_t* shard_out, int16_t* bin_out, int64_t* z_out, int64_t* perm_out) {
   if (!ctx || n < 0 || n > (int64_t)UINT32_MAX) return GM_E_INVALID;
   if (n == 0) return GM_OK;
-  if (!bin || !z || !bin_out || !z_out || !perm_out || ((shard == nullptr) != (shard_out == nullptr)))
+  if (!z || !z_out || !perm_out || ((shard == nullptr) != (shard_out == nullptr)) ||
+      ((bin == nullptr) != (bin_out == nullptr)))
     return GM_E_INVALID;
   hipStream_t s = ctx->stream;
+  if (!bin) {
+    // no time bin (Z2 / XZ2 tables): the sort runs over a zero bin column (constant, so no digit pass
+    // looks at it) and its bin output goes to scratch
+    void* zb = nullptr;
+    int rc = ctx_workspace(ctx, WS_SCAN, (((size_t)n * 2 + 15) & ~(size_t)15) * 2, &zb);
+    if (rc) return rc;
+    bin = (const int16_t*)zb;
+    bin_out = (int16_t*)((char*)zb + (((size_t)n * 2 + 15) & ~(size_t)15));
+    GM_HIP(hipMemsetAsync(zb, 0, (size_t)n * 2, s));
+  }
   const uint8_t* sh = shard;
   const KeyCols in{sh, (const uint16_t*)bin, (const uint64_t*)z};
   // 16-B z / 4-B bin / 2-B shard pair loads need aligned caller columns
@@ -877,6 +1093,89 @@ int gm_sort_keys(gm_ctx* ctx, const uint8_t* shard, const int16_t* bin, const in
   }
   ctx->sort_last = (int64_t)lsd.size() + (prefix_mode ? npre : 0);   // (a failed prefix attempt included)
   return passes(lsd, 8, true, prefix_mode ? npre : 0);
+}
+
+int gm_key_sample(gm_ctx* ctx, const uint8_t* shard, const int16_t* bin, const int64_t* z, int64_t n, int32_t n_samples,
+                  uint64_t* key_hi, uint64_t* key_lo) {
+  if (!ctx || n < 0 || n > (int64_t)UINT32_MAX || n_samples < 0 || n_samples > 65536) return GM_E_INVALID;
+  if (n == 0 || n_samples == 0) return GM_OK;
+  if (!bin || !z || !key_hi || !key_lo) return GM_E_INVALID;
+  void* ws = nullptr;
+  int rc = ctx_workspace(ctx, WS_SCAN, (size_t)n_samples * 16, &ws);
+  if (rc) return rc;
+  const KeyCols in{shard, (const uint16_t*)bin, (const uint64_t*)z};
+  const dim3 g((unsigned)((n_samples + 255) / 256));
+  if (shard) hipLaunchKernelGGL(k_key_sample<true>, g, dim3(256), 0, ctx->stream, in, n, (int)n_samples, (uint64_t*)ws);
+  else hipLaunchKernelGGL(k_key_sample<false>, g, dim3(256), 0, ctx->stream, in, n, (int)n_samples, (uint64_t*)ws);
+  GM_CHECK_LAUNCH();
+  std::vector<uint64_t> h((size_t)n_samples * 2);
+  rc = copy_d2h(ctx, h.data(), ws, h.size() * 8);
+  if (rc) return rc;
+  for (int32_t i = 0; i < n_samples; ++i) {
+    key_hi[i] = h[2 * (size_t)i];
+    key_lo[i] = h[2 * (size_t)i + 1];
+  }
+  return GM_OK;
+}
+
+int gm_key_partition(gm_ctx* ctx, const uint8_t* shard, const int16_t* bin, const int64_t* z, int64_t n,
+                     const uint64_t* split_hi, const uint64_t* split_lo, int32_t n_split, const int64_t* ids,
+                     int64_t id_base, uint8_t* shard_out, int16_t* bin_out, int64_t* z_out, int64_t* ids_out,
+                     uint32_t* rows_out, int64_t* dest_counts) {
+  if (!ctx || n < 0 || n > (int64_t)UINT32_MAX || n_split < 0 || n_split >= XMAX || !dest_counts) return GM_E_INVALID;
+  if (n_split > 0 && (!split_hi || !split_lo)) return GM_E_INVALID;
+  for (int32_t k = 0; k < n_split; ++k) {   // ascending splitters, keys of 24 bits + 64 bits
+    if (split_hi[k] >> 24) return set_error("gm_key_partition: splitter hi past 24 bits"), GM_E_INVALID;
+    if (k > 0 && (split_hi[k] < split_hi[k - 1] || (split_hi[k] == split_hi[k - 1] && split_lo[k] < split_lo[k - 1])))
+      return set_error("gm_key_partition: splitters not ascending"), GM_E_INVALID;
+  }
+  const int nd = n_split + 1;
+  for (int d = 0; d < nd; ++d) dest_counts[d] = 0;
+  if (n == 0) return GM_OK;
+  if (!bin || !z || !bin_out || !z_out || ((shard == nullptr) != (shard_out == nullptr))) return GM_E_INVALID;
+  hipStream_t s = ctx->stream;
+  const int64_t ntiles = (n + XTILE - 1) / XTILE, ncnt = ntiles * nd;
+  // workspace: splitters | counts (u32, destination-major) | their scan (i64) | scan partials | totals
+  auto al = [](size_t v) { return (v + 15) & ~(size_t)15; };
+  const size_t a_s = al((size_t)std::max(1, n_split) * 16), a_c = al((size_t)ncnt * 4), a_o = al((size_t)ncnt * 8),
+               a_p = al((size_t)scan_partials_len(ncnt) * 8), a_t = al((size_t)nd * 8);
+  void* base = nullptr;
+  int rc = ctx_workspace(ctx, WS_SCAN, a_s + a_c + a_o + a_p + a_t, &base);
+  if (rc) return rc;
+  char* q = (char*)base;
+  uint64_t* split = (uint64_t*)q; q += a_s;
+  uint32_t* cnt = (uint32_t*)q; q += a_c;
+  int64_t* offs = (int64_t*)q; q += a_o;
+  int64_t* partials = (int64_t*)q; q += a_p;
+  unsigned long long* dtot = (unsigned long long*)q;
+  if (n_split > 0) {
+    std::vector<uint64_t> hs((size_t)n_split * 2);
+    for (int32_t k = 0; k < n_split; ++k) { hs[2 * (size_t)k] = split_hi[k]; hs[2 * (size_t)k + 1] = split_lo[k]; }
+    rc = copy_h2d(ctx, split, hs.data(), hs.size() * 8);
+    if (rc) return rc;
+  }
+  GM_HIP(hipMemsetAsync(dtot, 0, (size_t)nd * 8, s));
+  int nbits = 0;
+  while ((1 << nbits) < nd) ++nbits;
+  const KeyCols in{shard, (const uint16_t*)bin, (const uint64_t*)z};
+  const dim3 grid((unsigned)ntiles);
+  if (shard) hipLaunchKernelGGL(k_part_count<true>, grid, dim3(XT), 0, s, in, n, split, n_split, nbits, cnt, ntiles, dtot);
+  else hipLaunchKernelGGL(k_part_count<false>, grid, dim3(XT), 0, s, in, n, split, n_split, nbits, cnt, ntiles, dtot);
+  GM_CHECK_LAUNCH();
+  launch_excl_scan<uint32_t, int64_t>(s, cnt, ncnt, offs, partials, nullptr);
+  GM_CHECK_LAUNCH();
+  void (*kern)(KeyCols, int64_t, const uint64_t*, int, int, const int64_t*, int64_t, const int64_t*, int64_t, int64_t*,
+               uint32_t*, uint8_t*, uint16_t*, uint64_t*) =
+      shard ? (ids ? k_part_scatter<true, true> : k_part_scatter<true, false>)
+            : (ids ? k_part_scatter<false, true> : k_part_scatter<false, false>);
+  hipLaunchKernelGGL(kern, grid, dim3(XT), 0, s, in, n, split, n_split, nbits, offs, ntiles, ids, id_base, ids_out, rows_out,
+                     shard_out, (uint16_t*)bin_out, (uint64_t*)z_out);
+  GM_CHECK_LAUNCH();
+  std::vector<unsigned long long> ht(nd);
+  rc = copy_d2h(ctx, ht.data(), dtot, (size_t)nd * 8);
+  if (rc) return rc;
+  for (int d = 0; d < nd; ++d) dest_counts[d] = (int64_t)ht[d];
+  return GM_OK;
 }
 
 }  // extern "C"

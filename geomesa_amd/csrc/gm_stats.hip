@@ -234,6 +234,9 @@ __global__ __launch_bounds__(HTPB) void k_z3_hist_lds(const double* __restrict__
     const int64_t np = a.n >> 1;
     // software-pipelined: the next HU pairs per lane are in flight while the current ones are binned
     constexpr int HU = 2;
+    // at least one block iteration between drains for the smaller (unobserve) room, or `since` never
+    // meets drain_every and the packed fields carry into their neighbours
+    static_assert(((1 << 20) - 1) / (HTPB * 2 * HU) - 1 >= 1, "WIDE drain schedule: HTPB * HU too large");
     const int drain_every = (int)(room / (HTPB * 2 * HU)) - 1;   // -1: the odd last row of block 0
     dv2 xa[HU], ya[HU];
     lv2 ta[HU];
@@ -270,6 +273,7 @@ __global__ __launch_bounds__(HTPB) void k_z3_hist_lds(const double* __restrict__
     }
     if ((a.n & 1) && blockIdx.x == 0 && threadIdx.x == 0) one(x[a.n - 1], y[a.n - 1], t[a.n - 1]);
   } else {
+    static_assert(((1 << 20) - 1) / HTPB >= 1, "WIDE drain schedule: HTPB too large");
     const int drain_every = (int)(room / HTPB);
     for (int64_t ib = (int64_t)blockIdx.x * HTPB; ib < a.n; ib += stride) {
       const int64_t i = ib + threadIdx.x;

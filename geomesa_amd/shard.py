@@ -244,8 +244,11 @@ def merge_histograms(pg, counts, present, bin_lo, length=None):
 # configs[2]: the table's rows are split into `world` contiguous key ranges, one per GPU, the way a
 # sorted store splits a table into tablets / regions; a query's scan ranges are clipped to each
 # slice (what the client's range binning does per tablet) and every GPU scans only its part.
-# Keys compare as the row bytes do: [shard][bin BE16][z BE64], unsigned.  In torch they are carried
-# as two int64 columns with the same lexicographic order:
+# Keys compare as the row bytes do: [shard][bin BE16][z BE64], unsigned.  The ingest (every rank's
+# unsorted rows -> sample_keys -> choose_splitters -> partition_rows -> exchange_partitioned -> one
+# gm_sort_keys of the received slice) carries them as (key_hi = shard << 16 | bin as u16, key_lo = z)
+# uint64 pairs; the slice bounds and range clipping below use two int64 values of the same
+# lexicographic order:
 #   hi = shard << 16 | bin as unsigned short       lo = z with the sign bit flipped
 
 _SIGN = -(1 << 63)
@@ -260,95 +263,102 @@ def table_key(shard, bin, z):
     return hi, z.to(torch.int64) ^ _SIGN
 
 
-def key_columns(hi, lo, sharded):
-    """Inverse of table_key: (shard uint8 or None, bin int16, z int64)."""
-    import torch
-    b = (((hi & 0xffff) ^ 0x8000) - 0x8000).to(torch.int16)
-    return ((hi >> 16).to(torch.uint8) if sharded else None), b, lo ^ _SIGN
+def sample_keys(ctx, shard, bin, z, samples=1024):
+    """`samples` keys of one rank's UNSORTED key columns (evenly spaced rows), gm_key_sample: (key_hi,
+    key_lo) uint64 numpy arrays, key_hi = shard << 16 | bin as u16, key_lo = z -- the row-key byte order."""
+    from . import _lib
+    n = int(z.numel())
+    k = min(int(samples), 65536) if n else 0
+    hi, lo = np.zeros(k, np.uint64), np.zeros(k, np.uint64)
+    if k:
+        _lib.check(ctx.lib.gm_key_sample(ctx.handle, _lib.ptr(shard), _lib.ptr(bin), _lib.ptr(z), n, k,
+                                         hi.ctypes.data, lo.ctypes.data), "gm_key_sample")
+    return hi, lo
 
 
-def sample_splitters(pg, hi, lo, samples=1024):
-    """world - 1 splitter keys (numpy int64 (hi, lo) arrays, identical on every rank) from `samples`
-    evenly spaced keys of each rank's SORTED local columns, weighted by the rank's row count, so each
-    key range holds about 1/world of all rows.  One all_gather of samples x 2 int64 per rank."""
+def choose_splitters(pg, s_hi, s_lo, n, samples=1024):
+    """world - 1 splitter keys (key_hi, key_lo uint64 numpy arrays, identical on every rank) from every
+    rank's key sample (sample_keys of its n rows, at most `samples` keys), each sample weighted by the
+    rows it stands for, so each key range holds about 1/world of all rows.  One all_gather of the
+    samples (host planning, like a client's split planning; no per-splitter device sync)."""
     import torch
     world = pg.get_world_size() if pg is not None else 1
-    n = int(hi.numel())
     if world == 1:
-        return np.zeros(0, np.int64), np.zeros(0, np.int64)
+        return np.zeros(0, np.uint64), np.zeros(0, np.uint64)
+    k = len(s_hi)
+    cap = max(1, min(int(samples), 65536))
+    if k > cap:
+        raise ValueError("%d samples for a cap of %d" % (k, cap))
     dev = _device_of(pg)
-    s = torch.zeros((samples, 3), dtype=torch.int64)
-    if n:
-        pos = ((torch.arange(samples, dtype=torch.float64) + 0.5) * (n / samples)).to(torch.int64).clamp_(0, n - 1)
-        pos = pos.to(hi.device)
-        s[:, 0] = hi[pos].cpu()
-        s[:, 1] = lo[pos].cpu()
-        s[:, 2] = n
+    s = torch.zeros((cap, 4), dtype=torch.int64)
+    if k:
+        s[:k, 0] = torch.from_numpy(np.ascontiguousarray(s_hi, np.uint64).view(np.int64))
+        s[:k, 1] = torch.from_numpy(np.ascontiguousarray(s_lo, np.uint64).view(np.int64))
+        s[:k, 2] = int(n)
+        s[:k, 3] = k
     parts = [torch.zeros_like(s).to(dev) for _ in range(world)]
     pg.all_gather(parts, s.to(dev))
     allv = torch.cat([p.cpu() for p in parts]).numpy()
-    w = allv[:, 2].astype(np.float64) / samples       # rows each sample stands for
-    keep = w > 0
-    allv, w = allv[keep], w[keep]
+    keep = allv[:, 3] > 0
+    allv = allv[keep]
     if len(allv) == 0:
-        return np.zeros(world - 1, np.int64), np.zeros(world - 1, np.int64)
-    order = np.lexsort((allv[:, 1], allv[:, 0]))
-    allv, cw = allv[order], np.cumsum(w[order])
-    total = cw[-1]
-    idx = np.minimum(np.searchsorted(cw, total * np.arange(1, world) / world, side="left"), len(allv) - 1)
-    return allv[idx, 0].copy(), allv[idx, 1].copy()
+        return np.zeros(world - 1, np.uint64), np.zeros(world - 1, np.uint64)
+    w = allv[:, 2].astype(np.float64) / allv[:, 3]       # rows each sample stands for
+    hi, lo = allv[:, 0].view(np.uint64), allv[:, 1].view(np.uint64)
+    order = np.lexsort((lo, hi))
+    cw = np.cumsum(w[order])
+    idx = np.minimum(np.searchsorted(cw, cw[-1] * np.arange(1, world) / world, side="left"), len(allv) - 1)
+    return hi[order][idx].copy(), lo[order][idx].copy()
 
 
-def split_positions(hi, lo, s_hi, s_lo):
-    """Row positions of the splitters in SORTED local (hi, lo) columns: p[k] = rows with key below
-    splitter k - 1 (p[0] = 0, p[world] = n); a key equal to a splitter goes to the upper range."""
+def partition_rows(ctx, shard, bin, z, sp_hi, sp_lo, ids=None, id_base=0, rows=False):
+    """The rank's rows grouped by destination key range (gm_key_partition: one count read, a device scan,
+    one scatter read; stable within a destination).  Returns ([shard?, bin, z, src], counts): device
+    columns in destination order -- src = ids[row] (ids given, int64), the input row as int32 (rows=True:
+    4 B on the wire instead of 8) or id_base + row (int64) -- and the per-destination row counts."""
     import torch
-    n = int(hi.numel())
-    pos = [0]
-    for sh, sl in zip(s_hi.tolist(), s_lo.tolist()):
-        t = torch.tensor([sh], dtype=torch.int64, device=hi.device)
-        a = int(torch.searchsorted(hi, t, right=False).item())
-        b = int(torch.searchsorted(hi, t, right=True).item())
-        c = a
-        if b > a:
-            c = a + int(torch.searchsorted(lo[a:b].contiguous(), torch.tensor([sl], dtype=torch.int64,
-                                                                               device=hi.device)).item())
-        pos.append(max(c, pos[-1]))
-    pos.append(max(n, pos[-1]))
-    return pos
+    from . import _lib
+    n = int(z.numel())
+    nd = len(sp_hi) + 1
+    dev = z.device
+    sh_o = torch.empty(n, dtype=torch.uint8, device=dev) if shard is not None else None
+    b_o, z_o = torch.empty(n, dtype=torch.int16, device=dev), torch.empty(n, dtype=torch.int64, device=dev)
+    src = torch.empty(n, dtype=torch.int32 if rows else torch.int64, device=dev)
+    counts = np.zeros(nd, np.int64)
+    hi = np.ascontiguousarray(sp_hi, np.uint64)
+    lo = np.ascontiguousarray(sp_lo, np.uint64)
+    _lib.check(ctx.lib.gm_key_partition(ctx.handle, _lib.ptr(shard), _lib.ptr(bin), _lib.ptr(z), n,
+                                        hi.ctypes.data if len(hi) else None, lo.ctypes.data if len(lo) else None,
+                                        len(hi), _lib.ptr(ids), int(id_base), _lib.ptr(sh_o), _lib.ptr(b_o),
+                                        _lib.ptr(z_o), None if rows else _lib.ptr(src), _lib.ptr(src) if rows else None,
+                                        counts.ctypes.data), "gm_key_partition")
+    cols = ([sh_o] if shard is not None else []) + [b_o, z_o, src]
+    return cols, counts.tolist()
 
 
-def exchange_by_key_range(pg, hi, lo, cols=(), samples=1024):
-    """All-to-all of SORTED local rows by key range: rank r receives every row whose key falls in
-    [splitter r-1, splitter r).  hi / lo / cols are 1-D int64 tensors of one length.  One all_to_all
-    of the counts, then one of the rows packed as (hi, lo, cols...) int64 records -- over RCCL a
-    grouped send / recv on every xGMI link at once.  Returns (hi, lo, cols, (s_hi, s_lo)) of the
-    received rows: `world` sorted runs, one per sender, in rank order (the caller re-sorts)."""
-    s_hi, s_lo = sample_splitters(pg, hi, lo, samples)
-    if pg is None or pg.get_world_size() == 1:
-        return hi, lo, list(cols), (s_hi, s_lo)
-    return _exchange_rows(pg, hi, lo, cols, s_hi, s_lo) + ((s_hi, s_lo),)
-
-
-def _exchange_rows(pg, hi, lo, cols, s_hi, s_lo):
-    """The exchange step of exchange_by_key_range for given splitters (valid at any world size; a
-    world of 1 keeps every row -- the RCCL test at world 1 runs it): (hi, lo, cols) received."""
+def exchange_partitioned(pg, cols, send):
+    """All-to-all of destination-grouped columns (partition_rows): rank r receives every peer's
+    destination-r slice of each column, in rank order.  One all_to_all of the counts, then one per column
+    (each column moved as bytes, so any dtype travels: RCCL has no int16); over RCCL every xGMI link
+    carries its peer's slice at once.  Returns (received columns, received counts per source rank)."""
     import torch
     world = pg.get_world_size()
     dev = _device_of(pg)
-    home = hi.device
-    pos = split_positions(hi, lo, s_hi, s_lo)
-    send = [pos[k + 1] - pos[k] for k in range(world)]
-    sc = torch.tensor(send, dtype=torch.int64, device=dev)
+    sc = torch.tensor([int(v) for v in send], dtype=torch.int64, device=dev)
     rc = torch.empty(world, dtype=torch.int64, device=dev)
     pg.all_to_all_single(rc, sc)
     recv = [int(v) for v in rc.cpu().tolist()]
-    rec = torch.stack([hi, lo] + [c.to(torch.int64) for c in cols], 1).to(dev).contiguous()
-    out = torch.empty((sum(recv), rec.shape[1]), dtype=torch.int64, device=dev)
-    pg.all_to_all_single(out, rec, recv, send)
-    del rec
-    out = out.to(home)
-    return out[:, 0].contiguous(), out[:, 1].contiguous(), [out[:, 2 + k].contiguous() for k in range(len(cols))]
+    out = []
+    def as_bytes(t):   # (an empty tensor has no byte view)
+        return t.contiguous().view(torch.uint8) if t.numel() else torch.empty(0, dtype=torch.uint8, device=t.device)
+    for c in cols:
+        k = c.element_size()
+        src = as_bytes(c).to(dev)
+        o = torch.empty(sum(recv) * k, dtype=torch.uint8, device=dev)
+        pg.all_to_all_single(o, src, [r * k for r in recv], [int(s) * k for s in send])
+        del src
+        out.append(o.to(c.device).view(c.dtype) if o.numel() else torch.empty(0, dtype=c.dtype, device=c.device))
+    return out, recv
 
 
 def clip_key_ranges(ranges, kmin, kmax):

@@ -125,46 +125,101 @@ class Z3Table:
 class PartitionedZ3Table:
     """configs[2]: a Z3 table range-partitioned over the GPUs of a process group, one slice per rank.
 
-    Every rank starts from its own rows (any split), keys them, sorts them (gm_sort_keys), and the
-    ranks agree on world - 1 splitter keys sampled from the sorted slices; one all-to-all moves every
-    row to the rank owning its key range (shard.exchange_by_key_range), which sorts what it received.
-    Afterwards rank r holds the rows of keys [splitter r-1, splitter r) in table order -- a sorted
-    store's table split into tablets / regions (the shard prefix of ShardStrategy.scala:75-80 stays
-    the key's first byte).  A query's scan ranges (getRangeBytes, Z3IndexKeySpace.scala:196-238) are
-    clipped to the slice's first and last key (the per-tablet range binning of a batch scanner) and
-    each rank scans only those; the ids that come back are global row ids, so the union over ranks
-    equals the scan of one unpartitioned table.  The slice keeps the ids in the order its rows arrived
-    (src_ids) beside the table's permutation, so a scan maps only its matches to ids (the seek
-    already resolves table rows through the permutation) instead of the ingest permuting every id.
-    pg None = a single unpartitioned slice."""
+    Every rank starts from its own UNSORTED key columns (any split).  The ranks sample keys
+    (gm_key_sample), agree on world - 1 splitter keys (one all_gather, host planning), and each rank
+    writes its rows grouped by destination key range in one partition pass (gm_key_partition); one
+    all-to-all per column moves every row to the rank owning its key range, which sorts what it
+    received once (gm_sort_keys) -- one sort per rank, no sort before the exchange.  Afterwards rank r
+    holds the rows of keys [splitter r-1, splitter r) in table order -- a sorted store's table split into
+    tablets / regions (the shard prefix of ShardStrategy.scala:75-80 stays the key's first byte).  A
+    query's scan ranges (getRangeBytes, Z3IndexKeySpace.scala:196-238) are clipped to the slice's first
+    and last key (the per-tablet range binning of a batch scanner) and each rank scans only those; the
+    ids that come back are global row ids, so the union over ranks equals the scan of one unpartitioned
+    table.  The slice keeps each received row's source beside the table's permutation, so a scan maps
+    only its matches to ids.  `ids` is either a column of global ids (8 B per row on the wire) or one
+    int, the id of the rank's first row (ids = ids + row: 4-B rows on the wire, mapped back through the
+    senders' bases).  pg None = a single unpartitioned slice.  `timing` holds the ingest's phases (ms,
+    HIP events on the context stream)."""
 
     def __init__(self, pg, bins, z, ids, shard=None, shards=None, period="week", samples=1024):
         import torch
         from . import shard as S
+        from .curve import _dev_col
         self.pg = pg
-        local = Z3Table(bins, z, shard, period)
         sharded = shard is not None
+        self.timing = {}
+        self._recv_end, self._id_base = None, 0
+        compact = isinstance(ids, (int, np.integer))
         if pg is None or pg.get_world_size() == 1:   # one slice: the local table is the table
-            self.table, self.splitters = local, (np.zeros(0, np.int64), np.zeros(0, np.int64))
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+            ev[0].record()
+            local = Z3Table(bins, z, shard, period)
+            ev[1].record()
+            self.table, self.splitters = local, (np.zeros(0, np.uint64), np.zeros(0, np.uint64))
             if sharded and shards:
                 self.table.shards = int(shards)
-            self.src_ids = torch.as_tensor(ids).to(local.z.device, torch.int64)
+            dev = local.z.device
+            self._recv_end, self._id_base = None, int(ids) if compact else 0
+            self.src_ids = None if compact else torch.as_tensor(ids).to(dev, torch.int64)
             self.n = local.n
+            ev[1].synchronize()
+            self.timing = {"sort_ms": ev[0].elapsed_time(ev[1])}
             self._bounds()
             return
-        hi, lo = S.table_key(local.shard, local.bin, local.z)
-        gid = torch.as_tensor(ids).to(local.z.device, torch.int64)[local.perm]
-        del local
-        hi, lo, (gid,), self.splitters = S.exchange_by_key_range(pg, hi, lo, [gid], samples)
-        sh, b, zz = S.key_columns(hi, lo, sharded)
-        del hi, lo
+        ctx = _lib.context()
+        bins, z = _dev_col(bins, torch.int16), _dev_col(z, torch.int64)
+        dev = z.device
+        sh_in = None
+        if sharded:
+            sh_in = torch.as_tensor(np.asarray(shard, np.uint8) if not isinstance(shard, torch.Tensor) else shard,
+                                    dtype=torch.uint8).to(dev).contiguous()
+        id_col = None if compact else torch.as_tensor(ids).to(dev, torch.int64).contiguous()
+        n = int(z.numel())
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+        ev[0].record()
+        s_hi, s_lo = S.sample_keys(ctx, sh_in, bins, z, samples)
+        self.splitters = S.choose_splitters(pg, s_hi, s_lo, n, samples)
+        cols, send = S.partition_rows(ctx, sh_in, bins, z, *self.splitters, ids=id_col,
+                                      id_base=int(ids) if compact else 0, rows=compact)
+        ev[1].record()
+        del id_col
+        cols, recv = S.exchange_partitioned(pg, cols, send)
+        ev[2].record()
+        src = cols.pop()
+        sh, b, zz = (cols if sharded else [None] + cols)
+        del cols
         self.table = Z3Table(b, zz, sh, period)
+        ev[3].record()
+        del sh, b, zz
         if sharded:
             self.table.shards = int(shards) if shards else (
                 int(S.all_reduce_scalar(pg, float(self.table.shards or 0), "max")))
-        self.src_ids = gid   # global row id of each received row (the table's perm maps table rows to them)
+        if compact:   # received row r of source rank k: id = base_k + its 4-B row
+            bases = torch.tensor([int(ids)], dtype=torch.int64, device=S._device_of(pg))
+            allb = [torch.zeros_like(bases) for _ in range(pg.get_world_size())]
+            pg.all_gather(allb, bases)
+            self._src_rows = src
+            self._src_base = torch.cat([v.to(dev) for v in allb])
+            self._recv_end = torch.as_tensor(np.cumsum(recv), dtype=torch.int64, device=dev)
+            self.src_ids = None
+        else:
+            self.src_ids = src   # global row id of each received row (the table's perm maps table rows to them)
         self.n = self.table.n
+        ev[3].synchronize()
+        self.timing = {"partition_ms": ev[0].elapsed_time(ev[1]), "exchange_ms": ev[1].elapsed_time(ev[2]),
+                       "sort_ms": ev[2].elapsed_time(ev[3]), "sent_rows": [int(v) for v in send],
+                       "received_rows": [int(v) for v in recv]}
         self._bounds()
+
+    def source_ids(self, rows):
+        """Global ids of received (slice input) rows."""
+        import torch
+        if self.src_ids is not None:
+            return self.src_ids[rows]
+        if self._recv_end is None:   # one slice with contiguous ids
+            return rows + self._id_base
+        k = torch.searchsorted(self._recv_end, rows, right=True)
+        return self._src_base[k] + (self._src_rows[rows].to(torch.int64) & 0xFFFFFFFF)
 
     def _bounds(self):
         """The slice's first and last key (the clipping bounds)."""
@@ -194,7 +249,7 @@ class PartitionedZ3Table:
         arr, _ = key_ranges(scan_ranges, self.table.shards)
         arr = self.clip(arr)
         rows, nm, ns = self.table.scan_key_ranges(arr, z3filter, map_rows=True)   # input rows of the slice
-        return self.src_ids[rows], nm, ns, len(arr)
+        return self.source_ids(rows), nm, ns, len(arr)
 
     def query(self, bboxes=None, intervals=None, target=2000):
         """bbox + during query (Z3Filter on the rows of the clipped ranges) on this rank's slice."""

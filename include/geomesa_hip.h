@@ -115,6 +115,10 @@ const char* gm_last_error(void);
                                    fewer than 2^14 polygons 8 sub-blocks with EMPTY and INTERIOR-of-one-
                                    polygon bits, else 16 EMPTY bits), 0 = EMPTY bits, 1 = EMPTY and
                                    INTERIOR bits.  Results never change */
+#define GM_PARAM_INDEX_CORE_RETIRED 7 /* ABI change (round 5): gm_pip_index_core and its parameter 7
+                                   (the row predicate's per-polygon core rectangles) were removed with the
+                                   rectangles.  Kept for one release as an accepted no-op: setting it
+                                   succeeds and changes nothing, reading it returns 0 */
 #define GM_PARAM_HIST_GRID 8    /* gm_z3_histogram: workgroups of the LDS-counter kernel (0 = default: one
                                    resident wave of workgroups); fewer workgroups each count more features
                                    and drain their packed counters more often.  Results never change */
@@ -166,6 +170,13 @@ int gm_xz2_index(gm_ctx* ctx, const double* xmin, const double* ymin, const doub
 int gm_xz3_index(gm_ctx* ctx, const double* xmin, const double* ymin, const double* zmin, const double* xmax,
                  const double* ymax, const double* zmax, int64_t n, int g, int period, int lenient,
                  int64_t* out, uint8_t* status, gm_batch_status* summary);
+/* XZ3IndexKeySpace.toIndexKey (idx/index/z3/XZ3IndexKeySpace.scala:60-95) over envelope + dtg columns:
+   bin = BinnedTime(period)(dtg) (t_ms NULL = every dtg null -> 0; a bad date fails even when lenient),
+   xz = XZ3SFC(g, period).index(xmin, ymin, offset, xmax, ymax, offset, lenient); a failed row gets
+   bin 0 and xz 0 and its status */
+int gm_xz3_index_key(gm_ctx* ctx, const double* xmin, const double* ymin, const double* xmax, const double* ymax,
+                     const int64_t* t_ms, int64_t n, int g, int period, int lenient, int16_t* bin, int64_t* xz,
+                     uint8_t* status, gm_batch_status* summary);
 
 /* ------------------------------------------------------------------ range decomposition */
 /* Batched ZN.zranges (z3/zorder/sfcurve/ZN.scala:110-242) as reached from Z3SFC.ranges
@@ -445,12 +456,41 @@ int gm_pip_index_create_arrow(gm_ctx* ctx, const gm_geom_column* polys, int32_t 
 int gm_z3_key_bytes(gm_ctx* ctx, const uint8_t* shard, const int16_t* bin, const int64_t* z, int64_t n,
                     uint8_t* out);
 
+/* The row-key prefix of the key spaces without a time bin: [shard?][z BE64] for Z2IndexKeySpace
+   (idx/index/z2/Z2IndexKeySpace.scala:48-76) and XZ2IndexKeySpace (idx/index/z2/XZ2IndexKeySpace.scala:
+   48-76, z = the XZ2 value): n * key_len bytes, key_len = 9 with a shard column, 8 without. */
+int gm_z2_key_bytes(gm_ctx* ctx, const uint8_t* shard, const int64_t* z, int64_t n, uint8_t* out);
+
 /* Sorts key columns into the table's row order -- the byte order of the row keys above: shard,
    then bin as an unsigned big-endian short, then z as an unsigned big-endian long (what Accumulo /
    HBase keep sorted).  Stable; perm_out[i] = the input row of table row i.  shard / shard_out may
-   be NULL together (unsharded table).  n < 2^32.  Device temporaries: about 32.5 B per row. */
+   be NULL together (unsharded table); bin / bin_out may be NULL together (a key space without a time
+   bin: Z2, XZ2).  n < 2^32.  Device temporaries: about 32.5 B per row (+ 4 B without a bin). */
 int gm_sort_keys(gm_ctx* ctx, const uint8_t* shard, const int16_t* bin, const int64_t* z, int64_t n,
                  uint8_t* shard_out, int16_t* bin_out, int64_t* z_out, int64_t* perm_out);
+
+/* Key-range partitioning of a table over GPUs (configs[2]: the table split into contiguous key ranges,
+   one per rank, as a sorted store splits a table into tablets / regions, the shard prefix of
+   ShardStrategy.scala:75-80 staying the key's first byte; it replaces the Spark shuffle of
+   RelationUtils.scala:30-33, groupByKey(new IndexPartitioner(...))).  A key is the pair
+   key_hi = shard << 16 | bin as u16 (0 <= key_hi < 2^24), key_lo = z as u64, compared unsigned
+   lexicographically -- the byte order of [shard][bin BE16][z BE64].
+
+   gm_key_sample: n_samples (<= 65536) keys of the UNSORTED columns at rows floor((2i+1) n / (2 n_samples))
+   into key_hi / key_lo (host arrays).  Synchronises the context stream. */
+int gm_key_sample(gm_ctx* ctx, const uint8_t* shard, const int16_t* bin, const int64_t* z, int64_t n, int32_t n_samples,
+                  uint64_t* key_hi, uint64_t* key_lo);
+/* gm_key_partition: every row's destination d = the number of the n_split (< 256) ascending splitter keys
+   (host arrays) <= its key; the rows are written grouped by destination (d ascending), keeping their
+   input order within a destination, into shard_out / bin_out / z_out (device; shard and shard_out NULL
+   together), with their source in ids_out (device, optional: ids[row] when ids (device) is given, else
+   id_base + row) and / or rows_out (device, optional: the input row).  dest_counts (host, n_split + 1)
+   receives each destination's row count; destination d's rows start at the sum of the counts before it.
+   n < 2^32.  Synchronises the context stream. */
+int gm_key_partition(gm_ctx* ctx, const uint8_t* shard, const int16_t* bin, const int64_t* z, int64_t n,
+                     const uint64_t* split_hi, const uint64_t* split_lo, int32_t n_split, const int64_t* ids,
+                     int64_t id_base, uint8_t* shard_out, int16_t* bin_out, int64_t* z_out, int64_t* ids_out,
+                     uint32_t* rows_out, int64_t* dest_counts);
 
 /* A scan range over the key prefix, inclusive at both ends in table order: what getRangeBytes
    makes of a ScanRange (idx/index/z3/Z3IndexKeySpace.scala:196-238), [toBytes(lo),
@@ -476,6 +516,46 @@ typedef struct {
 int gm_key_range_scan(gm_ctx* ctx, const uint8_t* shard, const int16_t* bin, const int64_t* z, int64_t n,
                       const gm_key_range* ranges, int64_t n_ranges, const uint8_t* filter_bytes, size_t filter_len,
                       const int64_t* perm, int64_t* ids, int64_t ids_cap, int64_t* n_match, int64_t* n_scanned);
+
+/* The filters a table scan applies to its candidates (all optional; zero-initialise the struct):
+   - the row filter the tablet server runs on each key (RowFilterIterator.scala:52-66): z3filter
+     (host, Z3Filter.serializeToBytes: Z3Filter.inBounds on (bin, z), idx/filters/Z3Filter.scala:26-62)
+     OR z2filter (host, Z2Filter.serializeToBytes: Z2Filter.inBounds on z, idx/filters/Z2Filter.scala:
+     20-35), not both;
+   - the full filter on the feature, which the XZ key spaces always apply (useFullFilter = true,
+     XZ2IndexKeySpace.scala:122-125, XZ3IndexKeySpace.scala:247-250): with n_boxes > 0 the feature's
+     envelope (xmin / ymin / xmax / ymax: device columns in INPUT order, reached through perm)
+     intersects at least one of the boxes (host, n_boxes x (xmin, ymin, xmax, ymax); JTS
+     Envelope.intersects, inclusive; a null envelope -- max < min -- never intersects), and with
+     during != 0 the feature's dtg (t_ms: device, input order) lies in (t_lo, t_hi), exclusive
+     (FastDuring, FastTemporalOperator.scala:116-129).  For a rectangular geometry the envelope test is
+     GeoTools BBOX exactly; for other geometries it is BBOX's envelope pre-check (geometry-geometry
+     relations are out of scope). */
+typedef struct {
+  const uint8_t* z3filter;
+  size_t z3filter_len;
+  const uint8_t* z2filter;
+  size_t z2filter_len;
+  const double* xmin;
+  const double* ymin;
+  const double* xmax;
+  const double* ymax;
+  const double* boxes;
+  int32_t n_boxes;
+  int32_t during;
+  const int64_t* t_ms;
+  int64_t t_lo;
+  int64_t t_hi;
+} gm_scan_filter;
+/* Seek-and-filter over any sorted key table (gm_sort_keys order): Z3 and XZ3 tables ([shard][bin][z]),
+   Z2 and XZ2 tables (bin = NULL: [shard][z]).  Every row inside any of the ranges (host array, merged as
+   gm_key_range_scan merges them; for bin = NULL give bin_lo = bin_hi = 0, XZ2IndexKeySpace.getRangeBytes
+   :104-120), then the filters of f (NULL = none).  ids (device, optional) receives the matching rows in
+   table order, mapped through perm (device, optional) to input rows; *n_match / *n_scanned (host) the
+   match and candidate counts; GM_E_CAPACITY when the matches exceed ids_cap.  Synchronises. */
+int gm_table_scan(gm_ctx* ctx, const uint8_t* shard, const int16_t* bin, const int64_t* z, int64_t n,
+                  const gm_key_range* ranges, int64_t n_ranges, const gm_scan_filter* f, const int64_t* perm,
+                  int64_t* ids, int64_t ids_cap, int64_t* n_match, int64_t* n_scanned);
 
 /* ------------------------------------------------------------------ legacy curves (reading / deleting old data) */
 /* LegacyZ3SFC(period) (z3/curve/LegacyZ3SFC.scala:18-49): SemiNormalizedDimension lon/lat (2^21-1) and

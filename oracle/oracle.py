@@ -579,3 +579,28 @@ def arrow_xz3_keys(arr, dtg, kind, g=12, period=WEEK, lenient=False, flip_axis=F
         if not s:
             b[i], z[i] = bb, zz
     return b, z, st
+
+
+# ---------------------------------------------------------------- key-range partition (multi-GPU ingest)
+def table_key_u64(shard, bins, zs):
+    """(key_hi, key_lo) uint64 of (shard u8 or None, bin i16, z i64): the [shard][bin BE16][z BE64] row-key
+    byte order (Z3IndexKeySpace.scala:81-92) as an unsigned pair."""
+    hi = np.asarray(bins).astype(np.int64).astype(np.uint64) & np.uint64(0xffff)
+    if shard is not None:
+        hi = hi | (np.asarray(shard).astype(np.uint64) << np.uint64(16))
+    return hi, np.asarray(zs).astype(np.int64).view(np.uint64)
+
+
+def key_partition(shard, bins, zs, sp_hi, sp_lo):
+    """The definition gm_key_partition implements: destination = number of splitters <= key (a key equal
+    to a splitter opens the upper range, the tablet split semantics of a sorted store); rows grouped by
+    destination, stable.  Returns (order, counts): the input rows in output order and the per-destination
+    row counts."""
+    hi, lo = table_key_u64(shard, bins, zs)
+    sp_hi = np.asarray(sp_hi, np.uint64)
+    sp_lo = np.asarray(sp_lo, np.uint64)
+    dest = np.zeros(len(hi), np.int64)
+    for h, l_ in zip(sp_hi, sp_lo):
+        dest += (hi > h) | ((hi == h) & (lo >= l_))
+    order = np.argsort(dest, kind="stable")
+    return order, np.bincount(dest, minlength=len(sp_hi) + 1).astype(np.int64)

@@ -262,32 +262,45 @@ def test_clip_key_ranges_matches_brute_force():
     assert len(clip_key_ranges(arr, None, None)) == 0
 
 
+def _sample_rows(n, k):
+    """The rows gm_key_sample reads: floor((2i + 1) n / (2k))."""
+    return (2 * np.arange(k, dtype=np.int64) + 1) * n // (2 * k)
+
+
 def _xchg_worker(rank, world, port, sizes, q):
     sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import torch
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        from geomesa_amd.shard import exchange_by_key_range, key_columns, table_key
+        import oracle as O
+        from geomesa_amd.shard import choose_splitters, exchange_partitioned
         rng = np.random.default_rng(100 + rank)
-        sh, b, z = _rand_keys(rng, sizes[rank])
-        hi, lo = table_key(torch.from_numpy(sh), torch.from_numpy(b), torch.from_numpy(z))
-        o = np.lexsort((lo.numpy(), hi.numpy()))
-        hi, lo = hi[o].contiguous(), lo[o].contiguous()
-        gid = torch.from_numpy(o.astype(np.int64) + rank * 10**6)
-        rh, rl, (rg,), spl = exchange_by_key_range(dist, hi, lo, [gid], samples=64)
-        s2, b2, z2 = key_columns(rh, rl, True)
-        q.put((rank, s2.numpy(), b2.numpy(), z2.numpy(), rg.numpy(), spl[0], spl[1]))
+        sh, b, z = _rand_keys(rng, sizes[rank])          # unsorted rows, as every rank starts
+        n, k = len(z), min(64, len(z))
+        hi, lo = O.table_key_u64(sh, b, z)
+        rows = _sample_rows(n, k)
+        spl = choose_splitters(dist, hi[rows], lo[rows], n, samples=64)
+        # the per-rank partition pass is the HIP kernel on the GPU; here its definition (the oracle)
+        order, counts = O.key_partition(sh, b, z, *spl)
+        gid = order.astype(np.int64) + rank * 10**6
+        cols = [torch.from_numpy(np.ascontiguousarray(c[order])) for c in (sh, b, z)] + [torch.from_numpy(gid)]
+        got, recv = exchange_partitioned(dist, cols, counts)
+        s2, b2, z2, rg = (c.numpy() for c in got)
+        q.put((rank, s2, b2, z2, rg, spl[0], spl[1], recv))
     finally:
         dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("world,sizes", [(2, (5000, 3001)), (3, (4000, 0, 2500))])
-def test_exchange_by_key_range(world, sizes):
-    """Every row lands on the rank owning its key range, nothing is lost or duplicated, the ranges
-    are ordered, and the split is balanced (an empty rank included)."""
+def test_partition_exchange_by_key_range(world, sizes):
+    """Splitters from every rank's UNSORTED sample, the stable partition, the per-column all-to-all: every
+    row lands on the rank owning its key range, nothing is lost or duplicated, the ranges are ordered,
+    the split is balanced (an empty rank included), and within each received slice the rows of one
+    sender keep that sender's input order (what makes the receiver's one stable sort tie-break by id)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -298,8 +311,9 @@ def test_exchange_by_key_range(world, sizes):
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    spl = [(int(h), int(l)) for h, l in zip(got[0][5], got[0][6])]
-    assert all(np.array_equal(g[5], got[0][5]) for g in got)       # same splitters everywhere
+    spl = list(zip(got[0][5].tolist(), got[0][6].tolist()))
+    assert len(spl) == world - 1 and spl == sorted(spl)
+    assert all(np.array_equal(g[5], got[0][5]) and np.array_equal(g[6], got[0][6]) for g in got)
     sent = []
     for r in range(world):
         rng = np.random.default_rng(100 + r)
@@ -307,20 +321,39 @@ def test_exchange_by_key_range(world, sizes):
         sent += [(k, i + r * 10**6) for i, k in enumerate(_order_key(sh, b, z))]
     recv = []
     bounds = []
-    for r, s2, b2, z2, rg, _, _ in got:
+    for r, s2, b2, z2, rg, _, _, rc in got:
+        assert sum(rc) == len(z2)
         ks = _order_key(s2, b2, z2)
         recv += list(zip(ks, rg.tolist()))
         bounds.append((min(ks), max(ks)) if ks else None)
-        for k in ks:   # key range of rank r: [splitter r-1, splitter r)
-            kk = (k[0] << 16 | k[1], k[2] ^ (1 << 63))
-            kk = (kk[0], kk[1] - (1 << 64) if kk[1] >= (1 << 63) else kk[1])
-            assert r == 0 or kk >= spl[r - 1]
-            assert r == world - 1 or kk < spl[r]
+        for kk in ks:   # key range of rank r: [splitter r-1, splitter r)
+            key = (kk[0] << 16 | kk[1], kk[2])
+            assert r == 0 or key >= spl[r - 1]
+            assert r == world - 1 or key < spl[r]
+        assert np.all(np.diff(rg // 10**6) >= 0)                       # senders in rank order
+        for src in np.unique(rg // 10**6):
+            assert np.all(np.diff(rg[rg // 10**6 == src]) > 0)          # each sender's rows in input order
     assert sorted(recv) == sorted(sent)
     nz = [bd for bd in bounds if bd]
     assert all(nz[i][1] <= nz[i + 1][0] for i in range(len(nz) - 1))
     n = sum(sizes)
     assert max(len(g[1]) for g in got) <= 1.35 * n / world
+
+
+def test_key_partition_definition():
+    """The oracle's partition: destination = number of splitters <= key, stable, counts per destination."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    rng = np.random.default_rng(5)
+    sh, b, z = _rand_keys(rng, 4000)
+    hi, lo = O.table_key_u64(sh, b, z)
+    keys = sorted(zip(hi.tolist(), lo.tolist()))
+    spl = [keys[1000], keys[1000], keys[2500]]          # a repeated splitter leaves an empty range
+    order, counts = O.key_partition(sh, b, z, [s[0] for s in spl], [s[1] for s in spl])
+    assert counts.sum() == 4000 and counts[1] == 0
+    d = [sum(1 for s in spl if s <= k) for k in zip(hi.tolist(), lo.tolist())]
+    exp = sorted(range(4000), key=lambda i: (d[i], i))
+    assert order.tolist() == exp
 
 
 def _granges_worker(rank, world, port, q, dst=0):

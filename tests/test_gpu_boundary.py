@@ -158,3 +158,11 @@ def test_filter_scan_rows_short_and_z2(gpu, oracle):
     assert short2 == len(lens[::7]) and np.array_equal(as_np(m2), exp) and k2 == int(exp.sum())
     # empty batch
     assert F.scan_rows(f2, b"", np.zeros(1, np.int64))[2:] == (0, 0)
+
+
+def test_retired_param_is_accepted_noop(gpu):
+    """GM_PARAM_INDEX_CORE_RETIRED (7): the round-5 ABI change keeps it for one release as a no-op."""
+    from geomesa_amd import _lib
+    gpu.set_param(7, 1)
+    assert gpu.get_param(7) == 0
+    assert gpu.lib.gm_ctx_set_param(gpu.handle, 10, 0) == _lib.GM_E_INVALID

@@ -97,7 +97,7 @@ TABLE_QUERIES = [([(-10, 35, 30, 60)], [(1590969600000, 1591617600000)]),
                  ([(0, 0, 0.5, 0.5)], [(1590969600000, 1594000000000)])]
 
 
-def _table_worker(rank, world, port, sharded, q):
+def _table_worker(rank, world, port, sharded, idmode, q):
     sys.path.insert(0, ROOT)
     import torch
     import torch.distributed as dist
@@ -111,36 +111,36 @@ def _table_worker(rank, world, port, sharded, q):
         torch.cuda.set_device(0)
         x, y, t, sh = _table_points()
         lo, hi = shard_bounds(len(x), rank, world)
-        tb = PartitionedZ3Table.from_points(dist, x[lo:hi], y[lo:hi], t[lo:hi], np.arange(lo, hi),
+        ids = np.arange(lo, hi) if idmode == "ids" else lo   # a global-id column, or the first row's id
+        tb = PartitionedZ3Table.from_points(dist, x[lo:hi], y[lo:hi], t[lo:hi], ids,
                                             shard=sh[lo:hi] if sharded else None, shards=4 if sharded else None,
                                             samples=256)
-        res = [tb.n]
+        res = [tb.n, tb.timing]
         for bxs, ts in TABLE_QUERIES:
-            ids, nm, ns, nr = tb.query(bxs, [during(a, b) for a, b in ts])
-            g = gather_rows(dist, [ids.cpu()])
+            got, nm, ns, nr = tb.query(bxs, [during(a, b) for a, b in ts])
+            g = gather_rows(dist, [got.cpu()])
             if rank == 0:
                 res.append(np.sort(g[0].numpy()))
-        if rank == 0:
-            q.put(res)
-        else:
-            q.put(res[:1])
+        q.put(res if rank == 0 else res[:2])
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("sharded", [False, True])
-def test_partitioned_table_equals_global_scan(gpu, sharded):
-    """2 ranks on the box's GPU (gloo): rows exchanged by key range, each rank scans the query
-    ranges clipped to its slice; the gathered ids equal one unpartitioned table's scan."""
-    from geomesa_amd.keyspace import during
-    from geomesa_amd.table import Z3Table
-    world = 2
+@pytest.mark.parametrize("sharded,idmode,world", [(False, "ids", 2), (True, "ids", 2), (False, "base", 2),
+                                                  (True, "base", 3)])
+def test_partitioned_table_equals_oracle_scan(gpu, oracle, sharded, idmode, world):
+    """Ranks sharing the box's GPU (gloo): each keys its unsorted rows, the ranks agree on splitters from
+    key samples, one partition pass + one all-to-all per column + one sort per rank builds the slices,
+    and each rank scans the query ranges clipped to its slice.  The gathered global ids equal the
+    oracle's z3filter_scan (C restatement of Z3Filter.inBounds, Z3Filter.scala:26-62) over every row."""
+    from geomesa_amd import filters as F
+    from geomesa_amd.keyspace import Z3IndexKeySpace, during
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_table_worker, args=(r, world, port, sharded, q)) for r in range(world)]
+    procs = [ctx.Process(target=_table_worker, args=(r, world, port, sharded, idmode, q)) for r in range(world)]
     for p in procs:
         p.start()
     got = [q.get(timeout=300) for _ in range(world)]
@@ -150,13 +150,17 @@ def test_partitioned_table_equals_global_scan(gpu, sharded):
     full = max(got, key=len)
     sizes = sorted(g[0] for g in got)
     x, y, t, sh = _table_points()
-    assert sum(sizes) == len(x) and sizes[0] > 0.4 * len(x)   # balanced key ranges
-    tb = Z3Table.from_points(x, y, t, shard=sh if sharded else None)
+    assert sum(sizes) == len(x) and sizes[0] > 0.8 * len(x) / world   # balanced key ranges
+    for g in got:   # one sort per rank: the ingest's phases are a partition, an exchange and a sort
+        assert set(g[1]) >= {"partition_ms", "exchange_ms", "sort_ms"} and sum(g[1]["received_rows"]) == g[0]
+    ks = Z3IndexKeySpace()
+    ob, oz, _ = oracle.z3_index_key_batch(x, y, t)
     for k, (bxs, ts) in enumerate(TABLE_QUERIES):
-        ids, nm, ns = tb.query(bxs, [during(a, b) for a, b in ts])
-        exp = np.sort(ids.cpu().numpy())
+        v = ks.get_index_values(bxs, [during(a, b) for a, b in ts])
+        om = oracle.z3filter_scan(F.serialize_to_bytes(F.Z3Filter.from_values(v)), ks.bin_ranges(v), ob, oz)
+        exp = np.nonzero(om)[0]
         assert len(exp) > 0 or k == 3
-        assert np.array_equal(full[1 + k], exp), k
+        assert np.array_equal(full[2 + k], exp), k
 
 
 def test_partitioned_table_single_slice(gpu):

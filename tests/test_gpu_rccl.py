@@ -2,7 +2,7 @@
 GPU.  Every other multi-rank test uses gloo; these run the device-tensor code paths that only the
 8-GPU scaling run would otherwise reach first: the index broadcast and its import
 (shard.broadcast_index), the exact-size point-to-point gather (shard.gather_rows, batch_isend_irecv
-with P2POp), the key-range all_to_all_single with splits (shard._exchange_rows), the scalar and
+with P2POp), the key-range partition + per-column all_to_all_single with splits (shard.exchange_partitioned), the scalar and
 histogram all-reduces, the ranges gather, and bench.py itself under torch.distributed.run with one
 rank.  With one rank the collectives degenerate (a broadcast or all-to-all to oneself), so these
 tests check plumbing -- arguments, devices, dtypes, P2POp construction -- not scaling.  They replace
@@ -64,14 +64,19 @@ def _rccl_worker(port, q):
         res["compact_equal"] = bool(torch.equal(ct, pt) and torch.equal(cl, pl) and ct.dtype == torch.int64 and
                                     cl.dtype == torch.int32)
         res["compact_wire"] = wire == [6 * int(pt.numel())]
-        # the key-range exchange step: all_to_all_single of the counts and of the packed records
-        hi = torch.arange(1000, dtype=torch.int64, device="cuda") // 7
-        lo = torch.arange(1000, dtype=torch.int64, device="cuda") * 3
-        ids = torch.arange(1000, dtype=torch.int64, device="cuda") + 10
-        h2, l2, c2 = S._exchange_rows(dist, hi, lo, [ids], np.zeros(0, np.int64), np.zeros(0, np.int64))
-        res["exchange_equal"] = bool(torch.equal(h2, hi) and torch.equal(l2, lo) and torch.equal(c2[0], ids))
-        h3, l3, c3, sp = S.exchange_by_key_range(dist, hi, lo, [ids])
-        res["exchange_world1"] = bool(torch.equal(h3, hi) and len(sp[0]) == 0)
+        # the key-range ingest: key sample, splitters, the partition kernel and the per-column
+        # all_to_all_single (bytes, with splits) of the destination runs, over RCCL device tensors
+        z = torch.arange(1000, dtype=torch.int64, device="cuda") * 7919 % 1000
+        b = (torch.arange(1000, device="cuda") % 5).to(torch.int16)
+        shc = (torch.arange(1000, device="cuda") % 3).to(torch.uint8)
+        s_hi, s_lo = S.sample_keys(ctx, shc, b, z, 64)
+        sp = S.choose_splitters(dist, s_hi, s_lo, 1000, 64)
+        cols, send = S.partition_rows(ctx, shc, b, z, *sp, id_base=10, rows=True)
+        got, recv = S.exchange_partitioned(dist, cols, send)
+        res["exchange_equal"] = bool(len(sp[0]) == 0 and send == [1000] and recv == [1000] and
+                                     all(torch.equal(g, c) for g, c in zip(got, cols)) and
+                                     got[0].device.type == "cuda" and got[1].dtype == torch.int16)
+        res["exchange_world1"] = bool(torch.equal(got[3].to(torch.int64), torch.arange(1000, device="cuda")))
         # scalar and histogram all-reduces
         res["max"] = S.all_reduce_scalar(dist, 3.5, "max")
         res["sum"] = S.all_reduce_scalar(dist, 2.0, "sum")

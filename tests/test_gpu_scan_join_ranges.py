@@ -352,6 +352,22 @@ def test_xz2_ranges_batch_parity(gpu, oracle, max_ranges):
 
 
 @pytest.mark.parametrize("dims", [2, 3])
+@pytest.mark.parametrize("max_ranges", [1 << 28, 1 << 30, (1 << 31) - 1])
+def test_xz_ranges_huge_budget(gpu, oracle, dims, max_ranges):
+    """A maxRanges far past the workspace caps (a caller meaning "unlimited") runs with the unbounded
+    caps instead of failing the call, and gives the oracle's lists."""
+    from geomesa_amd.curve import XZ2SFC, XZ3SFC
+    qs = [[b] for b, _ in ranges_queries(20, seed=71)] + [[(-180.0, -90.0, 180.0, 90.0)]]
+    if dims == 3:
+        qs = [[(b[0], b[1], 100.0, b[2], b[3], 5000.0)] for (b,) in qs]
+    sfc = XZ2SFC(12) if dims == 2 else XZ3SFC(12, "week")
+    got = sfc.ranges_batch(qs, max_ranges)
+    for q, g in zip(qs, got):
+        exp = oracle.xz2_ranges(q, max_ranges=max_ranges) if dims == 2 else oracle.xz3_ranges(q, max_ranges=max_ranges)
+        assert [tuple(r) for r in g] == exp
+
+
+@pytest.mark.parametrize("dims", [2, 3])
 def test_xz_ranges_many_windows(gpu, oracle, dims):
     """Queries with more windows than the first pass stages in LDS (16) run again in the second pass
     with every window in LDS; batched with one-window queries, the output equals the oracle's."""

@@ -321,3 +321,99 @@ def test_table_scan_open_ranges_and_capacity(gpu):
     assert n == len(exp) and len(got) == 7
     # empty table / no ranges
     assert tb.scan([], None)[1] == 0
+
+
+# ---------------------------------------------------------------- key-range partition (multi-GPU ingest)
+
+def _partition_keys(rng, n, kind):
+    sh = rng.integers(0, 4, n).astype(np.uint8)
+    if kind == "rand":
+        b = rng.choice(np.array([0, 1, 2600, 32767, -32768, -2], np.int16), n)
+        z = rng.integers(-(1 << 63), (1 << 63) - 1, n, dtype=np.int64, endpoint=True)
+    elif kind == "week":
+        x, y = rng.uniform(-180, 180, n), rng.uniform(-90, 90, n)
+        t = rng.integers(T2020, T2021, n)
+        from geomesa_amd.curve import Z3SFC
+        bb, zz = Z3SFC("week").index_keys(x, y, t)
+        b, z = as_np(bb), as_np(zz)
+    else:   # "dups": few distinct keys, many equal to a splitter
+        b = rng.integers(0, 3, n).astype(np.int16)
+        z = rng.integers(0, 5, n).astype(np.int64)
+    return sh, b, z
+
+
+@pytest.mark.parametrize("n", [0, 1, 2048, 2049, 100_003, 1_000_000])
+@pytest.mark.parametrize("kind", ["rand", "week", "dups"])
+@pytest.mark.parametrize("nd", [1, 3, 8, 17])
+@pytest.mark.parametrize("sharded", [False, True])
+def test_key_partition_equals_oracle(gpu, oracle, n, kind, nd, sharded):
+    """gm_key_partition against its definition (oracle.key_partition): the output columns are the input
+    rows in destination-then-input order, the sources (ids column, id_base + row, 4-B rows) follow, and
+    the counts match.  Splitters are drawn from the keys (so keys equal a splitter) and repeated."""
+    if kind == "rand" and n > 100_003 and nd > 3:
+        pytest.skip("covered by the smaller random cases")
+    import torch
+    from geomesa_amd import shard as S
+    rng = np.random.default_rng(n * 31 + nd * 7 + sharded)
+    sh, b, z = _partition_keys(rng, n, kind)
+    hi, lo = oracle.table_key_u64(sh if sharded else None, b, z)
+    if n:
+        pick = np.sort(rng.integers(0, n, nd - 1))
+        keys = sorted(zip(hi[pick].tolist(), lo[pick].tolist()))
+        if nd > 2:
+            keys[1] = keys[0]
+    else:
+        keys = sorted((int(rng.integers(0, 1 << 24)), int(rng.integers(0, 1 << 62))) for _ in range(nd - 1))
+    sp_hi = np.array([k[0] for k in keys], np.uint64)
+    sp_lo = np.array([k[1] for k in keys], np.uint64)
+    order, counts = oracle.key_partition(sh if sharded else None, b, z, sp_hi, sp_lo)
+    dev = gpu.device
+    tsh = torch.from_numpy(sh).cuda(dev) if sharded else None
+    tb, tz = torch.from_numpy(b).cuda(dev), torch.from_numpy(z).cuda(dev)
+    ids = rng.integers(-(1 << 62), 1 << 62, n).astype(np.int64)
+    for mode in ("ids", "base", "rows"):
+        cols, got = S.partition_rows(gpu, tsh, tb, tz, sp_hi, sp_lo,
+                                     ids=torch.from_numpy(ids).cuda(dev) if mode == "ids" else None,
+                                     id_base=12345, rows=mode == "rows")
+        assert got == counts.tolist()
+        src = as_np(cols[-1])
+        if sharded:
+            assert np.array_equal(as_np(cols[0]), sh[order])
+        assert np.array_equal(as_np(cols[-3]), b[order]) and np.array_equal(as_np(cols[-2]), z[order])
+        exp = {"ids": ids[order], "base": order + 12345, "rows": order.astype(np.int32)}[mode]
+        assert np.array_equal(src, exp), mode
+
+
+def test_key_partition_rejects_bad_splitters(gpu):
+    import ctypes
+    import torch
+    from geomesa_amd import _lib
+    z = torch.arange(10, dtype=torch.int64, device="cuda")
+    b = torch.zeros(10, dtype=torch.int16, device="cuda")
+    out_b, out_z = torch.empty_like(b), torch.empty_like(z)
+    cnt = np.zeros(3, np.int64)
+    P = _lib.ptr
+    for hi, lo in (([1, 0], [0, 0]), ([0, 0], [5, 4]), ([1 << 24, 1 << 24], [0, 0])):
+        h, lo_ = np.array(hi, np.uint64), np.array(lo, np.uint64)
+        rc = gpu.lib.gm_key_partition(gpu.handle, None, P(b), P(z), 10, h.ctypes.data, lo_.ctypes.data, 2, None, 0,
+                                      None, P(out_b), P(out_z), None, None, cnt.ctypes.data)
+        assert rc == _lib.GM_E_INVALID
+    big = np.zeros(256, np.uint64)
+    assert gpu.lib.gm_key_partition(gpu.handle, None, P(b), P(z), 10, big.ctypes.data, big.ctypes.data, 256, None, 0,
+                                    None, P(out_b), P(out_z), None, None, np.zeros(257, np.int64).ctypes.data) \
+        == _lib.GM_E_INVALID
+    del ctypes
+
+
+@pytest.mark.parametrize("n,k", [(1, 1), (1000, 64), (1_000_003, 1024), (70_000, 65536)])
+@pytest.mark.parametrize("sharded", [False, True])
+def test_key_sample(gpu, oracle, n, k, sharded):
+    import torch
+    from geomesa_amd import shard as S
+    rng = np.random.default_rng(n + k)
+    sh, b, z = _partition_keys(rng, n, "rand")
+    hi, lo = S.sample_keys(gpu, torch.from_numpy(sh).cuda() if sharded else None, torch.from_numpy(b).cuda(),
+                           torch.from_numpy(z).cuda(), k)
+    rows = (2 * np.arange(k, dtype=np.int64) + 1) * n // (2 * k)
+    eh, el = oracle.table_key_u64(sh if sharded else None, b, z)
+    assert np.array_equal(hi, eh[rows]) and np.array_equal(lo, el[rows])
