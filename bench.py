@@ -93,18 +93,22 @@ class Dist:
         return all_reduce_scalar(self.pg, v, "sum")
 
 
-def box_copy_gbs(dist, src):
-    """HBM rate (read + write bytes / time) of a 4 GB device-to-device copy (torch copy_, the best of
-    5) on this rank's GPU, the slowest rank's: the box's own streaming ceiling."""
+def box_copy_gbs(dist, src, ctx):
+    """HBM rate (read + write bytes / time) of a 4 GB device-to-device copy on this rank's GPU, the
+    slowest rank's, best of 5: the box's own streaming ceiling.  The copy is gm_device_copy (16 B per
+    lane, four vectors in flight per lane, non-temporal loads and stores -- the encode kernels' access
+    shape), timed with HIP events on the context stream; torch's byte copy_ had run slower than the
+    encode kernel itself, so a frac_of_box_copy above 1 meant nothing."""
     import torch
-    n = min(src.numel() * src.element_size(), 4 << 30)
+    from geomesa_amd import _lib
+    n = min(src.numel() * src.element_size(), 4 << 30) // 16 * 16
     a = src.view(torch.uint8)[:n]
     b = torch.empty(n, dtype=torch.uint8, device=src.device)
     best = None
-    for _ in range(5):
+    for _ in range(6):
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         s.record()
-        b.copy_(a)
+        _lib.check(ctx.lib.gm_device_copy(ctx.handle, _lib.ptr(b), _lib.ptr(a), n), "gm_device_copy")
         e.record()
         torch.cuda.synchronize()
         best = s.elapsed_time(e) if best is None else min(best, s.elapsed_time(e))
@@ -611,6 +615,20 @@ def bench_table(a, dist, ctx, b, z):
         holder["t"] = PartitionedZ3Table(dist.pg, bs, zs, dist.rank * NT)
     ms_ingest = timed(dist, ingest_step, 1, 1)
     pt = holder["t"]
+    # the partition pass of an N = 8 ingest on this rank's rows (7 splitters from its own key sample), timed
+    # at every world size: at N > 1 it is one of the ingest's phases, at N = 1 the ingest has none
+    from geomesa_amd import shard as S
+    s_hi, s_lo = S.sample_keys(ctx, None, bs, zs, 1024)
+    o = np.lexsort((s_lo, s_hi))
+    pick = o[(np.arange(1, 8) * len(o)) // 8]
+    sp8 = (s_hi[pick].copy(), s_lo[pick].copy())
+    prt = {}
+
+    def part_step():
+        prt["cols"], prt["counts"] = S.partition_rows(ctx, None, bs, zs, *sp8, id_base=0, rows=True)
+    ms_part = timed(dist, part_step, 3, 1)
+    part_counts = prt["counts"]
+    del prt
     phases = {k: (round(dist.max(v), 3) if isinstance(v, float) else v) for k, v in pt.timing.items()}
     slice_rows = [int(v) for v in (all_gather_ints(dist, pt.n))]
     v = ks.get_index_values([(-10, 35, 30, 60)], [during(1590969600000, 1591617600000)])
@@ -685,6 +703,13 @@ def bench_table(a, dist, ctx, b, z):
                               "(look-back, 16-B records) over the top ~log2(n) - 1 varying key bits, then every run of "
                               "equal prefixes ranked by full key in LDS (8-bit digit passes over every varying byte when "
                               "a run exceeds 256 rows); bytes: see sort_bytes"},
+        "table_partition": {"value": NT * dist.world / (ms_part * 1e-3), "unit": "rows/s", "ms_per_step": ms_part,
+                            "rows_per_gpu": NT, "destinations": 8, "rows_per_destination": part_counts,
+                            # count read (bin 2 + z 8) + scatter read (10) + writes (bin 2 + z 8 + 4-B row)
+                            "roofline": dict(roofline(34.0 * NT, ms_part), bytes_per_unit=34,
+                                             kernel="gm_key_partition (count + scan + scatter)"),
+                            "note": "gm_key_partition of the rank's unsorted rows into 8 key ranges (7 splitters from "
+                                    "its own key sample): the per-rank partition pass of an N = 8 ingest"},
         "table_ingest": {"value": NT * dist.world / (ms_ingest * 1e-3), "unit": "rows/s", "ms_per_step": ms_ingest,
                          "rows_per_gpu": NT, "slice_rows": slice_rows, "phases_max_over_ranks": phases,
                          "note": "key-range partitioned table from every rank's unsorted keys: key sample (1024 per "
@@ -902,10 +927,11 @@ def main():
         # this box's own streaming ceiling beside the spec peak: the HBM rate of a device-to-device copy
         # of the same 34 GB shape (HBM rates differ between boxes by up to ~15%), so the fraction can be
         # compared across captures
-        cp = box_copy_gbs(dist, z)
+        cp = box_copy_gbs(dist, x, ctx)
         out["roofline"]["box_copy_gbs"] = round(cp, 1)
         out["roofline"]["frac_of_box_copy"] = round(out["roofline"]["achieved"] / cp, 4)
-        out["roofline"]["box_copy_note"] = "4 GB device-to-device copy, best of 5, read + write bytes / time"
+        out["roofline"]["box_copy_note"] = ("4 GB device-to-device copy (gm_device_copy: 16 B per lane, non-temporal, "
+                                            "the encode kernels' access shape), best of 6, read + write bytes / time")
     out["config"] = {"workload": "configs[1]: Z3IndexKeySpace.toIndexKey batch (BinnedTime + Z3SFC(week).index), "
                                  "%d resident points per GPU" % N,
                      "points_per_gpu": N, "period": "week", "parallelism": "point shards, no collective"}

@@ -118,6 +118,7 @@ SIGNATURES = {
     "gm_device_free": (cint, [vp, vp]),
     "gm_copy_to_device": (cint, [vp, vp, vp, sz]),
     "gm_copy_to_host": (cint, [vp, vp, vp, sz]),
+    "gm_device_copy": (cint, [vp, vp, vp, sz]),
     "gm_timer_start": (cint, [vp]),
     "gm_timer_stop": (cint, [vp, vp]),
     "gm_z3_index": (cint, [vp, vp, vp, vp, i64, cint, cint, cint, vp, vp, vp]),

@@ -202,6 +202,13 @@ __global__ __launch_bounds__(256) void k_pair_move(PairOut o, const PairPlan* __
 // access holds one of the CU's outstanding-miss slots for its latency, so the cost is the count of
 // gathers by kind (the gather model); 42% of the bench's points stop at the
 // bitmap.
+// GM_JX_STAGE (timing builds only, never the shipped library: build.py refuses GM_JX_* there): the
+// lookup chain cut after a stage, on the same points, to price each stage -- 1 = the point stream and
+// the LDS bitmap only (no gather), 2 = + the coarse gathers (mixed coarse cells dropped), 3 = + the fine
+// gathers and their in-register decisions (items and list walks dropped), 4 = the whole join
+#ifndef GM_JX_STAGE
+#define GM_JX_STAGE 4
+#endif
 template <bool WRITE, int SRC, bool VEC>
 __global__ __launch_bounds__(QTPB) void k_pip_join_q(const double* __restrict__ px, const double* __restrict__ py,
                                                      int64_t n, int64_t id_base, PipDev d, PairOut po,
@@ -360,10 +367,12 @@ __global__ __launch_bounds__(QTPB) void k_pip_join_q(const double* __restrict__ 
         const int cx = cell_of(x, d.gx0, d.inv_cw, d.gx), cy = cell_of(y, d.gy0, d.inv_ch, d.gy);
         const int loc = sc8_locate(w8, x, y, d, cx, cy);
         if (loc >= 0) { ihit = join_hit(d.op, loc); w = CELL_EMPTY << 30; }
-        else w = d.cell_word[(int64_t)cy * d.gx + cx];   // near the line: the original word's blob decides
+        else if (GM_JX_STAGE >= 4) w = d.cell_word[(int64_t)cy * d.gx + cx];   // near the line: the original word's blob decides
       }
-      const uint32_t kind = w >> 30, ref = w & 0x3fffffffu;
+      uint32_t kind = w >> 30;
+      const uint32_t ref = w & 0x3fffffffu;
       pair_push(kind == CELL_INTERIOR || ihit, id, ihit ? sc8_poly(w8) : (int)ref);
+      if (GM_JX_STAGE < 4) kind = CELL_EMPTY;   // timing build: no items, no list walks
       const bool item = kind == CELL_BOUNDARY;
       item_push(item, item && lines_on && (ref & (BLOB_COMPACT | SC_LINE)) == (BLOB_COMPACT | SC_LINE), x, y, id, ref);
       l_j = 0;
@@ -407,14 +416,16 @@ __global__ __launch_bounds__(QTPB) void k_pip_join_q(const double* __restrict__ 
         g0 = g0 && !e0;
         g1 = g1 && !e1;
       }
-      if (g0) c0 = d.coarse_sc[(int64_t)(cy0 >> CF_LOG) * d.gxc + (cx0 >> CF_LOG)];
-      if (g1) c1 = d.coarse_sc[(int64_t)(cy1 >> CF_LOG) * d.gxc + (cx1 >> CF_LOG)];
+      if (GM_JX_STAGE >= 2) {
+        if (g0) c0 = d.coarse_sc[(int64_t)(cy0 >> CF_LOG) * d.gxc + (cx0 >> CF_LOG)];
+        if (g1) c1 = d.coarse_sc[(int64_t)(cy1 >> CF_LOG) * d.gxc + (cx1 >> CF_LOG)];
+      }
       c0 = coarse_mask(c0, cx0, cy0, d.coarse_fmt);
       c1 = coarse_mask(c1, cx1, cy1, d.coarse_fmt);
       const uint32_t id0 = (uint32_t)(2 * (step * 64 + lane)), id1 = id0 + 1;
       pair_push((c0 >> 30) == CELL_INTERIOR, id0, (int)(c0 & 0x3fffffffu));
       pair_push((c1 >> 30) == CELL_INTERIOR, id1, (int)(c1 & 0x3fffffffu));
-      const bool f0 = (c0 >> 30) == CELL_LIST, f1 = (c1 >> 30) == CELL_LIST;
+      const bool f0 = GM_JX_STAGE >= 3 && (c0 >> 30) == CELL_LIST, f1 = GM_JX_STAGE >= 3 && (c1 >> 30) == CELL_LIST;
       const uint64_t m0 = __ballot(f0), m1 = __ballot(f1);
       if (GM_REF_BAD(fn + 128 > FCAP)) { if (lane == 0 && (m0 | m1)) pip_fault(d, PIP_FAULT_QUEUE); }   // cannot happen: fn < 128
       else {

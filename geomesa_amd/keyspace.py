@@ -12,7 +12,8 @@ from dataclasses import dataclass, field
 
 import numpy as np
 
-from .curve import BinnedTime, IllegalArgumentException, LegacyZ3SFC, TimePeriod, Z2SFC, Z3SFC, max_offset
+from .curve import (BinnedTime, IllegalArgumentException, LegacyZ3SFC, TimePeriod, XZ2SFC, XZ3SFC, Z2SFC, Z3SFC,
+                    max_offset)
 
 SHORT_MAX = 32767
 WHOLE_WORLD = (-180.0, -90.0, 180.0, 90.0)
@@ -264,3 +265,113 @@ class Z2IndexKeySpace:
         geoms = [WHOLE_WORLD] if not bboxes else bboxes
         xy = [c for c in (_clip_world(b) for b in geoms) if c is not None]
         return Z2IndexValues(self.sfc, xy, disjoint=not xy)
+
+    # getRanges (Z2IndexKeySpace.scala:99-108): sfc.ranges(xy, 64, target) as BoundedRanges (no bin: 0)
+    def get_ranges(self, values, multiplier=1, target=2000):
+        if values.disjoint:
+            return []
+        rs = self.sfc.ranges(values.spatialBounds, 64, max(1, target // multiplier))
+        return [("bounded", (0, r.lower), (0, r.upper)) for r in rs]
+
+
+@dataclass
+class XZ3IndexValues:
+    """XZ3IndexValues(sfc, geometries, spatialBounds, intervals, temporalBounds, temporalUnbounded)."""
+    sfc: object
+    spatialBounds: list
+    intervals: list
+    temporalBounds: dict = field(default_factory=dict)
+    temporalUnbounded: list = field(default_factory=list)
+    disjoint: bool = False
+
+
+class XZ2IndexKeySpace:
+    """XZ2 index key space (geomesa-index-api/.../index/z2/XZ2IndexKeySpace.scala:28-126): the key is
+    [shard][XZ2 BE64] of the geometry's envelope; every query applies the full filter (:122-125)."""
+
+    def __init__(self, g=12):
+        self.sfc = XZ2SFC(g)
+
+    # getIndexValues (:78-95): the query geometries' bounds (a bbox is its own bounds), whole world if none
+    def get_index_values(self, bboxes=None):
+        geoms = [WHOLE_WORLD] if not bboxes else bboxes
+        xy = [c for c in (_clip_world(b) for b in geoms) if c is not None]
+        return Z2IndexValues(self.sfc, xy, disjoint=not xy)
+
+    # getRanges (:97-102): sfc.ranges(xy, target) as BoundedRanges (bin 0 in the gm_key_range rows)
+    def get_ranges(self, values, multiplier=1, target=2000):
+        if values.disjoint:
+            return []
+        rs = self.sfc.ranges(values.spatialBounds, max(1, target // multiplier))
+        return [("bounded", (0, r.lower), (0, r.upper)) for r in rs]
+
+
+class XZ3IndexKeySpace:
+    """XZ3 index key space (geomesa-index-api/.../index/z3/XZ3IndexKeySpace.scala:32-251): the key is
+    [shard][bin BE16][XZ3 BE64] of the envelope at the dtg's period offset; every query applies the full
+    filter (:247-250)."""
+
+    def __init__(self, period=TimePeriod.Week, g=12):
+        self.period = TimePeriod.of(period)
+        self.sfc = XZ3SFC(g, self.period)
+
+    # getIndexValues (:98-166)
+    def get_index_values(self, bboxes=None, intervals=None):
+        geoms = [WHOLE_WORLD] if not bboxes else bboxes
+        xy = [c for c in (_clip_world(b) for b in geoms) if c is not None]
+        ivs = [extract_interval(b, True) for b in (intervals or [])]
+        if any(iv.is_bounded_both_sides and iv.lower > iv.upper for iv in ivs):   # disjoint dates (:117-120)
+            return XZ3IndexValues(self.sfc, xy, ivs, {}, [], disjoint=True)
+        zmin, zmax = self.sfc.zBounds
+        max_dt = _epoch_ms_max(self.period) - 1
+        times = {}
+        unbounded = []
+
+        def update(b, lt, ut):   # updateTime (:133-139)
+            if b in times:
+                times[b] = (min(times[b][0], lt), max(times[b][1], ut))
+            else:
+                times[b] = (lt, ut)
+        for iv in ivs:
+            lo = 0 if iv.lower is None else min(max(iv.lower, 0), max_dt)       # boundsToIndexableDates
+            hi = max_dt if iv.upper is None else min(max(iv.upper, 0), max_dt)
+            lb, lt = binned_time_host(self.period, lo)
+            ub, ut = binned_time_host(self.period, hi)
+            if iv.is_bounded_both_sides:
+                if lb == ub:
+                    update(lb, float(lt), float(ut))
+                else:
+                    update(lb, float(lt), zmax)
+                    update(ub, zmin, float(ut))
+                    for b in range(lb + 1, ub):
+                        times[b] = (zmin, zmax)
+            elif iv.lower is not None:
+                update(lb, float(lt), zmax)
+                unbounded.append((lb + 1, SHORT_MAX))
+            elif iv.upper is not None:
+                update(ub, zmin, float(ut))
+                unbounded.append((0, ub - 1))
+        return XZ3IndexValues(self.sfc, xy, ivs, times, unbounded, disjoint=not xy)
+
+    # getRanges (:168-201): per bin the XZ3 ranges of the boxes x the bin's times, target split over bins
+    def get_ranges(self, values, multiplier=1, target=2000):
+        if values.disjoint:
+            return []
+        tb, ub = values.temporalBounds, values.temporalUnbounded
+        if not tb and not ub:
+            return [("unbounded", None, None)]
+        t = max(1, (target if not tb else target // len(tb)) // multiplier)
+        bins = sorted(tb)
+        queries = [[(x0, y0, tb[b][0], x1, y1, tb[b][1]) for (x0, y0, x1, y1) in values.spatialBounds] for b in bins]
+        rs = self.sfc.ranges_batch(queries, t) if queries else []
+        out = []
+        for b, rr in zip(bins, rs):
+            out.extend(("bounded", (b, r.lower), (b, r.upper)) for r in rr)
+        for (lo, hi) in ub:
+            if hi == SHORT_MAX:
+                out.append(("lower", (lo, 0), None))
+            elif lo == 0:
+                out.append(("upper", None, (hi, 2**63 - 1)))
+            else:
+                out.append(("unbounded", (0, 0), None))
+        return out

@@ -259,3 +259,162 @@ class PartitionedZ3Table:
             import torch
             return torch.zeros(0, dtype=torch.int64, device=self.table.z.device), 0, 0, 0
         return self.scan(ks.get_ranges(v, target=target), F.Z3Filter.from_values(v))
+
+
+# ---------------------------------------------------------------- Z2 / XZ2 / XZ3 tables
+class _KeyTable:
+    """Sorted (shard?, bin?, z) key columns of one GPU's slice of an index table (gm_sort_keys), the
+    sort's permutation, and the seek + filter of gm_table_scan.  bin None: a key space without a time
+    bin ([shard][z BE64]: Z2, XZ2)."""
+
+    def __init__(self, bins, z, shard=None, shards=None):
+        import torch
+        from .curve import _dev_col
+        self.ctx = _lib.context()
+        z = _dev_col(z, torch.int64)
+        self.n = z.numel()
+        dev = z.device
+        self.z = torch.empty_like(z)
+        self.perm = torch.empty(self.n, dtype=torch.int64, device=dev)
+        b_in = None if bins is None else _dev_col(bins, torch.int16)
+        self.bin = None if b_in is None else torch.empty_like(b_in)
+        self.shard, self.shards, sh_in = None, None, None
+        if shard is not None:
+            sh_in = torch.as_tensor(np.asarray(shard, np.uint8) if not isinstance(shard, torch.Tensor) else shard,
+                                    dtype=torch.uint8).to(dev).contiguous()
+            self.shard = torch.empty_like(sh_in)
+            self.shards = int(shards) if shards else (int(sh_in.max().item()) + 1 if self.n else 1)
+        check(self.ctx.lib.gm_sort_keys(self.ctx.handle, ptr(sh_in), ptr(b_in), ptr(z), self.n, ptr(self.shard),
+                                        ptr(self.bin), ptr(self.z), ptr(self.perm)), "gm_sort_keys")
+
+    def key_bytes(self):
+        """Row-key prefixes in table order: [shard?][bin BE16][z BE64] or, without a bin, [shard?][z BE64]."""
+        import torch
+        klen = (1 if self.shard is not None else 0) + (2 if self.bin is not None else 0) + 8
+        out = torch.empty((self.n, klen), dtype=torch.uint8, device=self.z.device)
+        if self.bin is not None:
+            check(self.ctx.lib.gm_z3_key_bytes(self.ctx.handle, ptr(self.shard), ptr(self.bin), ptr(self.z), self.n,
+                                               ptr(out)), "gm_z3_key_bytes")
+        else:
+            check(self.ctx.lib.gm_z2_key_bytes(self.ctx.handle, ptr(self.shard), ptr(self.z), self.n, ptr(out)),
+                  "gm_z2_key_bytes")
+        return out
+
+    def table_scan(self, arr, flt=None, map_rows=True, ids_cap=None):
+        """gm_table_scan over gm_key_range rows `arr` with a ScanFilter (None = no filter): (ids, n_match,
+        n_scanned); ids are input rows (map_rows) or table rows."""
+        import torch
+        arr = np.ascontiguousarray(arr, _lib.KEY_RANGE_DTYPE)
+        cap = self.n if ids_cap is None else ids_cap
+        ids = torch.empty(max(cap, 1), dtype=torch.int64, device=self.z.device)
+        nm, ns = ctypes.c_int64(), ctypes.c_int64()
+        rc = self.ctx.lib.gm_table_scan(self.ctx.handle, ptr(self.shard), ptr(self.bin), ptr(self.z), self.n,
+                                        arr.ctypes.data if len(arr) else None, len(arr),
+                                        ctypes.byref(flt) if flt is not None else None,
+                                        ptr(self.perm) if map_rows else None, ptr(ids), cap, ctypes.byref(nm),
+                                        ctypes.byref(ns))
+        if rc != _lib.GM_E_CAPACITY:
+            check(rc, "gm_table_scan")
+        return ids[:min(nm.value, cap)], nm.value, ns.value
+
+
+def _full_filter(cols, boxes, interval=None, t=None):
+    """ScanFilter for the XZ full filter: envelope columns x boxes, dtg during (lo, hi) exclusive.  The
+    host arrays it points to are returned beside it (they must outlive the call)."""
+    f = _lib.ScanFilter()
+    keep = []
+    if boxes:
+        bx = np.ascontiguousarray(np.asarray(boxes, np.float64).reshape(-1, 4))
+        keep.append(bx)
+        f.xmin, f.ymin, f.xmax, f.ymax = (c.data_ptr() for c in cols)
+        f.boxes, f.n_boxes = bx.ctypes.data, len(bx)
+    if interval is not None:
+        f.during, f.t_ms, f.t_lo, f.t_hi = 1, t.data_ptr(), int(interval[0]), int(interval[1])
+    return f, keep
+
+
+class Z2Table(_KeyTable):
+    """A Z2 point index table (Z2IndexKeySpace.scala:48-76: [shard][z BE64]).  query(): ranges
+    (getRanges :99-108) -> seek -> Z2Filter on the row keys (the loose bbox, the default), or with
+    strict=True the full filter (point in bbox, inclusive, on the x / y columns: useFullFilter :124-130)."""
+
+    def __init__(self, x, y, shard=None, shards=None, lenient=False):
+        import torch
+        from .curve import _dev_col
+        from .keyspace import Z2IndexKeySpace
+        self.ks = Z2IndexKeySpace()
+        self.x, self.y = _dev_col(x, torch.float64), _dev_col(y, torch.float64)
+        super().__init__(None, self.ks.sfc.index(self.x, self.y, lenient=lenient), shard, shards)
+
+    def query(self, bboxes=None, strict=False, target=2000):
+        v = self.ks.get_index_values(bboxes)
+        if v.disjoint:
+            import torch
+            return torch.zeros(0, dtype=torch.int64, device=self.z.device), 0, 0
+        arr, _ = key_ranges(self.ks.get_ranges(v, target=target), self.shards)
+        if strict:
+            f, keep = _full_filter((self.x, self.y, self.x, self.y), v.spatialBounds)
+        else:
+            fb = F.serialize_to_bytes(F.Z2Filter.from_values(v))
+            keep = [ctypes.create_string_buffer(fb, len(fb))]
+            f = _lib.ScanFilter()
+            f.z2filter, f.z2filter_len = ctypes.addressof(keep[0]), len(fb)
+        return self.table_scan(arr, f)
+
+
+class XZ2Table(_KeyTable):
+    """An XZ2 index table of geometry envelopes (XZ2IndexKeySpace.scala:48-76: [shard][XZ2 BE64]).
+    query(): ranges (getRanges :97-102) -> seek -> the full filter every XZ query applies (:122-125):
+    the feature envelope intersects a query box."""
+
+    def __init__(self, xmin, ymin, xmax, ymax, shard=None, shards=None, g=12, lenient=False):
+        import torch
+        from .curve import _dev_col
+        from .keyspace import XZ2IndexKeySpace
+        self.ks = XZ2IndexKeySpace(g)
+        self.env = tuple(_dev_col(c, torch.float64) for c in (xmin, ymin, xmax, ymax))
+        super().__init__(None, self.ks.sfc.index(*self.env, lenient=lenient), shard, shards)
+
+    def query(self, bboxes=None, target=2000, full_filter=True):
+        v = self.ks.get_index_values(bboxes)
+        if v.disjoint:
+            import torch
+            return torch.zeros(0, dtype=torch.int64, device=self.z.device), 0, 0
+        arr, _ = key_ranges(self.ks.get_ranges(v, target=target), self.shards)
+        f, keep = _full_filter(self.env, v.spatialBounds) if full_filter else (None, [])
+        return self.table_scan(arr, f)
+
+
+class XZ3Table(_KeyTable):
+    """An XZ3 index table (XZ3IndexKeySpace.scala:60-95: [shard][bin BE16][XZ3 BE64], keys from
+    gm_xz3_index_key).  query(): getIndexValues / getRanges (:98-201) -> seek -> the full filter
+    (:247-250): envelope intersects a query box AND dtg DURING the interval (exclusive)."""
+
+    def __init__(self, xmin, ymin, xmax, ymax, t_ms, shard=None, shards=None, g=12, period="week", lenient=False):
+        import torch
+        from .curve import _dev_col, _raise_first, _summary
+        from .keyspace import XZ3IndexKeySpace
+        self.ks = XZ3IndexKeySpace(period, g)
+        self.env = tuple(_dev_col(c, torch.float64) for c in (xmin, ymin, xmax, ymax))
+        self.t = _dev_col(t_ms, torch.int64)
+        n = self.t.numel()
+        ctx = _lib.context()
+        b = torch.empty(n, dtype=torch.int16, device=self.t.device)
+        xz = torch.empty(n, dtype=torch.int64, device=self.t.device)
+        st = _summary()
+        check(ctx.lib.gm_xz3_index_key(ctx.handle, *[ptr(c) for c in self.env], ptr(self.t), n, self.ks.sfc.g,
+                                       self.ks.period, int(bool(lenient)), ptr(b), ptr(xz), None, ctypes.byref(st)),
+              "gm_xz3_index_key")
+        _raise_first(st, "XZ3IndexKeySpace.toIndexKey")
+        super().__init__(b, xz, shard, shards)
+
+    def query(self, bboxes=None, interval=None, target=2000, full_filter=True):
+        """interval: (lo, hi) epoch millis of `dtg DURING lo/hi`, or None."""
+        from .keyspace import during
+        v = self.ks.get_index_values(bboxes, [during(*interval)] if interval is not None else None)
+        if v.disjoint:
+            import torch
+            return torch.zeros(0, dtype=torch.int64, device=self.z.device), 0, 0
+        arr, _ = key_ranges(self.ks.get_ranges(v, target=target), self.shards)
+        f, keep = _full_filter(self.env, v.spatialBounds, interval, self.t) if full_filter else (None, [])
+        return self.table_scan(arr, f)

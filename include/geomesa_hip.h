@@ -133,6 +133,9 @@ int gm_device_alloc(gm_ctx* ctx, size_t bytes, void** ptr);
 int gm_device_free(gm_ctx* ctx, void* ptr);
 int gm_copy_to_device(gm_ctx* ctx, void* dst, const void* host_src, size_t bytes);
 int gm_copy_to_host(gm_ctx* ctx, void* host_dst, const void* src, size_t bytes);
+/* device-to-device copy on the context stream (asynchronous): 16 B per lane with non-temporal loads and
+   stores when both pointers are 16-B aligned -- the streaming copy the benchmark calibrates HBM against */
+int gm_device_copy(gm_ctx* ctx, void* dst, const void* src, size_t bytes);
 /* HIP-event timing on the context stream: brackets any sequence of calls */
 int gm_timer_start(gm_ctx* ctx);
 int gm_timer_stop(gm_ctx* ctx, float* ms);

@@ -604,3 +604,22 @@ def key_partition(shard, bins, zs, sp_hi, sp_lo):
         dest += (hi > h) | ((hi == h) & (lo >= l_))
     order = np.argsort(dest, kind="stable")
     return order, np.bincount(dest, minlength=len(sp_hi) + 1).astype(np.int64)
+
+
+# ---------------------------------------------------------------- the XZ full filter (full-scan restatement)
+def envelope_scan(xmin, ymin, xmax, ymax, boxes, t_ms=None, interval=None):
+    """Mask of features whose envelope intersects any box (JTS Envelope.intersects: inclusive, a null
+    envelope -- max < min -- never intersects) AND, with an interval, whose dtg lies in (lo, hi) (FastDuring,
+    exclusive; FastTemporalOperator.scala:116-129): the full filter the XZ key spaces apply
+    (XZ2IndexKeySpace.scala:122-125, XZ3IndexKeySpace.scala:247-250), evaluated on every feature."""
+    xmin, ymin, xmax, ymax = (np.asarray(c, np.float64) for c in (xmin, ymin, xmax, ymax))
+    ok = np.zeros(len(xmin), bool)
+    valid = ~((xmax < xmin) | (ymax < ymin))
+    for (bx0, by0, bx1, by1) in boxes:
+        if bx1 < bx0 or by1 < by0:
+            continue
+        ok |= valid & ~((bx0 > xmax) | (bx1 < xmin) | (by0 > ymax) | (by1 < ymin))
+    if interval is not None:
+        t = np.asarray(t_ms, np.int64)
+        ok &= (t > interval[0]) & (t < interval[1])
+    return ok

@@ -67,6 +67,15 @@ for step in "$@"; do
           python3 bench.py --only join --no-cpu --steps 1 --warmup 0 --join-steps 1 > ${out}_pmc$i.log 2>&1
         i=$((i+1))
       done ;;
+    tpmc)   # the traffic-calibration probe: its own timing, then one counter group per rocprofv3 pass
+      timeout -k 10 120 tools/traffic_probe > ${out}_tprobe.txt 2>&1
+      i=0
+      for g in "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum" FETCH_SIZE WRITE_SIZE \
+               "TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum TCC_HIT_sum TCC_MISS_sum"; do
+        timeout -s KILL 120 rocprofv3 --kernel-trace --output-format csv --pmc $g -d ${out}_tpmc/p$i -o run -- \
+          tools/traffic_probe > ${out}_tpmc_p$i.log 2>&1
+        i=$((i+1))
+      done ;;
     kstats)
       timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d ${out}_kstats_$arg -o run -- \
         python3 bench.py $(leg_args $arg) > ${out}_kstats_$arg.json 2> ${out}_kstats_$arg.err
@@ -96,6 +105,22 @@ for step in "$@"; do
           $cmd > ${out}_pmc_$arg/p$i.log 2>&1 || { echo "pass $i ($g) failed: $?" >> ${out}_pmc_$arg/failed.txt; exit 1; }
         i=$((i+1))
       done ;;
+    vpmc)   # counter groups (PMC_GROUPS, ';'-separated, or the read-request sizes + hits / misses) over one leg,
+            # once per variant library: vpmc:LEG:lib1,lib2,...
+      leg=${arg%%:*}; libs=${arg#*:}
+      if [ -n "$PMC_GROUPS" ]; then IFS=";" read -ra vgroups <<< "$PMC_GROUPS"
+      else vgroups=("TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum"
+                    "TCC_HIT_sum TCC_MISS_sum TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum"); fi
+      for lib in ${libs//,/ }; do
+        if [ "$lib" = prod ]; then unset GEOMESA_HIP_LIB; else export GEOMESA_HIP_LIB=$PWD/geomesa_amd/lib/$lib.so; fi
+        i=0
+        for g in "${vgroups[@]}"; do
+          timeout -s KILL 200 rocprofv3 --kernel-trace --output-format csv --pmc $g -d ${out}_vpmc_${lib}/p$i -o run -- \
+            python3 bench.py $(leg_args $leg) > ${out}_vpmc_${lib}_p$i.log 2>&1
+          i=$((i+1))
+        done
+      done
+      unset GEOMESA_HIP_LIB ;;
     ab)
       leg=${arg%%:*}; libs=${arg#*:}
       for r in 1 2 3; do
