@@ -226,27 +226,71 @@ __global__ __launch_bounds__(QTPB) void k_pip_join_q(const double* __restrict__ 
   double* fx = s_fx[wv]; double* fy = s_fy[wv]; uint32_t* fid = s_fid[wv];
   double* qx = s_ix[wv]; double* qy = s_iy[wv]; uint32_t* qid = s_iid[wv]; uint32_t* qref = s_iref[wv];
   int fn = 0, qn = 0, qg = 0;   // wave-uniform fills: fine queue, line items, blob items
+  int jx_sink = 0;              // GM_JX_STAGE 1 only
   int64_t sbase = -1;           // wave-uniform: this wave's current output slab and its fill
   int sfill = SLAB;
   int my_count = 0;
   const bool lines_on = d.line_ent != nullptr;
 
-  // a wave's pairs go straight into its slab (see "pair output by slabs"); a full slab takes the
-  // next one with one atomic
-  auto pair_push = [&](bool hit, uint32_t id, int poly) __attribute__((always_inline)) {
-    if (!WRITE) { my_count += hit; return; }
-    const uint64_t m = __ballot(hit);
-    if (!m) return;
-    const int c = __popcll(m), off = lanes_below(m), room = SLAB - sfill;
-    if (hit && off < room) pair_store(po, sbase + sfill + off, id_base + id, poly);
-    if (c > room) {
+  // Pair staging: the wave's pending pairs sit one per lane in registers, lanes [0, pcnt).  A push moves
+  // its hit lanes' pairs, in lane order, into lanes pcnt, pcnt + 1, ... (mod 64) by one backward
+  // permute, and every 64 pending pairs leave as ONE coalesced 64-pair write at a 64-aligned position of
+  // the wave's slab (ids: four whole 128-B lines, polygons: two).  Storing each push's few hits where they
+  // fell -- two partial-line stores per push -- cost the join 2.5 of its 10 ms (a timing build without
+  // the stores ran 7.5 ms, profiles/r6/join_pairs_ab.txt).  A full slab takes the next with one atomic.
+  uint32_t st_id = 0;
+  int st_poly = 0;
+  int pcnt = 0;                 // wave-uniform: pending pairs
+  auto slab_room = [&]() __attribute__((always_inline)) {   // a slab with room for 64 (fills are multiples of 64)
+    if (sfill >= SLAB) {
       unsigned long long b = 0;
       if (lane == 0) b = atomicAdd(po.counter, (unsigned long long)SLAB);
       sbase = (int64_t)__shfl(b, 0, 64);
-      if (hit && off >= room) pair_store(po, sbase + (off - room), id_base + id, poly);
-      sfill = c - room;
+      sfill = 0;
+    }
+  };
+  auto pair_push = [&](bool hit, uint32_t id, int poly) __attribute__((always_inline)) {
+#ifdef GM_JX_NOPAIRS   // timing builds: the pairs are counted into the sink, nothing is stored
+    jx_sink += hit ? (int)(id ^ (uint32_t)poly) : 0;
+    return;
+#endif
+    if (!WRITE) { my_count += hit; return; }
+    const uint64_t m = __ballot(hit);
+    if (!m) return;
+#ifdef GM_JX_PAIRS_DIRECT   // timing builds: round 5's stores of each push's hits where they fell
+    {
+      const int c = __popcll(m), off = lanes_below(m), room = SLAB - sfill;
+      if (hit && off < room) pair_store(po, sbase + sfill + off, id_base + id, poly);
+      if (c > room) {
+        unsigned long long b = 0;
+        if (lane == 0) b = atomicAdd(po.counter, (unsigned long long)SLAB);
+        sbase = (int64_t)__shfl(b, 0, 64);
+        if (hit && off >= room) pair_store(po, sbase + (off - room), id_base + id, poly);
+        sfill = c - room;
+      } else {
+        sfill += c;
+      }
+      return;
+    }
+#endif
+    const int c = __popcll(m);
+    const int k = (lane - pcnt) & 63;   // this lane's slot takes the hit of rank k (when k < c)
+    const bool take = k < c;
+    // a forward permute over all 64 lanes: the hits go to slots pcnt, pcnt + 1, ... in lane order and the
+    // other lanes fill the remaining slots, so every slot receives exactly one value
+    const int dst = hit ? (pcnt + lanes_below(m)) & 63 : (pcnt + c + lanes_below(~m)) & 63;
+    const uint32_t nid = (uint32_t)__builtin_amdgcn_ds_permute(dst << 2, (int)id);
+    const int npoly = __builtin_amdgcn_ds_permute(dst << 2, poly);
+    if (pcnt + c < 64) {
+      if (take) { st_id = nid; st_poly = npoly; }
+      pcnt += c;
     } else {
-      sfill += c;
+      if (take && lane >= pcnt) { st_id = nid; st_poly = npoly; }   // completes the 64
+      slab_room();
+      pair_store(po, sbase + sfill + lane, id_base + st_id, st_poly);
+      sfill += 64;
+      if (take && lane < pcnt) { st_id = nid; st_poly = npoly; }    // the rest wraps to lanes 0, 1, ...
+      pcnt += c - 64;
     }
   };
   auto item_push = [&](bool valid, bool is_line, double x, double y, uint32_t id, uint32_t ref) __attribute__((always_inline)) {
@@ -395,8 +439,19 @@ __global__ __launch_bounds__(QTPB) void k_pip_join_q(const double* __restrict__ 
       const int cnt = min(fn, FBATCH);
       const int a = fn - cnt + lane;
       pend_w = make_uint2(CELL_EMPTY << 30, 0u);
+#ifdef GM_JX_FINE_AUX   // timing builds: the fine gathers as buffer loads with another cache policy (aux bits)
+      if (lane < cnt) {
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)d.cell_sc8, 0,
+                                                                            (int)((int64_t)d.gx * d.gy * 8), 0x00020000);
+        const int64_t ci = (int64_t)cell_of(fy[a], d.gy0, d.inv_ch, d.gy) * d.gx + cell_of(fx[a], d.gx0, d.inv_cw, d.gx);
+        typedef unsigned int u2v __attribute__((ext_vector_type(2)));
+        const u2v v = __builtin_amdgcn_raw_buffer_load_b64(rs, (int)(ci * 8), 0, GM_JX_FINE_AUX);
+        pend_w = make_uint2(v.x, v.y);
+      }
+#else
       if (lane < cnt)
         pend_w = d.cell_sc8[(int64_t)cell_of(fy[a], d.gy0, d.inv_ch, d.gy) * d.gx + cell_of(fx[a], d.gx0, d.inv_cw, d.gx)];
+#endif
       pb = fn - cnt;
       pc = cnt;
       pend = true;
@@ -419,6 +474,8 @@ __global__ __launch_bounds__(QTPB) void k_pip_join_q(const double* __restrict__ 
       if (GM_JX_STAGE >= 2) {
         if (g0) c0 = d.coarse_sc[(int64_t)(cy0 >> CF_LOG) * d.gxc + (cx0 >> CF_LOG)];
         if (g1) c1 = d.coarse_sc[(int64_t)(cy1 >> CF_LOG) * d.gxc + (cx1 >> CF_LOG)];
+      } else {   // timing build: keep the stream and the cell arithmetic alive (no pair depends on them)
+        jx_sink += (g0 ? cx0 + cy0 : 0) + (g1 ? cx1 + cy1 : 0);
       }
       c0 = coarse_mask(c0, cx0, cy0, d.coarse_fmt);
       c1 = coarse_mask(c1, cx1, cy1, d.coarse_fmt);
@@ -441,7 +498,13 @@ __global__ __launch_bounds__(QTPB) void k_pip_join_q(const double* __restrict__ 
     }
     break;   // every stage idle and the item queue empty (the item stage drains it once nothing else runs)
   }
+  if (jx_sink == 0x7fffffff) pip_fault(d, PIP_FAULT_QUEUE);   // timing builds only: a use of the sink (0 otherwise)
   if (WRITE) {
+    if (pcnt > 0) {   // the last pending pairs: a partial slab (k_pair_plan closes the hole behind them)
+      slab_room();
+      if (lane < pcnt) pair_store(po, sbase + sfill + lane, id_base + st_id, st_poly);
+      sfill += pcnt;
+    }
     if (lane == 0) po.desc[desc_base + (int64_t)blockIdx.x * NW + wv] = make_longlong2(sbase, sfill);
   } else {
     for (int off = 32; off > 0; off >>= 1) my_count += __shfl_down(my_count, off, 64);

@@ -57,12 +57,13 @@ for step in "$@"; do
       timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d ${out}_prof -o run -- \
         python3 bench.py --steps 10 --join-steps 3 --no-cpu > ${out}_prof_bench.json 2> ${out}_prof.err
       i=0
-      for g in FETCH_SIZE WRITE_SIZE; do
+      rq="TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum"
+      for g in FETCH_SIZE WRITE_SIZE "$rq"; do
         timeout -s KILL 200 rocprofv3 --kernel-trace --output-format csv --pmc $g -d ${out}_pmc/p$i -o run -- \
           python3 bench.py --only z3,extra,table --no-cpu --steps 2 --warmup 1 > ${out}_pmc$i.log 2>&1
         i=$((i+1))
       done
-      for g in FETCH_SIZE WRITE_SIZE SQ_INSTS_VALU_FLOPS_FP64; do
+      for g in FETCH_SIZE WRITE_SIZE SQ_INSTS_VALU_FLOPS_FP64 "$rq"; do
         timeout -s KILL 200 rocprofv3 --kernel-trace --output-format csv --pmc $g -d ${out}_pmc/p$i -o run -- \
           python3 bench.py --only join --no-cpu --steps 1 --warmup 0 --join-steps 1 > ${out}_pmc$i.log 2>&1
         i=$((i+1))

@@ -2,12 +2,15 @@
 
 usage: python tools/make_traffic.py PMC_DIR OUT_JSON [points] [join_points] [table_rows]
 
-FETCH_SIZE and WRITE_SIZE are in KiB per dispatch.  MI355X_MICROARCH.md (HBM section): on gfx950
-FETCH_SIZE reports exactly half of the bytes of a wide coalesced streaming read (16 B per lane), so
-it is doubled for the streaming kernels; WRITE_SIZE reads 16-B-per-lane streaming stores exactly.
-The join's gathers (index lookups) are other access widths the guide leaves uncalibrated: its
-FETCH_SIZE is reported raw and doubled side by side, and `bytes_per_launch` uses the doubled value
-(an upper bound for the gathers, exact for the streaming record reads).
+FETCH_SIZE and WRITE_SIZE are in KiB per dispatch.  The read side is calibrated on known byte counts
+(tools/traffic_probe.hip, profiles/r6/traffic_probe_pmc.txt): on gfx950 EVERY memory-side read request
+is a 128-B line -- TCC_EA0_RDREQ_128B = TCC_EA0_RDREQ for coalesced 16-B streams, whole-line gathers,
+one 4-B word per line, and random 4-, 8- and 16-B gathers over a 4 GiB table alike -- while FETCH_SIZE
+tallies 64 B per request, so it reports half the bytes for all of them (not only for wide streaming
+reads).  The read bytes are therefore 32 n_32B + 64 n_64B + 128 n_128B from the TCC_EA0_RDREQ size
+counters when that pass exists (`fetch_source` "rdreq_sizes"), else 2 x FETCH_SIZE, which the probe
+shows to be the same for these access shapes.  WRITE_SIZE (64 B per 64-B write request) reads 16-B
+streaming stores exactly (the probe's copy).
 """
 import csv
 import glob
@@ -64,34 +67,49 @@ def mean_for(d, sub, counter, largest=False):
     return sum(vals) / len(vals) if vals else None
 
 
+def read_bytes(d, sub, largest=False):
+    """(bytes read per dispatch, source): the TCC_EA0_RDREQ size counters when present, else 2 x FETCH_SIZE."""
+    n128 = mean_for(d, sub, "TCC_EA0_RDREQ_128B_sum", largest)
+    if n128 is not None:
+        n64 = mean_for(d, sub, "TCC_EA0_RDREQ_64B_sum", largest) or 0.0
+        n32 = mean_for(d, sub, "TCC_EA0_RDREQ_32B_sum", largest) or 0.0
+        return 128.0 * n128 + 64.0 * n64 + 32.0 * n32, "rdreq_sizes"
+    f = mean_for(d, sub, "FETCH_SIZE", largest)
+    return (None, None) if f is None else (2.0 * f * 1024, "fetch_size_x2")
+
+
 def main(root, out, points=1_000_000_000, join_points=1_000_000_000, table_rows=250_000_000):
     d = per_dispatch(root)
     res = {}
     for name, (sub, unit, alg) in STREAMING.items():
         f, w = mean_for(d, sub, "FETCH_SIZE", True), mean_for(d, sub, "WRITE_SIZE", True)
-        if f is None or w is None:
+        fb, src = read_bytes(d, sub, True)
+        if fb is None or w is None:
             continue
         n = points if unit == "points" else (table_rows if unit == "rows" else min(points, 100_000_000))
-        fb, wb = 2.0 * f * 1024, w * 1024
+        wb = w * 1024
         res[name] = {"n": n, "kernel": sub, "bytes_per_launch": fb + wb, "fetch_bytes": fb, "write_bytes": wb,
                      "fetch_size_raw_kib": f, "write_size_kib": w, "algorithmic_bytes": alg * n,
-                     "traffic_over_algorithmic": round((fb + wb) / (alg * n), 4),
-                     "correction": "FETCH_SIZE x2 (gfx950, 16-B/lane streaming reads)"}
+                     "traffic_over_algorithmic": round((fb + wb) / (alg * n), 4), "fetch_source": src,
+                     "correction": "read bytes = 128 B per TCC_EA0_RDREQ_128B request (= 2 x FETCH_SIZE on gfx950, "
+                                   "calibrated by tools/traffic_probe.hip)"}
     for mode, (kernels, chunk) in JOIN_MODES.items():
         nchunks = -(-join_points // chunk)
         parts, total_raw, total = {}, 0.0, 0.0
         for k in kernels:
             f, w = mean_for(d, k, "FETCH_SIZE"), mean_for(d, k, "WRITE_SIZE")
-            if f is None or w is None:
+            fb, src = read_bytes(d, k)
+            if f is None or w is None or fb is None:
                 continue
-            parts[k] = {"fetch_size_raw_kib": f, "write_size_kib": w}
+            parts[k] = {"fetch_size_raw_kib": f, "write_size_kib": w, "read_bytes": fb, "fetch_source": src}
             total_raw += (f + w) * 1024 * nchunks
-            total += (2 * f + w) * 1024 * nchunks
+            total += (fb + w * 1024) * nchunks
         if len(parts) == len(kernels):
             res["pip_join"] = {"n": join_points, "mode": mode, "kernels": parts, "dispatches": nchunks,
                                "bytes_per_launch": total, "bytes_raw": total_raw,
-                               "note": "whole join step; FETCH_SIZE doubled (exact for the streaming point reads, "
-                                       "uncalibrated for the index gathers: raw value in bytes_raw)"}
+                               "note": "whole join step; reads = 128 B per memory-side read request, the index gathers "
+                                       "included (every L2 miss fetches a whole 128-B line: tools/traffic_probe.hip); "
+                                       "FETCH_SIZE + WRITE_SIZE uncorrected in bytes_raw"}
     # FP64 VALU work of the join (SQ_INSTS_VALU_FLOPS_FP64 pass), per launch
     fp = mean_for(d, "k_pip_join_q<true", "SQ_INSTS_VALU_FLOPS_FP64")
     if fp is not None:
