@@ -1201,6 +1201,15 @@ def main():
                           % (J, n_polys)}
         pj["roofline"]["bytes_per_unit"] = "16 B/point + 12 B/pair"
         pj["roofline"]["gather_model"] = gather_model(census, J, npairs.value, jms)
+        tr = pj["roofline"].get("traffic")
+        if tr:   # the calibrated view: every L2 miss moves a whole 128-B line (tools/traffic_probe.hip), so the
+            # kernel's own line traffic (PMC bytes) against the box's streaming rate is its bandwidth roofline
+            pj["roofline"]["line_traffic"] = {
+                "bytes": tr, "over_algorithmic": round(tr / (16.0 * J + 12.0 * npairs.value), 3),
+                "gbs": round(tr / (jms * 1e-3) / 1e9, 1), "stream_gbs": PROBE_STREAM_GBS,
+                "frac_of_stream": round(tr / (jms * 1e-3) / 1e9 / PROBE_STREAM_GBS, 4),
+                "note": "PMC read bytes = 128 B per memory-side read request (TCC_EA0_RDREQ_128B) + WRITE_SIZE, from "
+                        "profiles/pmc_traffic.json; the join is bound by these whole-line misses"}
         # FP64 work: E_c = the edges of every (point, polygon) pair whose envelope test
         # passes, counted by the C restatement over a prefix of the same device point stream, scaled;
         # 7 FP64 ops per candidate edge is the reference walk's orientation arithmetic

@@ -202,13 +202,6 @@ __global__ __launch_bounds__(256) void k_pair_move(PairOut o, const PairPlan* __
 // access holds one of the CU's outstanding-miss slots for its latency, so the cost is the count of
 // gathers by kind (the gather model); 42% of the bench's points stop at the
 // bitmap.
-// GM_JX_STAGE (timing builds only, never the shipped library: build.py refuses GM_JX_* there): the
-// lookup chain cut after a stage, on the same points, to price each stage -- 1 = the point stream and
-// the LDS bitmap only (no gather), 2 = + the coarse gathers (mixed coarse cells dropped), 3 = + the fine
-// gathers and their in-register decisions (items and list walks dropped), 4 = the whole join
-#ifndef GM_JX_STAGE
-#define GM_JX_STAGE 4
-#endif
 template <bool WRITE, int SRC, bool VEC>
 __global__ __launch_bounds__(QTPB) void k_pip_join_q(const double* __restrict__ px, const double* __restrict__ py,
                                                      int64_t n, int64_t id_base, PipDev d, PairOut po,
@@ -226,7 +219,6 @@ __global__ __launch_bounds__(QTPB) void k_pip_join_q(const double* __restrict__ 
   double* fx = s_fx[wv]; double* fy = s_fy[wv]; uint32_t* fid = s_fid[wv];
   double* qx = s_ix[wv]; double* qy = s_iy[wv]; uint32_t* qid = s_iid[wv]; uint32_t* qref = s_iref[wv];
   int fn = 0, qn = 0, qg = 0;   // wave-uniform fills: fine queue, line items, blob items
-  int jx_sink = 0;              // GM_JX_STAGE 1 only
   int64_t sbase = -1;           // wave-uniform: this wave's current output slab and its fill
   int sfill = SLAB;
   int my_count = 0;
@@ -250,29 +242,9 @@ __global__ __launch_bounds__(QTPB) void k_pip_join_q(const double* __restrict__ 
     }
   };
   auto pair_push = [&](bool hit, uint32_t id, int poly) __attribute__((always_inline)) {
-#ifdef GM_JX_NOPAIRS   // timing builds: the pairs are counted into the sink, nothing is stored
-    jx_sink += hit ? (int)(id ^ (uint32_t)poly) : 0;
-    return;
-#endif
     if (!WRITE) { my_count += hit; return; }
     const uint64_t m = __ballot(hit);
     if (!m) return;
-#ifdef GM_JX_PAIRS_DIRECT   // timing builds: round 5's stores of each push's hits where they fell
-    {
-      const int c = __popcll(m), off = lanes_below(m), room = SLAB - sfill;
-      if (hit && off < room) pair_store(po, sbase + sfill + off, id_base + id, poly);
-      if (c > room) {
-        unsigned long long b = 0;
-        if (lane == 0) b = atomicAdd(po.counter, (unsigned long long)SLAB);
-        sbase = (int64_t)__shfl(b, 0, 64);
-        if (hit && off >= room) pair_store(po, sbase + (off - room), id_base + id, poly);
-        sfill = c - room;
-      } else {
-        sfill += c;
-      }
-      return;
-    }
-#endif
     const int c = __popcll(m);
     const int k = (lane - pcnt) & 63;   // this lane's slot takes the hit of rank k (when k < c)
     const bool take = k < c;
@@ -411,12 +383,10 @@ __global__ __launch_bounds__(QTPB) void k_pip_join_q(const double* __restrict__ 
         const int cx = cell_of(x, d.gx0, d.inv_cw, d.gx), cy = cell_of(y, d.gy0, d.inv_ch, d.gy);
         const int loc = sc8_locate(w8, x, y, d, cx, cy);
         if (loc >= 0) { ihit = join_hit(d.op, loc); w = CELL_EMPTY << 30; }
-        else if (GM_JX_STAGE >= 4) w = d.cell_word[(int64_t)cy * d.gx + cx];   // near the line: the original word's blob decides
+        else w = d.cell_word[(int64_t)cy * d.gx + cx];   // near the line: the original word's blob decides
       }
-      uint32_t kind = w >> 30;
-      const uint32_t ref = w & 0x3fffffffu;
+      const uint32_t kind = w >> 30, ref = w & 0x3fffffffu;
       pair_push(kind == CELL_INTERIOR || ihit, id, ihit ? sc8_poly(w8) : (int)ref);
-      if (GM_JX_STAGE < 4) kind = CELL_EMPTY;   // timing build: no items, no list walks
       const bool item = kind == CELL_BOUNDARY;
       item_push(item, item && lines_on && (ref & (BLOB_COMPACT | SC_LINE)) == (BLOB_COMPACT | SC_LINE), x, y, id, ref);
       l_j = 0;
@@ -439,19 +409,8 @@ __global__ __launch_bounds__(QTPB) void k_pip_join_q(const double* __restrict__ 
       const int cnt = min(fn, FBATCH);
       const int a = fn - cnt + lane;
       pend_w = make_uint2(CELL_EMPTY << 30, 0u);
-#ifdef GM_JX_FINE_AUX   // timing builds: the fine gathers as buffer loads with another cache policy (aux bits)
-      if (lane < cnt) {
-        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)d.cell_sc8, 0,
-                                                                            (int)((int64_t)d.gx * d.gy * 8), 0x00020000);
-        const int64_t ci = (int64_t)cell_of(fy[a], d.gy0, d.inv_ch, d.gy) * d.gx + cell_of(fx[a], d.gx0, d.inv_cw, d.gx);
-        typedef unsigned int u2v __attribute__((ext_vector_type(2)));
-        const u2v v = __builtin_amdgcn_raw_buffer_load_b64(rs, (int)(ci * 8), 0, GM_JX_FINE_AUX);
-        pend_w = make_uint2(v.x, v.y);
-      }
-#else
       if (lane < cnt)
         pend_w = d.cell_sc8[(int64_t)cell_of(fy[a], d.gy0, d.inv_ch, d.gy) * d.gx + cell_of(fx[a], d.gx0, d.inv_cw, d.gx)];
-#endif
       pb = fn - cnt;
       pc = cnt;
       pend = true;
@@ -471,18 +430,14 @@ __global__ __launch_bounds__(QTPB) void k_pip_join_q(const double* __restrict__ 
         g0 = g0 && !e0;
         g1 = g1 && !e1;
       }
-      if (GM_JX_STAGE >= 2) {
-        if (g0) c0 = d.coarse_sc[(int64_t)(cy0 >> CF_LOG) * d.gxc + (cx0 >> CF_LOG)];
-        if (g1) c1 = d.coarse_sc[(int64_t)(cy1 >> CF_LOG) * d.gxc + (cx1 >> CF_LOG)];
-      } else {   // timing build: keep the stream and the cell arithmetic alive (no pair depends on them)
-        jx_sink += (g0 ? cx0 + cy0 : 0) + (g1 ? cx1 + cy1 : 0);
-      }
+      if (g0) c0 = d.coarse_sc[(int64_t)(cy0 >> CF_LOG) * d.gxc + (cx0 >> CF_LOG)];
+      if (g1) c1 = d.coarse_sc[(int64_t)(cy1 >> CF_LOG) * d.gxc + (cx1 >> CF_LOG)];
       c0 = coarse_mask(c0, cx0, cy0, d.coarse_fmt);
       c1 = coarse_mask(c1, cx1, cy1, d.coarse_fmt);
       const uint32_t id0 = (uint32_t)(2 * (step * 64 + lane)), id1 = id0 + 1;
       pair_push((c0 >> 30) == CELL_INTERIOR, id0, (int)(c0 & 0x3fffffffu));
       pair_push((c1 >> 30) == CELL_INTERIOR, id1, (int)(c1 & 0x3fffffffu));
-      const bool f0 = GM_JX_STAGE >= 3 && (c0 >> 30) == CELL_LIST, f1 = GM_JX_STAGE >= 3 && (c1 >> 30) == CELL_LIST;
+      const bool f0 = (c0 >> 30) == CELL_LIST, f1 = (c1 >> 30) == CELL_LIST;
       const uint64_t m0 = __ballot(f0), m1 = __ballot(f1);
       if (GM_REF_BAD(fn + 128 > FCAP)) { if (lane == 0 && (m0 | m1)) pip_fault(d, PIP_FAULT_QUEUE); }   // cannot happen: fn < 128
       else {
@@ -498,7 +453,6 @@ __global__ __launch_bounds__(QTPB) void k_pip_join_q(const double* __restrict__ 
     }
     break;   // every stage idle and the item queue empty (the item stage drains it once nothing else runs)
   }
-  if (jx_sink == 0x7fffffff) pip_fault(d, PIP_FAULT_QUEUE);   // timing builds only: a use of the sink (0 otherwise)
   if (WRITE) {
     if (pcnt > 0) {   // the last pending pairs: a partial slab (k_pair_plan closes the hole behind them)
       slab_room();
