@@ -295,7 +295,8 @@ def _xchg_worker(rank, world, port, sizes, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,sizes", [(2, (5000, 3001)), (3, (4000, 0, 2500))])
+@pytest.mark.parametrize("world,sizes", [(2, (5000, 3001)), (3, (4000, 0, 2500)),
+                                         (8, (3000, 2000, 0, 4100, 1, 2500, 3333, 1800))])
 def test_partition_exchange_by_key_range(world, sizes):
     """Splitters from every rank's UNSORTED sample, the stable partition, the per-column all-to-all: every
     row lands on the rank owning its key range, nothing is lost or duplicated, the ranges are ordered,
