@@ -27,7 +27,7 @@ leg_args() {   # the bench arguments of one leg
   case $1 in
     join) echo "--only join --no-cpu --no-gather --steps 1 --warmup 0 --join-steps 3" ;;
     ranges) echo "--only extra --no-cpu --no-gather --steps 2 --warmup 1" ;;
-    table) echo "--only table --no-cpu --steps 2 --warmup 1" ;;
+    table) echo "--only z3,table --no-cpu --steps 2 --warmup 1" ;;   # the table's keys come from the z3 leg
     z3) echo "--only z3 --no-cpu --steps 10 --warmup 2" ;;
     extra) echo "--only extra --no-cpu --steps 6 --warmup 1" ;;
     *) echo "--no-cpu" ;;
@@ -124,15 +124,16 @@ for step in "$@"; do
       unset GEOMESA_HIP_LIB ;;
     ab)
       leg=${arg%%:*}; libs=${arg#*:}
+      aout=${out}_$leg   # one record set per leg (several ab steps in one lease)
       for r in 1 2 3; do
         for lib in ${libs//,/ }; do
           if [ "$lib" = prod ]; then unset GEOMESA_HIP_LIB; else export GEOMESA_HIP_LIB=$PWD/geomesa_amd/lib/$lib.so; fi
-          timeout -k 10 300 python -u bench.py $(leg_args $leg) > ${out}_ab_${lib}_$r.json 2> ${out}_ab_${lib}_$r.err
-          cp gpurun_out/bench_detail_n1.json ${out}_ab_${lib}_$r.detail.json
+          timeout -k 10 300 python -u bench.py $(leg_args $leg) > ${aout}_ab_${lib}_$r.json 2> ${aout}_ab_${lib}_$r.err
+          cp gpurun_out/bench_detail_n1.json ${aout}_ab_${lib}_$r.detail.json
         done
       done
       unset GEOMESA_HIP_LIB
-      python3 tools/show_ab.py ${out}_ab > ${out}_ab.txt ;;
+      python3 tools/show_ab.py ${aout}_ab > ${aout}_ab.txt ;;
     probe)
       timeout -k 10 400 python -u tools/$arg.py $PROBE_ARGS > ${out}_$arg.txt 2>&1 ;;
     abprobe)
