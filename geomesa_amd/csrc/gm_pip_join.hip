@@ -418,11 +418,11 @@ __global__ __launch_bounds__(QTPB) void k_pip_join_q(const double* __restrict__ 
     }
     if (streaming) {   // ---- stream step: 2 points per lane, their coarse words together
       uint32_t c0 = CELL_EMPTY << 30, c1 = CELL_EMPTY << 30;
-      int cx0 = 0, cy0 = 0, cx1 = 0, cy1 = 0;
       bool g0 = X0 >= d.gx0 && X0 <= d.gx1 && Y0 >= d.gy0 && Y0 <= d.gy1;   // NaN fails
       bool g1 = X1 >= d.gx0 && X1 <= d.gx1 && Y1 >= d.gy0 && Y1 <= d.gy1;
-      if (g0) { cx0 = cell_of(X0, d.gx0, d.inv_cw, d.gx); cy0 = cell_of(Y0, d.gy0, d.inv_ch, d.gy); }
-      if (g1) { cx1 = cell_of(X1, d.gx0, d.inv_cw, d.gx); cy1 = cell_of(Y1, d.gy0, d.inv_ch, d.gy); }
+      // every lane computes its cells (clamped, NaN -> 0; unused outside the grid): no branch around them
+      const int cx0 = cell_of(X0, d.gx0, d.inv_cw, d.gx), cy0 = cell_of(Y0, d.gy0, d.inv_ch, d.gy);
+      const int cx1 = cell_of(X1, d.gx0, d.inv_cw, d.gx), cy1 = cell_of(Y1, d.gy0, d.inv_ch, d.gy);
       if (cm_words) {   // EMPTY coarse blocks from the LDS bitmap: no gather
         const int b0 = ((cy0 >> CF_LOG) >> d.cm_shift_y) * d.cm_w + ((cx0 >> CF_LOG) >> d.cm_shift);
         const int b1 = ((cy1 >> CF_LOG) >> d.cm_shift_y) * d.cm_w + ((cx1 >> CF_LOG) >> d.cm_shift);

@@ -125,18 +125,17 @@ __global__ __launch_bounds__(RTPB) void k_pip_relate(const int32_t* __restrict__
       bool gat[RILP];
 #pragma unroll
       for (int u = 0; u < RILP; ++u) {
-        gat[u] = false;
-        cx[u] = cy[u] = 0;
-        if (p[u] >= 0 && p[u] < n_polys && x[u] >= d.gx0 && x[u] <= d.gx1 && y[u] >= d.gy0 && y[u] <= d.gy1) {
-          cx[u] = cell_of(x[u], d.gx0, d.inv_cw, d.gx);
-          cy[u] = cell_of(y[u], d.gy0, d.inv_ch, d.gy);
-          bool empty = false;
-          if (cm_words) {
-            const int b = ((cy[u] >> CF_LOG) >> bm_sy) * bm_w + ((cx[u] >> CF_LOG) >> bm_sx);
-            empty = (s_cm[b >> 5] >> (b & 31)) & 1u;
-          }
-          gat[u] = !empty;
+        // the cells of every row, clamped (unused for a row outside the grid): no branch around them
+        const bool in = p[u] >= 0 && p[u] < n_polys && x[u] >= d.gx0 && x[u] <= d.gx1 && y[u] >= d.gy0 &&
+                        y[u] <= d.gy1;
+        cx[u] = cell_of(x[u], d.gx0, d.inv_cw, d.gx);
+        cy[u] = cell_of(y[u], d.gy0, d.inv_ch, d.gy);
+        bool empty = false;
+        if (cm_words) {
+          const int b = ((cy[u] >> CF_LOG) >> bm_sy) * bm_w + ((cx[u] >> CF_LOG) >> bm_sx);
+          empty = (s_cm[b >> 5] >> (b & 31)) & 1u;
         }
+        gat[u] = in && !empty;
       }
       uint32_t craw[RILP];
 #pragma unroll
