@@ -257,22 +257,21 @@ __device__ __forceinline__ double log_near_pow2(int k, double x) {
 // XZ length l1 = floor(log(maxDim) / log(0.5)).toInt (z3/curve/XZ2SFC.scala:63, XZ3SFC.scala:62)
 __device__ __forceinline__ int32_t xz_l1(double maxdim) {
   const double LOG_HALF = -0.6931471805599453094;  // math.log(0.5), correctly rounded
-  if (maxdim == 0.0) return INT32_MAX;             // log(0) = -inf -> +inf -> Int.MaxValue
-  int e;
-  double f = frexp(maxdim, &e);                    // maxdim = f * 2^e, f in [0.5, 1)
-  double lg;
   const double NEAR = 1.9073486328125e-06;         // 2^-19
-  if (__dsub_rn(f, 0.5) < 0.5 * NEAR) {
-    lg = log_near_pow2(e - 1, __dsub_rn(__dmul_rn(2.0, f), 1.0));   // exact: 2f - 1
-  } else if (__dsub_rn(1.0, f) < 0.5 * NEAR) {
-    lg = log_near_pow2(e, __dsub_rn(f, 1.0));                         // exact: f - 1
-  } else {
-    // maxdim = f 2^e with |f - 0.5|, |1 - f| >= 2^-20: the quotient log(maxdim)/log(0.5) = -e - log2(f)
-    // lies in (-e, -e + 1), at least 1.4e-6 away from either integer -- far beyond the few ulps by
-    // which the JVM's rounded log and division can move it -- so its floor is exactly -e.
-    return -e;
+  int e;
+  const double f = frexp(maxdim, &e);              // maxdim = f * 2^e, f in [0.5, 1)
+  // Away from powers of two (|f - 0.5|, |1 - f| >= 2^-20) the quotient log(maxdim)/log(0.5) = -e - log2(f)
+  // lies in (-e, -e + 1), at least 1.4e-6 away from either integer -- far beyond the few ulps by which
+  // the JVM's rounded log and division can move it -- so its floor is exactly -e.  log(0) = -inf gives
+  // +inf -> Int.MaxValue.  Both are selects; only the rare near-power-of-two envelope branches.
+  const bool lo = __dsub_rn(f, 0.5) < 0.5 * NEAR, hi = __dsub_rn(1.0, f) < 0.5 * NEAR;
+  int32_t r = maxdim == 0.0 ? INT32_MAX : -e;
+  if (((int)lo | (int)hi) & (int)(maxdim != 0.0)) {
+    // m = 2^(e-1) (2f) with 2f - 1 exact, or m = 2^e f with f - 1 exact
+    const double lg = log_near_pow2(lo ? e - 1 : e, lo ? __dsub_rn(__dmul_rn(2.0, f), 1.0) : __dsub_rn(f, 1.0));
+    r = jvm_d2i(floor(__ddiv_rn(lg, LOG_HALF)));
   }
-  return jvm_d2i(floor(__ddiv_rn(lg, LOG_HALF)));
+  return r;
 }
 
 // ---------------------------------------------------------------- JTS orientation (CGAlgorithmsDD)

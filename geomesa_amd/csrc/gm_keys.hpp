@@ -102,7 +102,6 @@ __device__ __forceinline__ uint8_t z2_index_one(double x, double y, const NDim& 
 
 // ------------------------------------------------------------------ XZ2 / XZ3
 
-__device__ __forceinline__ double clampd(double v, double lo, double hi) { return v < lo ? lo : (v > hi ? hi : v); }
 __device__ __forceinline__ double jmax(double a, double b) { return a >= b ? a : b; }  // operands never NaN/-0 here
 
 // The XZ sequence code without the per-level FP loop.  XZ2SFC.sequenceCode (XZ2SFC.scala:264-286)
@@ -126,69 +125,85 @@ __device__ __forceinline__ bool xz_fits(double mn, double mx, double w2, double 
   return mx <= __dadd_rn(__dmul_rn(floor(__dmul_rn(mn, inv_w2)), w2), __dmul_rn(2.0, w2));
 }
 
-// XZ2SFC.index (z3/curve/XZ2SFC.scala:54-77) with normalize (:318-350), sequenceCode (:264-286)
+// RN(a / b) for the constant spans b = 360, 180 and a = v - lo in {0} u [2^-45, b] (v a finite clamped
+// coordinate, so a is 0 or at least ulp(180)): q = RN(a y) with y = RN(1 / b) is within one ulp of a / b,
+// r = a - q b is exact in one fma, and RN(q + r y) is the correctly rounded quotient (Markstein's
+// correction theorem; no underflow on this domain).  Three f64 ops against the ~10 of the IEEE divide
+// sequence; checked against a / b on 1.6e9 values here (random, every exponent down to 2^-45, and
+// +-3 ulp around every j b / 2^20) and bit-compared with the oracle by the GPU parity tests.
+__device__ __forceinline__ double div_span(double a, double b, double y) {
+#ifdef GM_XZ_DIV_IEEE
+  (void)y;
+  return __ddiv_rn(a, b);
+#else
+  const double q = __dmul_rn(a, y);
+  return __fma_rn(__fma_rn(-q, b, a), y, q);
+#endif
+}
+
+// the level count: l1 >= g -> g, else l1 + 1 when the envelope fits the next level's 2x2 cells
+// (XZ2SFC.scala:62-75), as selects.  l1 = Int.MaxValue (a zero-size envelope) is clamped before the
+// power of two is formed; that branch's fits value is never used.
+__device__ __forceinline__ int xz_length(int32_t l1, int g, int fits_all) {
+  return l1 >= g ? g : (fits_all ? l1 + 1 : l1);
+}
+
+// XZ2SFC.index (z3/curve/XZ2SFC.scala:54-77) with normalize (:318-350), sequenceCode (:264-286).
+// Branch-free in the common path: the status is a select, the out-of-range and NaN cases are clamped
+// (fmin / fmax drop NaN) and computed like any other envelope, and the key is zeroed at the end.
 template <bool LENIENT>
 __device__ __forceinline__ uint8_t xz2_one(int g, double xmin, double ymin, double xmax, double ymax, int64_t& out) {
-  if (!(xmin <= xmax && ymin <= ymax)) { out = 0; return ST_UNORDERED; }
-  if (!(xmin >= -180.0 && xmax <= 180.0 && ymin >= -90.0 && ymax <= 90.0)) {
-    if (!LENIENT) { out = 0; return ST_OUT_OF_BOUNDS; }
-    xmin = clampd(xmin, -180.0, 180.0); ymin = clampd(ymin, -90.0, 90.0);
-    xmax = clampd(xmax, -180.0, 180.0); ymax = clampd(ymax, -90.0, 90.0);
-  }
-  const double nxmin = __ddiv_rn(__dsub_rn(xmin, -180.0), 360.0);
-  const double nymin = __ddiv_rn(__dsub_rn(ymin, -90.0), 180.0);
-  const double nxmax = __ddiv_rn(__dsub_rn(xmax, -180.0), 360.0);
-  const double nymax = __ddiv_rn(__dsub_rn(ymax, -90.0), 180.0);
+  const bool ordered = xmin <= xmax && ymin <= ymax;
+  const bool inside = xmin >= -180.0 && xmax <= 180.0 && ymin >= -90.0 && ymax <= 90.0;
+  const uint8_t st = !ordered ? (uint8_t)ST_UNORDERED : ((LENIENT || inside) ? (uint8_t)ST_OK : (uint8_t)ST_OUT_OF_BOUNDS);
+  xmin = fmin(fmax(xmin, -180.0), 180.0); ymin = fmin(fmax(ymin, -90.0), 90.0);
+  xmax = fmin(fmax(xmax, -180.0), 180.0); ymax = fmin(fmax(ymax, -90.0), 90.0);
+  const double RX = 1.0 / 360.0, RY = 1.0 / 180.0;   // RN(1 / b), folded at compile time
+  const double nxmin = div_span(__dsub_rn(xmin, -180.0), 360.0, RX);
+  const double nymin = div_span(__dsub_rn(ymin, -90.0), 180.0, RY);
+  const double nxmax = div_span(__dsub_rn(xmax, -180.0), 360.0, RX);
+  const double nymax = div_span(__dsub_rn(ymax, -90.0), 180.0, RY);
   const double maxdim = jmax(__dsub_rn(nxmax, nxmin), __dsub_rn(nymax, nymin));
   const int32_t l1 = xz_l1(maxdim);
-  int length;
-  if (l1 >= g) {
-    length = g;
-  } else {
-    const double w2 = ldexp(1.0, -(l1 + 1)), inv = ldexp(1.0, l1 + 1);   // math.pow(0.5, l1 + 1), exact
-    length = (xz_fits(nxmin, nxmax, w2, inv) && xz_fits(nymin, nymax, w2, inv)) ? l1 + 1 : l1;
-  }
-  if (length == 0) { out = 0; return ST_OK; }
+  const int32_t lc = l1 < g ? l1 : g;
+  const double w2 = ldexp(1.0, -(lc + 1)), inv = ldexp(1.0, lc + 1);   // math.pow(0.5, l1 + 1), exact
+  const int length = xz_length(l1, g, (int)xz_fits(nxmin, nxmax, w2, inv) & (int)xz_fits(nymin, nymax, w2, inv));
   const uint32_t ix = xz_cell(nxmin, length), iy = xz_cell(nymin, length);
   const uint64_t il = z2_split(ix) | (z2_split(iy) << 1);
   const uint64_t num = (il << (2 * (g - length + 1))) - (uint64_t)(__popc(ix) + 2 * __popc(iy));
-  out = (int64_t)length + (int64_t)(num / 3u);
-  return ST_OK;
+  out = (st == ST_OK && length != 0) ? (int64_t)length + (int64_t)(num / 3u) : 0;
+  return st;
 }
 
-// XZ3SFC.index (z3/curve/XZ3SFC.scala:53-76) with normalize (:338-380), sequenceCode (:275-304)
+// XZ3SFC.index (z3/curve/XZ3SFC.scala:53-76) with normalize (:338-380), sequenceCode (:275-304).  The
+// time span zhi is a run-time value and z may be any double in [0, zhi], so z keeps the IEEE divide.
 template <bool LENIENT>
 __device__ __forceinline__ uint8_t xz3_one(int g, double zhi, double xmin, double ymin, double zmin, double xmax,
                                            double ymax, double zmax, int64_t& out) {
-  if (!(xmin <= xmax && ymin <= ymax && zmin <= zmax)) { out = 0; return ST_UNORDERED; }
-  if (!(xmin >= -180.0 && xmax <= 180.0 && ymin >= -90.0 && ymax <= 90.0 && zmin >= 0.0 && zmax <= zhi)) {
-    if (!LENIENT) { out = 0; return ST_OUT_OF_BOUNDS; }
-    xmin = clampd(xmin, -180.0, 180.0); ymin = clampd(ymin, -90.0, 90.0); zmin = clampd(zmin, 0.0, zhi);
-    xmax = clampd(xmax, -180.0, 180.0); ymax = clampd(ymax, -90.0, 90.0); zmax = clampd(zmax, 0.0, zhi);
-  }
+  const bool ordered = xmin <= xmax && ymin <= ymax && zmin <= zmax;
+  const bool inside = xmin >= -180.0 && xmax <= 180.0 && ymin >= -90.0 && ymax <= 90.0 && zmin >= 0.0 && zmax <= zhi;
+  const uint8_t st = !ordered ? (uint8_t)ST_UNORDERED : ((LENIENT || inside) ? (uint8_t)ST_OK : (uint8_t)ST_OUT_OF_BOUNDS);
+  xmin = fmin(fmax(xmin, -180.0), 180.0); ymin = fmin(fmax(ymin, -90.0), 90.0); zmin = fmin(fmax(zmin, 0.0), zhi);
+  xmax = fmin(fmax(xmax, -180.0), 180.0); ymax = fmin(fmax(ymax, -90.0), 90.0); zmax = fmin(fmax(zmax, 0.0), zhi);
+  const double RX = 1.0 / 360.0, RY = 1.0 / 180.0;
   const double zsize = __dsub_rn(zhi, 0.0);
-  const double nxmin = __ddiv_rn(__dsub_rn(xmin, -180.0), 360.0);
-  const double nymin = __ddiv_rn(__dsub_rn(ymin, -90.0), 180.0);
+  const double nxmin = div_span(__dsub_rn(xmin, -180.0), 360.0, RX);
+  const double nymin = div_span(__dsub_rn(ymin, -90.0), 180.0, RY);
   const double nzmin = __ddiv_rn(__dsub_rn(zmin, 0.0), zsize);
-  const double nxmax = __ddiv_rn(__dsub_rn(xmax, -180.0), 360.0);
-  const double nymax = __ddiv_rn(__dsub_rn(ymax, -90.0), 180.0);
+  const double nxmax = div_span(__dsub_rn(xmax, -180.0), 360.0, RX);
+  const double nymax = div_span(__dsub_rn(ymax, -90.0), 180.0, RY);
   const double nzmax = __ddiv_rn(__dsub_rn(zmax, 0.0), zsize);
   const double maxdim = jmax(jmax(__dsub_rn(nxmax, nxmin), __dsub_rn(nymax, nymin)), __dsub_rn(nzmax, nzmin));
   const int32_t l1 = xz_l1(maxdim);
-  int length;
-  if (l1 >= g) {
-    length = g;
-  } else {
-    const double w2 = ldexp(1.0, -(l1 + 1)), inv = ldexp(1.0, l1 + 1);
-    length = (xz_fits(nxmin, nxmax, w2, inv) && xz_fits(nymin, nymax, w2, inv) && xz_fits(nzmin, nzmax, w2, inv))
-                 ? l1 + 1 : l1;
-  }
-  if (length == 0) { out = 0; return ST_OK; }
+  const int32_t lc = l1 < g ? l1 : g;
+  const double w2 = ldexp(1.0, -(lc + 1)), inv = ldexp(1.0, lc + 1);
+  const int length = xz_length(l1, g, (int)xz_fits(nxmin, nxmax, w2, inv) & (int)xz_fits(nymin, nymax, w2, inv) &
+                                          (int)xz_fits(nzmin, nzmax, w2, inv));
   const uint32_t ix = xz_cell(nxmin, length), iy = xz_cell(nymin, length), iz = xz_cell(nzmin, length);
   const uint64_t il = z3_split(ix) | (z3_split(iy) << 1) | (z3_split(iz) << 2);
   const uint64_t num = (il << (3 * (g - length + 1))) - (uint64_t)(__popc(ix) + 2 * __popc(iy) + 4 * __popc(iz));
-  out = (int64_t)length + (int64_t)(num / 7u);
-  return ST_OK;
+  out = (st == ST_OK && length != 0) ? (int64_t)length + (int64_t)(num / 7u) : 0;
+  return st;
 }
 
 // ------------------------------------------------------------------ host-side dimension setup
