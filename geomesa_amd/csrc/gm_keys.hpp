@@ -126,8 +126,8 @@ __device__ __forceinline__ bool xz_fits(double mn, double mx, double w2, double 
 }
 
 // RN(a / b) for the constant spans b = 360, 180 and a = v - lo in {0} u [2^-45, b] (v a finite clamped
-// coordinate, so a is 0 or at least ulp(180)): q = RN(a y) with y = RN(1 / b) is within one ulp of a / b,
-// r = a - q b is exact in one fma, and RN(q + r y) is the correctly rounded quotient (Markstein's
+// coordinate, so a is 0 or at least ulp(180)): y = RN(1 / b) has y b = 1 + 0.34 * 2^-53 for both spans, so
+// q = RN(a y) is within one ulp of a / b, r = a - q b is exact in one fma, and RN(q + r y) is the correctly rounded quotient (Markstein's
 // correction theorem; no underflow on this domain).  Three f64 ops against the ~10 of the IEEE divide
 // sequence; checked against a / b on 1.6e9 values here (random, every exponent down to 2^-45, and
 // +-3 ulp around every j b / 2^20) and bit-compared with the oracle by the GPU parity tests.
