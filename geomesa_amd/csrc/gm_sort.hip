@@ -252,6 +252,10 @@ __global__ __launch_bounds__(CT) void k_sort_count(KeyCols c, int64_t n, DigitOf
 constexpr int PT = GM_SORT_PT, PW = PT / 64, PSLOT = GM_SORT_PSLOT, PTILE = PT * 2 * PSLOT;   // 8192 rows per tile
 static_assert(PT >= NB_MAX, "one thread per digit");
 constexpr uint64_t GR_VAL = (1ull << 48) - 1;
+#ifndef GM_SORT_LB
+#define GM_SORT_LB 4
+#endif
+constexpr int LB = GM_SORT_LB;   // look-back granules per round trip
 
 struct PassArgs {
   KeyCols in;             // the caller's columns (first pass) ...
@@ -412,12 +416,26 @@ __global__ __launch_bounds__(PT) void k_sort_pass(PassArgs a) {
     if (tile > 0) {
       const uint64_t tag_agg = 2 * a.tag, tag_pre = 2 * a.tag + 1;
       int64_t p = tile - 1;
+      // LB granules (tiles p, p - 1, ..., p - LB + 1) per round trip, all loads in flight together:
+      // the walk adds aggregates up to the first inclusive prefix, or re-polls from the first
+      // granule not yet published.  Tile 0 always publishes a prefix, so no walk passes below it.
       for (;;) {
-        const uint64_t v = __hip_atomic_load(a.status + p * nb + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const uint64_t tg = v >> 48;
-        if (tg == tag_pre) { excl += v & GR_VAL; break; }
-        if (tg == tag_agg) { excl += v & GR_VAL; --p; }
-        else __builtin_amdgcn_s_sleep(1);
+        uint64_t v[LB];
+#pragma unroll
+        for (int i = 0; i < LB; ++i)
+          v[i] = p - i >= 0 ? __hip_atomic_load(a.status + (p - i) * nb + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                            : 0ull;
+        int i = 0;
+        bool done = false;
+        for (; i < LB; ++i) {
+          const uint64_t tg = v[i] >> 48;
+          if (tg == tag_pre) { excl += v[i] & GR_VAL; done = true; break; }
+          if (tg != tag_agg) break;
+          excl += v[i] & GR_VAL;
+        }
+        if (done) break;
+        p -= i;
+        if (i < LB) __builtin_amdgcn_s_sleep(1);
       }
       __hip_atomic_store(a.status + tile * nb + t, ((uint64_t)(2 * a.tag + 1) << 48) | (excl + tot),
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
