@@ -286,6 +286,8 @@ __global__ __launch_bounds__(PT) void k_sort_pass(PassArgs a) {
   __shared__ uint32_t s_tile;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int w = a.w, nb = 1 << w;
+  // this pass's global count of digit t, loaded before anything waits (used after the ranking)
+  const uint32_t cg_early = t < nb ? a.counts[t] : 0u;
   if (t == 0) s_tile = atomicAdd(a.ctr, 1u);
   for (int i = t; i < PW * NB_MAX / 2; i += PT) ((uint32_t*)&s_wcnt[0][0])[i] = 0u;
   __syncthreads();
@@ -382,7 +384,7 @@ __global__ __launch_bounds__(PT) void k_sort_pass(PassArgs a) {
     // the tile's count for this digit, published before anything else
     const uint64_t g0 = ((uint64_t)(2 * a.tag + (tile == 0 ? 1 : 0)) << 48) | tot;
     __hip_atomic_store(a.status + tile * nb + t, g0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    cg = a.counts[t];
+    cg = cg_early;
   }
   xt = tot; xb = cg;
 #pragma unroll
