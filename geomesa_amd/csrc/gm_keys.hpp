@@ -127,10 +127,11 @@ __device__ __forceinline__ bool xz_fits(double mn, double mx, double w2, double 
 
 // RN(a / b) for the constant spans b = 360, 180 and a = v - lo in {0} u [2^-45, b] (v a finite clamped
 // coordinate, so a is 0 or at least ulp(180)): y = RN(1 / b) has y b = 1 + 0.34 * 2^-53 for both spans, so
-// q = RN(a y) is within one ulp of a / b, r = a - q b is exact in one fma, and RN(q + r y) is the correctly rounded quotient (Markstein's
-// correction theorem; no underflow on this domain).  Three f64 ops against the ~10 of the IEEE divide
-// sequence; checked against a / b on 1.6e9 values here (random, every exponent down to 2^-45, and
-// +-3 ulp around every j b / 2^20) and bit-compared with the oracle by the GPU parity tests.
+// q = RN(a y) is within one ulp of a / b, r = a - q b is exact in one fma, and RN(q + r y) is the
+// correctly rounded quotient (Markstein's correction theorem; no underflow on this domain).  Three f64
+// ops against the ~10 of the IEEE divide sequence; checked against a / b on the host (tools/div_check.c:
+// random, every exponent down to 2^-45, +-3 ulp around every j b / 2^20) and bit-compared with the
+// oracle by the GPU parity tests.
 __device__ __forceinline__ double div_span(double a, double b, double y) {
 #ifdef GM_XZ_DIV_IEEE
   (void)y;
@@ -138,6 +139,21 @@ __device__ __forceinline__ double div_span(double a, double b, double y) {
 #else
   const double q = __dmul_rn(a, y);
   return __fma_rn(__fma_rn(-q, b, a), y, q);
+#endif
+}
+
+// RN(a / b) for the time span b = BinnedTime.maxOffset(period) (86400000, 604800, 2678400 or 527050: the
+// only z bounds XZ3SFC is built with, XZ3SFC.scala:27-36) and a = z - 0 in [0, b]: RN(1/b) b = 1 + d with
+// |d| <= 0.42 * 2^-53 for all four, so div_span applies; a positive a below 2^-900 (where a y could lose
+// bits to underflow) takes the IEEE divide.  Checked against a / b on 1.67e9 values per the four spans
+// (tools/div_check.c).
+__device__ __forceinline__ double div_time(double a, double b, double y) {
+#if defined(GM_XZ_DIV_IEEE) || defined(GM_XZ3_ZDIV_IEEE)
+  (void)y;
+  return __ddiv_rn(a, b);
+#else
+  if (a > 0.0 && a < 0x1p-900) return __ddiv_rn(a, b);
+  return div_span(a, b, y);
 #endif
 }
 
@@ -175,8 +191,8 @@ __device__ __forceinline__ uint8_t xz2_one(int g, double xmin, double ymin, doub
   return st;
 }
 
-// XZ3SFC.index (z3/curve/XZ3SFC.scala:53-76) with normalize (:338-380), sequenceCode (:275-304).  The
-// time span zhi is a run-time value and z may be any double in [0, zhi], so z keeps the IEEE divide.
+// XZ3SFC.index (z3/curve/XZ3SFC.scala:53-76) with normalize (:338-380), sequenceCode (:275-304).  zhi is
+// BinnedTime.maxOffset(period) (every caller), so z divides as div_time.
 template <bool LENIENT>
 __device__ __forceinline__ uint8_t xz3_one(int g, double zhi, double xmin, double ymin, double zmin, double xmax,
                                            double ymax, double zmax, int64_t& out) {
@@ -189,10 +205,11 @@ __device__ __forceinline__ uint8_t xz3_one(int g, double zhi, double xmin, doubl
   const double zsize = __dsub_rn(zhi, 0.0);
   const double nxmin = div_span(__dsub_rn(xmin, -180.0), 360.0, RX);
   const double nymin = div_span(__dsub_rn(ymin, -90.0), 180.0, RY);
-  const double nzmin = __ddiv_rn(__dsub_rn(zmin, 0.0), zsize);
+  const double RZ = __ddiv_rn(1.0, zsize);   // uniform: hoisted out of the caller's loop
+  const double nzmin = div_time(__dsub_rn(zmin, 0.0), zsize, RZ);
   const double nxmax = div_span(__dsub_rn(xmax, -180.0), 360.0, RX);
   const double nymax = div_span(__dsub_rn(ymax, -90.0), 180.0, RY);
-  const double nzmax = __ddiv_rn(__dsub_rn(zmax, 0.0), zsize);
+  const double nzmax = div_time(__dsub_rn(zmax, 0.0), zsize, RZ);
   const double maxdim = jmax(jmax(__dsub_rn(nxmax, nxmin), __dsub_rn(nymax, nymin)), __dsub_rn(nzmax, nzmin));
   const int32_t l1 = xz_l1(maxdim);
   const int32_t lc = l1 < g ? l1 : g;
