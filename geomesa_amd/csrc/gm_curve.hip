@@ -378,13 +378,8 @@ __global__ __launch_bounds__(TPB) void k_xz2_index_v(const dv2* __restrict__ xmi
   }
 }
 
-#ifdef GM_XZ3_WPE   // tuning variant: waves per SIMD
-#define GM_XZ3_ATTR __attribute__((amdgpu_waves_per_eu(GM_XZ3_WPE)))
-#else
-#define GM_XZ3_ATTR
-#endif
 template <bool LENIENT, bool STATUS, int UNROLL>
-__global__ __launch_bounds__(TPB) GM_XZ3_ATTR void k_xz3_index_v(const dv2* __restrict__ xmin, const dv2* __restrict__ ymin,
+__global__ __launch_bounds__(TPB) void k_xz3_index_v(const dv2* __restrict__ xmin, const dv2* __restrict__ ymin,
                                                      const dv2* __restrict__ zmin, const dv2* __restrict__ xmax,
                                                      const dv2* __restrict__ ymax, const dv2* __restrict__ zmax,
                                                      int64_t n, int g, double zhi, lv2* __restrict__ out,
