@@ -191,6 +191,57 @@ def test_xz3_index_parity(gpu, oracle, lenient):
     assert np.array_equal(as_np(s1), os_[1:]) and np.array_equal(as_np(out1), oo[1:])
 
 
+def _ulp_walk(v, k):
+    """v moved k ulps (k < 0: down)."""
+    out = np.asarray(v, np.float64).copy()
+    for _ in range(abs(k)):
+        out = np.nextafter(out, np.inf if k > 0 else -np.inf)
+    return out
+
+
+def _division_edges(lo, span, rng, n_mult=4096):
+    """values v in [lo, lo + span] whose normalized (v - lo) / span sits on or next to a dyadic boundary
+    j / 2^20 (the cells floor((v - lo) / span * 2^L) turns on), plus the span's ends"""
+    j = rng.integers(0, 2**20 + 1, n_mult)
+    base = lo + np.ldexp(j.astype(np.float64), -20) * span
+    vals = [base] + [_ulp_walk(base, k) for k in (-3, -2, -1, 1, 2, 3)] + [np.array([lo, lo + span])]
+    return np.clip(np.concatenate(vals), lo, lo + span)
+
+
+@pytest.mark.parametrize("g", [12, 20])
+def test_xz_division_edges(gpu, oracle, g):
+    """The XZ keys divide by the lon / lat / time spans with a corrected reciprocal (gm_keys.hpp div_span,
+    div_time): degenerate and tiny envelopes whose normalized corners sit on, or 1-3 ulps beside, the
+    dyadic cell boundaries, z = 0, subnormal, around 2^-900 (the IEEE fallback's edge) and integer
+    offsets, for every period's span -- bit-equal keys with the oracle's IEEE division"""
+    from geomesa_amd.curve import XZ2SFC, XZ3SFC
+    rng = np.random.default_rng(17)
+    xs = _division_edges(-180.0, 360.0, rng); ys = _division_edges(-90.0, 180.0, rng)
+    n = max(len(xs), len(ys))
+    xs = np.resize(xs, n); ys = np.resize(rng.permutation(ys), n)
+    w = np.where(rng.random(n) < 0.5, 0.0, np.ldexp(1.0, -rng.integers(8, 40, n)))
+    env2 = [xs, ys, np.minimum(xs + w, 180.0), np.minimum(ys + w, 90.0)]
+    out, st = XZ2SFC(g).index(*env2, status=True)
+    oo, ost = oracle.xz2_index_batch(np.stack(env2, 1), g=g)
+    assert np.array_equal(as_np(st), ost) and np.array_equal(as_np(out), oo)
+    if g > 20:
+        return
+    for name, period in (("day", oracle.DAY), ("week", oracle.WEEK), ("month", oracle.MONTH), ("year", oracle.YEAR)):
+        span = float(XZ3SFC(g, name).zBounds[1])
+        special = np.array([0.0, 5e-324, 1e-310, 2.2250738585072014e-308, np.ldexp(1.0, -1000),
+                            np.ldexp(1.0, -900), np.nextafter(np.ldexp(1.0, -900), 0.0),
+                            np.nextafter(np.ldexp(1.0, -900), 1.0), 1.0, span - 1.0, span])
+        ints = rng.integers(0, int(span) + 1, 4096).astype(np.float64)
+        zs = np.resize(np.concatenate([_division_edges(0.0, span, rng), special, ints]), n)
+        zs = rng.permutation(zs)
+        dz = np.where(rng.random(n) < 0.5, 0.0, np.ldexp(span, -rng.integers(8, 40, n)))
+        env3 = [xs, ys, zs, env2[2], env2[3], np.minimum(zs + dz, span)]
+        out, st = XZ3SFC(g, name).index(*env3, status=True)
+        oo, ost = oracle.xz3_index_batch(np.stack(env3, 1), g=g, period=period)
+        assert np.array_equal(as_np(st), ost), name
+        assert np.array_equal(as_np(out), oo), name
+
+
 def test_z3_roundtrip_property_large(gpu):
     """Size-independent property at 2^26 points: invert(z) returns the centre of z's lon/lat cell, so
     re-encoding it reproduces z's lon/lat bits (encode -> invert -> encode idempotence; the time
