@@ -256,9 +256,6 @@ constexpr uint64_t GR_VAL = (1ull << 48) - 1;
 #define GM_SORT_LB 4
 #endif
 constexpr int LB = GM_SORT_LB;   // look-back granules per round trip
-#ifndef GM_SORT_SPEC
-#define GM_SORT_SPEC 1
-#endif
 
 struct PassArgs {
   KeyCols in;             // the caller's columns (first pass) ...
@@ -293,65 +290,53 @@ __global__ __launch_bounds__(PT) void k_sort_pass(PassArgs a) {
   const uint32_t cg_early = t < nb ? a.counts[t] : 0u;
   if (t == 0) s_tile = atomicAdd(a.ctr, 1u);
   for (int i = t; i < PW * NB_MAX / 2; i += PT) ((uint32_t*)&s_wcnt[0][0])[i] = 0u;
-  const int64_t n = a.n;
-  // this lane's rows of tile tl
+  __syncthreads();
+  const int64_t tile = s_tile, t0 = tile * PTILE, n = a.n;
+  // this lane's rows
   uint4 rv[PSLOT][2];
-  auto load = [&](int64_t tl) {
-    const int64_t t0 = tl * PTILE;
-    const bool full = t0 + PTILE <= n;   // every tile but the last (uniform)
-    const bool vec = a.vec && full;
-    if (IN_REC && full) {
-      // a full tile's loads are unconditional, so the compiler counts them: all 2 * PSLOT are in flight
-      // before the first wait.  (Under the per-row `i < n` selects each load sat in its own branch and
-      // was waited for before the next one was issued: one load in flight per lane.)
+  const bool full = t0 + PTILE <= n;   // every tile but the last (uniform)
+  const bool vec = a.vec && full;
+  if (IN_REC && full) {
+    // a full tile's loads are unconditional, so the compiler counts them: all 2 * PSLOT are in flight
+    // before the first wait.  (Under the per-row `i < n` selects each load sat in its own branch and
+    // was waited for before the next one was issued: one load in flight per lane.)
 #pragma unroll
-      for (int k = 0; k < PSLOT; ++k) {
-        const int64_t i = t0 + wave * (2 * 64 * PSLOT) + k * 128 + 2 * lane;
-        rv[k][0] = a.rec_in[i];
-        rv[k][1] = a.rec_in[i + 1];
+    for (int k = 0; k < PSLOT; ++k) {
+      const int64_t i = t0 + wave * (2 * 64 * PSLOT) + k * 128 + 2 * lane;
+      rv[k][0] = a.rec_in[i];
+      rv[k][1] = a.rec_in[i + 1];
+    }
+  } else if (!IN_REC && vec) {   // the same for the first pass's column loads
+#pragma unroll
+    for (int k = 0; k < PSLOT; ++k) {
+      const int64_t i = t0 + wave * (2 * 64 * PSLOT) + k * 128 + 2 * lane;
+      const ulonglong2 zz = *(const ulonglong2*)(a.in.z + i);
+      uint32_t bb = *(const uint32_t*)(a.in.bin + i);
+      uint32_t b0 = bb & 0xffffu, b1 = bb >> 16;
+      if (SH) {
+        const uint32_t ss = *(const uint16_t*)(a.in.sh + i);
+        b0 = squeeze_bs(b0 | (ss & 0xffu) << 16, a.sq); b1 = squeeze_bs(b1 | (ss >> 8) << 16, a.sq);
       }
-    } else if (!IN_REC && vec) {   // the same for the first pass's column loads
+      rv[k][0] = make_rec(zz.x, (uint32_t)i, b0);
+      rv[k][1] = make_rec(zz.y, (uint32_t)(i + 1), b1);
+    }
+  } else {
 #pragma unroll
-      for (int k = 0; k < PSLOT; ++k) {
-        const int64_t i = t0 + wave * (2 * 64 * PSLOT) + k * 128 + 2 * lane;
-        const ulonglong2 zz = *(const ulonglong2*)(a.in.z + i);
-        uint32_t bb = *(const uint32_t*)(a.in.bin + i);
-        uint32_t b0 = bb & 0xffffu, b1 = bb >> 16;
-        if (SH) {
-          const uint32_t ss = *(const uint16_t*)(a.in.sh + i);
-          b0 = squeeze_bs(b0 | (ss & 0xffu) << 16, a.sq); b1 = squeeze_bs(b1 | (ss >> 8) << 16, a.sq);
-        }
-        rv[k][0] = make_rec(zz.x, (uint32_t)i, b0);
-        rv[k][1] = make_rec(zz.y, (uint32_t)(i + 1), b1);
-      }
-    } else {
-#pragma unroll
-      for (int k = 0; k < PSLOT; ++k) {
-        const int64_t i = t0 + wave * (2 * 64 * PSLOT) + k * 128 + 2 * lane;
-        if (IN_REC) {
-          rv[k][0] = i < n ? a.rec_in[i] : make_uint4(0u, 0u, 0u, 0u);
-          rv[k][1] = i + 1 < n ? a.rec_in[i + 1] : make_uint4(0u, 0u, 0u, 0u);
-        } else {
-          uint64_t z0, z1;
-          uint32_t b0, b1;
-          load_pair<SH>(a.in, i, n, vec, z0, z1, b0, b1);
-          if (SH) { b0 = squeeze_bs(b0, a.sq); b1 = squeeze_bs(b1, a.sq); }
-          rv[k][0] = make_rec(z0, (uint32_t)i, b0);
-          rv[k][1] = make_rec(z1, (uint32_t)(i + 1), b1);
-        }
+    for (int k = 0; k < PSLOT; ++k) {
+      const int64_t i = t0 + wave * (2 * 64 * PSLOT) + k * 128 + 2 * lane;
+      if (IN_REC) {
+        rv[k][0] = i < n ? a.rec_in[i] : make_uint4(0u, 0u, 0u, 0u);
+        rv[k][1] = i + 1 < n ? a.rec_in[i + 1] : make_uint4(0u, 0u, 0u, 0u);
+      } else {
+        uint64_t z0, z1;
+        uint32_t b0, b1;
+        load_pair<SH>(a.in, i, n, vec, z0, z1, b0, b1);
+        if (SH) { b0 = squeeze_bs(b0, a.sq); b1 = squeeze_bs(b1, a.sq); }
+        rv[k][0] = make_rec(z0, (uint32_t)i, b0);
+        rv[k][1] = make_rec(z1, (uint32_t)(i + 1), b1);
       }
     }
-  };
-  // The tile counter's atomic is an L2 round trip before any load could be issued; blocks start in
-  // index order, so the counter almost always hands block b tile b: its loads are issued on that guess
-  // while the atomic is in flight, and redone only when the counter says otherwise (the counter, not
-  // the guess, keeps the look-back deadlock-free)
-  const int64_t guess = blockIdx.x;
-  const bool spec = GM_SORT_SPEC && (guess + 1) * PTILE <= n;
-  if (spec) load(guess);
-  __syncthreads();
-  const int64_t tile = s_tile, t0 = tile * PTILE;
-  if (!spec || tile != guess) load(tile);
+  }
   const uint64_t lt = lanemask_lt();
   uint32_t rd[PSLOT][2];   // wave rank | digit << 16; rank 0xffff = no row
 #pragma unroll
