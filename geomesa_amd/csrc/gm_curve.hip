@@ -435,6 +435,10 @@ __global__ __launch_bounds__(TPB) void k_xz3_index_v(const dv2* __restrict__ xmi
 #endif
 constexpr int UNROLL_KEY = GM_UNROLL_KEY;
 constexpr int UNROLL_INV = GM_UNROLL_INV;
+#ifndef GM_UNROLL_INV2
+#define GM_UNROLL_INV2 1   // the Z2 inverse: 1 pair per lane 3.68-3.83 vs 2 pairs 4.12-4.23 ms (profiles/r6/invert_unroll_ab.txt)
+#endif
+constexpr int UNROLL_INV2 = GM_UNROLL_INV2;
 constexpr int UNROLL_XZ = GM_UNROLL_XZ;
 #ifndef GM_UNROLL_Z2
 #define GM_UNROLL_Z2 2   // 2 / 4 / 8: 3.91 / 3.94-3.98 / 4.09-4.11 ms per 1B points (profiles/r2_curve_unroll_sweep.txt)
@@ -578,8 +582,8 @@ int gm_z2_invert(gm_ctx* ctx, const int64_t* z, int64_t n, int precision, double
   if (!z || !x || !y) return GM_E_INVALID;
   const NDim lon = lon_dim(precision), lat = lat_dim(precision);
   if (aligned16(z) && aligned16(x) && aligned16(y)) {
-    unsigned grid = grid_for((n >> 1) > 0 ? (n >> 1) : 1, (int64_t)TPB * UNROLL_INV);
-    hipLaunchKernelGGL((k_z2_invert<UNROLL_INV>), dim3(grid), dim3(TPB), 0, ctx->stream, (const lv2*)z, n,
+    unsigned grid = grid_for((n >> 1) > 0 ? (n >> 1) : 1, (int64_t)TPB * UNROLL_INV2);
+    hipLaunchKernelGGL((k_z2_invert<UNROLL_INV2>), dim3(grid), dim3(TPB), 0, ctx->stream, (const lv2*)z, n,
                        (dv2*)x, (dv2*)y, lon, lat);
   } else {
     hipLaunchKernelGGL(k_z2_invert_s, dim3(stride_grid(n)), dim3(TPB), 0, ctx->stream, z, n, x, y, lon, lat);
