@@ -10,7 +10,14 @@
 
 namespace gm {
 
-constexpr int TPB = 256;
+#ifndef GM_CURVE_TPB
+#define GM_CURVE_TPB 256
+#endif
+constexpr int TPB = GM_CURVE_TPB;
+#ifndef GM_XZ_TPB
+#define GM_XZ_TPB 128   // 64 / 128 / 256 / 512: profiles/r6/curve_block_unroll_ab.txt (128 and 64 ahead of 256 for both XZ kernels)
+#endif
+constexpr int XTPB = GM_XZ_TPB;   // the XZ kernels' block
 
 
 // ------------------------------------------------------------------ Z3 key (epoch ms -> bin, z)
@@ -339,16 +346,16 @@ __global__ __launch_bounds__(TPB) void k_xz3_index_key(const double* __restrict_
 // 16-B form: 2 envelopes per lane per column (one dwordx4 each), UNROLL pairs in flight per lane,
 // the same coalesced layout as the Z3 key kernel; the odd last envelope goes to lane 0 of block 0.
 template <bool LENIENT, bool STATUS, int UNROLL>
-__global__ __launch_bounds__(TPB) void k_xz2_index_v(const dv2* __restrict__ xmin, const dv2* __restrict__ ymin,
+__global__ __launch_bounds__(XTPB) void k_xz2_index_v(const dv2* __restrict__ xmin, const dv2* __restrict__ ymin,
                                                      const dv2* __restrict__ xmax, const dv2* __restrict__ ymax,
                                                      int64_t n, int g, lv2* __restrict__ out,
                                                      uchar2* __restrict__ status, int64_t* __restrict__ err) {
   const int64_t npairs = n >> 1;
-  const int64_t base = (int64_t)blockIdx.x * (TPB * UNROLL) + threadIdx.x;
+  const int64_t base = (int64_t)blockIdx.x * (XTPB * UNROLL) + threadIdx.x;
   dv2 a[UNROLL], b[UNROLL], c[UNROLL], d[UNROLL];
 #pragma unroll
   for (int u = 0; u < UNROLL; ++u) {
-    const int64_t p = base + (int64_t)u * TPB;
+    const int64_t p = base + (int64_t)u * XTPB;
     if (p < npairs) {
       a[u] = ld_stream(&xmin[p]); b[u] = ld_stream(&ymin[p]);
       c[u] = ld_stream(&xmax[p]); d[u] = ld_stream(&ymax[p]);
@@ -356,7 +363,7 @@ __global__ __launch_bounds__(TPB) void k_xz2_index_v(const dv2* __restrict__ xmi
   }
 #pragma unroll
   for (int u = 0; u < UNROLL; ++u) {
-    const int64_t p = base + (int64_t)u * TPB;
+    const int64_t p = base + (int64_t)u * XTPB;
     if (p < npairs) {
       int64_t o0, o1;
       const uint8_t s0 = xz2_one<LENIENT>(g, a[u].x, b[u].x, c[u].x, d[u].x, o0);
@@ -379,17 +386,17 @@ __global__ __launch_bounds__(TPB) void k_xz2_index_v(const dv2* __restrict__ xmi
 }
 
 template <bool LENIENT, bool STATUS, int UNROLL>
-__global__ __launch_bounds__(TPB) void k_xz3_index_v(const dv2* __restrict__ xmin, const dv2* __restrict__ ymin,
+__global__ __launch_bounds__(XTPB) void k_xz3_index_v(const dv2* __restrict__ xmin, const dv2* __restrict__ ymin,
                                                      const dv2* __restrict__ zmin, const dv2* __restrict__ xmax,
                                                      const dv2* __restrict__ ymax, const dv2* __restrict__ zmax,
                                                      int64_t n, int g, double zhi, lv2* __restrict__ out,
                                                      uchar2* __restrict__ status, int64_t* __restrict__ err) {
   const int64_t npairs = n >> 1;
-  const int64_t base = (int64_t)blockIdx.x * (TPB * UNROLL) + threadIdx.x;
+  const int64_t base = (int64_t)blockIdx.x * (XTPB * UNROLL) + threadIdx.x;
   dv2 a[UNROLL], b[UNROLL], c[UNROLL], d[UNROLL], e[UNROLL], f[UNROLL];
 #pragma unroll
   for (int u = 0; u < UNROLL; ++u) {
-    const int64_t p = base + (int64_t)u * TPB;
+    const int64_t p = base + (int64_t)u * XTPB;
     if (p < npairs) {
       a[u] = ld_stream(&xmin[p]); b[u] = ld_stream(&ymin[p]); c[u] = ld_stream(&zmin[p]);
       d[u] = ld_stream(&xmax[p]); e[u] = ld_stream(&ymax[p]); f[u] = ld_stream(&zmax[p]);
@@ -397,7 +404,7 @@ __global__ __launch_bounds__(TPB) void k_xz3_index_v(const dv2* __restrict__ xmi
   }
 #pragma unroll
   for (int u = 0; u < UNROLL; ++u) {
-    const int64_t p = base + (int64_t)u * TPB;
+    const int64_t p = base + (int64_t)u * XTPB;
     if (p < npairs) {
       int64_t o0, o1;
       const uint8_t s0 = xz3_one<LENIENT>(g, zhi, a[u].x, b[u].x, c[u].x, d[u].x, e[u].x, f[u].x, o0);
@@ -441,7 +448,7 @@ constexpr int UNROLL_INV = GM_UNROLL_INV;
 constexpr int UNROLL_INV2 = GM_UNROLL_INV2;
 constexpr int UNROLL_XZ = GM_UNROLL_XZ;
 #ifndef GM_UNROLL_Z2
-#define GM_UNROLL_Z2 2   // 2 / 4 / 8: 3.91 / 3.94-3.98 / 4.09-4.11 ms per 1B points (profiles/r2_curve_unroll_sweep.txt)
+#define GM_UNROLL_Z2 1   // round 6: 1 pair per lane 3.635-3.640 vs 2 pairs 3.84-4.01 ms per 1B points (profiles/r6/curve_block_unroll_ab.txt); round 2: 2 / 4 / 8 3.91 / 3.94-3.98 / 4.09-4.11
 #endif
 constexpr int UNROLL_Z2 = GM_UNROLL_Z2;
 
@@ -626,16 +633,16 @@ int gm_xz2_index(gm_ctx* ctx, const double* xmin, const double* ymin, const doub
   hipStream_t s = ctx->stream;
   if (aligned16(xmin) && aligned16(ymin) && aligned16(xmax) && aligned16(ymax) && aligned16(out) &&
       (((uintptr_t)status & 1u) == 0)) {
-    const unsigned vg = grid_for((n >> 1) > 0 ? (n >> 1) : 1, (int64_t)TPB * UNROLL_XZ);
+    const unsigned vg = grid_for((n >> 1) > 0 ? (n >> 1) : 1, (int64_t)XTPB * UNROLL_XZ);
     const dv2 *a = (const dv2*)xmin, *b = (const dv2*)ymin, *c = (const dv2*)xmax, *d = (const dv2*)ymax;
     lv2* o = (lv2*)out;
     uchar2* st = (uchar2*)status;
     if (lenient) {
-      if (status) hipLaunchKernelGGL((k_xz2_index_v<true, true, UNROLL_XZ>), dim3(vg), dim3(TPB), 0, s, a, b, c, d, n, g, o, st, ctx->d_err);
-      else hipLaunchKernelGGL((k_xz2_index_v<true, false, UNROLL_XZ>), dim3(vg), dim3(TPB), 0, s, a, b, c, d, n, g, o, st, ctx->d_err);
+      if (status) hipLaunchKernelGGL((k_xz2_index_v<true, true, UNROLL_XZ>), dim3(vg), dim3(XTPB), 0, s, a, b, c, d, n, g, o, st, ctx->d_err);
+      else hipLaunchKernelGGL((k_xz2_index_v<true, false, UNROLL_XZ>), dim3(vg), dim3(XTPB), 0, s, a, b, c, d, n, g, o, st, ctx->d_err);
     } else {
-      if (status) hipLaunchKernelGGL((k_xz2_index_v<false, true, UNROLL_XZ>), dim3(vg), dim3(TPB), 0, s, a, b, c, d, n, g, o, st, ctx->d_err);
-      else hipLaunchKernelGGL((k_xz2_index_v<false, false, UNROLL_XZ>), dim3(vg), dim3(TPB), 0, s, a, b, c, d, n, g, o, st, ctx->d_err);
+      if (status) hipLaunchKernelGGL((k_xz2_index_v<false, true, UNROLL_XZ>), dim3(vg), dim3(XTPB), 0, s, a, b, c, d, n, g, o, st, ctx->d_err);
+      else hipLaunchKernelGGL((k_xz2_index_v<false, false, UNROLL_XZ>), dim3(vg), dim3(XTPB), 0, s, a, b, c, d, n, g, o, st, ctx->d_err);
     }
   } else if (lenient) {
     if (status) hipLaunchKernelGGL((k_xz2_index<true, true>), dim3(grid), dim3(TPB), 0, s, xmin, ymin, xmax, ymax, n, g, out, status, ctx->d_err);
@@ -661,17 +668,17 @@ int gm_xz3_index(gm_ctx* ctx, const double* xmin, const double* ymin, const doub
   hipStream_t s = ctx->stream;
   if (aligned16(xmin) && aligned16(ymin) && aligned16(zmin) && aligned16(xmax) && aligned16(ymax) &&
       aligned16(zmax) && aligned16(out) && (((uintptr_t)status & 1u) == 0)) {
-    const unsigned vg = grid_for((n >> 1) > 0 ? (n >> 1) : 1, (int64_t)TPB * UNROLL_XZ);
+    const unsigned vg = grid_for((n >> 1) > 0 ? (n >> 1) : 1, (int64_t)XTPB * UNROLL_XZ);
     const dv2 *a = (const dv2*)xmin, *b = (const dv2*)ymin, *c = (const dv2*)zmin;
     const dv2 *d = (const dv2*)xmax, *e = (const dv2*)ymax, *f = (const dv2*)zmax;
     lv2* o = (lv2*)out;
     uchar2* st = (uchar2*)status;
     if (lenient) {
-      if (status) hipLaunchKernelGGL((k_xz3_index_v<true, true, UNROLL_XZ>), dim3(vg), dim3(TPB), 0, s, a, b, c, d, e, f, n, g, zhi, o, st, ctx->d_err);
-      else hipLaunchKernelGGL((k_xz3_index_v<true, false, UNROLL_XZ>), dim3(vg), dim3(TPB), 0, s, a, b, c, d, e, f, n, g, zhi, o, st, ctx->d_err);
+      if (status) hipLaunchKernelGGL((k_xz3_index_v<true, true, UNROLL_XZ>), dim3(vg), dim3(XTPB), 0, s, a, b, c, d, e, f, n, g, zhi, o, st, ctx->d_err);
+      else hipLaunchKernelGGL((k_xz3_index_v<true, false, UNROLL_XZ>), dim3(vg), dim3(XTPB), 0, s, a, b, c, d, e, f, n, g, zhi, o, st, ctx->d_err);
     } else {
-      if (status) hipLaunchKernelGGL((k_xz3_index_v<false, true, UNROLL_XZ>), dim3(vg), dim3(TPB), 0, s, a, b, c, d, e, f, n, g, zhi, o, st, ctx->d_err);
-      else hipLaunchKernelGGL((k_xz3_index_v<false, false, UNROLL_XZ>), dim3(vg), dim3(TPB), 0, s, a, b, c, d, e, f, n, g, zhi, o, st, ctx->d_err);
+      if (status) hipLaunchKernelGGL((k_xz3_index_v<false, true, UNROLL_XZ>), dim3(vg), dim3(XTPB), 0, s, a, b, c, d, e, f, n, g, zhi, o, st, ctx->d_err);
+      else hipLaunchKernelGGL((k_xz3_index_v<false, false, UNROLL_XZ>), dim3(vg), dim3(XTPB), 0, s, a, b, c, d, e, f, n, g, zhi, o, st, ctx->d_err);
     }
   } else if (lenient) {
     if (status) hipLaunchKernelGGL((k_xz3_index<true, true>), dim3(grid), dim3(TPB), 0, s, xmin, ymin, zmin, xmax, ymax, zmax, n, g, zhi, out, status, ctx->d_err);
