@@ -1138,7 +1138,11 @@ def main():
         extra["config0"] = bench_config0(a, dist, ctx, x, y, t)
     # ---------------------------------------------------------------- sorted table: ingest sort + seek-and-filter
     if "table" in only and not a.no_extra:
-        extra.update(bench_table(a, dist, ctx, b, z))
+        try:   # a failure here (every rank alike, e.g. a collective the backend refuses) keeps the line
+            extra.update(bench_table(a, dist, ctx, b, z))
+        except Exception as e:  # noqa: BLE001 -- reported in the JSON line
+            extra["table_error"] = repr(e)[:300]
+            torch.cuda.synchronize()
     del x, y, t, b, z
     torch.cuda.empty_cache()
 
