@@ -110,12 +110,10 @@ __global__ __launch_bounds__(TPB) void k_z3_index(const double* __restrict__ x, 
 
 // ------------------------------------------------------------------ Z3SFC.invert
 
-// the inverse's store shape: 1 = plain 16-B stores as each pair is computed (5.45-5.48 ms per 1B points
-// against 5.51-5.63 for non-temporal ones, 0, and 5.42-5.58 for 2 = all of a lane's outputs computed
-// before its stores; same box, profiles/r6/invert_store_ab.txt)
-#ifndef GM_INV_STORE
-#define GM_INV_STORE 1
-#endif
+// plain 16-B stores as each pair is computed: 5.45-5.48 ms per 1B points against 5.51-5.63 for
+// non-temporal ones and 5.42-5.58 with all of a lane's outputs computed before its stores, on one box
+// (profiles/r6/invert_store_ab.txt); a second box ranked the store kinds the other way round within its
+// noise (profiles/r6/store_kind_ab_box2.txt)
 template <int UNROLL>
 __global__ __launch_bounds__(TPB) void k_z3_invert(const lv2* __restrict__ z, int64_t n, dv2* __restrict__ x,
                                                    dv2* __restrict__ y, lv2* __restrict__ t, NDim lon,
@@ -128,22 +126,6 @@ __global__ __launch_bounds__(TPB) void k_z3_invert(const lv2* __restrict__ z, in
     const int64_t p = base + (int64_t)u * TPB;
     if (p < npairs) zv[u] = ld_stream(&z[p]);
   }
-#if GM_INV_STORE == 2   // tuning variant: every pair's three outputs computed first, then all the stores
-  dv2 xo[UNROLL], yo[UNROLL];
-  lv2 to[UNROLL];
-#pragma unroll
-  for (int u = 0; u < UNROLL; ++u) {
-    const int64_t a = zv[u].x, b = zv[u].y;
-    xo[u] = dv2{denormalize(lon, z3_combine(a)), denormalize(lon, z3_combine(b))};
-    yo[u] = dv2{denormalize(lat, z3_combine(a >> 1)), denormalize(lat, z3_combine(b >> 1))};
-    to[u] = lv2{jvm_d2l(denormalize(tim, z3_combine(a >> 2))), jvm_d2l(denormalize(tim, z3_combine(b >> 2)))};
-  }
-#pragma unroll
-  for (int u = 0; u < UNROLL; ++u) {
-    const int64_t p = base + (int64_t)u * TPB;
-    if (p < npairs) { st_stream(xo[u], &x[p]); st_stream(yo[u], &y[p]); st_stream(to[u], &t[p]); }
-  }
-#else
 #pragma unroll
   for (int u = 0; u < UNROLL; ++u) {
     const int64_t p = base + (int64_t)u * TPB;
@@ -152,14 +134,9 @@ __global__ __launch_bounds__(TPB) void k_z3_invert(const lv2* __restrict__ z, in
       const dv2 xo{denormalize(lon, z3_combine(a)), denormalize(lon, z3_combine(b))};
       const dv2 yo{denormalize(lat, z3_combine(a >> 1)), denormalize(lat, z3_combine(b >> 1))};
       const lv2 to{jvm_d2l(denormalize(tim, z3_combine(a >> 2))), jvm_d2l(denormalize(tim, z3_combine(b >> 2)))};
-#if GM_INV_STORE == 1   // tuning variant: plain (temporal) stores
       x[p] = xo; y[p] = yo; t[p] = to;
-#else
-      st_stream(xo, &x[p]); st_stream(yo, &y[p]); st_stream(to, &t[p]);
-#endif
     }
   }
-#endif
   if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
     const int64_t i = n - 1;
     const int64_t a = ((const int64_t*)z)[i];

@@ -27,20 +27,11 @@ enum : int { DAY = 0, WEEK = 1, MONTH = 2, YEAR = 3 };
 // JVM d2i: NaN -> 0, saturating.  Branch-free (clamp, convert, select): the three early returns compiled
 // to nested exec-mask branches, ~12 scalar instructions per conversion around ~4 vector ones, which the
 // VALU-heavy kernels (Z3Histogram: three normalizations per point) paid on every point.
-#ifndef GM_D2I_BRANCHES
 __device__ __forceinline__ int32_t jvm_d2i(double d) {
   const double c = __builtin_fmin(__builtin_fmax(d, -2147483648.0), 2147483647.0);   // NaN -> -2^31 here ...
   const int32_t r = (int32_t)c;                                                      // (in range: defined)
   return d == d ? r : 0;                                                             // ... and 0 here
 }
-#else   // tuning build: round 5's form
-__device__ __forceinline__ int32_t jvm_d2i(double d) {
-  if (!(d == d)) return 0;
-  if (d >= 2147483647.0) return INT32_MAX;
-  if (d <= -2147483648.0) return INT32_MIN;
-  return (int32_t)d;
-}
-#endif
 __device__ __forceinline__ int64_t jvm_d2l(double d) {
   if (!(d == d)) return 0;
   if (d >= 9223372036854775808.0) return INT64_MAX;
@@ -130,14 +121,9 @@ __host__ __device__ constexpr NDim make_ndim(double mn, double mx, int precision
               (int32_t)((1LL << precision) - 1)};
 }
 __device__ __forceinline__ int32_t normalize(const NDim& d, double x) {
-#ifndef GM_D2I_BRANCHES   // a select, not a branch (see jvm_d2i)
+  // a select, not a branch (see jvm_d2i)
   const int32_t r = jvm_d2i(floor(__dmul_rn(__dsub_rn(x, d.min), d.normalizer)));
   return x >= d.max ? d.max_index : r;
-#else
-  if (x >= d.max) return d.max_index;
-  double v = __dmul_rn(__dsub_rn(x, d.min), d.normalizer);
-  return jvm_d2i(floor(v));
-#endif
 }
 __device__ __forceinline__ double denormalize(const NDim& d, int32_t i) {
   double a = (i >= d.max_index) ? (double)d.max_index : (double)i;

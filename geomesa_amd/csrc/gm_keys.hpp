@@ -133,13 +133,8 @@ __device__ __forceinline__ bool xz_fits(double mn, double mx, double w2, double 
 // random, every exponent down to 2^-45, +-3 ulp around every j b / 2^20) and bit-compared with the
 // oracle by the GPU parity tests.
 __device__ __forceinline__ double div_span(double a, double b, double y) {
-#ifdef GM_XZ_DIV_IEEE
-  (void)y;
-  return __ddiv_rn(a, b);
-#else
   const double q = __dmul_rn(a, y);
   return __fma_rn(__fma_rn(-q, b, a), y, q);
-#endif
 }
 
 // RN(a / b) for the time span b = BinnedTime.maxOffset(period) (86400000, 604800, 2678400 or 527050: the
@@ -148,13 +143,8 @@ __device__ __forceinline__ double div_span(double a, double b, double y) {
 // bits to underflow) takes the IEEE divide.  Checked against a / b on 1.67e9 values per the four spans
 // (tools/div_check.c).
 __device__ __forceinline__ double div_time(double a, double b, double y) {
-#if defined(GM_XZ_DIV_IEEE) || defined(GM_XZ3_ZDIV_IEEE)
-  (void)y;
-  return __ddiv_rn(a, b);
-#else
   if (a > 0.0 && a < 0x1p-900) return __ddiv_rn(a, b);
   return div_span(a, b, y);
-#endif
 }
 
 // the level count: l1 >= g -> g, else l1 + 1 when the envelope fits the next level's 2x2 cells

@@ -139,19 +139,10 @@ struct RingHdr {
 
 // the cell of v on a g-cell axis, clamped (NaN -> 0).  Branch-free: a clamp by maxNum / minNum (NaN -> 0)
 // instead of two early returns, which compiled to exec-mask branches in every stream step
-#ifndef GM_CELL_BRANCHES
 __device__ __forceinline__ int cell_of(double v, double v0, double inv, int g) {
   const double c = floor(__dmul_rn(__dsub_rn(v, v0), inv));
   return (int)__builtin_fmin(__builtin_fmax(c, 0.0), (double)(g - 1));
 }
-#else   // tuning build: round 5's form
-__device__ __forceinline__ int cell_of(double v, double v0, double inv, int g) {
-  const double c = floor(__dmul_rn(__dsub_rn(v, v0), inv));
-  if (!(c >= 0.0)) return 0;
-  if (c >= (double)g) return g - 1;
-  return (int)c;
-}
-#endif
 
 // RayCrossingCounter.countSegment (JTS 1.20); returns true when the point is on the segment
 __device__ __forceinline__ bool count_segment(double p1x, double p1y, double p2x, double p2y, double px, double py,
