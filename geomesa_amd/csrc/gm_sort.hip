@@ -256,6 +256,12 @@ constexpr uint64_t GR_VAL = (1ull << 48) - 1;
 #define GM_SORT_LB 4
 #endif
 constexpr int LB = GM_SORT_LB;   // look-back granules per round trip
+#ifndef GM_SORT_SPLIT
+#define GM_SORT_SPLIT 1
+#endif
+#ifndef GM_SORT_LDSMATCH
+#define GM_SORT_LDSMATCH 1
+#endif
 
 struct PassArgs {
   KeyCols in;             // the caller's columns (first pass) ...
@@ -292,6 +298,88 @@ __global__ __launch_bounds__(PT) void k_sort_pass(PassArgs a) {
   for (int i = t; i < PW * NB_MAX / 2; i += PT) ((uint32_t*)&s_wcnt[0][0])[i] = 0u;
   __syncthreads();
   const int64_t tile = s_tile, t0 = tile * PTILE, n = a.n;
+#if GM_SORT_SPLIT
+  // this lane's rows: slot k of wave w holds rows r = t0 + 512 w + 128 k + lane (A) and r + 64 (B), so
+  // in input order a slot is its 64 A rows, then its 64 B rows, and each half ranks like one row per
+  // lane: 9 ballots and one mask per row.  (Round 5's pairs (2 lane, 2 lane + 1) interleave the halves
+  // and needed four cross masks per pair: ~80 instead of ~45 VALU per row in the ranking.)
+  uint4 rv[PSLOT][2];
+  const bool full = t0 + PTILE <= n;   // every tile but the last (uniform)
+  const bool vec = a.vec && full;
+  if (IN_REC && full) {
+    // a full tile's loads are unconditional, so the compiler counts them: all 2 * PSLOT are in flight
+    // before the first wait
+#pragma unroll
+    for (int k = 0; k < PSLOT; ++k) {
+      const int64_t i = t0 + wave * (2 * 64 * PSLOT) + k * 128 + lane;
+      rv[k][0] = a.rec_in[i];
+      rv[k][1] = a.rec_in[i + 64];
+    }
+  } else if (!IN_REC && vec) {   // the same for the first pass's column loads
+#pragma unroll
+    for (int k = 0; k < PSLOT; ++k)
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int64_t i = t0 + wave * (2 * 64 * PSLOT) + k * 128 + 64 * e + lane;
+        uint32_t b = (uint32_t)a.in.bin[i];
+        if (SH) b = squeeze_bs(b | (uint32_t)a.in.sh[i] << 16, a.sq);
+        rv[k][e] = make_rec(a.in.z[i], (uint32_t)i, b);
+      }
+  } else {
+#pragma unroll
+    for (int k = 0; k < PSLOT; ++k)
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int64_t i = t0 + wave * (2 * 64 * PSLOT) + k * 128 + 64 * e + lane;
+        if (IN_REC) {
+          rv[k][e] = i < n ? a.rec_in[i] : make_uint4(0u, 0u, 0u, 0u);
+        } else {
+          uint32_t b = i < n ? (uint32_t)a.in.bin[i] | (SH ? (uint32_t)a.in.sh[i] << 16 : 0u) : 0u;
+          if (SH) b = squeeze_bs(b, a.sq);
+          rv[k][e] = make_rec(i < n ? a.in.z[i] : 0ull, (uint32_t)i, b);
+        }
+      }
+  }
+  const uint64_t lt = lanemask_lt();
+  uint32_t rd[PSLOT][2];   // wave rank | digit << 16; rank 0xffff = no row
+#if GM_SORT_LDSMATCH
+  // lanes sharing a digit found through LDS instead of 9 ballot rounds: each row ORs its lane bit into
+  // its digit's 64-bit slot, reads the slot back, and clears it.  The slots (512 per wave, 64 KB) alias
+  // s_rec, which is written only after the ranking's barrier.
+  uint64_t* mslot = (uint64_t*)s_rec + wave * NB_MAX;
+  for (int j = lane; j < NB_MAX; j += 64) mslot[j] = 0ull;
+  wave_lds_sync();
+#endif
+#pragma unroll
+  for (int k = 0; k < PSLOT; ++k)
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int64_t i = t0 + wave * (2 * 64 * PSLOT) + k * 128 + 64 * e + lane;
+      const bool ok = i < n;
+      const uint32_t d = key_digit_w(rv[k][e].w, rec_z(rv[k][e]), a.off, w);
+#if GM_SORT_LDSMATCH
+      if (ok) atomicOr((unsigned long long*)&mslot[d], 1ull << lane);
+      wave_lds_sync();
+      const uint64_t m = ok ? mslot[d] : 0ull;   // lanes of this half whose row holds my row's digit
+      wave_lds_sync();
+      if (ok) mslot[d] = 0ull;
+#else
+      uint64_t m = __ballot(ok);   // lanes of this half whose row holds my row's digit
+#pragma unroll
+      for (int bit = 0; bit < WMAX; ++bit) {   // bits at or above w are 0 in every digit: no-op rounds
+        const uint64_t bb = __ballot((d >> bit) & 1u);
+        m &= ((d >> bit) & 1u) ? bb : ~bb;
+      }
+#endif
+      const int r = __popcll(m & lt);
+      // the wave's counter: read before this half's increment, then the first row of each digit adds
+      const uint32_t c = s_wcnt[wave][d];
+      rd[k][e] = (ok ? c + r : 0xffffu) | (d << 16);
+      __builtin_amdgcn_wave_barrier();
+      if (ok && r == 0) s_wcnt[wave][d] = (uint16_t)(c + __popcll(m));
+      __builtin_amdgcn_wave_barrier();
+    }
+#else
   // this lane's rows
   uint4 rv[PSLOT][2];
   const bool full = t0 + PTILE <= n;   // every tile but the last (uniform)
@@ -370,6 +458,7 @@ __global__ __launch_bounds__(PT) void k_sort_pass(PassArgs a) {
     if (ok1 && r1 == 0) s_wcnt[wave][d1] = (uint16_t)(c1 + __popcll(m10) + __popcll(m11));
     __builtin_amdgcn_wave_barrier();
   }
+#endif
   __syncthreads();
   // thread t owns digit t (t < nb): wave offsets, the tile total, scans of totals and global counts
   uint32_t tot = 0, xt = 0, xb = 0, cg = 0;
