@@ -639,8 +639,11 @@ __device__ __forceinline__ void wave_mem_sync() {   // this wave's global stores
   __builtin_amdgcn_wave_barrier();
 }
 
+// waves per SIMD: 6 for XZ2 (80 VGPRs, a few spills off the hot path) and 5 for XZ3 (96): 3.26-3.34 ->
+// 3.04-3.10 and 10.50-10.63 -> 9.88-9.97 ms per 100k queries into HBM against the compiler's choice
+// (89 / 103 VGPRs, 5 / 4 waves); 6 for XZ3 spilled more and ran 10.6-10.8 (profiles/r6/xz_ranges_occupancy_ab.txt)
 template <int D>
-__global__ __launch_bounds__(XW_TPB) void k_xzranges_w(XZWaveArgs a) {
+__global__ __launch_bounds__(XW_TPB) __attribute__((amdgpu_waves_per_eu(D == 2 ? 6 : 5))) void k_xzranges_w(XZWaveArgs a) {
   constexpr int NK = 1 << D;
   __shared__ int32_t s_lb[XW_TPB / 64][XW_MAXL + 1], s_le[XW_TPB / 64][XW_MAXL + 1], s_lnp[XW_TPB / 64][XW_MAXL + 1];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
